@@ -1,0 +1,148 @@
+// pybind11 bindings for the HIP side (_psx_hip): the worker local solver, the
+// server update, test-set evaluation and ring ingest.  Tensors are passed as
+// raw device pointers (torch `data_ptr()`), streams as `cuda_stream` handles;
+// the Python layer validates shapes/dtypes before calling in.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "../kernels/lr_kernels.h"
+#include "../solver/solver.h"
+
+namespace py = pybind11;
+using namespace psx;
+
+namespace {
+template <typename T>
+T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+
+py::dict ctrl_dict(const Ctrl& c, int H) {
+  py::dict d;
+  d["phase"] = c.phase;
+  d["action"] = c.action;
+  d["action_slot"] = c.action_slot;
+  d["iter"] = c.iter;
+  d["evals"] = c.evals;
+  d["m"] = c.m;
+  d["nacc"] = c.nacc;
+  d["ls_fail"] = c.ls_fail;
+  d["dir_reset"] = c.dir_reset;
+  d["t"] = c.t;
+  d["t_acc"] = c.t_acc;
+  d["f_c"] = c.f_c;
+  d["f_init"] = c.f_init;
+  d["dg0"] = c.dg0;
+  d["gg_c"] = c.gg_c;
+  d["gamma"] = c.gamma;
+  (void)H;
+  return d;
+}
+}  // namespace
+
+PYBIND11_MODULE(_psx_hip, m) {
+  m.doc() = "psx HIP kernels (gfx950)";
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_arch", [](int dev) {
+    hipDeviceProp_t p;
+    hip_check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["gcnArchName"] = std::string(p.gcnArchName);
+    d["multiProcessorCount"] = p.multiProcessorCount;
+    d["sharedMemPerBlock"] = (size_t)p.sharedMemPerBlock;
+    d["maxSharedMemoryPerMultiProcessor"] = (size_t)p.maxSharedMemoryPerMultiProcessor;
+    d["totalGlobalMem"] = (size_t)p.totalGlobalMem;
+    return d;
+  });
+  m.def("fp_supported", &fp_supported);
+  m.def("eval_lds_bytes", &eval_lds_bytes);
+
+  py::class_<SolverCfg>(m, "SolverCfg")
+      .def(py::init<>())
+      .def_readwrite("K", &SolverCfg::K)
+      .def_readwrite("F", &SolverCfg::F)
+      .def_readwrite("Fp", &SolverCfg::Fp)
+      .def_readwrite("P", &SolverCfg::P)
+      .def_readwrite("cap", &SolverCfg::cap)
+      .def_readwrite("iters", &SolverCfg::iters)
+      .def_readwrite("hist", &SolverCfg::hist)
+      .def_readwrite("ls_max", &SolverCfg::ls_max)
+      .def_readwrite("mode", &SolverCfg::mode)
+      .def_readwrite("center", &SolverCfg::center)
+      .def_readwrite("zero_const", &SolverCfg::zero_const)
+      .def_readwrite("nslots", &SolverCfg::nslots)
+      .def_readwrite("gd_lr", &SolverCfg::gd_lr)
+      .def_readwrite("tol", &SolverCfg::tol);
+
+  py::class_<LocalSolver>(m, "LocalSolver")
+      .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t y, uintptr_t w_old, uintptr_t delta,
+                       uintptr_t w_new, uintptr_t wf_hi, uintptr_t wf_lo, uintptr_t b_fin, uintptr_t loss,
+                       uintptr_t stats, int max_eval_wg, bool use_graph) {
+             SolverBuffers b;
+             b.X = P<const uint16_t>(X);
+             b.y = P<const int32_t>(y);
+             b.w_old = P<const float>(w_old);
+             b.delta = P<float>(delta);
+             b.w_new = P<float>(w_new);
+             b.wf_hi = P<uint16_t>(wf_hi);
+             b.wf_lo = P<uint16_t>(wf_lo);
+             b.b_fin = P<float>(b_fin);
+             b.loss = P<float>(loss);
+             b.stats = P<int>(stats);
+             return std::make_unique<LocalSolver>(cfg, b, max_eval_wg, use_graph);
+           }),
+           py::arg("cfg"), py::arg("X"), py::arg("y"), py::arg("w_old"), py::arg("delta"), py::arg("w_new"),
+           py::arg("wf_hi"), py::arg("wf_lo"), py::arg("b_fin"), py::arg("loss"), py::arg("stats"),
+           py::arg("max_eval_wg") = 512, py::arg("use_graph") = true)
+      .def("run", [](LocalSolver& s, int B, int start, uintptr_t stream) { s.run(B, start, S(stream)); })
+      .def("read_ctrl",
+           [](LocalSolver& s, uintptr_t stream) {
+             Ctrl c;
+             s.read_ctrl(&c, S(stream));
+             return ctrl_dict(c, s.cfg().hist);
+           })
+      .def_property_readonly("eval_wg", &LocalSolver::eval_wg)
+      .def_property_readonly("kernels_per_solve", &LocalSolver::kernels_per_solve);
+
+  m.def("test_eval", [](int FP, int K, uintptr_t Xt, uintptr_t yt, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b,
+                        uintptr_t conf, uintptr_t stream) {
+    prepare_kernels();
+    launch_test_eval(FP, K, P<const uint16_t>(Xt), P<const int32_t>(yt), T, P<const uint16_t>(whi),
+                     P<const uint16_t>(wlo), P<const float>(b), P<int>(conf), S(stream));
+    hip_check(hipGetLastError(), "test_eval launch");
+  });
+  m.def("logits", [](int FP, int K, uintptr_t X, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t out,
+                     uintptr_t stream) {
+    prepare_kernels();
+    launch_logits(FP, K, P<const uint16_t>(X), T, P<const uint16_t>(whi), P<const uint16_t>(wlo), P<const float>(b),
+                  P<float>(out), S(stream));
+    hip_check(hipGetLastError(), "logits launch");
+  });
+  m.def("server_apply", [](int K, int F, int FP, uintptr_t w, uintptr_t delta, float lr, uintptr_t whi,
+                           uintptr_t wlo, uintptr_t b, uintptr_t stream) {
+    launch_server_apply(K, F, FP, P<float>(w), P<const float>(delta), lr, P<uint16_t>(whi), P<uint16_t>(wlo),
+                        P<float>(b), S(stream));
+    hip_check(hipGetLastError(), "server_apply launch");
+  });
+  m.def("make_fragments", [](int K, int F, int FP, uintptr_t w, uintptr_t whi, uintptr_t wlo, uintptr_t b,
+                             uintptr_t stream) {
+    launch_make_fragments(K, F, FP, P<const float>(w), P<uint16_t>(whi), P<uint16_t>(wlo), P<float>(b), S(stream));
+    hip_check(hipGetLastError(), "make_fragments launch");
+  });
+  m.def("ring_ingest", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
+                          uintptr_t ring, uintptr_t yring, int64_t dst_first, int64_t cap, int FP, uintptr_t stream) {
+    launch_ring_ingest(P<const uint16_t>(src), P<const int32_t>(ysrc), src_first, src_step, n, P<uint16_t>(ring),
+                       P<int32_t>(yring), dst_first, cap, FP, S(stream));
+    hip_check(hipGetLastError(), "ring_ingest launch");
+  });
+}

@@ -1,0 +1,148 @@
+// pybind11 bindings for the native host runtime (_psx_host): tracker, sliding
+// window, dataset ingest, producer schedule, control plane and CSV logger.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../host/ctrl.h"
+#include "../host/dataset.h"
+#include "../host/logger.h"
+#include "../host/sampling.h"
+#include "../host/tracker.h"
+
+namespace py = pybind11;
+using namespace psx;
+
+PYBIND11_MODULE(_psx_host, m) {
+  m.doc() = "psx native host runtime";
+
+  py::class_<VectorClockTracker>(m, "VectorClockTracker")
+      .def(py::init<int, int>(), py::arg("num_workers"), py::arg("consistency_model"))
+      .def("received", &VectorClockTracker::received)
+      .def("sent", &VectorClockTracker::sent)
+      .def("releasable", &VectorClockTracker::releasable)
+      .def("on_delta", &VectorClockTracker::on_delta)
+      .def("min_clock", &VectorClockTracker::min_clock)
+      .def("max_clock", &VectorClockTracker::max_clock)
+      .def("clock", &VectorClockTracker::clock)
+      .def("is_sent", &VectorClockTracker::is_sent)
+      .def("clocks", &VectorClockTracker::clocks)
+      .def("sent_flags", &VectorClockTracker::sent_flags)
+      .def("restore", &VectorClockTracker::restore)
+      .def_property_readonly("num_workers", &VectorClockTracker::num_workers)
+      .def_property_readonly("consistency_model", &VectorClockTracker::consistency_model)
+      .def_property_readonly("max_gap", &VectorClockTracker::max_gap);
+
+  py::class_<RateEstimator>(m, "RateEstimator")
+      .def(py::init<int>(), py::arg("window") = 500)
+      .def("arrival", &RateEstimator::arrival)
+      .def("mean_interarrival_ms", &RateEstimator::mean_interarrival_ms)
+      .def_property_readonly("samples", &RateEstimator::samples);
+
+  py::class_<SlotAssignment>(m, "SlotAssignment")
+      .def_readonly("slot", &SlotAssignment::slot)
+      .def_readonly("insertion_id", &SlotAssignment::insertion_id)
+      .def_readonly("size", &SlotAssignment::size)
+      .def_readonly("target", &SlotAssignment::target);
+
+  py::class_<SlidingWindow>(m, "SlidingWindow")
+      .def(py::init<int64_t, int64_t, double, int>(), py::arg("min_size"), py::arg("max_size"),
+           py::arg("buffer_coefficient"), py::arg("rate_window") = 500)
+      .def("target_size", &SlidingWindow::target_size)
+      .def("insert", &SlidingWindow::insert)
+      .def("insert_many",
+           [](SlidingWindow& w, py::array_t<double, py::array::c_style | py::array::forcecast> t) {
+             auto n = t.size();
+             py::array_t<int64_t> slots(n);
+             w.insert_many(t.data(), n, slots.mutable_data());
+             return slots;
+           })
+      .def("restore", &SlidingWindow::restore)
+      .def_property_readonly("size", &SlidingWindow::size)
+      .def_property_readonly("capacity", &SlidingWindow::capacity)
+      .def_property_readonly("head", &SlidingWindow::head)
+      .def_property_readonly("start", &SlidingWindow::start)
+      .def_property_readonly("tuples_seen", &SlidingWindow::tuples_seen)
+      .def("mean_interarrival_ms", &SlidingWindow::mean_interarrival_ms);
+
+  py::class_<CsvInfo>(m, "CsvInfo")
+      .def_readonly("rows", &CsvInfo::rows)
+      .def_readonly("cols", &CsvInfo::cols)
+      .def_readonly("header", &CsvInfo::header)
+      .def_readonly("names", &CsvInfo::names);
+
+  m.def("csv_probe", &csv_probe, py::arg("path"), py::arg("header_mode") = 0);
+  m.def(
+      "csv_load",
+      [](const std::string& path, const CsvInfo& info, int label_col, int64_t row_stride, bool want_f32,
+         bool want_bf16, int threads) {
+        int64_t rows = info.rows;
+        py::array_t<float> xf;
+        py::array_t<uint16_t> xb;
+        py::array_t<int32_t> y(rows);
+        if (want_f32) xf = py::array_t<float>({rows, row_stride});
+        if (want_bf16) xb = py::array_t<uint16_t>({rows, row_stride});
+        {
+          py::gil_scoped_release rel;
+          csv_load(path, info, label_col, row_stride, want_f32 ? xf.mutable_data() : nullptr,
+                   want_bf16 ? xb.mutable_data() : nullptr, y.mutable_data(), threads);
+        }
+        return py::make_tuple(want_f32 ? py::object(xf) : py::none(), want_bf16 ? py::object(xb) : py::none(), y);
+      },
+      py::arg("path"), py::arg("info"), py::arg("label_col") = -1, py::arg("row_stride") = 0,
+      py::arg("want_f32") = true, py::arg("want_bf16") = false, py::arg("threads") = 0);
+  m.def("arrival_time_ms", &arrival_time_ms);
+  m.def("due_rows", [](int k, int n, double p, int64_t total, int64_t next_local, double now, int64_t max_rows) {
+    py::array_t<double> times(max_rows > 0 ? std::min<int64_t>(max_rows, 1 << 24) : 0);
+    int64_t c = due_rows(k, n, p, total, next_local, now, times.size(), times.mutable_data());
+    return py::make_tuple(c, times);
+  });
+  m.def("f32_to_bf16", &f32_to_bf16);
+
+  py::class_<CtrlToken>(m, "CtrlToken")
+      .def(py::init<>())
+      .def_readwrite("worker", &CtrlToken::worker)
+      .def_readwrite("kind", &CtrlToken::kind)
+      .def_readwrite("vc", &CtrlToken::vc)
+      .def_readwrite("aux", &CtrlToken::aux)
+      .def_readwrite("ts_us", &CtrlToken::ts_us);
+
+  py::class_<CtrlQueue>(m, "CtrlQueue")
+      .def(py::init<const std::string&, uint32_t, bool>(), py::arg("name"), py::arg("capacity"), py::arg("create"))
+      .def("try_push", &CtrlQueue::try_push)
+      .def("push", &CtrlQueue::push, py::arg("token"), py::arg("timeout_s") = -1.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("try_pop",
+           [](CtrlQueue& q) -> py::object {
+             CtrlToken t;
+             if (q.try_pop(&t)) return py::cast(t);
+             return py::none();
+           })
+      .def(
+          "pop",
+          [](CtrlQueue& q, double timeout_s) -> py::object {
+            CtrlToken t;
+            bool ok;
+            {
+              py::gil_scoped_release rel;
+              ok = q.pop(&t, timeout_s);
+            }
+            if (ok) return py::cast(t);
+            return py::none();
+          },
+          py::arg("timeout_s") = -1.0)
+      .def("unlink", &CtrlQueue::unlink)
+      .def_property_readonly("capacity", &CtrlQueue::capacity)
+      .def_property_readonly("name", &CtrlQueue::name);
+
+  m.def("java_double", &java_double);
+  py::class_<CsvLogger>(m, "CsvLogger")
+      .def(py::init<const std::string&, bool, bool>(), py::arg("path"), py::arg("worker_schema"),
+           py::arg("write_header") = true)
+      .def("log_worker", &CsvLogger::log_worker)
+      .def("log_server", &CsvLogger::log_server)
+      .def("log_line", &CsvLogger::log_line)
+      .def("flush", &CsvLogger::flush, py::call_guard<py::gil_scoped_release>())
+      .def("close", &CsvLogger::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("lines", &CsvLogger::lines);
+}

@@ -1,0 +1,76 @@
+// Native driver of one worker's local solve.
+//
+// The reference runs, per worker iteration, a Spark job: build a DataFrame from
+// the buffer, fit(), evaluate on the test set, diff the coefficients
+// (reference: LogisticRegressionTaskSpark.java:142-221).  Here the whole chain
+//   set_params -> stats -> prep -> [eval -> reduce/ctrl -> update] x nslots
+//   -> finalize
+// is captured ONCE into a hipGraph and replayed per iteration: the host pays
+// one graph launch (~10 us) and the device runs the chain back to back with no
+// host synchronisation; line-search control flow is resolved on device and
+// unused evaluation slots exit immediately.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../kernels/lr_kernels.h"
+
+namespace psx {
+
+struct SolverBuffers {
+  // caller-owned (torch tensors)
+  const uint16_t* X = nullptr;  // ring [cap][Fp] bf16
+  const int32_t* y = nullptr;   // ring labels [cap]
+  const float* w_old = nullptr; // [P] current model (worker copy)
+  float* delta = nullptr;       // [P] out: w_new - w_old
+  float* w_new = nullptr;       // [P] out (optional)
+  uint16_t* wf_hi = nullptr;    // [16*Fp] out: fragments of w_new (for test eval)
+  uint16_t* wf_lo = nullptr;
+  float* b_fin = nullptr;       // [16] out
+  float* loss = nullptr;        // [1] out
+  int* stats = nullptr;         // [4] out: evals, accepted steps, ls failures, direction resets
+};
+
+class LocalSolver {
+ public:
+  LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max_eval_wg, bool use_graph);
+  ~LocalSolver();
+  LocalSolver(const LocalSolver&) = delete;
+  LocalSolver& operator=(const LocalSolver&) = delete;
+
+  // Enqueue one local solve over window [start, start+B) of the ring on `stream`.
+  void run(int B, int start, hipStream_t stream);
+  const SolverCfg& cfg() const { return cfg_; }
+  int eval_wg() const { return nwg_eval_; }
+  int kernels_per_solve() const { return 4 + 3 * cfg_.nslots + 1; }
+  // Debug access to the device controller (synchronous copy).
+  void read_ctrl(Ctrl* out, hipStream_t stream);
+
+ private:
+  void enqueue_body(hipStream_t s);
+  SolverCfg cfg_;
+  SolverBuffers buf_;
+  int nwg_eval_;
+  int stats_row_blocks_;
+  bool use_graph_;
+  // workspace
+  void* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+  SolveParams* prm_ = nullptr;
+  Ctrl* ctrl_ = nullptr;
+  double* acc_ = nullptr;
+  double* dotpart_ = nullptr;
+  float *x_ = nullptr, *d_ = nullptr, *gc_ = nullptr, *gt_ = nullptr, *S_ = nullptr, *Y_ = nullptr;
+  float *std_ = nullptr, *inv_std_ = nullptr, *wfix_ = nullptr, *beff_ = nullptr;
+  uint16_t *whi_ = nullptr, *wlo_ = nullptr;
+  float *Gpart_ = nullptr, *Rpart_ = nullptr, *Lpart_ = nullptr;
+  hipStream_t cap_stream_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+void hip_check(hipError_t e, const char* what);
+
+}  // namespace psx

@@ -1,0 +1,160 @@
+"""Device ops for the logistic-regression parameter server.
+
+On a GPU every op goes through the hand-written HIP kernels in ``_psx_hip``
+(gfx950); there is no PyTorch fallback on the device -- a missing extension is
+a hard error.  On the CPU (tests, the plumbing config of BASELINE.json #1) the
+same ops run the PyTorch reference in :mod:`psx.models.reference`.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..models.logreg import ModelSpec
+from ..models.reference import local_solve_reference
+
+
+def is_gpu(device) -> bool:
+    return torch.device(device).type == "cuda"
+
+
+def stream_handle(device) -> int:
+    return torch.cuda.current_stream(torch.device(device)).cuda_stream
+
+
+@dataclass
+class SolverOptions:
+    iters: int = 2  # reference numMaxIter (LogisticRegressionTaskSpark.java:35)
+    hist: int = 10  # Spark/breeze L-BFGS history
+    ls_max: int = 4  # line-search evaluations per iteration (device slot budget)
+    mode: str = "lbfgs"  # or "gd"
+    gd_lr: float = 1.0
+    center: bool = True  # Spark centring when regParam == 0
+    zero_const: bool = True  # Spark: zero-std features get coefficient 0
+    tol: float = 1e-6
+    use_graph: bool = True
+    max_eval_wg: int = 512
+
+    @property
+    def nslots(self) -> int:
+        return 1 + self.iters * (1 if self.mode == "gd" else self.ls_max)
+
+
+class Fragments:
+    """bf16 hi/lo MFMA-fragment copy of a weight vector + fp32 intercepts."""
+
+    def __init__(self, spec: ModelSpec, device):
+        self.spec = spec
+        self.hi = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
+        self.lo = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
+        self.b = torch.zeros(16, dtype=torch.float32, device=device)
+
+    def refresh(self, w: torch.Tensor):
+        s = self.spec
+        _native.hip().make_fragments(s.K, s.F, s.Fp, w.data_ptr(), self.hi.data_ptr(), self.lo.data_ptr(),
+                                     self.b.data_ptr(), stream_handle(w.device))
+
+
+class LocalSolveOp:
+    """One worker's local solve: window of the device ring -> delta (+ new weights).
+
+    GPU: a native LocalSolver whose whole kernel chain is one hipGraph replay.
+    CPU: :func:`local_solve_reference`.
+    """
+
+    def __init__(self, spec: ModelSpec, cap: int, device, opts: SolverOptions):
+        self.spec, self.cap, self.device, self.opts = spec, cap, torch.device(device), opts
+        P = spec.P
+        self.delta = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.w_new = torch.zeros(P, dtype=torch.float32, device=self.device)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.stats = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self.frag = Fragments(spec, self.device) if is_gpu(self.device) else None
+        self._native = None
+        self._bound = None
+
+    def _bind(self, X: torch.Tensor, y: torch.Tensor, w_old: torch.Tensor):
+        key = (X.data_ptr(), y.data_ptr(), w_old.data_ptr())
+        if self._bound == key:
+            return
+        h = _native.hip()
+        s, o = self.spec, self.opts
+        cfg = h.SolverCfg()
+        cfg.K, cfg.F, cfg.Fp, cfg.P, cfg.cap = s.K, s.F, s.Fp, s.P, self.cap
+        cfg.iters, cfg.hist, cfg.ls_max = o.iters, o.hist, o.ls_max
+        cfg.mode = 1 if o.mode == "gd" else 0
+        cfg.center, cfg.zero_const = int(o.center), int(o.zero_const)
+        cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
+        self._native = h.LocalSolver(
+            cfg, X.data_ptr(), y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(), self.w_new.data_ptr(),
+            self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(), self.loss.data_ptr(),
+            self.stats.data_ptr(), o.max_eval_wg, o.use_graph)
+        self._bound = key
+
+    def run(self, X: torch.Tensor, y: torch.Tensor, B: int, start: int, w_old: torch.Tensor):
+        """Enqueue a solve over ring rows [start, start+B) (mod cap)."""
+        if B <= 0:
+            raise ValueError("local solve on an empty buffer")
+        if is_gpu(self.device):
+            if X.dtype != torch.bfloat16 or X.shape != (self.cap, self.spec.Fp) or y.dtype != torch.int32:
+                raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
+            self._bind(X, y, w_old)
+            self._native.run(int(B), int(start), stream_handle(self.device))
+            return
+        s, o = self.spec, self.opts
+        idx = (torch.arange(B) + start) % self.cap
+        Xw = X[idx, : s.F].float()
+        yw = y[idx].long()
+        res = local_solve_reference(
+            Xw, yw, s.coef(w_old), s.intercept(w_old), iters=o.iters, hist=o.hist, ls_max=o.ls_max,
+            nslots=o.nslots, mode=o.mode, gd_lr=o.gd_lr, center=o.center, zero_const=o.zero_const, tol=o.tol)
+        self.w_new.copy_(s.pack(res.coef, res.intercept))
+        self.delta.copy_(self.w_new - w_old)
+        self.loss.fill_(res.loss)
+        self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0], dtype=torch.int32))
+
+
+class EvalSet:
+    """Test data resident on the device + argmax/confusion evaluation."""
+
+    def __init__(self, spec: ModelSpec, X: torch.Tensor, y: torch.Tensor, device):
+        self.spec = spec
+        self.device = torch.device(device)
+        if X.shape[1] != spec.Fp:
+            raise ValueError(f"test set width {X.shape[1]} != model Fp {spec.Fp}")
+        self.X = X.to(self.device, torch.bfloat16).contiguous()
+        self.y = y.to(self.device, torch.int32).contiguous()
+        self.T = int(self.X.shape[0])
+        self._Xf = None
+
+    def confusion_async(self, frag: Fragments | None, w: torch.Tensor, out: torch.Tensor):
+        """Write the [16,16] confusion counts of model ``w`` into ``out`` (int32)."""
+        s = self.spec
+        if is_gpu(self.device):
+            out.zero_()
+            _native.hip().test_eval(s.Fp, s.K, self.X.data_ptr(), self.y.data_ptr(), self.T, frag.hi.data_ptr(),
+                                    frag.lo.data_ptr(), frag.b.data_ptr(), out.data_ptr(), stream_handle(self.device))
+            return
+        if self._Xf is None:
+            self._Xf = self.X[:, : s.F].float()
+        pred = (self._Xf @ s.coef(w).t() + s.intercept(w)).argmax(1)
+        yy = self.y.long().clamp(0, 15)
+        c = torch.zeros(16 * 16, dtype=torch.int64)
+        c.index_add_(0, yy * 16 + pred, torch.ones_like(yy))
+        out.view(-1).copy_(c.to(torch.int32))
+
+
+def server_apply(spec: ModelSpec, w: torch.Tensor, delta: torch.Tensor, lr: float, frag: Fragments | None):
+    """w += lr * delta over all P entries (quirk Q1 fixed) + refresh eval fragments."""
+    if is_gpu(w.device):
+        _native.hip().server_apply(spec.K, spec.F, spec.Fp, w.data_ptr(), delta.data_ptr(), float(lr),
+                                   frag.hi.data_ptr(), frag.lo.data_ptr(), frag.b.data_ptr(), stream_handle(w.device))
+    else:
+        w.add_(delta, alpha=lr)
+
+
+def confusion_to_numpy(conf: torch.Tensor, K: int) -> np.ndarray:
+    return conf.view(16, 16)[:K, :K].cpu().numpy()

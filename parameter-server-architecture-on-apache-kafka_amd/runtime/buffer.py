@@ -1,0 +1,109 @@
+"""Per-worker stream source + adaptive sliding-window buffer in device memory.
+
+Reference: the INPUT_DATA_BUFFER key-value store + WorkerSamplingProcessor
+(WorkerSamplingProcessor.java:50-135, WorkerApp.java:40-42) and the producer's
+round-robin / rate-limited delivery (CsvProducer.java:36-87).
+
+MI355X design:
+* the whole training set is resident in HBM (bf16 rows; 90k x 1024 is 184 MB
+  of 288 GB), so "delivering" a tuple is a device-side row copy into the
+  worker's ring -- no host staging, no serialisation;
+* worker k owns rows k, k+N, k+2N, ... (reference round-robin, ``row % N``);
+* arrival times follow the reference producer schedule (burst of N*128 rows,
+  then floor(1000/p) rows per second; native ``due_rows``), or, for
+  throughput runs, a fixed number of rows per iteration;
+* window bookkeeping (rate estimate, target size, O(1) slot choice) is the
+  native :class:`SlidingWindow`; the device ring has capacity ``max`` rows.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .. import _native
+from ..ops.lr import is_gpu, stream_handle
+
+
+class DeviceRing:
+    def __init__(self, cap: int, Fp: int, device):
+        self.cap, self.Fp, self.device = int(cap), int(Fp), torch.device(device)
+        self.X = torch.zeros(self.cap, self.Fp, dtype=torch.bfloat16, device=self.device)
+        self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+
+    def ingest(self, src_X: torch.Tensor, src_y: torch.Tensor, src_first: int, src_step: int, n: int, dst_first: int):
+        """Copy rows src_first + i*src_step (i < n) into slots (dst_first + i) % cap."""
+        if n <= 0:
+            return
+        if is_gpu(self.device):
+            _native.hip().ring_ingest(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
+                                      self.X.data_ptr(), self.y.data_ptr(), int(dst_first), self.cap, self.Fp,
+                                      stream_handle(self.device))
+        else:
+            src = torch.arange(n) * src_step + src_first
+            dst = (torch.arange(n) + dst_first) % self.cap
+            self.X[dst] = src_X[src]
+            self.y[dst] = src_y[src]
+
+
+class StreamSource:
+    """Delivers worker ``k``'s shard of a dataset into its ring per the arrival schedule.
+
+    mode "schedule": reference producer clock (``-p`` ms per event).
+    mode "per_iter": ``rows_per_iter`` new rows at every poll (throughput runs).
+    ``epochs``: how many passes over the shard (the reference stops after one).
+    """
+
+    def __init__(self, dataset, k: int, num_workers: int, ring: DeviceRing, window, *, p_ms: float = 200.0,
+                 mode: str = "schedule", rows_per_iter: int = 0, epochs: int = 1, t0: float | None = None):
+        self.ds, self.k, self.N, self.ring, self.win = dataset, int(k), int(num_workers), ring, window
+        self.p_ms, self.mode, self.rows_per_iter, self.epochs = float(p_ms), mode, int(rows_per_iter), int(epochs)
+        self.t0 = time.time() if t0 is None else t0
+        total = dataset.rows
+        self.local_total = max(0, (total - self.k + self.N - 1) // self.N) if total > self.k else 0
+        self.next_local = 0  # cursor into this worker's row list (may span epochs)
+        if self.local_total == 0:
+            raise ValueError(f"worker {k} has no rows (dataset has {total} rows for {num_workers} workers)")
+
+    @property
+    def exhausted(self) -> bool:
+        return self.next_local >= self.local_total * self.epochs
+
+    def poll(self, now: float | None = None) -> int:
+        """Ingest every due row; returns how many rows arrived."""
+        if self.exhausted:
+            return 0
+        now = time.time() if now is None else now
+        now_ms = (now - self.t0) * 1000.0
+        limit = self.local_total * self.epochs - self.next_local
+        if self.mode == "per_iter":
+            n = min(self.rows_per_iter, limit)
+            times = np.full(n, now_ms, dtype=np.float64)
+        else:
+            epoch = self.next_local // self.local_total
+            cur = self.next_local - epoch * self.local_total
+            n, times = _native.host.due_rows(self.k, self.N, self.p_ms, self.ds.rows, cur, now_ms,
+                                             min(limit, self.local_total - cur, 1 << 22))
+            times = times[:n] + epoch * 0.0
+        if n <= 0:
+            return 0
+        self._deliver(n, times)
+        return int(n)
+
+    def _deliver(self, n: int, times):
+        slots = self.win.insert_many(np.asarray(times, dtype=np.float64))
+        # only the last `cap` rows can survive in the window; copy those
+        keep = min(n, self.ring.cap)
+        skip = n - keep
+        first_slot = int(slots[skip])
+        pos = self.next_local + skip
+        remaining = keep
+        while remaining > 0:  # split at epoch boundaries of the shard
+            cur = pos % self.local_total
+            run = min(remaining, self.local_total - cur)
+            self.ring.ingest(self.ds.X, self.ds.y, self.k + cur * self.N, self.N, run, first_slot)
+            first_slot = (first_slot + run) % self.ring.cap
+            pos += run
+            remaining -= run
+        self.next_local += n

@@ -1,0 +1,66 @@
+"""Run configuration shared by the CLIs, the engines and bench.py.
+
+Defaults equal the reference's constants: numWorkers=4
+(BaseKafkaApp.java:25), min/max buffer 128/1024 and bc 0.3
+(WorkerAppRunner.java:56-58), -p 200 and -c 0 (ServerAppRunner.java:59-60),
+numMaxIter=2 (LogisticRegressionTaskSpark.java:35), server lr = 1/numWorkers
+(ServerProcessor.java:36).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+
+from ..ops.lr import SolverOptions
+
+
+@dataclass
+class PSConfig:
+    # data
+    train_path: str = "./data/train.csv"
+    test_path: str = "./data/test.csv"
+    header: str = "auto"
+    label_col: int = -1
+    num_features: int | None = None  # inferred from the CSV
+    num_classes: int | None = None  # inferred: max label + 1 (incl. phantom class 0)
+    # topology / consistency
+    num_workers: int = 4
+    consistency_model: int = 0  # 0 sequential, -1 eventual, D>0 bounded delay
+    # producer
+    producer_time_per_event: float = 200.0  # -p (ms per event; 0 = unthrottled)
+    stream_mode: str = "schedule"  # or "per_iter"
+    rows_per_iter: int = 0
+    epochs: int = 1
+    # buffer
+    min_buffer_size: int = 128
+    max_buffer_size: int = 1024
+    buffer_size_coefficient: float = 0.3
+    # model / solver
+    init: str = "zeros"
+    seed: int = 0
+    server_lr: float | None = None  # default 1/num_workers
+    solver: SolverOptions = field(default_factory=SolverOptions)
+    # run control
+    max_iters: int = 0  # per worker; 0 = until data exhausted + drained
+    max_wallclock_s: float = 0.0
+    idle_exit_s: float = 2.0  # stop when the stream is exhausted and this much time passed
+    # logging
+    logging: bool = False
+    log_dir: str = "."
+    verbose: bool = False
+    # distributed
+    bsp_schedule: str = "allreduce"  # allreduce | reduce_bcast | sharded
+    server_colocated: bool = True
+    # checkpoint
+    checkpoint_dir: str | None = None
+    checkpoint_every: int = 0
+    resume: bool = False
+    # fault injection / tracing
+    inject_worker_delay_ms: dict = field(default_factory=dict)  # worker -> ms per iteration
+    trace_path: str | None = None
+
+    @property
+    def lr(self) -> float:
+        return self.server_lr if self.server_lr is not None else 1.0 / self.num_workers
+
+    def to_dict(self) -> dict:
+        return asdict(self)

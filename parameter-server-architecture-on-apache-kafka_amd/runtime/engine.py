@@ -1,0 +1,259 @@
+"""In-process parameter-server engine: server + N workers on ONE device.
+
+This is the degenerate case of the multi-GPU RCCL schedules (psx.parallel.dist):
+push/pull become device-local copies, ordering comes from HIP streams and
+events.  It is what a single MI355X (or the CPU, for tests / the plumbing
+config) runs, and it exercises exactly the same roles, tracker, buffer, solver
+and logging code as the distributed engine.
+
+* BSP (c = 0): lock-step rounds on one stream -- every worker solves, the server
+  applies the summed deltas (lr = 1/N), evaluates, and broadcasts.
+* SSP (c = D > 0) / ASP (c = -1): one host thread + one HIP stream per worker,
+  the server on the calling thread consumes (worker, vc) tokens in arrival
+  order -- the analogue of the single-partition GRADIENTS_TOPIC
+  (ServerApp.java:36-38) -- and releases workers per the vector-clock tracker.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+
+import torch
+
+from ..models.logreg import ModelSpec
+from ..ops.lr import EvalSet, is_gpu
+from ..utils import data as data_mod
+from ..utils.checkpoint import maybe_checkpoint, maybe_resume
+from ..utils.logsink import LogSink, summarize
+from ..utils.trace import Tracer
+from .config import PSConfig
+from .roles import ServerRole, WorkerRole
+
+
+def load_datasets(cfg: PSConfig, train=None, test=None):
+    if train is None:
+        train = data_mod.load_any(cfg.train_path, header=cfg.header, label_col=cfg.label_col,
+                                  num_features=cfg.num_features)
+    if test is None and cfg.test_path:
+        test = data_mod.load_any(cfg.test_path, header=cfg.header, label_col=cfg.label_col,
+                                 num_features=train.num_features)
+    if cfg.num_classes is not None:
+        K = int(cfg.num_classes)
+    else:
+        mx = int(train.y.max())
+        if test is not None:
+            mx = max(mx, int(test.y.max()))
+        K = max(2, mx + 1)
+    spec = ModelSpec(train.num_features, K)
+    return spec, train, test
+
+
+class LocalEngine:
+    def __init__(self, cfg: PSConfig, device="cpu", train=None, test=None, log: LogSink | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.spec, train, test = load_datasets(cfg, train, test)
+        self.train = train.to(self.device)
+        self.evalset = EvalSet(self.spec, test.X, test.y, self.device) if test is not None else None
+        if log is None:
+            wp = f"{cfg.log_dir}/logs-worker.csv" if cfg.logging else None
+            sp = f"{cfg.log_dir}/logs-server.csv" if cfg.logging else None
+            log = LogSink(self.spec.K, self.device, wp, sp, to_stdout=not cfg.logging and cfg.verbose)
+        self.log = log
+        self.tracer = Tracer(cfg.trace_path)
+        w0 = self.spec.init(cfg.init, seed=cfg.seed)
+        self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0)
+        self.t0 = time.time()
+        self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
+                        for k in range(cfg.num_workers)]
+        self.rounds = 0
+        maybe_resume(cfg, self.server)
+
+    # ------------------------------------------------------------------
+    def _stop(self, iters_done: int, t_start: float, exhausted_since: float | None) -> bool:
+        c = self.cfg
+        if c.max_iters and iters_done >= c.max_iters:
+            return True
+        if c.max_wallclock_s and time.time() - t_start >= c.max_wallclock_s:
+            return True
+        if not c.max_iters and exhausted_since is not None and time.time() - exhausted_since >= c.idle_exit_s:
+            return True
+        return False
+
+    def run(self) -> dict:
+        if self.cfg.consistency_model == 0:
+            out = self._run_bsp()
+        else:
+            out = self._run_async()
+        self.log.close()
+        self.tracer.close()
+        if self.log.book is not None:
+            out.update(summarize(self.log.book))
+        out["max_vc_gap"] = int(self.server.tracker.max_gap)
+        return out
+
+    # ------------------------------------------------------------------
+    def _run_bsp(self) -> dict:
+        cfg, srv, W = self.cfg, self.server, self.workers
+        N = len(W)
+        for w in W:  # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87)
+            w.w.copy_(srv.w)
+            w.vc = 0
+        t_start = time.time()
+        exhausted_since = None
+        r = self.rounds
+        while not self._stop(r - self.rounds, t_start, exhausted_since):
+            with self.tracer.span("ingest"):
+                for w in W:
+                    w.ingest()
+            if all(w.source.exhausted for w in W):
+                exhausted_since = exhausted_since or time.time()
+            if not all(w.ready() for w in W):
+                time.sleep(0.001)
+                continue
+            with self.tracer.span("solve"):
+                deltas = [w.compute(self.log) for w in W]
+            with self.tracer.span("server"):
+                if N == 1:
+                    total = deltas[0]
+                else:
+                    total = srv.acc
+                    total.copy_(deltas[0])
+                    for d in deltas[1:]:
+                        total.add_(d)
+                srv.apply(total)
+                for k in range(N):
+                    srv.tracker.received(k, r)
+                srv.updates += N
+                srv.log_eval(r, self.log)
+                for k, w in enumerate(W):
+                    srv.tracker.sent(k, r + 1)
+                    w.w.copy_(srv.w)
+                    w.vc = r + 1
+            r += 1
+            maybe_checkpoint(cfg, srv, r)
+            self.log.drain()
+        if is_gpu(self.device):
+            torch.cuda.synchronize(self.device)
+        elapsed = time.time() - t_start
+        self.rounds = r
+        return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0}
+
+    # ------------------------------------------------------------------
+    def _run_async(self) -> dict:
+        cfg, srv, W = self.cfg, self.server, self.workers
+        gpu = is_gpu(self.device)
+        to_server: queue.Queue = queue.Queue()
+        inbox = [queue.Queue() for _ in W]
+        stop = threading.Event()
+        log_lock = threading.Lock()
+        errors = []
+
+        class _LockedLog:
+            def __init__(s, inner):
+                s.inner = inner
+
+            def submit_worker(s, *a, **k):
+                with log_lock:
+                    s.inner.submit_worker(*a, **k)
+
+        locked = _LockedLog(self.log)
+
+        def worker_loop(w: WorkerRole):
+            try:
+                stream = torch.cuda.Stream(self.device) if gpu else None
+                ctx = torch.cuda.stream(stream) if gpu else _Null()
+                with ctx:
+                    while True:
+                        msg = inbox[w.k].get()
+                        if msg is None:
+                            return
+                        vc, ev = msg
+                        if ev is not None:
+                            torch.cuda.current_stream(self.device).wait_event(ev)
+                        w.vc = vc
+                        w.ingest()
+                        while not w.ready():
+                            if stop.is_set():
+                                return
+                            time.sleep(0.001)
+                            w.ingest()
+                        delta = w.compute(locked)
+                        ev2 = None
+                        if gpu:
+                            ev2 = torch.cuda.Event()
+                            ev2.record(torch.cuda.current_stream(self.device))
+                        to_server.put((w.k, vc, delta, ev2, w.source.exhausted))
+            except Exception as e:  # surfaced by the server loop
+                errors.append(e)
+                to_server.put(None)
+
+        threads = [threading.Thread(target=worker_loop, args=(w,), daemon=True) for w in W]
+        for t in threads:
+            t.start()
+
+        def send(j: int, u: int):
+            W[j].w.copy_(srv.w)
+            ev = None
+            if gpu:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+            inbox[j].put((u, ev))
+
+        for j in range(len(W)):  # bootstrap: vc 0 to everybody, tracker untouched
+            send(j, 0)
+        t_start = time.time()
+        exhausted = set()
+        exhausted_since = None
+        per_worker = [0] * len(W)
+        while True:
+            if errors:
+                break
+            done_iters = min(per_worker)
+            if self._stop(done_iters, t_start, exhausted_since):
+                break
+            try:
+                tok = to_server.get(timeout=0.05)
+            except queue.Empty:
+                continue
+            if tok is None:
+                break
+            k, v, delta, ev, ex = tok
+            if ex:
+                exhausted.add(k)
+                if len(exhausted) == len(W):
+                    exhausted_since = exhausted_since or time.time()
+            if ev is not None:
+                torch.cuda.current_stream(self.device).wait_event(ev)
+            with log_lock:
+                srv.apply(delta)
+                srv.updates += 1
+                per_worker[k] += 1
+                if k == 0:
+                    srv.log_eval(v, self.log)
+                for j, u in srv.tracker.on_delta(k, v):
+                    send(j, u)
+                maybe_checkpoint(cfg, srv, srv.updates)
+                self.log.drain()
+        stop.set()
+        for q in inbox:
+            q.put(None)
+        for t in threads:
+            t.join(timeout=30)
+        if gpu:
+            torch.cuda.synchronize(self.device)
+        if errors:
+            raise errors[0]
+        elapsed = time.time() - t_start
+        return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0}
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

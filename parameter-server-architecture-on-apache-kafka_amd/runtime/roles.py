@@ -1,0 +1,93 @@
+"""Worker and server roles (device state + one iteration each).
+
+WorkerRole  <- WorkerTrainingProcessor + WorkerSamplingProcessor + the
+               per-key LogisticRegressionTaskSpark (reference:
+               WorkerTrainingProcessor.java:63-98, WorkerSamplingProcessor.java:50-113)
+ServerRole  <- ServerProcessor + MessageTracker (ServerProcessor.java:143-228,
+               MessageTracker.java:42-88)
+
+Transport-agnostic: the engines (in-process or RCCL multi-process) move the
+delta / weight tensors; roles only enqueue device work on the current stream.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from .. import _native
+from ..models.logreg import ModelSpec
+from ..ops.lr import EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply
+from .buffer import DeviceRing, StreamSource
+from .config import PSConfig
+
+
+class WorkerRole:
+    def __init__(self, k: int, spec: ModelSpec, cfg: PSConfig, device, train, evalset: EvalSet | None,
+                 t0: float | None = None):
+        self.k, self.spec, self.cfg, self.device = k, spec, cfg, torch.device(device)
+        self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device)
+        self.window = _native.host.SlidingWindow(cfg.min_buffer_size, cfg.max_buffer_size,
+                                                 cfg.buffer_size_coefficient, 500)
+        self.source = StreamSource(train, k, cfg.num_workers, self.ring, self.window,
+                                   p_ms=cfg.producer_time_per_event, mode=cfg.stream_mode,
+                                   rows_per_iter=cfg.rows_per_iter, epochs=cfg.epochs, t0=t0)
+        self.solver = LocalSolveOp(spec, cfg.max_buffer_size, self.device, cfg.solver)
+        self.evalset = evalset
+        self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
+        self.conf = torch.zeros(256, dtype=torch.int32, device=self.device)
+        self.vc = 0  # version of the weights currently held
+        self.iters = 0
+        self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
+
+    @property
+    def tuples_seen(self) -> int:
+        return int(self.window.tuples_seen)
+
+    def ingest(self) -> int:
+        return self.source.poll()
+
+    def ready(self) -> bool:
+        return self.window.size > 0
+
+    def compute(self, log=None) -> torch.Tensor:
+        """One local solve on the current window; returns the delta tensor.
+
+        The worker's metrics are those of the LOCALLY trained model
+        (LogisticRegressionTaskSpark.java:186), logged with the weights version
+        it trained from and numTuplesSeen = the newest insertion id.
+        """
+        if self.delay_s > 0:
+            time.sleep(self.delay_s)
+        B, start = int(self.window.size), int(self.window.start)
+        self.solver.run(self.ring.X, self.ring.y, B, start, self.w)
+        if log is not None and self.evalset is not None:
+            self.evalset.confusion_async(self.solver.frag, self.solver.w_new, self.conf)
+            log.submit_worker(self.k, self.vc, self.tuples_seen, self.solver.loss, self.conf)
+        self.iters += 1
+        return self.solver.delta
+
+
+class ServerRole:
+    def __init__(self, spec: ModelSpec, cfg: PSConfig, device, evalset: EvalSet | None, w0: torch.Tensor):
+        self.spec, self.cfg, self.device = spec, cfg, torch.device(device)
+        self.w = w0.to(self.device, torch.float32).clone()
+        self.frag = Fragments(spec, self.device) if is_gpu(self.device) else None
+        if self.frag is not None:
+            self.frag.refresh(self.w)
+        self.tracker = _native.host.VectorClockTracker(cfg.num_workers, cfg.consistency_model)
+        self.evalset = evalset
+        self.conf = torch.zeros(256, dtype=torch.int32, device=self.device)
+        self.updates = 0
+        self.acc = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
+
+    def apply(self, delta: torch.Tensor, lr: float | None = None):
+        """w += lr * delta   (ServerProcessor.java:148-151 with lr = 1/N)."""
+        server_apply(self.spec, self.w, delta, self.cfg.lr if lr is None else lr, self.frag)
+
+    def log_eval(self, vc: int, log):
+        """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
+        if log is None or self.evalset is None:
+            return
+        self.evalset.confusion_async(self.frag, self.w, self.conf)
+        log.submit_server(vc, self.conf)

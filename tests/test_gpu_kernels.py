@@ -1,0 +1,147 @@
+"""Numerics of the HIP kernels against plain PyTorch fp32/fp64 references (MI355X)."""
+import numpy as np
+import pytest
+import torch
+
+from psx import _native
+from psx.models.logreg import ModelSpec
+from psx.models.reference import local_solve_reference
+from psx.ops.lr import EvalSet, Fragments, LocalSolveOp, SolverOptions, server_apply, stream_handle
+from psx.runtime.buffer import DeviceRing
+from psx.utils.data import synth_binary, synth_finefood
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_w(spec, seed, scale=0.1):
+    g = torch.Generator().manual_seed(seed)
+    return spec.pack(torch.randn(spec.K, spec.F, generator=g) * scale, torch.randn(spec.K, generator=g) * scale)
+
+
+def test_native_hip_loaded(cuda):
+    h = _native.hip()
+    info = h.device_arch(0)
+    assert "gfx950" in info["gcnArchName"], info
+    assert _native.hip_loaded_path().endswith(".so")
+
+
+@pytest.mark.parametrize("F,K,T", [(1024, 6, 4877), (99, 2, 50), (300, 6, 97), (2000, 11, 130)])
+def test_logits_match_fp32(cuda, F, K, T):
+    spec = ModelSpec(F, K)
+    g = torch.Generator().manual_seed(F + K)
+    X = torch.zeros(T, spec.Fp)
+    X[:, :F] = torch.randn(T, F, generator=g) * 0.05
+    Xb = X.to(torch.bfloat16)
+    w = _rand_w(spec, 1)
+    frag = Fragments(spec, cuda)
+    wd = w.to(cuda)
+    frag.refresh(wd)
+    out = torch.zeros(T, K, device=cuda)
+    Xd = Xb.to(cuda)
+    _native.hip().logits(spec.Fp, K, Xd.data_ptr(), T, frag.hi.data_ptr(), frag.lo.data_ptr(), frag.b.data_ptr(),
+                         out.data_ptr(), stream_handle(cuda))
+    ref = Xb[:, :F].double() @ spec.coef(w).double().t() + spec.intercept(w).double()
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def _ring_with(ds, cap, start, B, device):
+    ring = DeviceRing(cap, ds.Fp, device)
+    Xc = ring.X.cpu()
+    yc = ring.y.cpu()
+    idx = (torch.arange(B) + start) % cap
+    Xc[idx] = ds.X[:B]
+    yc[idx] = ds.y[:B]
+    ring.X.copy_(Xc)
+    ring.y.copy_(yc)
+    return ring
+
+
+@pytest.mark.parametrize(
+    "mode,iters,B,start,F",
+    [("lbfgs", 2, 700, 900, 1024), ("lbfgs", 6, 1024, 0, 1024), ("gd", 3, 333, 10, 1024), ("lbfgs", 2, 50, 0, 99)],
+)
+def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
+    cap = 1024
+    if F == 99:
+        ds = synth_binary(B, F, seed=3)
+        spec = ModelSpec(F, 2)
+    else:
+        ds = synth_finefood(B, F, seed=4)
+        spec = ModelSpec(F, 6)
+    ring = _ring_with(ds, cap, start, B, cuda)
+    w_old = _rand_w(spec, 7, scale=0.05)
+    opts = SolverOptions(iters=iters, mode=mode, gd_lr=0.5, ls_max=6)
+    op = LocalSolveOp(spec, cap, cuda, opts)
+    wd = w_old.to(cuda)
+    op.run(ring.X, ring.y, B, start, wd)
+    torch.cuda.synchronize()
+    ref = local_solve_reference(ds.float_features(), ds.y.long(), spec.coef(w_old), spec.intercept(w_old),
+                                iters=iters, hist=opts.hist, ls_max=opts.ls_max, nslots=opts.nslots, mode=mode,
+                                gd_lr=opts.gd_lr)
+    delta = op.delta.cpu()
+    dc, db = spec.coef(delta), spec.intercept(delta)
+    scale = max(ref.delta_coef.abs().max().item(), 1e-6)
+    err = (dc - ref.delta_coef).abs().max().item() / scale
+    errb = (db - ref.delta_intercept).abs().max().item() / max(ref.delta_intercept.abs().max().item(), 1e-6)
+    stats = op.stats.cpu().tolist()
+    assert abs(op.loss.item() - ref.loss) < 1e-3 * max(1.0, abs(ref.loss)), (op.loss.item(), ref.loss, stats)
+    assert err < 2e-2 and errb < 2e-2, (err, errb, stats, ref.evals, ref.accepted)
+    assert stats[1] == ref.accepted, (stats, ref.accepted)
+
+
+def test_graph_and_eager_agree(cuda):
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(512, seed=5)
+    ring = _ring_with(ds, 1024, 100, 512, cuda)
+    w = _rand_w(spec, 2, 0.02).to(cuda)
+    outs = []
+    for g in (True, False):
+        op = LocalSolveOp(spec, 1024, cuda, SolverOptions(use_graph=g))
+        for _ in range(3):  # replays must be identical
+            op.run(ring.X, ring.y, 512, 100, w)
+        torch.cuda.synchronize()
+        outs.append(op.delta.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_confusion_matches_cpu(cuda):
+    spec = ModelSpec(1024, 6)
+    te = synth_finefood(4877, seed=9)
+    w = _rand_w(spec, 3, 0.5)
+    gpu = EvalSet(spec, te.X, te.y, cuda)
+    cpu = EvalSet(spec, te.X, te.y, "cpu")
+    frag = Fragments(spec, cuda)
+    wd = w.to(cuda)
+    frag.refresh(wd)
+    cg = torch.zeros(256, dtype=torch.int32, device=cuda)
+    cc = torch.zeros(256, dtype=torch.int32)
+    gpu.confusion_async(frag, wd, cg)
+    cpu.confusion_async(None, w, cc)
+    torch.cuda.synchronize()
+    diff = (cg.cpu() - cc).abs().sum().item()
+    assert cg.sum().item() == 4877
+    assert diff <= 4, diff  # argmax ties at bf16/fp32 boundaries
+
+
+def test_server_apply(cuda):
+    spec = ModelSpec(1024, 6)
+    w = _rand_w(spec, 4).to(cuda)
+    d = _rand_w(spec, 5).to(cuda)
+    ref = w + 0.25 * d
+    frag = Fragments(spec, cuda)
+    server_apply(spec, w, d, 0.25, frag)
+    torch.cuda.synchronize()
+    assert torch.allclose(w, ref, atol=1e-6)
+    assert torch.allclose(frag.b[: spec.K], spec.intercept(ref), atol=1e-6)
+
+
+def test_ring_ingest_strided_wrap(cuda):
+    ds = synth_finefood(300, seed=6).to(cuda)
+    ring = DeviceRing(64, ds.Fp, cuda)
+    ring.ingest(ds.X, ds.y, 3, 4, 50, 40)  # rows 3,7,...  into slots 40..63,0..25
+    torch.cuda.synchronize()
+    src = torch.arange(50) * 4 + 3
+    dst = (torch.arange(50) + 40) % 64
+    assert torch.equal(ring.X.cpu()[dst], ds.X.cpu()[src])
+    assert torch.equal(ring.y.cpu()[dst], ds.y.cpu()[src])

@@ -132,10 +132,22 @@ def main(argv=None):
         },
         "test_accuracy": out.get("final_server_acc"),
         "test_f1": out.get("final_server_f1"),
+        "best_test_f1": out.get("best_server_f1"),
+        "accuracy_vs_wallclock": _curve(eng.log.book.server, t0),
         "tuples_seen": eng.workers[0].tuples_seen,
     }
     print(json.dumps(res))
     return res
+
+
+def _curve(server_rows, t0_perf, points=10):
+    """[(seconds since the timed region started, test accuracy, weighted F1)] samples."""
+    if not server_rows:
+        return []
+    ts0 = server_rows[0][0]
+    idx = sorted({int(i * (len(server_rows) - 1) / max(1, points - 1)) for i in range(points)})
+    return [(round((server_rows[i][0] - ts0) / 1000.0, 4), round(server_rows[i][3], 4), round(server_rows[i][2], 4))
+            for i in idx]
 
 
 def _fresh_log(eng):

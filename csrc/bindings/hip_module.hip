@@ -67,7 +67,7 @@ PYBIND11_MODULE(_psx_hip, m) {
   m.def("fp_supported", &fp_supported);
   m.def("eval_lds_bytes", &eval_lds_bytes);
 
-  py::class_<SolverCfg>(m, "SolverCfg")
+  py::class_<SolverCfg>(m, "SolverCfg", py::module_local())
       .def(py::init<>())
       .def_readwrite("K", &SolverCfg::K)
       .def_readwrite("F", &SolverCfg::F)

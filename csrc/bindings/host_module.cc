@@ -9,6 +9,10 @@
 #include "../host/logger.h"
 #include "../host/sampling.h"
 #include "../host/tracker.h"
+#include "../kernels/solver_ctrl.h"
+
+#include <cstring>
+#include <memory>
 
 namespace py = pybind11;
 using namespace psx;
@@ -134,6 +138,60 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("unlink", &CtrlQueue::unlink)
       .def_property_readonly("capacity", &CtrlQueue::capacity)
       .def_property_readonly("name", &CtrlQueue::name);
+
+  // Host build of the device solver state machine (csrc/kernels/solver_ctrl.h),
+  // so the exact control logic the GPU runs can be unit-tested on the CPU.
+  py::class_<SolverCfg>(m, "SolverCfg", py::module_local())
+      .def(py::init<>())
+      .def_readwrite("K", &SolverCfg::K)
+      .def_readwrite("F", &SolverCfg::F)
+      .def_readwrite("Fp", &SolverCfg::Fp)
+      .def_readwrite("P", &SolverCfg::P)
+      .def_readwrite("cap", &SolverCfg::cap)
+      .def_readwrite("iters", &SolverCfg::iters)
+      .def_readwrite("hist", &SolverCfg::hist)
+      .def_readwrite("ls_max", &SolverCfg::ls_max)
+      .def_readwrite("mode", &SolverCfg::mode)
+      .def_readwrite("center", &SolverCfg::center)
+      .def_readwrite("zero_const", &SolverCfg::zero_const)
+      .def_readwrite("nslots", &SolverCfg::nslots)
+      .def_readwrite("gd_lr", &SolverCfg::gd_lr)
+      .def_readwrite("tol", &SolverCfg::tol);
+  py::class_<Ctrl>(m, "SolverCtrl", py::module_local())
+      .def(py::init([]() {
+        auto c = std::make_unique<Ctrl>();
+        std::memset(c.get(), 0, sizeof(Ctrl));
+        ctrl_init(*c);
+        return c;
+      }))
+      .def("step",
+           [](Ctrl& c, const SolverCfg& cfg, double f_t, const std::vector<double>& dots, int slot) {
+             if (static_cast<int>(dots.size()) < num_dots(cfg.hist)) throw std::invalid_argument("too few dots");
+             ctrl_step(c, cfg, f_t, dots.data(), slot);
+           })
+      .def_readonly("phase", &Ctrl::phase)
+      .def_readonly("action", &Ctrl::action)
+      .def_readonly("action_slot", &Ctrl::action_slot)
+      .def_readonly("iter", &Ctrl::iter)
+      .def_readonly("m", &Ctrl::m)
+      .def_readonly("head", &Ctrl::head)
+      .def_readonly("push_slot", &Ctrl::push_slot)
+      .def_readonly("nacc", &Ctrl::nacc)
+      .def_readonly("ls_fail", &Ctrl::ls_fail)
+      .def_readonly("evals", &Ctrl::evals)
+      .def_readonly("t", &Ctrl::t)
+      .def_readonly("t_acc", &Ctrl::t_acc)
+      .def_readonly("f_c", &Ctrl::f_c)
+      .def_readonly("cg", &Ctrl::cg)
+      .def_property_readonly("cs", [](const Ctrl& c) { return std::vector<double>(c.cs, c.cs + kMaxHist); })
+      .def_property_readonly("cy", [](const Ctrl& c) { return std::vector<double>(c.cy, c.cy + kMaxHist); });
+  m.attr("kActNone") = static_cast<int>(kActNone);
+  m.attr("kActInit") = static_cast<int>(kActInit);
+  m.attr("kActTrial") = static_cast<int>(kActTrial);
+  m.attr("kActAccept") = static_cast<int>(kActAccept);
+  m.attr("kActAcceptDone") = static_cast<int>(kActAcceptDone);
+  m.attr("kActDone") = static_cast<int>(kActDone);
+  m.attr("kPhDone") = static_cast<int>(kPhDone);
 
   m.def("java_double", &java_double);
   py::class_<CsvLogger>(m, "CsvLogger")

@@ -80,7 +80,7 @@ def build_host(force=False, jobs=8):
     sources = sorted(glob.glob(os.path.join(CSRC, "host", "*.cc"))) + [
         os.path.join(CSRC, "bindings", "host_module.cc")
     ]
-    headers = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
+    headers = sorted(glob.glob(os.path.join(CSRC, "host", "*.h"))) + [os.path.join(CSRC, "kernels", "solver_ctrl.h")]
     out = os.path.join(PKG, "_psx_host" + _ext_suffix())
     cflags = ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"] + [
         "-I" + i for i in _pybind_includes()

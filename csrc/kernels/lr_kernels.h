@@ -19,7 +19,7 @@ void launch_stats(const uint16_t* X, const SolveParams* prm, int cap, int FP, do
                   hipStream_t s);
 void launch_prep(const SolverCfg& cfg, const SolveParams* prm, const double* acc, const float* w_old, float* x,
                  float* d, float* g_c, float* std_, float* inv_std, float* wfix, uint16_t* wf_hi, uint16_t* wf_lo,
-                 float* b_eff, Ctrl* ctrl, hipStream_t s);
+                 float* b_eff, Ctrl* ctrl, int nrb, hipStream_t s);
 void launch_eval(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, int slot, const uint16_t* X,
                  const int32_t* y, const uint16_t* wf_hi, const uint16_t* wf_lo, const float* b_eff, float* Gpart,
                  float* Rpart, float* Lpart, int nwg, hipStream_t s);

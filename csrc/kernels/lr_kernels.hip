@@ -80,8 +80,9 @@ __global__ __launch_bounds__(256) void stats_kernel(const uint16_t* __restrict__
       a += red[0][r][t];
       b += red[1][r][t];
     }
-    atomicAdd(acc + blockIdx.x * 128 + t, a);
-    atomicAdd(acc + FP + blockIdx.x * 128 + t, b);
+    // per-row-block partials; prep sums them in a fixed order (deterministic)
+    acc[((size_t)blockIdx.y * 2 + 0) * FP + blockIdx.x * 128 + t] = a;
+    acc[((size_t)blockIdx.y * 2 + 1) * FP + blockIdx.x * 128 + t] = b;
   }
 }
 
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void prep_kernel(SolverCfg cfg, const SolvePar
                                                    const double* __restrict__ acc, const float* __restrict__ w_old,
                                                    float* x, float* d, float* g_c, float* std_, float* inv_std,
                                                    float* wfix, uint16_t* wf_hi, uint16_t* wf_lo, float* b_eff,
-                                                   Ctrl* ctrl) {
+                                                   Ctrl* ctrl, int nrb) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   const int KF = cfg.K * cfg.Fp;
   if (p == 0) ctrl_init(*ctrl);
@@ -118,8 +119,13 @@ __global__ __launch_bounds__(256) void prep_kernel(SolverCfg cfg, const SolvePar
     const double n = (double)prm->B;
     double sd = 0.0;
     if (f < cfg.F && n > 1.0) {
-      double mean = acc[f] / n;
-      double var = (acc[cfg.Fp + f] - n * mean * mean) / (n - 1.0);
+      double s1 = 0.0, s2 = 0.0;
+      for (int rb = 0; rb < nrb; ++rb) {
+        s1 += acc[((size_t)rb * 2 + 0) * cfg.Fp + f];
+        s2 += acc[((size_t)rb * 2 + 1) * cfg.Fp + f];
+      }
+      double mean = s1 / n;
+      double var = (s2 - n * mean * mean) / (n - 1.0);
       sd = var > 0.0 ? sqrt(var) : 0.0;
     }
     float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
@@ -142,9 +148,9 @@ __global__ __launch_bounds__(256) void prep_kernel(SolverCfg cfg, const SolvePar
 
 void launch_prep(const SolverCfg& cfg, const SolveParams* prm, const double* acc, const float* w_old, float* x,
                  float* d, float* g_c, float* std_, float* inv_std, float* wfix, uint16_t* wf_hi, uint16_t* wf_lo,
-                 float* b_eff, Ctrl* ctrl, hipStream_t s) {
+                 float* b_eff, Ctrl* ctrl, int nrb, hipStream_t s) {
   prep_kernel<<<(cfg.P + 255) / 256, 256, 0, s>>>(cfg, prm, acc, w_old, x, d, g_c, std_, inv_std, wfix, wf_hi,
-                                                  wf_lo, b_eff, ctrl);
+                                                  wf_lo, b_eff, ctrl, nrb);
 }
 
 // ---------------------------------------------------------------------------

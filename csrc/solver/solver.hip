@@ -35,7 +35,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   };
   const size_t o_prm = take(sizeof(SolveParams));
   const size_t o_ctrl = take(sizeof(Ctrl));
-  const size_t o_acc = take(2 * FP * sizeof(double));
+  const size_t o_acc = take((size_t)stats_row_blocks_ * 2 * FP * sizeof(double));
   const size_t o_dot = take((size_t)nwg_red * num_dots(cfg.hist) * sizeof(double));
   const size_t o_x = take(P * 4), o_d = take(P * 4), o_gc = take(P * 4), o_gt = take(P * 4);
   const size_t o_S = take(H * P * 4), o_Y = take(H * P * 4);
@@ -88,9 +88,9 @@ LocalSolver::~LocalSolver() {
 
 void LocalSolver::enqueue_body(hipStream_t s) {
   const SolverCfg& c = cfg_;
-  hip_check(hipMemsetAsync(acc_, 0, 2 * (size_t)c.Fp * sizeof(double), s), "memset(acc)");
   launch_stats(buf_.X, prm_, c.cap, c.Fp, acc_, stats_row_blocks_, s);
-  launch_prep(c, prm_, acc_, buf_.w_old, x_, d_, gc_, std_, inv_std_, wfix_, whi_, wlo_, beff_, ctrl_, s);
+  launch_prep(c, prm_, acc_, buf_.w_old, x_, d_, gc_, std_, inv_std_, wfix_, whi_, wlo_, beff_, ctrl_,
+              stats_row_blocks_, s);
   for (int slot = 0; slot < c.nslots; ++slot) {
     launch_eval(c, prm_, ctrl_, slot, buf_.X, buf_.y, whi_, wlo_, beff_, Gpart_, Rpart_, Lpart_, nwg_eval_, s);
     launch_reduce(c, prm_, ctrl_, slot, Gpart_, Rpart_, Lpart_, nwg_eval_, inv_std_, d_, gc_, gt_, S_, Y_, dotpart_,

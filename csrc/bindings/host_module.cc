@@ -195,8 +195,8 @@ PYBIND11_MODULE(_psx_host, m) {
 
   m.def("java_double", &java_double);
   py::class_<CsvLogger>(m, "CsvLogger")
-      .def(py::init<const std::string&, bool, bool>(), py::arg("path"), py::arg("worker_schema"),
-           py::arg("write_header") = true)
+      .def(py::init<const std::string&, bool, bool, bool>(), py::arg("path"), py::arg("worker_schema"),
+           py::arg("write_header") = true, py::arg("append") = false)
       .def("log_worker", &CsvLogger::log_worker)
       .def("log_server", &CsvLogger::log_server)
       .def("log_line", &CsvLogger::log_line)

@@ -42,11 +42,13 @@ std::string java_double(double v) {
   return neg ? "-" + out : out;
 }
 
-CsvLogger::CsvLogger(const std::string& path, bool worker_schema, bool write_header) {
+CsvLogger::CsvLogger(const std::string& path, bool worker_schema, bool write_header, bool append) {
   if (path.empty()) {
     f_ = stdout;
   } else {
-    f_ = std::fopen(path.c_str(), "w");
+    // append mode: several worker processes share one file; every write() is
+    // a run of whole lines on an O_APPEND descriptor, so lines never interleave
+    f_ = std::fopen(path.c_str(), append ? "a" : "w");
     if (!f_) throw std::runtime_error("cannot open log file " + path);
     own_ = true;
   }

@@ -24,7 +24,7 @@ std::string java_double(double v);
 class CsvLogger {
  public:
   // path empty => stdout.  `worker_schema` selects the 7-column header.
-  CsvLogger(const std::string& path, bool worker_schema, bool write_header);
+  CsvLogger(const std::string& path, bool worker_schema, bool write_header, bool append = false);
   ~CsvLogger();
   void log_worker(int64_t ts_ms, int64_t partition, int64_t vc, double loss, double f1, double acc,
                   int64_t tuples_seen);

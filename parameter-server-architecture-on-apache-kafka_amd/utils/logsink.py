@@ -32,11 +32,11 @@ class RecordBook:
 
 class LogSink:
     def __init__(self, K: int, device, worker_path: str | None = None, server_path: str | None = None,
-                 to_stdout: bool = False, pool: int = 64, keep_records: bool = True):
+                 to_stdout: bool = False, pool: int = 64, keep_records: bool = True, worker_append: bool = False):
         self.K = K
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
-        self.wlog = _native.host.CsvLogger(worker_path, True, True) if worker_path else (
+        self.wlog = _native.host.CsvLogger(worker_path, True, not worker_append, worker_append) if worker_path else (
             _native.host.CsvLogger("", True, False) if to_stdout else None)
         self.slog = _native.host.CsvLogger(server_path, False, True) if server_path else (
             _native.host.CsvLogger("", False, False) if to_stdout else None)

@@ -1,0 +1,116 @@
+"""Multi-process parameter server on CPU (gloo): the RCCL schedules' logic with
+world_size > 1, plus the ServerAppRunner/WorkerAppRunner pair as real processes."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, kw, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from psx.parallel.dist import DistEngine, init_from_env
+    from psx.runtime.config import PSConfig
+    from psx.utils.data import synth_finefood
+
+    r, w, dev = init_from_env(cpu=True)
+    cfg = PSConfig(**kw)
+    train, test = synth_finefood(1500, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
+    eng = DistEngine(cfg, r, w, dev, train=train, test=test)
+    out = eng.run()
+    if r == 0:
+        out_q.put((out, eng.server.w.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+BASE = dict(consistency_model=0, producer_time_per_event=0, stream_mode="per_iter", rows_per_iter=64, epochs=100,
+            max_iters=5, num_workers=3)
+
+
+def test_bsp_schedules_agree():
+    ws = {}
+    for sched in ("allreduce", "reduce_bcast", "sharded"):
+        out, w = _run(3, dict(BASE, bsp_schedule=sched))
+        assert out["rounds"] == 5 and out["updates"] == 15
+        ws[sched] = w
+    assert torch.allclose(ws["allreduce"], ws["reduce_bcast"], atol=1e-5)
+    assert torch.allclose(ws["allreduce"], ws["sharded"], atol=1e-5)
+
+
+def test_bsp_dedicated_server():
+    out, w = _run(3, dict(BASE, bsp_schedule="reduce_bcast", server_colocated=False))
+    assert out["updates"] == 10  # 2 worker ranks x 5 rounds
+
+
+@pytest.mark.parametrize("c", [-1, 2])
+def test_async_dedicated_server(c):
+    out, w = _run(3, dict(BASE, consistency_model=c, max_iters=6))
+    assert out["updates"] == 12
+    if c > 0:
+        assert out["max_vc_gap"] <= c + 1
+
+
+def test_app_runners_as_processes(tmp_path):
+    mock = "/root/reference/mockData/sample_input_data.csv"
+    if not os.path.exists(mock):
+        pytest.skip("reference mock data not mounted")
+    port = str(_free_port())
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    srv = subprocess.Popen([sys.executable, "-m", "psx.apps.server_app_runner", "-training", mock, "-test", mock,
+                            "-c", "0", "-p", "0", "--num_workers", "2", "--device", "cpu", "--max_iters", "4",
+                            "--master_port", port, "-l"], cwd=tmp_path, env=env)
+    wk = subprocess.run([sys.executable, "-m", "psx.apps.worker_app_runner", "-test", mock, "--num_workers", "2",
+                         "--device", "cpu", "--master_port", port, "-min", "8", "-max", "64"], cwd=tmp_path, env=env,
+                        timeout=240)
+    assert wk.returncode == 0
+    assert srv.wait(timeout=120) == 0
+    wl = (tmp_path / "logs-worker.csv").read_text().splitlines()
+    assert wl[0].endswith("numTuplesSeen") and len(wl) == 1 + 8
+    assert len((tmp_path / "logs-server.csv").read_text().splitlines()) == 1 + 4
+
+
+@pytest.mark.parametrize("args,code", [(["-h"], 0), (["stray"], 2), (["-c", "-2"], 2), (["--bogus"], 2)])
+def test_cli_exit_codes(args, code):
+    r = subprocess.run([sys.executable, "-m", "psx.apps.server_app_runner"] + args, cwd=ROOT, capture_output=True,
+                       text=True, timeout=120, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == code, r.stderr
+    if code in (0, 2) and args != ["-c", "-2"]:
+        assert "-training" in (r.stdout + r.stderr)
+
+
+def test_worker_cli_help():
+    r = subprocess.run([sys.executable, "-m", "psx.apps.worker_app_runner", "--help"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0 and "WorkerAppRunner" in r.stdout and "-bc" in r.stdout

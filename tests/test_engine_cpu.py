@@ -1,0 +1,93 @@
+"""In-process engine on CPU: BASELINE.json config #1 (sequential, 2 workers, mock data)
+and the asynchronous consistency models, checked from the logs the way the
+reference validated them."""
+import os
+
+import pytest
+import torch
+
+from psx.runtime.config import PSConfig
+from psx.runtime.engine import LocalEngine
+from psx.utils.checkpoint import load_server, save_server
+from psx.utils.data import synth_binary, synth_finefood
+
+MOCK = "/root/reference/mockData/sample_input_data.csv"
+
+
+def _mock_paths():
+    if os.path.exists(MOCK):
+        return MOCK, MOCK
+    pytest.skip("reference mock data not mounted")
+
+
+def test_config1_sequential_two_workers_mock(tmp_path):
+    tr, te = _mock_paths()
+    cfg = PSConfig(train_path=tr, test_path=te, num_workers=2, consistency_model=0, producer_time_per_event=0,
+                   max_iters=8, logging=True, log_dir=str(tmp_path))
+    out = LocalEngine(cfg, "cpu").run()
+    assert out["rounds"] == 8 and out["updates"] == 16
+    wl = (tmp_path / "logs-worker.csv").read_text().splitlines()
+    sl = (tmp_path / "logs-server.csv").read_text().splitlines()
+    assert wl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen"
+    assert sl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy"
+    assert len(wl) == 1 + 16 and len(sl) == 1 + 8
+    rows = [r.split(";") for r in wl[1:]]
+    assert {r[1] for r in rows} == {"0", "1"}
+    # each worker logs vector clocks 0..7 in order; numTuplesSeen = its shard (25 rows)
+    for k in ("0", "1"):
+        vcs = [int(r[2]) for r in rows if r[1] == k]
+        assert vcs == list(range(8))
+        assert all(int(r[6]) == 25 for r in rows if r[1] == k)
+    srows = [r.split(";") for r in sl[1:]]
+    assert all(r[1] == "-1" and r[3] == "-1" for r in srows)
+    assert float(srows[-1][5]) > 0.7  # mock data is nearly separable
+
+
+@pytest.mark.parametrize("c", [-1, 1, 3])
+def test_async_models_staleness(c):
+    train, test = synth_finefood(3000, num_features=128, seed=0), synth_finefood(300, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=3, consistency_model=c, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=64, epochs=100, max_iters=12, inject_worker_delay_ms={2: 15.0})
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    out = eng.run()
+    assert out["updates"] >= 36
+    if c > 0:
+        assert out["max_vc_gap"] <= c + 1
+    else:
+        assert out["max_vc_gap"] >= 2  # the straggler falls behind under eventual consistency
+
+
+def test_schedule_mode_arrival_burst():
+    """-p 200 with N=2: burst of 256 rows, then 5 rows per second in total."""
+    train, test = synth_finefood(2000, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=2, consistency_model=0, producer_time_per_event=200, max_iters=3)
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    eng.run()
+    for w in eng.workers:
+        assert 128 <= w.tuples_seen <= 140  # burst share + a few scheduled rows
+        assert w.window.size == min(w.tuples_seen, w.window.target_size())
+
+
+def test_checkpoint_roundtrip_and_resume(tmp_path):
+    train, test = synth_binary(200, 32, seed=0), synth_binary(50, 32, seed=1)
+    cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, max_iters=4,
+                   checkpoint_dir=str(tmp_path), checkpoint_every=2)
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    eng.run()
+    st = load_server(str(tmp_path))
+    assert st["updates"] == 4 and torch.equal(st["w"], eng.server.w)
+    cfg2 = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, max_iters=1,
+                    checkpoint_dir=str(tmp_path), resume=True)
+    eng2 = LocalEngine(cfg2, "cpu", train=train, test=test)
+    assert torch.equal(eng2.server.w, eng.server.w)
+    assert eng2.server.tracker.clocks() == [4]
+    save_server(str(tmp_path), eng2.server)
+
+
+def test_fault_injection_delay_slows_only_that_worker():
+    train, test = synth_finefood(2000, num_features=128, seed=0), synth_finefood(100, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=2, consistency_model=-1, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=32, epochs=100, max_iters=5, inject_worker_delay_ms={1: 40.0})
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    eng.run()
+    assert eng.workers[0].iters > eng.workers[1].iters

@@ -1,0 +1,93 @@
+"""Sliding-window buffer semantics (WorkerSamplingProcessor.java:50-135)."""
+import math
+
+import numpy as np
+import pytest
+
+from psx._native import host
+
+
+def java_target(deltas, bc, lo, hi):
+    mean = sum(deltas) / len(deltas) if deltas else 1000.0
+    per_min = 60000.0 / mean if mean > 0 else math.inf
+    v = math.floor(bc * per_min + 0.5) if math.isfinite(per_min) else hi
+    return max(lo, min(hi, v))
+
+
+def test_rate_estimator_window_of_500():
+    r = host.RateEstimator(500)
+    assert r.mean_interarrival_ms() == 1000.0  # default with no samples
+    t = 0.0
+    for i in range(700):
+        t += 10.0 if i < 600 else 20.0
+        r.arrival(t)
+    assert r.samples == 500
+    assert r.mean_interarrival_ms() == pytest.approx((400 * 10 + 100 * 20 - 0) / 500, rel=1e-9)
+
+
+def test_target_formula():
+    w = host.SlidingWindow(128, 1024, 0.3)
+    assert w.target_size() == java_target([], 0.3, 128, 1024)  # 0.3*60 = 18 -> clamp 128
+    times = np.cumsum(np.full(50, 5.0))  # 5 ms apart = 12000 events/min -> 3600 -> 1024
+    w.insert_many(times)
+    assert w.target_size() == 1024
+    w2 = host.SlidingWindow(1, 100000, 0.3)
+    w2.insert_many(np.cumsum(np.full(20, 40.0)))  # 1500/min -> 450
+    assert w2.target_size() == 450
+
+
+def reference_buffer(events, bc, lo, hi):
+    """Literal re-implementation of the reference's three cases over insertion ids."""
+    store = {}  # slot -> insertion id
+    deltas, last = [], None
+    for t in events:
+        if last is not None:
+            deltas.append(t - last)
+            deltas = deltas[-500:]
+        last = t
+        target = java_target(deltas, bc, lo, hi)
+        largest = max(store.values(), default=0)
+        size = len(store)
+        if size < target:
+            slot = min(set(range(hi)) - set(store))
+        elif size == target:
+            slot = min(store, key=store.get)
+        else:
+            order = sorted(store, key=store.get)
+            for s in order[: size - target]:
+                del store[s]
+            slot = order[size - target]
+        store[slot] = largest + 1
+    return sorted(store.values())
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_window_holds_most_recent_tuples(seed):
+    rng = np.random.default_rng(seed)
+    lo, hi, bc = 4, 40, 0.3
+    # alternate slow and fast phases so the target grows and shrinks
+    gaps = np.concatenate([rng.uniform(200, 400, 60), rng.uniform(5, 20, 80), rng.uniform(300, 900, 60)])
+    events = np.cumsum(gaps)
+    w = host.SlidingWindow(lo, hi, bc)
+    ids_ring = [None] * hi
+    for i, t in enumerate(events):
+        a = w.insert(float(t))
+        ids_ring[a.slot] = a.insertion_id
+        window_ids = sorted(ids_ring[(w.start + j) % hi] for j in range(w.size))
+        assert window_ids == list(range(a.insertion_id - w.size + 1, a.insertion_id + 1))
+    assert window_ids == reference_buffer(list(events), bc, lo, hi)
+
+
+def test_insert_many_consecutive_slots_and_wrap():
+    w = host.SlidingWindow(1, 8, 100.0)
+    slots = w.insert_many(np.arange(20, dtype=np.float64))
+    assert list(slots) == [i % 8 for i in range(20)]
+    assert w.tuples_seen == 20
+    assert w.head == 19 % 8
+
+
+def test_bad_arguments():
+    with pytest.raises(Exception):
+        host.SlidingWindow(10, 5, 0.3)
+    with pytest.raises(Exception):
+        host.SlidingWindow(1, 5, 0.0)

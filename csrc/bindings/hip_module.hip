@@ -111,6 +111,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              s.read_ctrl(&c, S(stream));
              return ctrl_dict(c, s.cfg().hist);
            })
+      .def("read_stamps", [](LocalSolver& s, uintptr_t stream) { return s.read_stamps(S(stream)); })
       .def_property_readonly("eval_wg", &LocalSolver::eval_wg)
       .def_property_readonly("kernels_per_solve", &LocalSolver::kernels_per_solve);
 

@@ -1,0 +1,44 @@
+// Fused local-solve kernels (see solve_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "solver_ctrl.h"
+
+namespace psx {
+
+// Device pointers of one solver instance (passed by value as a kernel argument).
+struct SolveDev {
+  const uint16_t* X;    // ring [cap][Fp] bf16
+  const int32_t* y;     // ring labels
+  const float* w_old;   // [P]
+  float *x, *d, *g_c;   // [P] iterate, direction, gradient at x
+  float *S, *Y;         // [hist][P] curvature pairs
+  float *std_, *inv_std;  // [Fp]
+  float* wfix;          // [P] frozen contributions (zero-variance features, non-Spark mode)
+  float* b_eff;         // [16] trial intercepts
+  uint16_t *whi, *wlo;  // trial weight fragments [16*Fp]
+  float *Gacc, *Racc, *Lacc;  // atomic accumulators (zero between slots)
+  // outputs
+  float* delta;
+  float* w_new;
+  uint16_t *out_hi, *out_lo;
+  float* b_fin;
+  float* loss;
+  int* stats;
+  // padded internal layout: KP classes (power of two >= K), feature stride FPI
+  int KP, FPI, PI, pad_;
+  long long* dbg;  // optional phase timeline (debug)
+};
+
+int padded_classes(int K);
+int padded_stride(int FP);
+void prepare_solve_kernels();
+size_t stats_prep_lds_bytes();
+size_t slot_lds_bytes(int FP);
+void launch_stats_prep(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s);
+void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
+void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
+                 hipStream_t s);
+
+}  // namespace psx

@@ -34,6 +34,14 @@ namespace psx {
 
 constexpr int kMaxHist = 16;
 
+// Workspace of the compact L-BFGS algebra.  On the device it lives in LDS (a
+// stack array would be scratch memory: each access an L1/L2 round trip for
+// the single controller thread).
+struct CtrlScratch {
+  int idx[kMaxHist];
+  double u[kMaxHist], v[kMaxHist], a[kMaxHist], rhs[kMaxHist], p[kMaxHist], dy[kMaxHist];
+};
+
 enum SolverMode : int { kModeLBFGS = 0, kModeGD = 1 };
 enum Phase : int { kPhInit = 0, kPhLS = 1, kPhDone = 2 };
 enum Action : int {
@@ -141,17 +149,17 @@ PSX_HD inline double ls_interp(double lt, double lf, double ld, double rt, doubl
 
 // Compact L-BFGS direction d = -H g for the current history.  Fills cg/cs/cy
 // and returns d . g.
-PSX_HD inline double ctrl_direction(Ctrl& c, int H) {
+PSX_HD inline double ctrl_direction(Ctrl& c, int H, CtrlScratch& ws) {
   for (int i = 0; i < kMaxHist; ++i) c.cs[i] = c.cy[i] = 0.0;
   const int m = c.m;
   if (m == 0) {
     c.cg = -1.0;
     return -c.gg_c;
   }
-  int idx[kMaxHist];  // logical (oldest..newest) -> physical
+  int* idx = ws.idx;  // logical (oldest..newest) -> physical
   for (int i = 0; i < m; ++i) idx[i] = ((c.head - (m - 1 - i)) % H + H) % H;
   const double gamma = c.gamma;
-  double u[kMaxHist], v[kMaxHist], a[kMaxHist], rhs[kMaxHist], p[kMaxHist];
+  double *u = ws.u, *v = ws.v, *a = ws.a, *rhs = ws.rhs, *p = ws.p;
   for (int i = 0; i < m; ++i) {
     u[i] = c.Sg[idx[i]];
     v[i] = c.Yg[idx[i]];
@@ -189,7 +197,8 @@ PSX_HD inline double ctrl_direction(Ctrl& c, int H) {
 
 // Accept the evaluated trial point (step t_eval): bookkeeping of the new
 // curvature pair and the next direction.  `dots` as produced by the reduction.
-PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot) {
+PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot,
+                               CtrlScratch& ws) {
   const int H = cfg.hist;
   const double tt = dots[0], td = dots[1], tc = dots[2];
   const double t = c.t;
@@ -224,10 +233,10 @@ PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const 
   }
   // --- new curvature pair s = t d, y = g_t - g_c ---
   const int m = c.m;
-  int idx[kMaxHist];
+  int* idx = ws.idx;
   for (int i = 0; i < m; ++i) idx[i] = ((c.head - (m - 1 - i)) % H + H) % H;
   // d . y_j for the stored pairs (d is known through its coefficients)
-  double dy[kMaxHist];
+  double* dy = ws.dy;
   for (int jj = 0; jj < m; ++jj) {
     int j = idx[jj];
     double s = c.cg * c.Yg[j];
@@ -272,12 +281,12 @@ PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const 
     }
   }
   c.gg_c = tt;
-  double dg = ctrl_direction(c, H);
+  double dg = ctrl_direction(c, H, ws);
   if (!(dg < 0.0)) {  // not a descent direction: drop the history, steepest descent
     c.m = 0;
     c.head = -1;
     c.dir_reset += 1;
-    dg = ctrl_direction(c, H);
+    dg = ctrl_direction(c, H, ws);
   }
   c.dg0 = dg;
   c.t = 1.0;
@@ -291,7 +300,8 @@ PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const 
 
 // Advance the state machine after the function evaluation of `slot`.
 // f_t = objective at the trial point, dots as documented above.
-PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot) {
+PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot,
+                             CtrlScratch& ws) {
   c.evals += 1;
   const double tt = dots[0], td = dots[1];
   const bool finite = f_t == f_t && fabs(f_t) < 1e300;
@@ -325,7 +335,7 @@ PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const do
   // ---- line search on phi(t) = f(x + t d) ----
   c.action_slot = slot;
   if (cfg.mode == kModeGD) {
-    ctrl_accept(c, cfg, f_t, dots, slot);
+    ctrl_accept(c, cfg, f_t, dots, slot, ws);
     return;
   }
   const double c1 = 1e-4, c2 = 0.9;
@@ -342,7 +352,7 @@ PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const do
       c.zoom = 1;
       tn = ls_interp(c.lo_t, c.lo_f, c.lo_d, c.hi_t, c.hi_f, c.hi_d);
     } else if (fabs(dd) <= c2 * fabs(c.dg0)) {
-      ctrl_accept(c, cfg, f_t, dots, slot);
+      ctrl_accept(c, cfg, f_t, dots, slot, ws);
       return;
     } else if (dd >= 0.0) {
       c.hi_t = c.lo_t; c.hi_f = c.lo_f; c.hi_d = c.lo_d;
@@ -358,7 +368,7 @@ PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const do
       c.hi_t = t; c.hi_f = f_t; c.hi_d = dd;
     } else {
       if (fabs(dd) <= c2 * fabs(c.dg0)) {
-        ctrl_accept(c, cfg, f_t, dots, slot);
+        ctrl_accept(c, cfg, f_t, dots, slot, ws);
         return;
       }
       if (dd * (c.hi_t - c.lo_t) >= 0.0) {
@@ -372,7 +382,7 @@ PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const do
   if (c.ls_i >= cfg.ls_max || out_of_slots) {
     c.ls_fail += 1;
     if (armijo && f_t < c.f_c) {  // settle for sufficient decrease
-      ctrl_accept(c, cfg, f_t, dots, slot);
+      ctrl_accept(c, cfg, f_t, dots, slot, ws);
       if (out_of_slots && c.phase != kPhDone) {
         c.action = kActAcceptDone;
         c.phase = kPhDone;
@@ -385,6 +395,12 @@ PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const do
   }
   c.t = tn;
   c.action = kActTrial;
+}
+
+// Convenience overload with a stack workspace (host code, tests).
+PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot) {
+  CtrlScratch ws;
+  ctrl_step(c, cfg, f_t, dots, slot, ws);
 }
 
 }  // namespace psx

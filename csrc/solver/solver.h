@@ -3,19 +3,20 @@
 // The reference runs, per worker iteration, a Spark job: build a DataFrame from
 // the buffer, fit(), evaluate on the test set, diff the coefficients
 // (reference: LogisticRegressionTaskSpark.java:142-221).  Here the whole chain
-//   set_params -> stats -> prep -> [eval -> reduce/ctrl -> update] x nslots
-//   -> finalize
-// is captured ONCE into a hipGraph and replayed per iteration: the host pays
-// one graph launch (~10 us) and the device runs the chain back to back with no
-// host synchronisation; line-search control flow is resolved on device and
-// unused evaluation slots exit immediately.
+//   set_params -> stats_prep -> slot_0 ... slot_{nslots-1}
+// (each slot = one fused evaluation + controller step, see
+// csrc/kernels/solve_kernels.hip) is captured ONCE into a hipGraph and
+// replayed per iteration: the host pays one graph launch and the device runs
+// the chain back to back with no host synchronisation; line-search control
+// flow is resolved on device and slots after convergence exit immediately.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <string>
+#include <vector>
 
 #include "../kernels/lr_kernels.h"
+#include "../kernels/solve_kernels.h"
 
 namespace psx {
 
@@ -44,28 +45,23 @@ class LocalSolver {
   void run(int B, int start, hipStream_t stream);
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
-  int kernels_per_solve() const { return 4 + 3 * cfg_.nslots + 1; }
+  int kernels_per_solve() const { return 3 + cfg_.nslots; }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
+  // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):
+  // [slot][k] s_memrealtime ticks (100 MHz); empty when disabled.
+  std::vector<long long> read_stamps(hipStream_t stream);
 
  private:
   void enqueue_body(hipStream_t s);
   SolverCfg cfg_;
-  SolverBuffers buf_;
+  SolveDev dv_{};
   int nwg_eval_;
-  int stats_row_blocks_;
   bool use_graph_;
-  // workspace
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;
   SolveParams* prm_ = nullptr;
   Ctrl* ctrl_ = nullptr;
-  double* acc_ = nullptr;
-  double* dotpart_ = nullptr;
-  float *x_ = nullptr, *d_ = nullptr, *gc_ = nullptr, *gt_ = nullptr, *S_ = nullptr, *Y_ = nullptr;
-  float *std_ = nullptr, *inv_std_ = nullptr, *wfix_ = nullptr, *beff_ = nullptr;
-  uint16_t *whi_ = nullptr, *wlo_ = nullptr;
-  float *Gpart_ = nullptr, *Rpart_ = nullptr, *Lpart_ = nullptr;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;

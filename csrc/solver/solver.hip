@@ -1,5 +1,6 @@
 #include "solver.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -12,21 +13,22 @@ void hip_check(hipError_t e, const char* what) {
 static size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max_eval_wg, bool use_graph)
-    : cfg_(cfg), buf_(buf), use_graph_(use_graph) {
+    : cfg_(cfg), use_graph_(use_graph) {
   if (!fp_supported(cfg.Fp)) throw std::invalid_argument("unsupported padded feature width " + std::to_string(cfg.Fp));
   if (cfg.K < 2 || cfg.K > 16) throw std::invalid_argument("num classes (incl. phantom) must be in [2,16]");
   if (cfg.P != cfg.K * cfg.Fp + cfg.K) throw std::invalid_argument("P mismatch");
   if (cfg.hist < 1 || cfg.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
   if (cfg.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
+  if (cfg.cap < 1) throw std::invalid_argument("ring capacity must be >= 1");
   const int tiles = (cfg.cap + kTileRows - 1) / kTileRows;
   nwg_eval_ = tiles < max_eval_wg ? tiles : max_eval_wg;
   if (nwg_eval_ < 1) nwg_eval_ = 1;
-  stats_row_blocks_ = (cfg.cap + 127) / 128;
-  if (stats_row_blocks_ > 64) stats_row_blocks_ = 64;
-  if (stats_row_blocks_ < 1) stats_row_blocks_ = 1;
 
-  const size_t P = cfg.P, FP = cfg.Fp, H = cfg.hist;
-  const int nwg_red = (cfg.P + 255) / 256;
+  // solver-private vectors use the padded layout of solve_kernels.hip
+  dv_.KP = padded_classes(cfg.K);
+  dv_.FPI = padded_stride(cfg.Fp);
+  dv_.PI = dv_.KP * dv_.FPI + 16;
+  const size_t PI = dv_.PI, FPI = dv_.FPI, FP = cfg.Fp, H = cfg.hist;
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -35,41 +37,46 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   };
   const size_t o_prm = take(sizeof(SolveParams));
   const size_t o_ctrl = take(sizeof(Ctrl));
-  const size_t o_acc = take((size_t)stats_row_blocks_ * 2 * FP * sizeof(double));
-  const size_t o_dot = take((size_t)nwg_red * num_dots(cfg.hist) * sizeof(double));
-  const size_t o_x = take(P * 4), o_d = take(P * 4), o_gc = take(P * 4), o_gt = take(P * 4);
-  const size_t o_S = take(H * P * 4), o_Y = take(H * P * 4);
-  const size_t o_std = take(FP * 4), o_istd = take(FP * 4), o_wfix = take(P * 4), o_beff = take(16 * 4);
+  const size_t o_x = take(PI * 4), o_d = take(PI * 4), o_gc = take(PI * 4);
+  const size_t o_S = take(H * PI * 4), o_Y = take(H * PI * 4);
+  const size_t o_std = take(FPI * 4), o_istd = take(FPI * 4), o_wfix = take(PI * 4), o_beff = take(16 * 4);
   const size_t o_whi = take(16 * FP * 2), o_wlo = take(16 * FP * 2);
-  const size_t o_G = take((size_t)nwg_eval_ * cfg.K * FP * 4);
-  const size_t o_R = take((size_t)nwg_eval_ * 16 * 4);
-  const size_t o_L = take((size_t)nwg_eval_ * 4);
+  const size_t o_G = take((size_t)dv_.KP * FPI * 4), o_R = take(16 * 4), o_L = take(16);
+  const bool stamps = std::getenv("PSX_SOLVER_STAMPS") != nullptr;
+  const size_t o_dbg = stamps ? take(32 * 16 * sizeof(long long)) : 0;
   ws_bytes_ = off;
   hip_check(hipMalloc(&ws_, ws_bytes_), "hipMalloc(solver workspace)");
   hip_check(hipMemset(ws_, 0, ws_bytes_), "hipMemset(solver workspace)");
   char* b = static_cast<char*>(ws_);
   prm_ = reinterpret_cast<SolveParams*>(b + o_prm);
   ctrl_ = reinterpret_cast<Ctrl*>(b + o_ctrl);
-  acc_ = reinterpret_cast<double*>(b + o_acc);
-  dotpart_ = reinterpret_cast<double*>(b + o_dot);
-  x_ = reinterpret_cast<float*>(b + o_x);
-  d_ = reinterpret_cast<float*>(b + o_d);
-  gc_ = reinterpret_cast<float*>(b + o_gc);
-  gt_ = reinterpret_cast<float*>(b + o_gt);
-  S_ = reinterpret_cast<float*>(b + o_S);
-  Y_ = reinterpret_cast<float*>(b + o_Y);
-  std_ = reinterpret_cast<float*>(b + o_std);
-  inv_std_ = reinterpret_cast<float*>(b + o_istd);
-  wfix_ = reinterpret_cast<float*>(b + o_wfix);
-  beff_ = reinterpret_cast<float*>(b + o_beff);
-  whi_ = reinterpret_cast<uint16_t*>(b + o_whi);
-  wlo_ = reinterpret_cast<uint16_t*>(b + o_wlo);
-  Gpart_ = reinterpret_cast<float*>(b + o_G);
-  Rpart_ = reinterpret_cast<float*>(b + o_R);
-  Lpart_ = reinterpret_cast<float*>(b + o_L);
+  dv_.X = buf.X;
+  dv_.y = buf.y;
+  dv_.w_old = buf.w_old;
+  dv_.x = reinterpret_cast<float*>(b + o_x);
+  dv_.d = reinterpret_cast<float*>(b + o_d);
+  dv_.g_c = reinterpret_cast<float*>(b + o_gc);
+  dv_.S = reinterpret_cast<float*>(b + o_S);
+  dv_.Y = reinterpret_cast<float*>(b + o_Y);
+  dv_.std_ = reinterpret_cast<float*>(b + o_std);
+  dv_.inv_std = reinterpret_cast<float*>(b + o_istd);
+  dv_.wfix = reinterpret_cast<float*>(b + o_wfix);
+  dv_.b_eff = reinterpret_cast<float*>(b + o_beff);
+  dv_.whi = reinterpret_cast<uint16_t*>(b + o_whi);
+  dv_.wlo = reinterpret_cast<uint16_t*>(b + o_wlo);
+  dv_.Gacc = reinterpret_cast<float*>(b + o_G);
+  dv_.Racc = reinterpret_cast<float*>(b + o_R);
+  dv_.Lacc = reinterpret_cast<float*>(b + o_L);
+  dv_.delta = buf.delta;
+  dv_.w_new = buf.w_new;
+  dv_.out_hi = buf.wf_hi;
+  dv_.out_lo = buf.wf_lo;
+  dv_.b_fin = buf.b_fin;
+  dv_.loss = buf.loss;
+  dv_.stats = buf.stats;
+  dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
 
-  // >64 KiB dynamic LDS for the wide tiles (gfx950 has 160 KiB per CU)
-  prepare_kernels();
+  prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
@@ -87,18 +94,9 @@ LocalSolver::~LocalSolver() {
 }
 
 void LocalSolver::enqueue_body(hipStream_t s) {
-  const SolverCfg& c = cfg_;
-  launch_stats(buf_.X, prm_, c.cap, c.Fp, acc_, stats_row_blocks_, s);
-  launch_prep(c, prm_, acc_, buf_.w_old, x_, d_, gc_, std_, inv_std_, wfix_, whi_, wlo_, beff_, ctrl_,
-              stats_row_blocks_, s);
-  for (int slot = 0; slot < c.nslots; ++slot) {
-    launch_eval(c, prm_, ctrl_, slot, buf_.X, buf_.y, whi_, wlo_, beff_, Gpart_, Rpart_, Lpart_, nwg_eval_, s);
-    launch_reduce(c, prm_, ctrl_, slot, Gpart_, Rpart_, Lpart_, nwg_eval_, inv_std_, d_, gc_, gt_, S_, Y_, dotpart_,
-                  s);
-    launch_update(c, ctrl_, slot, x_, d_, gc_, gt_, S_, Y_, inv_std_, wfix_, whi_, wlo_, beff_, s);
-  }
-  launch_finalize(c, ctrl_, x_, inv_std_, wfix_, buf_.w_old, buf_.delta, buf_.w_new, buf_.wf_hi, buf_.wf_lo,
-                  buf_.b_fin, buf_.loss, buf_.stats, s);
+  launch_stats_prep(cfg_, prm_, dv_, ctrl_, s);
+  for (int slot = 0; slot < cfg_.nslots; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
+  launch_finalize(cfg_, ctrl_, dv_, s);
   hip_check(hipGetLastError(), "solver kernel launch");
 }
 
@@ -111,6 +109,16 @@ void LocalSolver::run(int B, int start, hipStream_t stream) {
   } else {
     enqueue_body(stream);
   }
+}
+
+std::vector<long long> LocalSolver::read_stamps(hipStream_t stream) {
+  std::vector<long long> v;
+  if (!dv_.dbg) return v;
+  v.resize(32 * 16);
+  hip_check(hipMemcpyAsync(v.data(), dv_.dbg, v.size() * sizeof(long long), hipMemcpyDeviceToHost, stream),
+            "read stamps");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v;
 }
 
 void LocalSolver::read_ctrl(Ctrl* out, hipStream_t stream) {

@@ -102,7 +102,10 @@ def test_graph_and_eager_agree(cuda):
             op.run(ring.X, ring.y, 512, 100, w)
         torch.cuda.synchronize()
         outs.append(op.delta.clone())
-    assert torch.equal(outs[0], outs[1])
+    # the gradient sums use fp32 atomics (arrival order varies), so replays agree
+    # to rounding, not bitwise
+    scale = outs[0].abs().max().item()
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * scale
 
 
 def test_confusion_matches_cpu(cuda):

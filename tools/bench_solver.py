@@ -1,0 +1,102 @@
+"""Micro-benchmark of the worker local solve on one GPU (device time per solve).
+
+Variants isolate the cost of: the stats/prep kernel, one active slot (eval +
+tail), empty slots, and the buffer size.  Usage: python tools/bench_solver.py
+"""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from psx.models.logreg import ModelSpec  # noqa: E402
+from psx.ops.lr import LocalSolveOp, SolverOptions  # noqa: E402
+from psx.runtime.buffer import DeviceRing  # noqa: E402
+from psx.utils.data import synth_finefood  # noqa: E402
+
+
+def time_solve(op, ring, B, w, reps=200):
+    for _ in range(10):
+        op.run(ring.X, ring.y, B, 0, w)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        op.run(ring.X, ring.y, B, 0, w)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def stamps(B=1024, opts=None):
+    """Phase timeline of one solve (needs PSX_SOLVER_STAMPS=1)."""
+    import os
+
+    os.environ["PSX_SOLVER_STAMPS"] = "1"
+    dev = "cuda:0"
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(1024, seed=0)
+    ring = DeviceRing(1024, spec.Fp, dev)
+    ring.X.copy_(ds.X.to(dev))
+    ring.y.copy_(ds.y.to(dev))
+    w = spec.init("random", seed=1).to(dev)
+    op = LocalSolveOp(spec, 1024, dev, opts or SolverOptions())
+    for _ in range(5):
+        op.run(ring.X, ring.y, B, 0, w)
+    torch.cuda.synchronize()
+    h = torch.cuda.current_stream().cuda_stream
+    st = op._native.read_stamps(h)
+    names = ["eval0", "eval0_end", "tail", "swapped", "dots", "ctrl", "updated", "written", "end", "staged",
+             "fwd", "softmax", "bwd"]
+    order = [0, 9, 10, 11, 12, 1, 2, 3, 4, 5, 6, 7, 8]
+    print(f"--- stamps B={B} (us, relative to slot 0 start; 100 MHz) ---")
+    base = st[0]
+    for slot in range(op.opts.nslots):
+        row = st[slot * 16: slot * 16 + 13]
+        if row[0] == 0 or row[0] < base:
+            continue
+        print(f"slot {slot}: " + " ".join(f"{names[k]}={(row[k] - base) / 100.0:.2f}" for k in order
+                                          if row[k] >= base))
+
+
+def main():
+    if "--stamps" in sys.argv:
+        stamps(1024)
+        stamps(32)
+        return
+    dev = "cuda:0"
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(1024, seed=0)
+    ring = DeviceRing(1024, spec.Fp, dev)
+    ring.X.copy_(ds.X.to(dev))
+    ring.y.copy_(ds.y.to(dev))
+    w = spec.init("random", seed=1).to(dev)
+    rows = []
+    for name, opts, B in [
+        ("default lbfgs x2 (9 slots)", SolverOptions(), 1024),
+        ("lbfgs x2, ls_max=2 (5 slots)", SolverOptions(ls_max=2), 1024),
+        ("init only (1 slot)", SolverOptions(iters=1, ls_max=0), 1024),
+        ("gd x1 (2 slots)", SolverOptions(mode="gd", iters=1), 1024),
+        ("gd x4 (5 slots)", SolverOptions(mode="gd", iters=4), 1024),
+        ("default, B=32 (1 tile)", SolverOptions(), 32),
+        ("init only, B=32", SolverOptions(iters=1, ls_max=0), 32),
+        ("default, no graph", SolverOptions(use_graph=False), 1024),
+    ]:
+        op = LocalSolveOp(spec, 1024, dev, opts)
+        us = time_solve(op, ring, B, w)
+        st = op.stats.cpu().tolist()
+        rows.append((name, us, st))
+        print(f"{name:32s} {us:9.2f} us/solve  stats(evals,acc,lsfail,reset)={st}", flush=True)
+    # host-side cost of one graph launch (no sync)
+    op = LocalSolveOp(spec, 1024, dev, SolverOptions())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        op.run(ring.X, ring.y, 1024, 0, w)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f"host enqueue per solve: {(t1 - t0) / 200 * 1e6:.1f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -85,11 +85,12 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("tol", &SolverCfg::tol);
 
   py::class_<LocalSolver>(m, "LocalSolver")
-      .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t y, uintptr_t w_old, uintptr_t delta,
-                       uintptr_t w_new, uintptr_t wf_hi, uintptr_t wf_lo, uintptr_t b_fin, uintptr_t loss,
-                       uintptr_t stats, int max_eval_wg, bool use_graph) {
+      .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t XT, uintptr_t y, uintptr_t w_old,
+                       uintptr_t delta, uintptr_t w_new, uintptr_t wf_hi, uintptr_t wf_lo, uintptr_t b_fin,
+                       uintptr_t loss, uintptr_t stats, int max_eval_wg, bool use_graph) {
              SolverBuffers b;
              b.X = P<const uint16_t>(X);
+             b.XT = P<const uint16_t>(XT);
              b.y = P<const int32_t>(y);
              b.w_old = P<const float>(w_old);
              b.delta = P<float>(delta);
@@ -101,7 +102,8 @@ PYBIND11_MODULE(_psx_hip, m) {
              b.stats = P<int>(stats);
              return std::make_unique<LocalSolver>(cfg, b, max_eval_wg, use_graph);
            }),
-           py::arg("cfg"), py::arg("X"), py::arg("y"), py::arg("w_old"), py::arg("delta"), py::arg("w_new"),
+           py::arg("cfg"), py::arg("X"), py::arg("XT"), py::arg("y"), py::arg("w_old"), py::arg("delta"),
+           py::arg("w_new"),
            py::arg("wf_hi"), py::arg("wf_lo"), py::arg("b_fin"), py::arg("loss"), py::arg("stats"),
            py::arg("max_eval_wg") = 512, py::arg("use_graph") = true)
       .def("run", [](LocalSolver& s, int B, int start, uintptr_t stream) { s.run(B, start, S(stream)); })
@@ -141,9 +143,10 @@ PYBIND11_MODULE(_psx_hip, m) {
     hip_check(hipGetLastError(), "make_fragments launch");
   });
   m.def("ring_ingest", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
-                          uintptr_t ring, uintptr_t yring, int64_t dst_first, int64_t cap, int FP, uintptr_t stream) {
+                          uintptr_t ring, uintptr_t ringT, uintptr_t yring, int64_t dst_first, int64_t cap, int FP,
+                          uintptr_t stream) {
     launch_ring_ingest(P<const uint16_t>(src), P<const int32_t>(ysrc), src_first, src_step, n, P<uint16_t>(ring),
-                       P<int32_t>(yring), dst_first, cap, FP, S(stream));
+                       P<uint16_t>(ringT), P<int32_t>(yring), dst_first, cap, FP, S(stream));
     hip_check(hipGetLastError(), "ring_ingest launch");
   });
 }

@@ -50,8 +50,8 @@ PYBIND11_MODULE(_psx_host, m) {
       .def_readonly("target", &SlotAssignment::target);
 
   py::class_<SlidingWindow>(m, "SlidingWindow")
-      .def(py::init<int64_t, int64_t, double, int>(), py::arg("min_size"), py::arg("max_size"),
-           py::arg("buffer_coefficient"), py::arg("rate_window") = 500)
+      .def(py::init<int64_t, int64_t, double, int, int64_t>(), py::arg("min_size"), py::arg("max_size"),
+           py::arg("buffer_coefficient"), py::arg("rate_window") = 500, py::arg("ring_capacity") = 0)
       .def("target_size", &SlidingWindow::target_size)
       .def("insert", &SlidingWindow::insert)
       .def("insert_many",
@@ -64,6 +64,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("restore", &SlidingWindow::restore)
       .def_property_readonly("size", &SlidingWindow::size)
       .def_property_readonly("capacity", &SlidingWindow::capacity)
+      .def_property_readonly("max_size", &SlidingWindow::max_size)
       .def_property_readonly("head", &SlidingWindow::head)
       .def_property_readonly("start", &SlidingWindow::start)
       .def_property_readonly("tuples_seen", &SlidingWindow::tuples_seen)

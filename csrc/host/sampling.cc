@@ -25,8 +25,9 @@ double RateEstimator::mean_interarrival_ms() const {
   return sum_ / static_cast<double>(deltas_.size());
 }
 
-SlidingWindow::SlidingWindow(int64_t min_size, int64_t max_size, double bc, int rate_window)
-    : min_(min_size), max_(max_size), bc_(bc), rate_(rate_window) {
+SlidingWindow::SlidingWindow(int64_t min_size, int64_t max_size, double bc, int rate_window, int64_t ring_capacity)
+    : min_(min_size), max_(max_size), cap_(ring_capacity > max_size ? ring_capacity : max_size), bc_(bc),
+      rate_(rate_window) {
   if (min_size <= 0 || max_size <= 0 || min_size > max_size)
     throw std::invalid_argument("need 0 < min_buffer_size <= max_buffer_size");
   if (!(bc > 0.0)) throw std::invalid_argument("buffer_size_coefficient must be > 0");
@@ -49,7 +50,7 @@ SlotAssignment SlidingWindow::insert(double now_ms) {
     size_ += 1;
   else
     size_ = target;
-  head_ = (head_ + 1) % max_;
+  head_ = (head_ + 1) % cap_;
   seen_ += 1;
   return SlotAssignment{head_, seen_, size_, target};
 }
@@ -66,11 +67,11 @@ int64_t SlidingWindow::insert_many(const double* now_ms, int64_t n, int64_t* slo
 
 int64_t SlidingWindow::start() const {
   if (size_ == 0) return 0;
-  return ((head_ - size_ + 1) % max_ + max_) % max_;
+  return ((head_ - size_ + 1) % cap_ + cap_) % cap_;
 }
 
 void SlidingWindow::restore(int64_t head, int64_t size, int64_t seen) {
-  if (size < 0 || size > max_ || head < -1 || head >= max_) throw std::invalid_argument("bad window state");
+  if (size < 0 || size > max_ || head < -1 || head >= cap_) throw std::invalid_argument("bad window state");
   head_ = head;
   size_ = size;
   seen_ = seen;

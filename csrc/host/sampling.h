@@ -10,7 +10,7 @@
 //   * the buffer always holds the s most recent tuples, with
 //       s <- min(s + 1, target)  if s < target   (case I: fill an empty slot)
 //       s <- target              otherwise       (cases II/III: overwrite / shrink)
-// Here that becomes O(1) ring arithmetic: the device ring has capacity `max`,
+// Here that becomes O(1) ring arithmetic: the device ring has capacity >= `max`,
 // the newest tuple lands at `head`, and the trainable window is the `size`
 // slots ending at head.  No per-tuple scan.
 #pragma once
@@ -46,7 +46,10 @@ struct SlotAssignment {
 
 class SlidingWindow {
  public:
-  SlidingWindow(int64_t min_size, int64_t max_size, double buffer_coefficient, int rate_window = 500);
+  // ring_capacity (>= max_size; 0 = max_size): modulus of the slot ring, which
+  // the device side rounds up to whole 32-row tiles.
+  SlidingWindow(int64_t min_size, int64_t max_size, double buffer_coefficient, int rate_window = 500,
+                int64_t ring_capacity = 0);
 
   // Target size for the current arrival rate.
   int64_t target_size() const;
@@ -57,7 +60,8 @@ class SlidingWindow {
   int64_t insert_many(const double* now_ms, int64_t n, int64_t* slots_out);
 
   int64_t size() const { return size_; }
-  int64_t capacity() const { return max_; }
+  int64_t capacity() const { return cap_; }  // ring modulus
+  int64_t max_size() const { return max_; }
   int64_t head() const { return head_; }  // slot of the newest tuple (-1 when empty)
   // First slot of the window: the window is [start, start+size) modulo capacity.
   int64_t start() const;
@@ -67,7 +71,7 @@ class SlidingWindow {
   void restore(int64_t head, int64_t size, int64_t seen);
 
  private:
-  int64_t min_, max_;
+  int64_t min_, max_, cap_;
   double bc_;
   RateEstimator rate_;
   int64_t head_ = -1;

@@ -27,7 +27,9 @@ void launch_make_fragments(int K, int F, int FP, const float* w, uint16_t* wf_hi
                            hipStream_t s);
 // Copy n rows (row i of the batch = src row src_first + i*src_step) into ring
 // slots (dst_first + i) % cap, labels alongside.
+// ringT (optional): feature-major copy [FP][cap] kept in step with the ring.
 void launch_ring_ingest(const uint16_t* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
-                        uint16_t* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s);
+                        uint16_t* ring, uint16_t* ringT, int32_t* yring, int64_t dst_first, int64_t cap, int FP,
+                        hipStream_t s);
 
 }  // namespace psx

@@ -185,29 +185,43 @@ void launch_make_fragments(int K, int F, int FP, const float* w, uint16_t* wf_hi
 
 // ---------------------------------------------------------------------------
 // K1/K10: ring ingest (gather of round-robin rows into consecutive ring slots).
+// Rows land in the row-major ring (16-B chunks) and, when XT is given, in the
+// feature-major copy: each thread owns one 8-feature chunk of one row and
+// writes its 8 values to 8 feature rows of XT (the bwd/stats kernels then read
+// every 32-feature slice of a window contiguously).
 __global__ __launch_bounds__(256) void ring_ingest_kernel(const uint16_t* __restrict__ src,
                                                           const int32_t* __restrict__ ysrc, int64_t src_first,
                                                           int64_t src_step, int64_t n, uint16_t* ring,
-                                                          int32_t* yring, int64_t dst_first, int64_t cap, int FP) {
+                                                          uint16_t* ringT, int32_t* yring, int64_t dst_first,
+                                                          int64_t cap, int FP) {
   const int CPR = FP / 8;
   const int64_t total = n * CPR;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-    const int64_t i = q / CPR;
-    const int cg = (int)(q - i * CPR);
+    // consecutive threads take consecutive ROWS of one chunk, so the 2-B XT
+    // stores of a wave land in contiguous runs of each feature row
+    const int cg = (int)(q / n);
+    const int64_t i = q - (int64_t)cg * n;
     const int64_t sr = src_first + i * src_step;
     const int64_t dr = (dst_first + i) % cap;
-    *(u16x8*)(ring + dr * FP + cg * 8) = *(const u16x8*)(src + sr * FP + cg * 8);
+    const u16x8 v = *(const u16x8*)(src + sr * FP + cg * 8);
+    *(u16x8*)(ring + dr * FP + cg * 8) = v;
+    if (ringT) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ringT[(int64_t)(cg * 8 + e) * cap + dr] = v[e];
+    }
     if (cg == 0) yring[dr] = ysrc[sr];
   }
 }
 
 void launch_ring_ingest(const uint16_t* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
-                        uint16_t* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s) {
+                        uint16_t* ring, uint16_t* ringT, int32_t* yring, int64_t dst_first, int64_t cap, int FP,
+                        hipStream_t s) {
   if (n <= 0) return;
   const int64_t total = n * (FP / 8);
   int64_t grid = (total + 255) / 256;
   if (grid > 2048) grid = 2048;
-  ring_ingest_kernel<<<(int)grid, 256, 0, s>>>(src, ysrc, src_first, src_step, n, ring, yring, dst_first, cap, FP);
+  ring_ingest_kernel<<<(int)grid, 256, 0, s>>>(src, ysrc, src_first, src_step, n, ring, ringT, yring, dst_first, cap,
+                                               FP);
 }
 
 // ---------------------------------------------------------------------------

@@ -10,6 +10,7 @@ namespace psx {
 // Device pointers of one solver instance (passed by value as a kernel argument).
 struct SolveDev {
   const uint16_t* X;    // ring [cap][Fp] bf16
+  const uint16_t* XT;   // the same ring feature-major [Fp][cap] (cap % 32 == 0)
   const int32_t* y;     // ring labels
   const float* w_old;   // [P]
   float *x, *d, *g_c;   // [P] iterate, direction, gradient at x
@@ -18,7 +19,9 @@ struct SolveDev {
   float* wfix;          // [P] frozen contributions (zero-variance features, non-Spark mode)
   float* b_eff;         // [16] trial intercepts
   uint16_t *whi, *wlo;  // trial weight fragments [16*Fp]
-  float *Gacc, *Racc, *Lacc;  // atomic accumulators (zero between slots)
+  unsigned short* R;          // [tiles][2][16][32] bf16 hi/lo residuals (fwd -> bwd)
+  float* part;                // [fwd grid][32] per-workgroup intercept-gradient / loss partials
+  unsigned long long* xch;    // bwd_update_kernel cross-workgroup exchange words
   // outputs
   float* delta;
   float* w_new;
@@ -35,7 +38,10 @@ int padded_classes(int K);
 int padded_stride(int FP);
 void prepare_solve_kernels();
 size_t stats_prep_lds_bytes();
-size_t slot_lds_bytes(int FP);
+size_t fwd_lds_bytes(int FP);
+size_t bwd_lds_bytes();
+int bwd_grid(int FP);
+int xch_words();
 void launch_stats_prep(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s);
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,

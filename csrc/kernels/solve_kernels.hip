@@ -1,34 +1,36 @@
-// Fused worker local-solve kernels (gfx950).
+// Worker local-solve kernels (gfx950).
 //
 //   stats_prep_kernel : window statistics (per-feature mean/std, fp64) and the
-//                       initial point x0 = w_old * std, one workgroup per 128
-//                       features (no cross-workgroup reduction, deterministic).
-//   slot_kernel       : ONE function evaluation of the line search:
-//       eval part (all workgroups): 32-row tiles staged once in LDS, forward
-//         Z = X W_eff^T on MFMA, softmax / cross entropy, backward G = R^T X on
-//         MFMA through hardware-transposed LDS reads; partial G / intercept /
-//         loss sums accumulate with no-return fp32 atomics (memory side);
-//       tail (the LAST workgroup to arrive, split-K seam recipe): reads and
-//         zeroes the sums, builds g_t in the standardised space plus the dot
-//         products the L-BFGS controller needs, advances the controller on an
-//         LDS copy (csrc/kernels/solver_ctrl.h), applies the accepted step /
-//         curvature pair / new direction elementwise, writes W_eff for the
-//         next trial, and when the controller is done finalises (unscale,
-//         multinomial centring, delta, eval fragments).
-// A local solve is therefore 1 + nslots launches in one hipGraph; slots after
-// convergence exit on their first instruction.
+//                       initial point x0 = w_old * std; one workgroup per
+//                       32-feature slice.
+//   per line-search slot, two launches:
+//   fwd_kernel        : ROW-parallel.  Each workgroup owns whole 32-row tiles:
+//                       stage in LDS, forward Z = X W_eff^T on MFMA (bf16 hi/lo
+//                       weights), softmax / cross entropy.  The residuals
+//                       R = softmax - onehot leave as bf16 hi/lo tiles already
+//                       in the MFMA A-operand layout (2 KB per tile), plus
+//                       per-workgroup intercept-gradient / loss partials.
+//   bwd_update_kernel : FEATURE-parallel.  Each workgroup owns a 32-feature
+//                       slice of every class for ALL rows: G = R^T X on MFMA,
+//                       fed from the feature-major ring copy XT, needs no
+//                       cross-workgroup reduction; only the handful of dot
+//                       products the L-BFGS controller needs cross workgroups
+//                       (one all-gather: write-through stores + an arrival
+//                       counter).  Every workgroup then advances its own copy
+//                       of the (deterministic) controller (csrc/kernels/
+//                       solver_ctrl.h) -- no decision broadcast -- applies it
+//                       to its slice and writes that slice of the next trial
+//                       point's MFMA weight fragments.
+//   finalize_kernel   : unscale, multinomial centring, delta, eval fragments.
+// A local solve is 2 + 2*nslots launches captured in one hipGraph; slots after
+// convergence exit on their first instruction.  The ring capacity is a multiple
+// of 32 and the window is processed as ring-aligned 32-row tiles (WinTiles), so
+// every tile and every 8-row XT fragment is contiguous (no wrap inside a tile).
 //
-// The tail is latency-bound (one workgroup), so it is written in explicit
-// phases: every global load of a feature group is issued before any result
-// is consumed and before any store (stores to possibly-aliasing vectors would
-// otherwise pin each load behind the previous store), and the bf16 weight
-// fragments are assembled in LDS and leave in 16-byte stores.
-//
-// Solver-private vectors use a padded layout so the tail's loops are
-// branch-free (a guarded load/atomic makes hipcc wait vmcnt(0) per element):
-// class count KP = next power of two >= K (compile time), feature stride
-// FPI = max(FP, 256); coefficient (c, f) at c*FPI + f, intercept c at
-// KP*FPI + c (c < 16).  Padded entries are identically zero.
+// Solver-private vectors use a padded layout: class count KP = next power of
+// two >= K (compile time), feature stride FPI = max(FP, 256); coefficient
+// (c, f) at c*FPI + f, intercept c at KP*FPI + c (c < 16).  Padded entries are
+// identically zero.
 //
 // Reference semantics: LogisticRegressionTaskSpark.java:142-221 (Spark fit
 // with setMaxIter(2), standardisation, centring, delta = w_new - w_old).
@@ -43,69 +45,98 @@ namespace psx {
 // Debug timeline (tools/bench_solver.py --stamps): s_memrealtime (100 MHz) per
 // phase of slot `slot`, written by one lane; no effect when dv.dbg is null.
 __device__ __forceinline__ void stamp(const SolveDev& dv, int slot, int k) {
-  if (dv.dbg && slot < 31) dv.dbg[slot * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (dv.dbg && slot < 32) dv.dbg[slot * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // ---------------------------------------------------------------------------
-// stats + prep: grid = FP/128 workgroups of 1024 threads (16 chunks x 64 rows)
-__global__ __launch_bounds__(1024) void stats_prep_kernel(SolverCfg cfg, const SolveParams* prm, SolveDev dv,
-                                                          Ctrl* ctrl) {
+// Cross-workgroup exchange area of bwd_update_kernel: 64-bit words written
+// with agent-scope atomic stores (sc1 write-through) and read with agent-scope
+// atomic loads (sc1, bypass L1) -- the write-through hand-off form (R1) of the
+// CDNA4 playbook: every storing wave drains vmcnt before the signal (ticket RMW
+// or flag store), every consumer load is sc1, so no fences are needed.  Only
+// the arrival ticket is a read-modify-write.
+constexpr size_t ctrl_lds_bytes() { return ((sizeof(Ctrl) + 15) / 16) * 16; }
+constexpr int kND = 3 + 2 * kMaxHist;  // dot products: gt.gt, gt.d, gt.gc, S_i.gt, Y_i.gt
+constexpr int kNDX = kND + 1;          // + loss
+constexpr int kMaxSlices = 2048 / 32;
+constexpr int kXchTicket = kMaxSlices * kNDX;  // arrival counter (grows by #slices per slot)
+constexpr int kXchErr = kXchTicket + 1;
+int xch_words() { return kXchErr + 1; }
+constexpr int kPartStride = 32;  // fwd partials per workgroup: rsum[16], loss
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ unsigned long long xload(unsigned long long* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xstore(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The window [start, start+B) of the ring (cap % 32 == 0) as a run of ring-
+// aligned 32-row tiles: window tile i is ring tile (start/32 + i) mod cap/32,
+// its row rr is in the window iff 0 <= 32*i + rr - start%32 < B.
+struct WinTiles {
+  int s0, t0, T, nt;
+  __device__ __forceinline__ WinTiles(int start, int B, int cap)
+      : s0(start & 31), t0(start >> 5), T(cap >> 5), nt(((start & 31) + B + 31) >> 5) {}
+  __device__ __forceinline__ int ring_tile(int i) const { return t0 + i >= T ? t0 + i - T : t0 + i; }
+};
+__device__ __forceinline__ unsigned long long d2u(double v) { return __builtin_bit_cast(unsigned long long, v); }
+__device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_bit_cast(double, v); }
+
+// ---------------------------------------------------------------------------
+// stats + prep: grid = FP/32 workgroups of 256 threads; 8 lanes per feature
+// read the feature-major ring copy XT in contiguous 16-B pieces of 8 rows.
+__global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, const SolveParams* prm, SolveDev dv,
+                                                         Ctrl* ctrl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* rs = (float*)smem;   // [64][128]
-  float* rq = rs + 64 * 128;  // [64][128]
-  float* sdl = rq + 64 * 128; // [128]
-  float* ivl = sdl + 128;     // [128]
-  const int B = prm->B, start = prm->start, cap = cfg.cap, FP = cfg.Fp;
-  const int t = threadIdx.x, ch = t & 15, rl = t >> 4;
-  const int fb = blockIdx.x * 128;
-  float s[8], q[8];
+  double* rs = (double*)smem;  // [32]
+  double* rq = rs + 32;        // [32]
+  float* sdl = (float*)(rq + 32);  // [32]
+  float* ivl = sdl + 32;           // [32]
+  const int B = prm->B, cap = cfg.cap, FP = cfg.Fp;
+  const WinTiles wt(prm->start, B, cap);
+  const int t = threadIdx.x, j = t & 7, fl0 = t >> 3;
+  if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
+  const int fs = blockIdx.x * 32;
+  const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
+  const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
+  float s = 0.f, q = 0.f;
+  for (int q0 = j; q0 < nq; q0 += 8 * 8) {
+    u16x8 v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
-  for (int i0 = rl; i0 < B; i0 += 64 * 4) {
-    u16x8 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + 64 * u;
-      int r = start + (i < B ? i : 0);
-      if (r >= cap) r -= cap;
-      v[u] = *(const u16x8*)(dv.X + (size_t)r * FP + fb + ch * 8);
-      if (i >= B) v[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int u = 0; u < 8; ++u) {
+      const int qq = q0 + 8 * u;
+      const int qc = qq < nq ? qq : nq - 1;
+      v[u] = *(const u16x8*)(xt + wt.ring_tile(qc >> 2) * 32 + (qc & 3) * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u) {
+      const int qq = q0 + 8 * u;
+      const int o0 = (qq >> 2) * 32 + (qq & 3) * 8 - wt.s0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = bf2f(v[u][j]);
-        s[j] += x;
-        q[j] += x * x;
+      for (int e = 0; e < 8; ++e) {
+        const bool in = qq < nq && o0 + e >= 0 && o0 + e < B;
+        const float x = in ? bf2f(v[u][e]) : 0.f;
+        s += x;
+        q += x * x;
       }
-  }
-  // fold the 4 row lanes of each wave with shuffles, then 16 waves through LDS
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    s[j] += __shfl_xor(s[j], 16, 64);
-    s[j] += __shfl_xor(s[j], 32, 64);
-    q[j] += __shfl_xor(q[j], 16, 64);
-    q[j] += __shfl_xor(q[j], 32, 64);
-  }
-  const int wv = t >> 6;
-  if ((t & 63) < 16) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      rs[wv * 128 + ch * 8 + j] = s[j];
-      rq[wv * 128 + ch * 8 + j] = q[j];
     }
   }
-  (void)rl;
+  double a = s, b2 = q;
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+    a += __shfl_xor(a, o, 64);
+    b2 += __shfl_xor(b2, o, 64);
+  }
+  if (j == 0) {
+    rs[fl0] = a;
+    rq[fl0] = b2;
+  }
   __syncthreads();
-  if (t < 128) {
-    double a = 0.0, b = 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      a += rs[r * 128 + t];
-      b += rq[r * 128 + t];
-    }
-    const int f = fb + t;
+  if (t < 32) {
+    const double a = rs[t];
+    const double b = rq[t];
+    const int f = fs + t;
     const double n = (double)B;
     double sd = 0.0;
     if (f < cfg.F && n > 1.0) {
@@ -121,8 +152,8 @@ __global__ __launch_bounds__(1024) void stats_prep_kernel(SolverCfg cfg, const S
   }
   __syncthreads();
   const int K = cfg.K, KP = dv.KP, FPI = dv.FPI;
-  for (int e = t; e < 128 * KP; e += 1024) {
-    const int c = e >> 7, fl = e & 127, f = fb + fl;
+  for (int e = t; e < 32 * KP; e += 256) {
+    const int c = e >> 5, fl = e & 31, f = fs + fl;
     const int pi = c * FPI + f;
     const float wo = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
     const float xv = wo * sdl[fl];
@@ -142,150 +173,256 @@ __global__ __launch_bounds__(1024) void stats_prep_kernel(SolverCfg cfg, const S
       dv.g_c[pi] = 0.f;
       dv.b_eff[t] = b;
     }
-    if (t == 0) ctrl_init(*ctrl);
+    if (t == 32) ctrl_init(*ctrl);
+    if (t == 0) stamp(dv, 30, 1);
+    if (t == 64) xstore(dv.xch + kXchTicket, 0ull);
   }
 }
 
 // ---------------------------------------------------------------------------
-// LDS layout of the tail: [Ctrl copy] [dots] [controller workspace]
-constexpr size_t ctrl_lds_bytes() { return ((sizeof(Ctrl) + 15) / 16) * 16; }
-constexpr int kND = 3 + 2 * kMaxHist;
-
-// N consecutive floats <-> registers with the widest vector accesses.
-template <int N>
-__device__ __forceinline__ void vload(float (&d)[N], const float* __restrict__ p) {
-  if constexpr (N % 4 == 0) {
-#pragma unroll
-    for (int i = 0; i < N / 4; ++i) {
-      const float4 t = *(const float4*)(p + 4 * i);
-      d[4 * i] = t.x;
-      d[4 * i + 1] = t.y;
-      d[4 * i + 2] = t.z;
-      d[4 * i + 3] = t.w;
-    }
-  } else if constexpr (N == 2) {
-    const float2 t = *(const float2*)p;
-    d[0] = t.x;
-    d[1] = t.y;
-  } else {
-#pragma unroll
-    for (int i = 0; i < N; ++i) d[i] = p[i];
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void vstore(float* __restrict__ p, const float (&s)[N]) {
-  if constexpr (N % 4 == 0) {
-#pragma unroll
-    for (int i = 0; i < N / 4; ++i) *(float4*)(p + 4 * i) = make_float4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
-  } else if constexpr (N == 2) {
-    *(float2*)p = make_float2(s[0], s[1]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < N; ++i) p[i] = s[i];
-  }
-}
-
-// Write N consecutive features (f0 % N == 0, N <= 8) of class c into the MFMA
-// fragment layout: they sit in one 16-B chunk, so this is one store per array.
-template <int N>
-__device__ __forceinline__ void frag_store(uint16_t* hi, uint16_t* lo, int c, int f0, const float (&v)[N]) {
-  unsigned short h[N], l[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) split_bf16(v[i], h[i], l[i]);
-  const size_t o = ((size_t)(f0 >> 3) * 16 + c) * 8 + (f0 & 7);
-  if constexpr (N == 8) {
-    *(u16x8*)(hi + o) = u16x8{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
-    *(u16x8*)(lo + o) = u16x8{l[0], l[1], l[2], l[3], l[4], l[5], l[6], l[7]};
-  } else if constexpr (N == 4) {
-    *(u16x4*)(hi + o) = u16x4{h[0], h[1], h[2], h[3]};
-    *(u16x4*)(lo + o) = u16x4{l[0], l[1], l[2], l[3]};
-  } else {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      hi[o + i] = h[i];
-      lo[o + i] = l[i];
-    }
-  }
-}
-
-// The tail.  Thread t owns the FPT consecutive features [t*FPT, t*FPT+FPT) of
-// every class (and intercept t when t < 16), so every vector access is a 16-B
-// (or 8-B) per-lane load/store: the single tail workgroup is bound by memory
-// instructions in flight, and wide accesses move 4x the bytes per instruction.
-template <int FP, int KP>
-__device__ __forceinline__ void solve_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
-                                           const SolveDev& dv, char* lds) {
-  constexpr int FPI = FP > 256 ? FP : 256;
-  constexpr int FPT = FPI / 256;  // consecutive features owned per thread
-  constexpr int IB = KP * FPI;    // internal intercept base
+// fwd_kernel: loss and residuals at the trial point (row-parallel).
+template <int FP>
+__global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl, int slot,
+                                                  SolveDev dv) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot: exit at once
+  const int B = prm->B, K = cfg.K;
+  const WinTiles wt(prm->start, B, cfg.cap);
+  const int ntiles = wt.nt;
+  if ((int)blockIdx.x >= ntiles) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
+  char* red_base = lds + 32 * FP * 2;
+  unsigned short* rt = (unsigned short*)(red_base + 8192);  // [2][16][32]
+  int* ylds = (int*)(red_base + 8192 + 2048);
+  float* rsum = (float*)(ylds + 32);
+  float* lred = rsum + 16;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int f0 = tid * FPT;
-  const int K = cfg.K, H = cfg.hist;
+
+  if (tid < 16) rsum[tid] = 0.f;
+  float loss = 0.f;
+  const int sr = tid >> 3, sc0 = (tid & 7) * 2;
+  float rs0 = 0.f, rs1 = 0.f;
+  const float bz0 = dv.b_eff[sc0], bz1 = dv.b_eff[sc0 + 1];
+  // the trial weights do not depend on the tile: fetch them before staging so
+  // the two memory latencies overlap (register budget allows it up to FP 1024)
+  constexpr bool kPre = FP <= 1024;
+  WFrag<kPre ? FP : 128> wf;
+  if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
+    stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
+    if (tid < 32) ylds[tid] = dv.y[row0 + tid];
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 9);
+    f32x4 a0, a1;
+    if constexpr (kPre)
+      forward_tile_pre<FP>(lds, wf, a0, a1);
+    else
+      forward_tile<FP>(lds, dv.whi, dv.wlo, a0, a1);
+    store_partial_logits(red_base, a0, a1);
+    __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 10);
+    {  // softmax + cross entropy: 8 threads per row, 2 classes each
+      const bool v0 = sc0 < K, v1 = sc0 + 1 < K;
+      const float z0 = v0 ? load_logit(red_base, sr, sc0) + bz0 : -INFINITY;
+      const float z1 = v1 ? load_logit(red_base, sr, sc0 + 1) + bz1 : -INFINITY;
+      float mx = fmaxf(z0, z1);
+      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
+      const float e0 = v0 ? __expf(z0 - mx) : 0.f, e1 = v1 ? __expf(z1 - mx) : 0.f;
+      float se = e0 + e1;
+      se += __shfl_xor(se, 1, 64);
+      se += __shfl_xor(se, 2, 64);
+      se += __shfl_xor(se, 4, 64);
+      const int orow = tile * 32 + sr - wt.s0;  // offset in the window
+      const bool valid = orow >= 0 && orow < B;
+      const int yl = ylds[sr];
+      const float inv = 1.f / se;
+      const float r0 = valid && v0 ? e0 * inv - (yl == sc0 ? 1.f : 0.f) : 0.f;
+      const float r1 = valid && v1 ? e1 * inv - (yl == sc0 + 1 ? 1.f : 0.f) : 0.f;
+      if (valid) {
+        const float lse = mx + __logf(se);
+        if (yl == sc0) loss += lse - z0;
+        if (yl == sc0 + 1) loss += lse - z1;
+      }
+      rs0 += r0;
+      rs1 += r1;
+      unsigned short h, l;
+      split_bf16(r0, h, l);
+      rt[sc0 * 32 + sr] = h;
+      rt[512 + sc0 * 32 + sr] = l;
+      split_bf16(r1, h, l);
+      rt[(sc0 + 1) * 32 + sr] = h;
+      rt[512 + (sc0 + 1) * 32 + sr] = l;
+    }
+    __syncthreads();
+    // residual tile -> global, in the A-operand layout of the backward MFMA
+    *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
+    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 11);
+  }
+  atomicAdd(&rsum[sc0], rs0);
+  atomicAdd(&rsum[sc0 + 1], rs1);
+  loss = wave_sum(loss);
+  if (lane == 0) lred[w] = loss;
+  __syncthreads();
+  float* part = dv.part + (size_t)blockIdx.x * kPartStride;
+  if (tid < 16) part[tid] = rsum[tid];
+  if (tid == 16) part[16] = lred[0] + lred[1] + lred[2] + lred[3];
+  if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 1);
+}
+
+// ---------------------------------------------------------------------------
+// bwd_update_kernel: gradient of a 32-feature slice, controller step, update.
+// Both MFMA operands come straight from global memory in fragment shape: the
+// residual tiles R (class x 8 rows = 16 B per lane) and the feature-major ring
+// copy XT (feature x 8 consecutive rows = 16 B per lane), so no LDS staging.
+constexpr int kBwdBatch = 8;  // k-steps (32-row tiles) per wave whose loads are in flight together
+
+size_t bwd_lds_bytes() {
+  return (size_t)4 * 16 * 32 * 4 + 2 * 512 * 2 + ctrl_lds_bytes() +
+         (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) + sizeof(CtrlScratch);
+}
+
+template <int FP, int KP>
+__global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
+                                                         SolveDev dv, int fwd_grid) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int FPI = FP > 256 ? FP : 256;
+  constexpr int IB = KP * FPI;              // internal intercept base
+  constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
+  if (gctrl->phase == kPhDone) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 2);
+  float* gw = (float*)lds;                             // [4 waves][16 classes][32]
+  unsigned short* frl = (unsigned short*)(gw + 4 * 16 * 32);  // [2][512] fragment staging
+  Ctrl* cl = (Ctrl*)(frl + 1024);
+  double* sdot = (double*)((char*)cl + ctrl_lds_bytes());  // [4 waves][kNDX]
+  double* dots = sdot + 4 * kNDX;                          // [kNDX]
+  double* gat = dots + kNDX;                               // [slices][kNDX]
+  float* pr = (float*)(gat + kMaxSlices * kNDX);           // [15][17] fwd-partial stripes
+  CtrlScratch* csw = (CtrlScratch*)(pr + 256);
+  unsigned long long* xch = dv.xch;
+  {  // every workgroup runs the (deterministic) controller on its own LDS copy
+    constexpr int CW = sizeof(Ctrl) / 8;
+    for (int i = tid; i < CW; i += 256) ((unsigned long long*)cl)[i] = ((const unsigned long long*)gctrl)[i];
+  }
+
+  const int B = prm->B, cap = cfg.cap, K = cfg.K, H = cfg.hist;
+  const WinTiles wt(prm->start, B, cap);
   const size_t PI = dv.PI;
-  Ctrl* cl = (Ctrl*)lds;
-  double* sdot = (double*)(lds + ctrl_lds_bytes());  // [4 waves][kND]
-  double* dots = sdot + 4 * kND;
-  CtrlScratch* csw = (CtrlScratch*)(dots + kND);  // controller workspace (LDS)
-  // ---- 0) controller to LDS; read-and-zero the sums; every per-element input ----
-  constexpr int CW = sizeof(Ctrl) / 8;
-  {
-    const unsigned long long* src = (const unsigned long long*)gctrl;
-    unsigned long long* dst = (unsigned long long*)cl;
-    for (int i = tid; i < CW; i += 256) dst[i] = src[i];
+  const float invB = 1.f / (float)B;
+  const int fs = blockIdx.x * 32;
+  const int fl = tid & 31, cgp = tid >> 5;
+  const int f = fs + fl;
+  const bool wg0 = blockIdx.x == 0;
+
+  // ---- per-element state first (independent of the backward) ----
+  float DD[NE], GC[NE], XO[NE], FX[NE];
+  int idx[NE];
+  bool own[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cgp + 8 * e;
+    own[e] = c < KP;
+    idx[e] = (own[e] ? c : 0) * FPI + f;
+    DD[e] = dv.d[idx[e]];
+    GC[e] = dv.g_c[idx[e]];
+    XO[e] = dv.x[idx[e]];
+    FX[e] = dv.wfix[idx[e]];
   }
-  float g[KP][FPT];
-#pragma unroll
-  for (int c = 0; c < KP; ++c)
-#pragma unroll
-    for (int j = 0; j < FPT; ++j)
-      g[c][j] = __hip_atomic_exchange(dv.Gacc + c * FPI + f0 + j, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  float gb = 0.f;
-  if (tid < 16) gb = __hip_atomic_exchange(dv.Racc + tid, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  float DD[KP][FPT], GC[KP][FPT], XO[KP][FPT], FX[KP][FPT], ivs[FPT];
-  vload<FPT>(ivs, dv.inv_std + f0);
-#pragma unroll
-  for (int c = 0; c < KP; ++c) {
-    vload<FPT>(DD[c], dv.d + c * FPI + f0);
-    vload<FPT>(GC[c], dv.g_c + c * FPI + f0);
-    vload<FPT>(XO[c], dv.x + c * FPI + f0);
-    vload<FPT>(FX[c], dv.wfix + c * FPI + f0);
-  }
+  const float iv = dv.inv_std[f];
+  const int ntiles = wt.nt;
+  const int nfw = ntiles < fwd_grid ? ntiles : fwd_grid;
   float db0 = 0.f, gcb0 = 0.f, xb0 = 0.f;
-  if (tid < 16) {
+  if (wg0 && tid < 255) {  // intercept gradient / loss partials: 15 stripes x 17 values, fixed order
+    const int k = tid % 17, g0 = tid / 17;
+    float a = 0.f;
+#pragma unroll 4
+    for (int s = g0; s < nfw; s += 15) a += dv.part[(size_t)s * kPartStride + k];
+    pr[g0 * 17 + k] = a;
+  }
+  if (wg0 && tid < 16) {
     db0 = dv.d[IB + tid];
     gcb0 = dv.g_c[IB + tid];
     xb0 = dv.x[IB + tid];
   }
-  __syncthreads();  // controller copy complete
-  const int m = cl->m, head = cl->head;
-  const float invB = 1.f / (float)prm->B;
-  if (tid == 0) stamp(dv, slot, 3);
-  // ---- 1) gradient in the standardised space + dot products ----
-  double tt = 0.0, td = 0.0, tc = 0.0;
+  if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+
+  // ---- backward G[c][slice] = sum_r R[r][c] X[r][slice] ----
+  f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  {
+    const int m16 = lane & 15, kg = (lane >> 4) * 8;
+    const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
+    const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
+    const unsigned short* rp0 = dv.R + m16 * 32 + kg;
+    const bool live = m16 < K;
+    for (int kb = 0; kb < ntiles; kb += 4 * kBwdBatch) {
+      u16x8 ah[kBwdBatch], al[kBwdBatch], b0[kBwdBatch], b1[kBwdBatch];
 #pragma unroll
-  for (int c = 0; c < KP; ++c)
+      for (int u = 0; u < kBwdBatch; ++u) {  // every load of the batch in flight together
+        const int i = kb + w + 4 * u;
+        const int ic = i < ntiles ? i : ntiles - 1;
+        const size_t ro = (size_t)wt.ring_tile(ic) * 32;
+        ah[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024);
+        al[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024 + 512);
+        b0[u] = *(const u16x8*)(xt0 + ro);
+        b1[u] = *(const u16x8*)(xt1 + ro);
+      }
 #pragma unroll
-    for (int j = 0; j < FPT; ++j) {
-      const float gv = g[c][j] * invB * ivs[j];
-      g[c][j] = gv;
-      tt += (double)gv * gv;
-      td += (double)gv * DD[c][j];
-      tc += (double)gv * GC[c][j];
+      for (int u = 0; u < kBwdBatch; ++u) {
+        const int i = kb + w + 4 * u;
+        if (i >= ntiles || !live) ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        acc[0] = mfma16x16x32(as_bf16x8(ah[u]), as_bf16x8(b0[u]), acc[0]);
+        acc[0] = mfma16x16x32(as_bf16x8(al[u]), as_bf16x8(b0[u]), acc[0]);
+        acc[1] = mfma16x16x32(as_bf16x8(ah[u]), as_bf16x8(b1[u]), acc[1]);
+        acc[1] = mfma16x16x32(as_bf16x8(al[u]), as_bf16x8(b1[u]), acc[1]);
+      }
     }
-  if (tid < 16) {
-    gb *= invB;
-    tt += (double)gb * gb;
-    td += (double)gb * db0;
-    tc += (double)gb * gcb0;
   }
+  if (wg0 && tid == 0) stamp(dv, slot, 3);
+  // cross-wave reduction of the accumulators (D[class][feature])
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int c = (lane >> 4) * 4 + rr;
+      gw[(w * 16 + c) * 32 + j * 16 + (lane & 15)] = acc[j][rr];
+    }
+  __syncthreads();
+  float g[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = (cgp + 8 * e) & 15;
+    const float s = gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
+    g[e] = own[e] ? s * invB * iv : 0.f;
+  }
+  float rpart = 0.f;  // the cross-wave barrier above also published pr[]
+  if (wg0 && tid < 17)
+#pragma unroll
+    for (int g0 = 0; g0 < 15; ++g0) rpart += pr[g0 * 17 + tid];
+  const float gb = (wg0 && tid < 16) ? rpart * invB : 0.f;
+  if (wg0 && tid == 0) stamp(dv, slot, 4);
+
+  // ---- partial dot products -> exchange area ----
+  const int m = cl->m, head = cl->head;
+  double tt = (double)gb * gb, td = (double)gb * db0, tc = (double)gb * gcb0;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    tt += (double)g[e] * g[e];
+    td += (double)g[e] * DD[e];
+    tc += (double)g[e] * GC[e];
+  }
+  const double lsum = (wg0 && tid == 16) ? (double)rpart : 0.0;
   tt = wave_sum(tt);
   td = wave_sum(td);
   tc = wave_sum(tc);
+  const double ls = wave_sum(lsum);
   if (lane == 0) {
-    sdot[w * kND + 0] = tt;
-    sdot[w * kND + 1] = td;
-    sdot[w * kND + 2] = tc;
+    sdot[w * kNDX + 0] = tt;
+    sdot[w * kNDX + 1] = td;
+    sdot[w * kNDX + 2] = tc;
+    sdot[w * kNDX + kND] = ls;
   }
   for (int i = 0; i < H; ++i) {  // wave-uniform loop over stored pairs
     const bool valid = m > 0 && (m == H || (((i - (head - m + 1)) % H + H) % H) < m);
@@ -293,20 +430,12 @@ __device__ __forceinline__ void solve_tail(const SolverCfg& cfg, const SolvePara
     if (valid) {
       const float* Si = dv.S + (size_t)i * PI;
       const float* Yi = dv.Y + (size_t)i * PI;
-      float sv[KP][FPT], yv[KP][FPT];
 #pragma unroll
-      for (int c = 0; c < KP; ++c) {
-        vload<FPT>(sv[c], Si + c * FPI + f0);
-        vload<FPT>(yv[c], Yi + c * FPI + f0);
+      for (int e = 0; e < NE; ++e) {
+        si += (double)Si[idx[e]] * g[e];
+        yi += (double)Yi[idx[e]] * g[e];
       }
-#pragma unroll
-      for (int c = 0; c < KP; ++c)
-#pragma unroll
-        for (int j = 0; j < FPT; ++j) {
-          si += (double)sv[c][j] * g[c][j];
-          yi += (double)yv[c][j] * g[c][j];
-        }
-      if (tid < 16) {
+      if (wg0 && tid < 16) {
         si += (double)Si[IB + tid] * gb;
         yi += (double)Yi[IB + tid] * gb;
       }
@@ -314,72 +443,110 @@ __device__ __forceinline__ void solve_tail(const SolverCfg& cfg, const SolvePara
       yi = wave_sum(yi);
     }
     if (lane == 0) {
-      sdot[w * kND + 3 + i] = si;
-      sdot[w * kND + 3 + H + i] = yi;
+      sdot[w * kNDX + 3 + i] = si;
+      sdot[w * kNDX + 3 + kMaxHist + i] = yi;
     }
   }
   __syncthreads();
-  if (tid < 3 + 2 * H) dots[tid] = sdot[tid] + sdot[kND + tid] + sdot[2 * kND + tid] + sdot[3 * kND + tid];
-  __syncthreads();
-  if (tid == 0) {
-    const float L = __hip_atomic_exchange(dv.Lacc, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    stamp(dv, slot, 4);
-    ctrl_step(*cl, cfg, (double)L / (double)prm->B, dots, slot, *csw);
-    stamp(dv, slot, 5);
+  // ---- all-gather of the partial dots (write-through hand-off, R1): sc1
+  // stores, every storing wave drains, one arrival RMW per workgroup on a
+  // counter that only grows within a solve (reset by stats_prep), one lane
+  // polls it relaxed, then sc1 loads of every workgroup's partials ----
+  const int ns = gridDim.x;
+  if (tid < kNDX) {
+    const double v = sdot[tid] + sdot[kNDX + tid] + sdot[2 * kNDX + tid] + sdot[3 * kNDX + tid];
+    if (ns > 1)
+      xstore(xch + blockIdx.x * kNDX + tid, d2u(v));
+    else
+      gat[tid] = v;
+  }
+  if (ns > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      (void)__hip_atomic_fetch_add(xch + kXchTicket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long target = (unsigned long long)ns * (unsigned long long)(slot + 1);
+      int spins = 0;
+      while (xload(xch + kXchTicket) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 24)) {  // never expected: record and fall through rather than hang
+          xstore(xch + kXchErr, 1ull);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the sc1 loads below the poll
+    for (int i = tid; i < ns * kNDX; i += 256) gat[i] = u2d(xload(xch + i));  // all in flight
   }
   __syncthreads();
-  // ---- 2) apply the controller's action ----
+  if (tid < kNDX) {
+    double v = 0.0;
+    for (int b = 0; b < ns; ++b) v += gat[b * kNDX + tid];  // fixed order: identical in every workgroup
+    // compact order expected by ctrl_step: 3 scalars, S_i.g (H), Y_i.g (H); loss last
+    int pos = tid;
+    if (tid >= 3 && tid < 3 + kMaxHist)
+      pos = tid - 3 < H ? tid : -1;
+    else if (tid >= 3 + kMaxHist && tid < kND)
+      pos = tid - 3 - kMaxHist < H ? 3 + H + (tid - 3 - kMaxHist) : -1;
+    if (pos >= 0) dots[pos] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (wg0) stamp(dv, slot, 5);
+    ctrl_step(*cl, cfg, dots[kND] / (double)B, dots, slot, *csw);
+    if (wg0) stamp(dv, slot, 6);
+  }
+  __syncthreads();
+  if (wg0) {  // the next launches read the controller from global memory
+    constexpr int CW = sizeof(Ctrl) / 8;
+    for (int i = tid; i < CW; i += 256) ((unsigned long long*)gctrl)[i] = ((const unsigned long long*)cl)[i];
+  }
+  if (wg0 && tid == 0) stamp(dv, slot, 7);
+
+  // ---- apply the controller's action to this slice ----
   const int act = cl->action_slot == slot ? cl->action : kActNone;
   const bool done = cl->phase == kPhDone;
   const float t_next = (float)cl->t, t_acc = (float)cl->t_acc, cg = (float)cl->cg;
   const int ps = cl->push_slot;
   const bool accept = act == kActAccept || act == kActAcceptDone;
   const bool more = act == kActAccept;
-  float (&xv)[KP][FPT] = XO;  // updated in place
-  float (&dn)[KP][FPT] = DD;  // DD holds the previous direction until overwritten
-  float dold[KP][FPT];
+  float dn[NE];
 #pragma unroll
-  for (int c = 0; c < KP; ++c)
-#pragma unroll
-    for (int j = 0; j < FPT; ++j) dold[c][j] = DD[c][j];
+  for (int e = 0; e < NE; ++e) dn[e] = DD[e];
+  float dbv = db0, xbv = xb0;
+  const bool ib = wg0 && tid < 16;
   if (act == kActInit) {
 #pragma unroll
-    for (int c = 0; c < KP; ++c) {
-#pragma unroll
-      for (int j = 0; j < FPT; ++j) dn[c][j] = cg * g[c][j];
-      vstore<FPT>(dv.g_c + c * FPI + f0, g[c]);
-      vstore<FPT>(dv.d + c * FPI + f0, dn[c]);
-    }
-  } else if (accept) {
-#pragma unroll
-    for (int c = 0; c < KP; ++c) {
-#pragma unroll
-      for (int j = 0; j < FPT; ++j) xv[c][j] += t_acc * dold[c][j];
-      vstore<FPT>(dv.x + c * FPI + f0, xv[c]);
-      if (more) {
-        if (ps >= 0) {
-          float sn[FPT], yn[FPT];
-#pragma unroll
-          for (int j = 0; j < FPT; ++j) {
-            sn[j] = t_acc * dold[c][j];
-            yn[j] = g[c][j] - GC[c][j];
-          }
-          vstore<FPT>(dv.S + (size_t)ps * PI + c * FPI + f0, sn);
-          vstore<FPT>(dv.Y + (size_t)ps * PI + c * FPI + f0, yn);
-        }
-        vstore<FPT>(dv.g_c + c * FPI + f0, g[c]);
-#pragma unroll
-        for (int j = 0; j < FPT; ++j) dn[c][j] = cg * g[c][j];
+    for (int e = 0; e < NE; ++e) {
+      dn[e] = cg * g[e];
+      if (own[e]) {
+        dv.g_c[idx[e]] = g[e];
+        dv.d[idx[e]] = dn[e];
       }
     }
-  }
-  float dbv = db0, xbv = xb0;
-  if (tid < 16) {
-    if (act == kActInit) {
+    if (ib) {
       dbv = cg * gb;
       dv.g_c[IB + tid] = gb;
       dv.d[IB + tid] = dbv;
-    } else if (accept) {
+    }
+  } else if (accept) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      XO[e] += t_acc * DD[e];
+      if (own[e]) {
+        dv.x[idx[e]] = XO[e];
+        if (more) {
+          if (ps >= 0) {
+            dv.S[(size_t)ps * PI + idx[e]] = t_acc * DD[e];
+            dv.Y[(size_t)ps * PI + idx[e]] = g[e] - GC[e];
+          }
+          dv.g_c[idx[e]] = g[e];
+        }
+      }
+      if (more) dn[e] = cg * g[e];
+    }
+    if (ib) {
       xbv = xb0 + t_acc * db0;
       dv.x[IB + tid] = xbv;
       if (more) {
@@ -398,218 +565,43 @@ __device__ __forceinline__ void solve_tail(const SolverCfg& cfg, const SolvePara
       if (cs == 0.f && cy == 0.f) continue;  // uniform
       if (i == ps) {  // the pair pushed just now is still in registers
 #pragma unroll
-        for (int c = 0; c < KP; ++c)
-#pragma unroll
-          for (int j = 0; j < FPT; ++j) dn[c][j] += cs * (t_acc * dold[c][j]) + cy * (g[c][j] - GC[c][j]);
-        if (tid < 16) dbv += cs * (t_acc * db0) + cy * (gb - gcb0);
+        for (int e = 0; e < NE; ++e) dn[e] += cs * (t_acc * DD[e]) + cy * (g[e] - GC[e]);
+        if (ib) dbv += cs * (t_acc * db0) + cy * (gb - gcb0);
         continue;
       }
       const float* Si = dv.S + (size_t)i * PI;
       const float* Yi = dv.Y + (size_t)i * PI;
-      float sv[KP][FPT], yv[KP][FPT];
 #pragma unroll
-      for (int c = 0; c < KP; ++c) {
-        vload<FPT>(sv[c], Si + c * FPI + f0);
-        vload<FPT>(yv[c], Yi + c * FPI + f0);
-      }
-#pragma unroll
-      for (int c = 0; c < KP; ++c)
-#pragma unroll
-        for (int j = 0; j < FPT; ++j) dn[c][j] += cs * sv[c][j] + cy * yv[c][j];
-      if (tid < 16) dbv += cs * Si[IB + tid] + cy * Yi[IB + tid];
+      for (int e = 0; e < NE; ++e) dn[e] += cs * Si[idx[e]] + cy * Yi[idx[e]];
+      if (ib) dbv += cs * Si[IB + tid] + cy * Yi[IB + tid];
     }
 #pragma unroll
-    for (int c = 0; c < KP; ++c) vstore<FPT>(dv.d + c * FPI + f0, dn[c]);
-    if (tid < 16) dv.d[IB + tid] = dbv;
+    for (int e = 0; e < NE; ++e)
+      if (own[e]) dv.d[idx[e]] = dn[e];
+    if (ib) dv.d[IB + tid] = dbv;
   }
-  if (tid == 0) stamp(dv, slot, 6);
-  // ---- 3) next trial point as MFMA weight fragments (finalize_kernel runs
-  //         after the last slot when the controller is done) ----
+  // ---- next trial point: this slice of the MFMA weight fragments (16-B stores) ----
   if (!done) {
-    if (f0 < FP) {
 #pragma unroll
-      for (int c = 0; c < KP; ++c) {
-        float v[FPT];
-#pragma unroll
-        for (int j = 0; j < FPT; ++j) v[j] = (xv[c][j] + t_next * dn[c][j]) * ivs[j] + FX[c][j];
-        if constexpr (FPT <= 8) frag_store<FPT>(dv.whi, dv.wlo, c, f0, v);
-      }
-    }
-    if (tid < 16) dv.b_eff[tid] = xbv + t_next * dbv;
-  }
-  if (tid == 0) stamp(dv, slot, 7);
-  // ---- controller back to global memory (ticket re-armed) ----
-  if (tid == 0) cl->ticket = 0;
-  __syncthreads();
-  {
-    const unsigned long long* src = (const unsigned long long*)cl;
-    unsigned long long* dst = (unsigned long long*)gctrl;
-    for (int i = tid; i < CW; i += 256) dst[i] = src[i];
-  }
-}
-
-// ---------------------------------------------------------------------------
-template <int FP, int KP>
-__global__ __launch_bounds__(256) void slot_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* ctrl, int slot,
-                                                   SolveDev dv) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int NTW = FP / 64;  // 16-feature N-tiles per wave in the backward
-  constexpr int FPI = FP > 256 ? FP : 256;
-  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot: exit at once
-  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
-  const int B = prm->B, start = prm->start, cap = cfg.cap, K = cfg.K;
-  const int ntiles = (B + 31) / 32;
-  char* red_base = lds + 32 * FP * 2;
-  unsigned short* rt = (unsigned short*)(red_base + 8192);  // [2][16][32]
-  int* ylds = (int*)(red_base + 8192 + 2048);
-  float* rsum = (float*)(ylds + 32);
-  float* lred = rsum + 16;
-  int* flag = (int*)(lred + 4);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-
-  if ((int)blockIdx.x < ntiles) {
-    if (tid < 16) rsum[tid] = 0.f;
-    f32x4 accb[NTW];
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) accb[j] = f32x4{0, 0, 0, 0};
-    float loss = 0.f;
-    const int sr = tid >> 3, sc0 = (tid & 7) * 2;
-    float rs0 = 0.f, rs1 = 0.f;
-    const float bz0 = dv.b_eff[sc0], bz1 = dv.b_eff[sc0 + 1];
-    // the trial weights do not depend on the tile: fetch them before staging so
-    // the two memory latencies overlap (register budget allows it up to FP 1024)
-    constexpr bool kPre = FP <= 1024;
-    WFrag<kPre ? FP : 128> wf;
-    if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo);
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-      const int nrows = min(32, B - tile * 32);
-      int64_t row0 = (int64_t)start + (int64_t)tile * 32;
-      if (row0 >= cap) row0 -= cap;
-      stage_tile<FP>(lds, dv.X, row0, nrows, cap, true);
-      if (tid < 32) {
-        int yy = 0;
-        if (tid < nrows) {
-          int64_t r = row0 + tid;
-          if (r >= cap) r -= cap;
-          yy = dv.y[r];
-        }
-        ylds[tid] = yy;
-      }
-      __syncthreads();
-      if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 9);
-      f32x4 a0, a1;
-      if constexpr (kPre)
-        forward_tile_pre<FP>(lds, wf, a0, a1);
-      else
-        forward_tile<FP>(lds, dv.whi, dv.wlo, a0, a1);
-      store_partial_logits(red_base, a0, a1);
-      __syncthreads();
-      if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 10);
-      {  // softmax + cross entropy: 8 threads per row, 2 classes each
-        const bool v0 = sc0 < K, v1 = sc0 + 1 < K;
-        const float z0 = v0 ? load_logit(red_base, sr, sc0) + bz0 : -INFINITY;
-        const float z1 = v1 ? load_logit(red_base, sr, sc0 + 1) + bz1 : -INFINITY;
-        float mx = fmaxf(z0, z1);
-        mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 4, 64));
-        const float e0 = v0 ? __expf(z0 - mx) : 0.f, e1 = v1 ? __expf(z1 - mx) : 0.f;
-        float se = e0 + e1;
-        se += __shfl_xor(se, 1, 64);
-        se += __shfl_xor(se, 2, 64);
-        se += __shfl_xor(se, 4, 64);
-        const bool valid = sr < nrows;
-        const int yl = ylds[sr];
-        const float inv = 1.f / se;
-        const float r0 = valid && v0 ? e0 * inv - (yl == sc0 ? 1.f : 0.f) : 0.f;
-        const float r1 = valid && v1 ? e1 * inv - (yl == sc0 + 1 ? 1.f : 0.f) : 0.f;
-        if (valid) {
-          const float lse = mx + __logf(se);
-          if (yl == sc0) loss += lse - z0;
-          if (yl == sc0 + 1) loss += lse - z1;
-        }
-        rs0 += r0;
-        rs1 += r1;
+    for (int e = 0; e < NE; ++e) {
+      const int c = cgp + 8 * e;
+      if (own[e]) {
         unsigned short h, l;
-        split_bf16(r0, h, l);
-        rt[sc0 * 32 + sr] = h;
-        rt[512 + sc0 * 32 + sr] = l;
-        split_bf16(r1, h, l);
-        rt[(sc0 + 1) * 32 + sr] = h;
-        rt[512 + (sc0 + 1) * 32 + sr] = l;
-      }
-      __syncthreads();
-      if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 11);
-      {  // backward G[c][f] += sum_r R[r][c] X[r][f] (M = classes, N = features, K = rows)
-        const u16x8 ah = *(const u16x8*)(rt + (lane & 15) * 32 + (lane >> 4) * 8);
-        const u16x8 al = *(const u16x8*)(rt + 512 + (lane & 15) * 32 + (lane >> 4) * 8);
-        const int gq = lane >> 4, il = lane & 15, q = il >> 2, pp = il & 3;
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          const int nt = w * NTW + j, f0 = nt * 16;
-          const int sub = f0 >> 7, c0 = (f0 & 127) >> 3;
-          const int chk = c0 + (pp >> 1), inb = 8 * (pp & 1);
-          const char* base = lds + sub * 8192;
-          const s16x4 b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(base + lds_off(8 * gq + q, chk) + inb));
-          const s16x4 b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(base + lds_off(8 * gq + 4 + q, chk) + inb));
-          u16x8 bv;
-          bv[0] = b0[0]; bv[1] = b0[1]; bv[2] = b0[2]; bv[3] = b0[3];
-          bv[4] = b1[0]; bv[5] = b1[1]; bv[6] = b1[2]; bv[7] = b1[3];
-          accb[j] = mfma16x16x32(as_bf16x8(ah), as_bf16x8(bv), accb[j]);
-          accb[j] = mfma16x16x32(as_bf16x8(al), as_bf16x8(bv), accb[j]);
-        }
-      }
-      __syncthreads();
-      if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 12);
-    }
-    // ---- accumulate partial sums (no-return fp32 atomics at the memory side) ----
-    // The accumulator fragments hold 4 class rows x 16 features per lane group,
-    // half of them padding for K = 6; transposing through LDS turns them into
-    // K*FP/64 fully populated wave-instructions of 256 contiguous bytes each
-    // (the shape the memory-side atomic units serve at full rate).
-    float* gs = (float*)lds;  // [K][FP] (the X image is no longer needed)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int f = (w * NTW + j) * 16 + (lane & 15);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int c = (lane >> 4) * 4 + rr;
-        if (c < K) gs[c * FP + f] = accb[j][rr];
+        split_bf16((XO[e] + t_next * dn[e]) * iv + FX[e], h, l);
+        const int o = (fl >> 3) * 128 + c * 8 + (fl & 7);
+        frl[o] = h;
+        frl[512 + o] = l;
       }
     }
-    atomicAdd(&rsum[sc0], rs0);
-    atomicAdd(&rsum[sc0 + 1], rs1);
-    loss = wave_sum(loss);
-    if (lane == 0) lred[w] = loss;
+    if (ib) dv.b_eff[tid] = xbv + t_next * dbv;
     __syncthreads();
-    for (int e = tid; e < K * FP; e += 256) {
-      const int c = e / FP, f = e - c * FP;
-      atomicAdd(dv.Gacc + c * FPI + f, gs[e]);
+    if (tid < 128) {
+      const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
+      uint16_t* dst = tid < 64 ? dv.whi : dv.wlo;
+      *(u16x8*)(dst + go) = *(const u16x8*)(frl + tid * 8);
     }
-    if (tid < K) atomicAdd(dv.Racc + tid, rsum[tid]);
-    if (tid == 0) atomicAdd(dv.Lacc, lred[0] + lred[1] + lred[2] + lred[3]);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, slot, 1);
-  // ---- arrival ----
-  // Every wave drains its no-return atomics (vmcnt counts them until the memory
-  // side has performed them), then one lane takes a ticket.  No agent release /
-  // acquire pair is needed: this launch publishes nothing through plain
-  // stores -- the tail consumes only memory-side atomic sums (read back with
-  // atomic exchanges) and data written by EARLIER launches (kernel-boundary
-  // visibility); the eval part never reads a line the tail writes.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(&ctrl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  if (tid == 0) stamp(dv, slot, 2);
-  solve_tail<FP, KP>(cfg, prm, ctrl, slot, dv, lds);
-  if (tid == 0) stamp(dv, slot, 8);
+  if (wg0 && tid == 0) stamp(dv, slot, 8);
 }
 
 // ---------------------------------------------------------------------------
@@ -620,6 +612,7 @@ template <int KP>
 __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl* ctrl, SolveDev dv) {
   const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
   const int f = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
   if (f < FP) {
     const float iv = dv.inv_std[f];
     float xv[KP], fx[KP], wo[KP];
@@ -684,52 +677,52 @@ void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv,
 }
 
 // ---------------------------------------------------------------------------
-size_t stats_prep_lds_bytes() { return (size_t)(2 * 64 * 128 + 256) * sizeof(float); }
+size_t stats_prep_lds_bytes() { return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float); }
 
 void launch_stats_prep(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s) {
-  stats_prep_kernel<<<cfg.Fp / 128, 1024, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl);
+  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl);
 }
 
-size_t slot_lds_bytes(int FP) {
-  size_t a = eval_lds_bytes(FP);
-  size_t b = 2 * (size_t)16 * FP * 2 + ctrl_lds_bytes() + 5 * kND * sizeof(double) + sizeof(CtrlScratch) + 64;
-  return a > b ? a : b;
-}
-
+size_t fwd_lds_bytes(int FP) { return eval_lds_bytes(FP); }
 int padded_classes(int K) { return K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16; }
 int padded_stride(int FP) { return FP > 256 ? FP : 256; }
+int bwd_grid(int FP) { return FP / 32; }
 
 template <int FP>
 static void launch_slot_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
-                           int nwg, size_t lds, hipStream_t s) {
+                           int nwg, hipStream_t s) {
+  fwd_kernel<FP><<<nwg, 256, fwd_lds_bytes(FP), s>>>(cfg, prm, ctrl, slot, dv);
+  const int ng = bwd_grid(FP);
+  const size_t bl = bwd_lds_bytes();
   switch (dv.KP) {
-    case 2: slot_kernel<FP, 2><<<nwg, 256, lds, s>>>(cfg, prm, ctrl, slot, dv); break;
-    case 4: slot_kernel<FP, 4><<<nwg, 256, lds, s>>>(cfg, prm, ctrl, slot, dv); break;
-    case 8: slot_kernel<FP, 8><<<nwg, 256, lds, s>>>(cfg, prm, ctrl, slot, dv); break;
-    default: slot_kernel<FP, 16><<<nwg, 256, lds, s>>>(cfg, prm, ctrl, slot, dv); break;
+    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    default: bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
   }
 }
 
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                  hipStream_t s) {
-  const size_t lds = slot_lds_bytes(cfg.Fp);
   switch (cfg.Fp) {
-    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, lds, s); break;
-    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, lds, s); break;
-    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, lds, s); break;
-    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, lds, s); break;
-    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, lds, s); break;
+    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s); break;
+    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s); break;
+    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s); break;
+    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s); break;
+    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s); break;
     default: break;
   }
 }
 
 template <int FP>
 static void set_slot_attr() {
-  const int b = (int)slot_lds_bytes(FP);
-  (void)hipFuncSetAttribute((const void*)slot_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)slot_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)slot_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)slot_kernel<FP, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)fwd_kernel<FP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)fwd_lds_bytes(FP));
+  const int b = (int)bwd_lds_bytes();
+  (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 void prepare_solve_kernels() {
@@ -740,8 +733,6 @@ void prepare_solve_kernels() {
   set_slot_attr<512>();
   set_slot_attr<1024>();
   set_slot_attr<2048>();
-  (void)hipFuncSetAttribute((const void*)stats_prep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)stats_prep_lds_bytes());
   done = true;
 }
 

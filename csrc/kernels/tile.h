@@ -96,16 +96,23 @@ struct WFrag {
   u16x8 h[KS], l[KS];
 };
 
+// Lanes of classes >= K hold zero fragments without fetching them (the
+// fragment layout pads classes to 16; for K = 6 that skips 10/16 of the bytes).
 template <int FP>
 __device__ __forceinline__ void load_wfrag(WFrag<FP>& wf, const uint16_t* __restrict__ wf_hi,
-                                           const uint16_t* __restrict__ wf_lo) {
+                                           const uint16_t* __restrict__ wf_lo, int K = 16) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool live = (lane & 15) < K;
 #pragma unroll
   for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
     const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
     const size_t fo = ((size_t)cg * 16 + (lane & 15)) * 8;
-    wf.h[kk] = *(const u16x8*)(wf_hi + fo);
-    wf.l[kk] = *(const u16x8*)(wf_lo + fo);
+    wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      wf.h[kk] = *(const u16x8*)(wf_hi + fo);
+      wf.l[kk] = *(const u16x8*)(wf_lo + fo);
+    }
   }
 }
 

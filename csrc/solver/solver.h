@@ -3,8 +3,8 @@
 // The reference runs, per worker iteration, a Spark job: build a DataFrame from
 // the buffer, fit(), evaluate on the test set, diff the coefficients
 // (reference: LogisticRegressionTaskSpark.java:142-221).  Here the whole chain
-//   set_params -> stats_prep -> slot_0 ... slot_{nslots-1}
-// (each slot = one fused evaluation + controller step, see
+//   set_params -> stats_prep -> (eval, update) x nslots -> finalize
+// (each slot = one function evaluation + one controller step, see
 // csrc/kernels/solve_kernels.hip) is captured ONCE into a hipGraph and
 // replayed per iteration: the host pays one graph launch and the device runs
 // the chain back to back with no host synchronisation; line-search control
@@ -23,6 +23,7 @@ namespace psx {
 struct SolverBuffers {
   // caller-owned (torch tensors)
   const uint16_t* X = nullptr;  // ring [cap][Fp] bf16
+  const uint16_t* XT = nullptr; // ring feature-major [Fp][cap] bf16
   const int32_t* y = nullptr;   // ring labels [cap]
   const float* w_old = nullptr; // [P] current model (worker copy)
   float* delta = nullptr;       // [P] out: w_new - w_old
@@ -45,7 +46,7 @@ class LocalSolver {
   void run(int B, int start, hipStream_t stream);
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
-  int kernels_per_solve() const { return 3 + cfg_.nslots; }
+  int kernels_per_solve() const { return 2 + 2 * cfg_.nslots; }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):

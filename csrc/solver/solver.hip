@@ -19,8 +19,9 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   if (cfg.P != cfg.K * cfg.Fp + cfg.K) throw std::invalid_argument("P mismatch");
   if (cfg.hist < 1 || cfg.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
   if (cfg.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
-  if (cfg.cap < 1) throw std::invalid_argument("ring capacity must be >= 1");
-  const int tiles = (cfg.cap + kTileRows - 1) / kTileRows;
+  if (cfg.cap < 32 || cfg.cap % 32 != 0) throw std::invalid_argument("ring capacity must be a positive multiple of 32");
+  if (!buf.XT) throw std::invalid_argument("the solver needs the feature-major ring copy XT");
+  const int tiles = cfg.cap / kTileRows + 1;  // window tiles (ring-aligned; a wrapped window may touch one twice)
   nwg_eval_ = tiles < max_eval_wg ? tiles : max_eval_wg;
   if (nwg_eval_ < 1) nwg_eval_ = 1;
 
@@ -41,7 +42,9 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const size_t o_S = take(H * PI * 4), o_Y = take(H * PI * 4);
   const size_t o_std = take(FPI * 4), o_istd = take(FPI * 4), o_wfix = take(PI * 4), o_beff = take(16 * 4);
   const size_t o_whi = take(16 * FP * 2), o_wlo = take(16 * FP * 2);
-  const size_t o_G = take((size_t)dv_.KP * FPI * 4), o_R = take(16 * 4), o_L = take(16);
+  const size_t o_R = take((size_t)tiles * 1024 * 2);
+  const size_t o_part = take((size_t)nwg_eval_ * 32 * 4);
+  const size_t o_xch = take((size_t)xch_words() * 8);
   const bool stamps = std::getenv("PSX_SOLVER_STAMPS") != nullptr;
   const size_t o_dbg = stamps ? take(32 * 16 * sizeof(long long)) : 0;
   ws_bytes_ = off;
@@ -51,6 +54,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   prm_ = reinterpret_cast<SolveParams*>(b + o_prm);
   ctrl_ = reinterpret_cast<Ctrl*>(b + o_ctrl);
   dv_.X = buf.X;
+  dv_.XT = buf.XT;
   dv_.y = buf.y;
   dv_.w_old = buf.w_old;
   dv_.x = reinterpret_cast<float*>(b + o_x);
@@ -64,9 +68,9 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.b_eff = reinterpret_cast<float*>(b + o_beff);
   dv_.whi = reinterpret_cast<uint16_t*>(b + o_whi);
   dv_.wlo = reinterpret_cast<uint16_t*>(b + o_wlo);
-  dv_.Gacc = reinterpret_cast<float*>(b + o_G);
-  dv_.Racc = reinterpret_cast<float*>(b + o_R);
-  dv_.Lacc = reinterpret_cast<float*>(b + o_L);
+  dv_.R = reinterpret_cast<unsigned short*>(b + o_R);
+  dv_.part = reinterpret_cast<float*>(b + o_part);
+  dv_.xch = reinterpret_cast<unsigned long long*>(b + o_xch);
   dv_.delta = buf.delta;
   dv_.w_new = buf.w_new;
   dv_.out_hi = buf.wf_hi;

@@ -76,8 +76,8 @@ class LocalSolveOp:
         self._native = None
         self._bound = None
 
-    def _bind(self, X: torch.Tensor, y: torch.Tensor, w_old: torch.Tensor):
-        key = (X.data_ptr(), y.data_ptr(), w_old.data_ptr())
+    def _bind(self, ring, w_old: torch.Tensor):
+        key = (ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr())
         if self._bound == key:
             return
         h = _native.hip()
@@ -89,19 +89,22 @@ class LocalSolveOp:
         cfg.center, cfg.zero_const = int(o.center), int(o.zero_const)
         cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
         self._native = h.LocalSolver(
-            cfg, X.data_ptr(), y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(), self.w_new.data_ptr(),
-            self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(), self.loss.data_ptr(),
-            self.stats.data_ptr(), o.max_eval_wg, o.use_graph)
+            cfg, ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
+            self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
+            self.loss.data_ptr(), self.stats.data_ptr(), o.max_eval_wg, o.use_graph)
         self._bound = key
 
-    def run(self, X: torch.Tensor, y: torch.Tensor, B: int, start: int, w_old: torch.Tensor):
-        """Enqueue a solve over ring rows [start, start+B) (mod cap)."""
+    def run(self, ring, B: int, start: int, w_old: torch.Tensor):
+        """Enqueue a solve over the window [start, start+B) (mod cap) of ``ring`` (a DeviceRing)."""
         if B <= 0:
             raise ValueError("local solve on an empty buffer")
+        if ring.cap != self.cap:
+            raise ValueError(f"ring capacity {ring.cap} != solver capacity {self.cap}")
+        X, y = ring.X, ring.y
         if is_gpu(self.device):
             if X.dtype != torch.bfloat16 or X.shape != (self.cap, self.spec.Fp) or y.dtype != torch.int32:
                 raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
-            self._bind(X, y, w_old)
+            self._bind(ring, w_old)
             self._native.run(int(B), int(start), stream_handle(self.device))
             return
         s, o = self.spec, self.opts

@@ -13,7 +13,8 @@ MI355X design:
   then floor(1000/p) rows per second; native ``due_rows``), or, for
   throughput runs, a fixed number of rows per iteration;
 * window bookkeeping (rate estimate, target size, O(1) slot choice) is the
-  native :class:`SlidingWindow`; the device ring has capacity ``max`` rows.
+  native :class:`SlidingWindow`; the device ring has capacity ``max`` rows
+  rounded up to whole 32-row tiles.
 """
 from __future__ import annotations
 
@@ -27,10 +28,21 @@ from ..ops.lr import is_gpu, stream_handle
 
 
 class DeviceRing:
+    """Row ring of one worker.  ``cap`` is rounded up to whole 32-row tiles (the
+    solver walks windows as ring-aligned tiles); on the GPU a feature-major copy
+    ``XT`` [Fp][cap] is kept in step so the backward / statistics kernels read
+    every 32-feature slice of a window contiguously."""
+
+    TILE = 32
+
     def __init__(self, cap: int, Fp: int, device):
-        self.cap, self.Fp, self.device = int(cap), int(Fp), torch.device(device)
+        self.requested = int(cap)
+        self.cap = -(-int(cap) // self.TILE) * self.TILE
+        self.Fp, self.device = int(Fp), torch.device(device)
         self.X = torch.zeros(self.cap, self.Fp, dtype=torch.bfloat16, device=self.device)
         self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+        self.XT = (torch.zeros(self.Fp, self.cap, dtype=torch.bfloat16, device=self.device)
+                   if is_gpu(self.device) else None)
 
     def ingest(self, src_X: torch.Tensor, src_y: torch.Tensor, src_first: int, src_step: int, n: int, dst_first: int):
         """Copy rows src_first + i*src_step (i < n) into slots (dst_first + i) % cap."""
@@ -38,13 +50,26 @@ class DeviceRing:
             return
         if is_gpu(self.device):
             _native.hip().ring_ingest(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
-                                      self.X.data_ptr(), self.y.data_ptr(), int(dst_first), self.cap, self.Fp,
-                                      stream_handle(self.device))
+                                      self.X.data_ptr(), self.XT.data_ptr(), self.y.data_ptr(), int(dst_first),
+                                      self.cap, self.Fp, stream_handle(self.device))
         else:
             src = torch.arange(n) * src_step + src_first
             dst = (torch.arange(n) + dst_first) % self.cap
             self.X[dst] = src_X[src]
             self.y[dst] = src_y[src]
+
+    def place(self, X: torch.Tensor, y: torch.Tensor, first: int = 0):
+        """Write rows X[i], y[i] into slots (first + i) % cap (tests, tools)."""
+        idx = (torch.arange(X.shape[0]) + int(first)) % self.cap
+        idx = idx.to(self.device)
+        self.X[idx] = X.to(self.device, torch.bfloat16)
+        self.y[idx] = y.to(self.device, torch.int32)
+        self.sync_transposed()
+
+    def sync_transposed(self):
+        """Rebuild XT after direct writes to X."""
+        if self.XT is not None:
+            self.XT.copy_(self.X.t())
 
 
 class StreamSource:

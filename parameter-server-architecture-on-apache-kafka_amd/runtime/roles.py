@@ -28,11 +28,11 @@ class WorkerRole:
         self.k, self.spec, self.cfg, self.device = k, spec, cfg, torch.device(device)
         self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device)
         self.window = _native.host.SlidingWindow(cfg.min_buffer_size, cfg.max_buffer_size,
-                                                 cfg.buffer_size_coefficient, 500)
+                                                 cfg.buffer_size_coefficient, 500, self.ring.cap)
         self.source = StreamSource(train, k, cfg.num_workers, self.ring, self.window,
                                    p_ms=cfg.producer_time_per_event, mode=cfg.stream_mode,
                                    rows_per_iter=cfg.rows_per_iter, epochs=cfg.epochs, t0=t0)
-        self.solver = LocalSolveOp(spec, cfg.max_buffer_size, self.device, cfg.solver)
+        self.solver = LocalSolveOp(spec, self.ring.cap, self.device, cfg.solver)
         self.evalset = evalset
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
         self.conf = torch.zeros(256, dtype=torch.int32, device=self.device)
@@ -60,7 +60,7 @@ class WorkerRole:
         if self.delay_s > 0:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)
-        self.solver.run(self.ring.X, self.ring.y, B, start, self.w)
+        self.solver.run(self.ring, B, start, self.w)
         if log is not None and self.evalset is not None:
             self.evalset.confusion_async(self.solver.frag, self.solver.w_new, self.conf)
             log.submit_worker(self.k, self.vc, self.tuples_seen, self.solver.loss, self.conf)

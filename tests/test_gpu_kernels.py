@@ -47,19 +47,14 @@ def test_logits_match_fp32(cuda, F, K, T):
 
 def _ring_with(ds, cap, start, B, device):
     ring = DeviceRing(cap, ds.Fp, device)
-    Xc = ring.X.cpu()
-    yc = ring.y.cpu()
-    idx = (torch.arange(B) + start) % cap
-    Xc[idx] = ds.X[:B]
-    yc[idx] = ds.y[:B]
-    ring.X.copy_(Xc)
-    ring.y.copy_(yc)
+    ring.place(ds.X[:B], ds.y[:B], start)
     return ring
 
 
 @pytest.mark.parametrize(
     "mode,iters,B,start,F",
-    [("lbfgs", 2, 700, 900, 1024), ("lbfgs", 6, 1024, 0, 1024), ("gd", 3, 333, 10, 1024), ("lbfgs", 2, 50, 0, 99)],
+    [("lbfgs", 2, 700, 900, 1024), ("lbfgs", 6, 1024, 0, 1024), ("gd", 3, 333, 10, 1024), ("lbfgs", 2, 50, 0, 99),
+     ("lbfgs", 2, 1024, 1000, 1024)],  # full wrapped window: its first ring tile is visited twice
 )
 def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
     cap = 1024
@@ -74,7 +69,7 @@ def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
     opts = SolverOptions(iters=iters, mode=mode, gd_lr=0.5, ls_max=6)
     op = LocalSolveOp(spec, cap, cuda, opts)
     wd = w_old.to(cuda)
-    op.run(ring.X, ring.y, B, start, wd)
+    op.run(ring, B, start, wd)
     torch.cuda.synchronize()
     ref = local_solve_reference(ds.float_features(), ds.y.long(), spec.coef(w_old), spec.intercept(w_old),
                                 iters=iters, hist=opts.hist, ls_max=opts.ls_max, nslots=opts.nslots, mode=mode,
@@ -99,7 +94,7 @@ def test_graph_and_eager_agree(cuda):
     for g in (True, False):
         op = LocalSolveOp(spec, 1024, cuda, SolverOptions(use_graph=g))
         for _ in range(3):  # replays must be identical
-            op.run(ring.X, ring.y, 512, 100, w)
+            op.run(ring, 512, 100, w)
         torch.cuda.synchronize()
         outs.append(op.delta.clone())
     # the gradient sums use fp32 atomics (arrival order varies), so replays agree
@@ -148,3 +143,4 @@ def test_ring_ingest_strided_wrap(cuda):
     dst = (torch.arange(50) + 40) % 64
     assert torch.equal(ring.X.cpu()[dst], ds.X.cpu()[src])
     assert torch.equal(ring.y.cpu()[dst], ds.y.cpu()[src])
+    assert torch.equal(ring.XT.cpu(), ring.X.cpu().t())

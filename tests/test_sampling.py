@@ -91,3 +91,15 @@ def test_bad_arguments():
         host.SlidingWindow(10, 5, 0.3)
     with pytest.raises(Exception):
         host.SlidingWindow(1, 5, 0.0)
+
+
+def test_window_ring_capacity_rounding():
+    # the device ring rounds `max` up to whole 32-row tiles; the window size is
+    # still bounded by `max` while slots wrap at the ring capacity
+    w = host.SlidingWindow(10, 100, 100.0, 500, 128)
+    assert w.capacity == 128 and w.max_size == 100
+    for i in range(130):
+        w.insert(float(i))  # 1 ms apart: target clamps to max
+    assert w.size == 100
+    assert w.head == 129 % 128
+    assert w.start == (w.head - w.size + 1) % 128

@@ -17,12 +17,12 @@ from psx.utils.data import synth_finefood  # noqa: E402
 
 def time_solve(op, ring, B, w, reps=200):
     for _ in range(10):
-        op.run(ring.X, ring.y, B, 0, w)
+        op.run(ring, B, 0, w)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        op.run(ring.X, ring.y, B, 0, w)
+        op.run(ring, B, 0, w)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1000.0 / reps
@@ -37,20 +37,25 @@ def stamps(B=1024, opts=None):
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(1024, seed=0)
     ring = DeviceRing(1024, spec.Fp, dev)
-    ring.X.copy_(ds.X.to(dev))
-    ring.y.copy_(ds.y.to(dev))
+    ring.place(ds.X, ds.y)
     w = spec.init("random", seed=1).to(dev)
     op = LocalSolveOp(spec, 1024, dev, opts or SolverOptions())
     for _ in range(5):
-        op.run(ring.X, ring.y, B, 0, w)
+        op.run(ring, B, 0, w)
     torch.cuda.synchronize()
     h = torch.cuda.current_stream().cuda_stream
     st = op._native.read_stamps(h)
-    names = ["eval0", "eval0_end", "tail", "swapped", "dots", "ctrl", "updated", "written", "end", "staged",
-             "fwd", "softmax", "bwd"]
-    order = [0, 9, 10, 11, 12, 1, 2, 3, 4, 5, 6, 7, 8]
+    # fwd_kernel (workgroup 0): start, staged, fwd, softmax/R written, partials written;
+    # bwd_update_kernel (workgroup 0): start, backward done, G reduced, controller
+    # start / done (after the all-gather), controller written back, end
+    names = ["fwd0", "fwd_end", "bwd0", "bwd_mfma", "g_red", "ctrl", "ctrl_done", "ctrl_wb", "bwd_end", "staged",
+             "fwd", "softmax", "-"]
+    order = [0, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7, 8]
     print(f"--- stamps B={B} (us, relative to slot 0 start; 100 MHz) ---")
     base = st[0]
+    sv = st[30 * 16: 30 * 16 + 3]
+    print(f"stats_prep start={(sv[0] - base) / 100.0:.2f} end={(sv[1] - base) / 100.0:.2f}  "
+          f"finalize start={(sv[2] - base) / 100.0:.2f}")
     for slot in range(op.opts.nslots):
         row = st[slot * 16: slot * 16 + 13]
         if row[0] == 0 or row[0] < base:
@@ -68,8 +73,7 @@ def main():
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(1024, seed=0)
     ring = DeviceRing(1024, spec.Fp, dev)
-    ring.X.copy_(ds.X.to(dev))
-    ring.y.copy_(ds.y.to(dev))
+    ring.place(ds.X, ds.y)
     w = spec.init("random", seed=1).to(dev)
     rows = []
     for name, opts, B in [
@@ -92,7 +96,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(200):
-        op.run(ring.X, ring.y, 1024, 0, w)
+        op.run(ring, 1024, 0, w)
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     print(f"host enqueue per solve: {(t1 - t0) / 200 * 1e6:.1f} us")

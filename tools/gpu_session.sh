@@ -22,6 +22,13 @@ for s in $STEPS; do
       timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -2 $OUT/bench.log
       [ $rc -eq 0 ] || exit $rc ;;
+    solver)
+      timeout -k 10 240 python tools/bench_solver.py > $OUT/bench_solver.log 2>&1
+      rc=$?; echo "bench_solver rc=$rc"; tail -12 $OUT/bench_solver.log
+      [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 120 python tools/bench_solver.py --stamps > $OUT/stamps.log 2>&1
+      rc=$?; echo "stamps rc=$rc"; cat $OUT/stamps.log
+      [ $rc -eq 0 ] || exit $rc ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps ${PROF_STEPS:-300} --warmup 50 > $OUT/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -2 $OUT/prof.log

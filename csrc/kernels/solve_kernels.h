@@ -46,5 +46,10 @@ void launch_stats_prep(const SolverCfg& cfg, const SolveParams* prm, const Solve
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                  hipStream_t s);
+// Line-search retry slots [slot_begin, slot_end) in one persistent launch.
+void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
+                 const SolveDev& dv, int nwg, hipStream_t s);
+size_t tail_lds_bytes(int FP);
+int tail_grid(int FP, int nwg);
 
 }  // namespace psx

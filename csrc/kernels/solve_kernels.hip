@@ -60,7 +60,8 @@ constexpr int kND = 3 + 2 * kMaxHist;  // dot products: gt.gt, gt.d, gt.gc, S_i.
 constexpr int kNDX = kND + 1;          // + loss
 constexpr int kMaxSlices = 2048 / 32;
 constexpr int kXchTicket = kMaxSlices * kNDX;  // arrival counter (grows by #slices per slot)
-constexpr int kXchErr = kXchTicket + 1;
+constexpr int kXchBar = kXchTicket + 1;         // tail_kernel grid-barrier counter
+constexpr int kXchErr = kXchBar + 1;
 int xch_words() { return kXchErr + 1; }
 constexpr int kPartStride = 32;  // fwd partials per workgroup: rsum[16], loss
 
@@ -176,21 +177,22 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, const So
     if (t == 32) ctrl_init(*ctrl);
     if (t == 0) stamp(dv, 30, 1);
     if (t == 64) xstore(dv.xch + kXchTicket, 0ull);
+    if (t == 65) xstore(dv.xch + kXchBar, 0ull);
   }
 }
 
 // ---------------------------------------------------------------------------
 // fwd_kernel: loss and residuals at the trial point (row-parallel).
+// Body shared by fwd_kernel and tail_kernel: workgroup `wg` of `G` takes the
+// window tiles wg, wg+G, ...
 template <int FP>
-__global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl, int slot,
-                                                  SolveDev dv) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot: exit at once
+__device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams* prm, int slot, const SolveDev& dv,
+                                         char* lds, const int wg, const int G) {
   const int B = prm->B, K = cfg.K;
   const WinTiles wt(prm->start, B, cfg.cap);
   const int ntiles = wt.nt;
-  if ((int)blockIdx.x >= ntiles) return;
-  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
+  if (wg >= ntiles) return;
+  if (wg == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
   char* red_base = lds + 32 * FP * 2;
   unsigned short* rt = (unsigned short*)(red_base + 8192);  // [2][16][32]
   int* ylds = (int*)(red_base + 8192 + 2048);
@@ -208,12 +210,12 @@ __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolvePara
   constexpr bool kPre = FP <= 1024;
   WFrag<kPre ? FP : 128> wf;
   if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
     stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
     if (tid < 32) ylds[tid] = dv.y[row0 + tid];
     __syncthreads();
-    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 9);
+    if (wg == 0 && tid == 0) stamp(dv, slot, 9);
     f32x4 a0, a1;
     if constexpr (kPre)
       forward_tile_pre<FP>(lds, wf, a0, a1);
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolvePara
       forward_tile<FP>(lds, dv.whi, dv.wlo, a0, a1);
     store_partial_logits(red_base, a0, a1);
     __syncthreads();
-    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 10);
+    if (wg == 0 && tid == 0) stamp(dv, slot, 10);
     {  // softmax + cross entropy: 8 threads per row, 2 classes each
       const bool v0 = sc0 < K, v1 = sc0 + 1 < K;
       const float z0 = v0 ? load_logit(red_base, sr, sc0) + bz0 : -INFINITY;
@@ -259,17 +261,25 @@ __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolvePara
     __syncthreads();
     // residual tile -> global, in the A-operand layout of the backward MFMA
     *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
-    if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 11);
+    if (wg == 0 && tid == 0) stamp(dv, slot, 11);
   }
   atomicAdd(&rsum[sc0], rs0);
   atomicAdd(&rsum[sc0 + 1], rs1);
   loss = wave_sum(loss);
   if (lane == 0) lred[w] = loss;
   __syncthreads();
-  float* part = dv.part + (size_t)blockIdx.x * kPartStride;
+  float* part = dv.part + (size_t)wg * kPartStride;
   if (tid < 16) part[tid] = rsum[tid];
   if (tid == 16) part[16] = lred[0] + lred[1] + lred[2] + lred[3];
-  if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 1);
+  if (wg == 0 && tid == 0) stamp(dv, slot, 1);
+}
+
+template <int FP>
+__global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl, int slot,
+                                                  SolveDev dv) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot: exit at once
+  fwd_body<FP>(cfg, prm, slot, dv, lds, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -284,16 +294,15 @@ size_t bwd_lds_bytes() {
          (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) + sizeof(CtrlScratch);
 }
 
+// Body shared by bwd_update_kernel and tail_kernel: slice `wg` of `NS`.
 template <int FP, int KP>
-__global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
-                                                         SolveDev dv, int fwd_grid) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
+                                         const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS) {
   constexpr int FPI = FP > 256 ? FP : 256;
   constexpr int IB = KP * FPI;              // internal intercept base
   constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
-  if (gctrl->phase == kPhDone) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (blockIdx.x == 0 && tid == 0) stamp(dv, slot, 2);
+  if (wg == 0 && tid == 0) stamp(dv, slot, 2);
   float* gw = (float*)lds;                             // [4 waves][16 classes][32]
   unsigned short* frl = (unsigned short*)(gw + 4 * 16 * 32);  // [2][512] fragment staging
   Ctrl* cl = (Ctrl*)(frl + 1024);
@@ -312,10 +321,10 @@ __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const So
   const WinTiles wt(prm->start, B, cap);
   const size_t PI = dv.PI;
   const float invB = 1.f / (float)B;
-  const int fs = blockIdx.x * 32;
+  const int fs = wg * 32;
   const int fl = tid & 31, cgp = tid >> 5;
   const int f = fs + fl;
-  const bool wg0 = blockIdx.x == 0;
+  const bool wg0 = wg == 0;
 
   // ---- per-element state first (independent of the backward) ----
   float DD[NE], GC[NE], XO[NE], FX[NE];
@@ -452,11 +461,11 @@ __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const So
   // stores, every storing wave drains, one arrival RMW per workgroup on a
   // counter that only grows within a solve (reset by stats_prep), one lane
   // polls it relaxed, then sc1 loads of every workgroup's partials ----
-  const int ns = gridDim.x;
+  const int ns = NS;
   if (tid < kNDX) {
     const double v = sdot[tid] + sdot[kNDX + tid] + sdot[2 * kNDX + tid] + sdot[3 * kNDX + tid];
     if (ns > 1)
-      xstore(xch + blockIdx.x * kNDX + tid, d2u(v));
+      xstore(xch + wg * kNDX + tid, d2u(v));
     else
       gat[tid] = v;
   }
@@ -604,6 +613,70 @@ __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const So
   if (wg0 && tid == 0) stamp(dv, slot, 8);
 }
 
+template <int FP, int KP>
+__global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
+                                                         SolveDev dv, int fwd_grid) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (gctrl->phase == kPhDone) return;
+  bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, fwd_grid, lds, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// tail_kernel: the line-search retry slots [slot_begin, slot_end) in ONE
+// persistent launch.  The usual solve is done after 1 + iters evaluations
+// (every line search accepts its first trial), so this launch exits on its
+// first instruction; when a line search does need more evaluations they run
+// here as fwd phase -> grid barrier -> bwd phase -> grid barrier, instead of
+// as 2 launches per budgeted slot that are almost always empty.
+// Grid = max(fwd grid, slices); all workgroups are co-resident (<= 512).
+// Barriers: plain stores -> every wave drains -> __syncthreads -> lane 0
+// agent release fence -> drain -> arrival RMW on a monotone counter -> relaxed
+// poll -> agent acquire fence (the CDNA4 playbook's counter barrier); the
+// controller phase is re-read with sc1 loads (never through the scalar cache).
+__device__ __forceinline__ void grid_barrier(unsigned long long* ctr, unsigned long long target,
+                                             unsigned long long* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)__hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (xload(ctr) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 24)) {
+        xstore(err, 2ull);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int FP, int KP>
+__global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl,
+                                                   int slot_begin, int slot_end, SolveDev dv, int ns, int lds_flag) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
+  if (gctrl->phase == kPhDone) return;  // the common case: written by the previous launch
+  const int G = gridDim.x, wg = blockIdx.x;
+  unsigned long long* bar = dv.xch + kXchBar;
+  unsigned long long nb = 0;
+  for (int slot = slot_begin; slot < slot_end; ++slot) {
+    if (slot > slot_begin) {
+      if (threadIdx.x == 0) phase_s = (int)(unsigned)xload((unsigned long long*)&gctrl->phase);
+      __syncthreads();
+      if (phase_s == kPhDone) break;  // uniform: every workgroup read the same word after the barrier
+    }
+    fwd_body<FP>(cfg, prm, slot, dv, lds, wg, G);
+    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
+    if (wg < ns) bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, G, lds, wg, ns);
+    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Finalisation (after the last slot): back to the unstandardised space,
 // multinomial centring across classes, delta = w_new - w_old, eval fragments,
@@ -714,8 +787,48 @@ void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int s
   }
 }
 
+size_t tail_lds_bytes(int FP) {
+  const size_t a = fwd_lds_bytes(FP), b = bwd_lds_bytes();
+  return ((a > b ? a : b) + 15) / 16 * 16 + 16;
+}
+int tail_grid(int FP, int nwg) {
+  const int ns = bwd_grid(FP), g = nwg < 64 ? nwg : 64;
+  return g > ns ? g : ns;
+}
+
+template <int FP>
+static void launch_tail_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int s0, int s1,
+                           const SolveDev& dv, int nwg, hipStream_t s) {
+  const int G = tail_grid(FP, nwg), ns = bwd_grid(FP);
+  const size_t lb = tail_lds_bytes(FP);
+  const int flag = (int)(lb - 16);
+  switch (dv.KP) {
+    case 2: tail_kernel<FP, 2><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
+    case 4: tail_kernel<FP, 4><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
+    case 8: tail_kernel<FP, 8><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
+    default: tail_kernel<FP, 16><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
+  }
+}
+
+void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
+                 const SolveDev& dv, int nwg, hipStream_t s) {
+  switch (cfg.Fp) {
+    case 128: launch_tail_fp<128>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    case 256: launch_tail_fp<256>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    case 512: launch_tail_fp<512>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    case 1024: launch_tail_fp<1024>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    case 2048: launch_tail_fp<2048>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    default: break;
+  }
+}
+
 template <int FP>
 static void set_slot_attr() {
+  const int tb = (int)tail_lds_bytes(FP);
+  (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
+  (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
+  (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
+  (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
   (void)hipFuncSetAttribute((const void*)fwd_kernel<FP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)fwd_lds_bytes(FP));
   const int b = (int)bwd_lds_bytes();

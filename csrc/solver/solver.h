@@ -3,7 +3,7 @@
 // The reference runs, per worker iteration, a Spark job: build a DataFrame from
 // the buffer, fit(), evaluate on the test set, diff the coefficients
 // (reference: LogisticRegressionTaskSpark.java:142-221).  Here the whole chain
-//   set_params -> stats_prep -> (eval, update) x nslots -> finalize
+//   set_params -> stats_prep -> (fwd, bwd_update) x (1 + iters) -> tail -> finalize
 // (each slot = one function evaluation + one controller step, see
 // csrc/kernels/solve_kernels.hip) is captured ONCE into a hipGraph and
 // replayed per iteration: the host pays one graph launch and the device runs
@@ -46,7 +46,7 @@ class LocalSolver {
   void run(int B, int start, hipStream_t stream);
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
-  int kernels_per_solve() const { return 2 + 2 * cfg_.nslots; }
+  int kernels_per_solve() const { return 2 + 2 * nfast_ + (cfg_.nslots > nfast_ ? 1 : 0); }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):
@@ -58,6 +58,7 @@ class LocalSolver {
   SolverCfg cfg_;
   SolveDev dv_{};
   int nwg_eval_;
+  int nfast_;
   bool use_graph_;
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;

@@ -24,6 +24,10 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const int tiles = cfg.cap / kTileRows + 1;  // window tiles (ring-aligned; a wrapped window may touch one twice)
   nwg_eval_ = tiles < max_eval_wg ? tiles : max_eval_wg;
   if (nwg_eval_ < 1) nwg_eval_ = 1;
+  // slots launched one by one: the initial evaluation + one trial per iteration
+  // (what a solve whose line searches accept their first trial uses); the
+  // remaining budget runs in the persistent tail launch
+  nfast_ = cfg.mode == 1 ? cfg.nslots : (1 + cfg.iters < cfg.nslots ? 1 + cfg.iters : cfg.nslots);
 
   // solver-private vectors use the padded layout of solve_kernels.hip
   dv_.KP = padded_classes(cfg.K);
@@ -43,7 +47,8 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const size_t o_std = take(FPI * 4), o_istd = take(FPI * 4), o_wfix = take(PI * 4), o_beff = take(16 * 4);
   const size_t o_whi = take(16 * FP * 2), o_wlo = take(16 * FP * 2);
   const size_t o_R = take((size_t)tiles * 1024 * 2);
-  const size_t o_part = take((size_t)nwg_eval_ * 32 * 4);
+  const int npart = nwg_eval_ > tail_grid(cfg.Fp, nwg_eval_) ? nwg_eval_ : tail_grid(cfg.Fp, nwg_eval_);
+  const size_t o_part = take((size_t)npart * 32 * 4);
   const size_t o_xch = take((size_t)xch_words() * 8);
   const bool stamps = std::getenv("PSX_SOLVER_STAMPS") != nullptr;
   const size_t o_dbg = stamps ? take(32 * 16 * sizeof(long long)) : 0;
@@ -99,7 +104,8 @@ LocalSolver::~LocalSolver() {
 
 void LocalSolver::enqueue_body(hipStream_t s) {
   launch_stats_prep(cfg_, prm_, dv_, ctrl_, s);
-  for (int slot = 0; slot < cfg_.nslots; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
+  for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
+  if (cfg_.nslots > nfast_) launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s);
   launch_finalize(cfg_, ctrl_, dv_, s);
   hip_check(hipGetLastError(), "solver kernel launch");
 }

@@ -85,6 +85,30 @@ def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
     assert stats[1] == ref.accepted, (stats, ref.accepted)
 
 
+@pytest.mark.parametrize("seed,iters", [(4, 2), (5, 6)])
+def test_line_search_retries_run_in_tail(cuda, seed, iters):
+    """Large initial weights make some line searches need several evaluations:
+    those run in the persistent tail launch and must match the reference."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(512, 1024, seed=seed)
+    g = torch.Generator().manual_seed(seed + 100)
+    w_old = torch.randn(spec.P, generator=g) * 8.0
+    opts = SolverOptions(iters=iters, ls_max=6)
+    ring = _ring_with(ds, 1024, 37, 512, cuda)
+    op = LocalSolveOp(spec, 1024, cuda, opts)
+    op.run(ring, 512, 37, w_old.to(cuda))
+    torch.cuda.synchronize()
+    ref = local_solve_reference(ds.float_features(), ds.y.long(), spec.coef(w_old), spec.intercept(w_old),
+                                iters=iters, hist=opts.hist, ls_max=opts.ls_max, nslots=opts.nslots)
+    stats = op.stats.cpu().tolist()
+    assert ref.evals > ref.accepted + 1  # the case really exercises retries
+    assert stats[0] == ref.evals and stats[1] == ref.accepted, (stats, ref.evals, ref.accepted)
+    assert abs(op.loss.item() - ref.loss) < 1e-3 * max(1.0, abs(ref.loss)), (op.loss.item(), ref.loss)
+    delta = op.delta.cpu()
+    scale = max(ref.delta_coef.abs().max().item(), 1e-6)
+    assert (spec.coef(delta) - ref.delta_coef).abs().max().item() / scale < 2e-2
+
+
 def test_graph_and_eager_agree(cuda):
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(512, seed=5)

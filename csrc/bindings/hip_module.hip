@@ -4,6 +4,7 @@
 // the Python layer validates shapes/dtypes before calling in.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <cstring>
 #include <pybind11/stl.h>
 
 #include <memory>
@@ -117,12 +118,29 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("eval_wg", &LocalSolver::eval_wg)
       .def_property_readonly("kernels_per_solve", &LocalSolver::kernels_per_solve);
 
-  m.def("test_eval", [](int FP, int K, uintptr_t Xt, uintptr_t yt, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b,
-                        uintptr_t conf, uintptr_t stream) {
-    prepare_kernels();
-    launch_test_eval(FP, K, P<const uint16_t>(Xt), P<const int32_t>(yt), T, P<const uint16_t>(whi),
-                     P<const uint16_t>(wlo), P<const float>(b), P<int>(conf), S(stream));
-    hip_check(hipGetLastError(), "test_eval launch");
+  m.def(
+      "test_eval",
+      [](int FP, int K, uintptr_t Xt, uintptr_t yt, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t conf,
+         uintptr_t stream, uintptr_t ticket, uintptr_t slot, uintptr_t loss, unsigned long long seq) {
+        prepare_kernels();
+        launch_test_eval(FP, K, P<const uint16_t>(Xt), P<const int32_t>(yt), T, P<const uint16_t>(whi),
+                         P<const uint16_t>(wlo), P<const float>(b), P<int>(conf), S(stream), P<unsigned>(ticket),
+                         P<void>(slot), P<const float>(loss), seq);
+        hip_check(hipGetLastError(), "test_eval launch");
+      },
+      py::arg("FP"), py::arg("K"), py::arg("Xt"), py::arg("yt"), py::arg("T"), py::arg("whi"), py::arg("wlo"),
+      py::arg("b"), py::arg("conf"), py::arg("stream"), py::arg("ticket") = 0, py::arg("slot") = 0,
+      py::arg("loss") = 0, py::arg("seq") = 0);
+  // Fine-grained (coherent) pinned host memory: device stores land in host
+  // memory without a copy and device loads never see a stale cached line.
+  m.def("pinned_alloc", [](size_t bytes) {
+    void* p = nullptr;
+    hip_check(hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+    std::memset(p, 0, bytes);
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("pinned_free", [](uintptr_t p) {
+    if (p) (void)hipHostFree(reinterpret_cast<void*>(p));
   });
   m.def("logits", [](int FP, int K, uintptr_t X, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t out,
                      uintptr_t stream) {

@@ -7,6 +7,7 @@
 #include "../host/ctrl.h"
 #include "../host/dataset.h"
 #include "../host/logger.h"
+#include "../host/metrics_sink.h"
 #include "../host/sampling.h"
 #include "../host/tracker.h"
 #include "../kernels/solver_ctrl.h"
@@ -204,4 +205,49 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("flush", &CsvLogger::flush, py::call_guard<py::gil_scoped_release>())
       .def("close", &CsvLogger::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("lines", &CsvLogger::lines);
+
+  m.attr("EVAL_SLOT_BYTES") = (int)sizeof(EvalSlot);
+  m.def(
+      "weighted_f1_accuracy",
+      [](py::array_t<int32_t, py::array::c_style | py::array::forcecast> conf16, int K) {
+        if (conf16.size() != 256) throw std::invalid_argument("need a 16x16 confusion matrix");
+        double f1 = 0.0, acc = 0.0;
+        weighted_f1_accuracy(conf16.data(), K, &f1, &acc);
+        return py::make_tuple(f1, acc);
+      },
+      py::arg("conf16"), py::arg("K"));
+  py::class_<MetricsSink>(m, "MetricsSink")
+      .def(py::init([](uintptr_t slots, int nslots, int K, CsvLogger* wlog, CsvLogger* slog, bool keep) {
+             return std::make_unique<MetricsSink>(slots, nslots, K, wlog, slog, keep);
+           }),
+           py::arg("slots"), py::arg("nslots"), py::arg("K"), py::arg("wlog").none(true), py::arg("slog").none(true),
+           py::arg("keep_records") = true, py::keep_alive<1, 5>(), py::keep_alive<1, 6>())
+      .def(
+          "acquire",
+          [](MetricsSink& s) {
+            uint64_t seq = 0;
+            int slot;
+            {
+              py::gil_scoped_release nogil;
+              slot = s.acquire(&seq);
+            }
+            return py::make_tuple(slot, seq, s.slot_address(slot));
+          })
+      .def("submit", &MetricsSink::submit, py::arg("slot"), py::arg("seq"), py::arg("kind"), py::arg("ts"),
+           py::arg("partition"), py::arg("vc"), py::arg("nseen"))
+      .def("flush", &MetricsSink::flush, py::arg("timeout_s") = 0.0, py::call_guard<py::gil_scoped_release>())
+      .def("close", &MetricsSink::close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("processed", &MetricsSink::processed)
+      .def("worker_rows",
+           [](MetricsSink& s) {
+             py::list out;
+             for (const auto& r : s.worker_rows())
+               out.append(py::make_tuple(r.ts, r.partition, r.vc, r.loss, r.f1, r.acc, r.nseen));
+             return out;
+           })
+      .def("server_rows", [](MetricsSink& s) {
+        py::list out;
+        for (const auto& r : s.server_rows()) out.append(py::make_tuple(r.ts, r.vc, r.f1, r.acc));
+        return out;
+      });
 }

@@ -1,0 +1,152 @@
+#include "metrics_sink.h"
+
+#include <chrono>
+#include <stdexcept>
+
+namespace psx {
+
+void weighted_f1_accuracy(const int32_t* conf16, int K, double* f1, double* acc) {
+  // Spark MulticlassMetrics: weightedFMeasure = sum over labels present in the
+  // data of (label count / total) * F1(label); precision/recall are 0 when
+  // their denominator is 0 (reference Metrics.java:15-24).
+  double total = 0.0, tp_sum = 0.0, wf1 = 0.0;
+  double tc[16] = {0}, pc[16] = {0};
+  for (int t = 0; t < K; ++t)
+    for (int p = 0; p < K; ++p) {
+      const double v = conf16[t * 16 + p];
+      tc[t] += v;
+      pc[p] += v;
+      total += v;
+    }
+  if (total <= 0.0) {
+    *f1 = 0.0;
+    *acc = 0.0;
+    return;
+  }
+  for (int c = 0; c < K; ++c) {
+    const double tp = conf16[c * 16 + c];
+    tp_sum += tp;
+    const double prec = pc[c] > 0.0 ? tp / pc[c] : 0.0;
+    const double rec = tc[c] > 0.0 ? tp / tc[c] : 0.0;
+    const double f = prec + rec > 0.0 ? 2.0 * prec * rec / (prec + rec) : 0.0;
+    wf1 += tc[c] / total * f;
+  }
+  *f1 = wf1;
+  *acc = tp_sum / total;
+}
+
+MetricsSink::MetricsSink(uintptr_t slots, int nslots, int K, CsvLogger* wlog, CsvLogger* slog, bool keep_records)
+    : slots_(reinterpret_cast<EvalSlot*>(slots)), nslots_(nslots), K_(K), wlog_(wlog), slog_(slog),
+      keep_(keep_records) {
+  if (!slots_ || nslots_ < 1) throw std::invalid_argument("MetricsSink needs at least one slot");
+  if (K_ < 1 || K_ > 16) throw std::invalid_argument("MetricsSink: K must be in [1,16]");
+  for (int i = nslots_ - 1; i >= 0; --i) {
+    __atomic_store_n(&slots_[i].seq, 0ull, __ATOMIC_RELAXED);
+    free_.push_back(i);
+  }
+  th_ = std::thread([this] { run(); });
+}
+
+MetricsSink::~MetricsSink() { close(); }
+
+int MetricsSink::acquire(uint64_t* seq) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_free_.wait(lk, [&] { return !free_.empty() || stop_; });
+  if (stop_) throw std::runtime_error("MetricsSink is closed");
+  const int s = free_.back();
+  free_.pop_back();
+  *seq = next_seq_++;
+  return s;
+}
+
+uintptr_t MetricsSink::slot_address(int slot) const {
+  if (slot < 0 || slot >= nslots_) throw std::out_of_range("slot");
+  return reinterpret_cast<uintptr_t>(&slots_[slot]);
+}
+
+void MetricsSink::submit(int slot, uint64_t seq, int kind, int64_t ts, int64_t partition, int64_t vc,
+                         int64_t nseen) {
+  if (slot < 0 || slot >= nslots_) throw std::out_of_range("slot");
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    pending_.push_back(Pending{slot, seq, kind, ts, partition, vc, nseen});
+    ++submitted_;
+  }
+  cv_work_.notify_one();
+}
+
+void MetricsSink::run() {
+  for (;;) {
+    Pending p;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_work_.wait(lk, [&] { return stop_ || !pending_.empty(); });
+      if (pending_.empty()) return;  // stop requested and nothing left
+      p = pending_.front();
+    }
+    // the producer (a kernel or the CPU path) publishes seq after the payload
+    EvalSlot& s = slots_[p.slot];
+    int spins = 0;
+    while (__atomic_load_n(&s.seq, __ATOMIC_ACQUIRE) != p.seq) {
+      if (++spins < 64) continue;
+      std::this_thread::sleep_for(std::chrono::microseconds(spins < 4096 ? 5 : 200));
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_ && spins > 100000) break;  // closing with a producer that never ran: give up
+    }
+    double f1 = 0.0, acc = 0.0;
+    weighted_f1_accuracy(s.conf, K_, &f1, &acc);
+    const double loss = s.loss;
+    if (p.kind == 0) {
+      if (wlog_) wlog_->log_worker(p.ts, p.partition, p.vc, loss, f1, acc, p.nseen);
+    } else {
+      if (slog_) slog_->log_server(p.ts, p.vc, f1, acc);
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (keep_) {
+        if (p.kind == 0)
+          wrows_.push_back(WorkerRow{p.ts, p.partition, p.vc, loss, f1, acc, p.nseen});
+        else
+          srows_.push_back(ServerRow{p.ts, p.vc, f1, acc});
+      }
+      pending_.pop_front();
+      free_.push_back(p.slot);
+      processed_.fetch_add(1);
+    }
+    cv_free_.notify_one();
+    cv_done_.notify_all();
+  }
+}
+
+bool MetricsSink::flush(double timeout_s) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto done = [&] { return processed_.load() >= submitted_; };
+  if (timeout_s <= 0.0) {
+    cv_done_.wait(lk, done);
+    return true;
+  }
+  return cv_done_.wait_for(lk, std::chrono::duration<double>(timeout_s), done);
+}
+
+void MetricsSink::close() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stop_ && !th_.joinable()) return;
+    stop_ = true;
+  }
+  cv_work_.notify_all();
+  cv_free_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+std::vector<WorkerRow> MetricsSink::worker_rows() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return wrows_;
+}
+
+std::vector<ServerRow> MetricsSink::server_rows() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return srows_;
+}
+
+}  // namespace psx

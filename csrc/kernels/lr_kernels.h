@@ -16,8 +16,13 @@ void prepare_kernels();
 
 void launch_set_params(SolveParams* p, int B, int start, hipStream_t s);
 // Test-set prediction + KxK confusion counts (conf: zeroed int[16*16]).
+// Confusion counts of the test set.  slot == nullptr: accumulate into conf
+// (must be zeroed by the caller).  Otherwise conf is a private accumulator
+// (zero, left zero) with its `ticket` word, and the counts + *loss land in the
+// pinned host EvalSlot `slot`, published with sequence number `seq`.
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
-                      const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s);
+                      const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket = nullptr,
+                      void* slot = nullptr, const float* loss = nullptr, unsigned long long seq = 0);
 void launch_logits(int FP, int K, const uint16_t* X, int T, const uint16_t* wf_hi, const uint16_t* wf_lo,
                    const float* b, float* logits, hipStream_t s);
 // Server update w += lr * delta (all P entries) and refresh the eval fragments.

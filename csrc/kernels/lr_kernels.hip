@@ -35,16 +35,23 @@ void launch_set_params(SolveParams* p, int B, int start, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // K8/K9: test-set argmax + confusion matrix (LDS counts, one global atomic per
-// non-zero cell per workgroup).
+// non-zero cell per workgroup).  With an EvalSlot destination the workgroups
+// accumulate into a private device accumulator, and the last one to arrive
+// (ticket after draining its memory-side atomics) reads-and-zeroes it, writes
+// the counts (+ the worker's loss) into the pinned host slot, and publishes the
+// record's sequence number with a system-scope release store -- the host-side
+// MetricsSink picks it up with no copy, event or fill launch.
 template <int FP>
 __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* __restrict__ Xt,
                                                         const int32_t* __restrict__ yt, int T,
                                                         const uint16_t* __restrict__ wf_hi,
                                                         const uint16_t* __restrict__ wf_lo,
-                                                        const float* __restrict__ b, int* conf) {
+                                                        const float* __restrict__ b, int* acc, unsigned* ticket,
+                                                        char* slot, const float* loss, unsigned long long seq) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [16][16]
+  int* last = cl + 256;
   const int tid = threadIdx.x;
   cl[tid] = 0;
   const int ntiles = (T + 31) / 32;
@@ -74,18 +81,36 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   }
   __syncthreads();
   const int v = cl[tid];
-  if (v) atomicAdd(conf + tid, v);
+  if (v) atomicAdd(acc + tid, v);
+  if (slot == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!*last) return;
+  const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ((int*)slot)[tid] = tot;
+  if (tid == 0) *(float*)(slot + 1024) = loss ? *loss : 0.f;
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
-                      const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s) {
+                      const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket, void* slot,
+                      const float* loss, unsigned long long seq) {
   const size_t lds = eval_lds_bytes(FP);
   const int ntiles = (T + 31) / 32;
   const int grid = ntiles < 1024 ? ntiles : 1024;
   if (grid <= 0) return;
-#define PSX_TE(FPV)                                                                    \
-  case FPV:                                                                            \
-    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf); \
+  char* sl = static_cast<char*>(slot);
+#define PSX_TE(FPV)                                                                                        \
+  case FPV:                                                                                                \
+    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf, ticket, sl, loss, seq); \
     break;
   switch (FP) {
     PSX_TE(128)

@@ -87,16 +87,18 @@ __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_b
 // ---------------------------------------------------------------------------
 // stats + prep: grid = FP/32 workgroups of 256 threads; 8 lanes per feature
 // read the feature-major ring copy XT in contiguous 16-B pieces of 8 rows.
-__global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, const SolveParams* prm, SolveDev dv,
+__global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv,
                                                          Ctrl* ctrl) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* rs = (double*)smem;  // [32]
   double* rq = rs + 32;        // [32]
   float* sdl = (float*)(rq + 32);  // [32]
   float* ivl = sdl + 32;           // [32]
-  const int B = prm->B, cap = cfg.cap, FP = cfg.Fp;
-  const WinTiles wt(prm->start, B, cap);
+  const SolveParams pr = dv.prm_ring[*dv.prm_count & dv.prm_mask];  // this run's window
+  const int B = pr.B, cap = cfg.cap, FP = cfg.Fp;
+  const WinTiles wt(pr.start, B, cap);
   const int t = threadIdx.x, j = t & 7, fl0 = t >> 3;
+  if (blockIdx.x == 0 && t == 0) *prm = pr;  // the later launches read it from device memory
   if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
   const int fs = blockIdx.x * 32;
   const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
@@ -730,6 +732,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl
       dv.b_fin[c] = v;
     }
     *dv.loss = (float)ctrl->f_c;
+    *dv.prm_count += 1;  // the next run's parameters
     if (dv.stats) {
       dv.stats[0] = ctrl->evals;
       dv.stats[1] = ctrl->nacc;
@@ -752,7 +755,7 @@ void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv,
 // ---------------------------------------------------------------------------
 size_t stats_prep_lds_bytes() { return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float); }
 
-void launch_stats_prep(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s) {
+void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s) {
   stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl);
 }
 

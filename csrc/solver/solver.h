@@ -3,7 +3,7 @@
 // The reference runs, per worker iteration, a Spark job: build a DataFrame from
 // the buffer, fit(), evaluate on the test set, diff the coefficients
 // (reference: LogisticRegressionTaskSpark.java:142-221).  Here the whole chain
-//   set_params -> stats_prep -> (fwd, bwd_update) x (1 + iters) -> tail -> finalize
+//   stats_prep -> (fwd, bwd_update) x (1 + iters) -> tail -> finalize
 // (each slot = one function evaluation + one controller step, see
 // csrc/kernels/solve_kernels.hip) is captured ONCE into a hipGraph and
 // replayed per iteration: the host pays one graph launch and the device runs
@@ -63,6 +63,11 @@ class LocalSolver {
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;
   SolveParams* prm_ = nullptr;
+  static constexpr int kPrmRing = 1024;  // in-flight runs the parameter ring can hold
+  SolveParams* prm_host_ = nullptr;      // pinned fine-grained ring [kPrmRing]
+  unsigned long long runs_ = 0;
+  hipEvent_t ring_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ring_ev_used_[4] = {false, false, false, false};
   Ctrl* ctrl_ = nullptr;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

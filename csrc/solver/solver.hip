@@ -52,6 +52,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const size_t o_xch = take((size_t)xch_words() * 8);
   const bool stamps = std::getenv("PSX_SOLVER_STAMPS") != nullptr;
   const size_t o_dbg = stamps ? take(32 * 16 * sizeof(long long)) : 0;
+  const size_t o_cnt = take(16);
   ws_bytes_ = off;
   hip_check(hipMalloc(&ws_, ws_bytes_), "hipMalloc(solver workspace)");
   hip_check(hipMemset(ws_, 0, ws_bytes_), "hipMemset(solver workspace)");
@@ -84,6 +85,13 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.loss = buf.loss;
   dv_.stats = buf.stats;
   dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
+  hip_check(hipHostMalloc(reinterpret_cast<void**>(&prm_host_), kPrmRing * sizeof(SolveParams),
+                          hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(solver parameter ring)");
+  dv_.prm_ring = prm_host_;
+  dv_.prm_count = reinterpret_cast<unsigned*>(b + o_cnt);
+  dv_.prm_mask = kPrmRing - 1;
+  for (auto& e : ring_ev_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
 
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -99,6 +107,9 @@ LocalSolver::~LocalSolver() {
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
+  for (auto& e : ring_ev_)
+    if (e) (void)hipEventDestroy(e);
+  if (prm_host_) (void)hipHostFree(prm_host_);
   if (ws_) (void)hipFree(ws_);
 }
 
@@ -113,12 +124,29 @@ void LocalSolver::enqueue_body(hipStream_t s) {
 void LocalSolver::run(int B, int start, hipStream_t stream) {
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
-  launch_set_params(prm_, B, start, stream);
+  // Parameter ring: entry r & mask belongs to run r.  Every 256 runs an event
+  // marks progress; before reusing entries the host waits for the event
+  // recorded kPrmRing runs earlier (never in steady state: the engine's own
+  // back-pressure keeps far fewer runs in flight).
+  constexpr unsigned long long kChunk = kPrmRing / 4;
+  if (runs_ % kChunk == 0) {
+    // entries of chunk c were last used by chunk c-4, which has completed once
+    // the event recorded at the first run of chunk c-3 has
+    const int e = (int)((runs_ / kChunk + 1) % 4);
+    if (ring_ev_used_[e]) hip_check(hipEventSynchronize(ring_ev_[e]), "parameter ring wait");
+  }
+  prm_host_[runs_ & (kPrmRing - 1)] = SolveParams{B, start};
   if (use_graph_) {
     hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
   } else {
     enqueue_body(stream);
   }
+  if (runs_ % kChunk == 0) {
+    const int e = (int)((runs_ / kChunk) % 4);
+    hip_check(hipEventRecord(ring_ev_[e], stream), "parameter ring event");
+    ring_ev_used_[e] = true;
+  }
+  ++runs_;
 }
 
 std::vector<long long> LocalSolver::read_stamps(hipStream_t stream) {

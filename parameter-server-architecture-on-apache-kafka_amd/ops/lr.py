@@ -150,6 +150,42 @@ class EvalSet:
         out.view(-1).copy_(c.to(torch.int32))
 
 
+    def eval_to_slot(self, frag: Fragments | None, w: torch.Tensor, scratch: "EvalScratch", slot_addr: int, seq: int,
+                     loss: torch.Tensor | None = None):
+        """Confusion counts of ``w`` (+ ``loss``) into the host EvalSlot at ``slot_addr``, published with ``seq``.
+
+        GPU: one kernel; its last workgroup writes the pinned slot directly and
+        releases ``seq`` (no fill / copy / event).  CPU: computed here.
+        """
+        s = self.spec
+        if is_gpu(self.device):
+            _native.hip().test_eval(s.Fp, s.K, self.X.data_ptr(), self.y.data_ptr(), self.T, frag.hi.data_ptr(),
+                                    frag.lo.data_ptr(), frag.b.data_ptr(), scratch.acc.data_ptr(),
+                                    stream_handle(self.device), scratch.ticket.data_ptr(), int(slot_addr),
+                                    loss.data_ptr() if loss is not None else 0, int(seq))
+            return
+        conf = torch.zeros(256, dtype=torch.int32)
+        self.confusion_async(None, w, conf)
+        _write_slot_cpu(slot_addr, conf, float(loss.item()) if loss is not None else 0.0, seq)
+
+
+class EvalScratch:
+    """Private accumulator + ticket of one evaluation caller (stays zero between calls)."""
+
+    def __init__(self, device):
+        self.acc = torch.zeros(256, dtype=torch.int32, device=device)
+        self.ticket = torch.zeros(4, dtype=torch.int32, device=device)
+
+
+def _write_slot_cpu(addr: int, conf: torch.Tensor, loss: float, seq: int):
+    import ctypes
+
+    ctypes.memmove(addr, conf.contiguous().numpy().ctypes.data, 1024)
+    ctypes.c_float.from_address(addr + 1024).value = loss
+    # the native reader acquires seq; the GIL-held stores above are already visible
+    ctypes.c_uint64.from_address(addr + 1032).value = int(seq)
+
+
 def server_apply(spec: ModelSpec, w: torch.Tensor, delta: torch.Tensor, lr: float, frag: Fragments | None):
     """w += lr * delta over all P entries (quirk Q1 fixed) + refresh eval fragments."""
     if is_gpu(w.device):

@@ -97,8 +97,12 @@ class LocalEngine:
     def _run_bsp(self) -> dict:
         cfg, srv, W = self.cfg, self.server, self.workers
         N = len(W)
-        for w in W:  # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87)
-            w.w.copy_(srv.w)
+        # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87).  Under BSP every
+        # worker pulls the same version right after the server update, and all
+        # solves of a round finish (stream order) before the update, so the
+        # workers' pulled copy IS the server tensor: no per-round copies.
+        for w in W:
+            w.w = srv.w
             w.vc = 0
         t_start = time.time()
         exhausted_since = None
@@ -129,7 +133,6 @@ class LocalEngine:
                 srv.log_eval(r, self.log)
                 for k, w in enumerate(W):
                     srv.tracker.sent(k, r + 1)
-                    w.w.copy_(srv.w)
                     w.vc = r + 1
             r += 1
             maybe_checkpoint(cfg, srv, r)
@@ -155,9 +158,9 @@ class LocalEngine:
             def __init__(s, inner):
                 s.inner = inner
 
-            def submit_worker(s, *a, **k):
+            def worker_eval(s, *a, **k):
                 with log_lock:
-                    s.inner.submit_worker(*a, **k)
+                    s.inner.worker_eval(*a, **k)
 
         locked = _LockedLog(self.log)
 

@@ -17,7 +17,7 @@ import torch
 
 from .. import _native
 from ..models.logreg import ModelSpec
-from ..ops.lr import EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply
+from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply
 from .buffer import DeviceRing, StreamSource
 from .config import PSConfig
 
@@ -35,7 +35,7 @@ class WorkerRole:
         self.solver = LocalSolveOp(spec, self.ring.cap, self.device, cfg.solver)
         self.evalset = evalset
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
-        self.conf = torch.zeros(256, dtype=torch.int32, device=self.device)
+        self.scratch = EvalScratch(self.device)
         self.vc = 0  # version of the weights currently held
         self.iters = 0
         self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
@@ -62,8 +62,8 @@ class WorkerRole:
         B, start = int(self.window.size), int(self.window.start)
         self.solver.run(self.ring, B, start, self.w)
         if log is not None and self.evalset is not None:
-            self.evalset.confusion_async(self.solver.frag, self.solver.w_new, self.conf)
-            log.submit_worker(self.k, self.vc, self.tuples_seen, self.solver.loss, self.conf)
+            log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch, self.solver.loss,
+                            self.k, self.vc, self.tuples_seen)
         self.iters += 1
         return self.solver.delta
 
@@ -77,7 +77,7 @@ class ServerRole:
             self.frag.refresh(self.w)
         self.tracker = _native.host.VectorClockTracker(cfg.num_workers, cfg.consistency_model)
         self.evalset = evalset
-        self.conf = torch.zeros(256, dtype=torch.int32, device=self.device)
+        self.scratch = EvalScratch(self.device)
         self.updates = 0
         self.acc = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
 
@@ -89,5 +89,4 @@ class ServerRole:
         """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
         if log is None or self.evalset is None:
             return
-        self.evalset.confusion_async(self.frag, self.w, self.conf)
-        log.submit_server(vc, self.conf)
+        log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc)

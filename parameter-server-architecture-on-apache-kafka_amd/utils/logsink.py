@@ -1,21 +1,23 @@
-"""Asynchronous CSV log sink.
+"""Asynchronous evaluation-record sink.
 
-Device results (loss, 16x16 confusion counts) are copied into pinned host slots
-with non-blocking copies and an event; rows are finalised (weighted F1 /
-accuracy) and handed to the native :class:`CsvLogger` once their event has
-completed, so logging never stalls the training stream.  Row format is the
-reference's (ServerAppRunner.java:78-82, WorkerAppRunner.java:77-81).
+Each record reserves a slot of a pinned (GPU) or plain (CPU) host ring; the
+evaluation kernel writes the 16x16 confusion counts and the worker's loss into
+that slot itself and publishes the record's sequence number (see
+``test_eval_kernel``); the native :class:`MetricsSink` thread waits for the
+number, computes Spark's weighted F1 / accuracy (Metrics.java:15-24) and writes
+the row through the native :class:`CsvLogger` in the reference's schema
+(ServerAppRunner.java:78-82, WorkerAppRunner.java:77-81).  Logging therefore
+costs the training loop one slot reservation + one submit per record: no
+device->host copies, events, fills or Python-side metric math.
 """
 from __future__ import annotations
 
-import collections
 import time
 
 import numpy as np
 import torch
 
 from .. import _native
-from .metrics import metrics_from_confusion
 
 
 def now_ms() -> int:
@@ -25,14 +27,33 @@ def now_ms() -> int:
 class RecordBook:
     """In-memory copy of every logged row (tests, benchmarks, plots)."""
 
-    def __init__(self):
-        self.worker = []  # (ts, partition, vc, loss, f1, acc, nseen)
-        self.server = []  # (ts, vc, f1, acc)
+    def __init__(self, worker=None, server=None):
+        self.worker = worker if worker is not None else []  # (ts, partition, vc, loss, f1, acc, nseen)
+        self.server = server if server is not None else []  # (ts, vc, f1, acc)
+
+
+class _HostSlots:
+    """nslots EvalSlot records in host memory the device can write."""
+
+    def __init__(self, nslots: int, gpu: bool):
+        self.bytes = nslots * _native.host.EVAL_SLOT_BYTES
+        self.gpu = gpu
+        if gpu:
+            self.ptr = _native.hip().pinned_alloc(self.bytes)
+            self._buf = None
+        else:
+            self._buf = np.zeros(self.bytes, dtype=np.uint8)
+            self.ptr = self._buf.ctypes.data
+
+    def free(self):
+        if self.gpu and self.ptr:
+            _native.hip().pinned_free(self.ptr)
+            self.ptr = 0
 
 
 class LogSink:
     def __init__(self, K: int, device, worker_path: str | None = None, server_path: str | None = None,
-                 to_stdout: bool = False, pool: int = 64, keep_records: bool = True, worker_append: bool = False):
+                 to_stdout: bool = False, pool: int = 256, keep_records: bool = True, worker_append: bool = False):
         self.K = K
         self.device = torch.device(device)
         self.gpu = self.device.type == "cuda"
@@ -40,72 +61,50 @@ class LogSink:
             _native.host.CsvLogger("", True, False) if to_stdout else None)
         self.slog = _native.host.CsvLogger(server_path, False, True) if server_path else (
             _native.host.CsvLogger("", False, False) if to_stdout else None)
-        self.book = RecordBook() if keep_records else None
-        self.pending = collections.deque()
-        self.pool = pool
-        self._free = []
-        for _ in range(pool):
-            conf = torch.zeros(256, dtype=torch.int32, pin_memory=self.gpu)
-            loss = torch.zeros(1, dtype=torch.float32, pin_memory=self.gpu)
-            self._free.append((conf, loss))
+        self.keep = keep_records
+        self.slots = _HostSlots(pool, self.gpu)
+        self.native = _native.host.MetricsSink(self.slots.ptr, pool, K, self.wlog, self.slog, keep_records)
+        self._closed = False
 
-    def _slot(self):
-        while not self._free:
-            self.drain(block_one=True)
-        return self._free.pop()
+    # -- producers --------------------------------------------------------
+    def worker_eval(self, evalset, frag, w, scratch, loss_dev, partition: int, vc: int, nseen: int,
+                    ts: int | None = None):
+        """Evaluate the worker's local model ``w`` and log a worker row."""
+        slot, seq, addr = self.native.acquire()
+        ts = ts or now_ms()
+        evalset.eval_to_slot(frag, w, scratch, addr, seq, loss_dev)
+        self.native.submit(slot, seq, 0, ts, int(partition), int(vc), int(nseen))
 
-    def submit_worker(self, partition: int, vc: int, nseen: int, loss_dev: torch.Tensor, conf_dev: torch.Tensor,
-                      ts: int | None = None):
-        conf, loss = self._slot()
-        conf.copy_(conf_dev.view(-1), non_blocking=True)
-        loss.copy_(loss_dev.view(-1)[:1], non_blocking=True)
-        ev = self._event()
-        self.pending.append(("w", ts or now_ms(), partition, vc, nseen, conf, loss, ev))
+    def server_eval(self, evalset, frag, w, scratch, vc: int, ts: int | None = None):
+        """Evaluate the global model ``w`` and log a server row."""
+        slot, seq, addr = self.native.acquire()
+        ts = ts or now_ms()
+        evalset.eval_to_slot(frag, w, scratch, addr, seq, None)
+        self.native.submit(slot, seq, 1, ts, -1, int(vc), 0)
 
-    def submit_server(self, vc: int, conf_dev: torch.Tensor, ts: int | None = None):
-        conf, loss = self._slot()
-        conf.copy_(conf_dev.view(-1), non_blocking=True)
-        ev = self._event()
-        self.pending.append(("s", ts or now_ms(), -1, vc, 0, conf, loss, ev))
+    # -- consumers ---------------------------------------------------------
+    def drain(self, block: bool = False):
+        """Rows are finalised by the native thread; ``block`` waits for all of them."""
+        if block:
+            self.native.flush()
 
-    def _event(self):
-        if not self.gpu:
+    @property
+    def book(self) -> RecordBook | None:
+        if not self.keep:
             return None
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        return ev
-
-    def drain(self, block: bool = False, block_one: bool = False):
-        while self.pending:
-            kind, ts, part, vc, nseen, conf, loss, ev = self.pending[0]
-            if ev is not None and not ev.query():
-                if block or block_one:
-                    ev.synchronize()
-                else:
-                    return
-            self.pending.popleft()
-            c = conf.numpy().reshape(16, 16)[: self.K, : self.K]
-            f1, acc = metrics_from_confusion(c)
-            if kind == "w":
-                lv = float(loss.item())
-                if self.wlog is not None:
-                    self.wlog.log_worker(ts, part, vc, lv, f1, acc, nseen)
-                if self.book is not None:
-                    self.book.worker.append((ts, part, vc, lv, f1, acc, nseen))
-            else:
-                if self.slog is not None:
-                    self.slog.log_server(ts, vc, f1, acc)
-                if self.book is not None:
-                    self.book.server.append((ts, vc, f1, acc))
-            self._free.append((conf, loss))
-            if block_one:
-                return
+        self.native.flush()
+        return RecordBook(self.native.worker_rows(), self.native.server_rows())
 
     def close(self):
-        self.drain(block=True)
+        if self._closed:
+            return
+        self.native.flush()
+        self.native.close()
         for lg in (self.wlog, self.slog):
             if lg is not None:
                 lg.close()
+        self.slots.free()
+        self._closed = True
 
 
 def summarize(book: RecordBook) -> dict:

@@ -146,6 +146,40 @@ def test_confusion_matches_cpu(cuda):
     assert diff <= 4, diff  # argmax ties at bf16/fp32 boundaries
 
 
+def test_eval_to_pinned_slot(cuda):
+    """The slot path (kernel writes counts + loss into pinned host memory and
+    publishes a sequence number) matches the CPU confusion, repeatedly (the
+    private accumulator must come back to zero after each call)."""
+    from psx.ops.lr import EvalScratch
+    from psx.utils.logsink import LogSink
+
+    spec = ModelSpec(1024, 6)
+    te = synth_finefood(4877, seed=9)
+    gpu = EvalSet(spec, te.X, te.y, cuda)
+    cpu = EvalSet(spec, te.X, te.y, "cpu")
+    log = LogSink(spec.K, cuda, pool=4)
+    scratch = EvalScratch(cuda)
+    frag = Fragments(spec, cuda)
+    rows = []
+    for seed in (3, 4, 5):
+        w = _rand_w(spec, seed, 0.5)
+        wd = w.to(cuda)
+        frag.refresh(wd)
+        loss = torch.tensor([float(seed)], device=cuda)
+        log.worker_eval(gpu, frag, wd, scratch, loss, 0, seed, 0)
+        cc = torch.zeros(256, dtype=torch.int32)
+        cpu.confusion_async(None, w, cc)
+        rows.append(cc)
+    book = log.book
+    log.close()
+    from psx.utils.metrics import metrics_from_confusion
+
+    for r, cc in zip(book.worker, rows):
+        f1, acc = metrics_from_confusion(cc.view(16, 16)[:6, :6].numpy())
+        assert abs(r[5] - acc) <= 4 / 4877 and r[3] == float(r[2])
+    assert scratch.acc.abs().sum().item() == 0 and scratch.ticket.abs().sum().item() == 0
+
+
 def test_server_apply(cuda):
     spec = ModelSpec(1024, 6)
     w = _rand_w(spec, 4).to(cuda)

@@ -68,3 +68,55 @@ def test_weighted_f1_matches_sklearn():
 
 def test_metrics_empty():
     assert metrics_from_confusion(np.zeros((3, 3))) == (0.0, 0.0)
+
+
+def test_native_metrics_match_numpy():
+    import numpy as np
+
+    from psx import _native
+    from psx.utils.metrics import metrics_from_confusion
+
+    rng = np.random.default_rng(0)
+    for K in (2, 6, 16):
+        c = np.zeros((16, 16), dtype=np.int32)
+        c[:K, :K] = rng.integers(0, 50, size=(K, K))
+        c[0, :] = 0  # a label absent from the data
+        f1, acc = _native.host.weighted_f1_accuracy(c, K)
+        rf1, racc = metrics_from_confusion(c[:K, :K])
+        assert abs(f1 - rf1) < 1e-12 and abs(acc - racc) < 1e-12
+
+
+def test_metrics_sink_cpu_rows(tmp_path):
+    import torch
+
+    from psx.models.logreg import ModelSpec
+    from psx.ops.lr import EvalScratch, EvalSet
+    from psx.utils.data import synth_finefood
+    from psx.utils.logsink import LogSink
+    from psx.utils.metrics import metrics_from_confusion
+
+    spec = ModelSpec(64, 6)
+    te = synth_finefood(300, 64, seed=2)
+    ev = EvalSet(spec, te.X, te.y, "cpu")
+    w = spec.init("random", seed=3)
+    wp, sp = tmp_path / "w.csv", tmp_path / "s.csv"
+    log = LogSink(spec.K, "cpu", str(wp), str(sp), pool=2)  # tiny pool: exercises slot reuse / back-pressure
+    scratch = EvalScratch("cpu")
+    loss = torch.tensor([0.25])
+    for i in range(5):
+        log.worker_eval(ev, None, w, scratch, loss, 0, i, 10 * i)
+        log.server_eval(ev, None, w, scratch, i)
+    book = log.book
+    log.close()
+    conf = torch.zeros(256, dtype=torch.int32)
+    ev.confusion_async(None, w, conf)
+    f1, acc = metrics_from_confusion(conf.view(16, 16)[:6, :6].numpy())
+    assert len(book.worker) == 5 and len(book.server) == 5
+    assert [r[2] for r in book.worker] == list(range(5))
+    assert all(abs(r[4] - f1) < 1e-12 and abs(r[5] - acc) < 1e-12 and r[3] == 0.25 for r in book.worker)
+    assert [r[1] for r in book.server] == list(range(5))
+    wl = wp.read_text().strip().splitlines()
+    sl = sp.read_text().strip().splitlines()
+    assert wl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen" and len(wl) == 6
+    assert sl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy" and len(sl) == 6
+    assert sl[1].split(";")[1:4] == ["-1", "0", "-1"]  # server rows: partition -1, loss -1

@@ -14,7 +14,7 @@ bool fp_supported(int FP);
 // Raise dynamic-LDS limits for the wide tile kernels (call before capture).
 void prepare_kernels();
 
-void launch_set_params(SolveParams* p, int B, int start, hipStream_t s);
+
 // Test-set prediction + KxK confusion counts (conf: zeroed int[16*16]).
 // Confusion counts of the test set.  slot == nullptr: accumulate into conf
 // (must be zeroed by the caller).  Otherwise conf is a private accumulator

@@ -24,14 +24,6 @@ namespace psx {
 bool fp_supported(int FP) { return FP == 128 || FP == 256 || FP == 512 || FP == 1024 || FP == 2048; }
 
 // ---------------------------------------------------------------------------
-__global__ void set_params_kernel(SolveParams* p, int B, int start) {
-  p->B = B;
-  p->start = start;
-}
-
-void launch_set_params(SolveParams* p, int B, int start, hipStream_t s) {
-  set_params_kernel<<<1, 1, 0, s>>>(p, B, start);
-}
 
 // ---------------------------------------------------------------------------
 // K8/K9: test-set argmax + confusion matrix (LDS counts, one global atomic per

@@ -32,12 +32,7 @@ struct SolveDev {
   // padded internal layout: KP classes (power of two >= K), feature stride FPI
   int KP, FPI, PI, pad_;
   long long* dbg;  // optional phase timeline (debug)
-  // per-run parameters: the host writes run r's (B, start) into the pinned
-  // fine-grained ring entry r & prm_mask before launching the graph;
-  // stats_prep reads entry *prm_count, finalize advances the counter.
-  const SolveParams* prm_ring;
-  unsigned* prm_count;
-  int prm_mask, pad2_;
+  unsigned* prm_count;  // runs completed (finalize advances it): all-gather tag base
 };
 
 int padded_classes(int K);
@@ -48,7 +43,9 @@ size_t fwd_lds_bytes(int FP);
 size_t bwd_lds_bytes();
 int bwd_grid(int FP);
 int xch_words();
-void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s);
+void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int B, int start,
+                       hipStream_t s);
+const void* stats_prep_symbol();
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                  hipStream_t s);

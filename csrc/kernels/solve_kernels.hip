@@ -47,6 +47,12 @@ namespace psx {
 __device__ __forceinline__ void stamp(const SolveDev& dv, int slot, int k) {
   if (dv.dbg && slot < 32) dv.dbg[slot * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
+// Per-workgroup phase stamps of slot 1's bwd_update (rows 16..23: phase p,
+// workgroup wg < 32) -- arrival-skew diagnosis.
+__device__ __forceinline__ void wg_stamp(const SolveDev& dv, int slot, int p, int wg) {
+  if (dv.dbg && slot == 1 && wg < 32 && threadIdx.x == 0)
+    dv.dbg[(16 + p * 2 + (wg >> 4)) * 16 + (wg & 15)] = (long long)__builtin_amdgcn_s_memrealtime();
+}
 
 // ---------------------------------------------------------------------------
 // Cross-workgroup exchange area of bwd_update_kernel: 64-bit words written
@@ -59,8 +65,7 @@ constexpr size_t ctrl_lds_bytes() { return ((sizeof(Ctrl) + 15) / 16) * 16; }
 constexpr int kND = 3 + 2 * kMaxHist;  // dot products: gt.gt, gt.d, gt.gc, S_i.gt, Y_i.gt
 constexpr int kNDX = kND + 1;          // + loss
 constexpr int kMaxSlices = 2048 / 32;
-constexpr int kXchTicket = kMaxSlices * kNDX;  // arrival counter (grows by #slices per slot)
-constexpr int kXchBar = kXchTicket + 1;         // tail_kernel grid-barrier counter
+constexpr int kXchBar = kMaxSlices * 2 * kNDX;  // [slices][2*kNDX] dot granules, then the tail barrier counter
 constexpr int kXchErr = kXchBar + 1;
 int xch_words() { return kXchErr + 1; }
 constexpr int kPartStride = 32;  // fwd partials per workgroup: rsum[16], loss
@@ -87,14 +92,16 @@ __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_b
 // ---------------------------------------------------------------------------
 // stats + prep: grid = FP/32 workgroups of 256 threads; 8 lanes per feature
 // read the feature-major ring copy XT in contiguous 16-B pieces of 8 rows.
-__global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv,
-                                                         Ctrl* ctrl) {
+__global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv, Ctrl* ctrl,
+                                                         int B_arg, int start_arg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* rs = (double*)smem;  // [32]
   double* rq = rs + 32;        // [32]
   float* sdl = (float*)(rq + 32);  // [32]
   float* ivl = sdl + 32;           // [32]
-  const SolveParams pr = dv.prm_ring[*dv.prm_count & dv.prm_mask];  // this run's window
+  // this run's window arrives as kernel arguments (the host rewrites this graph
+  // node's parameters per run); later launches read it from device memory
+  const SolveParams pr{B_arg, start_arg, 0, 0};
   const int B = pr.B, cap = cfg.cap, FP = cfg.Fp;
   const WinTiles wt(pr.start, B, cap);
   const int t = threadIdx.x, j = t & 7, fl0 = t >> 3;
@@ -178,7 +185,6 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
     }
     if (t == 32) ctrl_init(*ctrl);
     if (t == 0) stamp(dv, 30, 1);
-    if (t == 64) xstore(dv.xch + kXchTicket, 0ull);
     if (t == 65) xstore(dv.xch + kXchBar, 0ull);
   }
 }
@@ -305,6 +311,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (wg == 0 && tid == 0) stamp(dv, slot, 2);
+  wg_stamp(dv, slot, 0, wg);
+  const unsigned run_tag = *dv.prm_count * 32u;  // early: needed by the all-gather
   float* gw = (float*)lds;                             // [4 waves][16 classes][32]
   unsigned short* frl = (unsigned short*)(gw + 4 * 16 * 32);  // [2][512] fragment staging
   Ctrl* cl = (Ctrl*)(frl + 1024);
@@ -392,6 +400,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     }
   }
   if (wg0 && tid == 0) stamp(dv, slot, 3);
+  wg_stamp(dv, slot, 1, wg);
   // cross-wave reduction of the accumulators (D[class][feature])
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -459,48 +468,73 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     }
   }
   __syncthreads();
-  // ---- all-gather of the partial dots (write-through hand-off, R1): sc1
-  // stores, every storing wave drains, one arrival RMW per workgroup on a
-  // counter that only grows within a solve (reset by stats_prep), one lane
-  // polls it relaxed, then sc1 loads of every workgroup's partials ----
+  // ---- all-gather of the partial dots as tagged granules (the data is its
+  // own flag: R2 of the CDNA4 playbook).  Each workgroup stores its nv partial
+  // sums as 2*nv 8-byte words {tag, 32-bit half of the fp64 value} with sc1
+  // stores; every workgroup sweeps all slices' words with sc1 loads until each
+  // carries this (run, slot)'s tag, which never repeats (no reset needed) ----
   const int ns = NS;
-  if (tid < kNDX) {
-    const double v = sdot[tid] + sdot[kNDX + tid] + sdot[2 * kNDX + tid] + sdot[3 * kNDX + tid];
+  const int nv = 4 + 2 * H;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (H), Y_i.gt (H)
+  const unsigned tag = run_tag + (unsigned)slot + 1u;
+  unsigned* gat32 = (unsigned*)gat;  // [ns][2*nv]
+  if (tid < 2 * nv) {
+    const int k = tid >> 1;
+    const int si = k < 3 ? k : (k == 3 ? kND : (k < 4 + H ? 3 + (k - 4) : 3 + kMaxHist + (k - 4 - H)));
+    const double v = sdot[si] + sdot[kNDX + si] + sdot[2 * kNDX + si] + sdot[3 * kNDX + si];
+    const unsigned long long u = d2u(v);
+    const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
     if (ns > 1)
-      xstore(xch + wg * kNDX + tid, d2u(v));
+      xstore(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
     else
-      gat[tid] = v;
+      gat32[tid] = half;
   }
-  if (ns > 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      (void)__hip_atomic_fetch_add(xch + kXchTicket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long target = (unsigned long long)ns * (unsigned long long)(slot + 1);
+  wg_stamp(dv, slot, 2, wg);
+  // The storing wave (wave 0) does not sweep: vmcnt retires in order, so its
+  // loads would wait for its own write-through stores to complete.
+  if (ns > 1 && tid >= 64) {
+    const int total = ns * 2 * nv, st = tid - 64;
+    for (int i0 = 0; i0 < total; i0 += 192 * 8) {
+      unsigned long long x[8];
       int spins = 0;
-      while (xload(xch + kXchTicket) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1 << 24)) {  // never expected: record and fall through rather than hang
-          xstore(xch + kXchErr, 1ull);
-          break;
+      bool ok;
+      do {  // all 8 loads of the sweep in flight, then check the tags
+        ok = true;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int i = i0 + st + 192 * j;
+          if (i < total) {
+            const int b = i / (2 * nv), r = i - b * (2 * nv);
+            x[j] = xload(xch + (size_t)b * (2 * kNDX) + r);
+            ok &= (unsigned)(x[j] >> 32) == tag;
+          }
         }
+        if (!ok) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1 << 22)) {  // never expected: record and fall through rather than hang
+            xstore(xch + kXchErr, 1ull);
+            break;
+          }
+        }
+      } while (!ok);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + st + 192 * j;
+        if (i < total) gat32[i] = (unsigned)x[j];
       }
     }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the sc1 loads below the poll
-    for (int i = tid; i < ns * kNDX; i += 256) gat[i] = u2d(xload(xch + i));  // all in flight
   }
   __syncthreads();
-  if (tid < kNDX) {
+  wg_stamp(dv, slot, 3, wg);
+  if (tid < nv) {
     double v = 0.0;
-    for (int b = 0; b < ns; ++b) v += gat[b * kNDX + tid];  // fixed order: identical in every workgroup
-    // compact order expected by ctrl_step: 3 scalars, S_i.g (H), Y_i.g (H); loss last
-    int pos = tid;
-    if (tid >= 3 && tid < 3 + kMaxHist)
-      pos = tid - 3 < H ? tid : -1;
-    else if (tid >= 3 + kMaxHist && tid < kND)
-      pos = tid - 3 - kMaxHist < H ? 3 + H + (tid - 3 - kMaxHist) : -1;
-    if (pos >= 0) dots[pos] = v;
+    for (int b = 0; b < ns; ++b) {  // fixed order: identical in every workgroup
+      const unsigned long long u =
+          (unsigned long long)gat32[b * 2 * nv + 2 * tid] | ((unsigned long long)gat32[b * 2 * nv + 2 * tid + 1] << 32);
+      v += u2d(u);
+    }
+    // compact order expected by ctrl_step: 3 scalars, S_i.g (H), Y_i.g (H); loss in dots[kND]
+    const int pos = tid < 3 ? tid : (tid == 3 ? kND : tid - 1);
+    dots[pos] = v;
   }
   __syncthreads();
   if (tid == 0) {
@@ -732,7 +766,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl
       dv.b_fin[c] = v;
     }
     *dv.loss = (float)ctrl->f_c;
-    *dv.prm_count += 1;  // the next run's parameters
+    *dv.prm_count += 1;  // run counter: makes the all-gather tags unique per run
     if (dv.stats) {
       dv.stats[0] = ctrl->evals;
       dv.stats[1] = ctrl->nacc;
@@ -755,9 +789,11 @@ void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv,
 // ---------------------------------------------------------------------------
 size_t stats_prep_lds_bytes() { return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float); }
 
-void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, hipStream_t s) {
-  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl);
+void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int B, int start,
+                       hipStream_t s) {
+  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl, B, start);
 }
+const void* stats_prep_symbol() { return (const void*)stats_prep_kernel; }
 
 size_t fwd_lds_bytes(int FP) { return eval_lds_bytes(FP); }
 int padded_classes(int K) { return K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : 16; }

@@ -54,7 +54,7 @@ class LocalSolver {
   std::vector<long long> read_stamps(hipStream_t stream);
 
  private:
-  void enqueue_body(hipStream_t s);
+  void enqueue_body(hipStream_t s, int B, int start);
   SolverCfg cfg_;
   SolveDev dv_{};
   int nwg_eval_;
@@ -63,11 +63,18 @@ class LocalSolver {
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;
   SolveParams* prm_ = nullptr;
-  static constexpr int kPrmRing = 1024;  // in-flight runs the parameter ring can hold
-  SolveParams* prm_host_ = nullptr;      // pinned fine-grained ring [kPrmRing]
-  unsigned long long runs_ = 0;
-  hipEvent_t ring_ev_[4] = {nullptr, nullptr, nullptr, nullptr};
-  bool ring_ev_used_[4] = {false, false, false, false};
+  // the graph's first node (stats_prep) takes the window as kernel arguments,
+  // rewritten per run with hipGraphExecKernelNodeSetParams
+  hipGraphNode_t stats_node_ = nullptr;
+  struct StatsArgs {
+    SolverCfg cfg;
+    SolveParams* prm;
+    SolveDev dv;
+    Ctrl* ctrl;
+    int B, start;
+  } stats_args_{};
+  void* stats_kp_[6] = {};
+  hipKernelNodeParams stats_params_{};
   Ctrl* ctrl_ = nullptr;
   hipStream_t cap_stream_ = nullptr;
   hipGraph_t graph_ = nullptr;

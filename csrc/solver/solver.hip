@@ -85,21 +85,40 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.loss = buf.loss;
   dv_.stats = buf.stats;
   dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
-  hip_check(hipHostMalloc(reinterpret_cast<void**>(&prm_host_), kPrmRing * sizeof(SolveParams),
-                          hipHostMallocCoherent | hipHostMallocMapped),
-            "hipHostMalloc(solver parameter ring)");
-  dv_.prm_ring = prm_host_;
   dv_.prm_count = reinterpret_cast<unsigned*>(b + o_cnt);
-  dv_.prm_mask = kPrmRing - 1;
-  for (auto& e : ring_ev_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
 
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    enqueue_body(cap_stream_);
+    enqueue_body(cap_stream_, cfg.cap, 0);
     hip_check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
     hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+    size_t n = 0;
+    hip_check(hipGraphGetNodes(graph_, nullptr, &n), "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    hip_check(hipGraphGetNodes(graph_, nodes.data(), &n), "hipGraphGetNodes");
+    for (auto nd : nodes) {
+      hipGraphNodeType t;
+      hip_check(hipGraphNodeGetType(nd, &t), "hipGraphNodeGetType");
+      if (t != hipGraphNodeTypeKernel) continue;
+      hipKernelNodeParams kp{};
+      hip_check(hipGraphKernelNodeGetParams(nd, &kp), "hipGraphKernelNodeGetParams");
+      if (kp.func == stats_prep_symbol()) {
+        stats_node_ = nd;
+        stats_params_ = kp;
+      }
+    }
+    if (!stats_node_) throw std::runtime_error("solver graph: stats_prep node not found");
+    stats_args_ = StatsArgs{cfg_, prm_, dv_, ctrl_, cfg.cap, 0};
+    stats_kp_[0] = &stats_args_.cfg;
+    stats_kp_[1] = &stats_args_.prm;
+    stats_kp_[2] = &stats_args_.dv;
+    stats_kp_[3] = &stats_args_.ctrl;
+    stats_kp_[4] = &stats_args_.B;
+    stats_kp_[5] = &stats_args_.start;
+    stats_params_.kernelParams = stats_kp_;
+    stats_params_.extra = nullptr;
   }
 }
 
@@ -107,14 +126,11 @@ LocalSolver::~LocalSolver() {
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
-  for (auto& e : ring_ev_)
-    if (e) (void)hipEventDestroy(e);
-  if (prm_host_) (void)hipHostFree(prm_host_);
   if (ws_) (void)hipFree(ws_);
 }
 
-void LocalSolver::enqueue_body(hipStream_t s) {
-  launch_stats_prep(cfg_, prm_, dv_, ctrl_, s);
+void LocalSolver::enqueue_body(hipStream_t s, int B, int start) {
+  launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, s);
   for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
   if (cfg_.nslots > nfast_) launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s);
   launch_finalize(cfg_, ctrl_, dv_, s);
@@ -124,29 +140,14 @@ void LocalSolver::enqueue_body(hipStream_t s) {
 void LocalSolver::run(int B, int start, hipStream_t stream) {
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
-  // Parameter ring: entry r & mask belongs to run r.  Every 256 runs an event
-  // marks progress; before reusing entries the host waits for the event
-  // recorded kPrmRing runs earlier (never in steady state: the engine's own
-  // back-pressure keeps far fewer runs in flight).
-  constexpr unsigned long long kChunk = kPrmRing / 4;
-  if (runs_ % kChunk == 0) {
-    // entries of chunk c were last used by chunk c-4, which has completed once
-    // the event recorded at the first run of chunk c-3 has
-    const int e = (int)((runs_ / kChunk + 1) % 4);
-    if (ring_ev_used_[e]) hip_check(hipEventSynchronize(ring_ev_[e]), "parameter ring wait");
-  }
-  prm_host_[runs_ & (kPrmRing - 1)] = SolveParams{B, start};
   if (use_graph_) {
+    stats_args_.B = B;
+    stats_args_.start = start;
+    hip_check(hipGraphExecKernelNodeSetParams(exec_, stats_node_, &stats_params_), "hipGraphExecKernelNodeSetParams");
     hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
   } else {
-    enqueue_body(stream);
+    enqueue_body(stream, B, start);
   }
-  if (runs_ % kChunk == 0) {
-    const int e = (int)((runs_ / kChunk) % 4);
-    hip_check(hipEventRecord(ring_ev_[e], stream), "parameter ring event");
-    ring_ev_used_[e] = true;
-  }
-  ++runs_;
 }
 
 std::vector<long long> LocalSolver::read_stamps(hipStream_t stream) {

@@ -169,6 +169,7 @@ class EvalSet:
         _write_slot_cpu(slot_addr, conf, float(loss.item()) if loss is not None else 0.0, seq)
 
 
+
 class EvalScratch:
     """Private accumulator + ticket of one evaluation caller (stays zero between calls)."""
 

@@ -199,15 +199,21 @@ class DistEngine:
                     wk.ingest()
             with self.tracer.span("solve"):
                 delta = wk.compute(self.log) if wk is not None else zeros
+            logged = False
             with self.tracer.span("comm", schedule=sched):
                 if sched == "allreduce":
                     dist.all_reduce(delta, op=dist.ReduceOp.SUM)
-                    srv.apply(delta, lr)
+                    if self.rank == 0:  # update + server eval row in one kernel
+                        srv.apply_and_log(delta, r, self.log, lr)
+                        logged = True
+                    else:
+                        srv.apply(delta, lr)
                     new_w = srv.w
                 elif sched == "reduce_bcast":
                     dist.reduce(delta, dst=0, op=dist.ReduceOp.SUM)
                     if srv is not None:
-                        srv.apply(delta, lr)
+                        srv.apply_and_log(delta, r, self.log, lr)
+                        logged = True
                         new_w = srv.w
                     else:
                         new_w = wk.w
@@ -226,7 +232,8 @@ class DistEngine:
                 if self.rank == 0:
                     for k in range(N):
                         srv.tracker.received(k, r)
-                    srv.log_eval(r, self.log)
+                    if not logged:
+                        srv.log_eval(r, self.log)
                     for k in range(N):
                         srv.tracker.sent(k, r + 1)
                     maybe_checkpoint(cfg, srv, r + 1)
@@ -282,10 +289,11 @@ class DistEngine:
             k, v = int(tok.worker), int(tok.vc)
             with self.tracer.span("recv", worker=k, vc=v):
                 dist.recv(buf, src=k + 1)
-            srv.apply(buf)
+            if k == 0:  # server eval rows follow worker-0 deltas (ServerProcessor.java:154-165)
+                srv.apply_and_log(buf, v, self.log)
+            else:
+                srv.apply(buf)
             srv.updates += 1
-            if k == 0:
-                srv.log_eval(v, self.log)
             if tok.kind == KIND_FINAL:
                 finished.add(k)
             for j, u in srv.tracker.on_delta(k, v):

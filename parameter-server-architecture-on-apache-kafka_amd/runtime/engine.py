@@ -126,11 +126,10 @@ class LocalEngine:
                     total.copy_(deltas[0])
                     for d in deltas[1:]:
                         total.add_(d)
-                srv.apply(total)
+                srv.apply_and_log(total, r, self.log)  # w += lr*total and the server eval row, one kernel
                 for k in range(N):
                     srv.tracker.received(k, r)
                 srv.updates += N
-                srv.log_eval(r, self.log)
                 for k, w in enumerate(W):
                     srv.tracker.sent(k, r + 1)
                     w.vc = r + 1
@@ -231,11 +230,12 @@ class LocalEngine:
             if ev is not None:
                 torch.cuda.current_stream(self.device).wait_event(ev)
             with log_lock:
-                srv.apply(delta)
+                if k == 0:  # server eval rows follow worker-0 deltas (ServerProcessor.java:154-165)
+                    srv.apply_and_log(delta, v, self.log)
+                else:
+                    srv.apply(delta)
                 srv.updates += 1
                 per_worker[k] += 1
-                if k == 0:
-                    srv.log_eval(v, self.log)
                 for j, u in srv.tracker.on_delta(k, v):
                     send(j, u)
                 maybe_checkpoint(cfg, srv, srv.updates)

@@ -85,6 +85,13 @@ class ServerRole:
         """w += lr * delta   (ServerProcessor.java:148-151 with lr = 1/N)."""
         server_apply(self.spec, self.w, delta, self.cfg.lr if lr is None else lr, self.frag)
 
+    def apply_and_log(self, delta: torch.Tensor, vc: int, log, lr: float | None = None):
+        """apply() then the global-model evaluation row.  (A single fused
+        update+eval kernel was measured slower: every workgroup rebuilt the
+        weight fragments from fp32 -- profiles/r01_v2.)"""
+        self.apply(delta, lr)
+        self.log_eval(vc, log)
+
     def log_eval(self, vc: int, log):
         """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
         if log is None or self.evalset is None:

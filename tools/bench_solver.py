@@ -56,6 +56,15 @@ def stamps(B=1024, opts=None):
     sv = st[30 * 16: 30 * 16 + 3]
     print(f"stats_prep start={(sv[0] - base) / 100.0:.2f} end={(sv[1] - base) / 100.0:.2f}  "
           f"finalize start={(sv[2] - base) / 100.0:.2f}")
+    ph = ["start", "mfma", "publish", "gathered"]
+    rows = []
+    for p_ in range(4):
+        v = [st[(16 + p_ * 2 + (wg >> 4)) * 16 + (wg & 15)] for wg in range(32)]
+        v = [(x - base) / 100.0 for x in v if x >= base]
+        if v:
+            rows.append(f"{ph[p_]} min={min(v):.2f} max={max(v):.2f}")
+    if rows:
+        print("slot 1 per-workgroup bwd phases: " + "; ".join(rows))
     for slot in range(op.opts.nslots):
         row = st[slot * 16: slot * 16 + 13]
         if row[0] == 0 or row[0] < base:

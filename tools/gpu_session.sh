@@ -19,7 +19,7 @@ for s in $STEPS; do
       rc=$?; echo "smoke rc=$rc"; tail -3 $OUT/smoke.log
       [ $rc -eq 0 ] || exit $rc ;;
     bench)
-      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 && timeout -k 10 300 python bench.py ${BENCH_ARGS:-} >> $OUT/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -2 $OUT/bench.log
       [ $rc -eq 0 ] || exit $rc ;;
     solver)

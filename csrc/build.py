@@ -109,13 +109,32 @@ def build_hip(force=False, jobs=8):
         "-fvisibility=hidden",
         "-Wno-unused-result",
         "-munsafe-fp-atomics",
-        "-D__HIP_PLATFORM_AMD__",
     ] + ["-I" + i for i in _pybind_includes()]
     ldflags = [f"--offload-arch={ARCH}", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"]
     digest = _hash(sources + headers, cflags + ldflags)
     if not force and _up_to_date(out, digest):
         return out
     _compile_link(hipcc, sources, out, cflags, ldflags, jobs, os.path.join(ROOT, "build", "hip"))
+    open(out + ".hash", "w").write(digest)
+    return out
+
+
+def build_selftest(sanitize: str = "address,undefined", force=False):
+    """Host-runtime self-test binary (csrc/tests/host_selftest.cc) under a
+    sanitizer: "address,undefined" or "thread" (SURVEY.md §5.2)."""
+    sources = [os.path.join(CSRC, "tests", "host_selftest.cc")] + sorted(glob.glob(os.path.join(CSRC, "host", "*.cc")))
+    headers = sorted(glob.glob(os.path.join(CSRC, "host", "*.h")))
+    tag = sanitize.replace(",", "_")
+    out = os.path.join(ROOT, "build", "selftest", f"host_selftest_{tag}")
+    flags = ["-O1", "-g", "-std=c++17", f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
+    if "undefined" in sanitize:
+        flags.append("-fno-sanitize-recover=undefined")
+    digest = _hash(sources + headers, flags)
+    if not force and _up_to_date(out, digest):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    _run(["g++"] + flags + sources + ["-o", out + ".tmp", "-pthread", "-lrt"])
+    os.replace(out + ".tmp", out)
     open(out + ".hash", "w").write(digest)
     return out
 

@@ -92,7 +92,10 @@ void CsvLogger::flush() {
 void CsvLogger::run() {
   std::unique_lock<std::mutex> g(mu_);
   for (;;) {
-    cv_.wait_for(g, std::chrono::milliseconds(200), [&] { return stop_ || flush_req_ || pending_.size() > (1u << 16); });
+    // system_clock deadline: pthread_cond_timedwait (the steady_clock form maps
+    // to pthread_cond_clockwait, which the toolchain's TSAN does not model)
+    cv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(200),
+                   [&] { return stop_ || flush_req_ || pending_.size() > (1u << 16); });
     std::string out;
     out.swap(pending_);
     bool fl = flush_req_;

@@ -125,7 +125,10 @@ bool MetricsSink::flush(double timeout_s) {
     cv_done_.wait(lk, done);
     return true;
   }
-  return cv_done_.wait_for(lk, std::chrono::duration<double>(timeout_s), done);
+  const auto deadline = std::chrono::system_clock::now() +
+                        std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                            std::chrono::duration<double>(timeout_s));
+  return cv_done_.wait_until(lk, deadline, done);
 }
 
 void MetricsSink::close() {

@@ -120,3 +120,25 @@ def test_metrics_sink_cpu_rows(tmp_path):
     assert wl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen" and len(wl) == 6
     assert sl[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy" and len(sl) == 6
     assert sl[1].split(";")[1:4] == ["-1", "0", "-1"]  # server rows: partition -1, loss -1
+
+
+def test_plot_logs_reads_reference_logs(tmp_path):
+    """tools/plot_logs.py consumes the reference's own evaluation logs (shared
+    schema) and recovers its consistency behaviour: BSP gap 1, SSP(10) gap 11."""
+    import os
+    import sys
+
+    ref = "/root/reference/evaluation/logs/"
+    if not os.path.exists(ref + "sequential_logs-server.csv"):
+        import pytest
+
+        pytest.skip("reference logs not present")
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    import plot_logs
+
+    s, w = plot_logs.load(ref + "sequential_")
+    assert plot_logs.max_vc_gap(w) == 1
+    s2, w2 = plot_logs.load(ref + "bounded_delay_10_")
+    assert plot_logs.max_vc_gap(w2) == 11
+    assert plot_logs.main([ref + "sequential_", "--out", str(tmp_path), "--names", "seq"]) == 0
+    assert (tmp_path / "seq_accuracy.png").exists() and (tmp_path / "seq_consistency.png").exists()

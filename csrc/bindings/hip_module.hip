@@ -11,6 +11,7 @@
 
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
+#include "../solver/wide_solver.h"
 
 namespace py = pybind11;
 using namespace psx;
@@ -160,6 +161,118 @@ PYBIND11_MODULE(_psx_hip, m) {
     launch_make_fragments(K, F, FP, P<const float>(w), P<uint16_t>(whi), P<uint16_t>(wlo), P<float>(b), S(stream));
     hip_check(hipGetLastError(), "make_fragments launch");
   });
+  // ---- wide / sparse model (BASELINE.json configs 4, 5) ----
+  py::class_<WideCfg>(m, "WideCfg", py::module_local())
+      .def(py::init([]() {
+        WideCfg c{};
+        c.sc.iters = 2;
+        c.sc.hist = 10;
+        c.sc.ls_max = 4;
+        c.sc.nslots = 9;
+        c.sc.tol = 1e-6f;
+        c.sc.gd_lr = 1.f;
+        c.K = 2;
+        c.KP = 2;
+        c.F = 1;
+        c.cap = 1;
+        c.NZ = 1;
+        c.standardize = 1;
+        c.center = 1;
+        return c;
+      }))
+      .def_property("iters", [](const WideCfg& c) { return c.sc.iters; }, [](WideCfg& c, int v) { c.sc.iters = v; })
+      .def_property("hist", [](const WideCfg& c) { return c.sc.hist; }, [](WideCfg& c, int v) { c.sc.hist = v; })
+      .def_property("ls_max", [](const WideCfg& c) { return c.sc.ls_max; }, [](WideCfg& c, int v) { c.sc.ls_max = v; })
+      .def_property("mode", [](const WideCfg& c) { return c.sc.mode; }, [](WideCfg& c, int v) { c.sc.mode = v; })
+      .def_property("nslots", [](const WideCfg& c) { return c.sc.nslots; }, [](WideCfg& c, int v) { c.sc.nslots = v; })
+      .def_property("gd_lr", [](const WideCfg& c) { return c.sc.gd_lr; }, [](WideCfg& c, float v) { c.sc.gd_lr = v; })
+      .def_property("tol", [](const WideCfg& c) { return c.sc.tol; }, [](WideCfg& c, float v) { c.sc.tol = v; })
+      .def_readwrite("K", &WideCfg::K)
+      .def_readwrite("KP", &WideCfg::KP)
+      .def_readwrite("F", &WideCfg::F)
+      .def_readwrite("cap", &WideCfg::cap)
+      .def_readwrite("NZ", &WideCfg::NZ)
+      .def_readwrite("standardize", &WideCfg::standardize)
+      .def_readwrite("center", &WideCfg::center)
+      .def_readwrite("zero_const", &WideCfg::zero_const)
+      .def_readwrite("dense_delta", &WideCfg::dense_delta);
+
+  py::class_<WideSolver>(m, "WideSolver")
+      .def(py::init([](const WideCfg& cfg, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz, uintptr_t ry,
+                       uintptr_t w_old, uintptr_t dloc, uintptr_t wloc, uintptr_t loss, uintptr_t stats,
+                       uintptr_t uniq, uintptr_t delta_dense, bool use_graph) {
+             WideBuffers b;
+             b.uniq = P<int32_t>(uniq);
+             b.ridx = P<const int32_t>(ridx);
+             b.rval = P<const uint16_t>(rval);
+             b.rnnz = P<const int32_t>(rnnz);
+             b.ry = P<const int32_t>(ry);
+             b.w_old = P<const float>(w_old);
+             b.dloc = P<float>(dloc);
+             b.wloc = P<float>(wloc);
+             b.loss = P<float>(loss);
+             b.stats = P<int>(stats);
+             b.delta_dense = P<float>(delta_dense);
+             return std::make_unique<WideSolver>(cfg, b, use_graph);
+           }),
+           py::arg("cfg"), py::arg("ridx"), py::arg("rval"), py::arg("rnnz"), py::arg("ry"), py::arg("w_old"),
+           py::arg("dloc"), py::arg("wloc"), py::arg("loss"), py::arg("stats"), py::arg("uniq"), py::arg("delta_dense") = 0,
+           py::arg("use_graph") = true)
+      .def("run", [](WideSolver& s, int B, int start, uintptr_t stream) { s.run(B, start, S(stream)); })
+      .def("read_ctrl",
+           [](WideSolver& s, uintptr_t stream) {
+             Ctrl c;
+             s.read_ctrl(&c, S(stream));
+             return ctrl_dict(c, s.cfg().sc.hist);
+           })
+      .def_property_readonly("plmax", &WideSolver::plmax)
+      .def_property_readonly("umax", [](const WideSolver& s) { return s.cfg().umax; })
+      .def_property_readonly("map_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.map()); })
+      .def_property_readonly("uniq_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.uniq()); })
+      .def_property_readonly("ucount_ptr",
+                             [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.ucount_dev()); })
+      .def_property_readonly("ucount_host", &WideSolver::ucount_host)
+      .def_property_readonly("workspace_bytes", &WideSolver::workspace_bytes)
+      .def_property_readonly("kernels_per_solve", &WideSolver::kernels_per_solve);
+
+  m.def("sparse_ring_ingest", [](uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int64_t src_first,
+                                 int64_t src_step, int64_t n, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz,
+                                 uintptr_t ry, int64_t dst_first, int cap, int NZ, uintptr_t trunc, uintptr_t stream) {
+    launch_sparse_ring_ingest(P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val),
+                              P<const int32_t>(y), src_first, src_step, n, P<int32_t>(ridx), P<uint16_t>(rval),
+                              P<int32_t>(rnnz), P<int32_t>(ry), dst_first, cap, NZ, P<int>(trunc), S(stream));
+    hip_check(hipGetLastError(), "sparse_ring_ingest launch");
+  });
+  m.def(
+      "wide_eval",
+      [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int T, uintptr_t w,
+         uintptr_t map, uintptr_t wloc, uintptr_t acc, uintptr_t ticket, uintptr_t slot, uintptr_t loss,
+         unsigned long long seq, uintptr_t stream) {
+        launch_wide_eval(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val),
+                         P<const int32_t>(y), T, P<const float>(w), P<const int32_t>(map), P<const float>(wloc),
+                         P<int>(acc), P<unsigned>(ticket), P<void>(slot), P<const float>(loss), seq, S(stream));
+        hip_check(hipGetLastError(), "wide_eval launch");
+      },
+      py::arg("K"), py::arg("KP"), py::arg("F"), py::arg("indptr"), py::arg("idx"), py::arg("val"), py::arg("y"),
+      py::arg("T"), py::arg("w"), py::arg("map"), py::arg("wloc"), py::arg("acc"), py::arg("ticket") = 0,
+      py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0, py::arg("stream") = 0);
+  m.def("wide_logits", [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, int T,
+                          uintptr_t w, uintptr_t out, uintptr_t stream) {
+    launch_wide_logits(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val), T,
+                       P<const float>(w), P<float>(out), S(stream));
+    hip_check(hipGetLastError(), "wide_logits launch");
+  });
+  m.def("wide_apply_sparse", [](uintptr_t w, int64_t F, int KP, uintptr_t U_dev, int U_host, uintptr_t uniq,
+                                uintptr_t dloc, float lr, int umax, uintptr_t stream) {
+    launch_wide_apply_sparse(P<float>(w), F, KP, P<const unsigned>(U_dev), U_host, P<const int32_t>(uniq),
+                             P<const float>(dloc), lr, umax, S(stream));
+    hip_check(hipGetLastError(), "wide_apply_sparse launch");
+  });
+  m.def("axpy", [](uintptr_t w, uintptr_t x, float a, int64_t n, uintptr_t stream) {
+    launch_axpy(P<float>(w), P<const float>(x), a, n, S(stream));
+    hip_check(hipGetLastError(), "axpy launch");
+  });
+
   m.def("ring_ingest", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
                           uintptr_t ring, uintptr_t ringT, uintptr_t yring, int64_t dst_first, int64_t cap, int FP,
                           uintptr_t stream) {

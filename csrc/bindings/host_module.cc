@@ -6,6 +6,7 @@
 
 #include "../host/ctrl.h"
 #include "../host/dataset.h"
+#include "../host/libsvm.h"
 #include "../host/logger.h"
 #include "../host/metrics_sink.h"
 #include "../host/sampling.h"
@@ -104,6 +105,36 @@ PYBIND11_MODULE(_psx_host, m) {
     return py::make_tuple(c, times);
   });
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def(
+      "libsvm_load",
+      [](const std::string& path, bool zero_based, int threads) {
+        SparseRows r;
+        {
+          py::gil_scoped_release rel;
+          r = libsvm_load(path, zero_based, threads);
+        }
+        auto mk = [](auto& v) {
+          using T = typename std::decay_t<decltype(v)>::value_type;
+          py::array_t<T> a(static_cast<py::ssize_t>(v.size()));
+          if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+          return a;
+        };
+        return py::make_tuple(mk(r.indptr), mk(r.idx), mk(r.val), mk(r.y), r.max_feature);
+      },
+      py::arg("path"), py::arg("zero_based") = false, py::arg("threads") = 0);
+  m.def(
+      "libsvm_save",
+      [](const std::string& path, py::array_t<int64_t, py::array::c_style | py::array::forcecast> indptr,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> idx,
+         py::array_t<uint16_t, py::array::c_style | py::array::forcecast> val,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> y, bool zero_based) {
+        const int64_t rows = static_cast<int64_t>(y.size());
+        if (indptr.size() != rows + 1) throw std::invalid_argument("indptr must have rows + 1 entries");
+        if (idx.size() != val.size() || (rows > 0 && indptr.data()[rows] != idx.size()))
+          throw std::invalid_argument("idx / val / indptr sizes disagree");
+        libsvm_save(path, indptr.data(), idx.data(), val.data(), y.data(), rows, zero_based);
+      },
+      py::arg("path"), py::arg("indptr"), py::arg("idx"), py::arg("val"), py::arg("y"), py::arg("zero_based") = false);
 
   py::class_<CtrlToken>(m, "CtrlToken")
       .def(py::init<>())

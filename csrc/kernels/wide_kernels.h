@@ -1,0 +1,125 @@
+// Wide / sparse logistic regression on gfx950: CSR feature rows, a dense
+// weight vector of F*KP + KP floats (F up to ~10^8 hashed features).
+//
+// BASELINE.json configs 4 (10M rows x 1M sparse features, ASP) and 5 (sharded
+// 100M-dim dense weight vector).  The reference has no sparse path: its worker
+// densifies 1024 hashed features into Spark rows
+// (LogisticRegressionTaskSpark.java:146-162) and the server loops over a boxed
+// HashMap (ServerProcessor.java:148-151).  The MI355X design:
+//
+//  * the window of a worker touches only U << F features, so the local solve
+//    runs in that U-dimensional subspace: a remap pass gives every distinct
+//    feature of the window a compact local id (wave-aggregated atomics), the
+//    old weights of those features are gathered once, and every L-BFGS vector
+//    (x, d, g, S_i, Y_i) is KP + U*KP floats instead of F*KP;
+//  * one wavefront per row: lanes gather the row's non-zeros, the K margins are
+//    reduced across the wave, softmax / cross-entropy in registers, and the
+//    same wave scatters the row's gradient with global float atomics
+//    (forward and backward fused, no residual round trip);
+//  * the line-search / L-BFGS control is the same on-device state machine as
+//    the dense solver (solver_ctrl.h), advanced by the last workgroup of the
+//    dot-product reduction; the whole solve is one hipGraph replay;
+//  * the output is sparse (U ids + U*KP deltas) with an optional dense scatter
+//    for the collective schedules.
+//
+// Device layouts:
+//   dense weights / deltas : [F][KP] coefficient (f, c) at f*KP + c, then KP
+//                            intercepts at F*KP + c (classes c >= K stay 0)
+//   local vectors          : KP intercepts first, then feature l at KP + l*KP
+//   ring (ELL)             : idx [cap][NZ] int32, val [cap][NZ] bf16,
+//                            nnz [cap] int32, y [cap] int32
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "solver_ctrl.h"
+
+namespace psx {
+
+struct WideCfg {
+  SolverCfg sc;       // iters / hist / ls_max / mode / nslots / gd_lr / tol (K F Fp P cap unused)
+  int K;              // logits (1 = binary sigmoid model, >= 2 softmax incl. phantom class)
+  int KP;             // padded classes: 1, 2, 4, 8 or 16
+  int64_t F;          // features
+  int cap;            // ring rows
+  int NZ;             // ring entries per row (<= 512)
+  int umax;           // max distinct features of a window = min(F, cap*NZ)
+  int standardize;    // Spark's feature scaling by 1/std over the window
+  int center;         // multinomial centring (Spark, regParam == 0)
+  int zero_const;     // zero-std features get coefficient 0 (Spark) instead of keeping w_old
+  int dense_delta;    // also scatter the delta into a dense [F*KP + KP] vector
+};
+
+struct WideParams {
+  int B, start, pad0, pad1;
+};
+
+// Everything the solve kernels touch (device pointers; passed by value).
+struct WideDev {
+  // ring (caller-owned)
+  const int32_t* ridx;
+  const uint16_t* rval;
+  const int32_t* rnnz;
+  const int32_t* ry;
+  const float* w_old;  // dense pulled weights [F*KP + KP]
+  // workspace
+  WideParams* prm;
+  Ctrl* ctrl;
+  unsigned* cnt;       // [0] U, [1] dots ticket, [2] U of the previous solve, [3] unused
+  int32_t* map;        // [F] local id or -1 (-2 transiently)
+  int32_t* uniq;       // [umax] local id -> feature
+  int32_t* lid;        // [cap*NZ] window entry -> local id (-1 = padding)
+  float* s1;           // [umax] feature sums over the window
+  float* s2;           // [umax] feature sums of squares
+  float* scale;        // [umax] effective coefficient = scale * x
+  float* gscale;       // [umax] gradient scale (0 for frozen features)
+  float *x, *d, *g_t, *g_c, *w0;  // [PLmax]
+  float *S, *Y;        // [hist][PLmax]
+  double* part;        // [nblk][kWideND] dot partials
+  double* loss_acc;    // [nslots]
+  // outputs (caller-owned)
+  float* dloc;         // [PLmax] local delta (intercepts first)
+  float* wloc;         // [PLmax] local new weights
+  int32_t* uniq_out;   // == uniq (exported)
+  float* loss;         // [1]
+  int* stats;          // [4] evals, accepted steps, ls failures, direction resets
+  float* delta_dense;  // [F*KP + KP] (dense_delta)
+  unsigned* host_u;    // pinned host mirror of U (optional)
+  int64_t PLmax;
+};
+
+constexpr int kWideND = 3 + 2 * kMaxHist;
+
+// Launchers (stream order; the solver captures them into one hipGraph).
+void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s);  // cleanup + params
+void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s);  // remap, assign, stats, prep
+void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dots, hipStream_t s);
+void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s);
+int wide_dots_blocks(int64_t PLmax);
+
+// Ring ingest: rows src_first + i*src_step of a CSR matrix (i < n) -> ring
+// slots (dst_first + i) % cap; rows longer than NZ are truncated and counted
+// in *trunc.
+void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y,
+                               int64_t src_first, int64_t src_step, int64_t n, int32_t* ridx, uint16_t* rval,
+                               int32_t* rnnz, int32_t* ry, int64_t dst_first, int cap, int NZ, int* trunc,
+                               hipStream_t s);
+
+// Test-set evaluation of a dense wide model (optionally overlaid with a
+// worker's local solution: features with map[f] >= 0 read wloc).  Same
+// EvalSlot protocol as launch_test_eval.
+void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                      const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
+                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s);
+// Margins of T rows (tests): out[T][KP].
+void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                        int T, const float* w, float* out, hipStream_t s);
+
+// Server updates.  Sparse: w[uniq[l]*KP + c] += lr * dloc[KP + l*KP + c] for
+// l < *U (device count) or U_host when U_dev is null, and the intercepts.
+void launch_wide_apply_sparse(float* w, int64_t F, int KP, const unsigned* U_dev, int U_host, const int32_t* uniq,
+                              const float* dloc, float lr, int umax, hipStream_t s);
+// Dense: w += lr * delta over n floats.
+void launch_axpy(float* w, const float* delta, float lr, int64_t n, hipStream_t s);
+
+}  // namespace psx

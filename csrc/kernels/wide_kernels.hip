@@ -1,0 +1,743 @@
+// Wide / sparse logistic-regression kernels (gfx950 / CDNA4).  See
+// wide_kernels.h for the design and layouts.
+//
+// Reference math being replaced: the worker's Spark fit on its buffer
+// (LogisticRegressionTaskSpark.java:142-221), test-set metrics
+// (LogisticRegressionTaskSpark.java:236-251, Metrics.java:15-24) and the
+// server's per-key update loop (ServerProcessor.java:148-151, 225-228).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "wide_kernels.h"
+
+namespace psx {
+
+namespace {
+
+typedef __attribute__((address_space(1))) unsigned long long gu64w;
+
+__device__ __forceinline__ double ld_agent_f64(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((gu64w*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int KP>
+__device__ __forceinline__ void ldk(const float* __restrict__ p, float (&o)[KP]) {
+  if constexpr (KP % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < KP / 4; ++q) {
+      const f32x4 t = *(const f32x4*)(p + 4 * q);
+      o[4 * q] = t[0];
+      o[4 * q + 1] = t[1];
+      o[4 * q + 2] = t[2];
+      o[4 * q + 3] = t[3];
+    }
+  } else if constexpr (KP == 2) {
+    const float2 t = *(const float2*)p;
+    o[0] = t.x;
+    o[1] = t.y;
+  } else {
+    o[0] = p[0];
+  }
+}
+
+// Class probabilities -> residual r = (p - onehot(y)) * invB and the row loss.
+// K == 1: binary sigmoid model (label y in {0,1}).
+template <int KP>
+__device__ __forceinline__ float row_residual(const float (&z)[KP], int K, int y, float invB, float (&r)[KP]) {
+  if (K == 1) {
+    const float zz = z[0];
+    const float yy = y > 0 ? 1.f : 0.f;
+    const float p = 1.f / (1.f + __expf(-zz));
+    r[0] = (p - yy) * invB;
+#pragma unroll
+    for (int c = 1; c < KP; ++c) r[c] = 0.f;
+    // softplus(z) - y z, stable for both signs
+    return fmaxf(zz, 0.f) + log1pf(__expf(-fabsf(zz))) - yy * zz;
+  }
+  const int yc = y < 0 ? 0 : (y >= K ? K - 1 : y);
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < KP; ++c)
+    if (c < K) m = fmaxf(m, z[c]);
+  float e[KP];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < KP; ++c) {
+    e[c] = c < K ? __expf(z[c] - m) : 0.f;
+    s += e[c];
+  }
+  const float is = 1.f / s;
+  float zy = 0.f;
+#pragma unroll
+  for (int c = 0; c < KP; ++c) {
+    r[c] = c < K ? (e[c] * is - (c == yc ? 1.f : 0.f)) * invB : 0.f;
+    if (c == yc) zy = z[c];
+  }
+  return __logf(s) + m - zy;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// begin: reset the previous solve's feature map entries, publish the window.
+__global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int start) {
+  const unsigned prevU = d.cnt[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.prm->B = B;
+    d.prm->start = start;
+    d.cnt[0] = 0u;  // not read by anybody else in this kernel
+    d.cnt[1] = 0u;
+  }
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256) d.map[d.uniq[i]] = -1;
+}
+
+// remap: every distinct feature of the window gets a compact id.  The first
+// entry to CAS map[f] from -1 wins; winners of a wave take consecutive ids
+// with ONE atomic per wave (ballot + popcount).
+__global__ __launch_bounds__(256) void wide_remap_kernel(WideDev d, int cap, int NZ) {
+  const int B = d.prm->B, start = d.prm->start;
+  const int64_t E = (int64_t)B * NZ;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int lane = __lane_id();
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += stride) {
+    const int64_t e = base + threadIdx.x;
+    bool win = false;
+    int f = 0;
+    if (e < E) {
+      const int r = (int)(e / NZ), j = (int)(e - (int64_t)r * NZ);
+      int sl = start + r;
+      if (sl >= cap) sl -= cap;
+      if (j < d.rnnz[sl]) {
+        f = d.ridx[(size_t)sl * NZ + j];
+        win = atomicCAS(&d.map[f], -1, -2) == -1;
+      }
+    }
+    const unsigned long long mask = __ballot(win);
+    if (mask) {
+      const int leader = __ffsll((long long)mask) - 1;
+      unsigned b0 = 0;
+      if (lane == leader) b0 = atomicAdd(&d.cnt[0], (unsigned)__popcll(mask));
+      b0 = __shfl(b0, leader, 64);
+      if (win) d.uniq[b0 + __popcll(mask & ((1ull << lane) - 1ull))] = f;
+    }
+  }
+}
+
+// assign: map[f] = id, gather the old weights of the window's features.
+__global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) {
+  const unsigned U = d.cnt[0];
+  const int KP = c.KP;
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+    const int f = d.uniq[i];
+    d.map[f] = (int)i;
+    const float* src = d.w_old + (int64_t)f * KP;
+    float* dst = d.w0 + KP + (int64_t)i * KP;
+    for (int k = 0; k < KP; ++k) dst[k] = src[k];
+    d.s1[i] = 0.f;
+    d.s2[i] = 0.f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < KP) d.w0[threadIdx.x] = d.w_old[c.F * KP + threadIdx.x];
+}
+
+// lid: local id of every window entry (+ feature sums for the 1/std scaling).
+__global__ __launch_bounds__(256) void wide_lid_kernel(WideCfg c, WideDev d) {
+  const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap;
+  const int64_t E = (int64_t)B * NZ;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < E; e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / NZ), j = (int)(e - (int64_t)r * NZ);
+    int sl = start + r;
+    if (sl >= cap) sl -= cap;
+    if (j >= d.rnnz[sl]) continue;
+    const int l = d.map[d.ridx[(size_t)sl * NZ + j]];
+    d.lid[e] = l;
+    if (c.standardize) {
+      const float v = bf2f(d.rval[(size_t)sl * NZ + j]);
+      atomicAdd(&d.s1[l], v);
+      atomicAdd(&d.s2[l], v * v);
+    }
+  }
+}
+
+// prep: per-feature scaling, starting point x, zeroed direction / gradients,
+// controller init.
+__global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
+  const unsigned U = d.cnt[0];
+  const int KP = c.KP, K = c.K;
+  const int B = d.prm->B;
+  const int64_t PL = KP + (int64_t)U * KP;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+  for (int64_t i = gid; i < U; i += gs) {
+    float sc = 1.f, gsc = 1.f, xs = 1.f;
+    if (c.standardize) {
+      const double n = (double)B;
+      double sd = 0.0;
+      if (n > 1.0) {
+        const double mean = (double)d.s1[i] / n;
+        const double var = ((double)d.s2[i] - n * mean * mean) / (n - 1.0);
+        sd = var > 0.0 ? sqrt(var) : 0.0;
+      }
+      if (sd > 0.0) {
+        sc = gsc = (float)(1.0 / sd);
+        xs = (float)sd;
+      } else {
+        gsc = 0.f;
+        sc = xs = c.zero_const ? 0.f : 1.f;
+      }
+    }
+    d.scale[i] = sc;
+    d.gscale[i] = gsc;
+    for (int k = 0; k < KP; ++k) {
+      const int64_t p = KP + i * KP + k;
+      d.x[p] = k < K ? d.w0[p] * xs : 0.f;
+    }
+  }
+  for (int64_t p = gid; p < PL; p += gs) {
+    d.d[p] = 0.f;
+    d.g_t[p] = 0.f;
+    d.g_c[p] = 0.f;
+    if (p < KP) d.x[p] = p < K ? d.w0[p] : 0.f;
+  }
+  if (gid == 0) {
+    ctrl_init(*d.ctrl);
+    d.ctrl->t = 0.0;
+    for (int s = 0; s < c.sc.nslots; ++s) d.loss_acc[s] = 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One function evaluation at x + t d: margins, softmax/CE, gradient scatter.
+// One wavefront per window row; 4 rows per workgroup pass.
+template <int KP, int NQ>
+__global__ __launch_bounds__(256) void wide_fwdbwd_kernel(WideCfg c, WideDev d, int slot) {
+  const Ctrl* ctrl = d.ctrl;
+  if (ctrl->phase == kPhDone) return;
+  const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap, K = c.K;
+  const float t = (float)ctrl->t;
+  const float invB = 1.f / (float)B;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ float red_r[4][KP];
+  __shared__ double red_l[4];
+  float racc[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) racc[k] = 0.f;
+  double lacc = 0.0;
+  const float* __restrict__ X = d.x;
+  const float* __restrict__ D = d.d;
+  for (int r = blockIdx.x * 4 + wv; r < B; r += gridDim.x * 4) {
+    int sl = start + r;
+    if (sl >= cap) sl -= cap;
+    const int nnz = d.rnnz[sl];
+    const int32_t* __restrict__ ids = d.lid + (int64_t)r * NZ;
+    const uint16_t* __restrict__ vals = d.rval + (int64_t)sl * NZ;
+    float z[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) z[k] = 0.f;
+    int lq[NQ];
+    float vq[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int j = lane + 64 * q;
+      lq[q] = -1;
+      vq[q] = 0.f;
+      if (j < nnz) {
+        const int l = ids[j];
+        const float v = bf2f(vals[j]);
+        lq[q] = l;
+        vq[q] = v;
+        const float sv = v * d.scale[l];
+        float xv[KP], dv[KP];
+        ldk<KP>(X + KP + (int64_t)l * KP, xv);
+        ldk<KP>(D + KP + (int64_t)l * KP, dv);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) z[k] += sv * (xv[k] + t * dv[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) z[k] = wave_sum(z[k]);
+    {
+      float xb[KP], db[KP];
+      ldk<KP>(X, xb);
+      ldk<KP>(D, db);
+#pragma unroll
+      for (int k = 0; k < KP; ++k) z[k] += xb[k] + t * db[k];
+    }
+    float rr[KP];
+    const float lrow = row_residual<KP>(z, K, d.ry[sl], invB, rr);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (lq[q] < 0) continue;
+      const float g = vq[q] * d.gscale[lq[q]];
+      if (g == 0.f) continue;
+      float* gp = d.g_t + KP + (int64_t)lq[q] * KP;
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (k < K) atomicAdd(gp + k, g * rr[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) racc[k] += rr[k];
+    lacc += (double)lrow;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) red_r[wv][k] = racc[k];
+    red_l[wv] = lacc;
+  }
+  __syncthreads();
+  if (threadIdx.x < KP && threadIdx.x < K) {
+    const float s = red_r[0][threadIdx.x] + red_r[1][threadIdx.x] + red_r[2][threadIdx.x] + red_r[3][threadIdx.x];
+    if (s != 0.f) atomicAdd(d.g_t + threadIdx.x, s);
+  }
+  if (threadIdx.x == 0) {
+    const double s = red_l[0] + red_l[1] + red_l[2] + red_l[3];
+    if (s != 0.0) atomicAdd(d.loss_acc + slot, s);
+  }
+}
+
+// Dot products of the new gradient (ctrl dots layout, solver_ctrl.h) + the
+// controller step in the last-arriving workgroup.
+__global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, int slot) {
+  Ctrl* ctrl = d.ctrl;
+  if (ctrl->phase == kPhDone) return;
+  __shared__ double red[4][kWideND];
+  __shared__ double dots[kWideND];
+  __shared__ int last;
+  __shared__ CtrlScratch ws;
+  const int H = c.sc.hist;
+  const int m = ctrl->m;
+  const unsigned U = d.cnt[0];
+  const int64_t PL = c.KP + (int64_t)U * c.KP, PLmax = d.PLmax;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  double aS[kMaxHist], aY[kMaxHist];
+#pragma unroll
+  for (int i = 0; i < kMaxHist; ++i) aS[i] = aY[i] = 0.0;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < PL; p += (int64_t)gridDim.x * 256) {
+    const float g = d.g_t[p];
+    a0 += (double)g * g;
+    a1 += (double)g * d.d[p];
+    a2 += (double)g * d.g_c[p];
+#pragma unroll
+    for (int i = 0; i < kMaxHist; ++i) {
+      if (i < m) {
+        aS[i] += (double)g * d.S[(int64_t)i * PLmax + p];
+        aY[i] += (double)g * d.Y[(int64_t)i * PLmax + p];
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  if (lane == 0) {
+    red[wv][0] = a0;
+    red[wv][1] = a1;
+    red[wv][2] = a2;
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxHist; ++i) {
+    if (i < m) {
+      const double s = wave_sum(aS[i]);
+      const double y = wave_sum(aY[i]);
+      if (lane == 0) {
+        red[wv][3 + i] = s;
+        red[wv][3 + H + i] = y;
+      }
+    }
+  }
+  __syncthreads();
+  const int nd = 3 + 2 * H;
+  if (threadIdx.x < nd) {
+    const int k = threadIdx.x;
+    const bool used = k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m);
+    const double s = used ? red[0][k] + red[1][k] + red[2][k] + red[3][k] : 0.0;
+    d.part[(int64_t)blockIdx.x * kWideND + k] = s;
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&d.cnt[1], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x < nd) {
+    double s = 0.0;
+    for (int b = 0; b < (int)gridDim.x; ++b) s += ld_agent_f64(d.part + (int64_t)b * kWideND + threadIdx.x);
+    dots[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.cnt[1] = 0u;
+    const double f = ld_agent_f64(d.loss_acc + slot) / (double)d.prm->B;
+    ctrl_step(*ctrl, c.sc, f, dots, slot, ws);
+  }
+}
+
+// Apply the controller's decision of `slot` to the local vectors; clears g_t
+// for the next evaluation.
+__global__ __launch_bounds__(256) void wide_apply_kernel(WideCfg c, WideDev d, int slot) {
+  const Ctrl* ctrl = d.ctrl;
+  if (ctrl->action_slot != slot) return;
+  const int act = ctrl->action;
+  if (act == kActDone) return;
+  const unsigned U = d.cnt[0];
+  const int64_t PL = c.KP + (int64_t)U * c.KP, PLmax = d.PLmax;
+  const float ta = (float)ctrl->t_acc;
+  const int ps = ctrl->push_slot;
+  const int m = ctrl->m;
+  const float cg = (float)ctrl->cg;
+  float cs[kMaxHist], cy[kMaxHist];
+#pragma unroll
+  for (int i = 0; i < kMaxHist; ++i) {
+    cs[i] = i < m ? (float)ctrl->cs[i] : 0.f;
+    cy[i] = i < m ? (float)ctrl->cy[i] : 0.f;
+  }
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < PL; p += (int64_t)gridDim.x * 256) {
+    const float gt = d.g_t[p];
+    d.g_t[p] = 0.f;
+    if (act == kActInit) {
+      d.g_c[p] = gt;
+      d.d[p] = -gt;
+    } else if (act == kActAccept || act == kActAcceptDone) {
+      const float dp = d.d[p];
+      d.x[p] += ta * dp;
+      if (act == kActAccept) {
+        if (ps >= 0) {
+          d.S[(int64_t)ps * PLmax + p] = ta * dp;
+          d.Y[(int64_t)ps * PLmax + p] = gt - d.g_c[p];
+        }
+        d.g_c[p] = gt;
+        float nd = cg * gt;
+#pragma unroll
+        for (int i = 0; i < kMaxHist; ++i)
+          if (i < m) nd += cs[i] * d.S[(int64_t)i * PLmax + p] + cy[i] * d.Y[(int64_t)i * PLmax + p];
+        d.d[p] = nd;
+      }
+    }
+  }
+}
+
+// finalize: effective coefficients, centring, local delta (+ dense scatter).
+__global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d) {
+  const unsigned U = d.cnt[0];
+  const int KP = c.KP, K = c.K;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int64_t i = gid; i <= (int64_t)U; i += (int64_t)gridDim.x * 256) {
+    // i < U: feature i ; i == U: the intercepts
+    const bool icpt = i == (int64_t)U;
+    const int64_t p0 = icpt ? 0 : KP + i * KP;
+    const float sc = icpt ? 1.f : d.scale[i];
+    float v[16];
+    float mean = 0.f;
+    for (int k = 0; k < KP; ++k) {
+      v[k] = k < K ? sc * d.x[p0 + k] : 0.f;
+      mean += v[k];
+    }
+    if (c.center && K >= 2) {
+      mean /= (float)K;
+      for (int k = 0; k < K; ++k) v[k] -= mean;
+    }
+    const int64_t dst = icpt ? c.F * KP : (int64_t)d.uniq[i] * KP;
+    for (int k = 0; k < KP; ++k) {
+      const float dl = k < K ? v[k] - d.w0[p0 + k] : 0.f;
+      d.wloc[p0 + k] = k < K ? v[k] : 0.f;
+      d.dloc[p0 + k] = dl;
+      if (c.dense_delta) d.delta_dense[dst + k] = dl;
+    }
+  }
+  if (gid == 0) {
+    const Ctrl* ctrl = d.ctrl;
+    *d.loss = (float)ctrl->f_c;
+    d.stats[0] = ctrl->evals;
+    d.stats[1] = ctrl->nacc;
+    d.stats[2] = ctrl->ls_fail;
+    d.stats[3] = ctrl->dir_reset;
+    d.cnt[2] = U;
+    if (d.host_u) __hip_atomic_store(d.host_u, U, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---------------------------------------------------------------------------
+static int grid_for(int64_t n, int cap_blocks) {
+  int64_t g = (n + 255) / 256;
+  if (g < 1) g = 1;
+  if (g > cap_blocks) g = cap_blocks;
+  return (int)g;
+}
+
+int wide_dots_blocks(int64_t PLmax) { return grid_for(PLmax / 4, 256); }
+
+void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s) {
+  wide_begin_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(d, B, start);
+}
+
+void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s) {
+  const int64_t E = (int64_t)c.cap * c.NZ;
+  wide_remap_kernel<<<grid_for(E, 2048), 256, 0, s>>>(d, c.cap, c.NZ);
+  wide_assign_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(c, d);
+  wide_lid_kernel<<<grid_for(E, 2048), 256, 0, s>>>(c, d);
+  wide_prep_kernel<<<grid_for(d.PLmax, 1024), 256, 0, s>>>(c, d);
+}
+
+template <int KP>
+static void launch_fwdbwd_kp(const WideCfg& c, const WideDev& d, int slot, int grid, hipStream_t s) {
+  const int nq = (c.NZ + 63) / 64;
+  if (nq <= 1)
+    wide_fwdbwd_kernel<KP, 1><<<grid, 256, 0, s>>>(c, d, slot);
+  else if (nq <= 2)
+    wide_fwdbwd_kernel<KP, 2><<<grid, 256, 0, s>>>(c, d, slot);
+  else if (nq <= 4)
+    wide_fwdbwd_kernel<KP, 4><<<grid, 256, 0, s>>>(c, d, slot);
+  else
+    wide_fwdbwd_kernel<KP, 8><<<grid, 256, 0, s>>>(c, d, slot);
+}
+
+void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dots, hipStream_t s) {
+  const int rows_grid = grid_for((int64_t)c.cap * 64, 2048);  // 4 rows per workgroup pass
+  switch (c.KP) {
+    case 1: launch_fwdbwd_kp<1>(c, d, slot, rows_grid, s); break;
+    case 2: launch_fwdbwd_kp<2>(c, d, slot, rows_grid, s); break;
+    case 4: launch_fwdbwd_kp<4>(c, d, slot, rows_grid, s); break;
+    case 8: launch_fwdbwd_kp<8>(c, d, slot, rows_grid, s); break;
+    default: launch_fwdbwd_kp<16>(c, d, slot, rows_grid, s); break;
+  }
+  wide_dots_kernel<<<nblk_dots, 256, 0, s>>>(c, d, slot);
+  wide_apply_kernel<<<grid_for(d.PLmax, 1024), 256, 0, s>>>(c, d, slot);
+}
+
+void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s) {
+  wide_finalize_kernel<<<grid_for((int64_t)c.umax + 1, 1024), 256, 0, s>>>(c, d);
+}
+
+const void* wide_begin_symbol() { return (const void*)wide_begin_kernel; }
+
+// ---------------------------------------------------------------------------
+// Ring ingest: one wavefront per row.
+__global__ __launch_bounds__(256) void sparse_ring_ingest_kernel(const int64_t* __restrict__ indptr,
+                                                                 const int32_t* __restrict__ idx,
+                                                                 const uint16_t* __restrict__ val,
+                                                                 const int32_t* __restrict__ y, int64_t src_first,
+                                                                 int64_t src_step, int64_t n, int32_t* ridx,
+                                                                 uint16_t* rval, int32_t* rnnz, int32_t* ry,
+                                                                 int64_t dst_first, int cap, int NZ, int* trunc) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += (int64_t)gridDim.x * 4) {
+    const int64_t sr = src_first + i * src_step;
+    const int64_t dr = (dst_first + i) % cap;
+    const int64_t a = indptr[sr], b = indptr[sr + 1];
+    const int64_t len = b - a;
+    const int nz = len < NZ ? (int)len : NZ;
+    for (int j = lane; j < nz; j += 64) {
+      ridx[dr * NZ + j] = idx[a + j];
+      rval[dr * NZ + j] = val[a + j];
+    }
+    if (lane == 0) {
+      rnnz[dr] = nz;
+      ry[dr] = y[sr];
+      if (len > NZ && trunc) atomicAdd(trunc, 1);
+    }
+  }
+}
+
+void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y,
+                               int64_t src_first, int64_t src_step, int64_t n, int32_t* ridx, uint16_t* rval,
+                               int32_t* rnnz, int32_t* ry, int64_t dst_first, int cap, int NZ, int* trunc,
+                               hipStream_t s) {
+  if (n <= 0) return;
+  sparse_ring_ingest_kernel<<<grid_for(n * 64, 2048), 256, 0, s>>>(indptr, idx, val, y, src_first, src_step, n, ridx,
+                                                                   rval, rnnz, ry, dst_first, cap, NZ, trunc);
+}
+
+// ---------------------------------------------------------------------------
+// Test-set evaluation: one wavefront per row, LDS confusion counts, last
+// workgroup publishes into the pinned EvalSlot (protocol of test_eval_kernel).
+template <int KP>
+__device__ __forceinline__ void wide_row_margins(int64_t F, const int64_t* __restrict__ indptr,
+                                                 const int32_t* __restrict__ idx, const uint16_t* __restrict__ val,
+                                                 int64_t row, const float* __restrict__ w,
+                                                 const int32_t* __restrict__ map, const float* __restrict__ wloc,
+                                                 float (&z)[KP]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z[k] = 0.f;
+  const int64_t a = indptr[row], b = indptr[row + 1];
+  for (int64_t e = a + lane; e < b; e += 64) {
+    const int f = idx[e];
+    const float v = bf2f(val[e]);
+    const float* src = w + (int64_t)f * KP;
+    if (map) {
+      const int l = map[f];
+      if (l >= 0) src = wloc + KP + (int64_t)l * KP;
+    }
+    float wv[KP];
+    ldk<KP>(src, wv);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) z[k] += v * wv[k];
+  }
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z[k] = wave_sum(z[k]);
+  float bv[KP];
+  ldk<KP>(map ? wloc : w + F * KP, bv);
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z[k] += bv[k];
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const int64_t* __restrict__ indptr,
+                                                        const int32_t* __restrict__ idx,
+                                                        const uint16_t* __restrict__ val,
+                                                        const int32_t* __restrict__ y, int T,
+                                                        const float* __restrict__ w, const int32_t* __restrict__ map,
+                                                        const float* __restrict__ wloc, int* acc, unsigned* ticket,
+                                                        char* slot, const float* loss, unsigned long long seq) {
+  __shared__ int cl[256];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  cl[tid] = 0;
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (tid >> 6); r < T; r += (int64_t)gridDim.x * 4) {
+    float z[KP];
+    wide_row_margins<KP>(F, indptr, idx, val, r, w, map, wloc, z);
+    if (lane == 0) {
+      int best = 0;
+      if (K == 1) {
+        best = z[0] > 0.f ? 1 : 0;
+      } else {
+        float bz = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+          if (k < K && z[k] > bz) {
+            bz = z[k];
+            best = k;
+          }
+      }
+      int yl = y[r];
+      if (K == 1) yl = yl > 0 ? 1 : 0;
+      yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
+      atomicAdd(&cl[yl * 16 + best], 1);
+    }
+  }
+  __syncthreads();
+  const int v = cl[tid];
+  if (v) atomicAdd(acc + tid, v);
+  if (slot == nullptr) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ((int*)slot)[tid] = tot;
+  if (tid == 0) *(float*)(slot + 1024) = loss ? *loss : 0.f;
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void wide_logits_kernel(int64_t F, const int64_t* __restrict__ indptr,
+                                                          const int32_t* __restrict__ idx,
+                                                          const uint16_t* __restrict__ val, int T,
+                                                          const float* __restrict__ w, float* out) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < T; r += (int64_t)gridDim.x * 4) {
+    float z[KP];
+    wide_row_margins<KP>(F, indptr, idx, val, r, w, nullptr, nullptr, z);
+    if (lane < KP) {
+      float o = 0.f;
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (k == lane) o = z[k];
+      out[r * KP + lane] = o;
+    }
+  }
+}
+
+void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                      const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
+                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s) {
+  if (T <= 0) return;
+  const int grid = grid_for((int64_t)T * 64, 1024);
+  char* sl = static_cast<char*>(slot);
+#define PSX_WE(KV)                                                                                              \
+  case KV:                                                                                                      \
+    wide_eval_kernel<KV><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc, ticket, sl, loss, \
+                                              seq);                                                             \
+    break;
+  switch (KP) {
+    PSX_WE(1)
+    PSX_WE(2)
+    PSX_WE(4)
+    PSX_WE(8)
+    PSX_WE(16)
+    default:
+      break;
+  }
+#undef PSX_WE
+}
+
+void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                        int T, const float* w, float* out, hipStream_t s) {
+  (void)K;
+  if (T <= 0) return;
+  const int grid = grid_for((int64_t)T * 64, 1024);
+#define PSX_WL(KV)                                                                      \
+  case KV:                                                                              \
+    wide_logits_kernel<KV><<<grid, 256, 0, s>>>(F, indptr, idx, val, T, w, out); \
+    break;
+  switch (KP) {
+    PSX_WL(1)
+    PSX_WL(2)
+    PSX_WL(4)
+    PSX_WL(8)
+    PSX_WL(16)
+    default:
+      break;
+  }
+#undef PSX_WL
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wide_apply_sparse_kernel(float* w, int64_t F, int KP, const unsigned* Ud,
+                                                                int Uh, const int32_t* __restrict__ uniq,
+                                                                const float* __restrict__ dloc, float lr) {
+  const int64_t U = Ud ? (int64_t)*Ud : (int64_t)Uh;
+  const int64_t n = KP + U * KP;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
+    const float v = dloc[p];
+    if (v == 0.f) continue;
+    if (p < KP) {
+      w[F * KP + p] += lr * v;
+    } else {
+      const int64_t l = (p - KP) / KP, k = (p - KP) - l * KP;
+      w[(int64_t)uniq[l] * KP + k] += lr * v;
+    }
+  }
+}
+
+void launch_wide_apply_sparse(float* w, int64_t F, int KP, const unsigned* U_dev, int U_host, const int32_t* uniq,
+                              const float* dloc, float lr, int umax, hipStream_t s) {
+  const int64_t n = KP + (int64_t)(U_dev ? umax : U_host) * KP;
+  wide_apply_sparse_kernel<<<grid_for(n, 2048), 256, 0, s>>>(w, F, KP, U_dev, U_host, uniq, dloc, lr);
+}
+
+__global__ __launch_bounds__(256) void axpy_kernel(float* __restrict__ w, const float* __restrict__ x, float a,
+                                                   int64_t n) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    f32x4 v = ((f32x4*)w)[i];
+    const f32x4 d = ((const f32x4*)x)[i];
+    v += a * d;
+    ((f32x4*)w)[i] = v;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) w[i] += a * x[i];
+}
+
+void launch_axpy(float* w, const float* delta, float lr, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  axpy_kernel<<<grid_for(n / 4 + 1, 4096), 256, 0, s>>>(w, delta, lr, n);
+}
+
+}  // namespace psx

@@ -1,0 +1,74 @@
+// Native driver of one worker's local solve on the wide / sparse model.
+//
+// Same role as LocalSolver (solver.h) for rows that are sparse and models too
+// wide for the dense MFMA tiles (BASELINE.json configs 4 and 5):
+//   begin -> remap -> assign -> lid/stats -> prep -> (fwdbwd, dots+ctrl, apply) x nslots
+//         -> [memset dense delta] -> finalize
+// is captured once into a hipGraph; per run only the first node's kernel
+// arguments (the window) change.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../kernels/wide_kernels.h"
+
+namespace psx {
+
+struct WideBuffers {
+  const int32_t* ridx = nullptr;  // ring [cap][NZ]
+  const uint16_t* rval = nullptr; // ring [cap][NZ] bf16
+  const int32_t* rnnz = nullptr;  // [cap]
+  const int32_t* ry = nullptr;    // [cap]
+  const float* w_old = nullptr;   // [F*KP + KP]
+  float* dloc = nullptr;          // [PLmax] out
+  float* wloc = nullptr;          // [PLmax] out
+  float* loss = nullptr;          // [1] out
+  int* stats = nullptr;           // [4] out
+  float* delta_dense = nullptr;   // [F*KP + KP] out (cfg.dense_delta)
+  int32_t* uniq = nullptr;        // [min(F, cap*NZ)] out: local id -> feature
+};
+
+class WideSolver {
+ public:
+  WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_graph);
+  ~WideSolver();
+  WideSolver(const WideSolver&) = delete;
+  WideSolver& operator=(const WideSolver&) = delete;
+
+  void run(int B, int start, hipStream_t stream);
+  const WideCfg& cfg() const { return cfg_; }
+  int64_t plmax() const { return dv_.PLmax; }
+  // Device arrays valid after a run (until the next run's first kernel):
+  const int32_t* map() const { return dv_.map; }
+  const int32_t* uniq() const { return dv_.uniq; }
+  const unsigned* ucount_dev() const { return dv_.cnt; }
+  // U of the last finished run (pinned host mirror; valid after the stream synced).
+  unsigned ucount_host() const { return host_u_ ? __atomic_load_n(host_u_, __ATOMIC_ACQUIRE) : 0u; }
+  void read_ctrl(Ctrl* out, hipStream_t stream);
+  size_t workspace_bytes() const { return ws_bytes_; }
+  int kernels_per_solve() const { return 5 + 3 * cfg_.sc.nslots + 1; }
+
+ private:
+  void enqueue_body(hipStream_t s, int B, int start);
+  WideCfg cfg_;
+  WideDev dv_{};
+  bool use_graph_;
+  int nblk_dots_ = 1;
+  void* ws_ = nullptr;
+  size_t ws_bytes_ = 0;
+  unsigned* host_u_ = nullptr;
+  hipGraphNode_t begin_node_ = nullptr;
+  struct BeginArgs {
+    WideDev d;
+    int B, start;
+  } begin_args_{};
+  void* begin_kp_[3] = {};
+  hipKernelNodeParams begin_params_{};
+  hipStream_t cap_stream_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+const void* wide_begin_symbol();
+
+}  // namespace psx

@@ -1,0 +1,152 @@
+#include "wide_solver.h"
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "solver.h"  // hip_check
+
+namespace psx {
+
+static size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_graph) : cfg_(cfg), use_graph_(use_graph) {
+  const int KP = cfg.KP;
+  if (!(KP == 1 || KP == 2 || KP == 4 || KP == 8 || KP == 16)) throw std::invalid_argument("KP must be 1/2/4/8/16");
+  if (cfg.K < 1 || cfg.K > KP) throw std::invalid_argument("K must be in [1, KP]");
+  if (cfg.F < 1 || cfg.F > (int64_t)0x7fffffff) throw std::invalid_argument("F out of range");
+  if (cfg.cap < 1 || cfg.NZ < 1 || cfg.NZ > 512) throw std::invalid_argument("ring must have cap >= 1 and 1 <= NZ <= 512");
+  if (cfg.sc.hist < 1 || cfg.sc.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
+  if (cfg.sc.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
+  if (cfg.dense_delta && !buf.delta_dense) throw std::invalid_argument("dense_delta needs a dense output buffer");
+  if (!buf.uniq || !buf.dloc || !buf.wloc || !buf.loss || !buf.stats) throw std::invalid_argument("missing output buffer");
+  const int64_t E = (int64_t)cfg.cap * cfg.NZ;
+  const int64_t umax = cfg.F < E ? cfg.F : E;
+  if (umax > 0x7fffffff / 2) throw std::invalid_argument("window too large");
+  cfg_.umax = (int)umax;
+  const int64_t PLmax = KP + umax * KP;
+  const size_t H = cfg.sc.hist;
+  nblk_dots_ = wide_dots_blocks(PLmax);
+
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = align256(off + bytes);
+    return o;
+  };
+  const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16);
+  const size_t o_map = take((size_t)cfg.F * 4), o_lid = take((size_t)E * 4);
+  const size_t o_s1 = take(umax * 4), o_s2 = take(umax * 4), o_sc = take(umax * 4), o_gs = take(umax * 4);
+  const size_t o_x = take(PLmax * 4), o_d = take(PLmax * 4), o_gt = take(PLmax * 4), o_gc = take(PLmax * 4),
+               o_w0 = take(PLmax * 4);
+  const size_t o_S = take(H * PLmax * 4), o_Y = take(H * PLmax * 4);
+  const size_t o_part = take((size_t)nblk_dots_ * kWideND * 8), o_loss = take((size_t)cfg.sc.nslots * 8);
+  ws_bytes_ = off;
+  hip_check(hipMalloc(&ws_, ws_bytes_), "hipMalloc(wide solver workspace)");
+  hip_check(hipMemset(ws_, 0, ws_bytes_), "hipMemset(wide solver workspace)");
+  char* b = static_cast<char*>(ws_);
+  hip_check(hipMemset(b + o_map, 0xff, (size_t)cfg.F * 4), "hipMemset(map)");  // all -1
+  hip_check(hipHostMalloc((void**)&host_u_, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
+  *host_u_ = 0;
+
+  dv_.ridx = buf.ridx;
+  dv_.rval = buf.rval;
+  dv_.rnnz = buf.rnnz;
+  dv_.ry = buf.ry;
+  dv_.w_old = buf.w_old;
+  dv_.prm = reinterpret_cast<WideParams*>(b + o_prm);
+  dv_.ctrl = reinterpret_cast<Ctrl*>(b + o_ctrl);
+  dv_.cnt = reinterpret_cast<unsigned*>(b + o_cnt);
+  dv_.map = reinterpret_cast<int32_t*>(b + o_map);
+  dv_.uniq = buf.uniq;
+  dv_.lid = reinterpret_cast<int32_t*>(b + o_lid);
+  dv_.s1 = reinterpret_cast<float*>(b + o_s1);
+  dv_.s2 = reinterpret_cast<float*>(b + o_s2);
+  dv_.scale = reinterpret_cast<float*>(b + o_sc);
+  dv_.gscale = reinterpret_cast<float*>(b + o_gs);
+  dv_.x = reinterpret_cast<float*>(b + o_x);
+  dv_.d = reinterpret_cast<float*>(b + o_d);
+  dv_.g_t = reinterpret_cast<float*>(b + o_gt);
+  dv_.g_c = reinterpret_cast<float*>(b + o_gc);
+  dv_.w0 = reinterpret_cast<float*>(b + o_w0);
+  dv_.S = reinterpret_cast<float*>(b + o_S);
+  dv_.Y = reinterpret_cast<float*>(b + o_Y);
+  dv_.part = reinterpret_cast<double*>(b + o_part);
+  dv_.loss_acc = reinterpret_cast<double*>(b + o_loss);
+  dv_.dloc = buf.dloc;
+  dv_.wloc = buf.wloc;
+  dv_.uniq_out = dv_.uniq;
+  dv_.loss = buf.loss;
+  dv_.stats = buf.stats;
+  dv_.delta_dense = buf.delta_dense;
+  dv_.host_u = host_u_;
+  dv_.PLmax = PLmax;
+
+  hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  if (use_graph_) {
+    hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    enqueue_body(cap_stream_, 1, 0);
+    hip_check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
+    hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+    size_t n = 0;
+    hip_check(hipGraphGetNodes(graph_, nullptr, &n), "hipGraphGetNodes");
+    std::vector<hipGraphNode_t> nodes(n);
+    hip_check(hipGraphGetNodes(graph_, nodes.data(), &n), "hipGraphGetNodes");
+    for (auto nd : nodes) {
+      hipGraphNodeType t;
+      hip_check(hipGraphNodeGetType(nd, &t), "hipGraphNodeGetType");
+      if (t != hipGraphNodeTypeKernel) continue;
+      hipKernelNodeParams kp{};
+      hip_check(hipGraphKernelNodeGetParams(nd, &kp), "hipGraphKernelNodeGetParams");
+      if (kp.func == wide_begin_symbol()) {
+        begin_node_ = nd;
+        begin_params_ = kp;
+      }
+    }
+    if (!begin_node_) throw std::runtime_error("wide solver graph: begin node not found");
+    begin_args_ = BeginArgs{dv_, 1, 0};
+    begin_kp_[0] = &begin_args_.d;
+    begin_kp_[1] = &begin_args_.B;
+    begin_kp_[2] = &begin_args_.start;
+    begin_params_.kernelParams = begin_kp_;
+    begin_params_.extra = nullptr;
+  }
+}
+
+WideSolver::~WideSolver() {
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
+  if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
+  if (ws_) (void)hipFree(ws_);
+  if (host_u_) (void)hipHostFree(host_u_);
+}
+
+void WideSolver::enqueue_body(hipStream_t s, int B, int start) {
+  wide_launch_begin(cfg_, dv_, B, start, s);
+  wide_launch_prepare(cfg_, dv_, s);
+  for (int slot = 0; slot < cfg_.sc.nslots; ++slot) wide_launch_slot(cfg_, dv_, slot, nblk_dots_, s);
+  if (cfg_.dense_delta)
+    hip_check(hipMemsetAsync(dv_.delta_dense, 0, (size_t)(cfg_.F * cfg_.KP + cfg_.KP) * 4, s), "memset delta");
+  wide_launch_finalize(cfg_, dv_, s);
+  hip_check(hipGetLastError(), "wide solver launch");
+}
+
+void WideSolver::run(int B, int start, hipStream_t stream) {
+  if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
+  if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
+  if (use_graph_) {
+    begin_args_.B = B;
+    begin_args_.start = start;
+    hip_check(hipGraphExecKernelNodeSetParams(exec_, begin_node_, &begin_params_), "hipGraphExecKernelNodeSetParams");
+    hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
+  } else {
+    enqueue_body(stream, B, start);
+  }
+}
+
+void WideSolver::read_ctrl(Ctrl* out, hipStream_t stream) {
+  hip_check(hipMemcpyAsync(out, dv_.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, stream), "read ctrl");
+  hip_check(hipStreamSynchronize(stream), "sync");
+}
+
+}  // namespace psx

@@ -47,8 +47,17 @@ def feature_std(X: torch.Tensor) -> torch.Tensor:
 
 
 def multinomial_loss_grad(X, y, coef_eff, b):
-    """Mean cross entropy and gradients w.r.t. the effective coefficients / intercepts."""
+    """Mean cross entropy and gradients w.r.t. the effective coefficients / intercepts.
+
+    One coefficient row (K == 1) is the binary sigmoid model with labels {0, 1}."""
     z = X @ coef_eff.t() + b
+    if coef_eff.shape[0] == 1:
+        zz = z[:, 0]
+        yy = (y > 0).to(z.dtype)
+        loss = (torch.nn.functional.softplus(zz) - yy * zz).mean()
+        r = (torch.sigmoid(zz) - yy).view(-1, 1)
+        n = X.shape[0]
+        return loss, (r.t() @ X) / n, r.sum(0) / n
     lse = torch.logsumexp(z, dim=1)
     loss = (lse - z.gather(1, y.view(-1, 1)).squeeze(1)).mean()
     p = torch.softmax(z, dim=1)
@@ -90,6 +99,7 @@ def local_solve_reference(
     center: bool = True,
     zero_const: bool = True,
     tol: float = 1e-6,
+    standardize: bool = True,
 ) -> SolveResult:
     """Run the worker's local solve on a buffer (X: [B, F] float, y: [B] int)."""
     X = X.double()
@@ -99,7 +109,7 @@ def local_solve_reference(
         nslots = 1 + iters * (1 if mode == "gd" else ls_max)
     w_old = coef_old.double()
     b_old = intercept_old.double()
-    sd = feature_std(X)
+    sd = feature_std(X) if standardize else torch.ones(X.shape[1], dtype=X.dtype)
     live = sd > 0
     inv = torch.where(live, 1.0 / torch.where(live, sd, torch.ones_like(sd)), torch.zeros_like(sd))
     wfix = torch.zeros_like(w_old) if zero_const else torch.where(live, torch.zeros_like(w_old), w_old)
@@ -250,7 +260,7 @@ def local_solve_reference(
                 break
     c, b = unpack(x)
     coef = torch.where(live, c * inv, wfix)
-    if center:
+    if center and K >= 2:
         coef = coef - coef.mean(0, keepdim=True)
         b = b - b.mean()
     return SolveResult(

@@ -35,6 +35,7 @@ class SolverOptions:
     center: bool = True  # Spark centring when regParam == 0
     zero_const: bool = True  # Spark: zero-std features get coefficient 0
     tol: float = 1e-6
+    standardize: bool = True  # Spark default; the dense MFMA solver always standardises
     use_graph: bool = True
     max_eval_wg: int = 512
 

@@ -192,3 +192,106 @@ def ensure_finefood_csv(directory: str, train_rows: int = 90000, test_rows: int 
     if not os.path.exists(te):
         write_csv(synth_finefood(test_rows, seed=seed + 1), te)
     return tr, te
+
+
+# ---------------------------------------------------------------------------
+# sparse (wide) datasets: BASELINE.json configs 4 (10M x 1M, labels 1..5) and
+# 5 (100M-dim weights, binary labels)
+def _mix_hash(x: torch.Tensor, salt: int) -> torch.Tensor:
+    """64-bit multiplicative hash (wrapping int64 arithmetic), non-negative result."""
+    h = (x + salt) * -7046029254386353131  # 0x9E3779B97F4A7C15 as int64
+    h = h ^ (h >> 29)
+    h = h * -4658895280553007687  # 0xBF58476D1CE4E5B9
+    return (h >> 17) & ((1 << 46) - 1)
+
+
+def synth_sparse(
+    rows: int,
+    num_features: int = 1 << 20,
+    labels: str = "finefood",
+    nnz_mean: float = 48.0,
+    max_nnz: int = 128,
+    seed: int = 0,
+    device="cpu",
+    signal: float = 0.10,
+    class_vocab: int = 2000,
+    vocab: int | None = None,
+    chunk_rows: int = 1 << 20,
+):
+    """Sparse hashed bag-of-words rows (CSR), generated on ``device`` in chunks.
+
+    * words are Zipf-like (log-uniform rank) over a vocabulary of ``vocab``
+      (default 4*F) hashed into ``num_features`` buckets with a hashed sign;
+    * with probability ``signal`` a word comes from the row's class vocabulary
+      (adjacent ratings share half of it), which plants the learnable signal;
+    * duplicate buckets of a row are merged and the row is L2-normalised, like
+      the reference's hashed + normalised review text (README.md:209-216);
+    * ``labels``: "finefood" = ratings 1..5 with the fine-food mix (multinomial,
+      K = 6 incl. the phantom class 0), "binary" = {0, 1} (sigmoid model, K = 1).
+    """
+    from ..ops.sparse import SparseDataset
+
+    dev = torch.device(device)
+    F = int(num_features)
+    V = int(vocab or 4 * F)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    mix = torch.tensor(FINEFOOD_LABEL_MIX / FINEFOOD_LABEL_MIX.sum(), dtype=torch.float32, device=dev)
+    lnV = float(np.log(V))
+    ips, ids, vals, ys = [], [], [], []
+    base = 0
+    for r0 in range(0, rows, chunk_rows):
+        n = min(chunk_rows, rows - r0)
+        if labels == "binary":
+            y = torch.randint(0, 2, (n,), generator=g, device=dev)
+            cls = y
+            ncls = 2
+        else:
+            y = torch.multinomial(mix, n, replacement=True, generator=g) + 1
+            cls = y - 1
+            ncls = 5
+        cnt = torch.poisson(torch.full((n,), float(nnz_mean), device=dev), generator=g).long().clamp_(4, max_nnz)
+        tot = int(cnt.sum())
+        row_of = torch.repeat_interleave(torch.arange(n, device=dev), cnt)
+        u = torch.rand(tot, generator=g, device=dev, dtype=torch.float64)
+        rank = torch.exp(u * lnV).long().clamp_(1, V)
+        use_cls = torch.rand(tot, generator=g, device=dev) < signal
+        pick = torch.randint(0, class_vocab, (tot,), generator=g, device=dev)
+        cword = V + 1 + cls[row_of] * (class_vocab // 2) + pick
+        word = torch.where(use_cls, cword, rank)
+        feat = _mix_hash(word, 0x51ED) % F
+        sign = (_mix_hash(word, 0x5EED) & 1).to(torch.float32) * 2.0 - 1.0
+        key = row_of * F + feat
+        uk, inv = torch.unique(key, sorted=True, return_inverse=True)
+        v = torch.zeros(uk.numel(), dtype=torch.float32, device=dev).index_add_(0, inv, sign)
+        keep = v != 0
+        uk, v = uk[keep], v[keep]
+        rr = uk // F
+        ff = (uk - rr * F).to(torch.int32)
+        norm = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, rr, v * v).clamp_min_(1e-12).sqrt_()
+        v = v / norm[rr]
+        per_row = torch.bincount(rr, minlength=n)
+        ips.append(torch.cumsum(per_row, 0) + base)
+        base += int(per_row.sum())
+        ids.append(ff)
+        vals.append(v.to(torch.bfloat16))
+        ys.append(y.to(torch.int32))
+        del key, inv, uk, u, rank, word, feat, sign, row_of
+    indptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev)] + ips)
+    return SparseDataset(indptr, torch.cat(ids), torch.cat(vals), torch.cat(ys), F)
+
+
+def load_libsvm(path: str, num_features: int | None = None, zero_based: bool = False, threads: int = 0):
+    """LIBSVM text -> :class:`SparseDataset` (native multithreaded parser)."""
+    from ..ops.sparse import SparseDataset
+
+    indptr, idx, val, y, maxf = _native.host.libsvm_load(path, zero_based, threads)
+    F = int(num_features) if num_features is not None else int(maxf) + 1
+    if maxf >= F:
+        raise ValueError(f"{path}: feature index {maxf} >= num_features {F}")
+    return SparseDataset(torch.from_numpy(indptr), torch.from_numpy(idx), torch.from_numpy(val.view(np.int16)).view(torch.bfloat16),
+                         torch.from_numpy(y), max(F, 1))
+
+
+def save_libsvm(ds, path: str, zero_based: bool = False) -> None:
+    _native.host.libsvm_save(path, ds.indptr.cpu().numpy(), ds.idx.cpu().numpy(),
+                             ds.val.cpu().view(torch.int16).numpy().view(np.uint16), ds.y.cpu().numpy(), zero_based)

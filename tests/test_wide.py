@@ -1,0 +1,233 @@
+"""Wide / sparse logistic-regression path (BASELINE.json configs 4 and 5).
+
+CPU tests pin the oracle path (subspace solve == dense solve on the densified
+window, sparse delta <-> dense delta, server apply, evaluation); GPU tests
+compare the HIP kernels (csrc/kernels/wide_kernels.hip) against it.
+"""
+import math
+
+import pytest
+import torch
+
+from psx.models.reference import local_solve_reference
+from psx.models.wide import WideSpec
+from psx.ops.lr import EvalScratch, SolverOptions
+from psx.ops.sparse import (SparseDelta, SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide_logits,
+                            wide_server_apply)
+from psx.utils.data import load_libsvm, save_libsvm, synth_sparse
+
+
+def _problem(F=3000, rows=400, labels="finefood", seed=0):
+    ds = synth_sparse(rows, num_features=F, labels=labels, nnz_mean=20, max_nnz=48, seed=seed, vocab=4 * F,
+                      class_vocab=200, signal=0.3)
+    K = 1 if labels == "binary" else 6
+    return ds, WideSpec(F, K)
+
+
+def _fill_ring(ds, cap, NZ, device, start=0, n=None):
+    ring = SparseRing(cap, NZ, device)
+    n = ds.rows if n is None else n
+    ring.ingest_from(ds.to(device), 0, 1, n, start)
+    return ring
+
+
+def test_synth_sparse_shape_and_norm():
+    ds, spec = _problem()
+    assert ds.rows == 400 and ds.indptr[-1] == ds.nnz
+    assert int(ds.idx.min()) >= 0 and int(ds.idx.max()) < spec.F
+    rows = ds.dense(range(5))
+    assert torch.allclose(rows.norm(dim=1), torch.ones(5), atol=2e-2)
+    assert set(ds.y.tolist()) <= {1, 2, 3, 4, 5}
+    b, _ = _problem(labels="binary")
+    assert set(b.y.tolist()) <= {0, 1}
+
+
+def test_libsvm_roundtrip(tmp_path):
+    ds, spec = _problem(rows=50)
+    p = str(tmp_path / "d.svm")
+    save_libsvm(ds, p)
+    back = load_libsvm(p, num_features=spec.F)
+    assert torch.equal(back.indptr, ds.indptr) and torch.equal(back.idx, ds.idx)
+    assert torch.equal(back.val.view(torch.int16), ds.val.view(torch.int16)) and torch.equal(back.y, ds.y)
+
+
+def test_nz_capacity():
+    assert nz_capacity(3) == 8 and nz_capacity(48) == 48 and nz_capacity(49) == 56
+    with pytest.raises(ValueError):
+        nz_capacity(513)
+
+
+def test_ring_wraps_and_truncates():
+    ds, _ = _problem(rows=30)
+    ring = SparseRing(16, 8, "cpu")
+    ring.ingest_from(ds, 0, 1, 30, 5)  # wraps; rows longer than 8 entries are cut
+    assert int(ring.trunc) == int(((ds.indptr[1:] - ds.indptr[:-1]) > 8).sum())
+    # slot (5 + 29) % 16 = 2 holds row 29
+    a = int(ds.indptr[29])
+    k = int(ring.nnz[2])
+    assert torch.equal(ring.idx[2, :k], ds.idx[a:a + k]) and int(ring.y[2]) == int(ds.y[29])
+
+
+@pytest.mark.parametrize("labels", ["finefood", "binary"])
+def test_cpu_subspace_solve_matches_dense_solve(labels):
+    """The wide op solves in the window's feature subspace; on the full feature
+    space the reference gives the same coefficients for the touched features."""
+    ds, spec = _problem(F=400, rows=120, labels=labels)
+    opts = SolverOptions(standardize=False, zero_const=False)
+    ring = _fill_ring(ds, 128, 48, "cpu")
+    g = torch.Generator().manual_seed(1)
+    w_old = spec.init("random", seed=3)
+    op = WideSolveOp(spec, 128, 48, "cpu", opts, dense_delta=True)
+    op.run(ring, 120, 0, w_old)
+    # dense oracle on all F features (untouched ones have zero gradient)
+    X = ds.dense().double()
+    coef = spec.coef(w_old).double()
+    b = spec.intercept(w_old).double()
+    res = local_solve_reference(X, ds.y.long(), coef, b, standardize=False, zero_const=False)
+    dense = spec.pack(res.delta_coef, res.delta_intercept)
+    touched = torch.zeros(spec.F, dtype=torch.bool)
+    touched[ds.idx.long()] = True
+    mask = torch.zeros(spec.P, dtype=torch.bool)
+    mask[: spec.F * spec.KP].view(spec.F, spec.KP)[touched] = True
+    mask[spec.F * spec.KP:] = True
+    if spec.K >= 2:  # centring also moves the untouched features' coefficients in the dense solve
+        assert torch.allclose(op.delta[mask], dense[mask], atol=1e-4), (op.delta - dense).abs().max()
+    else:
+        assert torch.allclose(op.delta, dense, atol=1e-5), (op.delta - dense).abs().max()
+    assert math.isclose(float(op.loss), res.loss, rel_tol=1e-5)
+    del g
+
+
+def test_sparse_delta_and_server_apply_cpu():
+    ds, spec = _problem(F=500, rows=64)
+    ring = _fill_ring(ds, 64, 48, "cpu")
+    op = WideSolveOp(spec, 64, 48, "cpu", SolverOptions(), dense_delta=True)
+    w = spec.init("random", seed=1)
+    op.run(ring, 64, 0, w)
+    sd = op.sparse_delta()
+    assert torch.allclose(sd.to_dense(), op.delta)
+    w1 = w.clone()
+    wide_server_apply(spec, w1, sd, 0.5)
+    w2 = w.clone()
+    wide_server_apply(spec, w2, op.delta, 0.5)
+    assert torch.allclose(w1, w2)
+
+
+def test_eval_cpu_matches_manual():
+    ds, spec = _problem(F=300, rows=200)
+    ev = WideEvalSet(spec, ds, "cpu")
+    w = spec.init("random", seed=2, scale=1.0)
+    z = ds.dense() @ spec.coef(w).t() + spec.intercept(w)
+    pred = z.argmax(1)
+    conf = ev.confusion_cpu(w).view(16, 16)
+    for t, p in zip(ds.y.tolist()[:50], pred.tolist()[:50]):
+        assert conf[t, p] > 0
+    assert int(conf.sum()) == ds.rows
+
+
+# ---------------------------------------------------------------------------
+# GPU: HIP kernels vs the CPU oracle
+def _gpu_vs_cpu(cuda, labels, opts, F=3000, rows=300, cap=320, start=250):
+    ds, spec = _problem(F=F, rows=rows, labels=labels)
+    NZ = nz_capacity(ds.max_nnz)
+    w = spec.init("random", seed=5, scale=0.05)
+    out = {}
+    for dev in ("cpu", cuda):
+        ring = _fill_ring(ds, cap, NZ, dev, start=start)
+        op = WideSolveOp(spec, cap, NZ, dev, opts, dense_delta=True)
+        op.run(ring, rows, start, w.to(dev))
+        if dev != "cpu":
+            torch.cuda.synchronize()
+            assert op.host_count() == int(torch.unique(ds.idx).numel())
+        out[dev] = (op.delta.cpu(), float(op.loss), op.stats.cpu().tolist(), op)
+    (dc, lc, sc, _), (dg, lg, sg, opg) = out["cpu"], out[cuda]
+    assert sc[0] == sg[0] and sc[1] == sg[1], (sc, sg)  # evaluations and accepted steps
+    assert math.isclose(lc, lg, rel_tol=1e-4), (lc, lg)
+    scale = dc.abs().max().item()
+    assert (dc - dg).abs().max().item() <= 2e-3 * scale + 1e-6, ((dc - dg).abs().max().item(), scale)
+    return spec, ds, opg, w
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("labels,std", [("finefood", True), ("finefood", False), ("binary", True), ("binary", False)])
+def test_gpu_wide_solve_matches_oracle(cuda, labels, std):
+    _gpu_vs_cpu(cuda, labels, SolverOptions(standardize=std, zero_const=False))
+
+
+@pytest.mark.gpu
+def test_gpu_wide_solve_gd_and_no_graph(cuda):
+    _gpu_vs_cpu(cuda, "finefood", SolverOptions(mode="gd", gd_lr=0.5, use_graph=False))
+
+
+@pytest.mark.gpu
+def test_gpu_wide_solve_repeated_windows(cuda):
+    """Back-to-back solves reuse the feature map (reset by the next solve's first kernel)."""
+    ds, spec = _problem(F=2000, rows=600)
+    NZ = nz_capacity(ds.max_nnz)
+    cap = 256
+    opts = SolverOptions(zero_const=False)
+    gring, cring = SparseRing(cap, NZ, cuda), SparseRing(cap, NZ, "cpu")
+    gop = WideSolveOp(spec, cap, NZ, cuda, opts, dense_delta=True)
+    cop = WideSolveOp(spec, cap, NZ, "cpu", opts, dense_delta=True)
+    w = spec.init("random", seed=9, scale=0.05)
+    wg = w.to(cuda)
+    dsg = ds.to(cuda)
+    for it in range(4):
+        first = it * 100
+        gring.ingest_from(dsg, first, 1, 200, first % cap)
+        cring.ingest_from(ds, first, 1, 200, first % cap)
+        gop.run(gring, 200, first % cap, wg)
+        cop.run(cring, 200, first % cap, w)
+        wide_server_apply(spec, wg, gop.sparse_delta(), 0.5)
+        wide_server_apply(spec, w, cop.delta, 0.5)
+    torch.cuda.synchronize()
+    assert (wg.cpu() - w).abs().max().item() < 2e-3 * w.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_gpu_wide_eval_and_logits(cuda):
+    from psx.utils.logsink import LogSink
+
+    ds, spec = _problem(F=1000, rows=500)
+    w = spec.init("random", seed=4, scale=1.0)
+    zc = wide_logits(spec, ds, w)
+    zg = wide_logits(spec, ds.to(cuda), w.to(cuda)).cpu()
+    assert torch.allclose(zc, zg, atol=1e-4)
+    ev_c, ev_g = WideEvalSet(spec, ds, "cpu"), WideEvalSet(spec, ds, cuda)
+    sinks = []
+    for ev, dev in ((ev_c, "cpu"), (ev_g, cuda)):
+        log = LogSink(spec.eval_classes, dev)
+        log.server_eval(ev, None, w.to(dev), EvalScratch(dev), 0)
+        sinks.append(log.book.server[0])
+        log.close()
+    assert abs(sinks[0][2] - sinks[1][2]) < 1e-9 and abs(sinks[0][3] - sinks[1][3]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_gpu_wide_eval_overlay(cuda):
+    """Worker rows evaluate the local model = pulled weights overlaid with the subspace solution."""
+    from psx.utils.logsink import LogSink
+
+    spec, ds, opg, w = _gpu_vs_cpu(cuda, "finefood", SolverOptions(zero_const=False))
+    ev = WideEvalSet(spec, ds, cuda)
+    log = LogSink(spec.eval_classes, cuda)
+    log.worker_eval(ev, opg, w.to(cuda), EvalScratch(cuda), opg.loss, 0, 0, 0)
+    row = log.book.worker[0]
+    log.close()
+    ref = WideEvalSet(spec, ds, "cpu").confusion_cpu(w + opg.delta.cpu()).view(16, 16)[:6, :6].double()
+    acc = float(ref.trace() / ref.sum())
+    assert abs(row[5] - acc) < 2e-3
+
+
+@pytest.mark.gpu
+def test_gpu_sparse_ring_ingest(cuda):
+    ds, _ = _problem(rows=100)
+    NZ = 16
+    rc, rg = SparseRing(64, NZ, "cpu"), SparseRing(64, NZ, cuda)
+    rc.ingest_from(ds, 3, 2, 40, 50)
+    rg.ingest_from(ds.to(cuda), 3, 2, 40, 50)
+    torch.cuda.synchronize()
+    assert torch.equal(rc.nnz, rg.nnz.cpu()) and torch.equal(rc.y, rg.y.cpu()) and int(rc.trunc) == int(rg.trunc)
+    for s in range(64):
+        k = int(rc.nnz[s])
+        assert torch.equal(rc.idx[s, :k], rg.idx[s, :k].cpu())

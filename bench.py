@@ -1,26 +1,34 @@
 """Headline benchmark: parameter-server updates/s + test accuracy on MI355X.
 
 Metric (BASELINE.json): "test-accuracy-vs-wallclock + SGD updates/sec, logistic
-regression, 1/2/4/8 workers".  One *step* is one Sequential-consistency (BSP)
-round: every worker ingests new stream rows into its HBM ring, runs the local
-solve on its adaptive window (2 L-BFGS iterations with strong-Wolfe line
-search on the standardised multinomial objective = the reference's Spark
-``setMaxIter(2)`` fit), evaluates its local model on the 4,877-row test set
-(the reference logs that every iteration), pushes its delta; the server
-applies the aggregate (lr = 1/N), evaluates the global model on the test set
-and all workers pull the new weights.  Nothing is skipped inside the timed
-region.
+regression, 1/2/4/8 workers".  One *step* is one round of the parameter
+server: under Sequential consistency (BSP) every worker ingests new stream
+rows into its HBM ring, runs the local solve on its adaptive window (2 L-BFGS
+iterations with strong-Wolfe line search on the standardised objective = the
+reference's Spark ``setMaxIter(2)`` fit, LogisticRegressionTaskSpark.java:
+170-184), evaluates its local model on the test set (the reference logs that
+every iteration), pushes its delta; the server applies the aggregate
+(lr = 1/N), evaluates the global model and all workers pull the new weights.
+Under ASP a step is one worker iteration per worker (the server applies every
+push on arrival).  Nothing is skipped inside the timed region.
 
-Config: multinomial LR, F = 1024 hashed features, labels 1..5 (+ phantom class
-0: K = 6, P = 6150), buffer min/max/bc = 128/1024/0.3, synthetic
-fine-food-reviews-shaped data (90k train / 4,877 test rows, random labels mix
-as the real set), random-init weights, bf16 features with fp32 master weights.
+--model dense  (default, BASELINE.json config 2/3 = the headline): multinomial
+    LR, F = 1024 hashed features, labels 1..5 (+ phantom class 0: K = 6,
+    P = 6150), buffer min/max/bc = 128/1024/0.3, fine-food-reviews-shaped
+    synthetic data (90k train / 4,877 test rows), random-init weights, bf16
+    features with fp32 master weights.  BSP, allreduce schedule.
+--model sparse1m  (config 4): 10M rows x 2^20 hashed sparse features, labels
+    1..5, ASP with a dedicated server rank (world >= 2; one GPU: in-process).
+--model sharded100m  (config 5): 10M rows x 10^8 hashed features, binary
+    sigmoid model, P = 10^8 + 1 dense fp32 weights, BSP key-range sharded
+    server (reduce-scatter of the dense delta + all-gather of the weights).
 
-value = server-applied updates per second over ALL workers (N * rounds / s).
-vs_baseline = value / reference updates/s (0.76 for 1 worker, 1.85 for the
-best 4-worker run).
+value = server-applied updates per second over ALL workers.
+vs_baseline = value / reference updates/s (dense: 0.76 for 1 worker, 1.85 for
+the best 4-worker run); null for the configs the reference never
+ran.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M]
        (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL.)
 """
 from __future__ import annotations
@@ -37,29 +45,48 @@ sys.path.insert(0, ROOT)
 REF_UPDATES_PER_S_1W = 0.76  # single worker, 804 updates / 1053 s
 REF_UPDATES_PER_S_4W = 1.85  # best 4-worker run
 
+MODELS = {
+    "dense": dict(features=1024, train_rows=90000, test_rows=4877, consistency=0, schedule="allreduce"),
+    "sparse1m": dict(features=1 << 20, train_rows=10_000_000, test_rows=20000, consistency=-1, schedule="allreduce"),
+    "sharded100m": dict(features=100_000_000, train_rows=10_000_000, test_rows=20000, consistency=0,
+                        schedule="sharded"),
+}
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--consistency", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 2000 dense, 300 wide)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 200 dense, 30 wide)")
+    ap.add_argument("--model", default="dense", choices=sorted(MODELS))
+    ap.add_argument("--consistency", type=int, default=None)
     ap.add_argument("--rows-per-step", type=int, default=64, help="new stream rows per worker per step")
-    ap.add_argument("--train-rows", type=int, default=90000)
-    ap.add_argument("--test-rows", type=int, default=4877)
-    ap.add_argument("--features", type=int, default=1024)
+    ap.add_argument("--train-rows", type=int, default=None)
+    ap.add_argument("--test-rows", type=int, default=None)
+    ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=2)
-    ap.add_argument("--schedule", default="allreduce", choices=["allreduce", "reduce_bcast", "sharded"])
+    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    m = MODELS[a.model]
+    wide = a.model != "dense"
+    for k in ("features", "train_rows", "test_rows", "consistency", "schedule"):
+        if getattr(a, k) is None:
+            setattr(a, k, m[k])
+    if a.steps is None:
+        a.steps = 300 if wide else 2000
+    if a.warmup is None:
+        a.warmup = 30 if wide else 200
+    return a
 
 
 def build_cfg(a, n_workers):
     from psx.ops.lr import SolverOptions
     from psx.runtime.config import PSConfig
 
+    wide = a.model != "dense"
     return PSConfig(
         num_workers=n_workers,
         consistency_model=a.consistency,
@@ -72,28 +99,90 @@ def build_cfg(a, n_workers):
         buffer_size_coefficient=0.3,
         init="random",
         seed=0,
-        solver=SolverOptions(iters=a.iters, use_graph=not a.no_graph),
+        model="wide" if wide else "dense",
+        sigmoid=a.model == "sharded100m",
+        solver=SolverOptions(iters=a.iters, use_graph=not a.no_graph, zero_const=not wide),
         bsp_schedule=a.schedule,
     )
+
+
+def make_data(a, device):
+    """Synthetic train/test sets of the configured shape (generated on the device for the wide configs)."""
+    from psx.utils.data import synth_finefood, synth_sparse
+
+    if a.model == "dense":
+        return (synth_finefood(a.train_rows, num_features=a.features, seed=0),
+                synth_finefood(a.test_rows, num_features=a.features, seed=1))
+    labels = "binary" if a.model == "sharded100m" else "finefood"
+    kw = dict(num_features=a.features, labels=labels, nnz_mean=48, max_nnz=128, device=device)
+    return synth_sparse(a.train_rows, seed=0, **kw), synth_sparse(a.test_rows, seed=1, **kw)
+
+
+def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
+    wide = a.model != "dense"
+    async_mode = a.consistency != 0
+    n_workers = cfg.num_workers
+    if a.model == "dense":
+        model = "multinomial-logreg F=1024 K=6 (P=6150), local solver L-BFGS x2 + strong-Wolfe"
+        data = "synthetic (fine-food-reviews-shaped, 90k train / 4877 test, random-init weights)"
+        ref = REF_UPDATES_PER_S_1W if world == 1 else REF_UPDATES_PER_S_4W
+        vs = round(ups / ref, 1)
+    else:
+        kind = "binary sigmoid" if a.model == "sharded100m" else "multinomial K=6"
+        model = f"sparse-input logreg F={a.features} {kind}, local solver L-BFGS x2 + strong-Wolfe (window subspace)"
+        data = (f"synthetic sparse hashed bag-of-words ({a.train_rows} train / {a.test_rows} test rows, "
+                f"~48 nnz/row, random-init weights)")
+        vs = None  # the reference never ran this configuration (BASELINE.md)
+    mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
+    if world == 1:
+        par = f"ps-{mode} w1 (server colocated)"
+    elif async_mode:
+        par = f"ps-{mode} 1 server + {n_workers} workers (RCCL p2p{', sparse push' if wide else ''})"
+    else:
+        par = f"ps-{mode} dp{world} ({cfg.bsp_schedule}, RCCL)"
+    res = {
+        "metric": "server_updates_per_s (PS push/pull rounds, logistic regression; test accuracy reported alongside)",
+        "value": round(ups, 2),
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt * 1000.0 / a.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": vs,
+        "dtype": "bf16",
+        "data": data,
+        "config": {
+            "model": model,
+            "global_batch": a.buffer * n_workers,
+            "seq_len": a.features,
+            "parallelism": par,
+            "consistency": a.consistency,
+            "rows_per_step_per_worker": a.rows_per_step,
+            "bench_model": a.model,
+        },
+        "test_accuracy": summ.get("final_server_acc"),
+        "test_f1": summ.get("final_server_f1"),
+        "best_test_f1": summ.get("best_server_f1"),
+    }
+    if tuples_seen is not None:
+        res["tuples_seen"] = tuples_seen
+    return res
 
 
 def main(argv=None):
     a = parse(argv)
     import torch
 
-    from psx.utils.data import synth_finefood
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 or world > 1:
-        from psx.parallel.dist import bench_distributed
-
-        return bench_distributed(a, build_cfg)
+        return bench_distributed(a)
 
     device = "cpu" if a.cpu else "cuda:0"
     from psx.runtime.engine import LocalEngine
 
-    train = synth_finefood(a.train_rows, num_features=a.features, seed=0)
-    test = synth_finefood(a.test_rows, num_features=a.features, seed=1)
+    train, test = make_data(a, device)
     cfg = build_cfg(a, 1)
     cfg.max_iters = a.warmup
     eng = LocalEngine(cfg, device, train=train, test=test)
@@ -108,35 +197,56 @@ def main(argv=None):
     if device != "cpu":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ups = a.steps * 1 / dt
-    res = {
-        "metric": "server_updates_per_s (PS push/pull rounds, multinomial LR; test accuracy reported alongside)",
-        "value": round(ups, 2),
-        "unit": "updates/s",
-        "n_gpus": 1,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(dt * 1000.0 / a.steps, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(ups / REF_UPDATES_PER_S_1W, 1),
-        "dtype": "bf16",
-        "data": "synthetic (fine-food-reviews-shaped, 90k train / 4877 test, random-init weights)",
-        "config": {
-            "model": "multinomial-logreg F=1024 K=6 (P=6150), local solver L-BFGS x2 + strong-Wolfe",
-            "global_batch": a.buffer,
-            "seq_len": a.features,
-            "parallelism": "ps-bsp w1 (server colocated)",
-            "consistency": a.consistency,
-            "rows_per_step_per_worker": a.rows_per_step,
-        },
-        "test_accuracy": out.get("final_server_acc"),
-        "test_f1": out.get("final_server_f1"),
-        "best_test_f1": out.get("best_server_f1"),
-        "accuracy_vs_wallclock": _curve(eng.log.book.server, t0),
-        "tuples_seen": eng.workers[0].tuples_seen,
-    }
+    ups = out["updates"] / dt
+    res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
+    res["accuracy_vs_wallclock"] = _curve(eng.log.book.server, t0)
     print(json.dumps(res))
+    return res
+
+
+def bench_distributed(a):
+    """N > 1 GPUs: one rank per GPU (torchrun), RCCL over xGMI."""
+    import torch
+    import torch.distributed as dist
+
+    from psx.ops.lr import is_gpu
+    from psx.parallel.dist import DistEngine, init_from_env
+    from psx.utils.logsink import LogSink, summarize
+
+    rank, world, device = init_from_env(cpu=a.cpu)
+    async_mode = a.consistency != 0
+    cfg = build_cfg(a, world - 1 if async_mode else world)
+    train, test = make_data(a, device)
+    cfg.max_iters = a.warmup
+    eng = DistEngine(cfg, rank, world, device, train=train, test=test)
+    if a.warmup:
+        eng._run_async() if async_mode else eng._run_bsp()
+    if eng.log is not None:
+        eng.log.close()
+        eng.log = LogSink(eng.spec.eval_classes, eng.device, keep_records=(rank == 0))
+    cfg.max_iters = a.steps
+    dist.barrier()
+    if is_gpu(device):
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    out = eng._run_async() if async_mode else eng._run_bsp()
+    dist.barrier()
+    if is_gpu(device):
+        torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    res = None
+    if rank == 0:
+        eng.log.close()
+        summ = summarize(eng.log.book)
+        ups = a.steps * cfg.num_workers / dt
+        res = describe(a, world, cfg, ups, dt, summ)
+        res["max_vc_gap"] = out.get("max_vc_gap")
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
     return res
 
 
@@ -154,7 +264,7 @@ def _fresh_log(eng):
     from psx.utils.logsink import LogSink
 
     eng.log.close()
-    return LogSink(eng.spec.K, eng.device)
+    return LogSink(eng.spec.eval_classes, eng.device)
 
 
 if __name__ == "__main__":

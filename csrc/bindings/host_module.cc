@@ -142,7 +142,8 @@ PYBIND11_MODULE(_psx_host, m) {
       .def_readwrite("kind", &CtrlToken::kind)
       .def_readwrite("vc", &CtrlToken::vc)
       .def_readwrite("aux", &CtrlToken::aux)
-      .def_readwrite("ts_us", &CtrlToken::ts_us);
+      .def_readwrite("ts_us", &CtrlToken::ts_us)
+      .def_readwrite("n", &CtrlToken::n);
 
   py::class_<CtrlQueue>(m, "CtrlQueue")
       .def(py::init<const std::string&, uint32_t, bool>(), py::arg("name"), py::arg("capacity"), py::arg("create"))

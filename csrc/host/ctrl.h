@@ -25,6 +25,7 @@ struct CtrlToken {
   int64_t vc;
   int64_t aux;   // free field (e.g. tuples seen)
   int64_t ts_us; // producer timestamp (for tracing)
+  int64_t n;     // payload size (sparse push: number of touched features)
 };
 
 class CtrlQueue {

@@ -52,6 +52,10 @@ class ModelSpec:
         return self.K * self.Fp + self.K
 
     @property
+    def eval_classes(self) -> int:
+        return self.K
+
+    @property
     def P_ref(self) -> int:  # reference parameter count
         return self.K * self.F + self.K
 

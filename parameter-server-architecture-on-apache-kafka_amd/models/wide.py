@@ -76,16 +76,17 @@ class WideSpec:
 
     def init(self, kind: str = "zeros", seed: int = 0, scale: float = 0.01, device=None) -> torch.Tensor:
         """Zeros (reference quirk Q6) or N(0, scale^2) coefficients.  Random
-        init is drawn on the target device in chunks (10^8 x KP floats)."""
+        init is drawn by a CPU generator (identical on every device and rank)
+        in chunks and streamed to the target device (10^8 x KP floats)."""
         dev = torch.device(device) if device is not None else torch.device("cpu")
         w = torch.zeros(self.P, dtype=torch.float32, device=dev)
         if kind == "random":
-            g = torch.Generator(device=dev).manual_seed(seed)
+            g = torch.Generator().manual_seed(seed)
             view = w[: self.F * self.KP].view(self.F, self.KP)
             step = 1 << 22
             for f0 in range(0, self.F, step):
                 f1 = min(self.F, f0 + step)
-                view[f0:f1, : self.K] = torch.randn(f1 - f0, self.K, generator=g, device=dev) * scale
+                view[f0:f1, : self.K] = (torch.randn(f1 - f0, self.K, generator=g) * scale).to(dev)
         elif kind != "zeros":
             raise ValueError(f"unknown init {kind!r}")
         return w

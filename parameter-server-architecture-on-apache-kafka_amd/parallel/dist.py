@@ -41,10 +41,11 @@ import torch.distributed as dist
 
 from .. import _native
 from ..models.logreg import ModelSpec
-from ..ops.lr import EvalSet, is_gpu
+from ..ops.lr import is_gpu
 from ..runtime.config import PSConfig
 from ..runtime.engine import load_datasets
-from ..runtime.roles import ServerRole, WorkerRole
+from ..ops.sparse import SparseDelta, nz_capacity
+from ..runtime.roles import ServerRole, WorkerRole, is_wide, make_evalset
 from ..utils.checkpoint import maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
@@ -87,10 +88,20 @@ class DistEngine:
         if cfg.num_workers != n_workers:
             cfg.num_workers = n_workers
         self.spec, train, test = load_datasets(cfg, train, test)
+        self.wide = is_wide(self.spec)
+        # wide model: collectives and dense p2p pushes need the dense delta;
+        # SSP/ASP with sparse_push send (feature ids, values) instead
+        self.sparse_push = self.wide and self.async_mode and cfg.sparse_push
+        if self.wide and not self.sparse_push:
+            cfg.wide_dense_delta = True
+        self._umax = 0
+        if self.wide:
+            nz = cfg.ring_nz or nz_capacity(train.max_nnz)
+            self._umax = min(self.spec.F, cfg.max_buffer_size * nz)
         self.is_server = rank == 0
         self.worker_id = (rank - 1) if self.dedicated else rank
         self.is_worker = self.worker_id >= 0
-        self.evalset = EvalSet(self.spec, test.X, test.y, self.device) if test is not None else None
+        self.evalset = make_evalset(self.spec, test, self.device)
         wp = sp = None
         append = False
         if cfg.logging:
@@ -109,9 +120,9 @@ class DistEngine:
             dist.barrier()
         # every rank evaluates (workers log their local model each iteration, as the
         # reference does); only files requested with -l are written
-        self.log = LogSink(self.spec.K, self.device, wp, sp, keep_records=(rank == 0), worker_append=append)
+        self.log = LogSink(self.spec.eval_classes, self.device, wp, sp, keep_records=(rank == 0), worker_append=append)
         self.tracer = Tracer(cfg.trace_path.replace(".json", f".rank{rank}.json") if cfg.trace_path else None, rank)
-        w0 = self.spec.init(cfg.init, seed=cfg.seed)
+        w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         # every rank keeps a server replica in the allreduce schedule; otherwise only rank 0
         replicated = (not self.async_mode) and cfg.bsp_schedule in ("allreduce", "sharded")
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0) if (self.is_server or replicated) else None
@@ -124,6 +135,7 @@ class DistEngine:
                                      t0=self.t0)
         self.rounds = 0
         self._ctrl = None
+        self._next_vc = 0
 
     # ------------------------------------------------------------------
     def run(self) -> dict:
@@ -277,8 +289,14 @@ class DistEngine:
     def _server_loop(self) -> dict:
         cfg, srv = self.cfg, self.server
         N = cfg.num_workers
-        buf = torch.zeros(self.spec.P, dtype=torch.float32, device=self.device)
+        buf = torch.zeros(self.spec.P, dtype=torch.float32, device=self.device) if not self.sparse_push else None
+        if self.sparse_push:
+            KP = self.spec.KP
+            ubuf = torch.zeros(self._umax, dtype=torch.int32, device=self.device)
+            dbuf = torch.zeros(KP + self._umax * KP, dtype=torch.float32, device=self.device)
         for j in range(N):  # bootstrap: vc 0 to every worker (tracker untouched)
+            if srv.tracker.clock(j) > 0:  # a later run of this engine: resume at the tracked clocks
+                srv.tracker.sent(j, srv.tracker.clock(j))
             dist.send(srv.w, dst=j + 1)
         finished = set()
         t_start = time.time()
@@ -288,11 +306,19 @@ class DistEngine:
                 raise TimeoutError("server: no worker token for 600 s (worker died?)")
             k, v = int(tok.worker), int(tok.vc)
             with self.tracer.span("recv", worker=k, vc=v):
-                dist.recv(buf, src=k + 1)
+                if self.sparse_push:
+                    U = int(tok.n)
+                    if U:
+                        dist.recv(ubuf[:U], src=k + 1)
+                    dist.recv(dbuf[: KP + U * KP], src=k + 1)
+                    delta = SparseDelta(self.spec, ubuf, dbuf, U)
+                else:
+                    dist.recv(buf, src=k + 1)
+                    delta = buf
             if k == 0:  # server eval rows follow worker-0 deltas (ServerProcessor.java:154-165)
-                srv.apply_and_log(buf, v, self.log)
+                srv.apply_and_log(delta, v, self.log)
             else:
-                srv.apply(buf)
+                srv.apply(delta)
             srv.updates += 1
             if tok.kind == KIND_FINAL:
                 finished.add(k)
@@ -314,7 +340,7 @@ class DistEngine:
         tok = _native.host.CtrlToken()
         tok.worker = wk.k
         dist.recv(wk.w, src=0)
-        wk.vc = 0
+        wk.vc = self._next_vc  # 0, or the server's clock for this worker on a later run
         max_iters = cfg.max_iters or 1 << 62
         t_start = time.time()
         it = 0
@@ -332,15 +358,24 @@ class DistEngine:
             tok.aux = wk.tuples_seen
             if is_gpu(self.device):
                 torch.cuda.current_stream(self.device).synchronize()  # delta ready before the token is visible
+            U = wk.solver.host_count() if self.sparse_push else 0
+            tok.n = U
             if not self._ctrl.push(tok, 600.0):
                 raise TimeoutError("worker: control queue full for 600 s")
-            dist.send(delta, dst=0)
+            if self.sparse_push:  # (ids, values) of the window's features only
+                KP = self.spec.KP
+                if U:
+                    dist.send(delta.uniq[:U], dst=0)
+                dist.send(delta.dloc[: KP + U * KP], dst=0)
+            else:
+                dist.send(delta, dst=0)
             if final:
                 break
             dist.recv(wk.w, src=0)
             wk.vc += 1
             if self.log is not None:
                 self.log.drain()
+        self._next_vc = wk.vc + 1
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start
@@ -355,69 +390,3 @@ def run_distributed(cfg: PSConfig, cpu: bool = False, train=None, test=None) -> 
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
-
-
-def bench_distributed(a, build_cfg) -> dict:
-    """bench.py body for N > 1 GPUs (one rank per GPU, launched by torchrun)."""
-    import bench as bench_mod  # noqa: F401  (constants)
-
-    from ..utils.data import synth_finefood
-
-    rank, world, device = init_from_env(cpu=a.cpu)
-    cfg = build_cfg(a, world)
-    train = synth_finefood(a.train_rows, num_features=a.features, seed=0)
-    test = synth_finefood(a.test_rows, num_features=a.features, seed=1)
-    cfg.max_iters = a.warmup
-    eng = DistEngine(cfg, rank, world, device, train=train, test=test)
-    if a.warmup:
-        eng._run_bsp() if not eng.async_mode else None
-    if eng.log is not None:
-        eng.log.close()
-        eng.log = LogSink(eng.spec.K, eng.device, keep_records=(rank == 0))
-    cfg.max_iters = a.steps
-    dist.barrier()
-    if is_gpu(device):
-        torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    out = eng._run_bsp()
-    dist.barrier()
-    if is_gpu(device):
-        torch.cuda.synchronize(device)
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    res = None
-    if rank == 0:
-        eng.log.close()
-        summ = summarize(eng.log.book)
-        ups = a.steps * world / dt
-        res = {
-            "metric": "server_updates_per_s (PS push/pull rounds, multinomial LR; test accuracy reported alongside)",
-            "value": round(ups, 2),
-            "unit": "updates/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(dt * 1000.0 / a.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(ups / bench_mod.REF_UPDATES_PER_S_4W, 1),
-            "dtype": "bf16",
-            "data": "synthetic (fine-food-reviews-shaped, 90k train / 4877 test, random-init weights)",
-            "config": {
-                "model": "multinomial-logreg F=1024 K=6 (P=6150), local solver L-BFGS x2 + strong-Wolfe",
-                "global_batch": a.buffer * world,
-                "seq_len": a.features,
-                "parallelism": f"ps-bsp dp{world} ({cfg.bsp_schedule}, RCCL)",
-                "consistency": a.consistency,
-                "rows_per_step_per_worker": a.rows_per_step,
-            },
-            "test_accuracy": summ.get("final_server_acc"),
-            "test_f1": summ.get("final_server_f1"),
-            "best_test_f1": summ.get("best_server_f1"),
-        }
-        print(json.dumps(res), flush=True)
-    dist.barrier()
-    dist.destroy_process_group()
-    return res

@@ -27,7 +27,7 @@ from .. import _native
 from ..ops.lr import is_gpu, stream_handle
 
 
-class DeviceRing:
+class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseRing
     """Row ring of one worker.  ``cap`` is rounded up to whole 32-row tiles (the
     solver walks windows as ring-aligned tiles); on the GPU a feature-major copy
     ``XT`` [Fp][cap] is kept in step so the backward / statistics kernels read
@@ -57,6 +57,9 @@ class DeviceRing:
             dst = (torch.arange(n) + dst_first) % self.cap
             self.X[dst] = src_X[src]
             self.y[dst] = src_y[src]
+
+    def ingest_from(self, ds, src_first: int, src_step: int, n: int, dst_first: int):
+        self.ingest(ds.X, ds.y, src_first, src_step, n, dst_first)
 
     def place(self, X: torch.Tensor, y: torch.Tensor, first: int = 0):
         """Write rows X[i], y[i] into slots (first + i) % cap (tests, tools)."""
@@ -127,7 +130,7 @@ class StreamSource:
         while remaining > 0:  # split at epoch boundaries of the shard
             cur = pos % self.local_total
             run = min(remaining, self.local_total - cur)
-            self.ring.ingest(self.ds.X, self.ds.y, self.k + cur * self.N, self.N, run, first_slot)
+            self.ring.ingest_from(self.ds, self.k + cur * self.N, self.N, run, first_slot)
             first_slot = (first_slot + run) % self.ring.cap
             pos += run
             remaining -= run

@@ -22,6 +22,14 @@ class PSConfig:
     label_col: int = -1
     num_features: int | None = None  # inferred from the CSV
     num_classes: int | None = None  # inferred: max label + 1 (incl. phantom class 0)
+    # model: "dense" (<= 2048 features, MFMA tiles), "wide" (sparse rows, up to
+    # ~10^8 features; BASELINE.json configs 4/5) or "auto" (wide for LIBSVM
+    # inputs / sparse datasets / more than 2048 features)
+    model: str = "auto"
+    sigmoid: bool = False  # wide model: one logit + sigmoid (binary labels)
+    ring_nz: int = 0  # wide model: non-zeros per ring row (0 = from the data)
+    wide_dense_delta: bool = False  # wide model: also produce a dense delta (collective pushes)
+    sparse_push: bool = True  # wide model, SSP/ASP across ranks: push (ids, values) instead of a dense delta
     # topology / consistency
     num_workers: int = 4
     consistency_model: int = 0  # 0 sequential, -1 eventual, D>0 bounded delay

@@ -22,16 +22,47 @@ import time
 import torch
 
 from ..models.logreg import ModelSpec
-from ..ops.lr import EvalSet, is_gpu
+from ..models.wide import WideSpec
+from ..ops.lr import is_gpu
 from ..utils import data as data_mod
 from ..utils.checkpoint import maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
 from .config import PSConfig
-from .roles import ServerRole, WorkerRole
+from .roles import ServerRole, WorkerRole, make_evalset
+
+
+def _wants_wide(cfg: PSConfig, train) -> bool:
+    if cfg.model in ("dense", "wide"):
+        return cfg.model == "wide"
+    if train is not None:
+        return not hasattr(train, "X")  # a SparseDataset
+    if data_mod.is_libsvm_path(cfg.train_path):
+        return True
+    return cfg.num_features is not None and cfg.num_features > 2048
 
 
 def load_datasets(cfg: PSConfig, train=None, test=None):
+    """Datasets + model spec: dense CSV/binary rows -> ModelSpec, sparse
+    (LIBSVM / SparseDataset) rows -> WideSpec."""
+    if _wants_wide(cfg, train):
+        if train is None:
+            train = data_mod.load_libsvm(cfg.train_path, num_features=cfg.num_features)
+        if test is None and cfg.test_path:
+            test = data_mod.load_libsvm(cfg.test_path, num_features=cfg.num_features or train.num_features)
+        F = max(train.num_features, test.num_features if test is not None else 0)
+        if cfg.num_features is not None:
+            F = int(cfg.num_features)
+        if cfg.sigmoid:
+            K = 1
+        elif cfg.num_classes is not None:
+            K = int(cfg.num_classes)
+        else:
+            mx = int(train.y.max())
+            if test is not None:
+                mx = max(mx, int(test.y.max()))
+            K = max(2, mx + 1)
+        return WideSpec(F, K), train, test
     if train is None:
         train = data_mod.load_any(cfg.train_path, header=cfg.header, label_col=cfg.label_col,
                                   num_features=cfg.num_features)
@@ -55,14 +86,14 @@ class LocalEngine:
         self.device = torch.device(device)
         self.spec, train, test = load_datasets(cfg, train, test)
         self.train = train.to(self.device)
-        self.evalset = EvalSet(self.spec, test.X, test.y, self.device) if test is not None else None
+        self.evalset = make_evalset(self.spec, test, self.device)
         if log is None:
             wp = f"{cfg.log_dir}/logs-worker.csv" if cfg.logging else None
             sp = f"{cfg.log_dir}/logs-server.csv" if cfg.logging else None
-            log = LogSink(self.spec.K, self.device, wp, sp, to_stdout=not cfg.logging and cfg.verbose)
+            log = LogSink(self.spec.eval_classes, self.device, wp, sp, to_stdout=not cfg.logging and cfg.verbose)
         self.log = log
         self.tracer = Tracer(cfg.trace_path)
-        w0 = self.spec.init(cfg.init, seed=cfg.seed)
+        w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0)
         self.t0 = time.time()
         self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
@@ -119,14 +150,7 @@ class LocalEngine:
             with self.tracer.span("solve"):
                 deltas = [w.compute(self.log) for w in W]
             with self.tracer.span("server"):
-                if N == 1:
-                    total = deltas[0]
-                else:
-                    total = srv.acc
-                    total.copy_(deltas[0])
-                    for d in deltas[1:]:
-                        total.add_(d)
-                srv.apply_and_log(total, r, self.log)  # w += lr*total and the server eval row, one kernel
+                srv.apply_round(deltas, r, self.log)  # w += lr*sum(deltas), then the server eval row
                 for k in range(N):
                     srv.tracker.received(k, r)
                 srv.updates += N
@@ -205,7 +229,10 @@ class LocalEngine:
             inbox[j].put((u, ev))
 
         for j in range(len(W)):  # bootstrap: vc 0 to everybody, tracker untouched
-            send(j, 0)
+            u = int(srv.tracker.clock(j))
+            if u > 0:  # a later run of this engine resumes at the tracked clocks
+                srv.tracker.sent(j, u)
+            send(j, u)
         t_start = time.time()
         exhausted = set()
         exhausted_since = None

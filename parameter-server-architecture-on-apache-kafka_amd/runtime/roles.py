@@ -17,22 +17,45 @@ import torch
 
 from .. import _native
 from ..models.logreg import ModelSpec
+from ..models.wide import WideSpec
 from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply
+from ..ops.sparse import SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide_server_apply
 from .buffer import DeviceRing, StreamSource
 from .config import PSConfig
 
 
+def is_wide(spec) -> bool:
+    return isinstance(spec, WideSpec)
+
+
+def make_evalset(spec, test, device):
+    """Device-resident test set of either model (dense MFMA tiles / sparse CSR)."""
+    if test is None:
+        return None
+    if is_wide(spec):
+        return WideEvalSet(spec, test, device)
+    return EvalSet(spec, test.X, test.y, device)
+
+
 class WorkerRole:
-    def __init__(self, k: int, spec: ModelSpec, cfg: PSConfig, device, train, evalset: EvalSet | None,
-                 t0: float | None = None):
+    def __init__(self, k: int, spec, cfg: PSConfig, device, train, evalset, t0: float | None = None):
         self.k, self.spec, self.cfg, self.device = k, spec, cfg, torch.device(device)
-        self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device)
+        self.wide = is_wide(spec)
+        if self.wide:
+            nz = cfg.ring_nz or nz_capacity(train.max_nnz)
+            self.ring = SparseRing(cfg.max_buffer_size, nz, self.device)
+        else:
+            self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device)
         self.window = _native.host.SlidingWindow(cfg.min_buffer_size, cfg.max_buffer_size,
                                                  cfg.buffer_size_coefficient, 500, self.ring.cap)
         self.source = StreamSource(train, k, cfg.num_workers, self.ring, self.window,
                                    p_ms=cfg.producer_time_per_event, mode=cfg.stream_mode,
                                    rows_per_iter=cfg.rows_per_iter, epochs=cfg.epochs, t0=t0)
-        self.solver = LocalSolveOp(spec, self.ring.cap, self.device, cfg.solver)
+        if self.wide:
+            self.solver = WideSolveOp(spec, self.ring.cap, self.ring.NZ, self.device, cfg.solver,
+                                      dense_delta=cfg.wide_dense_delta)
+        else:
+            self.solver = LocalSolveOp(spec, self.ring.cap, self.device, cfg.solver)
         self.evalset = evalset
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
         self.scratch = EvalScratch(self.device)
@@ -62,17 +85,24 @@ class WorkerRole:
         B, start = int(self.window.size), int(self.window.start)
         self.solver.run(self.ring, B, start, self.w)
         if log is not None and self.evalset is not None:
-            log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch, self.solver.loss,
-                            self.k, self.vc, self.tuples_seen)
+            if self.wide:  # local model = pulled weights overlaid with the subspace solution
+                log.worker_eval(self.evalset, self.solver, self.w, self.scratch, self.solver.loss, self.k, self.vc,
+                                self.tuples_seen)
+            else:
+                log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch, self.solver.loss,
+                                self.k, self.vc, self.tuples_seen)
         self.iters += 1
+        if self.wide and not self.solver.dense_delta:
+            return self.solver.sparse_delta()
         return self.solver.delta
 
 
 class ServerRole:
-    def __init__(self, spec: ModelSpec, cfg: PSConfig, device, evalset: EvalSet | None, w0: torch.Tensor):
+    def __init__(self, spec, cfg: PSConfig, device, evalset, w0: torch.Tensor):
         self.spec, self.cfg, self.device = spec, cfg, torch.device(device)
+        self.wide = is_wide(spec)
         self.w = w0.to(self.device, torch.float32).clone()
-        self.frag = Fragments(spec, self.device) if is_gpu(self.device) else None
+        self.frag = Fragments(spec, self.device) if is_gpu(self.device) and not self.wide else None
         if self.frag is not None:
             self.frag.refresh(self.w)
         self.tracker = _native.host.VectorClockTracker(cfg.num_workers, cfg.consistency_model)
@@ -83,7 +113,26 @@ class ServerRole:
 
     def apply(self, delta: torch.Tensor, lr: float | None = None):
         """w += lr * delta   (ServerProcessor.java:148-151 with lr = 1/N)."""
-        server_apply(self.spec, self.w, delta, self.cfg.lr if lr is None else lr, self.frag)
+        lr = self.cfg.lr if lr is None else lr
+        if self.wide:
+            wide_server_apply(self.spec, self.w, delta, lr)
+        else:
+            server_apply(self.spec, self.w, delta, lr, self.frag)
+
+    def apply_round(self, deltas, vc: int, log, lr: float | None = None):
+        """BSP round: w += lr * sum(deltas), then the server eval row."""
+        if len(deltas) == 1:
+            self.apply_and_log(deltas[0], vc, log, lr)
+            return
+        if all(isinstance(d, torch.Tensor) for d in deltas):
+            self.acc.copy_(deltas[0])
+            for d in deltas[1:]:
+                self.acc.add_(d)
+            self.apply_and_log(self.acc, vc, log, lr)
+            return
+        for d in deltas:  # sparse pushes: sequential applies == one applied sum
+            self.apply(d, lr)
+        self.log_eval(vc, log)
 
     def apply_and_log(self, delta: torch.Tensor, vc: int, log, lr: float | None = None):
         """apply() then the global-model evaluation row.  (A single fused

@@ -96,6 +96,10 @@ def load_bin(path: str) -> Dataset:
     return Dataset(X, torch.from_numpy(y.copy()), int(F))
 
 
+def is_libsvm_path(path: str | None) -> bool:
+    return bool(path) and path.endswith((".svm", ".libsvm", ".svmlight"))
+
+
 def load_any(path: str, **kw) -> Dataset:
     with open(path, "rb") as f:
         magic = f.read(8)

@@ -31,8 +31,16 @@ def _rank_main(rank, world, port, kw, out_q):
     from psx.utils.data import synth_finefood
 
     r, w, dev = init_from_env(cpu=True)
+    kw = dict(kw)
+    data = kw.pop("_data", "dense")
     cfg = PSConfig(**kw)
-    train, test = synth_finefood(1500, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
+    if data == "wide":
+        from psx.utils.data import synth_sparse
+
+        train = synth_sparse(1500, num_features=3000, nnz_mean=20, max_nnz=48, seed=0, vocab=12000, class_vocab=200)
+        test = synth_sparse(200, num_features=3000, nnz_mean=20, max_nnz=48, seed=1, vocab=12000, class_vocab=200)
+    else:
+        train, test = synth_finefood(1500, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
     eng = DistEngine(cfg, r, w, dev, train=train, test=test)
     out = eng.run()
     if r == 0:
@@ -114,3 +122,21 @@ def test_worker_cli_help():
     r = subprocess.run([sys.executable, "-m", "psx.apps.worker_app_runner", "--help"], cwd=ROOT, capture_output=True,
                        text=True, timeout=120, env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 0 and "WorkerAppRunner" in r.stdout and "-bc" in r.stdout
+
+
+def test_wide_bsp_schedules_agree():
+    """Sparse-input model over the collective schedules (dense delta pushes)."""
+    ws = {}
+    for sched in ("allreduce", "sharded"):
+        out, w = _run(3, dict(BASE, bsp_schedule=sched, _data="wide", max_buffer_size=256, min_buffer_size=64))
+        assert out["rounds"] == 5 and out["updates"] == 15
+        ws[sched] = w
+    assert w.numel() == 3000 * 8 + 8
+    assert torch.allclose(ws["allreduce"], ws["sharded"], atol=1e-5)
+
+
+@pytest.mark.parametrize("sparse_push", [True, False])
+def test_wide_async_push(sparse_push):
+    out, w = _run(3, dict(BASE, consistency_model=-1, max_iters=6, _data="wide", max_buffer_size=256,
+                          min_buffer_size=64, sparse_push=sparse_push))
+    assert out["updates"] == 12 and torch.isfinite(w).all()

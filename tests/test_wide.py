@@ -231,3 +231,59 @@ def test_gpu_sparse_ring_ingest(cuda):
     for s in range(64):
         k = int(rc.nnz[s])
         assert torch.equal(rc.idx[s, :k], rg.idx[s, :k].cpu())
+
+
+# ---------------------------------------------------------------------------
+# engines
+def _wide_cfg(N, c, device_iters=6, sigmoid=False):
+    from psx.runtime.config import PSConfig
+
+    return PSConfig(num_workers=N, consistency_model=c, producer_time_per_event=0, stream_mode="per_iter",
+                    rows_per_iter=64, epochs=50, max_iters=device_iters, min_buffer_size=64, max_buffer_size=256,
+                    init="random", sigmoid=sigmoid, solver=SolverOptions(zero_const=False))
+
+
+@pytest.mark.parametrize("c,N", [(0, 1), (0, 2), (-1, 2), (2, 3)])
+def test_engine_wide_cpu(c, N):
+    from psx.runtime.engine import LocalEngine
+
+    ds, spec = _problem(F=2000, rows=1200)
+    te, _ = _problem(F=2000, rows=300, seed=7)
+    eng = LocalEngine(_wide_cfg(N, c), "cpu", train=ds, test=te)
+    assert isinstance(eng.spec, WideSpec) and eng.spec.K == 6
+    out = eng.run()
+    assert out["updates"] >= 6 * N if c == 0 else out["updates"] >= 6
+    book = eng.log.book
+    assert book.server and book.worker
+    if c > 0:
+        assert out["max_vc_gap"] <= c
+
+
+def test_engine_wide_binary_cpu():
+    from psx.runtime.engine import LocalEngine
+
+    ds, _ = _problem(F=1500, rows=800, labels="binary")
+    te, _ = _problem(F=1500, rows=300, labels="binary", seed=3)
+    eng = LocalEngine(_wide_cfg(1, 0, 10, sigmoid=True), "cpu", train=ds, test=te)
+    out = eng.run()
+    assert eng.spec.K == 1 and out["rounds"] == 10
+    assert out["final_server_acc"] > 0.55  # planted signal is learnable
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,N", [(0, 1), (0, 2), (-1, 2)])
+def test_engine_wide_gpu(cuda, c, N):
+    from psx.runtime.engine import LocalEngine
+
+    ds, spec = _problem(F=2000, rows=1200)
+    te, _ = _problem(F=2000, rows=300, seed=7)
+    cfg = _wide_cfg(N, c, 8)
+    outs = {}
+    for dev in ("cpu", cuda):
+        eng = LocalEngine(_wide_cfg(N, c, 8), dev, train=ds, test=te)
+        outs[dev] = (eng.run(), eng.server.w.cpu())
+    if c == 0:  # BSP is deterministic up to float rounding
+        wc, wg = outs["cpu"][1], outs[cuda][1]
+        assert (wc - wg).abs().max().item() < 5e-3 * wc.abs().max().item()
+    assert outs[cuda][0]["server_rows"] >= 1
+    del cfg

@@ -225,6 +225,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              s.read_ctrl(&c, S(stream));
              return ctrl_dict(c, s.cfg().sc.hist);
            })
+      .def("read_stamps", [](WideSolver& s, uintptr_t stream) { return s.read_stamps(S(stream)); })
       .def_property_readonly("plmax", &WideSolver::plmax)
       .def_property_readonly("umax", [](const WideSolver& s) { return s.cfg().umax; })
       .def_property_readonly("map_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.map()); })

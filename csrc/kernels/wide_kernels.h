@@ -8,13 +8,19 @@
 // HashMap (ServerProcessor.java:148-151).  The MI355X design:
 //
 //  * the window of a worker touches only U << F features, so the local solve
-//    runs in that U-dimensional subspace: a remap pass gives every distinct
+//    runs in that U-dimensional subspace: a plan pass gives every distinct
 //    feature of the window a compact local id (wave-aggregated atomics), the
 //    old weights of those features are gathered once, and every L-BFGS vector
 //    (x, d, g, S_i, Y_i) is KP + U*KP floats instead of F*KP;
+//  * hashed text is Zipf-distributed: the few hottest features occur in most
+//    rows, and one global atomic per occurrence serialises on their cache
+//    lines.  The plan therefore groups the window's rows RB at a time and
+//    dedups each group's features in an LDS hash table once per solve; every
+//    later pass (feature sums, gradients) accumulates per group in LDS and
+//    issues ONE global atomic per (group, feature);
 //  * one wavefront per row: lanes gather the row's non-zeros, the K margins are
 //    reduced across the wave, softmax / cross-entropy in registers, and the
-//    same wave scatters the row's gradient with global float atomics
+//    same wave adds the row's gradient into its group's LDS accumulators
 //    (forward and backward fused, no residual round trip);
 //  * the line-search / L-BFGS control is the same on-device state machine as
 //    the dense solver (solver_ctrl.h), advanced by the last workgroup of the
@@ -68,7 +74,15 @@ struct WideDev {
   unsigned* cnt;       // [0] U, [1] dots ticket, [2] U of the previous solve, [3] unused
   int32_t* map;        // [F] local id or -1 (-2 transiently)
   int32_t* uniq;       // [umax] local id -> feature
-  int32_t* lid;        // [cap*NZ] window entry -> local id (-1 = padding)
+  int32_t* lid;        // [cap*NZ] window entry -> local id
+  // block plan (built once per solve): window rows are processed in groups of
+  // RB rows; every group dedups its entries' features in LDS so that hot
+  // features cost one global atomic per group instead of one per row
+  uint16_t* pslot;     // [cap*NZ] window entry -> distinct slot within its group
+  int32_t* bfeat;      // [ngroups][EB] distinct features of a group
+  int32_t* blid;       // [ngroups][EB] their local ids
+  int32_t* bcount;     // [ngroups] distinct features per group
+  int RB, EB, TS;      // rows per group, EB = RB*NZ, LDS hash size (pow2 >= 2*EB)
   float* s1;           // [umax] feature sums over the window
   float* s2;           // [umax] feature sums of squares
   float* scale;        // [umax] effective coefficient = scale * x
@@ -84,11 +98,16 @@ struct WideDev {
   float* loss;         // [1]
   int* stats;          // [4] evals, accepted steps, ls failures, direction resets
   float* delta_dense;  // [F*KP + KP] (dense_delta)
+  long long* dbg;      // [nslots][8] s_memrealtime stamps of the dots kernel (PSX_WIDE_STAMPS), or null
   unsigned* host_u;    // pinned host mirror of U (optional)
   int64_t PLmax;
 };
 
 constexpr int kWideND = 3 + 2 * kMaxHist;
+
+// Rows per group of the block plan for ring rows of NZ entries and KP classes
+// (LDS budgets: hash 8*TS + 4*EB bytes in the plan kernel, EB*KP*4 in fwdbwd).
+int wide_rows_per_group(int NZ, int KP);
 
 // Launchers (stream order; the solver captures them into one hipGraph).
 void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s);  // cleanup + params

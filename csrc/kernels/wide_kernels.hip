@@ -91,26 +91,72 @@ __global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int s
   for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256) d.map[d.uniq[i]] = -1;
 }
 
-// remap: every distinct feature of the window gets a compact id.  The first
-// entry to CAS map[f] from -1 wins; winners of a wave take consecutive ids
-// with ONE atomic per wave (ballot + popcount).
-__global__ __launch_bounds__(256) void wide_remap_kernel(WideDev d, int cap, int NZ) {
+// plan: per group of RB window rows, dedup the entries' features in an LDS
+// hash table (linear probing), give every entry its group slot, and give every
+// feature new to the window a compact id (first CAS on map[f] wins; winners of
+// a wave take consecutive ids with ONE atomic per wave).  A hot feature thus
+// costs one global CAS per group instead of one per row.
+__device__ __forceinline__ unsigned wide_hash(int f) { return (unsigned)f * 2654435761u; }
+
+__global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
+  extern __shared__ __attribute__((aligned(16))) int plan_lds[];
+  const int TS = d.TS, EB = d.EB, RB = d.RB, NZ = c.NZ, cap = c.cap;
+  int* keys = plan_lds;        // [TS]
+  int* sidx = keys + TS;       // [TS]
+  int* bf = sidx + TS;         // [EB]
+  __shared__ int nuq;
   const int B = d.prm->B, start = d.prm->start;
-  const int64_t E = (int64_t)B * NZ;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  const int lane = __lane_id();
-  for (int64_t base = (int64_t)blockIdx.x * 256; base < E; base += stride) {
-    const int64_t e = base + threadIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x, lane = __lane_id();
+  const int r0 = b * RB;
+  if (r0 >= B) return;
+  const int rows = min(RB, B - r0);
+  for (int h = t; h < TS; h += 256) keys[h] = -1;
+  if (t == 0) nuq = 0;
+  __syncthreads();
+  const int ne = rows * NZ;
+  for (int el = t; el < ne; el += 256) {
+    const int r = el / NZ, j = el - r * NZ;
+    int sl = start + r0 + r;
+    if (sl >= cap) sl -= cap;
+    if (j >= d.rnnz[sl]) continue;
+    const int f = d.ridx[(size_t)sl * NZ + j];
+    unsigned h = wide_hash(f) & (TS - 1);
+    while (true) {
+      const int old = atomicCAS(&keys[h], -1, f);
+      if (old == -1 || old == f) break;
+      h = (h + 1) & (TS - 1);
+    }
+  }
+  __syncthreads();
+  for (int h = t; h < TS; h += 256) {
+    const int k = keys[h];
+    if (k != -1) {
+      const int sidx_h = atomicAdd(&nuq, 1);
+      sidx[h] = sidx_h;
+      bf[sidx_h] = k;
+    }
+  }
+  __syncthreads();
+  const int n = nuq;
+  for (int el = t; el < ne; el += 256) {
+    const int r = el / NZ, j = el - r * NZ;
+    int sl = start + r0 + r;
+    if (sl >= cap) sl -= cap;
+    if (j >= d.rnnz[sl]) continue;
+    const int f = d.ridx[(size_t)sl * NZ + j];
+    unsigned h = wide_hash(f) & (TS - 1);
+    while (keys[h] != f) h = (h + 1) & (TS - 1);
+    d.pslot[(int64_t)(r0 + r) * NZ + j] = (uint16_t)sidx[h];
+  }
+  int32_t* gfeat = d.bfeat + (int64_t)b * EB;
+  for (int base = 0; base < n; base += 256) {  // uniform trip count: every lane reaches the ballot
+    const int si = base + t;
     bool win = false;
     int f = 0;
-    if (e < E) {
-      const int r = (int)(e / NZ), j = (int)(e - (int64_t)r * NZ);
-      int sl = start + r;
-      if (sl >= cap) sl -= cap;
-      if (j < d.rnnz[sl]) {
-        f = d.ridx[(size_t)sl * NZ + j];
-        win = atomicCAS(&d.map[f], -1, -2) == -1;
-      }
+    if (si < n) {
+      f = bf[si];
+      gfeat[si] = f;
+      win = atomicCAS(&d.map[f], -1, -2) == -1;
     }
     const unsigned long long mask = __ballot(win);
     if (mask) {
@@ -121,6 +167,7 @@ __global__ __launch_bounds__(256) void wide_remap_kernel(WideDev d, int cap, int
       if (win) d.uniq[b0 + __popcll(mask & ((1ull << lane) - 1ull))] = f;
     }
   }
+  if (t == 0) d.bcount[b] = n;
 }
 
 // assign: map[f] = id, gather the old weights of the window's features.
@@ -139,22 +186,50 @@ __global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) 
   if (blockIdx.x == 0 && threadIdx.x < KP) d.w0[threadIdx.x] = d.w_old[c.F * KP + threadIdx.x];
 }
 
-// lid: local id of every window entry (+ feature sums for the 1/std scaling).
-__global__ __launch_bounds__(256) void wide_lid_kernel(WideCfg c, WideDev d) {
-  const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap;
-  const int64_t E = (int64_t)B * NZ;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < E; e += (int64_t)gridDim.x * 256) {
-    const int r = (int)(e / NZ), j = (int)(e - (int64_t)r * NZ);
-    int sl = start + r;
+// stats: local ids of the group's features, every entry's local id, and the
+// feature sums for the 1/std scaling aggregated per group in LDS.
+__global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
+  extern __shared__ __attribute__((aligned(16))) int st_lds[];
+  const int EB = d.EB, RB = d.RB, NZ = c.NZ, cap = c.cap;
+  int* lid_s = st_lds;                  // [EB]
+  float* s1l = (float*)(lid_s + EB);    // [EB]
+  float* s2l = s1l + EB;                // [EB]
+  const int B = d.prm->B, start = d.prm->start;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int r0 = b * RB;
+  if (r0 >= B) return;
+  const int rows = min(RB, B - r0);
+  const int n = d.bcount[b];
+  const int32_t* gfeat = d.bfeat + (int64_t)b * EB;
+  int32_t* glid = d.blid + (int64_t)b * EB;
+  for (int si = t; si < n; si += 256) {
+    const int l = d.map[gfeat[si]];
+    lid_s[si] = l;
+    glid[si] = l;
+    s1l[si] = 0.f;
+    s2l[si] = 0.f;
+  }
+  __syncthreads();
+  const int ne = rows * NZ;
+  for (int el = t; el < ne; el += 256) {
+    const int r = el / NZ, j = el - r * NZ;
+    int sl = start + r0 + r;
     if (sl >= cap) sl -= cap;
     if (j >= d.rnnz[sl]) continue;
-    const int l = d.map[d.ridx[(size_t)sl * NZ + j]];
-    d.lid[e] = l;
+    const int64_t e = (int64_t)(r0 + r) * NZ + j;
+    const int ps = d.pslot[e];
+    d.lid[e] = lid_s[ps];
     if (c.standardize) {
       const float v = bf2f(d.rval[(size_t)sl * NZ + j]);
-      atomicAdd(&d.s1[l], v);
-      atomicAdd(&d.s2[l], v * v);
+      atomicAdd(&s1l[ps], v);
+      atomicAdd(&s2l[ps], v * v);
     }
+  }
+  if (!c.standardize) return;
+  __syncthreads();
+  for (int si = t; si < n; si += 256) {
+    atomicAdd(&d.s1[lid_s[si]], s1l[si]);
+    atomicAdd(&d.s2[lid_s[si]], s2l[si]);
   }
 }
 
@@ -205,44 +280,56 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
 }
 
 // ---------------------------------------------------------------------------
-// One function evaluation at x + t d: margins, softmax/CE, gradient scatter.
-// One wavefront per window row; 4 rows per workgroup pass.
+// One function evaluation at x + t d: margins, softmax/CE, gradient.  One
+// wavefront per window row, RB rows (one group of the plan) per workgroup; the
+// rows' gradient contributions are summed in LDS per distinct feature of the
+// group and flushed with one global atomic per (feature, class).
 template <int KP, int NQ>
-__global__ __launch_bounds__(256) void wide_fwdbwd_kernel(WideCfg c, WideDev d, int slot) {
+__global__ __launch_bounds__(512) void wide_fwdbwd_kernel(WideCfg c, WideDev d, int slot) {
+  extern __shared__ __attribute__((aligned(16))) float gacc[];  // [EB][KP]
   const Ctrl* ctrl = d.ctrl;
   if (ctrl->phase == kPhDone) return;
-  const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap, K = c.K;
+  const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap, K = c.K, RB = d.RB;
+  const int b = blockIdx.x;
+  const int r0 = b * RB;
+  if (r0 >= B) return;
   const float t = (float)ctrl->t;
   const float invB = 1.f / (float)B;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ float red_r[4][KP];
-  __shared__ double red_l[4];
-  float racc[KP];
-#pragma unroll
-  for (int k = 0; k < KP; ++k) racc[k] = 0.f;
-  double lacc = 0.0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nthr = blockDim.x;
+  __shared__ float red_r[8][KP];
+  __shared__ double red_l[8];
+  const int n = d.bcount[b];
+  for (int i = threadIdx.x; i < n * KP; i += nthr) gacc[i] = 0.f;
+  __syncthreads();
   const float* __restrict__ X = d.x;
   const float* __restrict__ D = d.d;
-  for (int r = blockIdx.x * 4 + wv; r < B; r += gridDim.x * 4) {
+  float rr[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) rr[k] = 0.f;
+  double lrow = 0.0;
+  const int r = r0 + wv;
+  if (wv < RB && r < B) {
     int sl = start + r;
     if (sl >= cap) sl -= cap;
     const int nnz = d.rnnz[sl];
-    const int32_t* __restrict__ ids = d.lid + (int64_t)r * NZ;
+    const int64_t e0 = (int64_t)r * NZ;
     const uint16_t* __restrict__ vals = d.rval + (int64_t)sl * NZ;
     float z[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) z[k] = 0.f;
-    int lq[NQ];
+    int lq[NQ], pq[NQ];
     float vq[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int j = lane + 64 * q;
       lq[q] = -1;
+      pq[q] = 0;
       vq[q] = 0.f;
       if (j < nnz) {
-        const int l = ids[j];
+        const int l = d.lid[e0 + j];
         const float v = bf2f(vals[j]);
         lq[q] = l;
+        pq[q] = d.pslot[e0 + j];
         vq[q] = v;
         const float sv = v * d.scale[l];
         float xv[KP], dv[KP];
@@ -261,37 +348,43 @@ __global__ __launch_bounds__(256) void wide_fwdbwd_kernel(WideCfg c, WideDev d, 
 #pragma unroll
       for (int k = 0; k < KP; ++k) z[k] += xb[k] + t * db[k];
     }
-    float rr[KP];
-    const float lrow = row_residual<KP>(z, K, d.ry[sl], invB, rr);
+    lrow = (double)row_residual<KP>(z, K, d.ry[sl], invB, rr);
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       if (lq[q] < 0) continue;
       const float g = vq[q] * d.gscale[lq[q]];
       if (g == 0.f) continue;
-      float* gp = d.g_t + KP + (int64_t)lq[q] * KP;
+      float* gp = gacc + pq[q] * KP;
 #pragma unroll
       for (int k = 0; k < KP; ++k)
         if (k < K) atomicAdd(gp + k, g * rr[k]);
     }
-#pragma unroll
-    for (int k = 0; k < KP; ++k) racc[k] += rr[k];
-    lacc += (double)lrow;
   }
-  if (lane == 0) {
+  if (lane == 0 && wv < 8) {
 #pragma unroll
-    for (int k = 0; k < KP; ++k) red_r[wv][k] = racc[k];
-    red_l[wv] = lacc;
+    for (int k = 0; k < KP; ++k) red_r[wv][k] = rr[k];
+    red_l[wv] = lrow;
   }
   __syncthreads();
+  const int nw = nthr >> 6;
   if (threadIdx.x < KP && threadIdx.x < K) {
-    const float s = red_r[0][threadIdx.x] + red_r[1][threadIdx.x] + red_r[2][threadIdx.x] + red_r[3][threadIdx.x];
-    if (s != 0.f) atomicAdd(d.g_t + threadIdx.x, s);
+    float sr = 0.f;
+    for (int w = 0; w < nw; ++w) sr += red_r[w][threadIdx.x];
+    if (sr != 0.f) atomicAdd(d.g_t + threadIdx.x, sr);
   }
   if (threadIdx.x == 0) {
-    const double s = red_l[0] + red_l[1] + red_l[2] + red_l[3];
-    if (s != 0.0) atomicAdd(d.loss_acc + slot, s);
+    double sl = 0.0;
+    for (int w = 0; w < nw; ++w) sl += red_l[w];
+    if (sl != 0.0) atomicAdd(d.loss_acc + slot, sl);
+  }
+  const int32_t* glid = d.blid + (int64_t)b * d.EB;
+  for (int i = threadIdx.x; i < n * K; i += nthr) {
+    const int si = i / K, k = i - si * K;
+    const float v = gacc[si * KP + k];
+    if (v != 0.f) atomicAdd(d.g_t + KP + (int64_t)glid[si] * KP + k, v);
   }
 }
+
 
 // Dot products of the new gradient (ctrl dots layout, solver_ctrl.h) + the
 // controller step in the last-arriving workgroup.
@@ -302,10 +395,14 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
   __shared__ double dots[kWideND];
   __shared__ int last;
   __shared__ CtrlScratch ws;
+  __shared__ Ctrl ctrl_lds;
+  static_assert(sizeof(Ctrl) % 8 == 0, "Ctrl is copied as 64-bit words");
   const int H = c.sc.hist;
   const int m = ctrl->m;
   const unsigned U = d.cnt[0];
   const int64_t PL = c.KP + (int64_t)U * c.KP, PLmax = d.PLmax;
+  long long* stp = d.dbg ? d.dbg + slot * 8 : nullptr;
+  if (stp && blockIdx.x == 0 && threadIdx.x == 0) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
   double aS[kMaxHist], aY[kMaxHist];
 #pragma unroll
@@ -349,25 +446,58 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
     const int k = threadIdx.x;
     const bool used = k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m);
     const double s = used ? red[0][k] + red[1][k] + red[2][k] + red[3][k] : 0.0;
-    d.part[(int64_t)blockIdx.x * kWideND + k] = s;
+    // write-through hand-off: agent-scope stores, drained before the ticket,
+    // agent-scope loads by the last workgroup -- no L2 writeback fence
+    __hip_atomic_store((gu64w*)(d.part + (int64_t)blockIdx.x * kWideND + k), __builtin_bit_cast(unsigned long long, s),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __threadfence();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&d.cnt[1], 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&d.cnt[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  __threadfence();
-  if (threadIdx.x < nd) {
-    double s = 0.0;
-    for (int b = 0; b < (int)gridDim.x; ++b) s += ld_agent_f64(d.part + (int64_t)b * kWideND + threadIdx.x);
-    dots[threadIdx.x] = s;
+  if (stp && threadIdx.x == 0) stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
+  // thread b loads workgroup b's partials -- only the dots the controller
+  // reads (3 + 2m of them), all loads in flight together -- then one wave
+  // reduction per dot in a fixed order (deterministic)
+  double v[kWideND];
+#pragma unroll
+  for (int k = 0; k < kWideND; ++k) {
+    const bool used = k < nd && (k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m));
+    v[k] = (used && threadIdx.x < gridDim.x) ? ld_agent_f64(d.part + (int64_t)threadIdx.x * kWideND + k) : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kWideND; ++k) {
+    const bool used = k < nd && (k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m));
+    if (used) {  // uniform across the block
+      const double w = wave_sum(v[k]);
+      if (lane == 0) red[wv][k] = w;
+    }
   }
   __syncthreads();
+  if (threadIdx.x < nd) {
+    const int k = threadIdx.x;
+    const bool used = k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m);
+    dots[k] = used ? red[0][k] + red[1][k] + red[2][k] + red[3][k] : 0.0;
+  }
+  __syncthreads();
+  if (stp && threadIdx.x == 0) stp[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  constexpr int kCW = (int)(sizeof(Ctrl) / 8);
+  unsigned long long* cg = reinterpret_cast<unsigned long long*>(ctrl);
+  unsigned long long* cs = reinterpret_cast<unsigned long long*>(&ctrl_lds);
+  for (int i = threadIdx.x; i < kCW; i += 256) cs[i] = cg[i];
+  __syncthreads();
   if (threadIdx.x == 0) {
+    if (stp) stp[3] = (long long)__builtin_amdgcn_s_memrealtime();
     d.cnt[1] = 0u;
     const double f = ld_agent_f64(d.loss_acc + slot) / (double)d.prm->B;
-    ctrl_step(*ctrl, c.sc, f, dots, slot, ws);
+    ctrl_step(ctrl_lds, c.sc, f, dots, slot, ws);
+    if (stp) stp[4] = (long long)__builtin_amdgcn_s_memrealtime();
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kCW; i += 256) cg[i] = cs[i];
+  if (stp && threadIdx.x == 0) stp[5] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
 // Apply the controller's decision of `slot` to the local vectors; clears g_t
@@ -462,35 +592,45 @@ static int grid_for(int64_t n, int cap_blocks) {
   return (int)g;
 }
 
-int wide_dots_blocks(int64_t PLmax) { return grid_for(PLmax / 4, 256); }
+int wide_dots_blocks(int64_t PLmax) { return grid_for(PLmax / 4, 256); }  // <= 256: one partial per thread
 
 void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s) {
   wide_begin_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(d, B, start);
 }
 
+int wide_rows_per_group(int NZ, int KP) {
+  int rb = 8;
+  while (rb > 1 && (rb * NZ > 2048 || rb * NZ * KP * 4 > 64512)) --rb;  // + static LDS < 64 KiB
+  return rb;
+}
+
+static int ngroups(const WideCfg& c, const WideDev& d) { return (c.cap + d.RB - 1) / d.RB; }
+
 void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s) {
-  const int64_t E = (int64_t)c.cap * c.NZ;
-  wide_remap_kernel<<<grid_for(E, 2048), 256, 0, s>>>(d, c.cap, c.NZ);
+  const int G = ngroups(c, d);
+  wide_plan_kernel<<<G, 256, (size_t)(2 * d.TS + d.EB) * 4, s>>>(c, d);
   wide_assign_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(c, d);
-  wide_lid_kernel<<<grid_for(E, 2048), 256, 0, s>>>(c, d);
+  wide_stats_kernel<<<G, 256, (size_t)d.EB * 12, s>>>(c, d);
   wide_prep_kernel<<<grid_for(d.PLmax, 1024), 256, 0, s>>>(c, d);
 }
 
 template <int KP>
 static void launch_fwdbwd_kp(const WideCfg& c, const WideDev& d, int slot, int grid, hipStream_t s) {
   const int nq = (c.NZ + 63) / 64;
+  const int thr = 64 * d.RB;
+  const size_t lds = (size_t)d.EB * KP * 4;
   if (nq <= 1)
-    wide_fwdbwd_kernel<KP, 1><<<grid, 256, 0, s>>>(c, d, slot);
+    wide_fwdbwd_kernel<KP, 1><<<grid, thr, lds, s>>>(c, d, slot);
   else if (nq <= 2)
-    wide_fwdbwd_kernel<KP, 2><<<grid, 256, 0, s>>>(c, d, slot);
+    wide_fwdbwd_kernel<KP, 2><<<grid, thr, lds, s>>>(c, d, slot);
   else if (nq <= 4)
-    wide_fwdbwd_kernel<KP, 4><<<grid, 256, 0, s>>>(c, d, slot);
+    wide_fwdbwd_kernel<KP, 4><<<grid, thr, lds, s>>>(c, d, slot);
   else
-    wide_fwdbwd_kernel<KP, 8><<<grid, 256, 0, s>>>(c, d, slot);
+    wide_fwdbwd_kernel<KP, 8><<<grid, thr, lds, s>>>(c, d, slot);
 }
 
 void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dots, hipStream_t s) {
-  const int rows_grid = grid_for((int64_t)c.cap * 64, 2048);  // 4 rows per workgroup pass
+  const int rows_grid = ngroups(c, d);  // one workgroup per group of RB rows
   switch (c.KP) {
     case 1: launch_fwdbwd_kp<1>(c, d, slot, rows_grid, s); break;
     case 2: launch_fwdbwd_kp<2>(c, d, slot, rows_grid, s); break;

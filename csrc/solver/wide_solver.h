@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../kernels/wide_kernels.h"
 
 namespace psx {
@@ -45,6 +47,9 @@ class WideSolver {
   // U of the last finished run (pinned host mirror; valid after the stream synced).
   unsigned ucount_host() const { return host_u_ ? __atomic_load_n(host_u_, __ATOMIC_ACQUIRE) : 0u; }
   void read_ctrl(Ctrl* out, hipStream_t stream);
+  // dots-kernel phase stamps of the last solve (PSX_WIDE_STAMPS=1 at construction): [slot][8]
+  // s_memrealtime ticks (100 MHz): entry, last block in, dots reduced, ctrl loaded, ctrl stepped, ctrl stored
+  std::vector<long long> read_stamps(hipStream_t stream);
   size_t workspace_bytes() const { return ws_bytes_; }
   int kernels_per_solve() const { return 5 + 3 * cfg_.sc.nslots + 1; }
 

@@ -1,5 +1,6 @@
 #include "wide_solver.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -36,11 +37,19 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   };
   const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16);
   const size_t o_map = take((size_t)cfg.F * 4), o_lid = take((size_t)E * 4);
+  const int RB = wide_rows_per_group(cfg.NZ, KP), EB = RB * cfg.NZ;
+  int TS = 1;
+  while (TS < 2 * EB) TS <<= 1;
+  const int G = (cfg.cap + RB - 1) / RB;
+  const size_t o_pslot = take((size_t)E * 2), o_bfeat = take((size_t)G * EB * 4), o_blid = take((size_t)G * EB * 4),
+               o_bcount = take((size_t)G * 4);
   const size_t o_s1 = take(umax * 4), o_s2 = take(umax * 4), o_sc = take(umax * 4), o_gs = take(umax * 4);
   const size_t o_x = take(PLmax * 4), o_d = take(PLmax * 4), o_gt = take(PLmax * 4), o_gc = take(PLmax * 4),
                o_w0 = take(PLmax * 4);
   const size_t o_S = take(H * PLmax * 4), o_Y = take(H * PLmax * 4);
   const size_t o_part = take((size_t)nblk_dots_ * kWideND * 8), o_loss = take((size_t)cfg.sc.nslots * 8);
+  const bool stamps = std::getenv("PSX_WIDE_STAMPS") != nullptr;
+  const size_t o_dbg = stamps ? take((size_t)cfg.sc.nslots * 8 * 8) : 0;
   ws_bytes_ = off;
   hip_check(hipMalloc(&ws_, ws_bytes_), "hipMalloc(wide solver workspace)");
   hip_check(hipMemset(ws_, 0, ws_bytes_), "hipMemset(wide solver workspace)");
@@ -60,6 +69,13 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.map = reinterpret_cast<int32_t*>(b + o_map);
   dv_.uniq = buf.uniq;
   dv_.lid = reinterpret_cast<int32_t*>(b + o_lid);
+  dv_.pslot = reinterpret_cast<uint16_t*>(b + o_pslot);
+  dv_.bfeat = reinterpret_cast<int32_t*>(b + o_bfeat);
+  dv_.blid = reinterpret_cast<int32_t*>(b + o_blid);
+  dv_.bcount = reinterpret_cast<int32_t*>(b + o_bcount);
+  dv_.RB = RB;
+  dv_.EB = EB;
+  dv_.TS = TS;
   dv_.s1 = reinterpret_cast<float*>(b + o_s1);
   dv_.s2 = reinterpret_cast<float*>(b + o_s2);
   dv_.scale = reinterpret_cast<float*>(b + o_sc);
@@ -80,6 +96,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.stats = buf.stats;
   dv_.delta_dense = buf.delta_dense;
   dv_.host_u = host_u_;
+  dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
   dv_.PLmax = PLmax;
 
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -142,6 +159,16 @@ void WideSolver::run(int B, int start, hipStream_t stream) {
   } else {
     enqueue_body(stream, B, start);
   }
+}
+
+std::vector<long long> WideSolver::read_stamps(hipStream_t stream) {
+  std::vector<long long> v;
+  if (!dv_.dbg) return v;
+  v.resize((size_t)cfg_.sc.nslots * 8);
+  hip_check(hipMemcpyAsync(v.data(), dv_.dbg, v.size() * sizeof(long long), hipMemcpyDeviceToHost, stream),
+            "read stamps");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v;
 }
 
 void WideSolver::read_ctrl(Ctrl* out, hipStream_t stream) {

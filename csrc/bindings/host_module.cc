@@ -35,6 +35,9 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("clocks", &VectorClockTracker::clocks)
       .def("sent_flags", &VectorClockTracker::sent_flags)
       .def("restore", &VectorClockTracker::restore)
+      .def("retire", &VectorClockTracker::retire)
+      .def("is_live", &VectorClockTracker::is_live)
+      .def_property_readonly("num_live", &VectorClockTracker::num_live)
       .def_property_readonly("num_workers", &VectorClockTracker::num_workers)
       .def_property_readonly("consistency_model", &VectorClockTracker::consistency_model)
       .def_property_readonly("max_gap", &VectorClockTracker::max_gap);

@@ -36,6 +36,13 @@ class VectorClockTracker {
   // received() + releasable() + sent() for every released pair.
   std::vector<std::pair<int, int64_t>> on_delta(int k, int64_t v);
 
+  // Fault tolerance: drop a failed worker.  Its clock stops counting towards
+  // min/max, and workers it was holding back under BSP/SSP are released
+  // (returned, already marked sent).
+  std::vector<std::pair<int, int64_t>> retire(int k);
+  bool is_live(int k) const { return live_.at(k) != 0; }
+  int num_live() const;
+
   int64_t min_clock() const;
   int64_t max_clock() const;
   int64_t clock(int k) const { return vc_.at(k); }
@@ -54,6 +61,7 @@ class VectorClockTracker {
   int c_;
   std::vector<int64_t> vc_;
   std::vector<uint8_t> sent_;
+  std::vector<uint8_t> live_;
   int64_t max_gap_ = 0;
 };
 

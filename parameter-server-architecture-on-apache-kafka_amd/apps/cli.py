@@ -14,6 +14,7 @@ import sys
 
 from ..ops.lr import SolverOptions
 from ..runtime.config import PSConfig
+from ..runtime.faults import parse_worker_map
 
 
 class _Parser(argparse.ArgumentParser):
@@ -67,6 +68,15 @@ def server_parser() -> argparse.ArgumentParser:
                    help="keep w_old for zero-variance features instead of Spark's zeroing")
     g.add_argument("--server_lr", type=float, default=None, help="server step (default 1/num_workers)")
     g.add_argument("--init", default="zeros", choices=["zeros", "random"])
+    g.add_argument("--model", default="auto", choices=["auto", "dense", "wide"],
+                   help="dense: <= 2048 features (MFMA tiles); wide: sparse rows up to ~1e8 hashed features "
+                        "(LIBSVM input); auto: wide for .svm/.libsvm inputs or > 2048 features")
+    g.add_argument("--sigmoid", action="store_true", help="wide model: binary sigmoid (one logit, labels 0/1)")
+    g.add_argument("--ring_nz", type=int, default=0, help="wide model: non-zeros per buffered row (0 = from data)")
+    g.add_argument("--no_standardize", action="store_true",
+                   help="wide model: skip Spark's 1/std feature scaling over the buffer")
+    g.add_argument("--dense_push", action="store_true",
+                   help="wide model, -c != 0: push the dense delta instead of (feature ids, values)")
     g = ap.add_argument_group("run control")
     g.add_argument("--max_iters", type=int, default=0, help="iterations per worker (0 = until data exhausted)")
     g.add_argument("--max_wallclock_s", type=float, default=0.0)
@@ -82,6 +92,12 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--resume", action="store_true")
     g.add_argument("--inject_worker_delay", action="append", default=[], metavar="K:MS",
                    help="fault injection: worker K sleeps MS ms per iteration (straggler)")
+    g.add_argument("--inject_worker_crash", action="append", default=[], metavar="K:ITER",
+                   help="fault injection: worker K fails at its ITER-th iteration")
+    g.add_argument("--worker_timeout", type=float, default=600.0,
+                   help="watchdog: a worker busy and silent this many seconds has failed")
+    g.add_argument("--on_worker_failure", default="auto", choices=["auto", "drop", "fail"],
+                   help="drop the failed worker and continue, or abort (auto: drop under -c -1)")
     return ap
 
 
@@ -110,11 +126,7 @@ def parse_or_exit(ap: argparse.ArgumentParser, argv):
 
 
 def parse_delays(items) -> dict:
-    out = {}
-    for it in items:
-        k, ms = it.split(":")
-        out[int(k)] = float(ms)
-    return out
+    return parse_worker_map(items)
 
 
 def server_config(a) -> PSConfig:
@@ -124,7 +136,8 @@ def server_config(a) -> PSConfig:
               file=sys.stderr)
         sys.exit(2)
     solver = SolverOptions(iters=a.local_iters, hist=a.lbfgs_history, ls_max=a.ls_max, mode=a.local_solver,
-                           gd_lr=a.gd_lr, center=not a.no_center, zero_const=not a.keep_constant_features)
+                           gd_lr=a.gd_lr, center=not a.no_center, zero_const=not a.keep_constant_features,
+                           standardize=not a.no_standardize)
     return PSConfig(
         train_path=a.training_data_file_path, test_path=a.test_data_file_path, header=a.header,
         label_col=a.label_col, num_features=a.num_features, num_classes=a.num_classes,
@@ -134,7 +147,10 @@ def server_config(a) -> PSConfig:
         solver=solver, max_iters=a.max_iters, max_wallclock_s=a.max_wallclock_s, idle_exit_s=a.idle_exit_s,
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
-        resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace)
+        resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
+        model=a.model, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
+        inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
+        worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)
 
 
 def print_params(title: str, items: dict):

@@ -8,6 +8,7 @@ as the solver -- the oracle the GPU path is tested against.
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -256,7 +257,9 @@ class WideEvalSet:
         s = self.spec
         if self._csr is None:
             ds = self.ds
-            self._csr = torch.sparse_csr_tensor(ds.indptr, ds.idx.long(), ds.val.float(), size=(ds.rows, s.F))
+            with warnings.catch_warnings():  # "sparse CSR support is in beta"
+                warnings.simplefilter("ignore", UserWarning)
+                self._csr = torch.sparse_csr_tensor(ds.indptr, ds.idx.long(), ds.val.float(), size=(ds.rows, s.F))
         W = w[: s.F * s.KP].view(s.F, s.KP).float()
         return (self._csr @ W) + w[s.F * s.KP:].float()
 

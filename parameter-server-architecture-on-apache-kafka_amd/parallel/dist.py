@@ -44,13 +44,14 @@ from ..models.logreg import ModelSpec
 from ..ops.lr import is_gpu
 from ..runtime.config import PSConfig
 from ..runtime.engine import load_datasets
+from ..runtime.faults import WorkerFailure, drop_on_failure
 from ..ops.sparse import SparseDelta, nz_capacity
 from ..runtime.roles import ServerRole, WorkerRole, is_wide, make_evalset
-from ..utils.checkpoint import maybe_checkpoint, maybe_resume
+from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
 
-KIND_DELTA, KIND_FINAL = 0, 1
+KIND_DELTA, KIND_FINAL, KIND_ERROR = 0, 1, 2
 
 
 def init_from_env(cpu: bool = False):
@@ -126,8 +127,6 @@ class DistEngine:
         # every rank keeps a server replica in the allreduce schedule; otherwise only rank 0
         replicated = (not self.async_mode) and cfg.bsp_schedule in ("allreduce", "sharded")
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0) if (self.is_server or replicated) else None
-        if self.server is not None and self.is_server:
-            maybe_resume(cfg, self.server)
         self.t0 = time.time()
         self.worker = None
         if self.is_worker:
@@ -136,6 +135,20 @@ class DistEngine:
         self.rounds = 0
         self._ctrl = None
         self._next_vc = 0
+        # resume: rank 0 restores the server, every worker rank its own worker file;
+        # BSP continues at the server's round (agreed over a collective)
+        resumed = maybe_resume(cfg, self.server if self.is_server else None,
+                               [self.worker] if self.worker is not None else [])
+        if resumed and self.server is not None and self.is_server:
+            self.rounds = int(self.server.tracker.min_clock())
+        if cfg.resume and cfg.checkpoint_dir and not self.async_mode:
+            t = torch.tensor([self.rounds], dtype=torch.int64, device=self.device)
+            dist.broadcast(t, src=0)
+            self.rounds = int(t.item())
+            if self.worker is not None:
+                self._next_vc = self.rounds
+        elif resumed and self.worker is not None:
+            self._next_vc = self.worker.vc + 1
 
     # ------------------------------------------------------------------
     def run(self) -> dict:
@@ -143,6 +156,7 @@ class DistEngine:
             out = self._run_async()
         else:
             out = self._run_bsp()
+        flush_checkpoints(self.cfg)
         if self.log is not None:
             self.log.close()
             if self.log.book is not None:
@@ -248,12 +262,13 @@ class DistEngine:
                         srv.log_eval(r, self.log)
                     for k in range(N):
                         srv.tracker.sent(k, r + 1)
-                    maybe_checkpoint(cfg, srv, r + 1)
                 srv.updates += N
             if wk is not None:
                 if new_w is not wk.w:
                     wk.w.copy_(new_w)
                 wk.vc = r + 1
+            # every rank writes its own worker file at the same round; rank 0 also the server
+            maybe_checkpoint(cfg, srv if self.rank == 0 else None, r + 1, [wk] if wk is not None else [])
             r += 1
             if self.log is not None:
                 self.log.drain()
@@ -299,11 +314,33 @@ class DistEngine:
                 srv.tracker.sent(j, srv.tracker.clock(j))
             dist.send(srv.w, dst=j + 1)
         finished = set()
+        failed = set()
         t_start = time.time()
+        busy_since = {j: t_start for j in range(N)}  # weights sent, delta not back yet (watchdog)
+
+        def fail(k: int, reason: str):
+            if not drop_on_failure(cfg):
+                raise WorkerFailure(k, reason)
+            print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
+            failed.add(k)
+            finished.add(k)
+            busy_since.pop(k, None)
+            for j, u in srv.tracker.retire(k):
+                if j not in finished:
+                    dist.send(srv.w, dst=j + 1)
+                    busy_since[j] = time.time()
+
         while len(finished) < N:
-            tok = self._ctrl.pop(600.0)
+            tok = self._ctrl.pop(min(1.0, cfg.worker_timeout_s))
             if tok is None:
-                raise TimeoutError("server: no worker token for 600 s (worker died?)")
+                now = time.time()
+                for j, since in list(busy_since.items()):
+                    if j not in finished and now - since > cfg.worker_timeout_s:
+                        fail(j, f"silent for {now - since:.0f} s while busy (watchdog)")
+                continue
+            if tok.kind == KIND_ERROR:
+                fail(int(tok.worker), "reported an error")
+                continue
             k, v = int(tok.worker), int(tok.vc)
             with self.tracer.span("recv", worker=k, vc=v):
                 if self.sparse_push:
@@ -315,7 +352,10 @@ class DistEngine:
                 else:
                     dist.recv(buf, src=k + 1)
                     delta = buf
-            if k == 0:  # server eval rows follow worker-0 deltas (ServerProcessor.java:154-165)
+            busy_since.pop(k, None)
+            # server eval rows follow the deltas of worker 0 (ServerProcessor.java:154-165),
+            # or of the lowest surviving worker once 0 has failed
+            if k == min(j for j in range(N) if j not in failed):
                 srv.apply_and_log(delta, v, self.log)
             else:
                 srv.apply(delta)
@@ -326,6 +366,7 @@ class DistEngine:
                 if j in finished:
                     continue
                 dist.send(srv.w, dst=j + 1)
+                busy_since[j] = time.time()
             maybe_checkpoint(cfg, srv, srv.updates)
             if self.log is not None:
                 self.log.drain()
@@ -333,7 +374,8 @@ class DistEngine:
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
-                "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap)}
+                "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
+                "failed_workers": sorted(failed)}
 
     def _worker_loop(self) -> dict:
         cfg, wk = self.cfg, self.worker
@@ -349,7 +391,13 @@ class DistEngine:
             while not wk.ready():
                 time.sleep(0.001)
                 wk.ingest()
-            delta = wk.compute(self.log)
+            try:
+                delta = wk.compute(self.log)
+            except WorkerFailure as e:  # report, then leave the protocol (the server retires or aborts)
+                tok.kind, tok.vc, tok.n = KIND_ERROR, wk.vc, 0
+                self._ctrl.push(tok, 600.0)
+                print(f"psx worker {wk.k}: {e}", flush=True)
+                return {"rounds": it, "updates": it, "failed": True}
             it += 1
             final = it >= max_iters or (cfg.max_wallclock_s and time.time() - t_start >= cfg.max_wallclock_s) or (
                 not cfg.max_iters and not cfg.max_wallclock_s and wk.source.exhausted)

@@ -25,10 +25,11 @@ from ..models.logreg import ModelSpec
 from ..models.wide import WideSpec
 from ..ops.lr import is_gpu
 from ..utils import data as data_mod
-from ..utils.checkpoint import maybe_checkpoint, maybe_resume
+from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
 from .config import PSConfig
+from .faults import WorkerFailure, drop_on_failure
 from .roles import ServerRole, WorkerRole, make_evalset
 
 
@@ -99,7 +100,10 @@ class LocalEngine:
         self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
                         for k in range(cfg.num_workers)]
         self.rounds = 0
-        maybe_resume(cfg, self.server)
+        self.failed: set[int] = set()
+        if maybe_resume(cfg, self.server, self.workers):
+            self.rounds = int(self.server.tracker.min_clock())
+            self.failed = {k for k in range(cfg.num_workers) if not self.server.tracker.is_live(k)}
 
     # ------------------------------------------------------------------
     def _stop(self, iters_done: int, t_start: float, exhausted_since: float | None) -> bool:
@@ -117,28 +121,41 @@ class LocalEngine:
             out = self._run_bsp()
         else:
             out = self._run_async()
+        flush_checkpoints(self.cfg)
         self.log.close()
         self.tracer.close()
         if self.log.book is not None:
             out.update(summarize(self.log.book))
         out["max_vc_gap"] = int(self.server.tracker.max_gap)
+        out["failed_workers"] = sorted(self.failed)
         return out
+
+    def _worker_failed(self, e: Exception, k: int):
+        """Policy on a failed worker: retire it (drop) or abort the run (fail)."""
+        if not drop_on_failure(self.cfg):
+            raise e if isinstance(e, WorkerFailure) else WorkerFailure(k, repr(e))
+        self.failed.add(k)
+        released = self.server.tracker.retire(k)
+        print(f"psx: worker {k} failed ({e}); continuing with {self.server.tracker.num_live} workers", flush=True)
+        return released
 
     # ------------------------------------------------------------------
     def _run_bsp(self) -> dict:
-        cfg, srv, W = self.cfg, self.server, self.workers
-        N = len(W)
+        cfg, srv = self.cfg, self.server
         # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87).  Under BSP every
         # worker pulls the same version right after the server update, and all
         # solves of a round finish (stream order) before the update, so the
         # workers' pulled copy IS the server tensor: no per-round copies.
-        for w in W:
+        for w in self.workers:
             w.w = srv.w
-            w.vc = 0
+            w.vc = self.rounds
         t_start = time.time()
         exhausted_since = None
         r = self.rounds
         while not self._stop(r - self.rounds, t_start, exhausted_since):
+            W = [w for w in self.workers if w.k not in self.failed]
+            if not W:
+                break
             with self.tracer.span("ingest"):
                 for w in W:
                     w.ingest()
@@ -147,18 +164,26 @@ class LocalEngine:
             if not all(w.ready() for w in W):
                 time.sleep(0.001)
                 continue
+            deltas, done = [], []
             with self.tracer.span("solve"):
-                deltas = [w.compute(self.log) for w in W]
+                for w in W:
+                    try:
+                        deltas.append(w.compute(self.log))
+                        done.append(w)
+                    except WorkerFailure as e:
+                        self._worker_failed(e, w.k)
+            if not deltas:
+                break
             with self.tracer.span("server"):
                 srv.apply_round(deltas, r, self.log)  # w += lr*sum(deltas), then the server eval row
-                for k in range(N):
-                    srv.tracker.received(k, r)
-                srv.updates += N
-                for k, w in enumerate(W):
-                    srv.tracker.sent(k, r + 1)
+                for w in done:
+                    srv.tracker.received(w.k, r)
+                srv.updates += len(done)
+                for w in done:
+                    srv.tracker.sent(w.k, r + 1)
                     w.vc = r + 1
             r += 1
-            maybe_checkpoint(cfg, srv, r)
+            maybe_checkpoint(cfg, srv, r, W)
             self.log.drain()
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
@@ -206,7 +231,11 @@ class LocalEngine:
                                 return
                             time.sleep(0.001)
                             w.ingest()
-                        delta = w.compute(locked)
+                        try:
+                            delta = w.compute(locked)
+                        except WorkerFailure as e:
+                            to_server.put(("fail", w.k, e))
+                            return
                         ev2 = None
                         if gpu:
                             ev2 = torch.cuda.Event()
@@ -228,7 +257,8 @@ class LocalEngine:
                 ev.record(torch.cuda.current_stream(self.device))
             inbox[j].put((u, ev))
 
-        for j in range(len(W)):  # bootstrap: vc 0 to everybody, tracker untouched
+        alive = {w.k for w in W if w.k not in self.failed}
+        for j in sorted(alive):  # bootstrap: vc 0 to everybody, tracker untouched
             u = int(srv.tracker.clock(j))
             if u > 0:  # a later run of this engine resumes at the tracked clocks
                 srv.tracker.sent(j, u)
@@ -236,11 +266,11 @@ class LocalEngine:
         t_start = time.time()
         exhausted = set()
         exhausted_since = None
-        per_worker = [0] * len(W)
-        while True:
+        per_worker = {k: 0 for k in alive}
+        while alive:
             if errors:
                 break
-            done_iters = min(per_worker)
+            done_iters = min(per_worker[k] for k in alive)
             if self._stop(done_iters, t_start, exhausted_since):
                 break
             try:
@@ -249,15 +279,24 @@ class LocalEngine:
                 continue
             if tok is None:
                 break
+            if tok[0] == "fail":
+                _, k, e = tok
+                with log_lock:
+                    for j, u in self._worker_failed(e, k):
+                        send(j, u)
+                alive.discard(k)
+                continue
             k, v, delta, ev, ex = tok
             if ex:
                 exhausted.add(k)
-                if len(exhausted) == len(W):
+                if alive <= exhausted:
                     exhausted_since = exhausted_since or time.time()
             if ev is not None:
                 torch.cuda.current_stream(self.device).wait_event(ev)
             with log_lock:
-                if k == 0:  # server eval rows follow worker-0 deltas (ServerProcessor.java:154-165)
+                # server eval rows follow the deltas of worker 0 (ServerProcessor.java:154-165),
+                # or of the lowest surviving worker once 0 has failed
+                if k == min(alive):
                     srv.apply_and_log(delta, v, self.log)
                 else:
                     srv.apply(delta)

@@ -22,6 +22,7 @@ from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, serv
 from ..ops.sparse import SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide_server_apply
 from .buffer import DeviceRing, StreamSource
 from .config import PSConfig
+from .faults import WorkerFailure
 
 
 def is_wide(spec) -> bool:
@@ -62,6 +63,8 @@ class WorkerRole:
         self.vc = 0  # version of the weights currently held
         self.iters = 0
         self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
+        crash = cfg.inject_worker_crash.get(k)
+        self.crash_at = int(crash) if crash is not None else None
 
     @property
     def tuples_seen(self) -> int:
@@ -80,6 +83,8 @@ class WorkerRole:
         (LogisticRegressionTaskSpark.java:186), logged with the weights version
         it trained from and numTuplesSeen = the newest insertion id.
         """
+        if self.crash_at is not None and self.iters >= self.crash_at:
+            raise WorkerFailure(self.k, f"injected crash at iteration {self.iters}")
         if self.delay_s > 0:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)

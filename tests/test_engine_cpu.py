@@ -91,3 +91,40 @@ def test_fault_injection_delay_slows_only_that_worker():
     eng = LocalEngine(cfg, "cpu", train=train, test=test)
     eng.run()
     assert eng.workers[0].iters > eng.workers[1].iters
+
+
+def test_checkpoint_resume_is_exact(tmp_path):
+    """6 BSP rounds straight == 3 rounds, checkpoint (server + worker rings/cursors), resume, 3 rounds."""
+    train, test = synth_finefood(3000, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
+
+    def cfg(**kw):
+        return PSConfig(num_workers=2, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                        rows_per_iter=48, epochs=10, min_buffer_size=100, max_buffer_size=100, init="random",
+                        **kw)
+
+    ref = LocalEngine(cfg(max_iters=6), "cpu", train=train, test=test)
+    ref.run()
+    a = LocalEngine(cfg(max_iters=3, checkpoint_dir=str(tmp_path), checkpoint_every=3), "cpu", train=train,
+                    test=test)
+    a.run()
+    assert (tmp_path / "server.ckpt").exists() and (tmp_path / "worker1.ckpt").exists()
+    b = LocalEngine(cfg(max_iters=3, checkpoint_dir=str(tmp_path), resume=True), "cpu", train=train, test=test)
+    assert b.rounds == 3 and b.workers[1].source.next_local == a.workers[1].source.next_local
+    b.run()
+    assert torch.allclose(b.server.w, ref.server.w, atol=1e-6), (b.server.w - ref.server.w).abs().max()
+    st = load_server(str(tmp_path))
+    assert st["model"] == "dense" and st["w_reference_layout"].numel() == 6 * 128 + 6
+
+
+def test_checkpoint_wide_model(tmp_path):
+    from psx.utils.data import synth_sparse
+
+    tr = synth_sparse(800, num_features=5000, nnz_mean=20, max_nnz=48, seed=0)
+    te = synth_sparse(100, num_features=5000, nnz_mean=20, max_nnz=48, seed=1)
+    c = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                 rows_per_iter=64, epochs=5, max_iters=4, min_buffer_size=64, max_buffer_size=128, init="random",
+                 checkpoint_dir=str(tmp_path), checkpoint_every=2)
+    eng = LocalEngine(c, "cpu", train=tr, test=te)
+    eng.run()
+    st = load_server(str(tmp_path))
+    assert st["model"] == "wide" and torch.equal(st["w"], eng.server.w) and "w_reference_layout" not in st

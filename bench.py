@@ -190,6 +190,7 @@ def main(argv=None):
     # timed region: exactly `steps` rounds, synchronised on both sides
     eng.cfg.max_iters = a.steps
     eng.log = _fresh_log(eng)
+    u0 = eng.server.updates  # the server's counter includes the warmup rounds
     if device != "cpu":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -197,7 +198,7 @@ def main(argv=None):
     if device != "cpu":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ups = out["updates"] / dt
+    ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res["accuracy_vs_wallclock"] = _curve(eng.log.book.server, t0)
     print(json.dumps(res))

@@ -38,7 +38,9 @@ def _common(ap: argparse.ArgumentParser):
     ap.add_argument("--device", default=None, help="cpu | cuda | cuda:N (default: cuda if available)")
     ap.add_argument("--log_dir", default=".")
     ap.add_argument("--master_port", type=int, default=None, help="rendezvous port (default $MASTER_PORT or 29500)")
-    ap.add_argument("--trace", default=None, help="write a Chrome trace of host phases to this path")
+    ap.add_argument("--trace", default=None, help="write a Chrome trace of host + device phases to this path")
+    ap.add_argument("--perf_log", action="store_true",
+                    help="write logs-perf.csv (per-round device phase times, updates/s) next to the CSV logs")
     ap.add_argument("--seed", type=int, default=0)
 
 
@@ -148,6 +150,7 @@ def server_config(a) -> PSConfig:
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
+        perf_log=a.perf_log,
         model=a.model, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)

@@ -122,7 +122,8 @@ class DistEngine:
         # every rank evaluates (workers log their local model each iteration, as the
         # reference does); only files requested with -l are written
         self.log = LogSink(self.spec.eval_classes, self.device, wp, sp, keep_records=(rank == 0), worker_append=append)
-        self.tracer = Tracer(cfg.trace_path.replace(".json", f".rank{rank}.json") if cfg.trace_path else None, rank)
+        self.tracer = Tracer(cfg.trace_path.replace(".json", f".rank{rank}.json") if cfg.trace_path else None, rank,
+                             self.device, f"{cfg.log_dir}/logs-perf.rank{rank}.csv" if cfg.perf_log else None)
         w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         # every rank keeps a server replica in the allreduce schedule; otherwise only rank 0
         replicated = (not self.async_mode) and cfg.bsp_schedule in ("allreduce", "sharded")
@@ -220,6 +221,7 @@ class DistEngine:
                 break
             if check_every and self._agree_stop(r - self.rounds, t_start):
                 break
+            self.tracer.round_begin()
             with self.tracer.span("ingest"):
                 if wk is not None:
                     wk.ingest()
@@ -269,6 +271,7 @@ class DistEngine:
                 wk.vc = r + 1
             # every rank writes its own worker file at the same round; rank 0 also the server
             maybe_checkpoint(cfg, srv if self.rank == 0 else None, r + 1, [wk] if wk is not None else [])
+            self.tracer.round_end(r, (r + 1 - self.rounds) * N)
             r += 1
             if self.log is not None:
                 self.log.drain()

@@ -93,7 +93,8 @@ class LocalEngine:
             sp = f"{cfg.log_dir}/logs-server.csv" if cfg.logging else None
             log = LogSink(self.spec.eval_classes, self.device, wp, sp, to_stdout=not cfg.logging and cfg.verbose)
         self.log = log
-        self.tracer = Tracer(cfg.trace_path)
+        self.tracer = Tracer(cfg.trace_path, 0, self.device,
+                             f"{cfg.log_dir}/logs-perf.csv" if cfg.perf_log else None)
         w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0)
         self.t0 = time.time()
@@ -152,10 +153,12 @@ class LocalEngine:
         t_start = time.time()
         exhausted_since = None
         r = self.rounds
+        u_start = srv.updates
         while not self._stop(r - self.rounds, t_start, exhausted_since):
             W = [w for w in self.workers if w.k not in self.failed]
             if not W:
                 break
+            self.tracer.round_begin()
             with self.tracer.span("ingest"):
                 for w in W:
                     w.ingest()
@@ -182,6 +185,7 @@ class LocalEngine:
                 for w in done:
                     srv.tracker.sent(w.k, r + 1)
                     w.vc = r + 1
+            self.tracer.round_end(r, srv.updates - u_start)
             r += 1
             maybe_checkpoint(cfg, srv, r, W)
             self.log.drain()

@@ -49,3 +49,41 @@ def test_gd_solver_mode(cuda):
     out = eng.run()
     assert out["rounds"] == 10
     torch.cuda.synchronize()
+
+
+def test_perf_log_device_phases(cuda, tmp_path):
+    import json
+
+    train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
+    eng = LocalEngine(_cfg(max_iters=12, log_dir=str(tmp_path), perf_log=True, trace_path=str(tmp_path / "t.json")),
+                      cuda, train=train, test=test)
+    eng.run()
+    rows = [r.split(";") for r in (tmp_path / "logs-perf.csv").read_text().strip().split("\n")[1:]]
+    assert len(rows) == 12
+    solve_us = [float(r[4]) for r in rows]
+    assert all(5.0 < s < 50000.0 for s in solve_us), solve_us  # device time of the local solve
+    ev = json.loads((tmp_path / "t.json").read_text())["traceEvents"]
+    assert any(e.get("tid") == "device" and e["name"] == "solve" for e in ev)
+
+
+def test_inprocess_checkpoint_resume_gpu(cuda, tmp_path):
+    train, test = synth_finefood(6000, seed=0), synth_finefood(500, seed=1)
+    kw = dict(num_workers=2, min_buffer_size=256, max_buffer_size=256, init="random")
+    ref = LocalEngine(_cfg(max_iters=6, **kw), cuda, train=train, test=test)
+    ref.run()
+    a = LocalEngine(_cfg(max_iters=3, checkpoint_dir=str(tmp_path), checkpoint_every=3, **kw), cuda, train=train,
+                    test=test)
+    a.run()
+    b = LocalEngine(_cfg(max_iters=3, checkpoint_dir=str(tmp_path), resume=True, **kw), cuda, train=train, test=test)
+    b.run()
+    torch.cuda.synchronize()
+    d = (b.server.w - ref.server.w).abs().max().item()
+    assert d < 1e-4 * max(1.0, ref.server.w.abs().max().item()), d
+
+
+def test_asp_crash_dropped_gpu(cuda):
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    eng = LocalEngine(_cfg(num_workers=3, consistency_model=-1, max_iters=10, inject_worker_crash={2: 4}), cuda,
+                      train=train, test=test)
+    out = eng.run()
+    assert out["failed_workers"] == [2] and eng.workers[0].iters >= 10

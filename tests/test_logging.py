@@ -142,3 +142,22 @@ def test_plot_logs_reads_reference_logs(tmp_path):
     assert plot_logs.max_vc_gap(w2) == 11
     assert plot_logs.main([ref + "sequential_", "--out", str(tmp_path), "--names", "seq"]) == 0
     assert (tmp_path / "seq_accuracy.png").exists() and (tmp_path / "seq_consistency.png").exists()
+
+
+def test_perf_log_and_trace(tmp_path):
+    import json
+
+    from psx.runtime.config import PSConfig
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    tr, te = synth_finefood(600, num_features=128, seed=0), synth_finefood(100, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=2, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=32, epochs=5, max_iters=5, min_buffer_size=32, max_buffer_size=64,
+                   log_dir=str(tmp_path), perf_log=True, trace_path=str(tmp_path / "t.json"))
+    LocalEngine(cfg, "cpu", train=tr, test=te).run()
+    rows = (tmp_path / "logs-perf.csv").read_text().strip().split("\n")
+    assert rows[0].startswith("round;timestamp;host_round_us") and len(rows) == 6
+    assert [int(r.split(";")[0]) for r in rows[1:]] == [0, 1, 2, 3, 4]
+    ev = json.loads((tmp_path / "t.json").read_text())["traceEvents"]
+    assert {"ingest", "solve", "server"} <= {e["name"] for e in ev}

@@ -36,6 +36,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("sent_flags", &VectorClockTracker::sent_flags)
       .def("restore", &VectorClockTracker::restore)
       .def("retire", &VectorClockTracker::retire)
+      .def("bsp_round", &VectorClockTracker::bsp_round)
       .def("is_live", &VectorClockTracker::is_live)
       .def_property_readonly("num_live", &VectorClockTracker::num_live)
       .def_property_readonly("num_workers", &VectorClockTracker::num_workers)

@@ -98,6 +98,13 @@ std::vector<std::pair<int, int64_t>> VectorClockTracker::on_delta(int k, int64_t
   return rel;
 }
 
+void VectorClockTracker::bsp_round(int64_t v) {
+  for (int k = 0; k < num_workers(); ++k)
+    if (live_[k]) received(k, v);
+  for (int k = 0; k < num_workers(); ++k)
+    if (live_[k]) sent(k, v + 1);
+}
+
 void VectorClockTracker::restore(const std::vector<int64_t>& vc, const std::vector<uint8_t>& sent) {
   if (vc.size() != vc_.size() || sent.size() != sent_.size())
     throw std::invalid_argument("tracker restore: worker count mismatch");

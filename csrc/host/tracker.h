@@ -33,6 +33,10 @@ class VectorClockTracker {
   // delta (k, v) has been applied.  Does not mutate; call sent() per pair.
   std::vector<std::pair<int, int64_t>> releasable(int k, int64_t v) const;
 
+  // A whole BSP round in one call: every live worker's delta of version v has
+  // been applied and every live worker receives version v + 1.
+  void bsp_round(int64_t v);
+
   // received() + releasable() + sent() for every released pair.
   std::vector<std::pair<int, int64_t>> on_delta(int k, int64_t v);
 

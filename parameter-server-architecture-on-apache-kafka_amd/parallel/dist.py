@@ -189,8 +189,14 @@ class DistEngine:
         srv, wk = self.server, self.worker
         P = spec.P
         zeros = torch.zeros(P, dtype=torch.float32, device=self.device)
-        if wk is not None:
-            wk.w.copy_(srv.w if srv is not None else zeros)
+        if wk is not None and srv is not None and wk.w is not srv.w:
+            # colocated server replica: the worker's pulled weights ARE the replica
+            # (BSP: every solve of a round precedes the update in stream order)
+            wk.w = srv.w
+            if getattr(wk.solver, "_bound", None) is not None:
+                wk.solver._bound = None
+        if wk is not None and srv is None:
+            wk.w.zero_()
         # bootstrap pull (vc 0): everybody starts from rank 0's weights
         boot = srv.w if srv is not None else (wk.w if wk is not None else zeros)
         dist.broadcast(boot, src=0)
@@ -207,10 +213,7 @@ class DistEngine:
             time.sleep(0.001)
         shard = (P + self.world - 1) // self.world
         if sched == "sharded":
-            pad = torch.zeros(shard * self.world, dtype=torch.float32, device=self.device)
-            wfull = torch.zeros(shard * self.world, dtype=torch.float32, device=self.device)
-            wfull[:P].copy_(srv.w)
-            myd = torch.zeros(shard, dtype=torch.float32, device=self.device)
+            wfull, pad, myd = self._sharded_buffers(shard)
         N = cfg.num_workers
         lr = cfg.lr
         t_start = time.time()
@@ -246,24 +249,23 @@ class DistEngine:
                     else:
                         new_w = wk.w
                     dist.broadcast(new_w, src=0)
-                else:  # sharded
-                    pad[:P].copy_(delta)
+                else:  # sharded: key-range shards of the master weights (KeyRange.java:11-49)
+                    srv.side.fence()  # srv.w / fragments are rewritten below
+                    if delta.data_ptr() != pad.data_ptr():  # the solver writes into pad[:P] directly
+                        pad[:P].copy_(delta)
                     dist.reduce_scatter_tensor(myd, pad, op=dist.ReduceOp.SUM)
                     lo = self.rank * shard
-                    wfull[lo:lo + shard].add_(myd, alpha=lr)
-                    dist.all_gather_into_tensor(wfull, wfull[lo:lo + shard].clone())
-                    srv.w.copy_(wfull[:P])
+                    mine = wfull[lo:lo + shard]
+                    mine.add_(myd, alpha=lr)
+                    dist.all_gather_into_tensor(wfull, mine)  # in place: srv.w is a view of wfull
                     if srv.frag is not None:
                         srv.frag.refresh(srv.w)
                     new_w = srv.w
             if srv is not None:
                 if self.rank == 0:
-                    for k in range(N):
-                        srv.tracker.received(k, r)
+                    srv.tracker.bsp_round(r)  # received(k, r) + sent(k, r + 1) for every worker
                     if not logged:
                         srv.log_eval(r, self.log)
-                    for k in range(N):
-                        srv.tracker.sent(k, r + 1)
                 srv.updates += N
             if wk is not None:
                 if new_w is not wk.w:
@@ -282,6 +284,27 @@ class DistEngine:
         return {"rounds": r, "updates": r * N, "elapsed_s": elapsed,
                 "updates_per_s": r * N / elapsed if elapsed > 0 else 0.0,
                 "max_vc_gap": int(srv.tracker.max_gap) if (srv is not None and self.rank == 0) else 0}
+
+    def _sharded_buffers(self, shard: int):
+        """Padded full weight vector whose first P entries ARE the server
+        replica (srv.w is re-pointed to a view of it) and a padded delta whose
+        first P entries ARE the solver's output: the only passes per round
+        are the collectives themselves and the shard update."""
+        if getattr(self, "_shard_bufs", None) is not None and self._shard_bufs[0].numel() == shard * self.world:
+            return self._shard_bufs
+        srv, wk, P = self.server, self.worker, self.spec.P
+        wfull = torch.zeros(shard * self.world, dtype=torch.float32, device=self.device)
+        wfull[:P].copy_(srv.w)
+        srv.w = wfull[:P]
+        pad = torch.zeros(shard * self.world, dtype=torch.float32, device=self.device)
+        if wk is not None:
+            wk.w = srv.w
+            wk.solver.delta = pad[:P]  # bound lazily by the native solver at its first run
+            if getattr(wk.solver, "_bound", None) is not None:
+                wk.solver._bound = None
+        myd = torch.zeros(shard, dtype=torch.float32, device=self.device)
+        self._shard_bufs = (wfull, pad, myd)
+        return self._shard_bufs
 
     # ------------------------------------------------------------------
     def _open_ctrl(self):

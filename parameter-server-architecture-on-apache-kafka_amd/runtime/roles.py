@@ -11,7 +11,9 @@ delta / weight tensors; roles only enqueue device work on the current stream.
 """
 from __future__ import annotations
 
+import os
 import time
+from contextlib import contextmanager
 
 import torch
 
@@ -23,6 +25,39 @@ from ..ops.sparse import SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide
 from .buffer import DeviceRing, StreamSource
 from .config import PSConfig
 from .faults import WorkerFailure
+
+
+class SideStream:
+    """Evaluation work off the critical path (GPU): it runs on its own stream
+    after the work that produced its inputs, and the next writer of those
+    inputs waits for it (:meth:`fence`).  On one MI355X the latency-bound
+    solver kernels leave most CUs idle, so a test-set evaluation on the side
+    stream overlaps the next solve instead of adding to the round time."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.gpu = is_gpu(self.device) and os.environ.get("PSX_SIDE_EVAL", "0") == "1"
+        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
+        self._ready = torch.cuda.Event() if self.gpu else None
+        self._done = torch.cuda.Event() if self.gpu else None
+        self._pending = False
+
+    @contextmanager
+    def run(self):
+        if not self.gpu:
+            yield
+            return
+        self._ready.record(torch.cuda.current_stream(self.device))
+        self.stream.wait_event(self._ready)
+        with torch.cuda.stream(self.stream):
+            yield
+        self._done.record(self.stream)
+        self._pending = True
+
+    def fence(self):
+        if self._pending:
+            torch.cuda.current_stream(self.device).wait_event(self._done)
+            self._pending = False
 
 
 def is_wide(spec) -> bool:
@@ -60,6 +95,7 @@ class WorkerRole:
         self.evalset = evalset
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
         self.scratch = EvalScratch(self.device)
+        self.side = SideStream(self.device)
         self.vc = 0  # version of the weights currently held
         self.iters = 0
         self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
@@ -88,14 +124,17 @@ class WorkerRole:
         if self.delay_s > 0:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)
+        self.side.fence()  # the last evaluation read the solver outputs this solve overwrites
         self.solver.run(self.ring, B, start, self.w)
         if log is not None and self.evalset is not None:
             if self.wide:  # local model = pulled weights overlaid with the subspace solution
+                # (in line: the overlay reads the pulled weights, which the server update rewrites)
                 log.worker_eval(self.evalset, self.solver, self.w, self.scratch, self.solver.loss, self.k, self.vc,
                                 self.tuples_seen)
             else:
-                log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch, self.solver.loss,
-                                self.k, self.vc, self.tuples_seen)
+                with self.side.run():
+                    log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch,
+                                    self.solver.loss, self.k, self.vc, self.tuples_seen)
         self.iters += 1
         if self.wide and not self.solver.dense_delta:
             return self.solver.sparse_delta()
@@ -113,12 +152,14 @@ class ServerRole:
         self.tracker = _native.host.VectorClockTracker(cfg.num_workers, cfg.consistency_model)
         self.evalset = evalset
         self.scratch = EvalScratch(self.device)
+        self.side = SideStream(self.device)
         self.updates = 0
         self.acc = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
 
     def apply(self, delta: torch.Tensor, lr: float | None = None):
         """w += lr * delta   (ServerProcessor.java:148-151 with lr = 1/N)."""
         lr = self.cfg.lr if lr is None else lr
+        self.side.fence()  # the last server evaluation reads w / the fragments rewritten here
         if self.wide:
             wide_server_apply(self.spec, self.w, delta, lr)
         else:
@@ -150,4 +191,5 @@ class ServerRole:
         """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
         if log is None or self.evalset is None:
             return
-        log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc)
+        with self.side.run():
+            log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc)

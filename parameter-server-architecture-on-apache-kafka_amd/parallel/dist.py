@@ -219,6 +219,7 @@ class DistEngine:
         t_start = time.time()
         r = self.rounds
         check_every = 1 if not cfg.max_iters else 0
+        pending_eval, pending_ts = None, None  # allreduce: server row of the previous round
         while True:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
@@ -228,19 +229,31 @@ class DistEngine:
             with self.tracer.span("ingest"):
                 if wk is not None:
                     wk.ingest()
-            with self.tracer.span("solve"):
-                delta = wk.compute(self.log) if wk is not None else zeros
             logged = False
-            with self.tracer.span("comm", schedule=sched):
-                if sched == "allreduce":
-                    dist.all_reduce(delta, op=dist.ReduceOp.SUM)
-                    if self.rank == 0:  # update + server eval row in one kernel
-                        srv.apply_and_log(delta, r, self.log, lr)
-                        logged = True
-                    else:
-                        srv.apply(delta, lr)
+            if sched == "allreduce":
+                # solve -> allreduce launched on the RCCL stream -> the evaluation rows
+                # (this round's worker row, the previous round's server row) run on
+                # the compute stream WHILE the collective is in flight -> update
+                with self.tracer.span("solve"):
+                    delta = wk.solve() if wk is not None else zeros
+                with self.tracer.span("comm", schedule=sched):
+                    work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
+                    if wk is not None:
+                        wk.log_eval(self.log)
+                    if pending_eval is not None:
+                        srv.log_eval(*pending_eval, self.log, ts=pending_ts)
+                        pending_eval = None
+                    work.wait()
+                    srv.apply(delta, lr)
+                    if self.rank == 0:
+                        pending_eval, pending_ts = (r,), int(time.time() * 1000)
+                    logged = True
                     new_w = srv.w
-                elif sched == "reduce_bcast":
+            else:
+                with self.tracer.span("solve"):
+                    delta = wk.compute(self.log) if wk is not None else zeros
+            with self.tracer.span("comm", schedule=sched):
+                if sched == "reduce_bcast":
                     dist.reduce(delta, dst=0, op=dist.ReduceOp.SUM)
                     if srv is not None:
                         srv.apply_and_log(delta, r, self.log, lr)
@@ -249,7 +262,7 @@ class DistEngine:
                     else:
                         new_w = wk.w
                     dist.broadcast(new_w, src=0)
-                else:  # sharded: key-range shards of the master weights (KeyRange.java:11-49)
+                elif sched == "sharded":  # key-range shards of the master weights (KeyRange.java:11-49)
                     srv.side.fence()  # srv.w / fragments are rewritten below
                     if delta.data_ptr() != pad.data_ptr():  # the solver writes into pad[:P] directly
                         pad[:P].copy_(delta)
@@ -277,6 +290,8 @@ class DistEngine:
             r += 1
             if self.log is not None:
                 self.log.drain()
+        if pending_eval is not None:
+            srv.log_eval(*pending_eval, self.log, ts=pending_ts)
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start

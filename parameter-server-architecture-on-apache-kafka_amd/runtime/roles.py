@@ -119,6 +119,14 @@ class WorkerRole:
         (LogisticRegressionTaskSpark.java:186), logged with the weights version
         it trained from and numTuplesSeen = the newest insertion id.
         """
+        delta = self.solve()
+        self.log_eval(log)
+        return delta
+
+    def solve(self):
+        """The local solve alone (the evaluation row is :meth:`log_eval`): lets a
+        multi-rank schedule put its collective between the two so that the
+        evaluation overlaps the communication."""
         if self.crash_at is not None and self.iters >= self.crash_at:
             raise WorkerFailure(self.k, f"injected crash at iteration {self.iters}")
         if self.delay_s > 0:
@@ -126,6 +134,14 @@ class WorkerRole:
         B, start = int(self.window.size), int(self.window.start)
         self.side.fence()  # the last evaluation read the solver outputs this solve overwrites
         self.solver.run(self.ring, B, start, self.w)
+        self.iters += 1
+        if self.wide and not self.solver.dense_delta:
+            return self.solver.sparse_delta()
+        return self.solver.delta
+
+    def log_eval(self, log):
+        """Worker row of the last solve: metrics of the LOCALLY trained model
+        (LogisticRegressionTaskSpark.java:186)."""
         if log is not None and self.evalset is not None:
             if self.wide:  # local model = pulled weights overlaid with the subspace solution
                 # (in line: the overlay reads the pulled weights, which the server update rewrites)
@@ -135,10 +151,6 @@ class WorkerRole:
                 with self.side.run():
                     log.worker_eval(self.evalset, self.solver.frag, self.solver.w_new, self.scratch,
                                     self.solver.loss, self.k, self.vc, self.tuples_seen)
-        self.iters += 1
-        if self.wide and not self.solver.dense_delta:
-            return self.solver.sparse_delta()
-        return self.solver.delta
 
 
 class ServerRole:
@@ -187,9 +199,9 @@ class ServerRole:
         self.apply(delta, lr)
         self.log_eval(vc, log)
 
-    def log_eval(self, vc: int, log):
+    def log_eval(self, vc: int, log, ts: int | None = None):
         """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
         if log is None or self.evalset is None:
             return
         with self.side.run():
-            log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc)
+            log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc, ts=ts)

@@ -72,6 +72,7 @@ def test_bsp_schedules_agree():
     for sched in ("allreduce", "reduce_bcast", "sharded"):
         out, w = _run(3, dict(BASE, bsp_schedule=sched))
         assert out["rounds"] == 5 and out["updates"] == 15
+        assert out["server_rows"] == 5  # allreduce: the last round's deferred server row is flushed
         ws[sched] = w
     assert torch.allclose(ws["allreduce"], ws["reduce_bcast"], atol=1e-5)
     assert torch.allclose(ws["allreduce"], ws["sharded"], atol=1e-5)

@@ -50,10 +50,13 @@ def load_datasets(cfg: PSConfig, train=None, test=None):
         if train is None:
             train = data_mod.load_libsvm(cfg.train_path, num_features=cfg.num_features)
         if test is None and cfg.test_path:
-            test = data_mod.load_libsvm(cfg.test_path, num_features=cfg.num_features or train.num_features)
+            test = data_mod.load_libsvm(cfg.test_path, num_features=cfg.num_features)
         F = max(train.num_features, test.num_features if test is not None else 0)
         if cfg.num_features is not None:
             F = int(cfg.num_features)
+        train.num_features = F  # hashed width: the larger of the two files' index ranges
+        if test is not None:
+            test.num_features = F
         if cfg.sigmoid:
             K = 1
         elif cfg.num_classes is not None:

@@ -12,6 +12,7 @@ device->host copies, events, fills or Python-side metric math.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -56,6 +57,9 @@ class LogSink:
                  to_stdout: bool = False, pool: int = 256, keep_records: bool = True, worker_append: bool = False):
         self.K = K
         self.device = torch.device(device)
+        for path in (worker_path, server_path):
+            if path and os.path.dirname(path):
+                os.makedirs(os.path.dirname(path), exist_ok=True)
         self.gpu = self.device.type == "cuda"
         self.wlog = _native.host.CsvLogger(worker_path, True, not worker_append, worker_append) if worker_path else (
             _native.host.CsvLogger("", True, False) if to_stdout else None)

@@ -287,3 +287,25 @@ def test_engine_wide_gpu(cuda, c, N):
         assert (wc - wg).abs().max().item() < 5e-3 * wc.abs().max().item()
     assert outs[cuda][0]["server_rows"] >= 1
     del cfg
+
+
+def test_cli_libsvm_inprocess(tmp_path):
+    """ServerAppRunner on LIBSVM files picks the wide model (reference CLI flags + new ones)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tr, _ = _problem(F=4000, rows=600)
+    te, _ = _problem(F=4000, rows=100, seed=3)
+    save_libsvm(tr, str(tmp_path / "train.svm"))
+    save_libsvm(te, str(tmp_path / "test.svm"))
+    cmd = [sys.executable, "-m", "psx.apps.server_app_runner", "-training", str(tmp_path / "train.svm"), "-test",
+           str(tmp_path / "test.svm"), "--inprocess", "--device", "cpu", "-p", "0", "--num_workers", "2", "-c", "2",
+           "--max_iters", "4", "-l", "--log_dir", str(tmp_path / "logs")]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    srows = (tmp_path / "logs" / "logs-server.csv").read_text().strip().split("\n")
+    wrows = (tmp_path / "logs" / "logs-worker.csv").read_text().strip().split("\n")
+    assert srows[0] == "timestamp;partition;vectorClock;loss;fMeasure;accuracy" and len(srows) >= 4
+    assert wrows[0].endswith(";numTuplesSeen") and len(wrows) >= 9

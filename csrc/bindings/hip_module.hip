@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include <memory>
+#include <stdexcept>
 
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
@@ -122,16 +123,20 @@ PYBIND11_MODULE(_psx_hip, m) {
   m.def(
       "test_eval",
       [](int FP, int K, uintptr_t Xt, uintptr_t yt, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t conf,
-         uintptr_t stream, uintptr_t ticket, uintptr_t slot, uintptr_t loss, unsigned long long seq) {
+         uintptr_t stream, uintptr_t ticket, uintptr_t slot, uintptr_t loss, unsigned long long seq, int coff1,
+         int coff2, uintptr_t slot2, unsigned long long seq2) {
         prepare_kernels();
+        if (coff1 < 0 || coff1 + K > 16 || (slot2 && (coff2 < 0 || coff2 + K > 16)))
+          throw std::invalid_argument("test_eval: class offset out of range");
         launch_test_eval(FP, K, P<const uint16_t>(Xt), P<const int32_t>(yt), T, P<const uint16_t>(whi),
                          P<const uint16_t>(wlo), P<const float>(b), P<int>(conf), S(stream), P<unsigned>(ticket),
-                         P<void>(slot), P<const float>(loss), seq);
+                         P<void>(slot), P<const float>(loss), seq, coff1, coff2, P<void>(slot2), seq2);
         hip_check(hipGetLastError(), "test_eval launch");
       },
       py::arg("FP"), py::arg("K"), py::arg("Xt"), py::arg("yt"), py::arg("T"), py::arg("whi"), py::arg("wlo"),
       py::arg("b"), py::arg("conf"), py::arg("stream"), py::arg("ticket") = 0, py::arg("slot") = 0,
-      py::arg("loss") = 0, py::arg("seq") = 0);
+      py::arg("loss") = 0, py::arg("seq") = 0, py::arg("coff1") = 0, py::arg("coff2") = 0, py::arg("slot2") = 0,
+      py::arg("seq2") = 0);
   // Fine-grained (coherent) pinned host memory: device stores land in host
   // memory without a copy and device loads never see a stale cached line.
   m.def("pinned_alloc", [](size_t bytes) {
@@ -150,17 +155,27 @@ PYBIND11_MODULE(_psx_hip, m) {
                   P<float>(out), S(stream));
     hip_check(hipGetLastError(), "logits launch");
   });
-  m.def("server_apply", [](int K, int F, int FP, uintptr_t w, uintptr_t delta, float lr, uintptr_t whi,
-                           uintptr_t wlo, uintptr_t b, uintptr_t stream) {
-    launch_server_apply(K, F, FP, P<float>(w), P<const float>(delta), lr, P<uint16_t>(whi), P<uint16_t>(wlo),
-                        P<float>(b), S(stream));
-    hip_check(hipGetLastError(), "server_apply launch");
-  });
-  m.def("make_fragments", [](int K, int F, int FP, uintptr_t w, uintptr_t whi, uintptr_t wlo, uintptr_t b,
-                             uintptr_t stream) {
-    launch_make_fragments(K, F, FP, P<const float>(w), P<uint16_t>(whi), P<uint16_t>(wlo), P<float>(b), S(stream));
-    hip_check(hipGetLastError(), "make_fragments launch");
-  });
+  m.def(
+      "server_apply",
+      [](int K, int F, int FP, uintptr_t w, uintptr_t delta, float lr, uintptr_t whi, uintptr_t wlo, uintptr_t b,
+         uintptr_t stream, int coff) {
+        if (coff < 0 || coff + K > 16) throw std::invalid_argument("fragment class offset out of range");
+        launch_server_apply(K, F, FP, P<float>(w), P<const float>(delta), lr, P<uint16_t>(whi), P<uint16_t>(wlo),
+                            P<float>(b), S(stream), coff);
+        hip_check(hipGetLastError(), "server_apply launch");
+      },
+      py::arg("K"), py::arg("F"), py::arg("FP"), py::arg("w"), py::arg("delta"), py::arg("lr"), py::arg("whi"),
+      py::arg("wlo"), py::arg("b"), py::arg("stream"), py::arg("coff") = 0);
+  m.def(
+      "make_fragments",
+      [](int K, int F, int FP, uintptr_t w, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t stream, int coff) {
+        if (coff < 0 || coff + K > 16) throw std::invalid_argument("fragment class offset out of range");
+        launch_make_fragments(K, F, FP, P<const float>(w), P<uint16_t>(whi), P<uint16_t>(wlo), P<float>(b), S(stream),
+                              coff);
+        hip_check(hipGetLastError(), "make_fragments launch");
+      },
+      py::arg("K"), py::arg("F"), py::arg("FP"), py::arg("w"), py::arg("whi"), py::arg("wlo"), py::arg("b"),
+      py::arg("stream"), py::arg("coff") = 0);
   // ---- wide / sparse model (BASELINE.json configs 4, 5) ----
   py::class_<WideCfg>(m, "WideCfg", py::module_local())
       .def(py::init([]() {

@@ -9,7 +9,7 @@ namespace psx {
 
 // Row tile and dynamic LDS footprint of the tile kernels for a padded width FP.
 constexpr int kTileRows = 32;
-inline size_t eval_lds_bytes(int FP) { return (size_t)kTileRows * FP * 2 + 8192 + 2048 + 512; }
+inline size_t eval_lds_bytes(int FP) { return (size_t)kTileRows * FP * 2 + 8192 + 2048 + 1024 + 512; }
 bool fp_supported(int FP);
 // Raise dynamic-LDS limits for the wide tile kernels (call before capture).
 void prepare_kernels();
@@ -22,14 +22,16 @@ void prepare_kernels();
 // pinned host EvalSlot `slot`, published with sequence number `seq`.
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
                       const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket = nullptr,
-                      void* slot = nullptr, const float* loss = nullptr, unsigned long long seq = 0);
+                      void* slot = nullptr, const float* loss = nullptr, unsigned long long seq = 0, int coff1 = 0,
+                      int coff2 = 0, void* slot2 = nullptr, unsigned long long seq2 = 0);
 void launch_logits(int FP, int K, const uint16_t* X, int T, const uint16_t* wf_hi, const uint16_t* wf_lo,
                    const float* b, float* logits, hipStream_t s);
 // Server update w += lr * delta (all P entries) and refresh the eval fragments.
+// coff: first class column of this model in the (shared) fragment buffer.
 void launch_server_apply(int K, int F, int FP, float* w, const float* delta, float lr, uint16_t* wf_hi,
-                         uint16_t* wf_lo, float* b_eff, hipStream_t s);
+                         uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff = 0);
 void launch_make_fragments(int K, int F, int FP, const float* w, uint16_t* wf_hi, uint16_t* wf_lo, float* b_eff,
-                           hipStream_t s);
+                           hipStream_t s, int coff = 0);
 // Copy n rows (row i of the batch = src row src_first + i*src_step) into ring
 // slots (dst_first + i) % cap, labels alongside.
 // ringT (optional): feature-major copy [FP][cap] kept in step with the ring.

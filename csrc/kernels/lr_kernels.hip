@@ -33,19 +33,30 @@ bool fp_supported(int FP) { return FP == 128 || FP == 256 || FP == 512 || FP == 
 // the counts (+ the worker's loss) into the pinned host slot, and publishes the
 // record's sequence number with a system-scope release store -- the host-side
 // MetricsSink picks it up with no copy, event or fill launch.
+//
+// The model's classes sit at columns [coff1, coff1 + K) of the fragments.
+// Paired mode (slot2 != nullptr): the 16 MFMA columns carry TWO models -- the
+// worker's locally trained model at [coff1, coff1 + K) and the server's global
+// model at [coff2, coff2 + K) of the same fragment buffer -- so the worker row
+// of this round and the server row of the previous round cost one pass over
+// the test set instead of two.
 template <int FP>
 __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* __restrict__ Xt,
                                                         const int32_t* __restrict__ yt, int T,
                                                         const uint16_t* __restrict__ wf_hi,
                                                         const uint16_t* __restrict__ wf_lo,
                                                         const float* __restrict__ b, int* acc, unsigned* ticket,
-                                                        char* slot, const float* loss, unsigned long long seq) {
+                                                        char* slot, const float* loss, unsigned long long seq,
+                                                        int coff1, int coff2, char* slot2, unsigned long long seq2) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [16][16]
   int* last = cl + 256;
+  int* cl2 = last + 4;                // [16][16] (paired mode)
   const int tid = threadIdx.x;
+  const bool pair = slot2 != nullptr;
   cl[tid] = 0;
+  if (pair) cl2[tid] = 0;
   const int ntiles = (T + 31) / 32;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int nrows = min(32, T - tile * 32);
@@ -59,7 +70,7 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
       int best = 0;
       float bz = -INFINITY;
       for (int c = 0; c < K; ++c) {
-        const float z = load_logit(red_base, tid, c) + b[c];
+        const float z = load_logit(red_base, tid, coff1 + c) + b[coff1 + c];
         if (z > bz) {
           bz = z;
           best = c;
@@ -68,12 +79,28 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
       int yl = yt[(size_t)tile * 32 + tid];
       yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
       atomicAdd(&cl[yl * 16 + best], 1);
+      if (pair) {
+        int best2 = 0;
+        float bz2 = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(red_base, tid, coff2 + c) + b[coff2 + c];
+          if (z > bz2) {
+            bz2 = z;
+            best2 = c;
+          }
+        }
+        atomicAdd(&cl2[yl * 16 + best2], 1);
+      }
     }
     __syncthreads();
   }
   __syncthreads();
   const int v = cl[tid];
   if (v) atomicAdd(acc + tid, v);
+  if (pair) {
+    const int v2 = cl2[tid];
+    if (v2) atomicAdd(acc + 256 + tid, v2);
+  }
   if (slot == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -84,25 +111,35 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ((int*)slot)[tid] = tot;
   if (tid == 0) *(float*)(slot + 1024) = loss ? *loss : 0.f;
+  if (pair) {
+    const int tot2 = __hip_atomic_exchange(acc + 256 + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ((int*)slot2)[tid] = tot2;
+    if (tid == 0) *(float*)(slot2 + 1024) = 0.f;
+  }
   __threadfence_system();
   __syncthreads();
   if (tid == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (pair)
+      __hip_atomic_store((unsigned long long*)(slot2 + 1032), seq2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
                       const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket, void* slot,
-                      const float* loss, unsigned long long seq) {
+                      const float* loss, unsigned long long seq, int coff1, int coff2, void* slot2,
+                      unsigned long long seq2) {
   const size_t lds = eval_lds_bytes(FP);
   const int ntiles = (T + 31) / 32;
   const int grid = ntiles < 1024 ? ntiles : 1024;
   if (grid <= 0) return;
   char* sl = static_cast<char*>(slot);
-#define PSX_TE(FPV)                                                                                        \
-  case FPV:                                                                                                \
-    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf, ticket, sl, loss, seq); \
+  char* sl2 = static_cast<char*>(slot2);
+#define PSX_TE(FPV)                                                                                          \
+  case FPV:                                                                                                  \
+    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf, ticket, sl, loss, seq, \
+                                                 coff1, coff2, sl2, seq2);                                  \
     break;
   switch (FP) {
     PSX_TE(128)
@@ -170,7 +207,7 @@ void launch_logits(int FP, int K, const uint16_t* X, int T, const uint16_t* wf_h
 __global__ __launch_bounds__(256) void server_apply_kernel(int K, int F, int FP, float* w,
                                                            const float* __restrict__ delta, float lr,
                                                            uint16_t* wf_hi, uint16_t* wf_lo, float* b_eff,
-                                                           int apply) {
+                                                           int apply, int coff) {
   const int P = K * FP + K, KF = K * FP;
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
@@ -181,23 +218,23 @@ __global__ __launch_bounds__(256) void server_apply_kernel(int K, int F, int FP,
   }
   if (p < KF) {
     const int c = p / FP, f = p - c * FP;
-    write_frag(wf_hi, wf_lo, c, f, f < F ? v : 0.f);
+    write_frag(wf_hi, wf_lo, coff + c, f, f < F ? v : 0.f);
   } else {
-    b_eff[p - KF] = v;
+    b_eff[coff + p - KF] = v;
   }
 }
 
 void launch_server_apply(int K, int F, int FP, float* w, const float* delta, float lr, uint16_t* wf_hi,
-                         uint16_t* wf_lo, float* b_eff, hipStream_t s) {
+                         uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff) {
   const int P = K * FP + K;
-  server_apply_kernel<<<(P + 255) / 256, 256, 0, s>>>(K, F, FP, w, delta, lr, wf_hi, wf_lo, b_eff, 1);
+  server_apply_kernel<<<(P + 255) / 256, 256, 0, s>>>(K, F, FP, w, delta, lr, wf_hi, wf_lo, b_eff, 1, coff);
 }
 
 void launch_make_fragments(int K, int F, int FP, const float* w, uint16_t* wf_hi, uint16_t* wf_lo, float* b_eff,
-                           hipStream_t s) {
+                           hipStream_t s, int coff) {
   const int P = K * FP + K;
   server_apply_kernel<<<(P + 255) / 256, 256, 0, s>>>(K, F, FP, const_cast<float*>(w), nullptr, 0.f, wf_hi, wf_lo,
-                                                      b_eff, 0);
+                                                      b_eff, 0, coff);
 }
 
 // ---------------------------------------------------------------------------

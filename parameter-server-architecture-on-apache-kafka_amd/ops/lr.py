@@ -45,18 +45,26 @@ class SolverOptions:
 
 
 class Fragments:
-    """bf16 hi/lo MFMA-fragment copy of a weight vector + fp32 intercepts."""
+    """bf16 hi/lo MFMA-fragment copy of a weight vector + fp32 intercepts.
 
-    def __init__(self, spec: ModelSpec, device):
+    The 16 fragment columns can carry two models: ``coff`` is the first class
+    column of the model written through THIS handle (a worker's solver writes
+    columns [0, KP), the colocated server [16 - K, 16); see EvalPair)."""
+
+    def __init__(self, spec: ModelSpec, device, coff: int = 0, share: "Fragments | None" = None):
         self.spec = spec
-        self.hi = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
-        self.lo = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
-        self.b = torch.zeros(16, dtype=torch.float32, device=device)
+        self.coff = int(coff)
+        if share is not None:
+            self.hi, self.lo, self.b = share.hi, share.lo, share.b
+        else:
+            self.hi = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
+            self.lo = torch.zeros(16 * spec.Fp, dtype=torch.int16, device=device)
+            self.b = torch.zeros(16, dtype=torch.float32, device=device)
 
     def refresh(self, w: torch.Tensor):
         s = self.spec
         _native.hip().make_fragments(s.K, s.F, s.Fp, w.data_ptr(), self.hi.data_ptr(), self.lo.data_ptr(),
-                                     self.b.data_ptr(), stream_handle(w.device))
+                                     self.b.data_ptr(), stream_handle(w.device), self.coff)
 
 
 class LocalSolveOp:
@@ -163,11 +171,29 @@ class EvalSet:
             _native.hip().test_eval(s.Fp, s.K, self.X.data_ptr(), self.y.data_ptr(), self.T, frag.hi.data_ptr(),
                                     frag.lo.data_ptr(), frag.b.data_ptr(), scratch.acc.data_ptr(),
                                     stream_handle(self.device), scratch.ticket.data_ptr(), int(slot_addr),
-                                    loss.data_ptr() if loss is not None else 0, int(seq))
+                                    loss.data_ptr() if loss is not None else 0, int(seq), frag.coff)
             return
         conf = torch.zeros(256, dtype=torch.int32)
         self.confusion_async(None, w, conf)
         _write_slot_cpu(slot_addr, conf, float(loss.item()) if loss is not None else 0.0, seq)
+
+    def eval_pair_to_slots(self, frag_a: Fragments | None, w_a: torch.Tensor, frag_b: Fragments | None,
+                           w_b: torch.Tensor, scratch: "EvalScratch", slot_a: int, seq_a: int, loss_a, slot_b: int,
+                           seq_b: int):
+        """Two models whose fragments share one buffer (columns frag_a.coff.. and
+        frag_b.coff..) evaluated in ONE pass over the test set."""
+        s = self.spec
+        if is_gpu(self.device):
+            if frag_a.hi.data_ptr() != frag_b.hi.data_ptr():
+                raise ValueError("paired evaluation needs one shared fragment buffer")
+            _native.hip().test_eval(s.Fp, s.K, self.X.data_ptr(), self.y.data_ptr(), self.T, frag_a.hi.data_ptr(),
+                                    frag_a.lo.data_ptr(), frag_a.b.data_ptr(), scratch.acc.data_ptr(),
+                                    stream_handle(self.device), scratch.ticket.data_ptr(), int(slot_a),
+                                    loss_a.data_ptr() if loss_a is not None else 0, int(seq_a), frag_a.coff,
+                                    frag_b.coff, int(slot_b), int(seq_b))
+            return
+        self.eval_to_slot(frag_a, w_a, scratch, slot_a, seq_a, loss_a)
+        self.eval_to_slot(frag_b, w_b, scratch, slot_b, seq_b, None)
 
 
 
@@ -175,7 +201,7 @@ class EvalScratch:
     """Private accumulator + ticket of one evaluation caller (stays zero between calls)."""
 
     def __init__(self, device):
-        self.acc = torch.zeros(256, dtype=torch.int32, device=device)
+        self.acc = torch.zeros(512, dtype=torch.int32, device=device)  # [2 models][16][16]
         self.ticket = torch.zeros(4, dtype=torch.int32, device=device)
 
 
@@ -192,7 +218,8 @@ def server_apply(spec: ModelSpec, w: torch.Tensor, delta: torch.Tensor, lr: floa
     """w += lr * delta over all P entries (quirk Q1 fixed) + refresh eval fragments."""
     if is_gpu(w.device):
         _native.hip().server_apply(spec.K, spec.F, spec.Fp, w.data_ptr(), delta.data_ptr(), float(lr),
-                                   frag.hi.data_ptr(), frag.lo.data_ptr(), frag.b.data_ptr(), stream_handle(w.device))
+                                   frag.hi.data_ptr(), frag.lo.data_ptr(), frag.b.data_ptr(), stream_handle(w.device),
+                                   frag.coff)
     else:
         w.add_(delta, alpha=lr)
 

@@ -46,7 +46,7 @@ from ..runtime.config import PSConfig
 from ..runtime.engine import load_datasets
 from ..runtime.faults import WorkerFailure, drop_on_failure
 from ..ops.sparse import SparseDelta, nz_capacity
-from ..runtime.roles import ServerRole, WorkerRole, is_wide, make_evalset
+from ..runtime.roles import EvalPair, ServerRole, WorkerRole, is_wide, make_evalset
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
@@ -136,6 +136,9 @@ class DistEngine:
         self.rounds = 0
         self._ctrl = None
         self._next_vc = 0
+        if (not self.async_mode and cfg.pair_eval and self.is_server and self.server is not None
+                and self.worker is not None):
+            EvalPair(self.server, self.worker)  # rank 0: worker row + previous server row in one eval pass
         # resume: rank 0 restores the server, every worker rank its own worker file;
         # BSP continues at the server's round (agreed over a collective)
         resumed = maybe_resume(cfg, self.server if self.is_server else None,
@@ -219,7 +222,6 @@ class DistEngine:
         t_start = time.time()
         r = self.rounds
         check_every = 1 if not cfg.max_iters else 0
-        pending_eval, pending_ts = None, None  # allreduce: server row of the previous round
         while True:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
@@ -232,21 +234,19 @@ class DistEngine:
             logged = False
             if sched == "allreduce":
                 # solve -> allreduce launched on the RCCL stream -> the evaluation rows
-                # (this round's worker row, the previous round's server row) run on
-                # the compute stream WHILE the collective is in flight -> update
+                # (this round's worker row and, on rank 0, the previous round's server
+                # row: one paired pass) run on the compute stream WHILE the collective
+                # is in flight -> update
                 with self.tracer.span("solve"):
                     delta = wk.solve() if wk is not None else zeros
                 with self.tracer.span("comm", schedule=sched):
                     work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
                     if wk is not None:
                         wk.log_eval(self.log)
-                    if pending_eval is not None:
-                        srv.log_eval(*pending_eval, self.log, ts=pending_ts)
-                        pending_eval = None
                     work.wait()
                     srv.apply(delta, lr)
                     if self.rank == 0:
-                        pending_eval, pending_ts = (r,), int(time.time() * 1000)
+                        srv.log_eval(r, self.log)  # deferred into the next round's paired pass
                     logged = True
                     new_w = srv.w
             else:
@@ -290,8 +290,8 @@ class DistEngine:
             r += 1
             if self.log is not None:
                 self.log.drain()
-        if pending_eval is not None:
-            srv.log_eval(*pending_eval, self.log, ts=pending_ts)
+        if srv is not None:
+            srv.flush_deferred(self.log)  # the last round's server row (rank 0)
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start

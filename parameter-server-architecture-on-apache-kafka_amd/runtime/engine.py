@@ -30,7 +30,7 @@ from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
 from .config import PSConfig
 from .faults import WorkerFailure, drop_on_failure
-from .roles import ServerRole, WorkerRole, make_evalset
+from .roles import EvalPair, ServerRole, WorkerRole, make_evalset
 
 
 def _wants_wide(cfg: PSConfig, train) -> bool:
@@ -104,6 +104,8 @@ class LocalEngine:
         self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
                         for k in range(cfg.num_workers)]
         self.rounds = 0
+        if cfg.consistency_model == 0 and cfg.pair_eval:  # worker 0's rows and the server rows: one eval pass
+            EvalPair(self.server, self.workers[0])
         self.failed: set[int] = set()
         if maybe_resume(cfg, self.server, self.workers):
             self.rounds = int(self.server.tracker.min_clock())
@@ -192,6 +194,7 @@ class LocalEngine:
             r += 1
             maybe_checkpoint(cfg, srv, r, W)
             self.log.drain()
+        srv.flush_deferred(self.log)  # the last round's server row
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start

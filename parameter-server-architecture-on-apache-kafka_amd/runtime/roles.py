@@ -96,6 +96,7 @@ class WorkerRole:
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
         self.scratch = EvalScratch(self.device)
         self.side = SideStream(self.device)
+        self.pair = None  # EvalPair with the colocated server (BSP)
         self.vc = 0  # version of the weights currently held
         self.iters = 0
         self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
@@ -142,6 +143,9 @@ class WorkerRole:
     def log_eval(self, log):
         """Worker row of the last solve: metrics of the LOCALLY trained model
         (LogisticRegressionTaskSpark.java:186)."""
+        if self.pair is not None:
+            self.pair.worker_row(log)
+            return
         if log is not None and self.evalset is not None:
             if self.wide:  # local model = pulled weights overlaid with the subspace solution
                 # (in line: the overlay reads the pulled weights, which the server update rewrites)
@@ -165,6 +169,7 @@ class ServerRole:
         self.evalset = evalset
         self.scratch = EvalScratch(self.device)
         self.side = SideStream(self.device)
+        self.pair = None  # EvalPair with the colocated worker (BSP)
         self.updates = 0
         self.acc = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
 
@@ -203,5 +208,78 @@ class ServerRole:
         """Global-model test metrics, logged on worker-0 deltas (ServerProcessor.java:154-165)."""
         if log is None or self.evalset is None:
             return
+        if self.pair is not None:  # evaluated together with the worker's next row
+            self.pair.defer_server_row(log, vc, ts)
+            return
         with self.side.run():
             log.server_eval(self.evalset, self.frag, self.w, self.scratch, vc, ts=ts)
+
+    def flush_deferred(self, log):
+        if self.pair is not None:
+            self.pair.flush(log)
+
+
+class EvalPair:
+    """Sequential consistency with a colocated server: the worker's row of
+    round r (its locally trained model) and the server's row of round r-1 (the
+    global model, unchanged until the update of round r) are evaluated in ONE
+    pass over the device-resident test set.  On the GPU the worker's solver and
+    the server share one MFMA fragment buffer -- worker classes in columns
+    [0, KP), server classes in [16 - K, 16) -- and the eval kernel computes both
+    models' logits with the same MFMAs.  Server rows keep the timestamp of the
+    update that produced them."""
+
+    def __init__(self, server: "ServerRole", worker: WorkerRole):
+        self.server, self.worker = server, worker
+        self.pending = None  # (log, vc, ts) of a deferred server row
+        spec = server.spec
+        self.shared = (is_gpu(server.device) and not server.wide and server.evalset is worker.evalset
+                       and server.evalset is not None and _solver_padded_classes(spec.K) + spec.K <= 16)
+        if self.shared:
+            server.frag = Fragments(spec, server.device, coff=16 - spec.K)
+            server.frag.refresh(server.w)
+            worker.solver.frag = Fragments(spec, worker.device, coff=0, share=server.frag)
+            worker.solver._bound = None  # rebind the native solver to the shared fragments
+        server.pair = self
+        worker.pair = self
+
+    def defer_server_row(self, log, vc: int, ts: int | None):
+        if self.pending is not None:
+            self.flush(self.pending[0])
+        self.pending = (log, int(vc), int(ts) if ts is not None else int(time.time() * 1000))
+
+    def worker_row(self, log):
+        wk, srv = self.worker, self.server
+        if log is None or wk.evalset is None:
+            return
+        pend = self.pending
+        self.pending = None
+        if pend is not None and pend[0] is not log:  # a different sink (bench swapped logs): flush separately
+            self._server_only(pend)
+            pend = None
+        if pend is not None and self.shared:
+            log.pair_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.solver.loss, wk.k, wk.vc, wk.tuples_seen,
+                          srv.frag, srv.w, pend[1], pend[2], wk.scratch)
+            return
+        if pend is not None:
+            self._server_only(pend)
+        if wk.wide:
+            log.worker_eval(wk.evalset, wk.solver, wk.w, wk.scratch, wk.solver.loss, wk.k, wk.vc, wk.tuples_seen)
+        else:
+            log.worker_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.scratch, wk.solver.loss, wk.k, wk.vc,
+                            wk.tuples_seen)
+
+    def _server_only(self, pend):
+        log, vc, ts = pend
+        srv = self.server
+        log.server_eval(srv.evalset, srv.frag, srv.w, srv.scratch, vc, ts=ts)
+
+    def flush(self, log=None):
+        if self.pending is not None:
+            pend = self.pending
+            self.pending = None
+            self._server_only(pend)
+
+
+def _solver_padded_classes(K: int) -> int:
+    return 2 if K <= 2 else 4 if K <= 4 else 8 if K <= 8 else 16

@@ -87,3 +87,25 @@ def test_asp_crash_dropped_gpu(cuda):
                       train=train, test=test)
     out = eng.run()
     assert out["failed_workers"] == [2] and eng.workers[0].iters >= 10
+
+
+@pytest.mark.parametrize("N", [1, 2])
+def test_paired_eval_rows_match_unpaired(cuda, N):
+    """Worker-0 rows + deferred server rows from one paired pass == separate evaluations."""
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    books, ws = [], []
+    for pair in (True, False):
+        eng = LocalEngine(_cfg(num_workers=N, max_iters=12, init="random", pair_eval=pair), cuda, train=train,
+                          test=test)
+        if pair:
+            assert eng.server.pair is not None and eng.server.pair.shared
+        eng.run()
+        books.append(eng.log.book)
+        ws.append(eng.server.w.cpu())
+    assert torch.equal(ws[0], ws[1])
+    s0 = sorted((r[1], r[2], r[3]) for r in books[0].server)
+    s1 = sorted((r[1], r[2], r[3]) for r in books[1].server)
+    assert s0 == s1 and len(s0) == 12
+    w0 = sorted((r[1], r[2], r[4], r[5]) for r in books[0].worker)
+    w1 = sorted((r[1], r[2], r[4], r[5]) for r in books[1].worker)
+    assert w0 == w1 and len(w0) == 12 * N

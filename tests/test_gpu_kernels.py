@@ -202,3 +202,33 @@ def test_ring_ingest_strided_wrap(cuda):
     assert torch.equal(ring.X.cpu()[dst], ds.X.cpu()[src])
     assert torch.equal(ring.y.cpu()[dst], ds.y.cpu()[src])
     assert torch.equal(ring.XT.cpu(), ring.X.cpu().t())
+
+
+def test_paired_eval_matches_single(cuda):
+    """Two models in one fragment buffer (columns [0,K) and [16-K,16)) evaluated in
+    one pass give exactly the confusion counts of two separate passes."""
+    from psx.ops.lr import EvalScratch
+    from psx.utils.logsink import LogSink
+
+    spec = ModelSpec(1024, 6)
+    te = synth_finefood(4877, seed=11)
+    ev = EvalSet(spec, te.X, te.y, cuda)
+    wa, wb = _rand_w(spec, 21, 0.5).to(cuda), _rand_w(spec, 22, 0.5).to(cuda)
+    shared_b = Fragments(spec, cuda, coff=16 - spec.K)
+    shared_a = Fragments(spec, cuda, coff=0, share=shared_b)
+    shared_a.refresh(wa)
+    shared_b.refresh(wb)
+    fa, fb = Fragments(spec, cuda), Fragments(spec, cuda)
+    fa.refresh(wa)
+    fb.refresh(wb)
+    log = LogSink(spec.K, cuda)
+    scratch = EvalScratch(cuda)
+    loss = torch.tensor([1.5], device=cuda)
+    log.pair_eval(ev, shared_a, wa, loss, 0, 7, 100, shared_b, wb, 6, 1234, scratch)
+    log.worker_eval(ev, fa, wa, scratch, loss, 0, 7, 100)
+    log.server_eval(ev, fb, wb, scratch, 6, ts=1234)
+    book = log.book
+    log.close()
+    (wr1, wr2), (sr1, sr2) = book.worker, book.server
+    assert wr1[1:] == wr2[1:] and sr1 == sr2 and sr1[0] == 1234
+    assert scratch.acc.abs().sum().item() == 0

@@ -50,8 +50,9 @@ void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv,
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                  hipStream_t s);
 // Line-search retry slots [slot_begin, slot_end) in one persistent launch.
+// with_finalize: the finalisation runs inside the tail launch (no separate finalize node).
 void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
-                 const SolveDev& dv, int nwg, hipStream_t s);
+                 const SolveDev& dv, int nwg, hipStream_t s, int with_finalize = 0);
 size_t tail_lds_bytes(int FP);
 int tail_grid(int FP, int nwg);
 

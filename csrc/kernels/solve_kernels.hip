@@ -691,37 +691,15 @@ __device__ __forceinline__ void grid_barrier(unsigned long long* ctr, unsigned l
   __syncthreads();
 }
 
-template <int FP, int KP>
-__global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl,
-                                                   int slot_begin, int slot_end, SolveDev dv, int ns, int lds_flag) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
-  if (gctrl->phase == kPhDone) return;  // the common case: written by the previous launch
-  const int G = gridDim.x, wg = blockIdx.x;
-  unsigned long long* bar = dv.xch + kXchBar;
-  unsigned long long nb = 0;
-  for (int slot = slot_begin; slot < slot_end; ++slot) {
-    if (slot > slot_begin) {
-      if (threadIdx.x == 0) phase_s = (int)(unsigned)xload((unsigned long long*)&gctrl->phase);
-      __syncthreads();
-      if (phase_s == kPhDone) break;  // uniform: every workgroup read the same word after the barrier
-    }
-    fwd_body<FP>(cfg, prm, slot, dv, lds, wg, G);
-    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
-    if (wg < ns) bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, G, lds, wg, ns);
-    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Finalisation (after the last slot): back to the unstandardised space,
 // multinomial centring across classes, delta = w_new - w_old, eval fragments,
 // loss and solver statistics.  One thread per feature (all classes).
 template <int KP>
-__global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl* ctrl, SolveDev dv) {
+__device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk) {
   const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
-  const int f = blockIdx.x * 256 + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
+  const int f = blk * 256 + threadIdx.x;
+  if (blk == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
   if (f < FP) {
     const float iv = dv.inv_std[f];
     float xv[KP], fx[KP], wo[KP];
@@ -749,7 +727,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl
       }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blk == 0 && threadIdx.x == 0) {
     const int IB = dv.KP * FPI;
     float bv[16];
     float mean = 0.f;
@@ -776,6 +754,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl
   }
 }
 
+template <int KP>
+__global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl* ctrl, SolveDev dv) {
+  finalize_body<KP>(cfg, ctrl, dv, blockIdx.x);
+}
+
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s) {
   const int grid = (cfg.Fp + 255) / 256;
   switch (dv.KP) {
@@ -784,6 +767,35 @@ void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv,
     case 8: finalize_kernel<8><<<grid, 256, 0, s>>>(cfg, ctrl, dv); break;
     default: finalize_kernel<16><<<grid, 256, 0, s>>>(cfg, ctrl, dv); break;
   }
+}
+
+template <int FP, int KP>
+__global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl,
+                                                   int slot_begin, int slot_end, SolveDev dv, int ns, int lds_flag,
+                                                   int nfin) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
+  if (gctrl->phase == kPhDone) {  // the common case: written by the previous launch
+    // the finalisation is folded into this launch (one graph node less per solve)
+    if (blockIdx.x < nfin) finalize_body<KP>(cfg, gctrl, dv, blockIdx.x);
+    return;
+  }
+  const int G = gridDim.x, wg = blockIdx.x;
+  unsigned long long* bar = dv.xch + kXchBar;
+  unsigned long long nb = 0;
+  for (int slot = slot_begin; slot < slot_end; ++slot) {
+    if (slot > slot_begin) {
+      if (threadIdx.x == 0) phase_s = (int)(unsigned)xload((unsigned long long*)&gctrl->phase);
+      __syncthreads();
+      if (phase_s == kPhDone) break;  // uniform: every workgroup read the same word after the barrier
+    }
+    fwd_body<FP>(cfg, prm, slot, dv, lds, wg, G);
+    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
+    if (wg < ns) bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, G, lds, wg, ns);
+    grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
+  }
+  // every exit of the loop follows a grid barrier: all slots' updates are visible
+  if (wg < nfin) finalize_body<KP>(cfg, gctrl, dv, wg);
 }
 
 // ---------------------------------------------------------------------------
@@ -837,26 +849,27 @@ int tail_grid(int FP, int nwg) {
 
 template <int FP>
 static void launch_tail_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int s0, int s1,
-                           const SolveDev& dv, int nwg, hipStream_t s) {
+                           const SolveDev& dv, int nwg, int fin, hipStream_t s) {
   const int G = tail_grid(FP, nwg), ns = bwd_grid(FP);
   const size_t lb = tail_lds_bytes(FP);
   const int flag = (int)(lb - 16);
+  const int nfin = fin ? (cfg.Fp + 255) / 256 : 0;  // <= G: G >= FP/32 workgroups
   switch (dv.KP) {
-    case 2: tail_kernel<FP, 2><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
-    case 4: tail_kernel<FP, 4><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
-    case 8: tail_kernel<FP, 8><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
-    default: tail_kernel<FP, 16><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag); break;
+    case 2: tail_kernel<FP, 2><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;
+    case 4: tail_kernel<FP, 4><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;
+    case 8: tail_kernel<FP, 8><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;
+    default: tail_kernel<FP, 16><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;
   }
 }
 
 void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
-                 const SolveDev& dv, int nwg, hipStream_t s) {
+                 const SolveDev& dv, int nwg, hipStream_t s, int with_finalize) {
   switch (cfg.Fp) {
-    case 128: launch_tail_fp<128>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
-    case 256: launch_tail_fp<256>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
-    case 512: launch_tail_fp<512>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
-    case 1024: launch_tail_fp<1024>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
-    case 2048: launch_tail_fp<2048>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, s); break;
+    case 128: launch_tail_fp<128>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, with_finalize, s); break;
+    case 256: launch_tail_fp<256>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, with_finalize, s); break;
+    case 512: launch_tail_fp<512>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, with_finalize, s); break;
+    case 1024: launch_tail_fp<1024>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, with_finalize, s); break;
+    case 2048: launch_tail_fp<2048>(cfg, prm, ctrl, slot_begin, slot_end, dv, nwg, with_finalize, s); break;
     default: break;
   }
 }

@@ -46,7 +46,7 @@ class LocalSolver {
   void run(int B, int start, hipStream_t stream);
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
-  int kernels_per_solve() const { return 2 + 2 * nfast_ + (cfg_.nslots > nfast_ ? 1 : 0); }
+  int kernels_per_solve() const { return 2 + 2 * nfast_; }  // stats_prep + slots + (tail with finalize | finalize)
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):

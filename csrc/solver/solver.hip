@@ -132,8 +132,10 @@ LocalSolver::~LocalSolver() {
 void LocalSolver::enqueue_body(hipStream_t s, int B, int start) {
   launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, s);
   for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
-  if (cfg_.nslots > nfast_) launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s);
-  launch_finalize(cfg_, ctrl_, dv_, s);
+  if (cfg_.nslots > nfast_)
+    launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s, /*with_finalize=*/1);
+  else
+    launch_finalize(cfg_, ctrl_, dv_, s);
   hip_check(hipGetLastError(), "solver kernel launch");
 }
 

@@ -167,6 +167,21 @@ PYBIND11_MODULE(_psx_hip, m) {
       py::arg("K"), py::arg("F"), py::arg("FP"), py::arg("w"), py::arg("delta"), py::arg("lr"), py::arg("whi"),
       py::arg("wlo"), py::arg("b"), py::arg("stream"), py::arg("coff") = 0);
   m.def(
+      "server_apply_n",
+      [](int K, int F, int FP, uintptr_t w, std::vector<uintptr_t> deltas, float lr, uintptr_t whi, uintptr_t wlo,
+         uintptr_t b, uintptr_t stream, int coff) {
+        if (coff < 0 || coff + K > 16) throw std::invalid_argument("fragment class offset out of range");
+        if (deltas.empty() || deltas.size() > 16) throw std::invalid_argument("1..16 deltas per call");
+        DeltaList dl{};
+        dl.n = (int)deltas.size();
+        for (int i = 0; i < dl.n; ++i) dl.p[i] = P<const float>(deltas[i]);
+        launch_server_apply_n(K, F, FP, P<float>(w), dl, lr, P<uint16_t>(whi), P<uint16_t>(wlo), P<float>(b),
+                              S(stream), coff);
+        hip_check(hipGetLastError(), "server_apply_n launch");
+      },
+      py::arg("K"), py::arg("F"), py::arg("FP"), py::arg("w"), py::arg("deltas"), py::arg("lr"), py::arg("whi"),
+      py::arg("wlo"), py::arg("b"), py::arg("stream"), py::arg("coff") = 0);
+  m.def(
       "make_fragments",
       [](int K, int F, int FP, uintptr_t w, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t stream, int coff) {
         if (coff < 0 || coff + K > 16) throw std::invalid_argument("fragment class offset out of range");

@@ -27,6 +27,13 @@ void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int 
 void launch_logits(int FP, int K, const uint16_t* X, int T, const uint16_t* wf_hi, const uint16_t* wf_lo,
                    const float* b, float* logits, hipStream_t s);
 // Server update w += lr * delta (all P entries) and refresh the eval fragments.
+struct DeltaList {
+  const float* p[16];
+  int n;
+};
+// w += lr * sum_i dl.p[i] (all P entries) + fragments, one kernel (n <= 16).
+void launch_server_apply_n(int K, int F, int FP, float* w, const DeltaList& dl, float lr, uint16_t* wf_hi,
+                           uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff = 0);
 // coff: first class column of this model in the (shared) fragment buffer.
 void launch_server_apply(int K, int F, int FP, float* w, const float* delta, float lr, uint16_t* wf_hi,
                          uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff = 0);

@@ -224,6 +224,32 @@ __global__ __launch_bounds__(256) void server_apply_kernel(int K, int F, int FP,
   }
 }
 
+// BSP round with N colocated workers: w += lr * (delta_0 + ... + delta_{n-1}) in ONE pass
+// (instead of a copy + N-1 adds + the update), fragments refreshed.
+__global__ __launch_bounds__(256) void server_apply_n_kernel(int K, int F, int FP, float* w, DeltaList dl, float lr,
+                                                             uint16_t* wf_hi, uint16_t* wf_lo, float* b_eff,
+                                                             int coff) {
+  const int P = K * FP + K, KF = K * FP;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  float sum = 0.f;
+  for (int i = 0; i < dl.n; ++i) sum += dl.p[i][p];
+  const float v = w[p] + lr * sum;
+  w[p] = v;
+  if (p < KF) {
+    const int c = p / FP, f = p - c * FP;
+    write_frag(wf_hi, wf_lo, coff + c, f, f < F ? v : 0.f);
+  } else {
+    b_eff[coff + p - KF] = v;
+  }
+}
+
+void launch_server_apply_n(int K, int F, int FP, float* w, const DeltaList& dl, float lr, uint16_t* wf_hi,
+                           uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff) {
+  const int P = K * FP + K;
+  server_apply_n_kernel<<<(P + 255) / 256, 256, 0, s>>>(K, F, FP, w, dl, lr, wf_hi, wf_lo, b_eff, coff);
+}
+
 void launch_server_apply(int K, int F, int FP, float* w, const float* delta, float lr, uint16_t* wf_hi,
                          uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff) {
   const int P = K * FP + K;

@@ -68,7 +68,8 @@ class PSConfig:
     worker_timeout_s: float = 600.0  # watchdog: a busy worker silent this long has failed
     on_worker_failure: str = "auto"  # drop | fail | auto (drop under eventual consistency)
     trace_path: str | None = None
-    pair_eval: bool = True  # BSP: worker-0 row + previous server row from one eval pass (EvalPair)
+    pair_eval: bool = True
+    concurrent_workers: bool = True  # in-process BSP on a GPU: one HIP stream per worker  # BSP: worker-0 row + previous server row from one eval pass (EvalPair)
     perf_log: bool = False  # write {log_dir}/logs-perf.csv (per-round device phase times)
 
     @property

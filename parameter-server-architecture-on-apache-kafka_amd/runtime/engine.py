@@ -159,14 +159,19 @@ class LocalEngine:
         exhausted_since = None
         r = self.rounds
         u_start = srv.updates
+        lanes = (_WorkerLanes(self.device, self.workers)
+                 if is_gpu(self.device) and len(self.workers) > 1 and cfg.concurrent_workers else None)
         while not self._stop(r - self.rounds, t_start, exhausted_since):
             W = [w for w in self.workers if w.k not in self.failed]
             if not W:
                 break
             self.tracer.round_begin()
+            if lanes is not None:  # workers run concurrently, one HIP stream each
+                lanes.begin()
             with self.tracer.span("ingest"):
                 for w in W:
-                    w.ingest()
+                    with lanes.on(w) if lanes is not None else _Null():
+                        w.ingest()
             if all(w.source.exhausted for w in W):
                 exhausted_since = exhausted_since or time.time()
             if not all(w.ready() for w in W):
@@ -176,10 +181,13 @@ class LocalEngine:
             with self.tracer.span("solve"):
                 for w in W:
                     try:
-                        deltas.append(w.compute(self.log))
+                        with lanes.on(w) if lanes is not None else _Null():
+                            deltas.append(w.compute(self.log))
                         done.append(w)
                     except WorkerFailure as e:
                         self._worker_failed(e, w.k)
+            if lanes is not None:
+                lanes.join(done)
             if not deltas:
                 break
             with self.tracer.span("server"):
@@ -328,6 +336,35 @@ class LocalEngine:
         elapsed = time.time() - t_start
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0}
+
+
+class _WorkerLanes:
+    """One HIP stream per in-process worker (BSP).  A local solve is a chain of
+    latency-bound kernels that occupies a few dozen of the 256 CUs, so the N
+    workers' solves of a round run side by side instead of back to back.
+    Round start: every lane waits for the previous server update (main
+    stream); round end: the server update waits for every lane."""
+
+    def __init__(self, device, workers):
+        self.device = torch.device(device)
+        self.streams = {w.k: torch.cuda.Stream(self.device) for w in workers}
+        self.done = {w.k: torch.cuda.Event() for w in workers}
+        self.start = torch.cuda.Event()
+
+    def begin(self):
+        self.start.record(torch.cuda.current_stream(self.device))
+        for st in self.streams.values():
+            st.wait_event(self.start)
+
+    def on(self, w):
+        return torch.cuda.stream(self.streams[w.k])
+
+    def join(self, workers):
+        main = torch.cuda.current_stream(self.device)
+        for w in workers:
+            ev = self.done[w.k]
+            ev.record(self.streams[w.k])
+            main.wait_event(ev)
 
 
 class _Null:

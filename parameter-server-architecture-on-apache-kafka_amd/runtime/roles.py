@@ -20,7 +20,7 @@ import torch
 from .. import _native
 from ..models.logreg import ModelSpec
 from ..models.wide import WideSpec
-from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply
+from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply, stream_handle
 from ..ops.sparse import SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide_server_apply
 from .buffer import DeviceRing, StreamSource
 from .config import PSConfig
@@ -188,6 +188,15 @@ class ServerRole:
             self.apply_and_log(deltas[0], vc, log, lr)
             return
         if all(isinstance(d, torch.Tensor) for d in deltas):
+            if self.frag is not None and not self.wide and len(deltas) <= 16:  # one fused kernel
+                self.side.fence()
+                sp = self.spec
+                _native.hip().server_apply_n(sp.K, sp.F, sp.Fp, self.w.data_ptr(), [d.data_ptr() for d in deltas],
+                                             float(self.cfg.lr if lr is None else lr), self.frag.hi.data_ptr(),
+                                             self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
+                                             stream_handle(self.device), self.frag.coff)
+                self.log_eval(vc, log)
+                return
             self.acc.copy_(deltas[0])
             for d in deltas[1:]:
                 self.acc.add_(d)

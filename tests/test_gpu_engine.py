@@ -112,3 +112,17 @@ def test_paired_eval_rows_match_unpaired(cuda, N):
     w1 = sorted((r[1], r[2], r[5]) for r in books[1].worker)
     assert len(w0) == len(w1) == 12 * N
     assert max(abs(a[2] - b[2]) for a, b in zip(w0, w1)) < 0.05
+
+
+def test_concurrent_worker_lanes_match_sequential(cuda):
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    ws, books = [], []
+    for conc in (True, False):
+        eng = LocalEngine(_cfg(num_workers=4, max_iters=10, init="random", concurrent_workers=conc,
+                               min_buffer_size=256, max_buffer_size=256), cuda, train=train, test=test)
+        out = eng.run()
+        assert out["rounds"] == 10 and out["updates"] == 40
+        ws.append(eng.server.w.cpu())
+        books.append(eng.log.book)
+    assert torch.allclose(ws[0], ws[1], atol=1e-4 * max(1.0, ws[1].abs().max().item()))
+    assert len(books[0].worker) == len(books[1].worker) == 40 and len(books[0].server) == 10

@@ -232,3 +232,19 @@ def test_paired_eval_matches_single(cuda):
     (wr1, wr2), (sr1, sr2) = book.worker, book.server
     assert wr1[1:] == wr2[1:] and sr1 == sr2 and sr1[0] == 1234
     assert scratch.acc.abs().sum().item() == 0
+
+
+def test_server_apply_n_matches_sum(cuda):
+    from psx import _native
+    from psx.ops.lr import stream_handle
+
+    spec = ModelSpec(1024, 6)
+    w = _rand_w(spec, 31).to(cuda)
+    deltas = [_rand_w(spec, 40 + i, 0.1).to(cuda) for i in range(5)]
+    ref = w + 0.2 * sum(deltas)
+    frag = Fragments(spec, cuda, coff=3)
+    _native.hip().server_apply_n(spec.K, spec.F, spec.Fp, w.data_ptr(), [d.data_ptr() for d in deltas], 0.2,
+                                 frag.hi.data_ptr(), frag.lo.data_ptr(), frag.b.data_ptr(), stream_handle(cuda), 3)
+    torch.cuda.synchronize()
+    assert torch.allclose(w, ref, atol=1e-6)
+    assert torch.allclose(frag.b[3:3 + spec.K], spec.intercept(ref), atol=1e-6)

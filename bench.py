@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--workers", type=int, default=1,
+                    help="single-GPU run: in-process workers sharing the GPU (one HIP stream each); default 1")
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
@@ -135,7 +137,7 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
         vs = None  # the reference never ran this configuration
     mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
     if world == 1:
-        par = f"ps-{mode} w1 (server colocated)"
+        par = f"ps-{mode} w{n_workers} (server colocated{', workers share the GPU' if n_workers > 1 else ''})"
     elif async_mode:
         par = f"ps-{mode} 1 server + {n_workers} workers (RCCL p2p{', sparse push' if wide else ''})"
     else:
@@ -183,7 +185,7 @@ def main(argv=None):
     from psx.runtime.engine import LocalEngine
 
     train, test = make_data(a, device)
-    cfg = build_cfg(a, 1)
+    cfg = build_cfg(a, a.workers)
     cfg.max_iters = a.warmup
     eng = LocalEngine(cfg, device, train=train, test=test)
     eng.run() if a.warmup > 0 else None

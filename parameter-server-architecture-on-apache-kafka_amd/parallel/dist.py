@@ -65,11 +65,21 @@ def init_from_env(cpu: bool = False):
         device = torch.device("cpu")
         backend = "gloo"
     else:
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
-        backend = "nccl"
+        # PSX_GPU_OVERSUBSCRIBE=1 (tests only): every rank on GPU 0 over gloo, so the
+        # multi-rank GPU schedules can be exercised on a one-GPU machine (RCCL
+        # refuses two ranks on one device)
+        over = os.environ.get("PSX_GPU_OVERSUBSCRIBE") == "1"
+        idx = 0 if over else local
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
+        backend = "gloo" if over else "nccl"
     if not dist.is_initialized():
         kw = {"device_id": device} if backend == "nccl" else {}
+        timeout = float(os.environ.get("PSX_PG_TIMEOUT_S", "0") or 0)
+        if timeout > 0:
+            import datetime
+
+            kw["timeout"] = datetime.timedelta(seconds=timeout)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, world, device
 

@@ -175,6 +175,10 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
 
 def main(argv=None):
     a = parse(argv)
+    if os.environ.get("PSX_HANG_DUMP_S"):  # debugging aid: dump every thread's stack, then exit
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["PSX_HANG_DUMP_S"]), exit=True)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

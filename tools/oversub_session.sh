@@ -3,6 +3,9 @@
 # (PSX_GPU_OVERSUBSCRIBE=1; RCCL itself needs one GPU per rank).  Exercises the
 # DistEngine GPU paths (replica aliasing, paired eval on rank 0, in-place
 # sharded all-gather, sparse p2p pushes, watchdog tokens) before an 8-GPU run.
+# Limitation of THIS harness only: gloo p2p of CUDA tensors of tens of MB in
+# both directions at once stalls (ASP with 2^20 x 8 weights), so the wide runs
+# use smaller feature spaces; RCCL p2p has no such issue and CPU gloo passes.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/oversub
@@ -24,7 +27,7 @@ done <<'LIST'
 3 --steps 200 --warmup 20 --schedule reduce_bcast
 3 --steps 100 --warmup 10 --consistency -1
 3 --steps 100 --warmup 10 --consistency 2
-3 --model sparse1m --train-rows 200000 --steps 100 --warmup 10
-2 --model sharded100m --train-rows 200000 --steps 50 --warmup 5
+3 --model sparse1m --features 100000 --train-rows 200000 --steps 100 --warmup 10
+2 --model sharded100m --features 10000000 --train-rows 200000 --steps 50 --warmup 5
 LIST
 echo oversub done

@@ -141,3 +141,30 @@ def test_wide_async_push(sparse_push):
     out, w = _run(3, dict(BASE, consistency_model=-1, max_iters=6, _data="wide", max_buffer_size=256,
                           min_buffer_size=64, sparse_push=sparse_push))
     assert out["updates"] == 12 and torch.isfinite(w).all()
+
+
+@pytest.mark.parametrize("c,bound", [(0, 1), (2, 3), (-1, None)])
+def test_log_derived_vc_gap(tmp_path, c, bound):
+    """The reference validates its consistency models from the logs
+    (iteration-vs-time plots, README.md:299-321); automated here: with a
+    straggler (worker 1 sleeps per iteration) the max in-flight vector-clock
+    gap read back from logs-worker.csv stays within the model's bound
+    (BSP <= 1 and SSP(D) <= D + 1 as logged -- SURVEY §4), and ASP runs ahead."""
+    import pandas as pd
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from plot_logs import max_vc_gap
+
+    kw = dict(BASE, consistency_model=c, max_iters=12, logging=True, log_dir=str(tmp_path),
+              inject_worker_delay_ms={1: 40.0})
+    if c != 0:
+        kw["server_colocated"] = False
+    out, _ = _run(3, kw)
+    w = pd.read_csv(tmp_path / "logs-worker.csv", sep=";")
+    s = pd.read_csv(tmp_path / "logs-server.csv", sep=";")
+    assert list(s.columns) == ["timestamp", "partition", "vectorClock", "loss", "fMeasure", "accuracy"]
+    gap = max_vc_gap(w)
+    if bound is not None:
+        assert gap <= bound, gap
+    else:
+        assert gap >= 3, gap  # eventual consistency: the fast worker is not held back

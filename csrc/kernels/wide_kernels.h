@@ -94,7 +94,6 @@ struct WideDev {
   // outputs (caller-owned)
   float* dloc;         // [PLmax] local delta (intercepts first)
   float* wloc;         // [PLmax] local new weights
-  int32_t* uniq_out;   // == uniq (exported)
   float* loss;         // [1]
   int* stats;          // [4] evals, accepted steps, ls failures, direction resets
   float* delta_dense;  // [F*KP + KP] (dense_delta)

@@ -91,7 +91,6 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.loss_acc = reinterpret_cast<double*>(b + o_loss);
   dv_.dloc = buf.dloc;
   dv_.wloc = buf.wloc;
-  dv_.uniq_out = dv_.uniq;
   dv_.loss = buf.loss;
   dv_.stats = buf.stats;
   dv_.delta_dense = buf.delta_dense;

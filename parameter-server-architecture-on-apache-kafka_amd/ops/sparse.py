@@ -103,11 +103,6 @@ class SparseRing:
             self.nnz[d] = k
             self.y[d] = ds.y[s]
 
-    def window(self, B: int, start: int):
-        """(slots, entries) of the window on the CPU: lists of (row, feature ids, values, label)."""
-        slots = (torch.arange(B) + start) % self.cap
-        return slots
-
 
 class SparseDelta:
     """A worker's push in the window subspace: ``dloc`` = KP intercepts then U*KP coefficients of features ``uniq``."""

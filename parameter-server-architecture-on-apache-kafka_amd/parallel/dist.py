@@ -232,6 +232,7 @@ class DistEngine:
         t_start = time.time()
         r = self.rounds
         check_every = 1 if not cfg.max_iters else 0
+        ingested_ahead = False
         while True:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
@@ -239,8 +240,9 @@ class DistEngine:
                 break
             self.tracer.round_begin()
             with self.tracer.span("ingest"):
-                if wk is not None:
+                if wk is not None and not ingested_ahead:
                     wk.ingest()
+            ingested_ahead = False
             logged = False
             if sched == "allreduce":
                 # solve -> allreduce launched on the RCCL stream -> the evaluation rows
@@ -253,6 +255,11 @@ class DistEngine:
                     work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
                     if wk is not None:
                         wk.log_eval(self.log)
+                        # the next round's stream rows land in the ring while the collective
+                        # is in flight (they overwrite only slots this round's solve has read)
+                        if not (cfg.max_iters and r + 1 - self.rounds >= cfg.max_iters):
+                            wk.ingest()
+                            ingested_ahead = True
                     work.wait()
                     srv.apply(delta, lr)
                     if self.rank == 0:

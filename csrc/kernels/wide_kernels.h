@@ -71,7 +71,7 @@ struct WideDev {
   // workspace
   WideParams* prm;
   Ctrl* ctrl;
-  unsigned* cnt;       // [0] U, [1] dots ticket, [2] U of the previous solve, [3] unused
+  unsigned* cnt;       // [0] U, [1] dots ticket, [2] U of the previous solve, [3] tail barrier error
   int32_t* map;        // [F] local id or -1 (-2 transiently)
   int32_t* uniq;       // [umax] local id -> feature
   int32_t* lid;        // [cap*NZ] window entry -> local id
@@ -83,6 +83,7 @@ struct WideDev {
   int32_t* blid;       // [ngroups][EB] their local ids
   int32_t* bcount;     // [ngroups] distinct features per group
   int RB, EB, TS;      // rows per group, EB = RB*NZ, LDS hash size (pow2 >= 2*EB)
+  unsigned long long* gbar;  // grid-barrier counter of the tail launch (reset per solve)
   float* s1;           // [umax] feature sums over the window
   float* s2;           // [umax] feature sums of squares
   float* scale;        // [umax] effective coefficient = scale * x
@@ -112,6 +113,9 @@ int wide_rows_per_group(int NZ, int KP);
 void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s);  // cleanup + params
 void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s);  // remap, assign, stats, prep
 void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dots, hipStream_t s);
+// Line-search retry slots [s0, s1) in one persistent launch (grid barriers).
+void wide_launch_tail(const WideCfg& c, const WideDev& d, int s0, int s1, hipStream_t s);
+void wide_prepare_kernels();  // LDS attributes of the tail kernels (call before capture)
 void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s);
 int wide_dots_blocks(int64_t PLmax);
 

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int s
     d.prm->start = start;
     d.cnt[0] = 0u;  // not read by anybody else in this kernel
     d.cnt[1] = 0u;
+    *d.gbar = 0ull;  // grid-barrier counter of this solve's tail launch
   }
   for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256) d.map[d.uniq[i]] = -1;
 }
@@ -280,25 +281,34 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
 }
 
 // ---------------------------------------------------------------------------
+// Shared-memory blocks of the slot phases (static in each kernel that runs them).
+struct WideFwdShared {
+  float red_r[8][16];
+  double red_l[8];
+};
+struct WideDotsShared {
+  double red[8][kWideND];
+  double dots[kWideND];
+  int last;
+  CtrlScratch ws;
+  Ctrl ctrl;
+};
+
 // One function evaluation at x + t d: margins, softmax/CE, gradient.  One
 // wavefront per window row, RB rows (one group of the plan) per workgroup; the
 // rows' gradient contributions are summed in LDS per distinct feature of the
 // group and flushed with one global atomic per (feature, class).
 template <int KP, int NQ>
-__global__ __launch_bounds__(512) void wide_fwdbwd_kernel(WideCfg c, WideDev d, int slot) {
-  extern __shared__ __attribute__((aligned(16))) float gacc[];  // [EB][KP]
+__device__ __forceinline__ void wide_fwdbwd_body(const WideCfg& c, const WideDev& d, int slot, int grp, float* gacc,
+                                                 WideFwdShared& sh) {
   const Ctrl* ctrl = d.ctrl;
-  if (ctrl->phase == kPhDone) return;
   const int B = d.prm->B, start = d.prm->start, NZ = c.NZ, cap = c.cap, K = c.K, RB = d.RB;
-  const int b = blockIdx.x;
-  const int r0 = b * RB;
-  if (r0 >= B) return;
+  const int r0 = grp * RB;
+  if (r0 >= B) return;  // uniform per workgroup
   const float t = (float)ctrl->t;
   const float invB = 1.f / (float)B;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nthr = blockDim.x;
-  __shared__ float red_r[8][KP];
-  __shared__ double red_l[8];
-  const int n = d.bcount[b];
+  const int n = d.bcount[grp];
   for (int i = threadIdx.x; i < n * KP; i += nthr) gacc[i] = 0.f;
   __syncthreads();
   const float* __restrict__ X = d.x;
@@ -362,52 +372,56 @@ __global__ __launch_bounds__(512) void wide_fwdbwd_kernel(WideCfg c, WideDev d, 
   }
   if (lane == 0 && wv < 8) {
 #pragma unroll
-    for (int k = 0; k < KP; ++k) red_r[wv][k] = rr[k];
-    red_l[wv] = lrow;
+    for (int k = 0; k < KP; ++k) sh.red_r[wv][k] = rr[k];
+    sh.red_l[wv] = lrow;
   }
   __syncthreads();
   const int nw = nthr >> 6;
   if (threadIdx.x < KP && threadIdx.x < K) {
     float sr = 0.f;
-    for (int w = 0; w < nw; ++w) sr += red_r[w][threadIdx.x];
+    for (int w = 0; w < nw; ++w) sr += sh.red_r[w][threadIdx.x];
     if (sr != 0.f) atomicAdd(d.g_t + threadIdx.x, sr);
   }
   if (threadIdx.x == 0) {
     double sl = 0.0;
-    for (int w = 0; w < nw; ++w) sl += red_l[w];
+    for (int w = 0; w < nw; ++w) sl += sh.red_l[w];
     if (sl != 0.0) atomicAdd(d.loss_acc + slot, sl);
   }
-  const int32_t* glid = d.blid + (int64_t)b * d.EB;
+  const int32_t* glid = d.blid + (int64_t)grp * d.EB;
   for (int i = threadIdx.x; i < n * K; i += nthr) {
     const int si = i / K, k = i - si * K;
     const float v = gacc[si * KP + k];
     if (v != 0.f) atomicAdd(d.g_t + KP + (int64_t)glid[si] * KP + k, v);
   }
+  __syncthreads();  // gacc is reused by the workgroup's next group
 }
 
+template <int KP, int NQ>
+__global__ __launch_bounds__(512) void wide_fwdbwd_kernel(WideCfg c, WideDev d, int slot) {
+  extern __shared__ __attribute__((aligned(16))) float gacc[];  // [EB][KP]
+  __shared__ WideFwdShared sh;
+  if (d.ctrl->phase == kPhDone) return;
+  wide_fwdbwd_body<KP, NQ>(c, d, slot, blockIdx.x, gacc, sh);
+}
 
 // Dot products of the new gradient (ctrl dots layout, solver_ctrl.h) + the
-// controller step in the last-arriving workgroup.
-__global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, int slot) {
+// controller step in the last-arriving workgroup (of nblk; workgroup `blk`).
+__device__ __forceinline__ void wide_dots_body(const WideCfg& c, const WideDev& d, int slot, int blk, int nblk,
+                                               WideDotsShared& sh) {
   Ctrl* ctrl = d.ctrl;
-  if (ctrl->phase == kPhDone) return;
-  __shared__ double red[4][kWideND];
-  __shared__ double dots[kWideND];
-  __shared__ int last;
-  __shared__ CtrlScratch ws;
-  __shared__ Ctrl ctrl_lds;
   static_assert(sizeof(Ctrl) % 8 == 0, "Ctrl is copied as 64-bit words");
   const int H = c.sc.hist;
   const int m = ctrl->m;
   const unsigned U = d.cnt[0];
+  const int nthr = blockDim.x, nw = nthr >> 6;
   const int64_t PL = c.KP + (int64_t)U * c.KP, PLmax = d.PLmax;
   long long* stp = d.dbg ? d.dbg + slot * 8 : nullptr;
-  if (stp && blockIdx.x == 0 && threadIdx.x == 0) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (stp && blk == 0 && threadIdx.x == 0) stp[0] = (long long)__builtin_amdgcn_s_memrealtime();
   double a0 = 0.0, a1 = 0.0, a2 = 0.0;
   double aS[kMaxHist], aY[kMaxHist];
 #pragma unroll
   for (int i = 0; i < kMaxHist; ++i) aS[i] = aY[i] = 0.0;
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < PL; p += (int64_t)gridDim.x * 256) {
+  for (int64_t p = (int64_t)blk * nthr + threadIdx.x; p < PL; p += (int64_t)nblk * nthr) {
     const float g = d.g_t[p];
     a0 += (double)g * g;
     a1 += (double)g * d.d[p];
@@ -425,9 +439,9 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
   a1 = wave_sum(a1);
   a2 = wave_sum(a2);
   if (lane == 0) {
-    red[wv][0] = a0;
-    red[wv][1] = a1;
-    red[wv][2] = a2;
+    sh.red[wv][0] = a0;
+    sh.red[wv][1] = a1;
+    sh.red[wv][2] = a2;
   }
 #pragma unroll
   for (int i = 0; i < kMaxHist; ++i) {
@@ -435,8 +449,8 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
       const double s = wave_sum(aS[i]);
       const double y = wave_sum(aY[i]);
       if (lane == 0) {
-        red[wv][3 + i] = s;
-        red[wv][3 + H + i] = y;
+        sh.red[wv][3 + i] = s;
+        sh.red[wv][3 + H + i] = y;
       }
     }
   }
@@ -445,18 +459,20 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
   if (threadIdx.x < nd) {
     const int k = threadIdx.x;
     const bool used = k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m);
-    const double s = used ? red[0][k] + red[1][k] + red[2][k] + red[3][k] : 0.0;
+    double s = 0.0;
+    if (used)
+      for (int w = 0; w < nw; ++w) s += sh.red[w][k];
     // write-through hand-off: agent-scope stores, drained before the ticket,
     // agent-scope loads by the last workgroup -- no L2 writeback fence
-    __hip_atomic_store((gu64w*)(d.part + (int64_t)blockIdx.x * kWideND + k), __builtin_bit_cast(unsigned long long, s),
+    __hip_atomic_store((gu64w*)(d.part + (int64_t)blk * kWideND + k), __builtin_bit_cast(unsigned long long, s),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(&d.cnt[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    sh.last = __hip_atomic_fetch_add(&d.cnt[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1;
   __syncthreads();
-  if (!last) return;
+  if (!sh.last) return;
   if (stp && threadIdx.x == 0) stp[1] = (long long)__builtin_amdgcn_s_memrealtime();
   // thread b loads workgroup b's partials -- only the dots the controller
   // reads (3 + 2m of them), all loads in flight together -- then one wave
@@ -465,49 +481,61 @@ __global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, in
 #pragma unroll
   for (int k = 0; k < kWideND; ++k) {
     const bool used = k < nd && (k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m));
-    v[k] = (used && threadIdx.x < gridDim.x) ? ld_agent_f64(d.part + (int64_t)threadIdx.x * kWideND + k) : 0.0;
+    v[k] = (used && threadIdx.x < nblk) ? ld_agent_f64(d.part + (int64_t)threadIdx.x * kWideND + k) : 0.0;
   }
 #pragma unroll
   for (int k = 0; k < kWideND; ++k) {
     const bool used = k < nd && (k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m));
     if (used) {  // uniform across the block
       const double w = wave_sum(v[k]);
-      if (lane == 0) red[wv][k] = w;
+      if (lane == 0) sh.red[wv][k] = w;
     }
   }
   __syncthreads();
   if (threadIdx.x < nd) {
     const int k = threadIdx.x;
     const bool used = k < 3 || (k < 3 + H ? k - 3 < m : k - 3 - H < m);
-    dots[k] = used ? red[0][k] + red[1][k] + red[2][k] + red[3][k] : 0.0;
+    double s = 0.0;
+    if (used)
+      for (int w = 0; w < nw; ++w) s += sh.red[w][k];
+    sh.dots[k] = s;
   }
   __syncthreads();
   if (stp && threadIdx.x == 0) stp[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  // the controller is a single thread doing dependent scalar work: run it on
+  // an LDS copy of the state (an L2 round trip per access otherwise)
   constexpr int kCW = (int)(sizeof(Ctrl) / 8);
   unsigned long long* cg = reinterpret_cast<unsigned long long*>(ctrl);
-  unsigned long long* cs = reinterpret_cast<unsigned long long*>(&ctrl_lds);
-  for (int i = threadIdx.x; i < kCW; i += 256) cs[i] = cg[i];
+  unsigned long long* cs = reinterpret_cast<unsigned long long*>(&sh.ctrl);
+  for (int i = threadIdx.x; i < kCW; i += nthr) cs[i] = cg[i];
   __syncthreads();
   if (threadIdx.x == 0) {
     if (stp) stp[3] = (long long)__builtin_amdgcn_s_memrealtime();
-    d.cnt[1] = 0u;
+    __hip_atomic_store(&d.cnt[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double f = ld_agent_f64(d.loss_acc + slot) / (double)d.prm->B;
-    ctrl_step(ctrl_lds, c.sc, f, dots, slot, ws);
+    ctrl_step(sh.ctrl, c.sc, f, sh.dots, slot, sh.ws);
     if (stp) stp[4] = (long long)__builtin_amdgcn_s_memrealtime();
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kCW; i += 256) cg[i] = cs[i];
+  for (int i = threadIdx.x; i < kCW; i += nthr) cg[i] = cs[i];
   if (stp && threadIdx.x == 0) stp[5] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+__global__ __launch_bounds__(256) void wide_dots_kernel(WideCfg c, WideDev d, int slot) {
+  __shared__ WideDotsShared sh;
+  if (d.ctrl->phase == kPhDone) return;
+  wide_dots_body(c, d, slot, blockIdx.x, gridDim.x, sh);
 }
 
 // Apply the controller's decision of `slot` to the local vectors; clears g_t
 // for the next evaluation.
-__global__ __launch_bounds__(256) void wide_apply_kernel(WideCfg c, WideDev d, int slot) {
+__device__ __forceinline__ void wide_apply_body(const WideCfg& c, const WideDev& d, int slot, int blk, int nblk) {
   const Ctrl* ctrl = d.ctrl;
   if (ctrl->action_slot != slot) return;
   const int act = ctrl->action;
   if (act == kActDone) return;
   const unsigned U = d.cnt[0];
+  const int nthr = blockDim.x;
   const int64_t PL = c.KP + (int64_t)U * c.KP, PLmax = d.PLmax;
   const float ta = (float)ctrl->t_acc;
   const int ps = ctrl->push_slot;
@@ -519,7 +547,7 @@ __global__ __launch_bounds__(256) void wide_apply_kernel(WideCfg c, WideDev d, i
     cs[i] = i < m ? (float)ctrl->cs[i] : 0.f;
     cy[i] = i < m ? (float)ctrl->cy[i] : 0.f;
   }
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < PL; p += (int64_t)gridDim.x * 256) {
+  for (int64_t p = (int64_t)blk * nthr + threadIdx.x; p < PL; p += (int64_t)nblk * nthr) {
     const float gt = d.g_t[p];
     d.g_t[p] = 0.f;
     if (act == kActInit) {
@@ -541,6 +569,64 @@ __global__ __launch_bounds__(256) void wide_apply_kernel(WideCfg c, WideDev d, i
         d.d[p] = nd;
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void wide_apply_kernel(WideCfg c, WideDev d, int slot) {
+  wide_apply_body(c, d, slot, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// wide_tail_kernel: the line-search retry slots [s0, s1) in ONE persistent
+// launch.  The usual solve is over after 1 + iters evaluations (every line
+// search accepts its first trial), so this launch exits at once; otherwise each
+// slot runs fwdbwd -> grid barrier -> dots + controller -> grid barrier ->
+// apply -> grid barrier, instead of three mostly-empty launches per budgeted
+// slot.  Grid <= 64 workgroups of 512 threads: co-resident on 256 CUs.
+// Barrier: every wave drains its stores, lane 0 releases at agent scope,
+// arrives on a monotone counter and polls it (agent-scope loads), acquires.
+__device__ __forceinline__ void wide_grid_barrier(unsigned long long* ctr, unsigned long long target,
+                                                  unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)__hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load((gu64w*)ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 24)) {  // never expected: a workgroup was not co-resident
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int KP, int NQ>
+__global__ __launch_bounds__(512) void wide_tail_kernel(WideCfg c, WideDev d, int s0, int s1) {
+  extern __shared__ __attribute__((aligned(16))) float gacc[];  // [EB][KP]
+  __shared__ WideFwdShared fsh;
+  __shared__ WideDotsShared dsh;
+  __shared__ int phase_s;
+  const int G = gridDim.x;
+  unsigned long long nb = 0;
+  for (int slot = s0; slot < s1; ++slot) {
+    if (threadIdx.x == 0)
+      phase_s = __hip_atomic_load(&d.ctrl->phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (phase_s == kPhDone) break;  // uniform: every workgroup read the word after the last barrier
+    const int B = d.prm->B;
+    for (int grp = blockIdx.x; grp * d.RB < B; grp += G) wide_fwdbwd_body<KP, NQ>(c, d, slot, grp, gacc, fsh);
+    wide_grid_barrier(d.gbar, (unsigned long long)G * ++nb, d.cnt + 3);
+    wide_dots_body(c, d, slot, blockIdx.x, G, dsh);
+    wide_grid_barrier(d.gbar, (unsigned long long)G * ++nb, d.cnt + 3);
+    wide_apply_body(c, d, slot, blockIdx.x, G);
+    wide_grid_barrier(d.gbar, (unsigned long long)G * ++nb, d.cnt + 3);
   }
 }
 
@@ -640,6 +726,59 @@ void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dot
   }
   wide_dots_kernel<<<nblk_dots, 256, 0, s>>>(c, d, slot);
   wide_apply_kernel<<<grid_for(d.PLmax, 1024), 256, 0, s>>>(c, d, slot);
+}
+
+int wide_tail_grid(const WideCfg& c, const WideDev& d) {
+  const int g = ngroups(c, d);
+  return g < 64 ? g : 64;
+}
+
+template <int KP>
+static void launch_tail_kp(const WideCfg& c, const WideDev& d, int s0, int s1, hipStream_t s) {
+  const int nq = (c.NZ + 63) / 64;
+  const int G = wide_tail_grid(c, d);
+  const size_t lds = (size_t)d.EB * KP * 4;
+  if (nq <= 1)
+    wide_tail_kernel<KP, 1><<<G, 512, lds, s>>>(c, d, s0, s1);
+  else if (nq <= 2)
+    wide_tail_kernel<KP, 2><<<G, 512, lds, s>>>(c, d, s0, s1);
+  else if (nq <= 4)
+    wide_tail_kernel<KP, 4><<<G, 512, lds, s>>>(c, d, s0, s1);
+  else
+    wide_tail_kernel<KP, 8><<<G, 512, lds, s>>>(c, d, s0, s1);
+}
+
+void wide_launch_tail(const WideCfg& c, const WideDev& d, int s0, int s1, hipStream_t s) {
+  switch (c.KP) {
+    case 1: launch_tail_kp<1>(c, d, s0, s1, s); break;
+    case 2: launch_tail_kp<2>(c, d, s0, s1, s); break;
+    case 4: launch_tail_kp<4>(c, d, s0, s1, s); break;
+    case 8: launch_tail_kp<8>(c, d, s0, s1, s); break;
+    default: launch_tail_kp<16>(c, d, s0, s1, s); break;
+  }
+}
+
+template <int KP, int NQ>
+static void set_tail_attr() {
+  (void)hipFuncSetAttribute((const void*)wide_tail_kernel<KP, NQ>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            96 * 1024);
+}
+template <int KP>
+static void set_tail_attr_kp() {
+  set_tail_attr<KP, 1>();
+  set_tail_attr<KP, 2>();
+  set_tail_attr<KP, 4>();
+  set_tail_attr<KP, 8>();
+}
+void wide_prepare_kernels() {
+  static bool done = false;
+  if (done) return;
+  set_tail_attr_kp<1>();
+  set_tail_attr_kp<2>();
+  set_tail_attr_kp<4>();
+  set_tail_attr_kp<8>();
+  set_tail_attr_kp<16>();
+  done = true;
 }
 
 void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s) {

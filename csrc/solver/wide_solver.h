@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../kernels/wide_kernels.h"
@@ -51,7 +52,10 @@ class WideSolver {
   // s_memrealtime ticks (100 MHz): entry, last block in, dots reduced, ctrl loaded, ctrl stepped, ctrl stored
   std::vector<long long> read_stamps(hipStream_t stream);
   size_t workspace_bytes() const { return ws_bytes_; }
-  int kernels_per_solve() const { return 5 + 3 * cfg_.sc.nslots + 1; }
+  int kernels_per_solve() const {
+    const int nf = cfg_.sc.mode == 1 ? cfg_.sc.nslots : std::min(cfg_.sc.nslots, 1 + cfg_.sc.iters);
+    return 5 + 3 * nf + (cfg_.sc.nslots > nf ? 1 : 0) + 1;
+  }
 
  private:
   void enqueue_body(hipStream_t s, int B, int start);

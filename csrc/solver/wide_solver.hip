@@ -35,7 +35,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
     off = align256(off + bytes);
     return o;
   };
-  const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16);
+  const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16), o_gbar = take(8);
   const size_t o_map = take((size_t)cfg.F * 4), o_lid = take((size_t)E * 4);
   const int RB = wide_rows_per_group(cfg.NZ, KP), EB = RB * cfg.NZ;
   int TS = 1;
@@ -47,7 +47,10 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   const size_t o_x = take(PLmax * 4), o_d = take(PLmax * 4), o_gt = take(PLmax * 4), o_gc = take(PLmax * 4),
                o_w0 = take(PLmax * 4);
   const size_t o_S = take(H * PLmax * 4), o_Y = take(H * PLmax * 4);
-  const size_t o_part = take((size_t)nblk_dots_ * kWideND * 8), o_loss = take((size_t)cfg.sc.nslots * 8);
+  // dot partials: one row per workgroup of the dots launches (nblk_dots_) AND of the
+  // persistent tail (up to 64 workgroups)
+  const int npart = nblk_dots_ > 64 ? nblk_dots_ : 64;
+  const size_t o_part = take((size_t)npart * kWideND * 8), o_loss = take((size_t)cfg.sc.nslots * 8);
   const bool stamps = std::getenv("PSX_WIDE_STAMPS") != nullptr;
   const size_t o_dbg = stamps ? take((size_t)cfg.sc.nslots * 8 * 8) : 0;
   ws_bytes_ = off;
@@ -66,6 +69,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.prm = reinterpret_cast<WideParams*>(b + o_prm);
   dv_.ctrl = reinterpret_cast<Ctrl*>(b + o_ctrl);
   dv_.cnt = reinterpret_cast<unsigned*>(b + o_cnt);
+  dv_.gbar = reinterpret_cast<unsigned long long*>(b + o_gbar);
   dv_.map = reinterpret_cast<int32_t*>(b + o_map);
   dv_.uniq = buf.uniq;
   dv_.lid = reinterpret_cast<int32_t*>(b + o_lid);
@@ -98,6 +102,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
   dv_.PLmax = PLmax;
 
+  wide_prepare_kernels();  // before any capture
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
@@ -140,7 +145,13 @@ WideSolver::~WideSolver() {
 void WideSolver::enqueue_body(hipStream_t s, int B, int start) {
   wide_launch_begin(cfg_, dv_, B, start, s);
   wide_launch_prepare(cfg_, dv_, s);
-  for (int slot = 0; slot < cfg_.sc.nslots; ++slot) wide_launch_slot(cfg_, dv_, slot, nblk_dots_, s);
+  // slots launched one by one: the initial evaluation + one trial per iteration
+  // (a solve whose line searches accept their first trial); the retry budget
+  // runs in the persistent tail launch
+  const int nfast = cfg_.sc.mode == 1 ? cfg_.sc.nslots
+                                      : (1 + cfg_.sc.iters < cfg_.sc.nslots ? 1 + cfg_.sc.iters : cfg_.sc.nslots);
+  for (int slot = 0; slot < nfast; ++slot) wide_launch_slot(cfg_, dv_, slot, nblk_dots_, s);
+  if (cfg_.sc.nslots > nfast) wide_launch_tail(cfg_, dv_, nfast, cfg_.sc.nslots, s);
   if (cfg_.dense_delta)
     hip_check(hipMemsetAsync(dv_.delta_dense, 0, (size_t)(cfg_.F * cfg_.KP + cfg_.KP) * 4, s), "memset delta");
   wide_launch_finalize(cfg_, dv_, s);

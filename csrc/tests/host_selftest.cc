@@ -6,7 +6,9 @@
 //   SlidingWindow + RateEstimator (cases I/II/III, ring wrap),
 //   CtrlQueue (POSIX-shm MPSC: 4 producer threads, 1 consumer),
 //   csv_probe / csv_load (header detection, multithreaded parse, bf16),
-//   CsvLogger + MetricsSink (producer thread publishing EvalSlots).
+//   CsvLogger + MetricsSink (producer thread publishing EvalSlots),
+//   tracker fault handling (retire / bsp_round),
+//   libsvm_save / libsvm_load round trip (multithreaded mmap parser).
 // Exit status 0 = all checks passed.
 #include <atomic>
 #include <cmath>
@@ -20,6 +22,7 @@
 
 #include "../host/ctrl.h"
 #include "../host/dataset.h"
+#include "../host/libsvm.h"
 #include "../host/logger.h"
 #include "../host/metrics_sink.h"
 #include "../host/sampling.h"
@@ -71,6 +74,64 @@ static void test_tracker() {
     threw = true;
   }
   CHECK(threw);
+}
+
+static void test_tracker_faults() {
+  // BSP with 3 workers: 0 and 1 wait for worker 2, which then fails; retiring
+  // it releases the two waiting workers with the next version.
+  VectorClockTracker bsp(3, 0);
+  CHECK(bsp.on_delta(0, 0).empty());
+  CHECK(bsp.on_delta(1, 0).empty());
+  auto rel = bsp.retire(2);
+  CHECK(rel.size() == 2);
+  for (auto& p : rel) CHECK(p.first != 2 && p.second == 1);
+  CHECK(!bsp.is_live(2) && bsp.num_live() == 2);
+  CHECK(bsp.min_clock() == 1);  // the dead worker's clock no longer counts
+  // later rounds involve the live workers only
+  CHECK(bsp.on_delta(0, 1).empty());
+  CHECK(bsp.on_delta(1, 1).size() == 2);
+  // SSP(0 slack = 1): a retired straggler stops holding the fast worker back
+  VectorClockTracker ssp(2, 1);
+  auto r = ssp.on_delta(0, 0);
+  CHECK(r.size() == 1 && r[0].second == 1);
+  CHECK(ssp.on_delta(0, 1).empty());  // 2 ahead of worker 1 -> held
+  auto r2 = ssp.retire(1);
+  CHECK(r2.size() == 1 && r2[0].first == 0 && r2[0].second == 2);
+  // whole BSP rounds in one call (the collective schedules)
+  VectorClockTracker b2(4, 0);
+  for (int64_t v = 0; v < 5; ++v) b2.bsp_round(v);
+  for (int k = 0; k < 4; ++k) CHECK(b2.clock(k) == 5 && b2.is_sent(k));
+  CHECK(b2.max_gap() <= 1);  // same as applying the deltas one by one
+}
+
+static void test_libsvm() {
+  char path[] = "/tmp/psx_selftest_svm_XXXXXX";
+  int fd = mkstemp(path);
+  CHECK(fd >= 0);
+  close(fd);
+  const int64_t rows = 5000;
+  std::vector<int64_t> indptr(1, 0);
+  std::vector<int32_t> idx;
+  std::vector<uint16_t> val;
+  std::vector<int32_t> y(rows);
+  for (int64_t r = 0; r < rows; ++r) {
+    const int n = (int)(r % 7);
+    for (int j = 0; j < n; ++j) {
+      idx.push_back((int32_t)((r * 131 + j * 977) % 100000 + j));
+      val.push_back(f32_to_bf16(0.25f * (float)(j + 1) * ((r & 1) ? -1.f : 1.f)));
+    }
+    indptr.push_back((int64_t)idx.size());
+    y[r] = (int32_t)(r % 5 + 1);
+  }
+  for (int zb = 0; zb < 2; ++zb) {
+    libsvm_save(path, indptr.data(), idx.data(), val.data(), y.data(), rows, zb != 0);
+    SparseRows s = libsvm_load(path, zb != 0, 4);
+    CHECK((int64_t)s.y.size() == rows && s.indptr == indptr && s.idx == idx && s.val == val && s.y == y);
+    int32_t mx = -1;
+    for (auto i : idx) mx = i > mx ? i : mx;
+    CHECK(s.max_feature == mx);
+  }
+  unlink(path);
 }
 
 static void test_window() {
@@ -196,6 +257,8 @@ static void test_metrics_sink() {
 
 int main() {
   test_tracker();
+  test_tracker_faults();
+  test_libsvm();
   test_window();
   test_ctrl_queue();
   test_csv();

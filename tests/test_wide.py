@@ -51,6 +51,25 @@ def test_libsvm_roundtrip(tmp_path):
     assert torch.equal(back.val.view(torch.int16), ds.val.view(torch.int16)) and torch.equal(back.y, ds.y)
 
 
+def test_libsvm_parser_edge_cases(tmp_path):
+    p = tmp_path / "e.svm"
+    p.write_text("# header comment\n3 1:0.5 7:-2 # trailing comment\n\n1\n  5 2:0 4:1e-1\r\n2 3:1.5")
+    ds = load_libsvm(str(p))
+    assert ds.y.tolist() == [3, 1, 5, 2] and ds.num_features == 7
+    assert ds.indptr.tolist() == [0, 2, 2, 3, 4]  # empty row kept, explicit zero dropped
+    assert ds.idx.tolist() == [0, 6, 3, 2]  # 1-based on disk
+    assert torch.allclose(ds.val.float(), torch.tensor([0.5, -2.0, 0.1, 1.5]), atol=1e-3)
+    z = load_libsvm(str(p), zero_based=True)
+    assert z.idx.tolist() == [1, 7, 4, 3] and z.num_features == 8
+    with pytest.raises(ValueError):
+        load_libsvm(str(p), num_features=4)
+    bad = tmp_path / "bad.svm"
+    for body in ("1 3:x\n", "a 1:1\n", "1 0:1\n", "1 3\n"):
+        bad.write_text(body)
+        with pytest.raises(RuntimeError):
+            load_libsvm(str(bad))
+
+
 def test_nz_capacity():
     assert nz_capacity(3) == 8 and nz_capacity(48) == 48 and nz_capacity(49) == 56
     with pytest.raises(ValueError):

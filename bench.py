@@ -252,6 +252,7 @@ def bench_distributed(a):
         res = describe(a, world, cfg, ups, dt, summ)
         res["max_vc_gap"] = out.get("max_vc_gap")
         print(json.dumps(res), flush=True)
+    eng.close()
     dist.barrier()
     dist.destroy_process_group()
     return res

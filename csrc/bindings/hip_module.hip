@@ -10,6 +10,7 @@
 #include <memory>
 #include <stdexcept>
 
+#include "../comm/rccl_comm.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
 #include "../solver/wide_solver.h"
@@ -110,6 +111,13 @@ PYBIND11_MODULE(_psx_hip, m) {
            py::arg("wf_hi"), py::arg("wf_lo"), py::arg("b_fin"), py::arg("loss"), py::arg("stats"),
            py::arg("max_eval_wg") = 512, py::arg("use_graph") = true)
       .def("run", [](LocalSolver& s, int B, int start, uintptr_t stream) { s.run(B, start, S(stream)); })
+      .def("run_ingest",
+           [](LocalSolver& s, int B, int start, uintptr_t stream, uintptr_t src, uintptr_t ysrc, int64_t first,
+              int64_t step, int n, int dst) {
+             RingIngest ing{reinterpret_cast<const uint16_t*>(src), reinterpret_cast<const int32_t*>(ysrc), first,
+                            step, n, dst};
+             s.run(B, start, S(stream), ing);
+           })
       .def("read_ctrl",
            [](LocalSolver& s, uintptr_t stream) {
              Ctrl c;
@@ -226,6 +234,49 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("center", &WideCfg::center)
       .def_readwrite("zero_const", &WideCfg::zero_const)
       .def_readwrite("dense_delta", &WideCfg::dense_delta);
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_static("available", &RcclComm::available)
+      .def(py::init([](py::bytes id, int nranks, int rank, int device) {
+             std::string sid = id;
+             py::gil_scoped_release nogil;  // blocks until every rank has joined
+             return std::make_unique<RcclComm>(sid, nranks, rank, device);
+           }),
+           py::arg("id"), py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("all_reduce", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, uintptr_t s) {
+        c.all_reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, S(s));
+      })
+      .def("reduce", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, int root, uintptr_t s) {
+        c.reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, root, S(s));
+      })
+      .def("broadcast", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, int root, uintptr_t s) {
+        c.broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, root, S(s));
+      })
+      .def("reduce_scatter", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, uintptr_t s) {
+        c.reduce_scatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, S(s));
+      })
+      .def("all_gather", [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, uintptr_t s) {
+        c.all_gather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, S(s));
+      })
+      .def("send", [](RcclComm& c, uintptr_t buf, size_t n, int dt, int peer, uintptr_t s) {
+        c.send(reinterpret_cast<const void*>(buf), n, dt, peer, S(s));
+      })
+      .def("recv", [](RcclComm& c, uintptr_t buf, size_t n, int dt, int peer, uintptr_t s) {
+        c.recv(reinterpret_cast<void*>(buf), n, dt, peer, S(s));
+      })
+      .def_property_readonly("side_stream", [](RcclComm& c) { return reinterpret_cast<uintptr_t>(c.side_stream()); })
+      .def("fork", [](RcclComm& c, uintptr_t s) { c.fork(S(s)); })
+      .def("join", [](RcclComm& c, uintptr_t s) { c.join(S(s)); })
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("close", [](RcclComm& c) {
+        py::gil_scoped_release nogil;
+        c.close();
+      })
+      .def("abort", &RcclComm::abort);
 
   py::class_<WideSolver>(m, "WideSolver")
       .def(py::init([](const WideCfg& cfg, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz, uintptr_t ry,

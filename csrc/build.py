@@ -98,8 +98,9 @@ def build_hip(force=False, jobs=8):
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     sources = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + sorted(
         glob.glob(os.path.join(CSRC, "solver", "*.hip"))
-    ) + [os.path.join(CSRC, "bindings", "hip_module.hip")]
-    headers = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "solver", "*.h")))
+    ) + sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip"))) + [os.path.join(CSRC, "bindings", "hip_module.hip")]
+    headers = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "solver", "*.h")) +
+                     glob.glob(os.path.join(CSRC, "comm", "*.h")))
     out = os.path.join(PKG, "_psx_hip" + _ext_suffix())
     cflags = [
         "-O3",
@@ -110,7 +111,7 @@ def build_hip(force=False, jobs=8):
         "-Wno-unused-result",
         "-munsafe-fp-atomics",
     ] + ["-I" + i for i in _pybind_includes()]
-    ldflags = [f"--offload-arch={ARCH}", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"]
+    ldflags = [f"--offload-arch={ARCH}", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-ldl"]
     digest = _hash(sources + headers, cflags + ldflags)
     if not force and _up_to_date(out, digest):
         return out

@@ -44,7 +44,7 @@ size_t bwd_lds_bytes();
 int bwd_grid(int FP);
 int xch_words();
 void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int B, int start,
-                       hipStream_t s);
+                       const RingIngest& ing, hipStream_t s);
 const void* stats_prep_symbol();
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,

@@ -92,13 +92,17 @@ __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_b
 // ---------------------------------------------------------------------------
 // stats + prep: grid = FP/32 workgroups of 256 threads; 8 lanes per feature
 // read the feature-major ring copy XT in contiguous 16-B pieces of 8 rows.
+// With a fused ingest (ing.n > 0) each workgroup first copies its 32-feature
+// slice of the new rows into X / XT (and workgroup 0 the labels); the new rows'
+// statistics come from an LDS copy, the old rows' from XT as before.
 __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv, Ctrl* ctrl,
-                                                         int B_arg, int start_arg) {
+                                                         int B_arg, int start_arg, RingIngest ing) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* rs = (double*)smem;  // [32]
   double* rq = rs + 32;        // [32]
   float* sdl = (float*)(rq + 32);  // [32]
   float* ivl = sdl + 32;           // [32]
+  unsigned short* nv = (unsigned short*)(ivl + 32);  // [kMaxFusedIngest][32] new rows of this slice
   // this run's window arrives as kernel arguments (the host rewrites this graph
   // node's parameters per run); later launches read it from device memory
   const SolveParams pr{B_arg, start_arg, 0, 0};
@@ -108,6 +112,25 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   if (blockIdx.x == 0 && t == 0) *prm = pr;  // the later launches read it from device memory
   if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
   const int fs = blockIdx.x * 32;
+  const int nin = ing.n;
+  if (nin > 0) {
+    // consecutive threads take consecutive rows of one 8-feature chunk, so the
+    // 2-B XT stores of a wave land in contiguous runs of each feature row
+    for (int it = t; it < nin * 4; it += 256) {
+      const int c = it / nin, i = it - c * nin;
+      const long long sr = ing.first + (long long)i * ing.step;
+      int dr = ing.dst + i;
+      dr = dr >= cap ? dr - cap : dr;
+      const u16x8 v = *(const u16x8*)(ing.src + sr * FP + fs + c * 8);
+      *(u16x8*)(const_cast<uint16_t*>(dv.X) + (size_t)dr * FP + fs + c * 8) = v;
+      *(u16x8*)(nv + i * 32 + c * 8) = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(size_t)(fs + c * 8 + e) * cap + dr] = v[e];
+      if (blockIdx.x == 0 && c == 0) const_cast<int32_t*>(dv.y)[dr] = ing.ysrc[sr];
+    }
+  }
+  // the newest min(nin, B) window rows are the fused ones: counted from LDS
+  const int bold = B - (nin < B ? nin : B);
   const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
   const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
   float s = 0.f, q = 0.f;
@@ -125,11 +148,19 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
       const int o0 = (qq >> 2) * 32 + (qq & 3) * 8 - wt.s0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const bool in = qq < nq && o0 + e >= 0 && o0 + e < B;
+        const bool in = qq < nq && o0 + e >= 0 && o0 + e < bold;
         const float x = in ? bf2f(v[u][e]) : 0.f;
         s += x;
         q += x * x;
       }
+    }
+  }
+  if (nin > 0) {
+    __syncthreads();
+    for (int i = nin - (B - bold) + j; i < nin; i += 8) {
+      const float x = bf2f(nv[i * 32 + fl0]);
+      s += x;
+      q += x * x;
     }
   }
   double a = s, b2 = q;
@@ -799,11 +830,13 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
 }
 
 // ---------------------------------------------------------------------------
-size_t stats_prep_lds_bytes() { return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float); }
+size_t stats_prep_lds_bytes() {
+  return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float) + kMaxFusedIngest * 32 * sizeof(uint16_t);
+}
 
 void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int B, int start,
-                       hipStream_t s) {
-  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl, B, start);
+                       const RingIngest& ing, hipStream_t s) {
+  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl, B, start, ing);
 }
 const void* stats_prep_symbol() { return (const void*)stats_prep_kernel; }
 

@@ -70,6 +70,18 @@ struct SolverCfg {
   float tol;   // convergence tolerance (Spark default 1e-6)
 };
 
+// New stream rows a solve ingests into its ring before reading the window
+// (fused into the first kernel of the solve): rows src_first + i*src_step
+// (i < n) of the resident dataset go to ring slots (dst + i) % cap, and must be
+// the newest n rows of the window.  n == 0: nothing to ingest.
+constexpr int kMaxFusedIngest = 256;
+struct RingIngest {
+  const uint16_t* src;   // dataset rows [*][Fp] bf16
+  const int32_t* ysrc;   // dataset labels
+  long long first, step;
+  int n, dst;
+};
+
 struct SolveParams {
   int B;      // rows in the window
   int start;  // first ring slot of the window

@@ -42,8 +42,10 @@ class LocalSolver {
   LocalSolver(const LocalSolver&) = delete;
   LocalSolver& operator=(const LocalSolver&) = delete;
 
-  // Enqueue one local solve over window [start, start+B) of the ring on `stream`.
-  void run(int B, int start, hipStream_t stream);
+  // Enqueue one local solve over window [start, start+B) of the ring on `stream`;
+  // `ing` (n > 0): first ingest those new rows, the newest of the window, into
+  // the ring inside the solve's first kernel.
+  void run(int B, int start, hipStream_t stream, const RingIngest& ing = RingIngest{});
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
   int kernels_per_solve() const { return 2 + 2 * nfast_; }  // stats_prep + slots + (tail with finalize | finalize)
@@ -54,7 +56,7 @@ class LocalSolver {
   std::vector<long long> read_stamps(hipStream_t stream);
 
  private:
-  void enqueue_body(hipStream_t s, int B, int start);
+  void enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing);
   SolverCfg cfg_;
   SolveDev dv_{};
   int nwg_eval_;
@@ -72,8 +74,9 @@ class LocalSolver {
     SolveDev dv;
     Ctrl* ctrl;
     int B, start;
+    RingIngest ing;
   } stats_args_{};
-  void* stats_kp_[6] = {};
+  void* stats_kp_[7] = {};
   hipKernelNodeParams stats_params_{};
   Ctrl* ctrl_ = nullptr;
   hipStream_t cap_stream_ = nullptr;

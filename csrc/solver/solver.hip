@@ -91,7 +91,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    enqueue_body(cap_stream_, cfg.cap, 0);
+    enqueue_body(cap_stream_, cfg.cap, 0, RingIngest{});
     hip_check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
     hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
     size_t n = 0;
@@ -110,13 +110,14 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
       }
     }
     if (!stats_node_) throw std::runtime_error("solver graph: stats_prep node not found");
-    stats_args_ = StatsArgs{cfg_, prm_, dv_, ctrl_, cfg.cap, 0};
+    stats_args_ = StatsArgs{cfg_, prm_, dv_, ctrl_, cfg.cap, 0, RingIngest{}};
     stats_kp_[0] = &stats_args_.cfg;
     stats_kp_[1] = &stats_args_.prm;
     stats_kp_[2] = &stats_args_.dv;
     stats_kp_[3] = &stats_args_.ctrl;
     stats_kp_[4] = &stats_args_.B;
     stats_kp_[5] = &stats_args_.start;
+    stats_kp_[6] = &stats_args_.ing;
     stats_params_.kernelParams = stats_kp_;
     stats_params_.extra = nullptr;
   }
@@ -129,8 +130,8 @@ LocalSolver::~LocalSolver() {
   if (ws_) (void)hipFree(ws_);
 }
 
-void LocalSolver::enqueue_body(hipStream_t s, int B, int start) {
-  launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, s);
+void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing) {
+  launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, ing, s);
   for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
   if (cfg_.nslots > nfast_)
     launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s, /*with_finalize=*/1);
@@ -139,16 +140,24 @@ void LocalSolver::enqueue_body(hipStream_t s, int B, int start) {
   hip_check(hipGetLastError(), "solver kernel launch");
 }
 
-void LocalSolver::run(int B, int start, hipStream_t stream) {
+void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& ing) {
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
+  if (ing.n < 0 || ing.n > kMaxFusedIngest || ing.n > cfg_.cap) throw std::invalid_argument("fused ingest: bad row count");
+  if (ing.n > 0) {
+    if (!ing.src || !ing.ysrc || ing.dst < 0 || ing.dst >= cfg_.cap || ing.first < 0 || ing.step < 1)
+      throw std::invalid_argument("fused ingest: bad source / destination");
+    if ((ing.dst + ing.n - 1) % cfg_.cap != (start + B - 1) % cfg_.cap)
+      throw std::invalid_argument("fused ingest: the new rows must end the window");
+  }
   if (use_graph_) {
     stats_args_.B = B;
     stats_args_.start = start;
+    stats_args_.ing = ing;
     hip_check(hipGraphExecKernelNodeSetParams(exec_, stats_node_, &stats_params_), "hipGraphExecKernelNodeSetParams");
     hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
   } else {
-    enqueue_body(stream, B, start);
+    enqueue_body(stream, B, start, ing);
   }
 }
 

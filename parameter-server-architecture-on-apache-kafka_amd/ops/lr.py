@@ -38,6 +38,7 @@ class SolverOptions:
     standardize: bool = True  # Spark default; the dense MFMA solver always standardises
     use_graph: bool = True
     max_eval_wg: int = 512
+    fused_ingest: bool = True  # GPU: new stream rows are copied into the ring by the solve's first kernel
 
     @property
     def nslots(self) -> int:
@@ -114,7 +115,13 @@ class LocalSolveOp:
             if X.dtype != torch.bfloat16 or X.shape != (self.cap, self.spec.Fp) or y.dtype != torch.int32:
                 raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
             self._bind(ring, w_old)
-            self._native.run(int(B), int(start), stream_handle(self.device))
+            pend = ring.take_pending(B, start) if hasattr(ring, "take_pending") else None
+            if pend is None:
+                self._native.run(int(B), int(start), stream_handle(self.device))
+            else:
+                sX, sy, first, step, n, dst = pend
+                self._native.run_ingest(int(B), int(start), stream_handle(self.device), sX.data_ptr(), sy.data_ptr(),
+                                        first, step, n, dst)
             return
         s, o = self.spec, self.opts
         idx = (torch.arange(B) + start) % self.cap

@@ -20,6 +20,9 @@ Sequential (BSP, c = 0) schedules, chosen with ``--bsp_schedule``:
   sharded       key-range sharded server (new capability): every
                 rank owns P/world of the master weights; ncclReduceScatter(delta)
                 -> shard update -> ncclAllGather(w).
+On GPUs the BSP collectives are issued through a native RCCL communicator
+(psx.parallel.comm, csrc/comm/rccl_comm.h): a few us of host time per call
+instead of ~30 us through torch.distributed, which otherwise bounds the round.
 
 Bounded-delay (SSP, c = D > 0) and eventual (ASP, c = -1) need a dedicated
 server rank 0 (workers are ranks 1..N).  A worker pushes a (worker, vc) token
@@ -46,6 +49,7 @@ from ..runtime.config import PSConfig
 from ..runtime.engine import load_datasets
 from ..runtime.faults import WorkerFailure, drop_on_failure
 from ..ops.sparse import SparseDelta, nz_capacity
+from .comm import make_comm
 from ..runtime.roles import EvalPair, ServerRole, WorkerRole, is_wide, make_evalset
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
@@ -166,10 +170,14 @@ class DistEngine:
 
     # ------------------------------------------------------------------
     def run(self) -> dict:
-        if self.async_mode:
-            out = self._run_async()
-        else:
-            out = self._run_bsp()
+        try:
+            out = self._run_async() if self.async_mode else self._run_bsp()
+        except BaseException:
+            comm, self.comm = getattr(self, "comm", None), None
+            if comm is not None:
+                comm.c.abort()  # peers may be gone: no collective teardown
+            raise
+        self.close()
         flush_checkpoints(self.cfg)
         if self.log is not None:
             self.log.close()
@@ -177,6 +185,13 @@ class DistEngine:
                 out.update(summarize(self.log.book))
         self.tracer.close()
         return out
+
+    def close(self):
+        """Release the native communicator (collective: every rank calls it)."""
+        comm = getattr(self, "comm", None)
+        self.comm = None
+        if comm is not None:
+            comm.close()
 
     def _all_ready(self) -> bool:
         flag = torch.tensor([1 if (self.worker is None or self.worker.ready()) else 0], dtype=torch.int32,
@@ -227,6 +242,10 @@ class DistEngine:
         shard = (P + self.world - 1) // self.world
         if sched == "sharded":
             wfull, pad, myd = self._sharded_buffers(shard)
+        if not hasattr(self, "comm"):  # created once per engine (init is ~0.1-0.5 s), closed by close()
+            self.comm = make_comm(self.rank, self.world, self.device)  # None: torch.distributed collectives
+        comm = self.comm
+        overlap = os.environ.get("PSX_COMM_OVERLAP", "0") == "1"
         N = cfg.num_workers
         lr = cfg.lr
         t_start = time.time()
@@ -252,7 +271,16 @@ class DistEngine:
                 with self.tracer.span("solve"):
                     delta = wk.solve() if wk is not None else zeros
                 with self.tracer.span("comm", schedule=sched):
-                    work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
+                    if comm is not None:
+                        # in stream order; PSX_COMM_OVERLAP=1 runs it on the communicator's side
+                        # stream beside the evaluations instead (the fork/join event pairs cost
+                        # ~20 us of host time, more than the overlap saves for a 24 KB delta)
+                        if overlap:
+                            comm.fork()
+                        comm.all_reduce(delta, side=overlap)
+                        work = comm
+                    else:
+                        work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
                     if wk is not None:
                         wk.log_eval(self.log)
                         # the next round's stream rows land in the ring while the collective
@@ -260,7 +288,11 @@ class DistEngine:
                         if not (cfg.max_iters and r + 1 - self.rounds >= cfg.max_iters):
                             wk.ingest()
                             ingested_ahead = True
-                    work.wait()
+                    if comm is not None:
+                        if overlap:
+                            comm.join()
+                    else:
+                        work.wait()
                     srv.apply(delta, lr)
                     if self.rank == 0:
                         srv.log_eval(r, self.log)  # deferred into the next round's paired pass
@@ -271,23 +303,34 @@ class DistEngine:
                     delta = wk.compute(self.log) if wk is not None else zeros
             with self.tracer.span("comm", schedule=sched):
                 if sched == "reduce_bcast":
-                    dist.reduce(delta, dst=0, op=dist.ReduceOp.SUM)
+                    if comm is not None:
+                        comm.reduce(delta, 0)
+                    else:
+                        dist.reduce(delta, dst=0, op=dist.ReduceOp.SUM)
                     if srv is not None:
                         srv.apply_and_log(delta, r, self.log, lr)
                         logged = True
                         new_w = srv.w
                     else:
                         new_w = wk.w
-                    dist.broadcast(new_w, src=0)
+                    if comm is not None:
+                        comm.broadcast(new_w, 0)
+                    else:
+                        dist.broadcast(new_w, src=0)
                 elif sched == "sharded":  # key-range shards of the master weights (KeyRange.java:11-49)
                     srv.side.fence()  # srv.w / fragments are rewritten below
                     if delta.data_ptr() != pad.data_ptr():  # the solver writes into pad[:P] directly
                         pad[:P].copy_(delta)
-                    dist.reduce_scatter_tensor(myd, pad, op=dist.ReduceOp.SUM)
                     lo = self.rank * shard
                     mine = wfull[lo:lo + shard]
-                    mine.add_(myd, alpha=lr)
-                    dist.all_gather_into_tensor(wfull, mine)  # in place: srv.w is a view of wfull
+                    if comm is not None:
+                        comm.reduce_scatter(myd, pad)
+                        mine.add_(myd, alpha=lr)
+                        comm.all_gather(wfull, mine)  # in place: srv.w is a view of wfull
+                    else:
+                        dist.reduce_scatter_tensor(myd, pad, op=dist.ReduceOp.SUM)
+                        mine.add_(myd, alpha=lr)
+                        dist.all_gather_into_tensor(wfull, mine)
                     if srv.frag is not None:
                         srv.frag.refresh(srv.w)
                     new_w = srv.w

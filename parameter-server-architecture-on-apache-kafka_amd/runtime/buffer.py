@@ -34,8 +34,9 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
     every 32-feature slice of a window contiguously."""
 
     TILE = 32
+    MAX_DEFERRED = 256  # kMaxFusedIngest (csrc/kernels/solver_ctrl.h)
 
-    def __init__(self, cap: int, Fp: int, device):
+    def __init__(self, cap: int, Fp: int, device, defer: bool = False):
         self.requested = int(cap)
         self.cap = -(-int(cap) // self.TILE) * self.TILE
         self.Fp, self.device = int(Fp), torch.device(device)
@@ -43,11 +44,42 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
         self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
         self.XT = (torch.zeros(self.Fp, self.cap, dtype=torch.bfloat16, device=self.device)
                    if is_gpu(self.device) else None)
+        # defer: the last ingest is not launched on its own but handed to the next
+        # local solve, whose first kernel copies it (LocalSolveOp.run); any other
+        # reader of the ring must call flush() first
+        self.defer = bool(defer) and is_gpu(self.device)
+        self.pending = None
 
     def ingest(self, src_X: torch.Tensor, src_y: torch.Tensor, src_first: int, src_step: int, n: int, dst_first: int):
         """Copy rows src_first + i*src_step (i < n) into slots (dst_first + i) % cap."""
         if n <= 0:
             return
+        self.flush()
+        if self.defer and n <= self.MAX_DEFERRED and src_X.dtype == torch.bfloat16 and src_X.shape[1] == self.Fp:
+            self.pending = (src_X, src_y, int(src_first), int(src_step), int(n), int(dst_first) % self.cap)
+            return
+        self._launch(src_X, src_y, src_first, src_step, n, dst_first)
+
+    def flush(self):
+        """Launch a deferred ingest now (stream order keeps it ahead of later readers)."""
+        if self.pending is not None:
+            p, self.pending = self.pending, None
+            self._launch(*p)
+
+    def take_pending(self, B: int, start: int):
+        """The deferred ingest for a solve over [start, start+B), if its rows end that
+        window (else it is launched on its own and None is returned)."""
+        p = self.pending
+        if p is None:
+            return None
+        n, dst = p[4], p[5]
+        if (dst + n - 1) % self.cap != (start + B - 1) % self.cap:
+            self.flush()
+            return None
+        self.pending = None
+        return p
+
+    def _launch(self, src_X, src_y, src_first, src_step, n, dst_first):
         if is_gpu(self.device):
             _native.hip().ring_ingest(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
                                       self.X.data_ptr(), self.XT.data_ptr(), self.y.data_ptr(), int(dst_first),
@@ -63,6 +95,7 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
 
     def place(self, X: torch.Tensor, y: torch.Tensor, first: int = 0):
         """Write rows X[i], y[i] into slots (first + i) % cap (tests, tools)."""
+        self.flush()
         idx = (torch.arange(X.shape[0]) + int(first)) % self.cap
         idx = idx.to(self.device)
         self.X[idx] = X.to(self.device, torch.bfloat16)
@@ -71,6 +104,7 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
 
     def sync_transposed(self):
         """Rebuild XT after direct writes to X."""
+        self.flush()
         if self.XT is not None:
             self.XT.copy_(self.X.t())
 

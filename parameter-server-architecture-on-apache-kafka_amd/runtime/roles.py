@@ -81,7 +81,7 @@ class WorkerRole:
             nz = cfg.ring_nz or nz_capacity(train.max_nnz)
             self.ring = SparseRing(cfg.max_buffer_size, nz, self.device)
         else:
-            self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device)
+            self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device, defer=cfg.solver.fused_ingest)
         self.window = _native.host.SlidingWindow(cfg.min_buffer_size, cfg.max_buffer_size,
                                                  cfg.buffer_size_coefficient, 500, self.ring.cap)
         self.source = StreamSource(train, k, cfg.num_workers, self.ring, self.window,

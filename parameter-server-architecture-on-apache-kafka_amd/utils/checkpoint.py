@@ -139,6 +139,8 @@ class Checkpointer:
 
 def worker_state(wk) -> dict:
     ring = wk.ring
+    if hasattr(ring, "flush"):
+        ring.flush()  # a deferred ingest belongs to the saved rows
     tensors = {}
     for name in ("X", "y", "idx", "val", "nnz"):
         t = getattr(ring, name, None)
@@ -159,6 +161,8 @@ def worker_state(wk) -> dict:
 
 def restore_worker(wk, state: dict) -> None:
     ring = wk.ring
+    if hasattr(ring, "pending"):
+        ring.pending = None  # superseded by the restored rows
     for name in ("X", "y", "idx", "val", "nnz"):
         key = "ring_" + name
         if key in state:

@@ -1,0 +1,74 @@
+"""Native RCCL communicator (csrc/comm/rccl_comm.h) on one MI355X: world size 1
+in-process (the multi-rank path runs in the driver's 8-GPU bench; RCCL refuses
+two ranks on one device)."""
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def pg(cuda):
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(cuda))
+    yield
+    dist.destroy_process_group()
+
+
+def test_native_comm_world1(cuda, pg):
+    from psx.parallel.comm import make_comm
+
+    comm = make_comm(0, 1, cuda)
+    assert comm is not None and comm.c.size == 1 and comm.c.rank == 0
+    x = torch.arange(1000, dtype=torch.float32, device=cuda)
+    ref = x.clone()
+    comm.all_reduce(x)
+    comm.reduce(x, 0)
+    comm.broadcast(x, 0)
+    i = torch.arange(64, dtype=torch.int32, device=cuda)
+    comm.all_reduce(i)
+    out = torch.empty(1000, dtype=torch.float32, device=cuda)
+    comm.reduce_scatter(out, x)
+    g = torch.zeros(1000, dtype=torch.float32, device=cuda)
+    comm.all_gather(g, out)
+    # side stream between fork / join, overlapping compute on the current stream
+    y = torch.ones(1 << 20, device=cuda)
+    comm.fork()
+    comm.all_reduce(y, side=True)
+    z = (x * 2).sum()
+    comm.join()
+    y += 1
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref) and torch.equal(g, ref) and torch.equal(i.cpu(), torch.arange(64, dtype=torch.int32))
+    assert torch.all(y == 2) and z.item() == 2 * ref.sum().item()
+    comm.close()
+
+
+def test_dist_engine_native_vs_torch_collectives(cuda, pg, monkeypatch):
+    """The BSP loop gives the same model through the native communicator and through torch.distributed."""
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
+    ws = {}
+    for native in ("1", "0"):
+        for sched in ("allreduce", "reduce_bcast", "sharded"):
+            monkeypatch.setenv("PSX_NATIVE_RCCL", native)
+            cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                           rows_per_iter=64, epochs=100, max_iters=8, init="random", bsp_schedule=sched,
+                           min_buffer_size=256, max_buffer_size=256)
+            eng = DistEngine(cfg, 0, 1, cuda, train=train, test=test)
+            out = eng.run()
+            assert out["rounds"] == 8
+            ws[(native, sched)] = eng.server.w.cpu()
+    base = ws[("0", "allreduce")]
+    for k, w in ws.items():
+        assert torch.allclose(w, base, atol=1e-4 * max(1.0, base.abs().max().item())), k

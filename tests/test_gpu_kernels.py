@@ -248,3 +248,46 @@ def test_server_apply_n_matches_sum(cuda):
     torch.cuda.synchronize()
     assert torch.allclose(w, ref, atol=1e-6)
     assert torch.allclose(frag.b[3:3 + spec.K], spec.intercept(ref), atol=1e-6)
+
+
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("n,B,pre", [(64, 512, 900), (200, 128, 300), (256, 1024, 1000), (1, 1, 0)])
+def test_fused_ingest_matches_separate(cuda, graph, n, B, pre):
+    """Rows ingested by the solve's first kernel == a separate ring_ingest + solve
+    (ring contents bitwise, delta to fp32-atomic rounding); covers ring wrap and
+    windows shorter than the ingest."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(4000, seed=7).to(cuda)
+    w = _rand_w(spec, 3, 0.02).to(cuda)
+    cap = 1024
+    dst = (pre + 37) % cap  # the new rows end the window and wrap the ring
+    start = (dst + n - B) % cap
+    outs, rings = [], []
+    for defer in (True, False):
+        ring = DeviceRing(cap, ds.Fp, cuda, defer=defer)
+        ring.ingest(ds.X, ds.y, 0, 1, min(cap, pre + 37), 0)  # older rows, launched on their own
+        ring.flush()
+        ring.ingest(ds.X, ds.y, 2000, 3, n, dst)
+        assert (ring.pending is not None) == defer
+        op = LocalSolveOp(spec, cap, cuda, SolverOptions(use_graph=graph))
+        op.run(ring, B, start, w)
+        assert ring.pending is None
+        torch.cuda.synchronize()
+        outs.append(op.delta.clone())
+        rings.append((ring.X.cpu(), ring.XT.cpu(), ring.y.cpu()))
+    for a, b in zip(*rings):
+        assert torch.equal(a, b)
+    assert torch.equal(rings[0][1], rings[0][0].t())
+    scale = outs[1].abs().max().item()
+    assert (outs[0] - outs[1]).abs().max().item() <= 2e-4 * scale
+
+
+def test_deferred_ingest_not_ending_window_is_flushed(cuda):
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(1000, seed=8).to(cuda)
+    ring = DeviceRing(256, ds.Fp, cuda, defer=True)
+    ring.ingest(ds.X, ds.y, 0, 1, 64, 0)
+    op = LocalSolveOp(spec, 256, cuda, SolverOptions())
+    op.run(ring, 32, 0, torch.zeros(spec.P, device=cuda))  # window [0,32) does not end at slot 63
+    torch.cuda.synchronize()
+    assert ring.pending is None and torch.equal(ring.X.cpu()[:64], ds.X.cpu()[:64])

@@ -70,6 +70,7 @@ def parse(argv=None):
                     help="single-GPU run: in-process workers sharing the GPU (one HIP stream each); default 1")
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
@@ -103,7 +104,8 @@ def build_cfg(a, n_workers):
         seed=0,
         model="wide" if wide else "dense",
         sigmoid=a.model == "sharded100m",
-        solver=SolverOptions(iters=a.iters, use_graph=not a.no_graph, zero_const=not wide),
+        solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
+                             zero_const=not wide),
         bsp_schedule=a.schedule,
     )
 

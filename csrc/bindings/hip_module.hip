@@ -145,6 +145,45 @@ PYBIND11_MODULE(_psx_hip, m) {
       py::arg("b"), py::arg("conf"), py::arg("stream"), py::arg("ticket") = 0, py::arg("slot") = 0,
       py::arg("loss") = 0, py::arg("seq") = 0, py::arg("coff1") = 0, py::arg("coff2") = 0, py::arg("slot2") = 0,
       py::arg("seq2") = 0);
+  m.def(
+      "eval_apply",
+      [](int FP, int K, int F, uintptr_t Xt, uintptr_t yt, int T, uintptr_t whi, uintptr_t wlo, uintptr_t wb,
+         uintptr_t shi, uintptr_t slo, uintptr_t sb, uintptr_t conf, uintptr_t stream, uintptr_t ticket,
+         uintptr_t slot, uintptr_t loss, unsigned long long seq, int coff1, int coff2, uintptr_t slot2,
+         unsigned long long seq2, uintptr_t w, std::vector<uintptr_t> deltas, float lr, uintptr_t ohi, uintptr_t olo,
+         uintptr_t ob) {
+        prepare_kernels();
+        if (coff1 < 0 || coff1 + K > coff2 || coff2 + K > 16)
+          throw std::invalid_argument("eval_apply: worker columns must precede the server's, within 16");
+        if (deltas.size() > 16) throw std::invalid_argument("eval_apply: at most 16 deltas");
+        if (!shi || !slo || !sb) throw std::invalid_argument("eval_apply: null server fragments");
+        if (!deltas.empty()) {
+          if (!w || !ohi || !olo || !ob) throw std::invalid_argument("eval_apply: null update buffer");
+          if (shi == ohi || slo == olo || sb == ob || whi == ohi || wlo == olo || wb == ob)
+            throw std::invalid_argument("eval_apply: the update would overwrite fragments this launch reads");
+        }
+        EvalApply ea{};
+        ea.shi = P<const uint16_t>(shi);
+        ea.slo = P<const uint16_t>(slo);
+        ea.sb = P<const float>(sb);
+        ea.w = P<float>(w);
+        ea.dl.n = (int)deltas.size();
+        for (size_t i = 0; i < deltas.size(); ++i) ea.dl.p[i] = P<const float>(deltas[i]);
+        ea.lr = lr;
+        ea.ohi = P<uint16_t>(ohi);
+        ea.olo = P<uint16_t>(olo);
+        ea.ob = P<float>(ob);
+        ea.F = F;
+        launch_eval_apply(FP, K, P<const uint16_t>(Xt), P<const int32_t>(yt), T, P<const uint16_t>(whi),
+                          P<const uint16_t>(wlo), P<const float>(wb), P<int>(conf), S(stream), P<unsigned>(ticket),
+                          P<void>(slot), P<const float>(loss), seq, coff1, coff2, P<void>(slot2), seq2, ea);
+        hip_check(hipGetLastError(), "eval_apply launch");
+      },
+      py::arg("FP"), py::arg("K"), py::arg("F"), py::arg("Xt"), py::arg("yt"), py::arg("T"), py::arg("whi"),
+      py::arg("wlo"), py::arg("wb"), py::arg("shi"), py::arg("slo"), py::arg("sb"), py::arg("conf"),
+      py::arg("stream"), py::arg("ticket"), py::arg("slot"), py::arg("loss"), py::arg("seq"), py::arg("coff1"),
+      py::arg("coff2"), py::arg("slot2"), py::arg("seq2"), py::arg("w"), py::arg("deltas"), py::arg("lr"),
+      py::arg("ohi"), py::arg("olo"), py::arg("ob"));
   // Fine-grained (coherent) pinned host memory: device stores land in host
   // memory without a copy and device loads never see a stale cached line.
   m.def("pinned_alloc", [](size_t bytes) {

@@ -20,6 +20,34 @@ void prepare_kernels();
 // (must be zeroed by the caller).  Otherwise conf is a private accumulator
 // (zero, left zero) with its `ticket` word, and the counts + *loss land in the
 // pinned host EvalSlot `slot`, published with sequence number `seq`.
+struct DeltaList {
+  const float* p[16];
+  int n;
+};
+
+// Paired evaluation fused with the server update of the same round.
+//   * worker row: the locally trained model, fragment columns [coff1, coff1+K)
+//     of (whi, wlo, wb);
+//   * server row (slot2 != nullptr): the global model of the PREVIOUS round,
+//     columns [coff2, coff2+K) of (shi, slo, sb) -- a separate buffer;
+//   * apply (dl.n > 0): w += lr * sum(dl) and the new global model's fragments
+//     into (ohi, olo, ob) at coff2 -- the other buffer of the server's pair, so
+//     nothing this launch reads is written.
+struct EvalApply {
+  const uint16_t *shi, *slo;
+  const float* sb;
+  float* w;
+  DeltaList dl;
+  float lr;
+  uint16_t *ohi, *olo;
+  float* ob;
+  int F;
+  int tgrid;  // workgroups evaluating test tiles (set by the launcher); the rest update
+};
+void launch_eval_apply(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* whi,
+                       const uint16_t* wlo, const float* wb, int* conf, hipStream_t s, unsigned* ticket, void* slot,
+                       const float* loss, unsigned long long seq, int coff1, int coff2, void* slot2,
+                       unsigned long long seq2, const EvalApply& ea);
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
                       const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket = nullptr,
                       void* slot = nullptr, const float* loss = nullptr, unsigned long long seq = 0, int coff1 = 0,
@@ -27,10 +55,7 @@ void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int 
 void launch_logits(int FP, int K, const uint16_t* X, int T, const uint16_t* wf_hi, const uint16_t* wf_lo,
                    const float* b, float* logits, hipStream_t s);
 // Server update w += lr * delta (all P entries) and refresh the eval fragments.
-struct DeltaList {
-  const float* p[16];
-  int n;
-};
+
 // w += lr * sum_i dl.p[i] (all P entries) + fragments, one kernel (n <= 16).
 void launch_server_apply_n(int K, int F, int FP, float* w, const DeltaList& dl, float lr, uint16_t* wf_hi,
                            uint16_t* wf_lo, float* b_eff, hipStream_t s, int coff = 0);

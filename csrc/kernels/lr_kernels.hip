@@ -40,6 +40,11 @@ bool fp_supported(int FP) { return FP == 128 || FP == 256 || FP == 512 || FP == 
 // model at [coff2, coff2 + K) of the same fragment buffer -- so the worker row
 // of this round and the server row of the previous round cost one pass over
 // the test set instead of two.
+//
+// eval_apply (ea.shi != nullptr): the server model's columns come from their own
+// fragment buffer, and the launch also performs the round's server update into
+// the other buffer of the server's pair (see lr_kernels.h: EvalApply) -- one
+// launch per round for the worker row, the server row and the update.
 template <int FP>
 __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* __restrict__ Xt,
                                                         const int32_t* __restrict__ yt, int T,
@@ -47,7 +52,8 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
                                                         const uint16_t* __restrict__ wf_lo,
                                                         const float* __restrict__ b, int* acc, unsigned* ticket,
                                                         char* slot, const float* loss, unsigned long long seq,
-                                                        int coff1, int coff2, char* slot2, unsigned long long seq2) {
+                                                        int coff1, int coff2, char* slot2, unsigned long long seq2,
+                                                        EvalApply ea) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [16][16]
@@ -57,13 +63,38 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   const bool pair = slot2 != nullptr;
   cl[tid] = 0;
   if (pair) cl2[tid] = 0;
-  const int ntiles = (T + 31) / 32;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // workgroups [0, tgrid) evaluate test tiles; the extra workgroups [tgrid, grid)
+  // perform the round's server update (independent of everything this launch
+  // reads) on otherwise idle CUs, beside the evaluation
+  const int tgrid = ea.tgrid > 0 ? ea.tgrid : gridDim.x;
+  if (ea.dl.n > 0 && (int)blockIdx.x >= tgrid) {
+    const int P = K * FP + K, KF = K * FP;
+    for (int p = (blockIdx.x - tgrid) * 256 + tid; p < P; p += (gridDim.x - tgrid) * 256) {
+      float sum = 0.f;
+      for (int i = 0; i < ea.dl.n; ++i) sum += ea.dl.p[i][p];
+      const float v = ea.w[p] + ea.lr * sum;
+      ea.w[p] = v;
+      if (p < KF) {
+        const int c = p / FP, f = p - c * FP;
+        write_frag(ea.ohi, ea.olo, coff2 + c, f, f < ea.F ? v : 0.f);
+      } else {
+        ea.ob[coff2 + p - KF] = v;
+      }
+    }
+  }
+  // per-lane B-operand source: server columns from the server's own buffer
+  const bool split = ea.shi != nullptr;
+  const int lcls = tid & 15;
+  const uint16_t* fh = (split && lcls >= coff2) ? ea.shi : wf_hi;
+  const uint16_t* fl = (split && lcls >= coff2) ? ea.slo : wf_lo;
+  const float* b2 = split ? ea.sb : b;
+  const int ntiles = (int)blockIdx.x < tgrid ? (T + 31) / 32 : 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += tgrid) {
     const int nrows = min(32, T - tile * 32);
     stage_tile<FP>(lds, Xt, (int64_t)tile * 32, nrows, 0, false);
     __syncthreads();
     f32x4 a0, a1;
-    forward_tile<FP>(lds, wf_hi, wf_lo, a0, a1);
+    forward_tile<FP>(lds, fh, fl, a0, a1);
     store_partial_logits(red_base, a0, a1);
     __syncthreads();
     if (tid < nrows) {
@@ -83,7 +114,7 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
         int best2 = 0;
         float bz2 = -INFINITY;
         for (int c = 0; c < K; ++c) {
-          const float z = load_logit(red_base, tid, coff2 + c) + b[coff2 + c];
+          const float z = load_logit(red_base, tid, coff2 + c) + b2[coff2 + c];
           if (z > bz2) {
             bz2 = z;
             best2 = c;
@@ -130,16 +161,29 @@ void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int 
                       const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket, void* slot,
                       const float* loss, unsigned long long seq, int coff1, int coff2, void* slot2,
                       unsigned long long seq2) {
+  EvalApply none{};
+  launch_eval_apply(FP, K, Xt, yt, T, wf_hi, wf_lo, b, conf, s, ticket, slot, loss, seq, coff1, coff2, slot2, seq2,
+                    none);
+}
+
+void launch_eval_apply(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
+                       const uint16_t* wf_lo, const float* b, int* conf, hipStream_t s, unsigned* ticket, void* slot,
+                       const float* loss, unsigned long long seq, int coff1, int coff2, void* slot2,
+                       unsigned long long seq2, const EvalApply& ea) {
   const size_t lds = eval_lds_bytes(FP);
   const int ntiles = (T + 31) / 32;
-  const int grid = ntiles < 1024 ? ntiles : 1024;
+  const int tgrid = ntiles < 1024 ? ntiles : 1024;
+  int grid = tgrid;
+  EvalApply a = ea;
+  a.tgrid = tgrid;
+  if (ea.dl.n > 0) grid += (K * FP + K + 255) / 256;  // update workgroups
   if (grid <= 0) return;
   char* sl = static_cast<char*>(slot);
   char* sl2 = static_cast<char*>(slot2);
 #define PSX_TE(FPV)                                                                                          \
   case FPV:                                                                                                  \
     test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf, ticket, sl, loss, seq, \
-                                                 coff1, coff2, sl2, seq2);                                  \
+                                                 coff1, coff2, sl2, seq2, a);                               \
     break;
   switch (FP) {
     PSX_TE(128)

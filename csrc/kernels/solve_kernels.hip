@@ -90,61 +90,62 @@ __device__ __forceinline__ unsigned long long d2u(double v) { return __builtin_b
 __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_bit_cast(double, v); }
 
 // ---------------------------------------------------------------------------
-// stats + prep: grid = FP/32 workgroups of 256 threads; 8 lanes per feature
-// read the feature-major ring copy XT in contiguous 16-B pieces of 8 rows.
-// With a fused ingest (ing.n > 0) each workgroup first copies its 32-feature
+// stats + prep: grid = FP/kStatW workgroups of 256 threads; kStatL = 256/kStatW
+// lanes per feature read the feature-major ring copy XT in contiguous 16-B
+// pieces of 8 rows (8 features per workgroup: 128 workgroups for FP 1024, each
+// with few loads per lane, so the window read is not latency-serialised).
+constexpr int kStatW = 8;
+constexpr int kStatL = 256 / kStatW;
+// With a fused ingest (ing.n > 0) each workgroup first copies its kStatW-feature
 // slice of the new rows into X / XT (and workgroup 0 the labels); the new rows'
 // statistics come from an LDS copy, the old rows' from XT as before.
 __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv, Ctrl* ctrl,
                                                          int B_arg, int start_arg, RingIngest ing) {
+  static_assert(kStatW == 8, "the ingest copy moves one 16-B chunk (8 features) per row");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* rs = (double*)smem;  // [32]
-  double* rq = rs + 32;        // [32]
-  float* sdl = (float*)(rq + 32);  // [32]
-  float* ivl = sdl + 32;           // [32]
-  unsigned short* nv = (unsigned short*)(ivl + 32);  // [kMaxFusedIngest][32] new rows of this slice
+  double* rs = (double*)smem;          // [kStatW]
+  double* rq = rs + kStatW;            // [kStatW]
+  float* sdl = (float*)(rq + kStatW);  // [kStatW]
+  float* ivl = sdl + kStatW;           // [kStatW]
+  unsigned short* nv = (unsigned short*)(ivl + kStatW);  // [kMaxFusedIngest][kStatW] new rows of this slice
   // this run's window arrives as kernel arguments (the host rewrites this graph
   // node's parameters per run); later launches read it from device memory
   const SolveParams pr{B_arg, start_arg, 0, 0};
   const int B = pr.B, cap = cfg.cap, FP = cfg.Fp;
   const WinTiles wt(pr.start, B, cap);
-  const int t = threadIdx.x, j = t & 7, fl0 = t >> 3;
+  const int t = threadIdx.x, j = t % kStatL, fl0 = t / kStatL;
   if (blockIdx.x == 0 && t == 0) *prm = pr;  // the later launches read it from device memory
   if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
-  const int fs = blockIdx.x * 32;
+  const int fs = blockIdx.x * kStatW;
   const int nin = ing.n;
-  if (nin > 0) {
-    // consecutive threads take consecutive rows of one 8-feature chunk, so the
-    // 2-B XT stores of a wave land in contiguous runs of each feature row
-    for (int it = t; it < nin * 4; it += 256) {
-      const int c = it / nin, i = it - c * nin;
-      const long long sr = ing.first + (long long)i * ing.step;
-      int dr = ing.dst + i;
-      dr = dr >= cap ? dr - cap : dr;
-      const u16x8 v = *(const u16x8*)(ing.src + sr * FP + fs + c * 8);
-      *(u16x8*)(const_cast<uint16_t*>(dv.X) + (size_t)dr * FP + fs + c * 8) = v;
-      *(u16x8*)(nv + i * 32 + c * 8) = v;
+  for (int i = t; i < nin; i += 256) {  // fused ingest: one 16-B chunk of each new row
+    const long long sr = ing.first + (long long)i * ing.step;
+    int dr = ing.dst + i;
+    dr = dr >= cap ? dr - cap : dr;
+    const u16x8 v = *(const u16x8*)(ing.src + sr * FP + fs);
+    *(u16x8*)(const_cast<uint16_t*>(dv.X) + (size_t)dr * FP + fs) = v;
+    *(u16x8*)(nv + i * kStatW) = v;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(size_t)(fs + c * 8 + e) * cap + dr] = v[e];
-      if (blockIdx.x == 0 && c == 0) const_cast<int32_t*>(dv.y)[dr] = ing.ysrc[sr];
-    }
+    for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(size_t)(fs + e) * cap + dr] = v[e];
+    if (blockIdx.x == 0) const_cast<int32_t*>(dv.y)[dr] = ing.ysrc[sr];
   }
   // the newest min(nin, B) window rows are the fused ones: counted from LDS
   const int bold = B - (nin < B ? nin : B);
   const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
   const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
   float s = 0.f, q = 0.f;
-  for (int q0 = j; q0 < nq; q0 += 8 * 8) {
-    u16x8 v[8];
+  constexpr int U = 4;  // pieces per lane in flight
+  for (int q0 = j; q0 < nq; q0 += kStatL * U) {
+    u16x8 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int qq = q0 + 8 * u;
+    for (int u = 0; u < U; ++u) {
+      const int qq = q0 + kStatL * u;
       const int qc = qq < nq ? qq : nq - 1;
       v[u] = *(const u16x8*)(xt + wt.ring_tile(qc >> 2) * 32 + (qc & 3) * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int qq = q0 + 8 * u;
+    for (int u = 0; u < U; ++u) {
+      const int qq = q0 + kStatL * u;
       const int o0 = (qq >> 2) * 32 + (qq & 3) * 8 - wt.s0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -157,15 +158,15 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   }
   if (nin > 0) {
     __syncthreads();
-    for (int i = nin - (B - bold) + j; i < nin; i += 8) {
-      const float x = bf2f(nv[i * 32 + fl0]);
+    for (int i = nin - (B - bold) + j; i < nin; i += kStatL) {
+      const float x = bf2f(nv[i * kStatW + fl0]);
       s += x;
       q += x * x;
     }
   }
   double a = s, b2 = q;
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) {
+  for (int o = 1; o < kStatL; o <<= 1) {
     a += __shfl_xor(a, o, 64);
     b2 += __shfl_xor(b2, o, 64);
   }
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
     rq[fl0] = b2;
   }
   __syncthreads();
-  if (t < 32) {
+  if (t < kStatW) {
     const double a = rs[t];
     const double b = rq[t];
     const int f = fs + t;
@@ -193,8 +194,8 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   }
   __syncthreads();
   const int K = cfg.K, KP = dv.KP, FPI = dv.FPI;
-  for (int e = t; e < 32 * KP; e += 256) {
-    const int c = e >> 5, fl = e & 31, f = fs + fl;
+  for (int e = t; e < kStatW * KP; e += 256) {
+    const int c = e / kStatW, fl = e % kStatW, f = fs + fl;
     const int pi = c * FPI + f;
     const float wo = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
     const float xv = wo * sdl[fl];
@@ -299,7 +300,8 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
     }
     __syncthreads();
     // residual tile -> global, in the A-operand layout of the backward MFMA
-    *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
+    // (rows of the padding classes >= K are never read by the backward)
+    if ((((tid * 4) & 511) >> 5) < K) *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
     if (wg == 0 && tid == 0) stamp(dv, slot, 11);
   }
   atomicAdd(&rsum[sc0], rs0);
@@ -414,15 +416,18 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
         const int i = kb + w + 4 * u;
         const int ic = i < ntiles ? i : ntiles - 1;
         const size_t ro = (size_t)wt.ring_tile(ic) * 32;
-        ah[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024);
-        al[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024 + 512);
+        ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (live) {  // padding-class rows of R are neither written nor read
+          ah[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024);
+          al[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024 + 512);
+        }
         b0[u] = *(const u16x8*)(xt0 + ro);
         b1[u] = *(const u16x8*)(xt1 + ro);
       }
 #pragma unroll
       for (int u = 0; u < kBwdBatch; ++u) {
         const int i = kb + w + 4 * u;
-        if (i >= ntiles || !live) ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (i >= ntiles) ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         acc[0] = mfma16x16x32(as_bf16x8(ah[u]), as_bf16x8(b0[u]), acc[0]);
         acc[0] = mfma16x16x32(as_bf16x8(al[u]), as_bf16x8(b0[u]), acc[0]);
         acc[1] = mfma16x16x32(as_bf16x8(ah[u]), as_bf16x8(b1[u]), acc[1]);
@@ -831,12 +836,12 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
 
 // ---------------------------------------------------------------------------
 size_t stats_prep_lds_bytes() {
-  return 2 * 32 * sizeof(double) + 2 * 32 * sizeof(float) + kMaxFusedIngest * 32 * sizeof(uint16_t);
+  return 2 * kStatW * sizeof(double) + 2 * kStatW * sizeof(float) + kMaxFusedIngest * kStatW * sizeof(uint16_t);
 }
 
 void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int B, int start,
                        const RingIngest& ing, hipStream_t s) {
-  stats_prep_kernel<<<cfg.Fp / 32, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl, B, start, ing);
+  stats_prep_kernel<<<cfg.Fp / kStatW, 256, stats_prep_lds_bytes(), s>>>(cfg, prm, dv, ctrl, B, start, ing);
 }
 const void* stats_prep_symbol() { return (const void*)stats_prep_kernel; }
 

@@ -36,7 +36,11 @@ class SolverOptions:
     zero_const: bool = True  # Spark: zero-std features get coefficient 0
     tol: float = 1e-6
     standardize: bool = True  # Spark default; the dense MFMA solver always standardises
-    use_graph: bool = True
+    # None = per-solver default: the dense solve launches eagerly (measured faster on
+    # MI355X: a graph's completion barrier costs ~8 us before the next launch, more
+    # than the 8 eager launches' host time, which the GPU-bound loop hides), the
+    # wide solve replays one hipGraph
+    use_graph: bool | None = None
     max_eval_wg: int = 512
     fused_ingest: bool = True  # GPU: new stream rows are copied into the ring by the solve's first kernel
 
@@ -101,7 +105,7 @@ class LocalSolveOp:
         self._native = h.LocalSolver(
             cfg, ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
-            self.loss.data_ptr(), self.stats.data_ptr(), o.max_eval_wg, o.use_graph)
+            self.loss.data_ptr(), self.stats.data_ptr(), o.max_eval_wg, bool(o.use_graph))
         self._bound = key
 
     def run(self, ring, B: int, start: int, w_old: torch.Tensor):
@@ -186,21 +190,36 @@ class EvalSet:
 
     def eval_pair_to_slots(self, frag_a: Fragments | None, w_a: torch.Tensor, frag_b: Fragments | None,
                            w_b: torch.Tensor, scratch: "EvalScratch", slot_a: int, seq_a: int, loss_a, slot_b: int,
-                           seq_b: int):
-        """Two models whose fragments share one buffer (columns frag_a.coff.. and
-        frag_b.coff..) evaluated in ONE pass over the test set."""
+                           seq_b: int, apply=None):
+        """Model a (fragment columns frag_a.coff..) and model b (columns frag_b.coff..,
+        its own buffer; slot_b = 0: no row for b) evaluated in ONE pass over the
+        test set.  ``apply`` = (w, deltas, lr, frag_out): the same launch also does
+        the server update w += lr * sum(deltas) with the new fragments written to
+        ``frag_out`` (a buffer this launch does not read)."""
         s = self.spec
         if is_gpu(self.device):
-            if frag_a.hi.data_ptr() != frag_b.hi.data_ptr():
-                raise ValueError("paired evaluation needs one shared fragment buffer")
-            _native.hip().test_eval(s.Fp, s.K, self.X.data_ptr(), self.y.data_ptr(), self.T, frag_a.hi.data_ptr(),
-                                    frag_a.lo.data_ptr(), frag_a.b.data_ptr(), scratch.acc.data_ptr(),
-                                    stream_handle(self.device), scratch.ticket.data_ptr(), int(slot_a),
-                                    loss_a.data_ptr() if loss_a is not None else 0, int(seq_a), frag_a.coff,
-                                    frag_b.coff, int(slot_b), int(seq_b))
+            if frag_a.coff + s.K > frag_b.coff:
+                raise ValueError("paired evaluation: model a's columns must precede model b's")
+            w = ds = None
+            lr, fo = 0.0, None
+            if apply is not None:
+                w, ds, lr, fo = apply
+            _native.hip().eval_apply(
+                s.Fp, s.K, s.F, self.X.data_ptr(), self.y.data_ptr(), self.T, frag_a.hi.data_ptr(),
+                frag_a.lo.data_ptr(), frag_a.b.data_ptr(), frag_b.hi.data_ptr(), frag_b.lo.data_ptr(),
+                frag_b.b.data_ptr(), scratch.acc.data_ptr(), stream_handle(self.device), scratch.ticket.data_ptr(),
+                int(slot_a), loss_a.data_ptr() if loss_a is not None else 0, int(seq_a), frag_a.coff, frag_b.coff,
+                int(slot_b), int(seq_b), w.data_ptr() if w is not None else 0,
+                [d.data_ptr() for d in ds] if ds else [], float(lr), fo.hi.data_ptr() if fo else 0,
+                fo.lo.data_ptr() if fo else 0, fo.b.data_ptr() if fo else 0)
             return
         self.eval_to_slot(frag_a, w_a, scratch, slot_a, seq_a, loss_a)
-        self.eval_to_slot(frag_b, w_b, scratch, slot_b, seq_b, None)
+        if slot_b:
+            self.eval_to_slot(frag_b, w_b, scratch, slot_b, seq_b, None)
+        if apply is not None:
+            w, ds, lr, _ = apply
+            for d in ds:
+                w.add_(d, alpha=lr)
 
 
 

@@ -165,7 +165,8 @@ class WideSolveOp:
         self._native = h.WideSolver(c, ring.idx.data_ptr(), ring.val.data_ptr(), ring.nnz.data_ptr(),
                                     ring.y.data_ptr(), w_old.data_ptr(), self.dloc.data_ptr(), self.wloc.data_ptr(),
                                     self.loss.data_ptr(), self.stats.data_ptr(), self.uniq.data_ptr(),
-                                    self.delta.data_ptr() if self.delta is not None else 0, o.use_graph)
+                                    self.delta.data_ptr() if self.delta is not None else 0,
+                                    o.use_graph is not False)
         self._bound = key
 
     @property

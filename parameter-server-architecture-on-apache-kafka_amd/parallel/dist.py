@@ -318,7 +318,7 @@ class DistEngine:
                     else:
                         dist.broadcast(new_w, src=0)
                 elif sched == "sharded":  # key-range shards of the master weights (KeyRange.java:11-49)
-                    srv.side.fence()  # srv.w / fragments are rewritten below
+                    srv.before_update()  # srv.w / fragments are rewritten below
                     if delta.data_ptr() != pad.data_ptr():  # the solver writes into pad[:P] directly
                         pad[:P].copy_(delta)
                     lo = self.rank * shard

@@ -133,6 +133,8 @@ class WorkerRole:
         if self.delay_s > 0:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)
+        if self.pair is not None:
+            self.pair.flush_worker()  # a deferred row reads the model this solve overwrites
         self.side.fence()  # the last evaluation read the solver outputs this solve overwrites
         self.solver.run(self.ring, B, start, self.w)
         self.iters += 1
@@ -163,6 +165,7 @@ class ServerRole:
         self.wide = is_wide(spec)
         self.w = w0.to(self.device, torch.float32).clone()
         self.frag = Fragments(spec, self.device) if is_gpu(self.device) and not self.wide else None
+        self.frag_next = None  # EvalPair: the second fragment buffer of the fused update
         if self.frag is not None:
             self.frag.refresh(self.w)
         self.tracker = _native.host.VectorClockTracker(cfg.num_workers, cfg.consistency_model)
@@ -176,11 +179,20 @@ class ServerRole:
     def apply(self, delta: torch.Tensor, lr: float | None = None):
         """w += lr * delta   (ServerProcessor.java:148-151 with lr = 1/N)."""
         lr = self.cfg.lr if lr is None else lr
-        self.side.fence()  # the last server evaluation reads w / the fragments rewritten here
+        if self.pair is not None and self.pair.fused_apply([delta], lr):
+            return
+        self.before_update()  # the last server evaluation reads w / the fragments rewritten here
         if self.wide:
             wide_server_apply(self.spec, self.w, delta, lr)
         else:
             server_apply(self.spec, self.w, delta, lr, self.frag)
+
+    def before_update(self):
+        """Every reader of the current global model is enqueued before w / the
+        fragments are rewritten (a deferred paired row, a side-stream evaluation)."""
+        if self.pair is not None:
+            self.pair.flush_worker()
+        self.side.fence()
 
     def apply_round(self, deltas, vc: int, log, lr: float | None = None):
         """BSP round: w += lr * sum(deltas), then the server eval row."""
@@ -188,8 +200,11 @@ class ServerRole:
             self.apply_and_log(deltas[0], vc, log, lr)
             return
         if all(isinstance(d, torch.Tensor) for d in deltas):
+            if self.pair is not None and self.pair.fused_apply(deltas, self.cfg.lr if lr is None else lr):
+                self.log_eval(vc, log)
+                return
             if self.frag is not None and not self.wide and len(deltas) <= 16:  # one fused kernel
-                self.side.fence()
+                self.before_update()
                 sp = self.spec
                 _native.hip().server_apply_n(sp.K, sp.F, sp.Fp, self.w.data_ptr(), [d.data_ptr() for d in deltas],
                                              float(self.cfg.lr if lr is None else lr), self.frag.hi.data_ptr(),
@@ -232,23 +247,32 @@ class EvalPair:
     """Sequential consistency with a colocated server: the worker's row of
     round r (its locally trained model) and the server's row of round r-1 (the
     global model, unchanged until the update of round r) are evaluated in ONE
-    pass over the device-resident test set.  On the GPU the worker's solver and
-    the server share one MFMA fragment buffer -- worker classes in columns
-    [0, KP), server classes in [16 - K, 16) -- and the eval kernel computes both
-    models' logits with the same MFMAs.  Server rows keep the timestamp of the
-    update that produced them."""
+    pass over the device-resident test set, and on the GPU that same launch also
+    performs the server update of round r:
+
+    * the worker's solver writes its model's MFMA fragments at columns [0, KP)
+      of its own buffer; the server keeps TWO fragment buffers (columns
+      [16 - K, 16)) -- ``server.frag`` holds the current global model, the update
+      writes the other one, then they swap -- so nothing a launch reads is
+      written by it;
+    * the worker row is deferred from ``worker_row`` to the server update that
+      follows it (``fused_apply``); if no update comes before the worker's next
+      solve, it is evaluated on its own first.
+
+    Server rows keep the timestamp of the update that produced them."""
 
     def __init__(self, server: "ServerRole", worker: WorkerRole):
         self.server, self.worker = server, worker
         self.pending = None  # (log, vc, ts) of a deferred server row
+        self.pending_worker = None  # (log, vc, nseen, ts) of a deferred worker row
+        self.fuse = os.environ.get("PSX_FUSED_APPLY", "1") != "0"
         spec = server.spec
         self.shared = (is_gpu(server.device) and not server.wide and server.evalset is worker.evalset
                        and server.evalset is not None and _solver_padded_classes(spec.K) + spec.K <= 16)
         if self.shared:
             server.frag = Fragments(spec, server.device, coff=16 - spec.K)
             server.frag.refresh(server.w)
-            worker.solver.frag = Fragments(spec, worker.device, coff=0, share=server.frag)
-            worker.solver._bound = None  # rebind the native solver to the shared fragments
+            server.frag_next = Fragments(spec, server.device, coff=16 - spec.K)
         server.pair = self
         worker.pair = self
 
@@ -258,25 +282,58 @@ class EvalPair:
         self.pending = (log, int(vc), int(ts) if ts is not None else int(time.time() * 1000))
 
     def worker_row(self, log):
-        wk, srv = self.worker, self.server
+        wk = self.worker
         if log is None or wk.evalset is None:
             return
+        self.flush_worker()
+        if self.shared:  # evaluated together with the server update that follows
+            self.pending_worker = (log, int(wk.vc), int(wk.tuples_seen), int(time.time() * 1000))
+            return
+        self.flush(self.pending[0] if self.pending is not None else None)
+        self._worker_only(log, int(wk.vc), int(wk.tuples_seen))
+
+    def fused_apply(self, deltas, lr: float) -> bool:
+        """The server update of this round in the launch that evaluates the
+        deferred worker row (and the pending server row).  False: nothing to fuse
+        with (the caller applies on its own)."""
+        pw = self.pending_worker
+        if pw is None or not self.shared or not self.fuse or not (1 <= len(deltas) <= 16):
+            return False
+        if not all(isinstance(d, torch.Tensor) for d in deltas):
+            return False
+        self.pending_worker = None
+        srv = self.server
+        srv.side.fence()
+        self._pair(pw, apply=(srv.w, list(deltas), float(lr), srv.frag_next))
+        srv.frag, srv.frag_next = srv.frag_next, srv.frag
+        return True
+
+    def flush_worker(self):
+        """Evaluate a deferred worker row now (before the solver overwrites its model)."""
+        pw = self.pending_worker
+        if pw is None:
+            return
+        self.pending_worker = None
+        self._pair(pw)
+
+    def _pair(self, pw, apply=None):
+        log, vc, nseen, ts = pw
+        wk, srv = self.worker, self.server
         pend = self.pending
-        self.pending = None
         if pend is not None and pend[0] is not log:  # a different sink (bench swapped logs): flush separately
             self._server_only(pend)
             pend = None
-        if pend is not None and self.shared:
-            log.pair_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.solver.loss, wk.k, wk.vc, wk.tuples_seen,
-                          srv.frag, srv.w, pend[1], pend[2], wk.scratch)
-            return
-        if pend is not None:
-            self._server_only(pend)
+        self.pending = None
+        log.pair_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.solver.loss, wk.k, vc, nseen, srv.frag, srv.w,
+                      pend[1] if pend is not None else None, pend[2] if pend is not None else 0, wk.scratch, ts_w=ts,
+                      apply=apply)
+
+    def _worker_only(self, log, vc: int, nseen: int):
+        wk = self.worker
         if wk.wide:
-            log.worker_eval(wk.evalset, wk.solver, wk.w, wk.scratch, wk.solver.loss, wk.k, wk.vc, wk.tuples_seen)
+            log.worker_eval(wk.evalset, wk.solver, wk.w, wk.scratch, wk.solver.loss, wk.k, vc, nseen)
         else:
-            log.worker_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.scratch, wk.solver.loss, wk.k, wk.vc,
-                            wk.tuples_seen)
+            log.worker_eval(wk.evalset, wk.solver.frag, wk.solver.w_new, wk.scratch, wk.solver.loss, wk.k, vc, nseen)
 
     def _server_only(self, pend):
         log, vc, ts = pend
@@ -284,6 +341,7 @@ class EvalPair:
         log.server_eval(srv.evalset, srv.frag, srv.w, srv.scratch, vc, ts=ts)
 
     def flush(self, log=None):
+        self.flush_worker()
         if self.pending is not None:
             pend = self.pending
             self.pending = None

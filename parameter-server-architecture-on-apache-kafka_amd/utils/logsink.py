@@ -87,13 +87,17 @@ class LogSink:
         self.native.submit(slot, seq, 1, ts, -1, int(vc), 0)
 
     def pair_eval(self, evalset, frag_w, w_w, loss_dev, partition: int, vc_w: int, nseen: int, frag_s, w_s,
-                  vc_s: int, ts_s: int, scratch):
-        """Worker row (local model) + server row (global model) from one evaluation pass."""
+                  vc_s: int | None, ts_s: int, scratch, ts_w: int | None = None, apply=None):
+        """Worker row (local model) + server row (global model; vc_s None: none)
+        from one evaluation pass, optionally fused with the server update (``apply``)."""
         slot_w, seq_w, addr_w = self.native.acquire()
-        slot_s, seq_s, addr_s = self.native.acquire()
-        ts_w = now_ms()
-        evalset.eval_pair_to_slots(frag_w, w_w, frag_s, w_s, scratch, addr_w, seq_w, loss_dev, addr_s, seq_s)
-        self.native.submit(slot_s, seq_s, 1, int(ts_s), -1, int(vc_s), 0)
+        slot_s = seq_s = addr_s = 0
+        if vc_s is not None:
+            slot_s, seq_s, addr_s = self.native.acquire()
+        ts_w = now_ms() if ts_w is None else int(ts_w)
+        evalset.eval_pair_to_slots(frag_w, w_w, frag_s, w_s, scratch, addr_w, seq_w, loss_dev, addr_s, seq_s, apply)
+        if vc_s is not None:
+            self.native.submit(slot_s, seq_s, 1, int(ts_s), -1, int(vc_s), 0)
         self.native.submit(slot_w, seq_w, 0, ts_w, int(partition), int(vc_w), int(nseen))
 
     # -- consumers ---------------------------------------------------------

@@ -234,6 +234,53 @@ def test_paired_eval_matches_single(cuda):
     assert scratch.acc.abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("ndeltas,server_row", [(1, True), (3, True), (1, False)])
+def test_eval_apply_fused(cuda, ndeltas, server_row):
+    """Worker row + previous server row + the server update in ONE launch: rows
+    exactly those of separate evaluations, update == server_apply_n, and the new
+    fragments land in the other buffer (the one read stays untouched)."""
+    from psx.ops.lr import EvalScratch
+    from psx.utils.logsink import LogSink
+
+    spec = ModelSpec(1024, 6)
+    te = synth_finefood(4877, seed=12)
+    ev = EvalSet(spec, te.X, te.y, cuda)
+    wa, ws = _rand_w(spec, 23, 0.5).to(cuda), _rand_w(spec, 24, 0.5).to(cuda)
+    deltas = [_rand_w(spec, 50 + i, 0.2).to(cuda) for i in range(ndeltas)]
+    fa = Fragments(spec, cuda)
+    fa.refresh(wa)
+    cur, nxt = Fragments(spec, cuda, coff=16 - spec.K), Fragments(spec, cuda, coff=16 - spec.K)
+    cur.refresh(ws)
+    cur_hi = cur.hi.clone()
+    w_srv = ws.clone()
+    ref = ws + 0.25 * sum(deltas)
+    log = LogSink(spec.K, cuda)
+    scratch = EvalScratch(cuda)
+    loss = torch.tensor([0.75], device=cuda)
+    log.pair_eval(ev, fa, wa, loss, 0, 9, 100, cur, w_srv, 8 if server_row else None, 4321, scratch,
+                  apply=(w_srv, deltas, 0.25, nxt))
+    fb = Fragments(spec, cuda, coff=16 - spec.K)
+    fb.refresh(ws)
+    log.worker_eval(ev, fa, wa, scratch, loss, 0, 9, 100)
+    if server_row:
+        log.server_eval(ev, fb, ws, scratch, 8, ts=4321)
+    book = log.book
+    log.close()
+    torch.cuda.synchronize()
+    assert len(book.worker) == 2 and book.worker[0][1:] == book.worker[1][1:]
+    if server_row:
+        assert len(book.server) == 2 and book.server[0] == book.server[1]
+    else:
+        assert not book.server
+    assert torch.allclose(w_srv, ref, atol=1e-6)
+    fr = Fragments(spec, cuda, coff=16 - spec.K)
+    fr.refresh(ref)
+    assert torch.equal(nxt.hi, fr.hi) and torch.equal(nxt.lo, fr.lo)
+    assert torch.allclose(nxt.b[16 - spec.K:], spec.intercept(ref), atol=1e-6)
+    assert torch.equal(cur.hi, cur_hi)
+    assert scratch.acc.abs().sum().item() == 0
+
+
 def test_server_apply_n_matches_sum(cuda):
     from psx import _native
     from psx.ops.lr import stream_handle

@@ -93,7 +93,7 @@ def main():
         ("gd x4 (5 slots)", SolverOptions(mode="gd", iters=4), 1024),
         ("default, B=32 (1 tile)", SolverOptions(), 32),
         ("init only, B=32", SolverOptions(iters=1, ls_max=0), 32),
-        ("default, no graph", SolverOptions(use_graph=False), 1024),
+        ("default, hipGraph replay", SolverOptions(use_graph=True), 1024),
     ]:
         op = LocalSolveOp(spec, 1024, dev, opts)
         us = time_solve(op, ring, B, w)

@@ -139,21 +139,26 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
     *last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!*last) return;
+  // Publication into the pinned (fine-grained, uncached) host slot: the counts
+  // go out as system-scope relaxed stores, every wave drains them (vmcnt), and
+  // only then is the sequence number stored.  No release fence: it would write
+  // back this XCD's whole L2 (the solver's dirty lines included), and nothing
+  // cached is being published.
   const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ((int*)slot)[tid] = tot;
-  if (tid == 0) *(float*)(slot + 1024) = loss ? *loss : 0.f;
+  __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (pair) {
     const int tot2 = __hip_atomic_exchange(acc + 256 + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ((int*)slot2)[tid] = tot2;
-    if (tid == 0) *(float*)(slot2 + 1024) = 0.f;
+    __hip_atomic_store((int*)slot2 + tid, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) __hip_atomic_store((float*)(slot2 + 1024), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (pair)
-      __hip_atomic_store((unsigned long long*)(slot2 + 1032), seq2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store((unsigned long long*)(slot2 + 1032), seq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

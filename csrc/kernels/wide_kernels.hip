@@ -666,7 +666,8 @@ __global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d
     d.stats[2] = ctrl->ls_fail;
     d.stats[3] = ctrl->dir_reset;
     d.cnt[2] = U;
-    if (d.host_u) __hip_atomic_store(d.host_u, U, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // read by the host after a stream synchronisation: no release (an L2 writeback) needed
+    if (d.host_u) __hip_atomic_store(d.host_u, U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -903,14 +904,16 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
     last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
+  // publication as in test_eval_kernel: drained system-scope stores into the
+  // uncached host slot, then the sequence number (no L2-writeback fence)
   const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  ((int*)slot)[tid] = tot;
-  if (tid == 0) *(float*)(slot + 1024) = loss ? *loss : 0.f;
-  __threadfence_system();
+  __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

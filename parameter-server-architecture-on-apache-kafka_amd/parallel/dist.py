@@ -150,9 +150,11 @@ class DistEngine:
         self.rounds = 0
         self._ctrl = None
         self._next_vc = 0
-        if (not self.async_mode and cfg.pair_eval and self.is_server and self.server is not None
-                and self.worker is not None):
-            EvalPair(self.server, self.worker)  # rank 0: worker row + previous server row in one eval pass
+        if (not self.async_mode and cfg.pair_eval and (self.is_server or cfg.bsp_schedule == "allreduce")
+                and self.server is not None and self.worker is not None):
+            # rank 0: worker row + previous server row + the update in one launch; the other
+            # allreduce ranks: worker row + their replica's update in one launch
+            EvalPair(self.server, self.worker)
         # resume: rank 0 restores the server, every worker rank its own worker file;
         # BSP continues at the server's round (agreed over a collective)
         resumed = maybe_resume(cfg, self.server if self.is_server else None,

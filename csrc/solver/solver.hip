@@ -1,6 +1,4 @@
 #include "solver.h"
-
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 

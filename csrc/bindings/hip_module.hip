@@ -368,15 +368,19 @@ PYBIND11_MODULE(_psx_hip, m) {
       "wide_eval",
       [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int T, uintptr_t w,
          uintptr_t map, uintptr_t wloc, uintptr_t acc, uintptr_t ticket, uintptr_t slot, uintptr_t loss,
-         unsigned long long seq, uintptr_t stream) {
+         unsigned long long seq, uintptr_t stream, uintptr_t slot2, unsigned long long seq2) {
+        if (slot2 && (!slot || !map || !wloc))
+          throw std::invalid_argument("wide_eval: the paired row needs a slot and the overlay");
         launch_wide_eval(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val),
                          P<const int32_t>(y), T, P<const float>(w), P<const int32_t>(map), P<const float>(wloc),
-                         P<int>(acc), P<unsigned>(ticket), P<void>(slot), P<const float>(loss), seq, S(stream));
+                         P<int>(acc), P<unsigned>(ticket), P<void>(slot), P<const float>(loss), seq, S(stream),
+                         P<void>(slot2), seq2);
         hip_check(hipGetLastError(), "wide_eval launch");
       },
       py::arg("K"), py::arg("KP"), py::arg("F"), py::arg("indptr"), py::arg("idx"), py::arg("val"), py::arg("y"),
       py::arg("T"), py::arg("w"), py::arg("map"), py::arg("wloc"), py::arg("acc"), py::arg("ticket") = 0,
-      py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0, py::arg("stream") = 0);
+      py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0, py::arg("stream") = 0, py::arg("slot2") = 0,
+      py::arg("seq2") = 0);
   m.def("wide_logits", [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, int T,
                           uintptr_t w, uintptr_t out, uintptr_t stream) {
     launch_wide_logits(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val), T,

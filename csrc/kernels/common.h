@@ -5,6 +5,10 @@
 
 namespace psx {
 
+// Private evaluation accumulators (EvalSlot mode): cell i at acc[i * kAccStride],
+// one 128-B cache line per cell; [2 models][256 cells] -> 2*256*kAccStride ints.
+constexpr int kAccStride = 32;
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));

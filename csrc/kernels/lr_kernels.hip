@@ -127,10 +127,13 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   }
   __syncthreads();
   const int v = cl[tid];
-  if (v) atomicAdd(acc + tid, v);
+  // the private accumulator (slot mode) spreads its cells one per 128-B line, so
+  // the workgroups' atomics are not serialised on a few cache lines (kAccStride)
+  const int ast = slot ? kAccStride : 1;
+  if (v) atomicAdd(acc + tid * ast, v);
   if (pair) {
     const int v2 = cl2[tid];
-    if (v2) atomicAdd(acc + 256 + tid, v2);
+    if (v2) atomicAdd(acc + (256 + tid) * ast, v2);
   }
   if (slot == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -144,11 +147,11 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   // only then is the sequence number stored.  No release fence: it would write
   // back this XCD's whole L2 (the solver's dirty lines included), and nothing
   // cached is being published.
-  const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int tot = __hip_atomic_exchange(acc + tid * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (pair) {
-    const int tot2 = __hip_atomic_exchange(acc + 256 + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int tot2 = __hip_atomic_exchange(acc + (256 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((int*)slot2 + tid, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid == 0) __hip_atomic_store((float*)(slot2 + 1024), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }

@@ -132,7 +132,8 @@ void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const 
 // EvalSlot protocol as launch_test_eval.
 void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
                       const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
-                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s);
+                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
+                      void* slot2 = nullptr, unsigned long long seq2 = 0);
 // Margins of T rows (tests): out[T][KP].
 void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
                         int T, const float* w, float* out, hipStream_t s);

@@ -859,44 +859,136 @@ __device__ __forceinline__ void wide_row_margins(int64_t F, const int64_t* __res
   for (int k = 0; k < KP; ++k) z[k] += bv[k];
 }
 
+// Margins of up to 4 rows per wave for the evaluation: 16 lanes per row, each
+// lane with 4 entries' loads in flight (ids/values, then the local-model map,
+// then the weight rows), so a wave keeps 4 rows x 64 gathers outstanding
+// instead of walking one row's dependent load chain at a time.
+// PAIR: also the margins zb of the plain model w (no overlay) from the same
+// gathers -- the worker's local model and the global model it was trained from
+// differ only on the window's features.
+template <int KP, bool PAIR>
+__device__ __forceinline__ void wide_rows4_margins(int64_t F, const int64_t* __restrict__ indptr,
+                                                  const int32_t* __restrict__ idx,
+                                                  const uint16_t* __restrict__ val, int64_t row, bool valid,
+                                                  const float* __restrict__ w, const int32_t* __restrict__ map,
+                                                  const float* __restrict__ wloc, float (&z)[KP], float (&zb)[KP]) {
+  const int l = threadIdx.x & 15;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z[k] = zb[k] = 0.f;
+  if (valid) {
+    const int64_t a = indptr[row], b = indptr[row + 1];
+    for (int64_t e0 = a + l; e0 < b; e0 += 64) {
+      int f[4];
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t e = e0 + 16 * u;
+        const bool ok = e < b;
+        f[u] = ok ? idx[e] : -1;
+        v[u] = ok ? bf2f(val[e]) : 0.f;
+      }
+      const float* src[4];
+      bool ov[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        src[u] = f[u] >= 0 ? w + (int64_t)f[u] * KP : nullptr;
+        ov[u] = false;
+        if (map && f[u] >= 0) {
+          const int li = map[f[u]];
+          if (li >= 0) {
+            src[u] = wloc + KP + (int64_t)li * KP;
+            ov[u] = true;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (src[u]) {
+          float wv[KP];
+          ldk<KP>(src[u], wv);
+#pragma unroll
+          for (int k = 0; k < KP; ++k) z[k] += v[u] * wv[k];
+          if constexpr (PAIR) {
+            if (ov[u]) ldk<KP>(w + (int64_t)f[u] * KP, wv);
+#pragma unroll
+            for (int k = 0; k < KP; ++k) zb[k] += v[u] * wv[k];
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      z[k] += __shfl_xor(z[k], o, 64);
+      if constexpr (PAIR) zb[k] += __shfl_xor(zb[k], o, 64);
+    }
+  }
+  float bv[KP];
+  ldk<KP>(map ? wloc : w + F * KP, bv);
+#pragma unroll
+  for (int k = 0; k < KP; ++k) z[k] += bv[k];
+  if constexpr (PAIR) {
+    ldk<KP>(w + F * KP, bv);
+#pragma unroll
+    for (int k = 0; k < KP; ++k) zb[k] += bv[k];
+  }
+}
+
 template <int KP>
+__device__ __forceinline__ int wide_argmax(int K, const float (&z)[KP]) {
+  if (K == 1) return z[0] > 0.f ? 1 : 0;
+  int best = 0;
+  float bz = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < KP; ++k)
+    if (k < K && z[k] > bz) {
+      bz = z[k];
+      best = k;
+    }
+  return best;
+}
+
+// Paired mode (slot2 != nullptr, needs the overlay): row 1 = the overlay model
+// (the worker's local model), row 2 = the plain model w (the global model it was
+// trained from), one pass.
+template <int KP, bool PAIR>
 __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const int64_t* __restrict__ indptr,
                                                         const int32_t* __restrict__ idx,
                                                         const uint16_t* __restrict__ val,
                                                         const int32_t* __restrict__ y, int T,
                                                         const float* __restrict__ w, const int32_t* __restrict__ map,
                                                         const float* __restrict__ wloc, int* acc, unsigned* ticket,
-                                                        char* slot, const float* loss, unsigned long long seq) {
-  __shared__ int cl[256];
+                                                        char* slot, const float* loss, unsigned long long seq,
+                                                        char* slot2, unsigned long long seq2) {
+  __shared__ int cl[2][256];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63;
-  cl[tid] = 0;
+  cl[0][tid] = 0;
+  cl[1][tid] = 0;
   __syncthreads();
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (tid >> 6); r < T; r += (int64_t)gridDim.x * 4) {
-    float z[KP];
-    wide_row_margins<KP>(F, indptr, idx, val, r, w, map, wloc, z);
-    if (lane == 0) {
-      int best = 0;
-      if (K == 1) {
-        best = z[0] > 0.f ? 1 : 0;
-      } else {
-        float bz = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < KP; ++k)
-          if (k < K && z[k] > bz) {
-            bz = z[k];
-            best = k;
-          }
-      }
+  // 16 rows per workgroup pass: wave (tid >> 6), lane group (lane >> 4)
+  for (int64_t r0 = (int64_t)blockIdx.x * 16; r0 < T; r0 += (int64_t)gridDim.x * 16) {
+    const int64_t r = r0 + (tid >> 4);
+    float z[KP], zb[KP];
+    wide_rows4_margins<KP, PAIR>(F, indptr, idx, val, r, r < T, w, map, wloc, z, zb);
+    if ((lane & 15) == 0 && r < T) {
       int yl = y[r];
       if (K == 1) yl = yl > 0 ? 1 : 0;
       yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
-      atomicAdd(&cl[yl * 16 + best], 1);
+      atomicAdd(&cl[0][yl * 16 + wide_argmax<KP>(K, z)], 1);
+      if constexpr (PAIR) atomicAdd(&cl[1][yl * 16 + wide_argmax<KP>(K, zb)], 1);
     }
   }
   __syncthreads();
-  const int v = cl[tid];
-  if (v) atomicAdd(acc + tid, v);
+  const int ast = slot ? kAccStride : 1;  // slot mode: one cell per 128-B line (see test_eval_kernel)
+  const int v = cl[0][tid];
+  if (v) atomicAdd(acc + tid * ast, v);
+  if constexpr (PAIR) {
+    const int v2 = cl[1][tid];
+    if (v2) atomicAdd(acc + (256 + tid) * ast, v2);
+  }
   if (slot == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -906,14 +998,21 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
   if (!last) return;
   // publication as in test_eval_kernel: drained system-scope stores into the
   // uncached host slot, then the sequence number (no L2-writeback fence)
-  const int tot = __hip_atomic_exchange(acc + tid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int tot = __hip_atomic_exchange(acc + tid * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if constexpr (PAIR) {
+    const int tot2 = __hip_atomic_exchange(acc + (256 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((int*)slot2 + tid, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) __hip_atomic_store((float*)(slot2 + 1024), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if constexpr (PAIR)
+      __hip_atomic_store((unsigned long long*)(slot2 + 1032), seq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -938,14 +1037,21 @@ __global__ __launch_bounds__(256) void wide_logits_kernel(int64_t F, const int64
 
 void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
                       const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
-                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s) {
+                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
+                      void* slot2, unsigned long long seq2) {
   if (T <= 0) return;
-  const int grid = grid_for((int64_t)T * 64, 1024);
+  const int grid = grid_for((int64_t)T * 16, 1024);  // 16 rows per workgroup pass
   char* sl = static_cast<char*>(slot);
-#define PSX_WE(KV)                                                                                              \
-  case KV:                                                                                                      \
-    wide_eval_kernel<KV><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc, ticket, sl, loss, \
-                                              seq);                                                             \
+  char* sl2 = static_cast<char*>(slot2);
+  const bool pair = sl2 != nullptr;
+#define PSX_WE(KV)                                                                                             \
+  case KV:                                                                                                     \
+    if (pair)                                                                                                  \
+      wide_eval_kernel<KV, true><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc, ticket, \
+                                                      sl, loss, seq, sl2, seq2);                              \
+    else                                                                                                       \
+      wide_eval_kernel<KV, false><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc,       \
+                                                       ticket, sl, loss, seq, nullptr, 0);                    \
     break;
   switch (KP) {
     PSX_WE(1)

@@ -223,11 +223,15 @@ class EvalSet:
 
 
 
+ACC_STRIDE = 32
+
+
 class EvalScratch:
     """Private accumulator + ticket of one evaluation caller (stays zero between calls)."""
 
     def __init__(self, device):
-        self.acc = torch.zeros(512, dtype=torch.int32, device=device)  # [2 models][16][16]
+        # [2 models][16][16] cells, one per 128-B line (kAccStride in csrc/kernels/lr_kernels.h)
+        self.acc = torch.zeros(2 * 256 * ACC_STRIDE, dtype=torch.int32, device=device)
         self.ticket = torch.zeros(4, dtype=torch.int32, device=device)
 
 

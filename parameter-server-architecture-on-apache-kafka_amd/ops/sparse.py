@@ -290,6 +290,27 @@ class WideEvalSet:
         weff = overlay.local_model(w) if overlay is not None else w
         _write_slot_cpu(slot_addr, self.confusion_cpu(weff), float(loss.item()) if loss is not None else 0.0, seq)
 
+    def eval_pair_to_slots(self, overlay, w_a: torch.Tensor, _frag_b, w_b: torch.Tensor, scratch, slot_a: int,
+                           seq_a: int, loss_a, slot_b: int, seq_b: int, apply=None):
+        """Row a: ``w_a`` overlaid with the worker's local solution; row b: the plain
+        global model ``w_b``.  On the GPU, when ``w_b`` IS ``w_a`` (the worker
+        trained from the current global model), both come from ONE pass: the two
+        models differ only on the window's features."""
+        if apply is not None:
+            raise ValueError("the wide evaluation does not fuse the server update")
+        if (is_gpu(self.device) and slot_b and overlay is not None and w_a.data_ptr() == w_b.data_ptr()):
+            s = self.spec
+            _native.hip().wide_eval(s.K, s.KP, s.F, self.ds.indptr.data_ptr(), self.ds.idx.data_ptr(),
+                                    self.ds.val.data_ptr(), self.ds.y.data_ptr(), self.T, w_a.data_ptr(),
+                                    overlay.map_ptr, overlay.wloc.data_ptr(), scratch.acc.data_ptr(),
+                                    scratch.ticket.data_ptr(), int(slot_a),
+                                    loss_a.data_ptr() if loss_a is not None else 0, int(seq_a),
+                                    stream_handle(self.device), int(slot_b), int(seq_b))
+            return
+        self.eval_to_slot(overlay, w_a, scratch, slot_a, seq_a, loss_a)
+        if slot_b:
+            self.eval_to_slot(None, w_b, scratch, slot_b, seq_b, None)
+
 
 def wide_server_apply(spec: WideSpec, w: torch.Tensor, delta, lr: float):
     """w += lr * delta; ``delta`` dense [P] or a :class:`SparseDelta`."""

@@ -104,7 +104,9 @@ class LocalEngine:
         self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
                         for k in range(cfg.num_workers)]
         self.rounds = 0
-        if cfg.consistency_model == 0 and cfg.pair_eval:  # worker 0's rows and the server rows: one eval pass
+        # worker 0's rows and the server rows: one eval pass (sequential consistency,
+        # or one worker, which every model runs lock-step)
+        if (cfg.consistency_model == 0 or cfg.num_workers == 1) and cfg.pair_eval:
             EvalPair(self.server, self.workers[0])
         self.failed: set[int] = set()
         if maybe_resume(cfg, self.server, self.workers):
@@ -123,7 +125,11 @@ class LocalEngine:
         return False
 
     def run(self) -> dict:
-        if self.cfg.consistency_model == 0:
+        live = [w for w in self.workers if w.k not in self.failed]
+        if self.cfg.consistency_model == 0 or len(live) == 1:
+            # with a single worker every consistency model releases that worker right
+            # after its delta is applied (tracker: BSP, SSP(D) and ASP coincide), so the
+            # lock-step loop runs it without the thread / queue / event hand-offs
             out = self._run_bsp()
         else:
             out = self._run_async()

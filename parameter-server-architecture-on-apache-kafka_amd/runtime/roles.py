@@ -269,6 +269,8 @@ class EvalPair:
         spec = server.spec
         self.shared = (is_gpu(server.device) and not server.wide and server.evalset is worker.evalset
                        and server.evalset is not None and _solver_padded_classes(spec.K) + spec.K <= 16)
+        self.wide_pair = (is_gpu(server.device) and server.wide and server.evalset is worker.evalset
+                          and server.evalset is not None)
         if self.shared:
             server.frag = Fragments(spec, server.device, coff=16 - spec.K)
             server.frag.refresh(server.w)
@@ -288,6 +290,14 @@ class EvalPair:
         self.flush_worker()
         if self.shared:  # evaluated together with the server update that follows
             self.pending_worker = (log, int(wk.vc), int(wk.tuples_seen), int(time.time() * 1000))
+            return
+        pend, srv = self.pending, self.server
+        if (pend is not None and pend[0] is log and self.wide_pair and wk.w.data_ptr() == srv.w.data_ptr()):
+            # wide model: the worker's local model (overlay) and the global model it
+            # was trained from (= the previous server row's model) in one pass
+            self.pending = None
+            log.pair_eval(wk.evalset, wk.solver, wk.w, wk.solver.loss, wk.k, int(wk.vc), int(wk.tuples_seen), None,
+                          srv.w, pend[1], pend[2], wk.scratch)
             return
         self.flush(self.pending[0] if self.pending is not None else None)
         self._worker_only(log, int(wk.vc), int(wk.tuples_seen))

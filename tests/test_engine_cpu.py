@@ -57,6 +57,25 @@ def test_async_models_staleness(c):
         assert out["max_vc_gap"] >= 2  # the straggler falls behind under eventual consistency
 
 
+@pytest.mark.parametrize("c", [-1, 2])
+def test_single_worker_async_equals_sequential(c):
+    """One worker: every consistency model releases it right after its delta, so an
+    asynchronous run gives the sequential run's model and log rows."""
+    train, test = synth_finefood(2000, num_features=128, seed=0), synth_finefood(300, num_features=128, seed=1)
+    ws, books = [], []
+    for cm in (c, 0):
+        cfg = PSConfig(num_workers=1, consistency_model=cm, producer_time_per_event=0, stream_mode="per_iter",
+                       rows_per_iter=64, epochs=100, max_iters=6, min_buffer_size=128, max_buffer_size=128)
+        eng = LocalEngine(cfg, "cpu", train=train, test=test)
+        out = eng.run()
+        assert out["rounds"] == 6 and out["updates"] == 6 and out["max_vc_gap"] <= 1
+        ws.append(eng.server.w.clone())
+        books.append(eng.log.book)
+    assert torch.allclose(ws[0], ws[1], atol=1e-6)
+    assert [r[1:] for r in books[0].server] == [r[1:] for r in books[1].server]
+    assert [r[1:3] for r in books[0].worker] == [r[1:3] for r in books[1].worker]
+
+
 def test_schedule_mode_arrival_burst():
     """-p 200 with N=2: burst of 256 rows, then 5 rows per second in total."""
     train, test = synth_finefood(2000, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)

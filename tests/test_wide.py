@@ -239,6 +239,27 @@ def test_gpu_wide_eval_overlay(cuda):
 
 
 @pytest.mark.gpu
+def test_gpu_wide_paired_eval(cuda):
+    """The worker's local model (overlay) and the global model it was trained from,
+    evaluated in one pass == two separate passes (exact confusion counts)."""
+    from psx.utils.logsink import LogSink
+
+    spec, ds, opg, w = _gpu_vs_cpu(cuda, "finefood", SolverOptions(zero_const=False))
+    ev = WideEvalSet(spec, ds, cuda)
+    wg = w.to(cuda)
+    sc = EvalScratch(cuda)
+    log = LogSink(spec.eval_classes, cuda)
+    log.pair_eval(ev, opg, wg, opg.loss, 0, 5, 77, None, wg, 4, 999, sc)
+    log.worker_eval(ev, opg, wg, sc, opg.loss, 0, 5, 77)
+    log.server_eval(ev, None, wg, sc, 4, ts=999)
+    book = log.book
+    log.close()
+    (w1, w2), (s1, s2) = book.worker, book.server
+    assert w1[1:] == w2[1:] and s1 == s2 and s1[0] == 999
+    assert sc.acc.abs().sum().item() == 0
+
+
+@pytest.mark.gpu
 def test_gpu_sparse_ring_ingest(cuda):
     ds, _ = _problem(rows=100)
     NZ = 16

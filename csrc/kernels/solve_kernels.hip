@@ -510,12 +510,15 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // stores; every workgroup sweeps all slices' words with sc1 loads until each
   // carries this (run, slot)'s tag, which never repeats (no reset needed) ----
   const int ns = NS;
-  const int nv = 4 + 2 * H;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (H), Y_i.gt (H)
+  // only the m stored pairs' dots travel (ring slots (head - m + 1 + j) mod H)
+  const int nv = 4 + 2 * m;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (m), Y_i.gt (m)
+  const int hbase = ((head - m + 1) % H + H) % H;
   const unsigned tag = run_tag + (unsigned)slot + 1u;
   unsigned* gat32 = (unsigned*)gat;  // [ns][2*nv]
   if (tid < 2 * nv) {
     const int k = tid >> 1;
-    const int si = k < 3 ? k : (k == 3 ? kND : (k < 4 + H ? 3 + (k - 4) : 3 + kMaxHist + (k - 4 - H)));
+    const int ring = k < 4 ? 0 : (hbase + (k < 4 + m ? k - 4 : k - 4 - m)) % H;
+    const int si = k < 3 ? k : (k == 3 ? kND : (k < 4 + m ? 3 + ring : 3 + kMaxHist + ring));
     const double v = sdot[si] + sdot[kNDX + si] + sdot[2 * kNDX + si] + sdot[3 * kNDX + si];
     const unsigned long long u = d2u(v);
     const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
@@ -561,6 +564,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   }
   __syncthreads();
   wg_stamp(dv, slot, 3, wg);
+  if (tid < kNDX) dots[tid] = 0.0;  // pairs not stored stay 0
+  __syncthreads();
   if (tid < nv) {
     double v = 0.0;
     for (int b = 0; b < ns; ++b) {  // fixed order: identical in every workgroup
@@ -568,8 +573,9 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
           (unsigned long long)gat32[b * 2 * nv + 2 * tid] | ((unsigned long long)gat32[b * 2 * nv + 2 * tid + 1] << 32);
       v += u2d(u);
     }
-    // compact order expected by ctrl_step: 3 scalars, S_i.g (H), Y_i.g (H); loss in dots[kND]
-    const int pos = tid < 3 ? tid : (tid == 3 ? kND : tid - 1);
+    // order expected by ctrl_step: 3 scalars, S_i.g (H ring slots), Y_i.g (H); loss in dots[kND]
+    const int ring = tid < 4 ? 0 : (hbase + (tid < 4 + m ? tid - 4 : tid - 4 - m)) % H;
+    const int pos = tid < 3 ? tid : (tid == 3 ? kND : (tid < 4 + m ? 3 + ring : 3 + H + ring));
     dots[pos] = v;
   }
   __syncthreads();

@@ -89,12 +89,27 @@ __global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* _
   const uint16_t* fl = (split && lcls >= coff2) ? ea.slo : wf_lo;
   const float* b2 = split ? ea.sb : b;
   const int ntiles = (int)blockIdx.x < tgrid ? (T + 31) / 32 : 0;
+  // The weight fragments are usually fresh (written by the solve / update just
+  // before, so not in this XCD's L2): fetch them into registers BEFORE staging
+  // the first tile so the two memory latencies overlap (as fwd_kernel does);
+  // only the columns of the evaluated models are fetched.
+  constexpr bool kPre = FP <= 1024;
+  WFrag<kPre ? FP : 128> wf;
+  if constexpr (kPre) {
+    if (ntiles > (int)blockIdx.x) {
+      const bool live = (lcls >= coff1 && lcls < coff1 + K) || (pair && lcls >= coff2 && lcls < coff2 + K);
+      load_wfrag<FP>(wf, fh, fl, live ? 16 : 0);
+    }
+  }
   for (int tile = blockIdx.x; tile < ntiles; tile += tgrid) {
     const int nrows = min(32, T - tile * 32);
     stage_tile<FP>(lds, Xt, (int64_t)tile * 32, nrows, 0, false);
     __syncthreads();
     f32x4 a0, a1;
-    forward_tile<FP>(lds, fh, fl, a0, a1);
+    if constexpr (kPre)
+      forward_tile_pre<FP>(lds, wf, a0, a1);
+    else
+      forward_tile<FP>(lds, fh, fl, a0, a1);
     store_partial_logits(red_base, a0, a1);
     __syncthreads();
     if (tid < nrows) {

@@ -38,6 +38,8 @@ def main():
         "paired two buffers": lambda: log.pair_eval(ev, fa, w, loss, 0, 0, 0, cur, w, 0, 0, sc),
         "paired + fused update": lambda: log.pair_eval(ev, fa, w, loss, 0, 0, 0, cur, w, 0, 0, sc,
                                                        apply=(w, [d], 1.0, nxt)),
+        "paired, fresh fragments": lambda: (fa.refresh(w), cur.refresh(w),
+                                            log.pair_eval(ev, fa, w, loss, 0, 0, 0, cur, w, 0, 0, sc)),
     }
     for name, fn in cases.items():
         for _ in range(20):

@@ -118,6 +118,15 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
   const int fs = blockIdx.x * kStatW;
   const int nin = ing.n;
+  // the pulled weights were just written by the server update: fetch them now so
+  // their latency overlaps the window read (one element per thread: kStatW*KP <= 256)
+  const int KP0 = dv.KP;
+  float wo_pre = 0.f, b_pre = 0.f;
+  if (t < kStatW * KP0) {
+    const int c = t / kStatW, f = fs + t % kStatW;
+    if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
+  }
+  if (blockIdx.x == 0 && t < 16 && t < cfg.K) b_pre = dv.w_old[cfg.K * FP + t];
   for (int i = t; i < nin; i += 256) {  // fused ingest: one 16-B chunk of each new row
     const long long sr = ing.first + (long long)i * ing.step;
     int dr = ing.dst + i;
@@ -194,10 +203,12 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   }
   __syncthreads();
   const int K = cfg.K, KP = dv.KP, FPI = dv.FPI;
-  for (int e = t; e < kStatW * KP; e += 256) {
+  static_assert(kStatW * 16 <= 256, "one element per thread");
+  if (t < kStatW * KP) {
+    const int e = t;
     const int c = e / kStatW, fl = e % kStatW, f = fs + fl;
     const int pi = c * FPI + f;
-    const float wo = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
+    const float wo = wo_pre;
     const float xv = wo * sdl[fl];
     dv.x[pi] = xv;
     dv.d[pi] = 0.f;
@@ -209,7 +220,7 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   if (blockIdx.x == 0) {
     if (t < 16) {
       const int pi = KP * FPI + t;
-      const float b = t < K ? dv.w_old[K * FP + t] : 0.f;
+      const float b = b_pre;
       dv.x[pi] = b;
       dv.d[pi] = 0.f;
       dv.g_c[pi] = 0.f;

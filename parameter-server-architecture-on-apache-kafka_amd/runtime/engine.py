@@ -15,6 +15,7 @@ and logging code as the distributed engine.
 """
 from __future__ import annotations
 
+import dataclasses
 import queue
 import threading
 import time
@@ -98,6 +99,11 @@ class LocalEngine:
         self.log = log
         self.tracer = Tracer(cfg.trace_path, 0, self.device,
                              f"{cfg.log_dir}/logs-perf.csv" if cfg.perf_log else None)
+        if cfg.solver.use_graph is None and cfg.num_workers > 2:
+            # many in-process workers share this process's launch thread: one graph
+            # replay per solve beats 8 eager launches there (bench.py --workers 8:
+            # 17.7k vs 13.4k updates/s); a lone worker is GPU-bound and runs eagerly
+            cfg.solver = dataclasses.replace(cfg.solver, use_graph=True)
         w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0)
         self.t0 = time.time()

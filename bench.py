@@ -71,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
+    ap.add_argument("--async-scheduler", default="auto", choices=["auto", "events", "threads"],
+                    help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
@@ -107,6 +109,7 @@ def build_cfg(a, n_workers):
         solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
                              zero_const=not wide),
         bsp_schedule=a.schedule,
+        async_scheduler=a.async_scheduler,
     )
 
 

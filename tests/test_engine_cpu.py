@@ -147,3 +147,41 @@ def test_checkpoint_wide_model(tmp_path):
     eng.run()
     st = load_server(str(tmp_path))
     assert st["model"] == "wide" and torch.equal(st["w"], eng.server.w) and "w_reference_layout" not in st
+
+
+@pytest.mark.parametrize("c", [-1, 2])
+def test_event_scheduler_async(c):
+    """The one-thread event-polling scheduler (the GPU default for SSP/ASP) on CPU:
+    every worker steps, the staleness bound holds and the run matches the
+    tracker's accounting."""
+    train, test = synth_finefood(3000, num_features=128, seed=0), synth_finefood(300, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=3, consistency_model=c, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=64, epochs=100, max_iters=10, async_scheduler="events")
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    assert eng._event_scheduler()
+    out = eng.run()
+    assert out["updates"] >= 30 and min(w.iters for w in eng.workers) >= 10
+    assert out["max_vc_gap"] <= (c + 1 if c > 0 else 1)  # completion order is FIFO on the CPU
+    assert {r[1] for r in eng.log.book.worker} == {0, 1, 2}
+    assert out["server_rows"] >= 10
+
+
+def test_event_scheduler_crash_is_dropped():
+    train, test = synth_finefood(3000, num_features=128, seed=0), synth_finefood(300, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=3, consistency_model=-1, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=64, epochs=100, max_iters=8, async_scheduler="events",
+                   inject_worker_crash={0: 2})
+    eng = LocalEngine(cfg, "cpu", train=train, test=test)
+    out = eng.run()
+    assert out["failed_workers"] == [0] and eng.workers[0].iters == 2
+    assert min(eng.workers[1].iters, eng.workers[2].iters) >= 8
+    assert out["server_rows"] >= 8  # worker 0's rows, then the lowest survivor's
+
+
+def test_async_scheduler_choice():
+    cfg = PSConfig(num_workers=2, consistency_model=-1, async_scheduler="bogus")
+    train, test = synth_finefood(500, num_features=128, seed=0), synth_finefood(100, num_features=128, seed=1)
+    with pytest.raises(ValueError):
+        LocalEngine(cfg, "cpu", train=train, test=test)._event_scheduler()
+    cfg.async_scheduler = "auto"
+    assert not LocalEngine(cfg, "cpu", train=train, test=test)._event_scheduler()  # CPU: threads

@@ -126,3 +126,20 @@ def test_concurrent_worker_lanes_match_sequential(cuda):
         books.append(eng.log.book)
     assert torch.allclose(ws[0], ws[1], atol=1e-4 * max(1.0, ws[1].abs().max().item()))
     assert len(books[0].worker) == len(books[1].worker) == 40 and len(books[0].server) == 10
+
+
+@pytest.mark.parametrize("c", [-1, 3])
+def test_async_event_scheduler_four_workers(cuda, c):
+    """SSP/ASP default on a GPU: one host thread polling per-worker HIP events."""
+    train, test = synth_finefood(16000, seed=0), synth_finefood(1000, seed=1)
+    cfg = _cfg(num_workers=4, consistency_model=c, max_iters=40)
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    assert eng._event_scheduler()
+    out = eng.run()
+    # solves still in flight when the run stops are not applied
+    assert min(w.iters for w in eng.workers) >= 40 and 160 <= out["updates"] <= sum(w.iters for w in eng.workers)
+    if c > 0:
+        assert out["max_vc_gap"] <= c + 1
+    assert {r[1] for r in eng.log.book.worker} == {0, 1, 2, 3}
+    accs = [r[3] for r in eng.log.book.server]
+    assert len(accs) >= 40 and accs[-1] > 0.25

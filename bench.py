@@ -125,6 +125,15 @@ def make_data(a, device):
     return synth_sparse(a.train_rows, seed=0, **kw), synth_sparse(a.test_rows, seed=1, **kw)
 
 
+def _backend_label() -> str:
+    """What carried the multi-rank traffic: RCCL, or gloo (CPU runs, PSX_GPU_OVERSUBSCRIBE)."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return "RCCL"
+    return "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
+
+
 def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
     wide = a.model != "dense"
     async_mode = a.consistency != 0
@@ -141,12 +150,13 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
                 f"~48 nnz/row, random-init weights)")
         vs = None  # the reference never ran this configuration
     mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
+    backend = _backend_label()
     if world == 1:
         par = f"ps-{mode} w{n_workers} (server colocated{', workers share the GPU' if n_workers > 1 else ''})"
     elif async_mode:
-        par = f"ps-{mode} 1 server + {n_workers} workers (RCCL p2p{', sparse push' if wide else ''})"
+        par = f"ps-{mode} 1 server + {n_workers} workers ({backend} p2p{', sparse push' if wide else ''})"
     else:
-        par = f"ps-{mode} dp{world} ({cfg.bsp_schedule}, RCCL)"
+        par = f"ps-{mode} dp{world} ({cfg.bsp_schedule}, {backend})"
     res = {
         "metric": "server_updates_per_s (PS push/pull rounds, logistic regression; test accuracy reported alongside)",
         "value": round(ups, 2),

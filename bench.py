@@ -73,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--async-scheduler", default="auto", choices=["auto", "events", "threads"],
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
+    ap.add_argument("--rccl-trace", action="store_true",
+                    help="RCCL collective/p2p trace into ./rccl-trace.<host>.<pid>.log (multi-GPU runs)")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
@@ -232,9 +234,11 @@ def bench_distributed(a):
     import torch.distributed as dist
 
     from psx.ops.lr import is_gpu
-    from psx.parallel.dist import DistEngine, init_from_env
+    from psx.parallel.dist import DistEngine, init_from_env, rccl_trace_env
     from psx.utils.logsink import LogSink, summarize
 
+    if a.rccl_trace:
+        os.environ.update(rccl_trace_env("."))
     rank, world, device = init_from_env(cpu=a.cpu)
     async_mode = a.consistency != 0
     cfg = build_cfg(a, world - 1 if async_mode else world)

@@ -185,3 +185,15 @@ def test_async_scheduler_choice():
         LocalEngine(cfg, "cpu", train=train, test=test)._event_scheduler()
     cfg.async_scheduler = "auto"
     assert not LocalEngine(cfg, "cpu", train=train, test=test)._event_scheduler()  # CPU: threads
+
+
+def test_cli_async_scheduler_and_rccl_trace(tmp_path):
+    from psx.apps.cli import parse_or_exit, server_config, server_parser
+    from psx.parallel.dist import rccl_trace_env
+
+    a = parse_or_exit(server_parser(), ["--inprocess", "--async_scheduler", "events", "--rccl_trace",
+                                        "--log_dir", str(tmp_path), "-c", "-1"])
+    assert server_config(a).async_scheduler == "events" and a.rccl_trace
+    env = rccl_trace_env(str(tmp_path))
+    assert env["NCCL_DEBUG"] == "INFO" and "COLL" in env["NCCL_DEBUG_SUBSYS"]
+    assert env["NCCL_DEBUG_FILE"].startswith(str(tmp_path)) and "%p" in env["NCCL_DEBUG_FILE"]

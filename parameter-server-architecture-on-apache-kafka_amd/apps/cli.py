@@ -42,6 +42,8 @@ def _common(ap: argparse.ArgumentParser):
     ap.add_argument("--perf_log", action="store_true",
                     help="write logs-perf.csv (per-round device phase times, updates/s) next to the CSV logs")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--rccl_trace", action="store_true",
+                    help="RCCL collective/p2p trace into <log_dir>/rccl-trace.<host>.<pid>.log (multi-rank runs)")
 
 
 def server_parser() -> argparse.ArgumentParser:
@@ -88,6 +90,9 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--rows_per_iter", type=int, default=0)
     g.add_argument("--inprocess", action="store_true",
                    help="run server + all workers in this process on one device (single-GPU / CPU mode)")
+    g.add_argument("--async_scheduler", default="auto", choices=["auto", "events", "threads"],
+                   help="--inprocess SSP/ASP: one host thread polling the workers' HIP events, or a thread "
+                        "per worker (auto: events on a GPU unless a delay is injected)")
     g.add_argument("--bsp_schedule", default="reduce_bcast", choices=["allreduce", "reduce_bcast", "sharded"])
     g.add_argument("--checkpoint_dir", default=None)
     g.add_argument("--checkpoint_every", type=int, default=0)
@@ -150,7 +155,7 @@ def server_config(a) -> PSConfig:
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
-        perf_log=a.perf_log,
+        perf_log=a.perf_log, async_scheduler=a.async_scheduler,
         model=a.model, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)

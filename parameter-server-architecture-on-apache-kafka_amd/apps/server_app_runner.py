@@ -51,8 +51,10 @@ def main(argv=None) -> int:
     else:
         import torch.distributed as dist
 
-        from ..parallel.dist import DistEngine, init_from_env
+        from ..parallel.dist import DistEngine, init_from_env, rccl_trace_env
 
+        if a.rccl_trace:
+            os.environ.update(rccl_trace_env(a.log_dir))
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = str(torch.device(device).index or 0) if device.startswith("cuda") else "0"
         os.environ["WORLD_SIZE"] = str(cfg.num_workers + 1)

@@ -67,6 +67,10 @@ def main(argv=None) -> int:
         env["MASTER_PORT"] = str(a.master_port)
     elif "MASTER_PORT" in os.environ:
         env["MASTER_PORT"] = os.environ["MASTER_PORT"]
+    if a.rccl_trace:
+        from ..parallel.dist import rccl_trace_env
+
+        env.update(rccl_trace_env(a.log_dir))
     a_dict = vars(a).copy()
     if a_dict["device"] is None:
         a_dict["device"] = "auto"

@@ -58,6 +58,19 @@ from ..utils.trace import Tracer
 KIND_DELTA, KIND_FINAL, KIND_ERROR = 0, 1, 2
 
 
+def rccl_trace_env(log_dir: str = ".") -> dict:
+    """Environment that turns on RCCL's own collective / p2p trace (SURVEY.md §5.1:
+    the analogue of the reference's Confluent monitoring interceptors,
+    BaseKafkaApp.java:73-78).  RCCL reads it at communicator creation, so it must
+    be in the environment before :func:`init_from_env`; one file per host and
+    process under ``log_dir``."""
+    return {
+        "NCCL_DEBUG": "INFO",
+        "NCCL_DEBUG_SUBSYS": "INIT,COLL,P2P",
+        "NCCL_DEBUG_FILE": os.path.join(os.path.abspath(log_dir), "rccl-trace.%h.%p.log"),
+    }
+
+
 def init_from_env(cpu: bool = False):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK)."""
     rank = int(os.environ.get("RANK", "0"))

@@ -69,7 +69,11 @@ class PSConfig:
     on_worker_failure: str = "auto"  # drop | fail | auto (drop under eventual consistency)
     trace_path: str | None = None
     pair_eval: bool = True
-    concurrent_workers: bool = True  # in-process BSP on a GPU: one HIP stream per worker  # BSP: worker-0 row + previous server row from one eval pass (EvalPair)
+    concurrent_workers: bool = True  # in-process BSP on a GPU: one HIP stream per worker
+    # in-process SSP/ASP: "events" (one host thread launches the released workers'
+    # solves on their HIP streams and polls completion events), "threads" (a thread
+    # per worker; needed for injected delays) or "auto" (events on a GPU)
+    async_scheduler: str = "auto"
     perf_log: bool = False  # write {log_dir}/logs-perf.csv (per-round device phase times)
 
     @property

@@ -8,10 +8,12 @@ and logging code as the distributed engine.
 
 * BSP (c = 0): lock-step rounds on one stream -- every worker solves, the server
   applies the summed deltas (lr = 1/N), evaluates, and broadcasts.
-* SSP (c = D > 0) / ASP (c = -1): one host thread + one HIP stream per worker,
-  the server on the calling thread consumes (worker, vc) tokens in arrival
-  order -- the analogue of the single-partition GRADIENTS_TOPIC
-  (ServerApp.java:36-38) -- and releases workers per the vector-clock tracker.
+* SSP (c = D > 0) / ASP (c = -1): one HIP stream per worker; the server applies
+  deltas in completion order -- the analogue of the single-partition
+  GRADIENTS_TOPIC (ServerApp.java:36-38) -- and releases workers per the
+  vector-clock tracker.  On a GPU one host thread launches every worker's solve
+  and polls completion events (_run_async_events); with injected stragglers, or
+  on the CPU, each worker runs on its own host thread (_run_async).
 """
 from __future__ import annotations
 
@@ -256,11 +258,16 @@ class LocalEngine:
         pending: dict[int, tuple[int, object]] = {}  # released, not yet launched: k -> (vc, ev)
         inflight: list[tuple[int, int, torch.Tensor, object]] = []  # (k, vc, delta, ev), launch order
 
+        # a worker has at most one release pending and one solve in flight, so one
+        # event of each kind per worker is reused (no event creation per update)
+        rel_ev = {w.k: torch.cuda.Event() for w in W} if gpu else {}
+        done_ev = {w.k: torch.cuda.Event() for w in W} if gpu else {}
+
         def release(j: int, u: int):
             W[j].w.copy_(srv.w)
             ev = None
             if gpu:
-                ev = torch.cuda.Event()
+                ev = rel_ev[j]
                 ev.record(main)
             pending[j] = (u, ev)
 
@@ -284,7 +291,7 @@ class LocalEngine:
                     return True
                 done = None
                 if gpu:
-                    done = torch.cuda.Event()
+                    done = done_ev[k]
                     done.record(streams[k])
             inflight.append((k, u, delta, done))
             return True

@@ -143,3 +143,16 @@ def test_async_event_scheduler_four_workers(cuda, c):
     assert {r[1] for r in eng.log.book.worker} == {0, 1, 2, 3}
     accs = [r[3] for r in eng.log.book.server]
     assert len(accs) >= 40 and accs[-1] > 0.25
+
+
+def test_async_event_scheduler_drops_crashed_worker(cuda):
+    """Event scheduler on a GPU: an injected crash retires the worker (ASP) and the
+    survivors keep stepping; server rows move to the lowest surviving worker."""
+    train, test = synth_finefood(12000, seed=0), synth_finefood(1000, seed=1)
+    cfg = _cfg(num_workers=3, consistency_model=-1, max_iters=20, inject_worker_crash={0: 3})
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    assert eng._event_scheduler()
+    out = eng.run()
+    assert out["failed_workers"] == [0] and eng.workers[0].iters == 3
+    assert min(eng.workers[1].iters, eng.workers[2].iters) >= 20
+    assert len(eng.log.book.server) >= 20

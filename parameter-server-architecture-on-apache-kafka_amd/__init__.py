@@ -12,4 +12,12 @@ The importable name is ``psx``; the on-disk package directory is
 """
 __version__ = "0.1.0"
 
+import os as _os
+
+# Kernel arguments in device memory: a local solve is a chain of ~8 dependent
+# latency-bound launches, and host-memory kernargs cost ~20 us per solve
+# (tools/bench_solver.py: 84.3 us with 0, 63.8 us with 1; profiles/r01_v8).
+# Read by the HIP runtime at its first call, so set before any GPU work.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 from . import _native  # noqa: F401  (loads the native host runtime)

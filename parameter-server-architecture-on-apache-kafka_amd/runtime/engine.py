@@ -274,26 +274,33 @@ class LocalEngine:
         def launch(k: int) -> bool:
             w = W[k]
             u, ev = pending[k]
-            with torch.cuda.stream(streams[k]) if gpu else _Null():
-                if ev is not None:
-                    streams[k].wait_event(ev)
-                w.vc = u
+            w.vc = u
+            failure = None
+            if gpu:  # (set_stream: the stream context manager costs ~10 us of host time)
+                torch.cuda.set_stream(streams[k])
+            try:
                 w.ingest()
                 if not w.ready():
                     return False
                 del pending[k]
+                if ev is not None:  # the pulled weights (copied on the main stream)
+                    streams[k].wait_event(ev)
                 try:
                     delta = w.compute(self.log)
                 except WorkerFailure as e:
-                    for j, v in self._worker_failed(e, k):
-                        release(j, v)
-                    alive.discard(k)
-                    return True
-                done = None
+                    failure = e
+                else:
+                    if gpu:
+                        done_ev[k].record(streams[k])
+            finally:
                 if gpu:
-                    done = done_ev[k]
-                    done.record(streams[k])
-            inflight.append((k, u, delta, done))
+                    torch.cuda.set_stream(main)
+            if failure is not None:  # releases copy on the main stream, like every pull
+                for j, v in self._worker_failed(failure, k):
+                    release(j, v)
+                alive.discard(k)
+                return True
+            inflight.append((k, u, delta, done_ev[k] if gpu else None))
             return True
 
         for j in sorted(alive):  # bootstrap: the current version to everybody

@@ -21,8 +21,19 @@ def is_gpu(device) -> bool:
     return torch.device(device).type == "cuda"
 
 
+_DEV_INDEX: dict = {}
+
+
 def stream_handle(device) -> int:
-    return torch.cuda.current_stream(torch.device(device)).cuda_stream
+    """hipStream_t of the current stream of `device` (every native launch asks).
+    torch.cuda.current_stream() builds a Stream object and re-resolves the device
+    on each call; the raw accessor with a cached index is a single C call."""
+    idx = _DEV_INDEX.get(device)
+    if idx is None:
+        d = torch.device(device)
+        idx = d.index if d.index is not None else torch.cuda.current_device()
+        _DEV_INDEX[device] = idx
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 @dataclass

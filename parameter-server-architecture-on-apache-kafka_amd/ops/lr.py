@@ -105,6 +105,8 @@ class LocalSolveOp:
         key = (ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr())
         if self._bound == key:
             return
+        if ring.X.dtype != torch.bfloat16 or ring.X.shape != (self.cap, self.spec.Fp) or ring.y.dtype != torch.int32:
+            raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
         h = _native.hip()
         s, o = self.spec, self.opts
         cfg = h.SolverCfg()
@@ -126,9 +128,7 @@ class LocalSolveOp:
         if ring.cap != self.cap:
             raise ValueError(f"ring capacity {ring.cap} != solver capacity {self.cap}")
         X, y = ring.X, ring.y
-        if is_gpu(self.device):
-            if X.dtype != torch.bfloat16 or X.shape != (self.cap, self.spec.Fp) or y.dtype != torch.int32:
-                raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
+        if self.frag is not None:  # GPU
             self._bind(ring, w_old)
             pend = ring.take_pending(B, start) if hasattr(ring, "take_pending") else None
             if pend is None:

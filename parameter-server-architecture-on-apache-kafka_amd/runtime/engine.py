@@ -494,11 +494,11 @@ class _WorkerLanes:
         self.streams = {w.k: torch.cuda.Stream(self.device) for w in workers}
         self.done = {w.k: torch.cuda.Event() for w in workers}
         self.start = torch.cuda.Event()
-        main = torch.cuda.current_stream(self.device)
-        self._on = {k: _OnStream(st, main) for k, st in self.streams.items()}
+        self.main = torch.cuda.current_stream(self.device)  # the engine loop's stream
+        self._on = {k: _OnStream(st, self.main) for k, st in self.streams.items()}
 
     def begin(self):
-        self.start.record(torch.cuda.current_stream(self.device))
+        self.start.record(self.main)
         for st in self.streams.values():
             st.wait_event(self.start)
 
@@ -506,7 +506,7 @@ class _WorkerLanes:
         return self._on[w.k]
 
     def join(self, workers):
-        main = torch.cuda.current_stream(self.device)
+        main = self.main
         for w in workers:
             ev = self.done[w.k]
             ev.record(self.streams[w.k])

@@ -156,3 +156,22 @@ def test_async_event_scheduler_drops_crashed_worker(cuda):
     assert out["failed_workers"] == [0] and eng.workers[0].iters == 3
     assert min(eng.workers[1].iters, eng.workers[2].iters) >= 20
     assert len(eng.log.book.server) >= 20
+
+
+def test_stream_handle_follows_current_stream(cuda):
+    """Every native launch takes its stream from stream_handle: it must follow
+    set_stream / stream contexts exactly like torch.cuda.current_stream."""
+    from psx.ops.lr import stream_handle
+
+    dev = torch.device(cuda)
+    main = torch.cuda.current_stream(dev)
+    assert stream_handle(dev) == main.cuda_stream == stream_handle(cuda)
+    side = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(side)
+    try:
+        assert stream_handle(dev) == side.cuda_stream
+    finally:
+        torch.cuda.set_stream(main)
+    with torch.cuda.stream(side):
+        assert stream_handle(cuda) == side.cuda_stream
+    assert stream_handle(dev) == main.cuda_stream

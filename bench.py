@@ -29,7 +29,13 @@ the best 4-worker run); null for the configs the reference never
 ran.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M]
-       (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL.)
+       N > 1: one rank per GPU over RCCL.  Under torch.distributed.run the
+       ranks come from its environment; a plain ``python bench.py --gpus N``
+       spawns the N ranks itself (before anything touches the GPU) and every
+       rank checks that the world it joined has exactly N ranks.
+       --dedicated-server: BASELINE config 2 (1 server rank + N-1 worker ranks,
+       RCCL reduce + broadcast); --consistency D>0 / -1: configs 3/4 (dedicated
+       server rank, RCCL point-to-point).
 """
 from __future__ import annotations
 
@@ -75,6 +81,8 @@ def parse(argv=None):
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--rccl-trace", action="store_true",
                     help="RCCL collective/p2p trace into ./rccl-trace.<host>.<pid>.log (multi-GPU runs)")
+    ap.add_argument("--dedicated-server", action="store_true",
+                    help="multi-GPU BSP with a dedicated server rank (BASELINE config 2: reduce + broadcast)")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
@@ -86,6 +94,8 @@ def parse(argv=None):
         a.steps = 300 if wide else 2000
     if a.warmup is None:
         a.warmup = 30 if wide else 200
+    if a.dedicated_server and a.schedule == "allreduce":
+        a.schedule = "reduce_bcast"
     return a
 
 
@@ -111,6 +121,7 @@ def build_cfg(a, n_workers):
         solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
                              zero_const=not wide),
         bsp_schedule=a.schedule,
+        server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,
     )
 
@@ -136,14 +147,14 @@ def _backend_label() -> str:
     return "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
 
 
-def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
-    wide = a.model != "dense"
+def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
     async_mode = a.consistency != 0
     n_workers = cfg.num_workers
     if a.model == "dense":
-        model = "multinomial-logreg F=1024 K=6 (P=6150), local solver L-BFGS x2 + strong-Wolfe"
-        data = "synthetic (fine-food-reviews-shaped, 90k train / 4877 test, random-init weights)"
-        ref = REF_UPDATES_PER_S_1W if world == 1 else REF_UPDATES_PER_S_4W
+        model = f"multinomial-logreg F={a.features} K=6 (P={6 * a.features + 6}), local solver L-BFGS x2 + strong-Wolfe"
+        data = (f"synthetic (fine-food-reviews-shaped, {a.train_rows} train / {a.test_rows} test rows, "
+                f"random-init weights)")
+        ref = REF_UPDATES_PER_S_1W if n_workers == 1 else REF_UPDATES_PER_S_4W
         vs = round(ups / ref, 1)
     else:
         kind = "binary sigmoid" if a.model == "sharded100m" else "multinomial K=6"
@@ -156,7 +167,9 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
     if world == 1:
         par = f"ps-{mode} w{n_workers} (server colocated{', workers share the GPU' if n_workers > 1 else ''})"
     elif async_mode:
-        par = f"ps-{mode} 1 server + {n_workers} workers ({backend} p2p{', sparse push' if wide else ''})"
+        par = f"ps-{mode} 1 server + {n_workers} workers ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
+    elif not cfg.server_colocated:
+        par = f"ps-{mode} 1 server + {n_workers} workers ({cfg.bsp_schedule}, {backend})"
     else:
         par = f"ps-{mode} dp{world} ({cfg.bsp_schedule}, {backend})"
     res = {
@@ -174,10 +187,16 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
         "data": data,
         "config": {
             "model": model,
+            # a PS step has no batch / sequence: the per-step work is every worker's
+            # sliding window (rows x features); seq_len does not apply
             "global_batch": a.buffer * n_workers,
-            "seq_len": a.features,
+            "seq_len": None,
+            "window_rows_total": a.buffer * n_workers,
+            "window_rows_per_worker": a.buffer,
+            "features": a.features,
             "parallelism": par,
             "consistency": a.consistency,
+            "workers": n_workers,
             "rows_per_step_per_worker": a.rows_per_step,
             "bench_model": a.model,
         },
@@ -185,6 +204,8 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
         "test_f1": summ.get("final_server_f1"),
         "best_test_f1": summ.get("best_server_f1"),
     }
+    if rccl_ranks is not None:
+        res["rccl_ranks"] = rccl_ranks
     if tuples_seen is not None:
         res["tuples_seen"] = tuples_seen
     return res
@@ -192,14 +213,21 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None):
 
 def main(argv=None):
     a = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if a.gpus > 1 and world_env is None:
+        # plain `python bench.py --gpus N`: start the N ranks here.  This process
+        # never touches the GPU (no torch.cuda call before or after the spawn).
+        return _spawn_ranks(a.gpus, sys.argv[1:] if argv is None else list(argv))
     if os.environ.get("PSX_HANG_DUMP_S"):  # debugging aid: dump every thread's stack, then exit
         import faulthandler
 
         faulthandler.dump_traceback_later(float(os.environ["PSX_HANG_DUMP_S"]), exit=True)
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.gpus > 1 or world > 1:
+    world = int(world_env or "1")
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
+    if world > 1:
         return bench_distributed(a)
 
     device = "cpu" if a.cpu else "cuda:0"
@@ -223,13 +251,58 @@ def main(argv=None):
     dt = time.perf_counter() - t0
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
-    res["accuracy_vs_wallclock"] = _curve(eng.log.book.server, t0)
+    res.update(_accuracy_fields(eng.log.book.server))
     print(json.dumps(res))
     return res
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n: int, argv) -> int:
+    """One child process per GPU with torchrun's environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_*); rank 0 prints the JSON line.  A failed rank takes the
+    others down (their collectives would never complete)."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, TORCHELASTIC_RUN_ID=f"psxbench{port}")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                pending.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:
+                        if q.poll() is None:
+                            q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    if rc != 0:
+        sys.exit(rc if rc > 0 else 1)
+    return 0
+
+
 def bench_distributed(a):
-    """N > 1 GPUs: one rank per GPU (torchrun), RCCL over xGMI."""
+    """N > 1 GPUs: one rank per GPU (torchrun or _spawn_ranks), RCCL over xGMI."""
     import torch
     import torch.distributed as dist
 
@@ -240,8 +313,11 @@ def bench_distributed(a):
     if a.rccl_trace:
         os.environ.update(rccl_trace_env("."))
     rank, world, device = init_from_env(cpu=a.cpu)
+    if dist.get_world_size() != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
     async_mode = a.consistency != 0
-    cfg = build_cfg(a, world - 1 if async_mode else world)
+    dedicated = async_mode or a.dedicated_server
+    cfg = build_cfg(a, world - 1 if dedicated else world)
     train, test = make_data(a, device)
     cfg.max_iters = a.warmup
     eng = DistEngine(cfg, rank, world, device, train=train, test=test)
@@ -263,13 +339,21 @@ def bench_distributed(a):
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    comm = getattr(eng, "comm", None)
+    # ranks of the RCCL communicator that carried the traffic: the native one (BSP
+    # collectives) or torch.distributed's (nccl backend = RCCL); None on gloo
+    rccl = comm.c.size if comm is not None else (dist.get_world_size() if dist.get_backend() == "nccl" else None)
     res = None
     if rank == 0:
         eng.log.close()
-        summ = summarize(eng.log.book)
+        book = eng.log.book
+        summ = summarize(book)
         ups = a.steps * cfg.num_workers / dt
-        res = describe(a, world, cfg, ups, dt, summ)
+        res = describe(a, world, cfg, ups, dt, summ, rccl_ranks=rccl)
         res["max_vc_gap"] = out.get("max_vc_gap")
+        res.update(_accuracy_fields(book.server))
+        if rccl is not None and rccl != world:
+            raise SystemExit(f"bench.py: RCCL communicator has {rccl} ranks, world is {world}")
         print(json.dumps(res), flush=True)
     eng.close()
     dist.barrier()
@@ -277,7 +361,20 @@ def bench_distributed(a):
     return res
 
 
-def _curve(server_rows, t0_perf, points=10):
+def _accuracy_fields(server_rows, threshold=0.40):
+    """Accuracy half of the metric from the timed region's server rows (global
+    model on the test set, ServerProcessor.java:154-165): the curve, the best
+    weighted F1 and the time to reach F1 >= threshold (None: never)."""
+    out = {"accuracy_vs_wallclock": _curve(server_rows)}
+    if server_rows:
+        ts0 = server_rows[0][0]
+        hit = next((r for r in server_rows if r[2] >= threshold), None)
+        out["time_to_f1_0.40_s"] = round((hit[0] - ts0) / 1000.0, 4) if hit is not None else None
+        out["server_rows"] = len(server_rows)
+    return out
+
+
+def _curve(server_rows, points=10):
     """[(seconds since the timed region started, test accuracy, weighted F1)] samples."""
     if not server_rows:
         return []

@@ -1,0 +1,61 @@
+"""bench.py contract: `--gpus N` runs N ranks (spawned by bench.py itself when no
+launcher set WORLD_SIZE), rank 0 prints ONE JSON line with n_gpus == N, and a
+launcher world that disagrees with --gpus is an error (CPU / gloo here; the
+driver runs the same code path over RCCL on an 8-GPU node)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--cpu", "--steps", "4", "--warmup", "1", "--train-rows", "3000", "--test-rows", "400"]
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    e["OMP_NUM_THREADS"] = "2"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, env=e, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p, lines
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_spawns_n_ranks(n):
+    p, lines = _run(["--gpus", str(n)] + SMALL)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n
+    assert d["steps"] == 4 and d["warmup"] == 1
+    assert d["config"]["workers"] == n  # allreduce schedule: every rank is a worker
+    assert d["config"]["parallelism"].startswith(f"ps-bsp dp{n}")
+    assert d["config"]["features"] == 1024 and d["config"]["window_rows_total"] == 1024 * n
+    assert "3000 train / 400 test" in d["data"]
+    assert "time_to_f1_0.40_s" in d and d["best_test_f1"] is not None
+
+
+def test_bench_dedicated_server_config2():
+    p, lines = _run(["--gpus", "2", "--dedicated-server"] + SMALL)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["workers"] == 1
+    assert "1 server + 1 workers" in d["config"]["parallelism"]
+
+
+def test_bench_world_mismatch_is_an_error():
+    p, _ = _run(["--gpus", "2"] + SMALL, env={"WORLD_SIZE": "1", "RANK": "0", "MASTER_PORT": "29731"})
+    assert p.returncode != 0
+    assert "--gpus 2" in (p.stderr + p.stdout)
+
+
+def test_bench_single_gpu_default_unchanged():
+    p, lines = _run(SMALL)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w1")

@@ -195,6 +195,13 @@ PYBIND11_MODULE(_psx_hip, m) {
   m.def("pinned_free", [](uintptr_t p) {
     if (p) (void)hipHostFree(reinterpret_cast<void*>(p));
   });
+  // stream-ordered device -> pinned host copy (the host polls the bytes later,
+  // no synchronisation): the BSP stop vote's lagged read
+  m.def("memcpy_d2h_async", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t stream) {
+    hip_check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), bytes,
+                             hipMemcpyDeviceToHost, S(stream)),
+              "hipMemcpyAsync(d2h)");
+  });
   m.def("logits", [](int FP, int K, uintptr_t X, int T, uintptr_t whi, uintptr_t wlo, uintptr_t b, uintptr_t out,
                      uintptr_t stream) {
     prepare_kernels();

@@ -35,7 +35,12 @@ SlidingWindow::SlidingWindow(int64_t min_size, int64_t max_size, double bc, int 
 
 int64_t SlidingWindow::target_size() const {
   double mean = rate_.mean_interarrival_ms();
-  // events per minute; a zero mean (burst) means "as fast as possible" -> max
+  // events per minute.  Deliberate deviation: a zero mean inter-arrival time (a
+  // burst; every row of a per-iteration poll shares one timestamp) means "as fast
+  // as possible" -> the max window.  The reference computes (int) Math.round(
+  // bc * 60000 / 0.0) = (int) Long.MAX_VALUE = -1 there and so clamps to the MIN
+  // window (WorkerSamplingProcessor.java:115-122) -- an overflow artefact, not a
+  // policy.  Pinned by tests/test_sampling.py::test_zero_mean_interarrival_policy.
   double per_min = mean > 0.0 ? 60000.0 / mean : static_cast<double>(max_) / bc_ + 1.0;
   double t = std::floor(bc_ * per_min + 0.5);  // java.lang.Math.round
   if (!(t == t)) t = static_cast<double>(max_);

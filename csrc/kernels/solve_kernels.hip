@@ -803,6 +803,14 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
       dv.stats[1] = ctrl->nacc;
       dv.stats[2] = ctrl->ls_fail;
       dv.stats[3] = ctrl->dir_reset;
+      // a cross-workgroup wait that timed out (a workgroup was not co-resident):
+      // this solve's result is garbage -- sticky flag for the host, NaN loss in the logs
+      const unsigned long long err = xload(dv.xch + kXchErr);
+      if (err) {
+        dv.stats[4] |= (int)err;
+        xstore(dv.xch + kXchErr, 0ull);
+        *dv.loss = __builtin_nanf("");
+      }
     }
   }
 }

@@ -665,6 +665,14 @@ __global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d
     d.stats[1] = ctrl->nacc;
     d.stats[2] = ctrl->ls_fail;
     d.stats[3] = ctrl->dir_reset;
+    // a grid barrier that timed out (a workgroup was not co-resident): sticky flag
+    // for the host, NaN loss in the logs
+    const unsigned err = __hip_atomic_load(d.cnt + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (err) {
+      d.stats[4] |= (int)err;
+      __hip_atomic_store(d.cnt + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *d.loss = __builtin_nanf("");
+    }
     d.cnt[2] = U;
     // read by the host after a stream synchronisation: no release (an L2 writeback) needed
     if (d.host_u) __hip_atomic_store(d.host_u, U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -101,6 +101,8 @@ def server_parser() -> argparse.ArgumentParser:
                    help="fault injection: worker K sleeps MS ms per iteration (straggler)")
     g.add_argument("--inject_worker_crash", action="append", default=[], metavar="K:ITER",
                    help="fault injection: worker K fails at its ITER-th iteration")
+    g.add_argument("--inject_worker_stop", action="append", default=[], metavar="K:ITER",
+                   help="worker K leaves the run cleanly (final push) after ITER iterations")
     g.add_argument("--worker_timeout", type=float, default=600.0,
                    help="watchdog: a worker busy and silent this many seconds has failed")
     g.add_argument("--on_worker_failure", default="auto", choices=["auto", "drop", "fail"],
@@ -158,6 +160,7 @@ def server_config(a) -> PSConfig:
         perf_log=a.perf_log, async_scheduler=a.async_scheduler,
         model=a.model, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
+        inject_worker_stop={k: int(v) for k, v in parse_worker_map(a.inject_worker_stop).items()},
         worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)
 
 

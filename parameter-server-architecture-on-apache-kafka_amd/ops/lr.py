@@ -96,7 +96,7 @@ class LocalSolveOp:
         self.delta = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.w_new = torch.zeros(P, dtype=torch.float32, device=self.device)
         self.loss = torch.zeros(1, dtype=torch.float32, device=self.device)
-        self.stats = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self.stats = torch.zeros(8, dtype=torch.int32, device=self.device)
         self.frag = Fragments(spec, self.device) if is_gpu(self.device) else None
         self._native = None
         self._bound = None
@@ -120,6 +120,12 @@ class LocalSolveOp:
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
             self.loss.data_ptr(), self.stats.data_ptr(), o.max_eval_wg, bool(o.use_graph))
         self._bound = key
+
+    def barrier_errors(self) -> int:
+        """Sticky flag of the device solver: a cross-workgroup wait timed out (a
+        workgroup was not co-resident) and a solve's result was garbage.  Reads
+        the device (a stream sync): the engines check it at the end of a run."""
+        return int(self.stats[4].item()) if self.frag is not None else 0
 
     def run(self, ring, B: int, start: int, w_old: torch.Tensor):
         """Enqueue a solve over the window [start, start+B) (mod cap) of ``ring`` (a DeviceRing)."""
@@ -148,7 +154,7 @@ class LocalSolveOp:
         self.w_new.copy_(s.pack(res.coef, res.intercept))
         self.delta.copy_(self.w_new - w_old)
         self.loss.fill_(res.loss)
-        self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0], dtype=torch.int32))
+        self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0, 0, 0, 0, 0], dtype=torch.int32))
 
 
 class EvalSet:
@@ -243,7 +249,7 @@ class EvalScratch:
     def __init__(self, device):
         # [2 models][16][16] cells, one per 128-B line (kAccStride in csrc/kernels/lr_kernels.h)
         self.acc = torch.zeros(2 * 256 * ACC_STRIDE, dtype=torch.int32, device=device)
-        self.ticket = torch.zeros(4, dtype=torch.int32, device=device)
+        self.ticket = torch.zeros(8, dtype=torch.int32, device=device)
 
 
 def _write_slot_cpu(addr: int, conf: torch.Tensor, loss: float, seq: int):

@@ -140,7 +140,7 @@ class WideSolveOp:
         self.wloc = torch.zeros(self.plmax, dtype=torch.float32, device=dev)
         self.uniq = torch.zeros(self.umax, dtype=torch.int32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.stats = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(8, dtype=torch.int32, device=dev)
         self.dense_delta = bool(dense_delta)
         self.delta = torch.zeros(spec.P, dtype=torch.float32, device=dev) if dense_delta else None
         self._native = None
@@ -186,6 +186,10 @@ class WideSolveOp:
             return
         self._run_cpu(ring, B, start, w_old)
 
+    def barrier_errors(self) -> int:
+        """Sticky flag: a grid barrier of the device solver timed out (see LocalSolveOp)."""
+        return int(self.stats[4].item()) if is_gpu(self.device) else 0
+
     def sparse_delta(self) -> SparseDelta:
         if is_gpu(self.device):
             return SparseDelta(self.spec, self.uniq, self.dloc, None, self._native.ucount_ptr)
@@ -228,7 +232,7 @@ class WideSolveOp:
         self._count_cpu = U
         self._map_cpu = pos
         self.loss.fill_(res.loss)
-        self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0], dtype=torch.int32))
+        self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0, 0, 0, 0, 0], dtype=torch.int32))
         if self.delta is not None:
             self.delta.copy_(self.sparse_delta().to_dense())
 

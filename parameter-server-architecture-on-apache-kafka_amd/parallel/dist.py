@@ -105,6 +105,67 @@ def ctrl_queue_name() -> str:
     return f"/psx_ctrl_{os.environ.get('MASTER_PORT', '29500')}_{os.environ.get('TORCHELASTIC_RUN_ID', 'x')}"[:250]
 
 
+class StopVote:
+    """Run-stop agreement of the BSP ranks without a host synchronisation per round.
+
+    A rank that wants to stop (its stream is exhausted, or its wall-clock budget
+    is spent) writes 1 into a device word that the round's collective sums over
+    the ranks: the allreduce schedule carries it as one extra element of the
+    delta payload (no extra traffic), the other schedules all-reduce it beside
+    their collectives.  The reduced word is copied stream-ordered into pinned
+    host memory and read ``LAG`` rounds later, when that copy has long landed,
+    so every rank stops before the same round without waiting for the device.
+    Replaces a per-round all_reduce + .item() (a full device sync per round)."""
+
+    LAG = 2
+    _RING = 4
+
+    def __init__(self, device, word: torch.Tensor, first_round: int):
+        self.gpu = is_gpu(device)
+        self.word = word  # one float32 element on the device, reduced each round
+        self.first = first_round
+        self.voted = False
+        self._cpu = {}
+        self._ring = _native.hip().pinned_alloc(4 * self._RING) if self.gpu else 0
+
+    def vote(self):
+        if not self.voted:
+            self.word.fill_(1.0)  # stream-ordered before this round's collective
+            self.voted = True
+
+    def _slot(self, r: int):
+        import ctypes
+
+        return ctypes.c_float.from_address(self._ring + 4 * (r % self._RING))
+
+    def post(self, r: int, stream: int):
+        """After the collective of round r (on ``stream``)."""
+        if self.gpu:
+            self._slot(r).value = -1.0
+            _native.hip().memcpy_d2h_async(self._ring + 4 * (r % self._RING), self.word.data_ptr(), 4, stream)
+        else:
+            self._cpu[r] = float(self.word.item())  # gloo collectives complete on return
+
+    def decided(self, r: int) -> bool:
+        """Before round r: did the vote of round r - LAG pass?"""
+        k = r - self.LAG
+        if k < self.first:
+            return False
+        if not self.gpu:
+            return self._cpu.pop(k, 0.0) > 0.0
+        slot = self._slot(k)
+        t0 = time.time()
+        while slot.value < 0.0:  # the copy was enqueued LAG rounds ago: normally already landed
+            if time.time() - t0 > 600.0:
+                raise TimeoutError("BSP stop vote: the device copy never landed")
+        return slot.value > 0.0
+
+    def close(self):
+        if self._ring:
+            _native.hip().pinned_free(self._ring)
+            self._ring = 0
+
+
 class DistEngine:
     def __init__(self, cfg: PSConfig, rank: int, world: int, device, train=None, test=None):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, torch.device(device)
@@ -194,6 +255,8 @@ class DistEngine:
             raise
         self.close()
         flush_checkpoints(self.cfg)
+        if self.worker is not None and not out.get("failed"):
+            self.worker.check_device_health()
         if self.log is not None:
             self.log.close()
             if self.log.book is not None:
@@ -212,17 +275,6 @@ class DistEngine:
         flag = torch.tensor([1 if (self.worker is None or self.worker.ready()) else 0], dtype=torch.int32,
                             device=self.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item())
-
-    def _agree_stop(self, rounds_done: int, t_start: float) -> bool:
-        c = self.cfg
-        if c.max_iters:
-            return rounds_done >= c.max_iters
-        local = 1 if (c.max_wallclock_s and time.time() - t_start >= c.max_wallclock_s) else 0
-        if not c.max_wallclock_s and self.worker is not None and self.worker.source.exhausted:
-            local = 1
-        flag = torch.tensor([local], dtype=torch.int32, device=self.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         return bool(flag.item())
 
     # ------------------------------------------------------------------
@@ -265,13 +317,23 @@ class DistEngine:
         lr = cfg.lr
         t_start = time.time()
         r = self.rounds
-        check_every = 1 if not cfg.max_iters else 0
+        vote = None
+        if not cfg.max_iters:  # run until the data / the wall clock says stop: agreed without host syncs
+            if sched == "allreduce" and wk is not None:
+                payload = self._vote_payload()
+                vote = StopVote(self.device, payload[P:], r)
+            else:
+                vote = StopVote(self.device, torch.zeros(1, dtype=torch.float32, device=self.device), r)
         ingested_ahead = False
         while True:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
-            if check_every and self._agree_stop(r - self.rounds, t_start):
-                break
+            if vote is not None:
+                if vote.decided(r):
+                    break
+                if (cfg.max_wallclock_s and time.time() - t_start >= cfg.max_wallclock_s) or (
+                        not cfg.max_wallclock_s and wk is not None and wk.source.exhausted):
+                    vote.vote()
             self.tracer.round_begin()
             with self.tracer.span("ingest"):
                 if wk is not None and not ingested_ahead:
@@ -286,16 +348,18 @@ class DistEngine:
                 with self.tracer.span("solve"):
                     delta = wk.solve() if wk is not None else zeros
                 with self.tracer.span("comm", schedule=sched):
+                    # the stop vote rides in the payload's extra element (allreduce schedule)
+                    payload = self._payload if (vote is not None and wk is not None) else delta
                     if comm is not None:
                         # in stream order; PSX_COMM_OVERLAP=1 runs it on the communicator's side
                         # stream beside the evaluations instead (the fork/join event pairs cost
                         # ~20 us of host time, more than the overlap saves for a 24 KB delta)
                         if overlap:
                             comm.fork()
-                        comm.all_reduce(delta, side=overlap)
+                        comm.all_reduce(payload, side=overlap)
                         work = comm
                     else:
-                        work = dist.all_reduce(delta, op=dist.ReduceOp.SUM, async_op=True)
+                        work = dist.all_reduce(payload, op=dist.ReduceOp.SUM, async_op=True)
                     if wk is not None:
                         wk.log_eval(self.log)
                         # the next round's stream rows land in the ring while the collective
@@ -349,6 +413,13 @@ class DistEngine:
                     if srv.frag is not None:
                         srv.frag.refresh(srv.w)
                     new_w = srv.w
+            if vote is not None:
+                if sched != "allreduce" or wk is None:  # the vote word travels on its own
+                    if comm is not None:
+                        comm.all_reduce(vote.word)
+                    else:
+                        dist.all_reduce(vote.word, op=dist.ReduceOp.SUM)
+                vote.post(r, torch.cuda.current_stream(self.device).cuda_stream if is_gpu(self.device) else 0)
             if srv is not None:
                 if self.rank == 0:
                     srv.tracker.bsp_round(r)  # received(k, r) + sent(k, r + 1) for every worker
@@ -369,11 +440,29 @@ class DistEngine:
             srv.flush_deferred(self.log)  # the last round's server row (rank 0)
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
+        if vote is not None:
+            vote.close()
         elapsed = time.time() - t_start
         self.rounds = r
         return {"rounds": r, "updates": r * N, "elapsed_s": elapsed,
                 "updates_per_s": r * N / elapsed if elapsed > 0 else 0.0,
                 "max_vc_gap": int(srv.tracker.max_gap) if (srv is not None and self.rank == 0) else 0}
+
+    def _vote_payload(self) -> torch.Tensor:
+        """[P + 1] all-reduce payload: the solver writes its delta into the first P
+        entries in place, entry P is the stop vote (StopVote)."""
+        P, wk = self.spec.P, self.worker
+        pl = getattr(self, "_payload", None)
+        if pl is None or pl.numel() != P + 1:
+            pl = torch.zeros(P + 1, dtype=torch.float32, device=self.device)
+            self._payload = pl
+        else:
+            pl[P:].zero_()
+        if wk.solver.delta.data_ptr() != pl.data_ptr():
+            wk.solver.delta = pl[:P]  # bound by the native solver at its next run
+            if getattr(wk.solver, "_bound", None) is not None:
+                wk.solver._bound = None
+        return pl
 
     def _sharded_buffers(self, shard: int):
         """Padded full weight vector whose first P entries ARE the server
@@ -476,9 +565,13 @@ class DistEngine:
             else:
                 srv.apply(delta)
             srv.updates += 1
+            released = srv.tracker.on_delta(k, v)
             if tok.kind == KIND_FINAL:
+                # a finished worker no longer holds the others back (its clock would
+                # freeze min_clock: an SSP worker D ahead would wait forever)
                 finished.add(k)
-            for j, u in srv.tracker.on_delta(k, v):
+                released = list(released) + list(srv.tracker.retire(k))
+            for j, u in released:
                 if j in finished:
                     continue
                 dist.send(srv.w, dst=j + 1)
@@ -499,7 +592,7 @@ class DistEngine:
         tok.worker = wk.k
         dist.recv(wk.w, src=0)
         wk.vc = self._next_vc  # 0, or the server's clock for this worker on a later run
-        max_iters = cfg.max_iters or 1 << 62
+        max_iters = cfg.inject_worker_stop.get(wk.k) or cfg.max_iters or 1 << 62
         t_start = time.time()
         it = 0
         while True:

@@ -65,6 +65,7 @@ class PSConfig:
     # fault injection / tracing
     inject_worker_delay_ms: dict = field(default_factory=dict)  # worker -> ms per iteration
     inject_worker_crash: dict = field(default_factory=dict)  # worker -> iteration at which it fails
+    inject_worker_stop: dict = field(default_factory=dict)  # worker -> iterations after which it leaves cleanly
     worker_timeout_s: float = 600.0  # watchdog: a busy worker silent this long has failed
     on_worker_failure: str = "auto"  # drop | fail | auto (drop under eventual consistency)
     trace_path: str | None = None

@@ -144,6 +144,9 @@ class LocalEngine:
         else:
             out = self._run_async()
         flush_checkpoints(self.cfg)
+        for w in self.workers:
+            if w.k not in self.failed:
+                w.check_device_health()
         self.log.close()
         self.tracer.close()
         if self.log.book is not None:

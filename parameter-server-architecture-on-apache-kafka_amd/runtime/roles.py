@@ -142,6 +142,12 @@ class WorkerRole:
             return self.solver.sparse_delta()
         return self.solver.delta
 
+    def check_device_health(self):
+        """Raise if any device solve of this worker hit a timed-out cross-workgroup
+        wait (its delta was garbage; the logged loss of that row is NaN)."""
+        if self.solver.barrier_errors():
+            raise WorkerFailure(self.k, "device solver: a cross-workgroup wait timed out (non-resident workgroup)")
+
     def log_eval(self, log):
         """Worker row of the last solve: metrics of the LOCALLY trained model
         (LogisticRegressionTaskSpark.java:186)."""

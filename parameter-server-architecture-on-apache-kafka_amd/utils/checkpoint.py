@@ -45,24 +45,36 @@ def _atomic_save(state: dict, final: str) -> str:
 
 
 class _HostCopy:
-    """D2H snapshot of a device tensor on a side stream (pinned destination)."""
+    """D2H snapshot of a device tensor, off the hot path.
+
+    The tensor is first cloned on the PRODUCING stream (an HBM-speed device copy
+    ordered right after the update that produced it), and the pinned-host copy
+    then reads that clone on a side stream.  The next update on the producing
+    stream can therefore rewrite the tensor at once without tearing the snapshot
+    (the clone is only reused after the previous write finished: Checkpointer.submit
+    waits for it)."""
 
     def __init__(self):
         self.buf = None
+        self.dev = None
         self.event = None
 
     def start(self, t: torch.Tensor) -> torch.Tensor:
         if t.device.type != "cuda":
             self.event = None
             return t.detach().clone()
+        flat = t.detach().view(-1)
         if self.buf is None or self.buf.numel() != t.numel() or self.buf.dtype != t.dtype:
             self.buf = torch.empty(t.numel(), dtype=t.dtype, pin_memory=True)
+            self.dev = torch.empty_like(flat)
+        main = torch.cuda.current_stream(t.device)
+        self.dev.copy_(flat)  # snapshot in stream order: before the next update of t
         side = _side_stream(t.device)
         ready = torch.cuda.Event()
-        ready.record(torch.cuda.current_stream(t.device))
+        ready.record(main)
         side.wait_event(ready)
         with torch.cuda.stream(side):
-            self.buf.copy_(t.detach().view(-1), non_blocking=True)
+            self.buf.copy_(self.dev, non_blocking=True)
             self.event = torch.cuda.Event()
             self.event.record(side)
         return self.buf

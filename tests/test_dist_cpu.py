@@ -34,6 +34,16 @@ def _rank_main(rank, world, port, kw, out_q):
     r, w, dev = init_from_env(cpu=True)
     kw = dict(kw)
     data = kw.pop("_data", "dense")
+    count = kw.pop("_count_collectives", False)
+    calls = {"all_reduce": 0, "item": 0}
+    if count:  # every all_reduce issued by the engine after the bootstrap
+        real = dist.all_reduce
+
+        def counting(*a, **k):
+            calls["all_reduce"] += 1
+            return real(*a, **k)
+
+        dist.all_reduce = counting
     cfg = PSConfig(**kw)
     if data == "wide":
         from psx.utils.data import synth_sparse
@@ -44,6 +54,9 @@ def _rank_main(rank, world, port, kw, out_q):
         train, test = synth_finefood(1500, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
     eng = DistEngine(cfg, r, w, dev, train=train, test=test)
     out = eng.run()
+    if count:
+        dist.all_reduce = real
+        out["all_reduce_calls"] = calls["all_reduce"]
     if r == 0:
         out_q.put((out, eng.server.w.cpu().numpy().copy()))  # by value: no fd the exiting rank owns
     dist.barrier()
@@ -79,6 +92,26 @@ def test_bsp_schedules_agree():
     assert torch.allclose(ws["allreduce"], ws["sharded"], atol=1e-5)
 
 
+@pytest.mark.parametrize("sched", ["allreduce", "reduce_bcast", "sharded"])
+def test_bsp_runs_until_exhausted_without_host_sync(sched):
+    """CLI mode (max_iters = 0): the ranks agree to stop through the StopVote word
+    (lagged read, no per-round all_reduce + .item()).  1500 rows over 3 ranks at 64
+    rows per round: the 8th and last ingest happens in round 6 (startup ingest +
+    rounds 0..6; the allreduce schedule ingests the next round's rows while its
+    collective is in flight, so one round earlier), the vote is cast at the top
+    of the next round and the ranks stop LAG rounds later.  The allreduce schedule
+    issues exactly one collective per round (the delta payload carries the vote)."""
+    from psx.parallel.dist import StopVote
+
+    kw = dict(BASE, bsp_schedule=sched, max_iters=0, epochs=1, _count_collectives=True)
+    out, w = _run(3, kw)
+    voted = 6 if sched == "allreduce" else 7
+    assert out["rounds"] == voted + StopVote.LAG
+    if sched == "allreduce":
+        # startup readiness polls aside, one all_reduce per round
+        assert out["all_reduce_calls"] - out["rounds"] <= 2, out
+
+
 def test_bsp_dedicated_server():
     out, w = _run(3, dict(BASE, bsp_schedule="reduce_bcast", server_colocated=False))
     assert out["updates"] == 10  # 2 worker ranks x 5 rounds
@@ -90,6 +123,14 @@ def test_async_dedicated_server(c):
     assert out["updates"] == 12
     if c > 0:
         assert out["max_vc_gap"] <= c + 1
+
+
+@pytest.mark.parametrize("c", [1, 3])
+def test_ssp_worker_stops_early(c):
+    """SSP(D): a worker that finishes early is retired, so the others keep being
+    released (its frozen clock must not hold min_clock back forever)."""
+    out, w = _run(4, dict(BASE, consistency_model=c, max_iters=10, inject_worker_stop={0: 2}))
+    assert out["updates"] == 2 + 2 * 10
 
 
 def test_app_runners_as_processes(tmp_path):

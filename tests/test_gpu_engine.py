@@ -81,6 +81,27 @@ def test_inprocess_checkpoint_resume_gpu(cuda, tmp_path):
     assert d < 1e-4 * max(1.0, ref.server.w.abs().max().item()), d
 
 
+def test_checkpoint_mid_run_snapshot_gpu(cuda, tmp_path):
+    """A checkpoint taken mid-run holds exactly the weights of its step, although
+    the run keeps updating them while the D2H copy is in flight (step 5 of 9)."""
+    from psx.utils.checkpoint import load_server
+
+    train, test = synth_finefood(6000, seed=0), synth_finefood(500, seed=1)
+    kw = dict(num_workers=2, min_buffer_size=256, max_buffer_size=256, init="random")
+    ref = LocalEngine(_cfg(max_iters=5, **kw), cuda, train=train, test=test)
+    ref.run()
+    a = LocalEngine(_cfg(max_iters=9, checkpoint_dir=str(tmp_path), checkpoint_every=5, **kw), cuda, train=train,
+                    test=test)
+    a.run()
+    torch.cuda.synchronize()
+    st = load_server(str(tmp_path))
+    assert st["extra"]["step"] == 5
+    w5 = st["w"].to(cuda)
+    d = (w5 - ref.server.w).abs().max().item()
+    assert d < 1e-5 * max(1.0, ref.server.w.abs().max().item()), d
+    assert (a.server.w - ref.server.w).abs().max().item() > 0  # the run did move on after the snapshot
+
+
 def test_asp_crash_dropped_gpu(cuda):
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     eng = LocalEngine(_cfg(num_workers=3, consistency_model=-1, max_iters=10, inject_worker_crash={2: 4}), cuda,

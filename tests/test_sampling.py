@@ -103,3 +103,17 @@ def test_window_ring_capacity_rounding():
     assert w.size == 100
     assert w.head == 129 % 128
     assert w.start == (w.head - w.size + 1) % 128
+
+
+def test_zero_mean_interarrival_policy():
+    """A burst (every arrival at the same millisecond: mean inter-arrival 0) gives
+    the MAX window here.  Documented deviation: Java's (int) Math.round(Infinity)
+    = (int) Long.MAX_VALUE = -1, so the reference clamps such a burst to the MIN
+    window (WorkerSamplingProcessor.java:115-122); an overflow artefact, not a
+    policy (csrc/host/sampling.cc)."""
+    w = host.SlidingWindow(128, 1024, 0.3)
+    for _ in range(10):
+        w.insert(5.0)  # identical timestamps
+    assert w.target_size() == 1024
+    java_int_cast = ((2 ** 63 - 1) + 2 ** 31) % 2 ** 32 - 2 ** 31  # (int) Long.MAX_VALUE
+    assert java_int_cast == -1 and max(128, min(1024, java_int_cast)) == 128

@@ -11,6 +11,7 @@
 #include <stdexcept>
 
 #include "../comm/rccl_comm.h"
+#include "../runtime/async_server.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
 #include "../solver/wide_solver.h"
@@ -404,6 +405,88 @@ PYBIND11_MODULE(_psx_hip, m) {
     launch_axpy(P<float>(w), P<const float>(x), a, n, S(stream));
     hip_check(hipGetLastError(), "axpy launch");
   });
+
+  // Native SSP/ASP server loop (csrc/runtime/async_server.h).  `cfg`: a dict of
+  // ints / floats; pointers are device addresses (torch data_ptr) or host-runtime
+  // handles (VectorClockTracker.handle, CtrlQueue.handle, MetricsSink.handle,
+  // _psx_host.capi()).
+  py::class_<P2P>(m, "P2P");
+  py::class_<RcclP2P, P2P>(m, "RcclP2P").def(py::init<RcclComm*>(), py::arg("comm"), py::keep_alive<1, 2>());
+  py::class_<LocalP2P, P2P>(m, "LocalP2P")
+      .def(py::init<int, const std::vector<uintptr_t>&, const std::vector<uintptr_t>&, const std::vector<uintptr_t>&>(),
+           py::arg("nworkers"), py::arg("out_f32"), py::arg("out_i32"), py::arg("inbox"))
+      .def("released", &LocalP2P::released);
+  py::class_<LocalFeeder>(m, "LocalFeeder")
+      .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double>(), py::arg("api"),
+           py::arg("ctrl"), py::arg("p2p"), py::arg("nworkers"), py::arg("iters"), py::arg("token_n") = 0,
+           py::arg("timeout_s") = 60.0, py::keep_alive<1, 4>())
+      .def("start", &LocalFeeder::start)
+      .def("join", &LocalFeeder::join, py::call_guard<py::gil_scoped_release>());
+  py::class_<AsyncServer>(m, "AsyncServer")
+      .def(py::init([](P2P& comm, py::dict d, uintptr_t stream) {
+             auto I = [&](const char* k, int64_t def) {
+               return d.contains(k) ? d[k].cast<int64_t>() : def;
+             };
+             auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
+             AsyncServerCfg c;
+             c.nworkers = (int)I("nworkers", 0);
+             c.model = (int)I("model", kAsyncDense);
+             c.lr = d.contains("lr") ? d["lr"].cast<float>() : 1.f;
+             c.P = I("P", 0);
+             c.w = P<float>(U("w"));
+             c.buf = P<float>(U("buf"));
+             c.K = (int)I("K", 0);
+             c.F = (int)I("F", 0);
+             c.FP = (int)I("FP", 0);
+             c.coff = (int)I("coff", 0);
+             c.fhi = P<uint16_t>(U("fhi"));
+             c.flo = P<uint16_t>(U("flo"));
+             c.fb = P<float>(U("fb"));
+             c.Xt = P<const uint16_t>(U("Xt"));
+             c.yt = P<const int32_t>(U("yt"));
+             c.T = (int)I("T", 0);
+             c.KP = (int)I("KP", 0);
+             c.Fw = I("Fw", 0);
+             c.umax = (int)I("umax", 0);
+             c.ubuf = P<int32_t>(U("ubuf"));
+             c.dbuf = P<float>(U("dbuf"));
+             c.t_indptr = P<const int64_t>(U("t_indptr"));
+             c.t_idx = P<const int32_t>(U("t_idx"));
+             c.t_val = P<const uint16_t>(U("t_val"));
+             c.t_y = P<const int32_t>(U("t_y"));
+             c.acc = P<int>(U("acc"));
+             c.ticket = P<unsigned>(U("ticket"));
+             c.api = U("api");
+             c.tracker = U("tracker");
+             c.ctrl = U("ctrl");
+             c.sink = U("sink");
+             c.worker_timeout_s = d.contains("worker_timeout_s") ? d["worker_timeout_s"].cast<double>() : 600.0;
+             if (c.model == kAsyncDense || c.sink) prepare_kernels();
+             return std::make_unique<AsyncServer>(&comm, c, S(stream));
+           }),
+           py::arg("p2p"), py::arg("cfg"), py::arg("stream"), py::keep_alive<1, 2>())
+      .def("begin", &AsyncServer::begin)
+      .def(
+          "run",
+          [](AsyncServer& s, int64_t checkpoint_every) {
+            AsyncStatus st;
+            {
+              py::gil_scoped_release nogil;
+              st = s.run(checkpoint_every);
+            }
+            return py::make_tuple(st.code, st.worker, st.updates);
+          },
+          py::arg("checkpoint_every") = 0)
+      .def("fail", &AsyncServer::fail)
+      .def("set_stream", [](AsyncServer& s, uintptr_t st) { s.set_stream(S(st)); })
+      .def_property("updates", &AsyncServer::updates, &AsyncServer::set_updates)
+      .def_property_readonly("tokens", &AsyncServer::tokens)
+      .def_property_readonly("host_us_per_update", &AsyncServer::host_us_per_update)
+      .def_property_readonly("failed", &AsyncServer::failed);
+  m.attr("ASYNC_DONE") = (int)kAsyncDone;
+  m.attr("ASYNC_ERROR_TOKEN") = (int)kAsyncErrorToken;
+  m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;
+  m.attr("ASYNC_CHECKPOINT") = (int)kAsyncCheckpoint;
 
   m.def("ring_ingest", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
                           uintptr_t ring, uintptr_t ringT, uintptr_t yring, int64_t dst_first, int64_t cap, int FP,

@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../host/capi.h"
 #include "../host/ctrl.h"
 #include "../host/dataset.h"
 #include "../host/libsvm.h"
@@ -20,6 +21,10 @@ namespace py = pybind11;
 using namespace psx;
 
 PYBIND11_MODULE(_psx_host, m) {
+  // C ABI table for the GPU runtime's native server loop (capi.h)
+  m.def("capi", []() { return reinterpret_cast<uintptr_t>(host_api()); });
+  m.attr("CAPI_VERSION") = kHostApiVersion;
+
   m.doc() = "psx native host runtime";
 
   py::class_<VectorClockTracker>(m, "VectorClockTracker")
@@ -41,7 +46,8 @@ PYBIND11_MODULE(_psx_host, m) {
       .def_property_readonly("num_live", &VectorClockTracker::num_live)
       .def_property_readonly("num_workers", &VectorClockTracker::num_workers)
       .def_property_readonly("consistency_model", &VectorClockTracker::consistency_model)
-      .def_property_readonly("max_gap", &VectorClockTracker::max_gap);
+      .def_property_readonly("max_gap", &VectorClockTracker::max_gap)
+      .def_property_readonly("handle", [](VectorClockTracker& t) { return reinterpret_cast<uintptr_t>(&t); });
 
   py::class_<RateEstimator>(m, "RateEstimator")
       .def(py::init<int>(), py::arg("window") = 500)
@@ -175,7 +181,8 @@ PYBIND11_MODULE(_psx_host, m) {
           py::arg("timeout_s") = -1.0)
       .def("unlink", &CtrlQueue::unlink)
       .def_property_readonly("capacity", &CtrlQueue::capacity)
-      .def_property_readonly("name", &CtrlQueue::name);
+      .def_property_readonly("name", &CtrlQueue::name)
+      .def_property_readonly("handle", [](CtrlQueue& q) { return reinterpret_cast<uintptr_t>(&q); });
 
   // Host build of the device solver state machine (csrc/kernels/solver_ctrl.h),
   // so the exact control logic the GPU runs can be unit-tested on the CPU.
@@ -274,6 +281,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("flush", &MetricsSink::flush, py::arg("timeout_s") = 0.0, py::call_guard<py::gil_scoped_release>())
       .def("close", &MetricsSink::close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("processed", &MetricsSink::processed)
+      .def_property_readonly("handle", [](MetricsSink& s) { return reinterpret_cast<uintptr_t>(&s); })
       .def("worker_rows",
            [](MetricsSink& s) {
              py::list out;

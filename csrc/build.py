@@ -98,9 +98,11 @@ def build_hip(force=False, jobs=8):
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     sources = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))) + sorted(
         glob.glob(os.path.join(CSRC, "solver", "*.hip"))
-    ) + sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip"))) + [os.path.join(CSRC, "bindings", "hip_module.hip")]
+    ) + sorted(glob.glob(os.path.join(CSRC, "comm", "*.hip"))) + sorted(
+        glob.glob(os.path.join(CSRC, "runtime", "*.hip"))) + [os.path.join(CSRC, "bindings", "hip_module.hip")]
     headers = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "solver", "*.h")) +
-                     glob.glob(os.path.join(CSRC, "comm", "*.h")))
+                     glob.glob(os.path.join(CSRC, "comm", "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h")) +
+                     [os.path.join(CSRC, "host", "capi.h"), os.path.join(CSRC, "host", "ctrl.h")])
     out = os.path.join(PKG, "_psx_hip" + _ext_suffix())
     cflags = [
         "-O3",

@@ -1,0 +1,96 @@
+// C ABI table of the host runtime (see capi.h).
+#include "capi.h"
+
+#include <exception>
+#include <string>
+
+#include "metrics_sink.h"
+#include "tracker.h"
+
+namespace psx {
+namespace {
+
+thread_local std::string g_err;
+
+template <class F>
+int guarded(F&& f, int on_error) {
+  try {
+    g_err.clear();
+    return f();
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown exception";
+  }
+  return on_error;
+}
+
+int copy_out(const std::vector<std::pair<int, int64_t>>& rel, int* ks, int64_t* vs, int cap) {
+  if ((int)rel.size() > cap) throw std::length_error("release list larger than the caller's buffer");
+  for (size_t i = 0; i < rel.size(); ++i) {
+    ks[i] = rel[i].first;
+    vs[i] = rel[i].second;
+  }
+  return (int)rel.size();
+}
+
+int c_on_delta(void* t, int k, int64_t v, int* ks, int64_t* vs, int cap) {
+  return guarded([&] { return copy_out(static_cast<VectorClockTracker*>(t)->on_delta(k, v), ks, vs, cap); }, -1);
+}
+int c_retire(void* t, int k, int* ks, int64_t* vs, int cap) {
+  return guarded([&] { return copy_out(static_cast<VectorClockTracker*>(t)->retire(k), ks, vs, cap); }, -1);
+}
+int c_is_live(void* t, int k) {
+  return guarded([&] { return static_cast<VectorClockTracker*>(t)->is_live(k) ? 1 : 0; }, -1);
+}
+int64_t c_clock(void* t, int k) {
+  try {
+    g_err.clear();
+    return static_cast<VectorClockTracker*>(t)->clock(k);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  }
+  return -1;
+}
+void c_sent(void* t, int k, int64_t v) {
+  guarded(
+      [&] {
+        static_cast<VectorClockTracker*>(t)->sent(k, v);
+        return 0;
+      },
+      -1);
+}
+int c_pop(void* q, CtrlToken* out, double timeout_s) {
+  return guarded([&] { return static_cast<CtrlQueue*>(q)->pop(out, timeout_s) ? 1 : 0; }, -1);
+}
+int c_push(void* q, const CtrlToken* t, double timeout_s) {
+  return guarded([&] { return static_cast<CtrlQueue*>(q)->push(*t, timeout_s) ? 1 : 0; }, -1);
+}
+int c_acquire(void* s, uint64_t* seq, uintptr_t* addr) {
+  return guarded(
+      [&] {
+        auto* sink = static_cast<MetricsSink*>(s);
+        const int slot = sink->acquire(seq);
+        *addr = sink->slot_address(slot);
+        return slot;
+      },
+      -1);
+}
+void c_submit(void* s, int slot, uint64_t seq, int kind, int64_t ts, int64_t partition, int64_t vc, int64_t nseen) {
+  guarded(
+      [&] {
+        static_cast<MetricsSink*>(s)->submit(slot, seq, kind, ts, partition, vc, nseen);
+        return 0;
+      },
+      -1);
+}
+const char* c_last_error() { return g_err.c_str(); }
+
+const HostApi kApi{kHostApiVersion, c_on_delta, c_retire, c_is_live, c_clock,     c_sent,
+                   c_pop,           c_push,     c_acquire, c_submit,  c_last_error};
+
+}  // namespace
+
+const HostApi* host_api() { return &kApi; }
+
+}  // namespace psx

@@ -1,0 +1,42 @@
+// C ABI of the host runtime (_psx_host) for the GPU runtime (_psx_hip).
+//
+// The two extensions are separate shared objects (the host one builds with g++
+// and needs no GPU).  The native asynchronous server loop in _psx_hip drives
+// objects the host runtime owns -- the vector-clock tracker (MessageTracker),
+// the shared-memory token queue (the GRADIENTS_TOPIC control plane) and the
+// metrics sink (the server CSV log) -- through this table of plain function
+// pointers: no C++ object crosses the library boundary, only opaque handles.
+#pragma once
+#include <cstdint>
+
+#include "ctrl.h"
+
+namespace psx {
+
+constexpr int kHostApiVersion = 1;
+
+struct HostApi {
+  int version;
+  // VectorClockTracker (tracker.h).  The release lists are written to
+  // (ks[i], vs[i]), at most `cap` entries; the return value is the count.
+  int (*tracker_on_delta)(void* tracker, int k, int64_t v, int* ks, int64_t* vs, int cap);
+  int (*tracker_retire)(void* tracker, int k, int* ks, int64_t* vs, int cap);
+  int (*tracker_is_live)(void* tracker, int k);
+  int64_t (*tracker_clock)(void* tracker, int k);
+  void (*tracker_sent)(void* tracker, int k, int64_t v);
+  // CtrlQueue (ctrl.h): 1 = token popped / pushed, 0 = timeout
+  int (*ctrl_pop)(void* queue, CtrlToken* out, double timeout_s);
+  int (*ctrl_push)(void* queue, const CtrlToken* tok, double timeout_s);
+  // MetricsSink (metrics_sink.h): reserve an EvalSlot (its host address is
+  // written to *addr) and hand the finished record to the logger thread
+  int (*sink_acquire)(void* sink, uint64_t* seq, uintptr_t* addr);
+  void (*sink_submit)(void* sink, int slot, uint64_t seq, int kind, int64_t ts, int64_t partition, int64_t vc,
+                      int64_t nseen);
+  // Exceptions thrown by the functions above are caught at this boundary: the
+  // message of the last failure on this thread (empty: none).
+  const char* (*last_error)();
+};
+
+const HostApi* host_api();
+
+}  // namespace psx

@@ -1,0 +1,286 @@
+// Native asynchronous server loop (see async_server.h).
+#include "async_server.h"
+
+#include <chrono>
+#include <stdexcept>
+#include <string>
+
+#include "../kernels/lr_kernels.h"
+#include "../kernels/wide_kernels.h"
+#include "../solver/solver.h"
+
+namespace psx {
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+int64_t epoch_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+constexpr int kKindDelta = 0, kKindFinal = 1, kKindError = 2;
+
+}  // namespace
+
+RcclP2P::RcclP2P(RcclComm* c) : c_(c) {
+  if (!c_) throw std::invalid_argument("RcclP2P: null communicator");
+  if (c_->rank() != 0) throw std::invalid_argument("the asynchronous server runs on rank 0");
+}
+
+LocalP2P::LocalP2P(int nworkers, const std::vector<uintptr_t>& out_f32, const std::vector<uintptr_t>& out_i32,
+                   const std::vector<uintptr_t>& inbox)
+    : n_(nworkers), out_f32_(out_f32), out_i32_(out_i32), inbox_(inbox),
+      released_(new std::atomic<int64_t>[nworkers > 0 ? nworkers : 1]) {
+  if (nworkers < 1 || (int)out_f32.size() != nworkers || (int)inbox.size() != nworkers ||
+      (!out_i32.empty() && (int)out_i32.size() != nworkers))
+    throw std::invalid_argument("LocalP2P: one outbox / inbox per worker");
+  for (int k = 0; k < nworkers; ++k) released_[k].store(0);
+}
+
+void LocalP2P::send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) {
+  if (peer < 1 || peer > n_ || dtype != RcclComm::kF32) throw std::invalid_argument("LocalP2P::send: weights only");
+  hip_check(hipMemcpyAsync(reinterpret_cast<void*>(inbox_[peer - 1]), buf, count * 4, hipMemcpyDeviceToDevice, s),
+            "LocalP2P send copy");
+  released_[peer - 1].fetch_add(1, std::memory_order_release);
+}
+
+void LocalP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) {
+  if (peer < 1 || peer > n_) throw std::invalid_argument("LocalP2P::recv: peer");
+  uintptr_t src = dtype == RcclComm::kI32 ? (out_i32_.empty() ? 0 : out_i32_[peer - 1]) : out_f32_[peer - 1];
+  if (!src) throw std::invalid_argument("LocalP2P::recv: no outbox of that dtype");
+  hip_check(hipMemcpyAsync(buf, reinterpret_cast<const void*>(src), count * 4, hipMemcpyDeviceToDevice, s),
+            "LocalP2P recv copy");
+}
+
+int64_t LocalP2P::released(int k) const { return released_[k].load(std::memory_order_acquire); }
+
+LocalFeeder::LocalFeeder(uintptr_t api, uintptr_t ctrl, LocalP2P* p2p, int nworkers, int64_t iters, int64_t token_n,
+                         double timeout_s)
+    : api_(reinterpret_cast<const HostApi*>(api)), ctrl_(ctrl), p2p_(p2p), n_(nworkers), iters_(iters),
+      token_n_(token_n), timeout_s_(timeout_s) {
+  if (!api_ || api_->version != kHostApiVersion || !ctrl || !p2p || nworkers < 1 || iters < 1)
+    throw std::invalid_argument("LocalFeeder: bad arguments");
+}
+
+LocalFeeder::~LocalFeeder() { join(); }
+
+void LocalFeeder::start() {
+  for (int k = 0; k < n_; ++k) th_.emplace_back([this, k] { run(k); });
+}
+
+bool LocalFeeder::join() {
+  for (auto& t : th_)
+    if (t.joinable()) t.join();
+  th_.clear();
+  return failed_.load() == 0;
+}
+
+void LocalFeeder::run(int k) {
+  for (int64_t it = 0; it < iters_; ++it) {
+    const double t0 = now_s();
+    while (p2p_->released(k) < it + 1) {  // the weights of clock `it` were sent to k
+      if (now_s() - t0 > timeout_s_) {
+        failed_.fetch_add(1);
+        return;
+      }
+      std::this_thread::yield();
+    }
+    CtrlToken t{};
+    t.worker = k;
+    t.kind = it + 1 == iters_ ? kKindFinal : kKindDelta;
+    t.vc = it;
+    t.n = token_n_;
+    if (api_->ctrl_push((void*)ctrl_, &t, timeout_s_) != 1) {
+      failed_.fetch_add(1);
+      return;
+    }
+  }
+}
+
+AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t stream)
+    : comm_(comm), cfg_(cfg), stream_(stream) {
+  if (!comm_) throw std::invalid_argument("AsyncServer: null transport");
+  if (cfg.nworkers < 1 || comm_->size() != cfg.nworkers + 1)
+    throw std::invalid_argument("AsyncServer: the communicator must hold the server + every worker");
+  if (!cfg.api || !cfg.tracker || !cfg.ctrl) throw std::invalid_argument("AsyncServer: missing host runtime handles");
+  api_ = reinterpret_cast<const HostApi*>(cfg.api);
+  if (api_->version != kHostApiVersion) throw std::runtime_error("AsyncServer: host runtime C ABI version mismatch");
+  if (!cfg.w || cfg.P <= 0) throw std::invalid_argument("AsyncServer: no weights");
+  if (cfg.model == kAsyncWideSparse) {
+    if (!cfg.ubuf || !cfg.dbuf || cfg.KP < 1 || cfg.umax < 0) throw std::invalid_argument("AsyncServer: sparse buffers");
+  } else if (!cfg.buf) {
+    throw std::invalid_argument("AsyncServer: no receive buffer");
+  }
+  if (cfg.model == kAsyncDense && cfg.sink && (!cfg.fhi || !cfg.flo || !cfg.fb || !cfg.Xt || !cfg.yt))
+    throw std::invalid_argument("AsyncServer: dense evaluation needs fragments and a test set");
+  if (cfg.sink && (!cfg.acc || !cfg.ticket)) throw std::invalid_argument("AsyncServer: evaluation scratch");
+  finished_.assign(cfg.nworkers, 0);
+  failed_.assign(cfg.nworkers, 0);
+  busy_since_.assign(cfg.nworkers, -1.0);
+  rel_k_.resize(cfg.nworkers + 1);
+  rel_v_.resize(cfg.nworkers + 1);
+}
+
+void AsyncServer::check_api(int rc, const char* what) const {
+  if (rc < 0) throw std::runtime_error(std::string("AsyncServer: ") + what + ": " + api_->last_error());
+}
+
+int AsyncServer::log_worker() const {
+  // server rows follow the deltas of worker 0 (ServerProcessor.java:154-165), or of
+  // the lowest surviving worker once 0 has failed
+  for (int j = 0; j < cfg_.nworkers; ++j)
+    if (!failed_[j]) return j;
+  return -1;
+}
+
+std::vector<int> AsyncServer::failed() const {
+  std::vector<int> out;
+  for (int j = 0; j < cfg_.nworkers; ++j)
+    if (failed_[j]) out.push_back(j);
+  return out;
+}
+
+void AsyncServer::send_weights(const int* ks, const int64_t* vs, int n) {
+  (void)vs;
+  bool any = false;
+  for (int i = 0; i < n; ++i) any |= !finished_[ks[i]];
+  if (!any) return;
+  const double t = now_s();
+  comm_->group_start();
+  for (int i = 0; i < n; ++i) {
+    const int j = ks[i];
+    if (finished_[j]) continue;
+    comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
+    busy_since_[j] = t;
+  }
+  comm_->group_end();
+}
+
+void AsyncServer::begin() {
+  std::fill(finished_.begin(), finished_.end(), 0);
+  std::fill(failed_.begin(), failed_.end(), 0);
+  std::fill(busy_since_.begin(), busy_since_.end(), -1.0);
+  int n = 0;
+  for (int j = 0; j < cfg_.nworkers; ++j) {
+    const int live = api().tracker_is_live((void*)cfg_.tracker, j);
+    check_api(live, "tracker is_live");
+    if (!live) {  // retired in an earlier run (checkpoint of a degraded run)
+      failed_[j] = finished_[j] = 1;
+      continue;
+    }
+    const int64_t u = api().tracker_clock((void*)cfg_.tracker, j);
+    if (u > 0) api().tracker_sent((void*)cfg_.tracker, j, u);  // a later run resumes at the tracked clocks
+    rel_k_[n] = j;
+    rel_v_[n] = u;
+    ++n;
+  }
+  send_weights(rel_k_.data(), rel_v_.data(), n);  // the bootstrap (ServerProcessor.java:75-87)
+}
+
+void AsyncServer::apply_and_log(const CtrlToken& t) {
+  const int k = t.worker;
+  const int peer = k + 1;
+  const int64_t v = t.vc;
+  if (cfg_.model == kAsyncWideSparse) {
+    const int64_t U = t.n;
+    if (U < 0 || U > cfg_.umax) throw std::runtime_error("AsyncServer: sparse push larger than the buffer");
+    if (U) comm_->recv(cfg_.ubuf, (size_t)U, RcclComm::kI32, peer, stream_);
+    comm_->recv(cfg_.dbuf, (size_t)(cfg_.KP + U * cfg_.KP), RcclComm::kF32, peer, stream_);
+    launch_wide_apply_sparse(cfg_.w, cfg_.Fw, cfg_.KP, nullptr, (int)U, cfg_.ubuf, cfg_.dbuf, cfg_.lr, cfg_.umax,
+                             stream_);
+  } else {
+    comm_->recv(cfg_.buf, (size_t)cfg_.P, RcclComm::kF32, peer, stream_);
+    if (cfg_.model == kAsyncDense)
+      launch_server_apply(cfg_.K, cfg_.F, cfg_.FP, cfg_.w, cfg_.buf, cfg_.lr, cfg_.fhi, cfg_.flo, cfg_.fb, stream_,
+                          cfg_.coff);
+    else
+      launch_axpy(cfg_.w, cfg_.buf, cfg_.lr, cfg_.P, stream_);
+  }
+  ++updates_;
+  ++updates_run_;
+  if (cfg_.sink && k == log_worker()) {  // the global model's test metrics, one server row
+    uint64_t seq = 0;
+    uintptr_t addr = 0;
+    const int slot = api().sink_acquire((void*)cfg_.sink, &seq, &addr);
+    check_api(slot, "metrics sink acquire");
+    if (cfg_.model == kAsyncDense)
+      launch_test_eval(cfg_.FP, cfg_.K, cfg_.Xt, cfg_.yt, cfg_.T, cfg_.fhi, cfg_.flo, cfg_.fb, cfg_.acc, stream_,
+                       cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, cfg_.coff);
+    else
+      launch_wide_eval(cfg_.K, cfg_.KP, cfg_.Fw, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, cfg_.w,
+                       nullptr, nullptr, cfg_.acc, cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, stream_);
+    api().sink_submit((void*)cfg_.sink, slot, seq, 1, epoch_ms(), -1, v, 0);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("AsyncServer launch: ") + hipGetErrorString(e));
+}
+
+void AsyncServer::fail(int k) {
+  if (k < 0 || k >= cfg_.nworkers) throw std::out_of_range("AsyncServer::fail: worker id");
+  failed_[k] = finished_[k] = 1;
+  busy_since_[k] = -1.0;
+  const int n = api().tracker_retire((void*)cfg_.tracker, k, rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
+  check_api(n, "tracker retire");
+  send_weights(rel_k_.data(), rel_v_.data(), n);
+}
+
+AsyncStatus AsyncServer::run(int64_t checkpoint_every) {
+  AsyncStatus st;
+  const double poll = cfg_.worker_timeout_s < 1.0 ? cfg_.worker_timeout_s : 1.0;
+  for (;;) {
+    int open = 0;
+    for (int j = 0; j < cfg_.nworkers; ++j) open += !finished_[j];
+    if (open == 0) break;
+    CtrlToken t;
+    const int got = api().ctrl_pop((void*)cfg_.ctrl, &t, poll);
+    check_api(got, "token pop");
+    if (!got) {  // watchdog: a worker holding weights that stays silent has failed
+      const double now = now_s();
+      for (int j = 0; j < cfg_.nworkers; ++j)
+        if (!finished_[j] && busy_since_[j] >= 0.0 && now - busy_since_[j] > cfg_.worker_timeout_s) {
+          st.code = kAsyncWatchdog;
+          st.worker = j;
+          st.updates = updates_;
+          return st;
+        }
+      continue;
+    }
+    const auto h0 = std::chrono::steady_clock::now();
+    ++tokens_;
+    const int k = t.worker;
+    if (k < 0 || k >= cfg_.nworkers) throw std::runtime_error("AsyncServer: token from an unknown worker");
+    if (t.kind == kKindError) {
+      st.code = kAsyncErrorToken;
+      st.worker = k;
+      st.updates = updates_;
+      return st;
+    }
+    if (finished_[k]) throw std::runtime_error("AsyncServer: delta from a finished worker " + std::to_string(k));
+    busy_since_[k] = -1.0;
+    apply_and_log(t);
+    int n = api().tracker_on_delta((void*)cfg_.tracker, k, t.vc, rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
+    check_api(n, "tracker on_delta");
+    if (t.kind == kKindFinal) {
+      // a finished worker no longer holds the others back (its frozen clock would
+      // stall an SSP worker D ahead forever)
+      finished_[k] = 1;
+      const int m = api().tracker_retire((void*)cfg_.tracker, k, rel_k_.data() + n, rel_v_.data() + n,
+                                         (int)rel_k_.size() - n);
+      check_api(m, "tracker retire");
+      n += m;
+    }
+    send_weights(rel_k_.data(), rel_v_.data(), n);
+    host_ns_ += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - h0).count();
+    if (checkpoint_every > 0 && updates_ % checkpoint_every == 0) {
+      st.code = kAsyncCheckpoint;
+      st.updates = updates_;
+      return st;
+    }
+  }
+  st.code = kAsyncDone;
+  st.updates = updates_;
+  return st;
+}
+
+}  // namespace psx

@@ -98,6 +98,13 @@ class NativeComm:
             raise ValueError("all_gather: output must be world x input")
         self.c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _dtype(inp), self._s(side))
 
+    # -- point-to-point (SSP / ASP pushes and pulls) -----------------------------
+    def send(self, t: torch.Tensor, peer: int, side: bool = False):
+        self.c.send(t.data_ptr(), t.numel(), _dtype(t), int(peer), self._s(side))
+
+    def recv(self, t: torch.Tensor, peer: int, side: bool = False):
+        self.c.recv(t.data_ptr(), t.numel(), _dtype(t), int(peer), self._s(side))
+
     def close(self):
         torch.cuda.current_stream(self.device).synchronize()
         self.c.close()

@@ -497,8 +497,12 @@ class DistEngine:
 
     def _run_async(self) -> dict:
         self._open_ctrl()
+        if not hasattr(self, "comm"):  # collective: every rank creates it (None on gloo / CPU)
+            self.comm = make_comm(self.rank, self.world, self.device)
         try:
             if self.is_server:
+                if self.comm is not None and os.environ.get("PSX_NATIVE_ASYNC", "1") != "0":
+                    return self._server_loop_native()
                 return self._server_loop()
             return self._worker_loop()
         finally:
@@ -586,11 +590,109 @@ class DistEngine:
                 "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
                 "failed_workers": sorted(failed)}
 
+    def _native_server(self):
+        """The C++ server loop (csrc/runtime/async_server.h) bound to this engine's
+        tensors, token queue, tracker and metrics sink (created once per engine)."""
+        a = getattr(self, "_aserver", None)
+        if a is not None:
+            return a
+        cfg, srv, spec = self.cfg, self.server, self.spec
+        h = _native.hip()
+        d = dict(nworkers=cfg.num_workers, lr=float(cfg.lr), P=int(spec.P), w=srv.w.data_ptr(),
+                 api=_native.host.capi(), tracker=srv.tracker.handle, ctrl=self._ctrl.handle,
+                 worker_timeout_s=float(cfg.worker_timeout_s))
+        keep = []
+        if self.wide:
+            d.update(KP=spec.KP, K=spec.K, Fw=int(spec.F))
+            if self.sparse_push:
+                KP = spec.KP
+                ubuf = torch.zeros(max(1, self._umax), dtype=torch.int32, device=self.device)
+                dbuf = torch.zeros(KP + self._umax * KP, dtype=torch.float32, device=self.device)
+                keep += [ubuf, dbuf]
+                d.update(model=1, umax=int(self._umax), ubuf=ubuf.data_ptr(), dbuf=dbuf.data_ptr())
+            else:
+                buf = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
+                keep.append(buf)
+                d.update(model=2, buf=buf.data_ptr())
+        else:
+            buf = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
+            keep.append(buf)
+            fr = srv.frag
+            d.update(model=0, buf=buf.data_ptr(), K=spec.K, F=spec.F, FP=spec.Fp, coff=fr.coff, fhi=fr.hi.data_ptr(),
+                     flo=fr.lo.data_ptr(), fb=fr.b.data_ptr())
+        ev = self.evalset
+        if self.log is not None and ev is not None:
+            d.update(sink=self.log.native.handle, acc=srv.scratch.acc.data_ptr(), ticket=srv.scratch.ticket.data_ptr(),
+                     T=int(ev.T))
+            if self.wide:
+                ds = ev.ds
+                d.update(t_indptr=ds.indptr.data_ptr(), t_idx=ds.idx.data_ptr(), t_val=ds.val.data_ptr(),
+                         t_y=ds.y.data_ptr())
+            else:
+                d.update(Xt=ev.X.data_ptr(), yt=ev.y.data_ptr())
+        p2p = h.RcclP2P(self.comm.c)
+        a = h.AsyncServer(p2p, d, torch.cuda.current_stream(self.device).cuda_stream)
+        self._aserver, self._aserver_keep = a, keep + [p2p]
+        return a
+
+    def _server_loop_native(self) -> dict:
+        """SSP / ASP server over native RCCL p2p: the C++ loop pops tokens, enqueues
+        recv -> update (-> evaluation row) -> grouped sends of the new weights on
+        this rank's stream and never synchronises with the device; Python only
+        handles checkpoints and failed workers (ServerProcessor.java:143-183)."""
+        cfg, srv = self.cfg, self.server
+        h = _native.hip()
+        a = self._native_server()
+        if self.log is not None:
+            # rows logged natively go to the sink bound at creation: rebind if swapped
+            if getattr(self, "_aserver_sink", None) not in (None, self.log.native.handle):
+                self._aserver = None
+                a = self._native_server()
+            self._aserver_sink = self.log.native.handle
+        a.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        a.updates = srv.updates
+        t_start = time.time()
+        u0 = srv.updates
+        a.begin()
+        while True:
+            code, k, upd = a.run(int(cfg.checkpoint_every or 0) if cfg.checkpoint_dir else 0)
+            srv.updates = int(upd)
+            if code == h.ASYNC_DONE:
+                break
+            if code == h.ASYNC_CHECKPOINT:
+                maybe_checkpoint(cfg, srv, srv.updates)
+                continue
+            reason = "reported an error" if code == h.ASYNC_ERROR_TOKEN else "busy and silent (watchdog)"
+            if not drop_on_failure(cfg):
+                raise WorkerFailure(int(k), reason)
+            print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
+            a.fail(int(k))
+        torch.cuda.synchronize(self.device)
+        elapsed = time.time() - t_start
+        n = srv.updates - u0
+        return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": n / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
+                "failed_workers": list(a.failed), "host_us_per_update": a.host_us_per_update, "native_server": True}
+
     def _worker_loop(self) -> dict:
         cfg, wk = self.cfg, self.worker
         tok = _native.host.CtrlToken()
         tok.worker = wk.k
-        dist.recv(wk.w, src=0)
+        comm = self.comm
+        gpu = is_gpu(self.device)
+        done = torch.cuda.Event() if gpu else None
+
+        def send(t):
+            comm.send(t, 0) if comm is not None else dist.send(t, dst=0)
+
+        def recv(t):
+            comm.recv(t, 0) if comm is not None else dist.recv(t, src=0)
+
+        recv(wk.w)
+        if gpu and not wk.wide:
+            from ..runtime.roles import SideStream
+
+            wk.side = SideStream(self.device, force=True)
         wk.vc = self._next_vc  # 0, or the server's clock for this worker on a later run
         max_iters = cfg.inject_worker_stop.get(wk.k) or cfg.max_iters or 1 << 62
         t_start = time.time()
@@ -601,20 +703,33 @@ class DistEngine:
                 time.sleep(0.001)
                 wk.ingest()
             try:
-                delta = wk.compute(self.log)
+                delta = wk.solve()
             except WorkerFailure as e:  # report, then leave the protocol (the server retires or aborts)
                 tok.kind, tok.vc, tok.n = KIND_ERROR, wk.vc, 0
                 self._ctrl.push(tok, 600.0)
                 print(f"psx worker {wk.k}: {e}", flush=True)
                 return {"rounds": it, "updates": it, "failed": True}
+            if gpu:
+                done.record(torch.cuda.current_stream(self.device))  # the delta is complete here
+            early = comm is not None and not self.sparse_push
+            if early:  # stream-ordered RCCL send, enqueued now: it moves as soon as the server posts the recv
+                send(delta)
+            # the local model's row (LogisticRegressionTaskSpark.java:186) on the side
+            # stream: it overlaps the push/pull instead of delaying them
+            wk.log_eval(self.log)
             it += 1
             final = it >= max_iters or (cfg.max_wallclock_s and time.time() - t_start >= cfg.max_wallclock_s) or (
                 not cfg.max_iters and not cfg.max_wallclock_s and wk.source.exhausted)
             tok.vc = wk.vc
             tok.kind = KIND_FINAL if final else KIND_DELTA
             tok.aux = wk.tuples_seen
-            if is_gpu(self.device):
-                torch.cuda.current_stream(self.device).synchronize()  # delta ready before the token is visible
+            if gpu:
+                # the token says "my delta is complete": the server serves tokens in
+                # arrival order, so it must not wait on a delta still being computed.
+                # Poll this solve's completion event (no full stream synchronisation:
+                # the evaluation row enqueued behind it keeps running)
+                while not done.query():
+                    pass
             U = wk.solver.host_count() if self.sparse_push else 0
             tok.n = U
             if not self._ctrl.push(tok, 600.0):
@@ -622,13 +737,13 @@ class DistEngine:
             if self.sparse_push:  # (ids, values) of the window's features only
                 KP = self.spec.KP
                 if U:
-                    dist.send(delta.uniq[:U], dst=0)
-                dist.send(delta.dloc[: KP + U * KP], dst=0)
-            else:
-                dist.send(delta, dst=0)
+                    send(delta.uniq[:U])
+                send(delta.dloc[: KP + U * KP])
+            elif not early:  # gloo sends block until received: only after the token
+                send(delta)
             if final:
                 break
-            dist.recv(wk.w, src=0)
+            recv(wk.w)  # stream-ordered: the next solve enqueued below waits for it on the device
             wk.vc += 1
             if self.log is not None:
                 self.log.drain()

@@ -34,9 +34,9 @@ class SideStream:
     solver kernels leave most CUs idle, so a test-set evaluation on the side
     stream overlaps the next solve instead of adding to the round time."""
 
-    def __init__(self, device):
+    def __init__(self, device, force: bool = False):
         self.device = torch.device(device)
-        self.gpu = is_gpu(self.device) and os.environ.get("PSX_SIDE_EVAL", "0") == "1"
+        self.gpu = is_gpu(self.device) and (force or os.environ.get("PSX_SIDE_EVAL", "0") == "1")
         self.stream = torch.cuda.Stream(self.device) if self.gpu else None
         self._ready = torch.cuda.Event() if self.gpu else None
         self._done = torch.cuda.Event() if self.gpu else None

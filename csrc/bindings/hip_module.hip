@@ -417,9 +417,10 @@ PYBIND11_MODULE(_psx_hip, m) {
            py::arg("nworkers"), py::arg("out_f32"), py::arg("out_i32"), py::arg("inbox"))
       .def("released", &LocalP2P::released);
   py::class_<LocalFeeder>(m, "LocalFeeder")
-      .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double>(), py::arg("api"),
-           py::arg("ctrl"), py::arg("p2p"), py::arg("nworkers"), py::arg("iters"), py::arg("token_n") = 0,
-           py::arg("timeout_s") = 60.0, py::keep_alive<1, 4>())
+      .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double, const std::vector<int64_t>&>(),
+           py::arg("api"), py::arg("ctrl"), py::arg("p2p"), py::arg("nworkers"), py::arg("iters"),
+           py::arg("token_n") = 0, py::arg("timeout_s") = 60.0, py::arg("vc0") = std::vector<int64_t>{},
+           py::keep_alive<1, 4>())
       .def("start", &LocalFeeder::start)
       .def("join", &LocalFeeder::join, py::call_guard<py::gil_scoped_release>());
   py::class_<AsyncServer>(m, "AsyncServer")

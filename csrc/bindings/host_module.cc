@@ -41,6 +41,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("sent_flags", &VectorClockTracker::sent_flags)
       .def("restore", &VectorClockTracker::restore)
       .def("retire", &VectorClockTracker::retire)
+      .def("revive", &VectorClockTracker::revive)
       .def("bsp_round", &VectorClockTracker::bsp_round)
       .def("is_live", &VectorClockTracker::is_live)
       .def_property_readonly("num_live", &VectorClockTracker::num_live)

@@ -43,6 +43,14 @@ int c_retire(void* t, int k, int* ks, int64_t* vs, int cap) {
 int c_is_live(void* t, int k) {
   return guarded([&] { return static_cast<VectorClockTracker*>(t)->is_live(k) ? 1 : 0; }, -1);
 }
+int c_revive(void* t, int k) {
+  return guarded(
+      [&] {
+        static_cast<VectorClockTracker*>(t)->revive(k);
+        return 0;
+      },
+      -1);
+}
 int64_t c_clock(void* t, int k) {
   try {
     g_err.clear();
@@ -86,8 +94,8 @@ void c_submit(void* s, int slot, uint64_t seq, int kind, int64_t ts, int64_t par
 }
 const char* c_last_error() { return g_err.c_str(); }
 
-const HostApi kApi{kHostApiVersion, c_on_delta, c_retire, c_is_live, c_clock,     c_sent,
-                   c_pop,           c_push,     c_acquire, c_submit,  c_last_error};
+const HostApi kApi{kHostApiVersion, c_on_delta, c_retire, c_is_live, c_revive,  c_clock,
+                   c_sent,          c_pop,      c_push,   c_acquire, c_submit,  c_last_error};
 
 }  // namespace
 

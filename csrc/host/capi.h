@@ -22,6 +22,7 @@ struct HostApi {
   int (*tracker_on_delta)(void* tracker, int k, int64_t v, int* ks, int64_t* vs, int cap);
   int (*tracker_retire)(void* tracker, int k, int* ks, int64_t* vs, int cap);
   int (*tracker_is_live)(void* tracker, int k);
+  int (*tracker_revive)(void* tracker, int k);
   int64_t (*tracker_clock)(void* tracker, int k);
   void (*tracker_sent)(void* tracker, int k, int64_t v);
   // CtrlQueue (ctrl.h): 1 = token popped / pushed, 0 = timeout

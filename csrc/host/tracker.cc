@@ -65,6 +65,11 @@ std::vector<std::pair<int, int64_t>> VectorClockTracker::retire(int k) {
   return out;
 }
 
+void VectorClockTracker::revive(int k) {
+  if (k < 0 || k >= num_workers()) throw std::out_of_range("worker id " + std::to_string(k));
+  live_[k] = 1;
+}
+
 int VectorClockTracker::num_live() const {
   int n = 0;
   for (auto l : live_) n += l ? 1 : 0;

@@ -44,6 +44,9 @@ class VectorClockTracker {
   // min/max, and workers it was holding back under BSP/SSP are released
   // (returned, already marked sent).
   std::vector<std::pair<int, int64_t>> retire(int k);
+  // A worker retired because it FINISHED a run rejoins the next run at its clock
+  // (failed workers stay retired).
+  void revive(int k);
   bool is_live(int k) const { return live_.at(k) != 0; }
   int num_live() const;
 

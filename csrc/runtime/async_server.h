@@ -133,8 +133,9 @@ struct AsyncStatus {
 class AsyncServer {
  public:
   AsyncServer(P2P* p2p, const AsyncServerCfg& cfg, hipStream_t stream);
-  // New run: clear the finished / failed sets, send every live worker the
-  // weights of its current clock (the bootstrap: vc 0 on a fresh tracker).
+  // New run: workers that finished the previous run rejoin (failed ones stay
+  // retired), every live worker gets the weights of its current clock (the
+  // bootstrap: vc 0 on a fresh tracker).
   void begin();
   // Serve tokens until every worker finished (or a code that needs the caller).
   AsyncStatus run(int64_t checkpoint_every);
@@ -159,7 +160,8 @@ class AsyncServer {
   AsyncServerCfg cfg_;
   hipStream_t stream_;
   const HostApi* api_;
-  std::vector<uint8_t> finished_, failed_;
+  std::vector<uint8_t> finished_, failed_;  // this run
+  std::vector<uint8_t> dead_;               // failed in any run: never revived
   std::vector<double> busy_since_;  // < 0: not busy (weights not sent / delta back)
   std::vector<int> rel_k_;
   std::vector<int64_t> rel_v_;
@@ -174,8 +176,10 @@ class AsyncServer {
 // protocol, the tracker decisions and the server's host cost in isolation.
 class LocalFeeder {
  public:
+  // vc0[k]: worker k's clock at the start (the tracker's); the release counter's
+  // value at construction is the baseline (construct before the server's begin())
   LocalFeeder(uintptr_t api, uintptr_t ctrl, LocalP2P* p2p, int nworkers, int64_t iters, int64_t token_n,
-              double timeout_s);
+              double timeout_s, const std::vector<int64_t>& vc0);
   ~LocalFeeder();
   void start();
   // true: every thread pushed all its tokens; false: a thread timed out waiting
@@ -189,6 +193,7 @@ class LocalFeeder {
   int n_;
   int64_t iters_, token_n_;
   double timeout_s_;
+  std::vector<int64_t> vc0_, base_;
   std::vector<std::thread> th_;
   std::atomic<int> failed_{0};
 };

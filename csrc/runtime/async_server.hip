@@ -56,11 +56,15 @@ void LocalP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s)
 int64_t LocalP2P::released(int k) const { return released_[k].load(std::memory_order_acquire); }
 
 LocalFeeder::LocalFeeder(uintptr_t api, uintptr_t ctrl, LocalP2P* p2p, int nworkers, int64_t iters, int64_t token_n,
-                         double timeout_s)
+                         double timeout_s, const std::vector<int64_t>& vc0)
     : api_(reinterpret_cast<const HostApi*>(api)), ctrl_(ctrl), p2p_(p2p), n_(nworkers), iters_(iters),
-      token_n_(token_n), timeout_s_(timeout_s) {
+      token_n_(token_n), timeout_s_(timeout_s), vc0_(vc0), base_(nworkers, 0) {
   if (!api_ || api_->version != kHostApiVersion || !ctrl || !p2p || nworkers < 1 || iters < 1)
     throw std::invalid_argument("LocalFeeder: bad arguments");
+  if (vc0_.empty()) vc0_.assign(nworkers, 0);
+  if ((int)vc0_.size() != nworkers) throw std::invalid_argument("LocalFeeder: one start clock per worker");
+  // construct BEFORE the server's begin(): its bootstrap sends count as releases
+  for (int k = 0; k < n_; ++k) base_[k] = p2p_->released(k);
 }
 
 LocalFeeder::~LocalFeeder() { join(); }
@@ -79,7 +83,7 @@ bool LocalFeeder::join() {
 void LocalFeeder::run(int k) {
   for (int64_t it = 0; it < iters_; ++it) {
     const double t0 = now_s();
-    while (p2p_->released(k) < it + 1) {  // the weights of clock `it` were sent to k
+    while (p2p_->released(k) < base_[k] + it + 1) {  // the weights of this clock were sent to k
       if (now_s() - t0 > timeout_s_) {
         failed_.fetch_add(1);
         return;
@@ -89,7 +93,7 @@ void LocalFeeder::run(int k) {
     CtrlToken t{};
     t.worker = k;
     t.kind = it + 1 == iters_ ? kKindFinal : kKindDelta;
-    t.vc = it;
+    t.vc = vc0_[k] + it;
     t.n = token_n_;
     if (api_->ctrl_push((void*)ctrl_, &t, timeout_s_) != 1) {
       failed_.fetch_add(1);
@@ -117,6 +121,7 @@ AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t strea
   if (cfg.sink && (!cfg.acc || !cfg.ticket)) throw std::invalid_argument("AsyncServer: evaluation scratch");
   finished_.assign(cfg.nworkers, 0);
   failed_.assign(cfg.nworkers, 0);
+  dead_.assign(cfg.nworkers, 0);
   busy_since_.assign(cfg.nworkers, -1.0);
   rel_k_.resize(cfg.nworkers + 1);
   rel_v_.resize(cfg.nworkers + 1);
@@ -163,10 +168,14 @@ void AsyncServer::begin() {
   std::fill(busy_since_.begin(), busy_since_.end(), -1.0);
   int n = 0;
   for (int j = 0; j < cfg_.nworkers; ++j) {
-    const int live = api().tracker_is_live((void*)cfg_.tracker, j);
+    int live = api().tracker_is_live((void*)cfg_.tracker, j);
     check_api(live, "tracker is_live");
-    if (!live) {  // retired in an earlier run (checkpoint of a degraded run)
-      failed_[j] = finished_[j] = 1;
+    if (!live && !dead_[j]) {  // retired because it finished the previous run: rejoins
+      check_api(api().tracker_revive((void*)cfg_.tracker, j), "tracker revive");
+      live = 1;
+    }
+    if (!live) {  // failed in an earlier run (or retired in a resumed checkpoint)
+      failed_[j] = finished_[j] = dead_[j] = 1;
       continue;
     }
     const int64_t u = api().tracker_clock((void*)cfg_.tracker, j);
@@ -218,7 +227,7 @@ void AsyncServer::apply_and_log(const CtrlToken& t) {
 
 void AsyncServer::fail(int k) {
   if (k < 0 || k >= cfg_.nworkers) throw std::out_of_range("AsyncServer::fail: worker id");
-  failed_[k] = finished_[k] = 1;
+  failed_[k] = finished_[k] = dead_[k] = 1;
   busy_since_[k] = -1.0;
   const int n = api().tracker_retire((void*)cfg_.tracker, k, rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
   check_api(n, "tracker retire");

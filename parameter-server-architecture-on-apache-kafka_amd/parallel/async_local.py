@@ -60,8 +60,9 @@ class LocalAsyncHarness:
     def run(self, iters: int, timeout_s: float = 120.0) -> dict:
         """Every stand-in worker pushes ``iters`` deltas (the last one final)."""
         h = _native.hip()
+        vc0 = [int(self.tracker.clock(k)) for k in range(self.N)]  # a later run continues at the tracked clocks
         feeder = h.LocalFeeder(_native.host.capi(), self.queue.handle, self.p2p, self.N, int(iters), 0,
-                               float(timeout_s))
+                               float(timeout_s), vc0)
         torch.cuda.synchronize(self.device)
         u0 = self.server.updates
         t0 = time.perf_counter()

@@ -518,12 +518,17 @@ class DistEngine:
             KP = self.spec.KP
             ubuf = torch.zeros(self._umax, dtype=torch.int32, device=self.device)
             dbuf = torch.zeros(KP + self._umax * KP, dtype=torch.float32, device=self.device)
+        dead = self.__dict__.setdefault("_dead_workers", set())  # failed in any run: stay retired
+        finished = set(dead)
+        failed = set(dead)
         for j in range(N):  # bootstrap: vc 0 to every worker (tracker untouched)
+            if j in dead:
+                continue
+            if not srv.tracker.is_live(j):  # finished the previous run of this engine: rejoins
+                srv.tracker.revive(j)
             if srv.tracker.clock(j) > 0:  # a later run of this engine: resume at the tracked clocks
                 srv.tracker.sent(j, srv.tracker.clock(j))
             dist.send(srv.w, dst=j + 1)
-        finished = set()
-        failed = set()
         t_start = time.time()
         busy_since = {j: t_start for j in range(N)}  # weights sent, delta not back yet (watchdog)
 
@@ -533,6 +538,7 @@ class DistEngine:
             print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
             failed.add(k)
             finished.add(k)
+            dead.add(k)
             busy_since.pop(k, None)
             for j, u in srv.tracker.retire(k):
                 if j not in finished:

@@ -59,3 +59,14 @@ def test_bench_single_gpu_default_unchanged():
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w1")
+
+
+@pytest.mark.parametrize("c", [2, -1])
+def test_bench_async_two_runs_same_engine(c):
+    """Warm-up run then timed run of the same engine (SSP / ASP with a dedicated
+    server rank): the workers that finished the warm-up rejoin the timed run."""
+    p, lines = _run(["--gpus", "3", "--consistency", str(c)] + SMALL)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 3 and d["config"]["workers"] == 2
+    assert d["value"] > 0

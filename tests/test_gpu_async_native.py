@@ -43,5 +43,9 @@ def test_native_async_server_two_runs(cuda):
     try:
         out = hs.run(10)
         assert out["updates"] == 20 and hs.server.updates == 20
+        # every worker finished (retired) at the end of run 1: run 2 revives them
+        out = hs.run(7)
+        assert out["updates"] == 14 and hs.server.updates == 34
+        assert [hs.tracker.clock(k) for k in range(2)] == [17, 17]
     finally:
         hs.close()

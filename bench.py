@@ -155,7 +155,10 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
         data = (f"synthetic (fine-food-reviews-shaped, {a.train_rows} train / {a.test_rows} test rows, "
                 f"random-init weights)")
         ref = REF_UPDATES_PER_S_1W if n_workers == 1 else REF_UPDATES_PER_S_4W
-        vs = round(ups / ref, 1)
+        # the reference's buffer is -max 1024; larger windows are a new config
+        vs = round(ups / ref, 1) if a.buffer == 1024 else None
+        if a.buffer != 1024:
+            model += f", window {a.buffer} rows/worker"
     else:
         kind = "binary sigmoid" if a.model == "sharded100m" else "multinomial K=6"
         model = f"sparse-input logreg F={a.features} {kind}, local solver L-BFGS x2 + strong-Wolfe (window subspace)"

@@ -70,6 +70,7 @@ PYBIND11_MODULE(_psx_hip, m) {
     return d;
   });
   m.def("fp_supported", &fp_supported);
+  m.def("solver_rows_mode", &rows_mode_for, py::arg("cap"));
   m.def("eval_lds_bytes", &eval_lds_bytes);
 
   py::class_<SolverCfg>(m, "SolverCfg", py::module_local())
@@ -127,6 +128,7 @@ PYBIND11_MODULE(_psx_hip, m) {
            })
       .def("read_stamps", [](LocalSolver& s, uintptr_t stream) { return s.read_stamps(S(stream)); })
       .def_property_readonly("eval_wg", &LocalSolver::eval_wg)
+      .def_property_readonly("rows_mode", &LocalSolver::rows_mode)
       .def_property_readonly("kernels_per_solve", &LocalSolver::kernels_per_solve);
 
   m.def(

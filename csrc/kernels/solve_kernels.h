@@ -33,6 +33,11 @@ struct SolveDev {
   int KP, FPI, PI, pad_;
   long long* dbg;  // optional phase timeline (debug)
   unsigned* prm_count;  // runs completed (finalize advances it): all-gather tag base
+  // large-window ("rows") mode: row-parallel fused forward+backward with
+  // per-workgroup partials instead of the feature-major ring copy XT
+  float* gpart;   // [G][KP][FP] partial gradients (raw sums of R^T X)
+  double* spart;  // [G][2][FP] partial column sums / sums of squares
+  float* gred;    // [KP][FPI] reduced gradient sums (bwd_update reads them when non-null)
 };
 
 int padded_classes(int K);
@@ -55,5 +60,22 @@ void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int s
                  const SolveDev& dv, int nwg, hipStream_t s, int with_finalize = 0);
 size_t tail_lds_bytes(int FP);
 int tail_grid(int FP, int nwg);
+
+// ---- large-window ("rows") mode: every pass over the window is row-parallel
+// over G workgroups (no XT copy, no residual buffer); see solve_kernels.hip ----
+// Windows of more than this many ring rows use it (PSX_SOLVER_ROWS=0/1 forces).
+constexpr int kRowsModeMinCap = 8192;
+bool rows_mode_for(int cap);
+void launch_stats_rows(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, int B, int start, int G,
+                       hipStream_t s);
+void launch_prep_rows(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int G,
+                      hipStream_t s);
+void launch_fwdbwd_rows(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, int slot, const SolveDev& dv,
+                        int G, hipStream_t s);
+void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, const SolveDev& dv, int G,
+                     hipStream_t s);
+void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
+                hipStream_t s);
+size_t stats_rows_lds_bytes();
 
 }  // namespace psx

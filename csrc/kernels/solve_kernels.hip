@@ -36,6 +36,8 @@
 // with setMaxIter(2), standardisation, centring, delta = w_new - w_old).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "lr_kernels.h"
 #include "solve_kernels.h"
 #include "tile.h"
@@ -96,6 +98,62 @@ __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_b
 // with few loads per lane, so the window read is not latency-serialised).
 constexpr int kStatW = 8;
 constexpr int kStatL = 256 / kStatW;
+// Shared tail of the window-statistics kernels: rs / rq (LDS) hold the kStatW
+// features' column sums and sums of squares over the window; derive std /
+// 1/std, the initial point x0 = w_old * std (Spark standardisation), reset the
+// solver vectors, write the first trial fragments and initialise the controller.
+__device__ __forceinline__ void prep_epilogue(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, int B, int fs,
+                                              const double* rs, const double* rq, float* sdl, float* ivl, float wo_pre,
+                                              float b_pre) {
+  const int t = threadIdx.x;
+  if (t < kStatW) {
+    const double a = rs[t];
+    const double b = rq[t];
+    const int f = fs + t;
+    const double n = (double)B;
+    double sd = 0.0;
+    if (f < cfg.F && n > 1.0) {
+      const double mean = a / n;
+      const double var = (b - n * mean * mean) / (n - 1.0);
+      sd = var > 0.0 ? sqrt(var) : 0.0;
+    }
+    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
+    sdl[t] = sdf;
+    ivl[t] = inv;
+    dv.std_[f] = sdf;
+    dv.inv_std[f] = inv;
+  }
+  __syncthreads();
+  const int K = cfg.K, KP = dv.KP, FPI = dv.FPI;
+  static_assert(kStatW * 16 <= 256, "one element per thread");
+  if (t < kStatW * KP) {
+    const int e = t;
+    const int c = e / kStatW, fl = e % kStatW, f = fs + fl;
+    const int pi = c * FPI + f;
+    const float wo = wo_pre;
+    const float xv = wo * sdl[fl];
+    dv.x[pi] = xv;
+    dv.d[pi] = 0.f;
+    dv.g_c[pi] = 0.f;
+    const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo;
+    dv.wfix[pi] = fix;
+    write_frag(dv.whi, dv.wlo, c, f, xv * ivl[fl] + fix);
+  }
+  if (blockIdx.x == 0) {
+    if (t < 16) {
+      const int pi = KP * FPI + t;
+      const float b = b_pre;
+      dv.x[pi] = b;
+      dv.d[pi] = 0.f;
+      dv.g_c[pi] = 0.f;
+      dv.b_eff[t] = b;
+    }
+    if (t == 32) ctrl_init(*ctrl);
+    if (t == 0) stamp(dv, 30, 1);
+    if (t == 65) xstore(dv.xch + kXchBar, 0ull);
+  }
+}
+
 // With a fused ingest (ing.n > 0) each workgroup first copies its kStatW-feature
 // slice of the new rows into X / XT (and workgroup 0 the labels); the new rows'
 // statistics come from an LDS copy, the old rows' from XT as before.
@@ -184,61 +242,44 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
     rq[fl0] = b2;
   }
   __syncthreads();
-  if (t < kStatW) {
-    const double a = rs[t];
-    const double b = rq[t];
-    const int f = fs + t;
-    const double n = (double)B;
-    double sd = 0.0;
-    if (f < cfg.F && n > 1.0) {
-      const double mean = a / n;
-      const double var = (b - n * mean * mean) / (n - 1.0);
-      sd = var > 0.0 ? sqrt(var) : 0.0;
-    }
-    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
-    sdl[t] = sdf;
-    ivl[t] = inv;
-    dv.std_[f] = sdf;
-    dv.inv_std[f] = inv;
-  }
-  __syncthreads();
-  const int K = cfg.K, KP = dv.KP, FPI = dv.FPI;
-  static_assert(kStatW * 16 <= 256, "one element per thread");
-  if (t < kStatW * KP) {
-    const int e = t;
-    const int c = e / kStatW, fl = e % kStatW, f = fs + fl;
-    const int pi = c * FPI + f;
-    const float wo = wo_pre;
-    const float xv = wo * sdl[fl];
-    dv.x[pi] = xv;
-    dv.d[pi] = 0.f;
-    dv.g_c[pi] = 0.f;
-    const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo;
-    dv.wfix[pi] = fix;
-    write_frag(dv.whi, dv.wlo, c, f, xv * ivl[fl] + fix);
-  }
-  if (blockIdx.x == 0) {
-    if (t < 16) {
-      const int pi = KP * FPI + t;
-      const float b = b_pre;
-      dv.x[pi] = b;
-      dv.d[pi] = 0.f;
-      dv.g_c[pi] = 0.f;
-      dv.b_eff[t] = b;
-    }
-    if (t == 32) ctrl_init(*ctrl);
-    if (t == 0) stamp(dv, 30, 1);
-    if (t == 65) xstore(dv.xch + kXchBar, 0ull);
-  }
+  prep_epilogue(cfg, dv, ctrl, B, fs, rs, rq, sdl, ivl, wo_pre, b_pre);
 }
 
 // ---------------------------------------------------------------------------
 // fwd_kernel: loss and residuals at the trial point (row-parallel).
 // Body shared by fwd_kernel and tail_kernel: workgroup `wg` of `G` takes the
 // window tiles wg, wg+G, ...
+// Rows mode: G^T partial of one tile, acc[n] (this wave's N-tiles of 16 features)
+// += R_tile^T X_tile on MFMA.  A = R^T (class x 8 rows, bf16 hi + lo from the
+// LDS residual tile rt[c][32 rows]); B = 8 rows x 16 features of the staged X
+// image, read TRANSPOSED by ds_read_b64_tr_b16 from the same dual-use image the
+// forward reads row-wise (no feature-major copy of the ring).
 template <int FP>
+__device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned short* rt, f32x4* acc) {
+  constexpr int NT = FP / 64;  // 16-feature N-tiles per wave
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const u16x8 ah = *(const u16x8*)(rt + i * 32 + 8 * g);  // class i, rows 8g..8g+7
+  const u16x8 al = *(const u16x8*)(rt + 512 + i * 32 + 8 * g);
+  const int r0 = 8 * g + q;  // lane 4q+p of the group supplies row q of the 4-row block
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int f0 = (w * NT + n) * 16;
+    const char* sub = lds + (f0 >> 7) * 8192;
+    const int ch = ((f0 & 127) >> 3) + (p >> 1);
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + lds_off(r0, ch) + 8 * (p & 1)));
+    const s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sub + lds_off(r0 + 4, ch) + 8 * (p & 1)));
+    const u16x8 b = u16x8{(unsigned short)v1[0], (unsigned short)v1[1], (unsigned short)v1[2], (unsigned short)v1[3],
+                          (unsigned short)v2[0], (unsigned short)v2[1], (unsigned short)v2[2], (unsigned short)v2[3]};
+    acc[n] = mfma16x16x32(as_bf16x8(ah), as_bf16x8(b), acc[n]);
+    acc[n] = mfma16x16x32(as_bf16x8(al), as_bf16x8(b), acc[n]);
+  }
+}
+
+template <int FP, bool kRows = false>
 __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams* prm, int slot, const SolveDev& dv,
-                                         char* lds, const int wg, const int G) {
+                                         char* lds, const int wg, const int G, f32x4* gacc = nullptr) {
   const int B = prm->B, K = cfg.K;
   const WinTiles wt(prm->start, B, cfg.cap);
   const int ntiles = wt.nt;
@@ -310,9 +351,15 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
       rt[512 + (sc0 + 1) * 32 + sr] = l;
     }
     __syncthreads();
-    // residual tile -> global, in the A-operand layout of the backward MFMA
-    // (rows of the padding classes >= K are never read by the backward)
-    if ((((tid * 4) & 511) >> 5) < K) *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
+    if constexpr (kRows) {  // the backward of this tile while it is in LDS
+      bwd_tile_acc<FP>(lds, rt, gacc);
+      __syncthreads();  // the next tile's staging overwrites the image and rt
+    } else {
+      // residual tile -> global, in the A-operand layout of the backward MFMA
+      // (rows of the padding classes >= K are never read by the backward)
+      if ((((tid * 4) & 511) >> 5) < K)
+        *(u16x4*)(dv.R + (size_t)tile * 1024 + tid * 4) = *(const u16x4*)(rt + tid * 4);
+    }
     if (wg == 0 && tid == 0) stamp(dv, slot, 11);
   }
   atomicAdd(&rsum[sc0], rs0);
@@ -413,8 +460,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 
   // ---- backward G[c][slice] = sum_r R[r][c] X[r][slice] ----
+  // (rows mode: already summed by fwdbwd_rows + reduce_g into dv.gred)
+  const bool gred = dv.gred != nullptr;
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  {
+  if (!gred) {
     const int m16 = lane & 15, kg = (lane >> 4) * 8;
     const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
     const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
@@ -449,19 +498,22 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (wg0 && tid == 0) stamp(dv, slot, 3);
   wg_stamp(dv, slot, 1, wg);
   // cross-wave reduction of the accumulators (D[class][feature])
+  if (!gred) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int c = (lane >> 4) * 4 + rr;
-      gw[(w * 16 + c) * 32 + j * 16 + (lane & 15)] = acc[j][rr];
-    }
+      for (int rr = 0; rr < 4; ++rr) {
+        const int c = (lane >> 4) * 4 + rr;
+        gw[(w * 16 + c) * 32 + j * 16 + (lane & 15)] = acc[j][rr];
+      }
+  }
   __syncthreads();
   float g[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
     const int c = (cgp + 8 * e) & 15;
-    const float s = gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
+    const float s = gred ? (own[e] ? dv.gred[idx[e]] : 0.f)
+                         : gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
     g[e] = own[e] ? s * invB * iv : 0.f;
   }
   float rpart = 0.f;  // the cross-wave barrier above also published pr[]
@@ -889,6 +941,31 @@ static void launch_slot_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* c
   }
 }
 
+template <int FP>
+static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
+                          int nwg, hipStream_t s) {
+  const int ng = bwd_grid(FP);
+  const size_t bl = bwd_lds_bytes();
+  switch (dv.KP) {
+    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    default: bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+  }
+}
+
+void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
+                hipStream_t s) {
+  switch (cfg.Fp) {
+    case 128: launch_bwd_fp<128>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    case 256: launch_bwd_fp<256>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    case 512: launch_bwd_fp<512>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    case 1024: launch_bwd_fp<1024>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    case 2048: launch_bwd_fp<2048>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    default: break;
+  }
+}
+
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                  hipStream_t s) {
   switch (cfg.Fp) {
@@ -937,6 +1014,213 @@ void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int s
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-window ("rows") mode.  A window of up to tens of millions of ring rows
+// (the reference's -max, WorkerAppRunner.java:56-57) is streamed
+// row-parallel by G workgroups, each taking ring tiles wg, wg+G, ...:
+//   stats_rows_kernel   partial column sums / squares          -> spart[G]
+//   prep_rows_kernel    reduce them (fixed order), std, x0, controller
+//   per slot: fwdbwd_rows_kernel  forward + softmax + backward of each tile
+//                                 while it sits in LDS        -> gpart[G]
+//             reduce_g_kernel     G = sum over workgroups (fixed order)
+//             bwd_update_kernel   (gred mode) dots, controller, update
+// Every evaluation reads the window ONCE (the small-window path reads X for the
+// forward and the feature-major copy XT for the backward), no XT copy exists,
+// and no residual buffer is materialised.  Deterministic: every reduction runs
+// in a fixed order.
+bool rows_mode_for(int cap) {
+  const char* e = std::getenv("PSX_SOLVER_ROWS");
+  if (e && *e) return e[0] == '1';
+  return cap > kRowsModeMinCap;
+}
+
+template <int FP>
+__global__ __launch_bounds__(256) void stats_rows_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv, int B,
+                                                         int start) {
+  constexpr int C = FP / 8;   // 16-B chunks per row
+  constexpr int L = 256 / C;  // row lanes
+  static_assert(C * L == 256, "FP in {128..2048}");
+  constexpr int RPL = 32 / L;  // rows of a tile per lane
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* red = (double*)smem;  // [L][C][16]
+  if (blockIdx.x == 0 && threadIdx.x == 0) *prm = SolveParams{B, start, 0, 0};
+  const WinTiles wt(start, B, cfg.cap);
+  const int t = threadIdx.x, ch = t % C, rl = t / C;
+  double s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
+  for (int tile = blockIdx.x; tile < wt.nt; tile += gridDim.x) {
+    const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
+    u16x8 v[RPL];
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) v[j] = *(const u16x8*)(dv.X + (row0 + rl + L * j) * FP + ch * 8);
+    float fs[8], fq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fs[e] = fq[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int o = tile * 32 + rl + L * j - wt.s0;  // offset in the window
+      const bool in = o >= 0 && o < B;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = in ? bf2f(v[j][e]) : 0.f;
+        fs[e] += x;
+        fq[e] += x * x;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s[e] += fs[e];
+      q[e] += fq[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(rl * C + ch) * 16 + e] = s[e];
+    red[(rl * C + ch) * 16 + 8 + e] = q[e];
+  }
+  __syncthreads();
+  for (int k = t; k < C * 16; k += 256) {  // k = chunk * 16 + {sum e | square e}
+    double a = 0.0;
+    for (int r = 0; r < L; ++r) a += red[r * C * 16 + k];
+    const int c = k >> 4, e = k & 15, f = c * 8 + (e & 7);
+    dv.spart[((size_t)blockIdx.x * 2 + (e >> 3)) * FP + f] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void prep_rows_kernel(SolverCfg cfg, const SolveParams* prm, SolveDev dv,
+                                                        Ctrl* ctrl, int G) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* rs = (double*)smem;          // [kStatW]
+  double* rq = rs + kStatW;            // [kStatW]
+  float* sdl = (float*)(rq + kStatW);  // [kStatW]
+  float* ivl = sdl + kStatW;           // [kStatW]
+  double* part = (double*)(ivl + kStatW);  // [16 lanes][16]
+  const int t = threadIdx.x, FP = cfg.Fp, B = prm->B;
+  const int fs = blockIdx.x * kStatW;
+  const int KP0 = dv.KP;
+  float wo_pre = 0.f, b_pre = 0.f;
+  if (t < kStatW * KP0) {
+    const int c = t / kStatW, f = fs + t % kStatW;
+    if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
+  }
+  if (blockIdx.x == 0 && t < 16 && t < cfg.K) b_pre = dv.w_old[cfg.K * FP + t];
+  {  // thread: (feature fl, sum|square) x 16 lanes over the G partials
+    const int fl = t & 7, kind = (t >> 3) & 1, lane = t >> 4;
+    double a = 0.0;
+    for (int g = lane; g < G; g += 16) a += dv.spart[((size_t)g * 2 + kind) * FP + fs + fl];
+    part[lane * 16 + kind * 8 + fl] = a;
+  }
+  __syncthreads();
+  if (t < 16) {
+    double a = 0.0;
+    for (int lane = 0; lane < 16; ++lane) a += part[lane * 16 + t];  // fixed order
+    if (t < 8)
+      rs[t] = a;
+    else
+      rq[t - 8] = a;
+  }
+  __syncthreads();
+  prep_epilogue(cfg, dv, ctrl, B, fs, rs, rq, sdl, ivl, wo_pre, b_pre);
+}
+
+template <int FP>
+__global__ __launch_bounds__(256) void fwdbwd_rows_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl,
+                                                          int slot, SolveDev dv) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot
+  constexpr int NT = FP / 64;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
+  const int wg = blockIdx.x;
+  const WinTiles wt(prm->start, prm->B, cfg.cap);
+  if (wg >= wt.nt) return;
+  fwd_body<FP, true>(cfg, prm, slot, dv, lds, wg, gridDim.x, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, KP = dv.KP;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int f = (w * NT + n) * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = (lane >> 4) * 4 + i;
+      if (c < KP) dv.gpart[((size_t)wg * KP + c) * FP + f] = acc[n][i];
+    }
+  }
+}
+
+// gred[c][f] = sum over the forward workgroups of gpart (fixed order): 64
+// elements per workgroup, 4 partial sums per element combined in order.
+__global__ __launch_bounds__(256) void reduce_g_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl,
+                                                       SolveDev dv, int G) {
+  __shared__ float red[4][64];
+  if (ctrl->phase == kPhDone) return;
+  const WinTiles wt(prm->start, prm->B, cfg.cap);
+  const int nfw = wt.nt < G ? wt.nt : G;
+  const int FP = cfg.Fp, KP = dv.KP;
+  const int t = threadIdx.x, e = blockIdx.x * 64 + (t & 63), sub = t >> 6;
+  const int c = e / FP, f = e - c * FP;
+  float a = 0.f;
+  if (c < KP) {
+    const float* src = dv.gpart + (size_t)c * FP + f;
+    const size_t stride = (size_t)KP * FP;
+    constexpr int U = 8;
+    for (int g0 = sub; g0 < nfw; g0 += 4 * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int g = g0 + 4 * u;
+        v[u] = g < nfw ? src[(size_t)g * stride] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) a += v[u];
+    }
+  }
+  red[sub][t & 63] = a;
+  __syncthreads();
+  if (t < 64 && c < KP) dv.gred[c * dv.FPI + f] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+
+size_t stats_rows_lds_bytes() { return (size_t)256 * 16 * sizeof(double); }
+
+void launch_stats_rows(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, int B, int start, int G,
+                       hipStream_t s) {
+  const size_t lb = stats_rows_lds_bytes();
+  switch (cfg.Fp) {
+    case 128: stats_rows_kernel<128><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+    case 256: stats_rows_kernel<256><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+    case 512: stats_rows_kernel<512><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+    case 1024: stats_rows_kernel<1024><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+    case 2048: stats_rows_kernel<2048><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+    default: break;
+  }
+}
+
+void launch_prep_rows(const SolverCfg& cfg, const SolveParams* prm, const SolveDev& dv, Ctrl* ctrl, int G,
+                      hipStream_t s) {
+  const size_t lb = 2 * kStatW * sizeof(double) + 2 * kStatW * sizeof(float) + 16 * 16 * sizeof(double);
+  prep_rows_kernel<<<cfg.Fp / kStatW, 256, lb, s>>>(cfg, prm, dv, ctrl, G);
+}
+
+void launch_fwdbwd_rows(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, int slot, const SolveDev& dv,
+                        int G, hipStream_t s) {
+  const size_t lb = fwd_lds_bytes(cfg.Fp);
+  switch (cfg.Fp) {
+    case 128: fwdbwd_rows_kernel<128><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+    case 256: fwdbwd_rows_kernel<256><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+    case 512: fwdbwd_rows_kernel<512><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+    case 1024: fwdbwd_rows_kernel<1024><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+    case 2048: fwdbwd_rows_kernel<2048><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+    default: break;
+  }
+}
+
+void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, const SolveDev& dv, int G,
+                     hipStream_t s) {
+  const int n = dv.KP * cfg.Fp;
+  reduce_g_kernel<<<(n + 63) / 64, 256, 0, s>>>(cfg, prm, ctrl, dv, G);
+}
+
 template <int FP>
 static void set_slot_attr() {
   const int tb = (int)tail_lds_bytes(FP);
@@ -945,6 +1229,8 @@ static void set_slot_attr() {
   (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
   (void)hipFuncSetAttribute((const void*)tail_kernel<FP, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, tb);
   (void)hipFuncSetAttribute((const void*)fwd_kernel<FP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)fwd_lds_bytes(FP));
+  (void)hipFuncSetAttribute((const void*)fwdbwd_rows_kernel<FP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)fwd_lds_bytes(FP));
   const int b = (int)bwd_lds_bytes();
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);

@@ -48,7 +48,10 @@ class LocalSolver {
   void run(int B, int start, hipStream_t stream, const RingIngest& ing = RingIngest{});
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
-  int kernels_per_solve() const { return 2 + 2 * nfast_; }  // stats_prep + slots + (tail with finalize | finalize)
+  int kernels_per_solve() const {  // stats_prep + slots + (tail with finalize | finalize); rows: 3 per slot
+    return rows_mode_ ? 3 + 3 * cfg_.nslots : 2 + 2 * nfast_;
+  }
+  bool rows_mode() const { return rows_mode_; }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):
@@ -61,6 +64,7 @@ class LocalSolver {
   SolveDev dv_{};
   int nwg_eval_;
   int nfast_;
+  bool rows_mode_ = false;  // large window: row-parallel fused passes (solve_kernels.h)
   bool use_graph_;
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;

@@ -18,10 +18,16 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   if (cfg.hist < 1 || cfg.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
   if (cfg.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
   if (cfg.cap < 32 || cfg.cap % 32 != 0) throw std::invalid_argument("ring capacity must be a positive multiple of 32");
-  if (!buf.XT) throw std::invalid_argument("the solver needs the feature-major ring copy XT");
+  rows_mode_ = rows_mode_for(cfg.cap);
+  if (!rows_mode_ && !buf.XT) throw std::invalid_argument("the solver needs the feature-major ring copy XT");
   const int tiles = cfg.cap / kTileRows + 1;  // window tiles (ring-aligned; a wrapped window may touch one twice)
   nwg_eval_ = tiles < max_eval_wg ? tiles : max_eval_wg;
   if (nwg_eval_ < 1) nwg_eval_ = 1;
+  if (rows_mode_) {
+    use_graph_ = false;  // eager: the rows chain has no per-run node to patch
+    // two workgroups per CU keep >= 128 KB of each CU's window tiles in flight
+    nwg_eval_ = tiles < 512 ? tiles : 512;
+  }
   // slots launched one by one: the initial evaluation + one trial per iteration
   // (what a solve whose line searches accept their first trial uses); the
   // remaining budget runs in the persistent tail launch
@@ -44,7 +50,11 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const size_t o_S = take(H * PI * 4), o_Y = take(H * PI * 4);
   const size_t o_std = take(FPI * 4), o_istd = take(FPI * 4), o_wfix = take(PI * 4), o_beff = take(16 * 4);
   const size_t o_whi = take(16 * FP * 2), o_wlo = take(16 * FP * 2);
-  const size_t o_R = take((size_t)tiles * 1024 * 2);
+  const size_t o_R = take(rows_mode_ ? 256 : (size_t)tiles * 1024 * 2);  // rows mode keeps no residual tiles
+  const size_t G = (size_t)nwg_eval_;
+  const size_t o_gpart = rows_mode_ ? take(G * dv_.KP * FP * 4) : 0;
+  const size_t o_spart = rows_mode_ ? take(G * 2 * FP * 8) : 0;
+  const size_t o_gred = rows_mode_ ? take((size_t)dv_.KP * FPI * 4) : 0;
   const int npart = nwg_eval_ > tail_grid(cfg.Fp, nwg_eval_) ? nwg_eval_ : tail_grid(cfg.Fp, nwg_eval_);
   const size_t o_part = take((size_t)npart * 32 * 4);
   const size_t o_xch = take((size_t)xch_words() * 8);
@@ -84,6 +94,9 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.stats = buf.stats;
   dv_.dbg = stamps ? reinterpret_cast<long long*>(b + o_dbg) : nullptr;
   dv_.prm_count = reinterpret_cast<unsigned*>(b + o_cnt);
+  dv_.gpart = rows_mode_ ? reinterpret_cast<float*>(b + o_gpart) : nullptr;
+  dv_.spart = rows_mode_ ? reinterpret_cast<double*>(b + o_spart) : nullptr;
+  dv_.gred = rows_mode_ ? reinterpret_cast<float*>(b + o_gred) : nullptr;
 
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -129,6 +142,19 @@ LocalSolver::~LocalSolver() {
 }
 
 void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing) {
+  if (rows_mode_) {
+    const int G = nwg_eval_;
+    launch_stats_rows(cfg_, prm_, dv_, B, start, G, s);
+    launch_prep_rows(cfg_, prm_, dv_, ctrl_, G, s);
+    for (int slot = 0; slot < cfg_.nslots; ++slot) {  // slots after convergence exit at once
+      launch_fwdbwd_rows(cfg_, prm_, ctrl_, slot, dv_, G, s);
+      launch_reduce_g(cfg_, prm_, ctrl_, dv_, G, s);
+      launch_bwd(cfg_, prm_, ctrl_, slot, dv_, G, s);
+    }
+    launch_finalize(cfg_, ctrl_, dv_, s);
+    hip_check(hipGetLastError(), "solver kernel launch (rows mode)");
+    return;
+  }
   launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, ing, s);
   for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
   if (cfg_.nslots > nfast_)
@@ -142,6 +168,7 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
   if (ing.n < 0 || ing.n > kMaxFusedIngest || ing.n > cfg_.cap) throw std::invalid_argument("fused ingest: bad row count");
+  if (ing.n > 0 && rows_mode_) throw std::invalid_argument("fused ingest is not available for large windows");
   if (ing.n > 0) {
     if (!ing.src || !ing.ysrc || ing.dst < 0 || ing.dst >= cfg_.cap || ing.first < 0 || ing.step < 1)
       throw std::invalid_argument("fused ingest: bad source / destination");

@@ -102,7 +102,8 @@ class LocalSolveOp:
         self._bound = None
 
     def _bind(self, ring, w_old: torch.Tensor):
-        key = (ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr())
+        xt = ring.XT.data_ptr() if ring.XT is not None else 0  # None: large-window (rows) solver
+        key = (ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr())
         if self._bound == key:
             return
         if ring.X.dtype != torch.bfloat16 or ring.X.shape != (self.cap, self.spec.Fp) or ring.y.dtype != torch.int32:
@@ -116,7 +117,7 @@ class LocalSolveOp:
         cfg.center, cfg.zero_const = int(o.center), int(o.zero_const)
         cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
         self._native = h.LocalSolver(
-            cfg, ring.X.data_ptr(), ring.XT.data_ptr(), ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
+            cfg, ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
             self.loss.data_ptr(), self.stats.data_ptr(), o.max_eval_wg, bool(o.use_graph))
         self._bound = key

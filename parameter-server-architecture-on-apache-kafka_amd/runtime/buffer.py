@@ -42,12 +42,15 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
         self.Fp, self.device = int(Fp), torch.device(device)
         self.X = torch.zeros(self.cap, self.Fp, dtype=torch.bfloat16, device=self.device)
         self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+        # large windows: the solver streams row-parallel fused passes and needs no
+        # feature-major copy (csrc/kernels/solve_kernels.h, "rows" mode)
+        self.rows_mode = is_gpu(self.device) and bool(_native.hip().solver_rows_mode(self.cap))
         self.XT = (torch.zeros(self.Fp, self.cap, dtype=torch.bfloat16, device=self.device)
-                   if is_gpu(self.device) else None)
+                   if is_gpu(self.device) and not self.rows_mode else None)
         # defer: the last ingest is not launched on its own but handed to the next
         # local solve, whose first kernel copies it (LocalSolveOp.run); any other
         # reader of the ring must call flush() first
-        self.defer = bool(defer) and is_gpu(self.device)
+        self.defer = bool(defer) and is_gpu(self.device) and not self.rows_mode
         self.pending = None
 
     def ingest(self, src_X: torch.Tensor, src_y: torch.Tensor, src_first: int, src_step: int, n: int, dst_first: int):
@@ -82,7 +85,8 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
     def _launch(self, src_X, src_y, src_first, src_step, n, dst_first):
         if is_gpu(self.device):
             _native.hip().ring_ingest(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
-                                      self.X.data_ptr(), self.XT.data_ptr(), self.y.data_ptr(), int(dst_first),
+                                      self.X.data_ptr(), self.XT.data_ptr() if self.XT is not None else 0,
+                                      self.y.data_ptr(), int(dst_first),
                                       self.cap, self.Fp, stream_handle(self.device))
         else:
             src = torch.arange(n) * src_step + src_first

@@ -72,6 +72,8 @@ def parse(argv=None):
     ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--buffer", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="dense model feature rows (fp32: row-parallel solver with hi+lo MFMA operands)")
     ap.add_argument("--workers", type=int, default=1,
                     help="single-GPU run: in-process workers sharing the GPU (one HIP stream each); default 1")
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
@@ -117,6 +119,7 @@ def build_cfg(a, n_workers):
         init="random",
         seed=0,
         model="wide" if wide else "dense",
+        dtype=a.dtype,
         sigmoid=a.model == "sharded100m",
         solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
                              zero_const=not wide),
@@ -131,7 +134,7 @@ def make_data(a, device):
     from psx.utils.data import synth_finefood, synth_sparse
 
     if a.model == "dense":
-        return (synth_finefood(a.train_rows, num_features=a.features, seed=0),
+        return (synth_finefood(a.train_rows, num_features=a.features, seed=0, dtype=a.dtype),
                 synth_finefood(a.test_rows, num_features=a.features, seed=1))
     labels = "binary" if a.model == "sharded100m" else "finefood"
     kw = dict(num_features=a.features, labels=labels, nnz_mean=48, max_nnz=128, device=device)
@@ -186,7 +189,7 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": vs,
-        "dtype": "bf16",
+        "dtype": a.dtype,
         "data": data,
         "config": {
             "model": model,

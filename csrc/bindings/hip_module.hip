@@ -88,14 +88,18 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("zero_const", &SolverCfg::zero_const)
       .def_readwrite("nslots", &SolverCfg::nslots)
       .def_readwrite("gd_lr", &SolverCfg::gd_lr)
-      .def_readwrite("tol", &SolverCfg::tol);
+      .def_readwrite("tol", &SolverCfg::tol)
+      .def_readwrite("xf32", &SolverCfg::xf32);
 
   py::class_<LocalSolver>(m, "LocalSolver")
       .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t XT, uintptr_t y, uintptr_t w_old,
                        uintptr_t delta, uintptr_t w_new, uintptr_t wf_hi, uintptr_t wf_lo, uintptr_t b_fin,
                        uintptr_t loss, uintptr_t stats, int max_eval_wg, bool use_graph) {
              SolverBuffers b;
-             b.X = P<const uint16_t>(X);
+             if (cfg.xf32)
+               b.Xf = P<const float>(X);  // the ring holds fp32 rows
+             else
+               b.X = P<const uint16_t>(X);
              b.XT = P<const uint16_t>(XT);
              b.y = P<const int32_t>(y);
              b.w_old = P<const float>(w_old);
@@ -491,6 +495,12 @@ PYBIND11_MODULE(_psx_hip, m) {
   m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;
   m.attr("ASYNC_CHECKPOINT") = (int)kAsyncCheckpoint;
 
+  m.def("ring_ingest_f32", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
+                              uintptr_t ring, uintptr_t yring, int64_t dst_first, int64_t cap, int FP, uintptr_t stream) {
+    launch_ring_ingest_f32(P<const float>(src), P<const int32_t>(ysrc), src_first, src_step, n, P<float>(ring),
+                           P<int32_t>(yring), dst_first, cap, FP, S(stream));
+    hip_check(hipGetLastError(), "ring_ingest_f32 launch");
+  });
   m.def("ring_ingest", [](uintptr_t src, uintptr_t ysrc, int64_t src_first, int64_t src_step, int64_t n,
                           uintptr_t ring, uintptr_t ringT, uintptr_t yring, int64_t dst_first, int64_t cap, int FP,
                           uintptr_t stream) {

@@ -202,7 +202,8 @@ PYBIND11_MODULE(_psx_host, m) {
       .def_readwrite("zero_const", &SolverCfg::zero_const)
       .def_readwrite("nslots", &SolverCfg::nslots)
       .def_readwrite("gd_lr", &SolverCfg::gd_lr)
-      .def_readwrite("tol", &SolverCfg::tol);
+      .def_readwrite("tol", &SolverCfg::tol)
+      .def_readwrite("xf32", &SolverCfg::xf32);
   py::class_<Ctrl>(m, "SolverCtrl", py::module_local())
       .def(py::init([]() {
         auto c = std::make_unique<Ctrl>();

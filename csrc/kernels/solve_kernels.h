@@ -38,6 +38,7 @@ struct SolveDev {
   float* gpart;   // [G][KP][FP] partial gradients (raw sums of R^T X)
   double* spart;  // [G][2][FP] partial column sums / sums of squares
   float* gred;    // [KP][FPI] reduced gradient sums (bwd_update reads them when non-null)
+  const float* Xf;  // fp32 ring rows [cap][Fp] (cfg.xf32; X is then unused)
 };
 
 int padded_classes(int K);
@@ -65,6 +66,8 @@ int tail_grid(int FP, int nwg);
 // over G workgroups (no XT copy, no residual buffer); see solve_kernels.hip ----
 // Windows of more than this many ring rows use it (PSX_SOLVER_ROWS=0/1 forces).
 constexpr int kRowsModeMinCap = 8192;
+// rows-mode grids up to this many workgroups reduce their partials inside bwd_update
+constexpr int kRowsReduceInBwd = 64;
 bool rows_mode_for(int cap);
 void launch_stats_rows(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, int B, int start, int G,
                        hipStream_t s);
@@ -77,5 +80,8 @@ void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* c
 void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
                 hipStream_t s);
 size_t stats_rows_lds_bytes();
+// fp32 ring rows: rows src_first + i*src_step -> slots (dst_first + i) % cap
+void launch_ring_ingest_f32(const float* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
+                            float* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s);
 
 }  // namespace psx

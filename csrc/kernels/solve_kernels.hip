@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
 // LDS residual tile rt[c][32 rows]); B = 8 rows x 16 features of the staged X
 // image, read TRANSPOSED by ds_read_b64_tr_b16 from the same dual-use image the
 // forward reads row-wise (no feature-major copy of the ring).
-template <int FP>
+template <int FP, bool kHiOnly = false>
 __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned short* rt, f32x4* acc) {
   constexpr int NT = FP / 64;  // 16-feature N-tiles per wave
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -273,19 +273,24 @@ __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned sho
     const u16x8 b = u16x8{(unsigned short)v1[0], (unsigned short)v1[1], (unsigned short)v1[2], (unsigned short)v1[3],
                           (unsigned short)v2[0], (unsigned short)v2[1], (unsigned short)v2[2], (unsigned short)v2[3]};
     acc[n] = mfma16x16x32(as_bf16x8(ah), as_bf16x8(b), acc[n]);
-    acc[n] = mfma16x16x32(as_bf16x8(al), as_bf16x8(b), acc[n]);
+    if constexpr (!kHiOnly) acc[n] = mfma16x16x32(as_bf16x8(al), as_bf16x8(b), acc[n]);
   }
 }
 
-template <int FP, bool kRows = false>
+// kF32 (rows mode only): fp32 ring rows staged as hi + lo bf16 images (the lo
+// image right after the hi one), forward x_hi.(W_hi + W_lo) + x_lo.W_hi and
+// backward (R_hi + R_lo)^T x_hi + R_hi^T x_lo -- near-fp32 products on bf16 MFMA.
+template <int FP, bool kRows = false, bool kF32 = false>
 __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams* prm, int slot, const SolveDev& dv,
                                          char* lds, const int wg, const int G, f32x4* gacc = nullptr) {
+  static_assert(!kF32 || (kRows && FP <= 1024), "fp32 rows: rows mode, FP <= 1024 (two tile images in LDS)");
   const int B = prm->B, K = cfg.K;
   const WinTiles wt(prm->start, B, cfg.cap);
   const int ntiles = wt.nt;
   if (wg >= ntiles) return;
   if (wg == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
-  char* red_base = lds + 32 * FP * 2;
+  char* lds_lo = lds + 32 * FP * 2;  // kF32: the lo image
+  char* red_base = lds + (kF32 ? 2 : 1) * 32 * FP * 2;
   unsigned short* rt = (unsigned short*)(red_base + 8192);  // [2][16][32]
   int* ylds = (int*)(red_base + 8192 + 2048);
   float* rsum = (float*)(ylds + 32);
@@ -304,7 +309,10 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
   for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-    stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
+    if constexpr (kF32)
+      stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
+    else
+      stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
     if (tid < 32) ylds[tid] = dv.y[row0 + tid];
     __syncthreads();
     if (wg == 0 && tid == 0) stamp(dv, slot, 9);
@@ -313,6 +321,7 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
       forward_tile_pre<FP>(lds, wf, a0, a1);
     else
       forward_tile<FP>(lds, dv.whi, dv.wlo, a0, a1);
+    if constexpr (kF32) forward_tile_pre_lo<FP>(lds_lo, wf, a0, a1);
     store_partial_logits(red_base, a0, a1);
     __syncthreads();
     if (wg == 0 && tid == 0) stamp(dv, slot, 10);
@@ -353,6 +362,7 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
     __syncthreads();
     if constexpr (kRows) {  // the backward of this tile while it is in LDS
       bwd_tile_acc<FP>(lds, rt, gacc);
+      if constexpr (kF32) bwd_tile_acc<FP, true>(lds_lo, rt, gacc);
       __syncthreads();  // the next tile's staging overwrites the image and rt
     } else {
       // residual tile -> global, in the A-operand layout of the backward MFMA
@@ -460,8 +470,9 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
 
   // ---- backward G[c][slice] = sum_r R[r][c] X[r][slice] ----
-  // (rows mode: already summed by fwdbwd_rows + reduce_g into dv.gred)
-  const bool gred = dv.gred != nullptr;
+  // (rows mode: partial sums of the fwdbwd_rows workgroups, already reduced by
+  // reduce_g into dv.gred for large grids, summed here in a fixed order otherwise)
+  const bool gred = dv.gpart != nullptr;
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   if (!gred) {
     const int m16 = lane & 15, kg = (lane >> 4) * 8;
@@ -512,8 +523,27 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
     const int c = (cgp + 8 * e) & 15;
-    const float s = gred ? (own[e] ? dv.gred[idx[e]] : 0.f)
-                         : gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
+    float s;
+    if (!gred) {
+      s = gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
+    } else if (dv.gred) {
+      s = own[e] ? dv.gred[idx[e]] : 0.f;
+    } else {  // small grid: sum the workgroups' partials here (fixed order)
+      s = 0.f;
+      if (own[e]) {
+        const int nfw_g = wt.nt < fwd_grid ? wt.nt : fwd_grid;
+        const size_t stride = (size_t)dv.KP * cfg.Fp;
+        const float* src = dv.gpart + (size_t)(cgp + 8 * e) * cfg.Fp + f;
+        constexpr int U = 8;
+        for (int g0 = 0; g0 < nfw_g; g0 += U) {
+          float v[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) v[u] = g0 + u < nfw_g ? src[(size_t)(g0 + u) * stride] : 0.f;
+#pragma unroll
+          for (int u = 0; u < U; ++u) s += v[u];
+        }
+      }
+    }
     g[e] = own[e] ? s * invB * iv : 0.f;
   }
   float rpart = 0.f;  // the cross-wave barrier above also published pr[]
@@ -1034,7 +1064,7 @@ bool rows_mode_for(int cap) {
   return cap > kRowsModeMinCap;
 }
 
-template <int FP>
+template <int FP, bool kF32 = false>
 __global__ __launch_bounds__(256) void stats_rows_kernel(SolverCfg cfg, SolveParams* prm, SolveDev dv, int B,
                                                          int start) {
   constexpr int C = FP / 8;   // 16-B chunks per row
@@ -1051,21 +1081,46 @@ __global__ __launch_bounds__(256) void stats_rows_kernel(SolverCfg cfg, SolvePar
   for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.0;
   for (int tile = blockIdx.x; tile < wt.nt; tile += gridDim.x) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-    u16x8 v[RPL];
-#pragma unroll
-    for (int j = 0; j < RPL; ++j) v[j] = *(const u16x8*)(dv.X + (row0 + rl + L * j) * FP + ch * 8);
     float fs[8], fq[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) fs[e] = fq[e] = 0.f;
+    if constexpr (kF32) {
+      constexpr int RB = RPL < 8 ? RPL : 8;  // rows whose 32 B are in flight together
 #pragma unroll
-    for (int j = 0; j < RPL; ++j) {
-      const int o = tile * 32 + rl + L * j - wt.s0;  // offset in the window
-      const bool in = o >= 0 && o < B;
+      for (int j0 = 0; j0 < RPL; j0 += RB) {
+        f32x4 v[RB][2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = in ? bf2f(v[j][e]) : 0.f;
-        fs[e] += x;
-        fq[e] += x * x;
+        for (int j = 0; j < RB; ++j) {
+          const float* src = dv.Xf + (row0 + rl + L * (j0 + j)) * FP + ch * 8;
+          v[j][0] = *(const f32x4*)src;
+          v[j][1] = *(const f32x4*)(src + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+          const int o = tile * 32 + rl + L * (j0 + j) - wt.s0;
+          const bool in = o >= 0 && o < B;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = in ? v[j][e >> 2][e & 3] : 0.f;
+            fs[e] += x;
+            fq[e] += x * x;
+          }
+        }
+      }
+    } else {
+      u16x8 v[RPL];
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) v[j] = *(const u16x8*)(dv.X + (row0 + rl + L * j) * FP + ch * 8);
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const int o = tile * 32 + rl + L * j - wt.s0;  // offset in the window
+        const bool in = o >= 0 && o < B;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = in ? bf2f(v[j][e]) : 0.f;
+          fs[e] += x;
+          fq[e] += x * x;
+        }
       }
     }
 #pragma unroll
@@ -1124,7 +1179,7 @@ __global__ __launch_bounds__(256) void prep_rows_kernel(SolverCfg cfg, const Sol
   prep_epilogue(cfg, dv, ctrl, B, fs, rs, rq, sdl, ivl, wo_pre, b_pre);
 }
 
-template <int FP>
+template <int FP, bool kF32 = false>
 __global__ __launch_bounds__(256) void fwdbwd_rows_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl,
                                                           int slot, SolveDev dv) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1136,7 +1191,7 @@ __global__ __launch_bounds__(256) void fwdbwd_rows_kernel(SolverCfg cfg, const S
   const int wg = blockIdx.x;
   const WinTiles wt(prm->start, prm->B, cfg.cap);
   if (wg >= wt.nt) return;
-  fwd_body<FP, true>(cfg, prm, slot, dv, lds, wg, gridDim.x, acc);
+  fwd_body<FP, true, kF32>(cfg, prm, slot, dv, lds, wg, gridDim.x, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, KP = dv.KP;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -1183,9 +1238,45 @@ __global__ __launch_bounds__(256) void reduce_g_kernel(SolverCfg cfg, const Solv
 
 size_t stats_rows_lds_bytes() { return (size_t)256 * 16 * sizeof(double); }
 
+// fp32 ring ingest: one workgroup per row group, 16 B per thread per step.
+__global__ __launch_bounds__(256) void ring_ingest_f32_kernel(const float* src, const int32_t* ysrc, int64_t first,
+                                                              int64_t step, int64_t n, float* ring, int32_t* yring,
+                                                              int64_t dst, int64_t cap, int FP) {
+  const int64_t q = FP / 4;  // float4 chunks per row
+  const int64_t total = n * q;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / q, c = i - r * q;
+    int64_t d = dst + r;
+    d = d >= cap ? d % cap : d;
+    const int64_t sr = first + r * step;
+    *(f32x4*)(ring + d * FP + c * 4) = *(const f32x4*)(src + sr * FP + c * 4);
+    if (c == 0) yring[d] = ysrc[sr];
+  }
+}
+
+void launch_ring_ingest_f32(const float* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
+                            float* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t total = n * (FP / 4);
+  int64_t grid = (total + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  ring_ingest_f32_kernel<<<(unsigned)grid, 256, 0, s>>>(src, ysrc, src_first, src_step, n, ring, yring, dst_first,
+                                                         cap, FP);
+}
+
 void launch_stats_rows(const SolverCfg& cfg, SolveParams* prm, const SolveDev& dv, int B, int start, int G,
                        hipStream_t s) {
   const size_t lb = stats_rows_lds_bytes();
+  if (cfg.xf32) {
+    switch (cfg.Fp) {
+      case 128: stats_rows_kernel<128, true><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+      case 256: stats_rows_kernel<256, true><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+      case 512: stats_rows_kernel<512, true><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+      case 1024: stats_rows_kernel<1024, true><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
+      default: break;
+    }
+    return;
+  }
   switch (cfg.Fp) {
     case 128: stats_rows_kernel<128><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
     case 256: stats_rows_kernel<256><<<G, 256, lb, s>>>(cfg, prm, dv, B, start); break;
@@ -1202,8 +1293,21 @@ void launch_prep_rows(const SolverCfg& cfg, const SolveParams* prm, const SolveD
   prep_rows_kernel<<<cfg.Fp / kStatW, 256, lb, s>>>(cfg, prm, dv, ctrl, G);
 }
 
+size_t fwdbwd_rows_lds_bytes(int FP, bool f32) { return fwd_lds_bytes(FP) + (f32 ? (size_t)32 * FP * 2 : 0); }
+
 void launch_fwdbwd_rows(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, int slot, const SolveDev& dv,
                         int G, hipStream_t s) {
+  if (cfg.xf32) {
+    const size_t lb = fwdbwd_rows_lds_bytes(cfg.Fp, true);
+    switch (cfg.Fp) {
+      case 128: fwdbwd_rows_kernel<128, true><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+      case 256: fwdbwd_rows_kernel<256, true><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+      case 512: fwdbwd_rows_kernel<512, true><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+      case 1024: fwdbwd_rows_kernel<1024, true><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
+      default: break;
+    }
+    return;
+  }
   const size_t lb = fwd_lds_bytes(cfg.Fp);
   switch (cfg.Fp) {
     case 128: fwdbwd_rows_kernel<128><<<G, 256, lb, s>>>(cfg, prm, ctrl, slot, dv); break;
@@ -1232,6 +1336,9 @@ static void set_slot_attr() {
                             (int)fwd_lds_bytes(FP));
   (void)hipFuncSetAttribute((const void*)fwdbwd_rows_kernel<FP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)fwd_lds_bytes(FP));
+  if constexpr (FP <= 1024)
+    (void)hipFuncSetAttribute((const void*)fwdbwd_rows_kernel<FP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)fwdbwd_rows_lds_bytes(FP, true));
   const int b = (int)bwd_lds_bytes();
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);

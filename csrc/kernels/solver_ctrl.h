@@ -68,6 +68,7 @@ struct SolverCfg {
   int nslots;  // evaluation slots in the graph
   float gd_lr; // step for mode GD
   float tol;   // convergence tolerance (Spark default 1e-6)
+  int xf32 = 0;  // fp32 feature rows (--dtype fp32): row-parallel solver with hi+lo bf16 MFMA operands
 };
 
 // New stream rows a solve ingests into its ring before reading the window

@@ -55,6 +55,43 @@ __device__ __forceinline__ void stage_tile(char* lds, const uint16_t* __restrict
   }
 }
 
+// fp32 rows: stage a 32-row tile split into TWO bf16 images, hi = bf16(x) and
+// lo = bf16(x - hi) (x = hi + lo to ~16 mantissa bits), same layout as stage_tile.
+template <int FP>
+__device__ __forceinline__ void stage_tile_f32(char* lds_hi, char* lds_lo, const float* __restrict__ X, int64_t row0) {
+  constexpr int CPR = FP / 8;           // 8-feature chunks per row
+  constexpr int PER_T = 32 * CPR / 256;  // chunks per thread
+  constexpr int BATCH = PER_T < 8 ? PER_T : 8;
+#pragma unroll
+  for (int b0 = 0; b0 < PER_T; b0 += BATCH) {
+    f32x4 v[BATCH][2];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int q = threadIdx.x + 256 * (b0 + j);
+      const int row = q / CPR, cg = q - row * CPR;
+      const float* src = X + (row0 + row) * FP + cg * 8;
+      v[j][0] = *(const f32x4*)src;
+      v[j][1] = *(const f32x4*)(src + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int q = threadIdx.x + 256 * (b0 + j);
+      const int row = q / CPR, cg = q - row * CPR;
+      u16x8 h, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        unsigned short hh, ll;
+        split_bf16(v[j][e >> 2][e & 3], hh, ll);
+        h[e] = hh;
+        l[e] = ll;
+      }
+      const int o = (cg >> 4) * 8192 + lds_off(row, cg & 15);
+      *(u16x8*)(lds_hi + o) = h;
+      *(u16x8*)(lds_lo + o) = l;
+    }
+  }
+}
+
 template <int FP>
 __device__ __forceinline__ void forward_tile(const char* lds, const uint16_t* __restrict__ wf_hi,
                                              const uint16_t* __restrict__ wf_lo, f32x4& acc0, f32x4& acc1) {
@@ -132,6 +169,23 @@ __device__ __forceinline__ void forward_tile_pre(const char* lds, const WFrag<FP
     acc0 = mfma16x16x32(as_bf16x8(a0), as_bf16x8(wf.l[kk]), acc0);
     acc1 = mfma16x16x32(as_bf16x8(a1), as_bf16x8(wf.h[kk]), acc1);
     acc1 = mfma16x16x32(as_bf16x8(a1), as_bf16x8(wf.l[kk]), acc1);
+  }
+}
+
+// The lo image's share of the forward (x_lo . W_hi; x_lo . W_lo is below the
+// precision of the hi + lo split), accumulated onto forward_tile_pre's result.
+template <int FP>
+__device__ __forceinline__ void forward_tile_pre_lo(const char* lds, const WFrag<FP>& wf, f32x4& acc0, f32x4& acc1) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+    const int cg = (w * WFrag<FP>::KS + kk) * 4 + kq;
+    const char* sub = lds + (cg >> 4) * 8192;
+    const u16x8 a0 = *(const u16x8*)(sub + lds_off(r, cg & 15));
+    const u16x8 a1 = *(const u16x8*)(sub + lds_off(16 + r, cg & 15));
+    acc0 = mfma16x16x32(as_bf16x8(a0), as_bf16x8(wf.h[kk]), acc0);
+    acc1 = mfma16x16x32(as_bf16x8(a1), as_bf16x8(wf.h[kk]), acc1);
   }
 }
 

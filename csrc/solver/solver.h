@@ -23,6 +23,7 @@ namespace psx {
 struct SolverBuffers {
   // caller-owned (torch tensors)
   const uint16_t* X = nullptr;  // ring [cap][Fp] bf16
+  const float* Xf = nullptr;    // ring [cap][Fp] fp32 (cfg.xf32)
   const uint16_t* XT = nullptr; // ring feature-major [Fp][cap] bf16
   const int32_t* y = nullptr;   // ring labels [cap]
   const float* w_old = nullptr; // [P] current model (worker copy)
@@ -49,7 +50,7 @@ class LocalSolver {
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
   int kernels_per_solve() const {  // stats_prep + slots + (tail with finalize | finalize); rows: 3 per slot
-    return rows_mode_ ? 3 + 3 * cfg_.nslots : 2 + 2 * nfast_;
+    return rows_mode_ ? 3 + (dv_.gred ? 3 : 2) * cfg_.nslots : 2 + 2 * nfast_;
   }
   bool rows_mode() const { return rows_mode_; }
   // Debug access to the device controller (synchronous copy).

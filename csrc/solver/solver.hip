@@ -18,7 +18,9 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   if (cfg.hist < 1 || cfg.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
   if (cfg.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
   if (cfg.cap < 32 || cfg.cap % 32 != 0) throw std::invalid_argument("ring capacity must be a positive multiple of 32");
-  rows_mode_ = rows_mode_for(cfg.cap);
+  rows_mode_ = cfg.xf32 || rows_mode_for(cfg.cap);  // fp32 rows: only the row-parallel solver reads them
+  if (cfg.xf32 && (!buf.Xf || cfg.Fp > 1024))
+    throw std::invalid_argument("fp32 rows: need the fp32 ring, at most 1024 padded features");
   if (!rows_mode_ && !buf.XT) throw std::invalid_argument("the solver needs the feature-major ring copy XT");
   const int tiles = cfg.cap / kTileRows + 1;  // window tiles (ring-aligned; a wrapped window may touch one twice)
   nwg_eval_ = tiles < max_eval_wg ? tiles : max_eval_wg;
@@ -68,6 +70,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   prm_ = reinterpret_cast<SolveParams*>(b + o_prm);
   ctrl_ = reinterpret_cast<Ctrl*>(b + o_ctrl);
   dv_.X = buf.X;
+  dv_.Xf = buf.Xf;
   dv_.XT = buf.XT;
   dv_.y = buf.y;
   dv_.w_old = buf.w_old;
@@ -96,7 +99,8 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.prm_count = reinterpret_cast<unsigned*>(b + o_cnt);
   dv_.gpart = rows_mode_ ? reinterpret_cast<float*>(b + o_gpart) : nullptr;
   dv_.spart = rows_mode_ ? reinterpret_cast<double*>(b + o_spart) : nullptr;
-  dv_.gred = rows_mode_ ? reinterpret_cast<float*>(b + o_gred) : nullptr;
+  // small grids sum the partials inside bwd_update (one launch less per slot)
+  dv_.gred = rows_mode_ && nwg_eval_ > kRowsReduceInBwd ? reinterpret_cast<float*>(b + o_gred) : nullptr;
 
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -148,7 +152,7 @@ void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest
     launch_prep_rows(cfg_, prm_, dv_, ctrl_, G, s);
     for (int slot = 0; slot < cfg_.nslots; ++slot) {  // slots after convergence exit at once
       launch_fwdbwd_rows(cfg_, prm_, ctrl_, slot, dv_, G, s);
-      launch_reduce_g(cfg_, prm_, ctrl_, dv_, G, s);
+      if (dv_.gred) launch_reduce_g(cfg_, prm_, ctrl_, dv_, G, s);
       launch_bwd(cfg_, prm_, ctrl_, slot, dv_, G, s);
     }
     launch_finalize(cfg_, ctrl_, dv_, s);

@@ -75,6 +75,8 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--model", default="auto", choices=["auto", "dense", "wide"],
                    help="dense: <= 2048 features (MFMA tiles); wide: sparse rows up to ~1e8 hashed features "
                         "(LIBSVM input); auto: wide for .svm/.libsvm inputs or > 2048 features")
+    g.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                   help="dense model feature rows: bf16 (default) or fp32 (row-parallel solver, hi+lo MFMA operands)")
     g.add_argument("--sigmoid", action="store_true", help="wide model: binary sigmoid (one logit, labels 0/1)")
     g.add_argument("--ring_nz", type=int, default=0, help="wide model: non-zeros per buffered row (0 = from data)")
     g.add_argument("--no_standardize", action="store_true",
@@ -88,6 +90,9 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--epochs", type=int, default=1)
     g.add_argument("--stream_mode", default="schedule", choices=["schedule", "per_iter"])
     g.add_argument("--rows_per_iter", type=int, default=0)
+    g.add_argument("--iter_new_rows", type=int, default=0,
+                   help="a worker iterates only after this many new tuples reached its buffer (0: continuously, "
+                        "the reference's behaviour)")
     g.add_argument("--inprocess", action="store_true",
                    help="run server + all workers in this process on one device (single-GPU / CPU mode)")
     g.add_argument("--async_scheduler", default="auto", choices=["auto", "events", "threads"],
@@ -152,13 +157,13 @@ def server_config(a) -> PSConfig:
         label_col=a.label_col, num_features=a.num_features, num_classes=a.num_classes,
         num_workers=a.num_workers, consistency_model=a.consistency_model,
         producer_time_per_event=a.producer_time_per_event, stream_mode=a.stream_mode,
-        rows_per_iter=a.rows_per_iter, epochs=a.epochs, init=a.init, seed=a.seed, server_lr=a.server_lr,
+        rows_per_iter=a.rows_per_iter, iter_new_rows=a.iter_new_rows, epochs=a.epochs, init=a.init, seed=a.seed, server_lr=a.server_lr,
         solver=solver, max_iters=a.max_iters, max_wallclock_s=a.max_wallclock_s, idle_exit_s=a.idle_exit_s,
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
         perf_log=a.perf_log, async_scheduler=a.async_scheduler,
-        model=a.model, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
+        model=a.model, dtype=a.dtype, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         inject_worker_stop={k: int(v) for k, v in parse_worker_map(a.inject_worker_stop).items()},
         worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)

@@ -106,8 +106,9 @@ class LocalSolveOp:
         key = (ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr())
         if self._bound == key:
             return
-        if ring.X.dtype != torch.bfloat16 or ring.X.shape != (self.cap, self.spec.Fp) or ring.y.dtype != torch.int32:
-            raise ValueError("ring must be bf16 [cap, Fp] with int32 labels")
+        if (ring.X.dtype not in (torch.bfloat16, torch.float32) or ring.X.shape != (self.cap, self.spec.Fp)
+                or ring.y.dtype != torch.int32):
+            raise ValueError("ring must be bf16 / fp32 [cap, Fp] with int32 labels")
         h = _native.hip()
         s, o = self.spec, self.opts
         cfg = h.SolverCfg()
@@ -116,6 +117,7 @@ class LocalSolveOp:
         cfg.mode = 1 if o.mode == "gd" else 0
         cfg.center, cfg.zero_const = int(o.center), int(o.zero_const)
         cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
+        cfg.xf32 = int(ring.X.dtype == torch.float32)
         self._native = h.LocalSolver(
             cfg, ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),

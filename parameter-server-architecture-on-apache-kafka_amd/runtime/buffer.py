@@ -36,15 +36,19 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
     TILE = 32
     MAX_DEFERRED = 256  # kMaxFusedIngest (csrc/kernels/solver_ctrl.h)
 
-    def __init__(self, cap: int, Fp: int, device, defer: bool = False):
+    def __init__(self, cap: int, Fp: int, device, defer: bool = False, dtype: str = "bf16"):
         self.requested = int(cap)
         self.cap = -(-int(cap) // self.TILE) * self.TILE
         self.Fp, self.device = int(Fp), torch.device(device)
-        self.X = torch.zeros(self.cap, self.Fp, dtype=torch.bfloat16, device=self.device)
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError(f"ring dtype must be bf16 or fp32, not {dtype!r}")
+        self.f32 = dtype == "fp32"
+        self.X = torch.zeros(self.cap, self.Fp, dtype=torch.float32 if self.f32 else torch.bfloat16,
+                             device=self.device)
         self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
-        # large windows: the solver streams row-parallel fused passes and needs no
-        # feature-major copy (csrc/kernels/solve_kernels.h, "rows" mode)
-        self.rows_mode = is_gpu(self.device) and bool(_native.hip().solver_rows_mode(self.cap))
+        # large windows (and fp32 rows): the solver streams row-parallel fused passes
+        # and needs no feature-major copy (csrc/kernels/solve_kernels.h, "rows" mode)
+        self.rows_mode = is_gpu(self.device) and (self.f32 or bool(_native.hip().solver_rows_mode(self.cap)))
         self.XT = (torch.zeros(self.Fp, self.cap, dtype=torch.bfloat16, device=self.device)
                    if is_gpu(self.device) and not self.rows_mode else None)
         # defer: the last ingest is not launched on its own but handed to the next
@@ -83,7 +87,13 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
         return p
 
     def _launch(self, src_X, src_y, src_first, src_step, n, dst_first):
-        if is_gpu(self.device):
+        if src_X.dtype != self.X.dtype:
+            raise ValueError(f"ring holds {self.X.dtype} rows, the source has {src_X.dtype}")
+        if is_gpu(self.device) and self.f32:
+            _native.hip().ring_ingest_f32(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
+                                          self.X.data_ptr(), self.y.data_ptr(), int(dst_first), self.cap, self.Fp,
+                                          stream_handle(self.device))
+        elif is_gpu(self.device):
             _native.hip().ring_ingest(src_X.data_ptr(), src_y.data_ptr(), int(src_first), int(src_step), int(n),
                                       self.X.data_ptr(), self.XT.data_ptr() if self.XT is not None else 0,
                                       self.y.data_ptr(), int(dst_first),
@@ -102,7 +112,7 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
         self.flush()
         idx = (torch.arange(X.shape[0]) + int(first)) % self.cap
         idx = idx.to(self.device)
-        self.X[idx] = X.to(self.device, torch.bfloat16)
+        self.X[idx] = X.to(self.device, self.X.dtype)
         self.y[idx] = y.to(self.device, torch.int32)
         self.sync_transposed()
 

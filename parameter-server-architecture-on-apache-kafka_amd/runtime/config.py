@@ -26,6 +26,7 @@ class PSConfig:
     # ~10^8 features; BASELINE.json configs 4/5) or "auto" (wide for LIBSVM
     # inputs / sparse datasets / more than 2048 features)
     model: str = "auto"
+    dtype: str = "bf16"  # feature rows of the dense model: bf16 or fp32 (the reference fits in fp64)
     sigmoid: bool = False  # wide model: one logit + sigmoid (binary labels)
     ring_nz: int = 0  # wide model: non-zeros per ring row (0 = from the data)
     wide_dense_delta: bool = False  # wide model: also produce a dense delta (collective pushes)
@@ -38,6 +39,7 @@ class PSConfig:
     stream_mode: str = "schedule"  # or "per_iter"
     rows_per_iter: int = 0
     epochs: int = 1
+    iter_new_rows: int = 0  # a worker iterates once this many new tuples arrived (0: continuously)
     # buffer
     min_buffer_size: int = 128
     max_buffer_size: int = 1024

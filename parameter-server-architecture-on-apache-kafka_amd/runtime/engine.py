@@ -50,6 +50,8 @@ def load_datasets(cfg: PSConfig, train=None, test=None):
     """Datasets + model spec: dense CSV/binary rows -> ModelSpec, sparse
     (LIBSVM / SparseDataset) rows -> WideSpec."""
     if _wants_wide(cfg, train):
+        if cfg.dtype != "bf16":
+            raise ValueError("--dtype fp32 applies to the dense model (the wide model's values are bf16)")
         if train is None:
             train = data_mod.load_libsvm(cfg.train_path, num_features=cfg.num_features)
         if test is None and cfg.test_path:
@@ -72,10 +74,11 @@ def load_datasets(cfg: PSConfig, train=None, test=None):
         return WideSpec(F, K), train, test
     if train is None:
         train = data_mod.load_any(cfg.train_path, header=cfg.header, label_col=cfg.label_col,
-                                  num_features=cfg.num_features)
+                                  num_features=cfg.num_features, dtype=cfg.dtype)
     if test is None and cfg.test_path:
         test = data_mod.load_any(cfg.test_path, header=cfg.header, label_col=cfg.label_col,
                                  num_features=train.num_features)
+    train = train.as_dtype(cfg.dtype)  # the training rows in the run's feature dtype (test rows: bf16)
     if cfg.num_classes is not None:
         K = int(cfg.num_classes)
     else:

@@ -81,7 +81,8 @@ class WorkerRole:
             nz = cfg.ring_nz or nz_capacity(train.max_nnz)
             self.ring = SparseRing(cfg.max_buffer_size, nz, self.device)
         else:
-            self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device, defer=cfg.solver.fused_ingest)
+            self.ring = DeviceRing(cfg.max_buffer_size, spec.Fp, self.device, defer=cfg.solver.fused_ingest,
+                                   dtype=cfg.dtype)
         self.window = _native.host.SlidingWindow(cfg.min_buffer_size, cfg.max_buffer_size,
                                                  cfg.buffer_size_coefficient, 500, self.ring.cap)
         self.source = StreamSource(train, k, cfg.num_workers, self.ring, self.window,
@@ -99,6 +100,7 @@ class WorkerRole:
         self.pair = None  # EvalPair with the colocated server (BSP)
         self.vc = 0  # version of the weights currently held
         self.iters = 0
+        self._seen_at_solve = 0  # tuples seen when the last solve started (--iter_new_rows)
         self.delay_s = float(cfg.inject_worker_delay_ms.get(k, 0.0)) / 1000.0
         crash = cfg.inject_worker_crash.get(k)
         self.crash_at = int(crash) if crash is not None else None
@@ -111,7 +113,13 @@ class WorkerRole:
         return self.source.poll()
 
     def ready(self) -> bool:
-        return self.window.size > 0
+        """Data to train on; with --iter_new_rows K, only once K new tuples arrived
+        since the last solve (a stream-driven cadence: re-solving an unchanged
+        window only re-fits the same rows)."""
+        if self.window.size <= 0:
+            return False
+        K = self.cfg.iter_new_rows
+        return K <= 0 or self.tuples_seen - self._seen_at_solve >= K or self.source.exhausted
 
     def compute(self, log=None) -> torch.Tensor:
         """One local solve on the current window; returns the delta tensor.
@@ -133,6 +141,7 @@ class WorkerRole:
         if self.delay_s > 0:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)
+        self._seen_at_solve = self.tuples_seen
         if self.pair is not None:
             self.pair.flush_worker()  # a deferred row reads the model this solve overwrites
         self.side.fence()  # the last evaluation read the solver outputs this solve overwrites

@@ -26,7 +26,7 @@ _MAGIC = b"PSXB0001"
 
 @dataclass
 class Dataset:
-    X: torch.Tensor  # [N, Fp] bfloat16 (padded columns are zero)
+    X: torch.Tensor  # [N, Fp] bfloat16, or float32 for --dtype fp32 (padded columns are zero)
     y: torch.Tensor  # [N] int32
     num_features: int  # real feature count F
     names: list | None = None
@@ -45,6 +45,13 @@ class Dataset:
     def float_features(self) -> torch.Tensor:
         return self.X[:, : self.num_features].float()
 
+    def as_dtype(self, dtype: str) -> "Dataset":
+        """Rows as "bf16" or "fp32" (the --dtype of the run)."""
+        t = torch.float32 if dtype == "fp32" else torch.bfloat16
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError(f"dtype must be bf16 or fp32, not {dtype!r}")
+        return self if self.X.dtype == t else Dataset(self.X.to(t), self.y, self.num_features, self.names)
+
 
 def _header_mode(header) -> int:
     if header in (None, "auto"):
@@ -56,8 +63,9 @@ def _header_mode(header) -> int:
     raise ValueError(f"bad header mode {header!r}")
 
 
-def load_csv(path: str, header="auto", label_col: int = -1, num_features: int | None = None, threads: int = 0) -> Dataset:
-    """Parse a dense CSV with the native multithreaded parser into bf16 rows.
+def load_csv(path: str, header="auto", label_col: int = -1, num_features: int | None = None, threads: int = 0,
+             dtype: str = "bf16") -> Dataset:
+    """Parse a dense CSV with the native multithreaded parser into bf16 (or fp32) rows.
 
     The last column (or ``label_col``) is the integer label; all other columns
     are features.  Width is inferred from the file (reference hard-codes 1024,
@@ -70,8 +78,9 @@ def load_csv(path: str, header="auto", label_col: int = -1, num_features: int | 
     if num_features is not None and num_features != F:
         raise ValueError(f"{path}: has {F} feature columns, expected {num_features}")
     Fp = padded_width(F)
-    _, xb, y = _native.host.csv_load(path, info, label_col, Fp, False, True, threads)
-    X = torch.from_numpy(xb.view(np.int16)).view(torch.bfloat16)
+    f32 = dtype == "fp32"
+    xf, xb, y = _native.host.csv_load(path, info, label_col, Fp, f32, not f32, threads)
+    X = torch.from_numpy(xf) if f32 else torch.from_numpy(xb.view(np.int16)).view(torch.bfloat16)
     return Dataset(X, torch.from_numpy(y), F, list(info.names) if info.header else None)
 
 
@@ -100,12 +109,12 @@ def is_libsvm_path(path: str | None) -> bool:
     return bool(path) and path.endswith((".svm", ".libsvm", ".svmlight"))
 
 
-def load_any(path: str, **kw) -> Dataset:
+def load_any(path: str, dtype: str = "bf16", **kw) -> Dataset:
     with open(path, "rb") as f:
         magic = f.read(8)
-    if magic == _MAGIC:
-        return load_bin(path)
-    return load_csv(path, **kw)
+    if magic == _MAGIC:  # the binary cache stores bf16 rows
+        return load_bin(path).as_dtype(dtype)
+    return load_csv(path, dtype=dtype, **kw)
 
 
 # ---------------------------------------------------------------------------
@@ -125,6 +134,7 @@ def synth_finefood(
     vocab: int = 20000,
     words_per_row: float = 45.0,
     class_vocab: int = 400,
+    dtype: str = "bf16",
 ) -> Dataset:
     """Fine-food-reviews-shaped synthetic rows (labels 1..5, hashed L2-normalised text)."""
     rng = np.random.default_rng(seed)
@@ -158,7 +168,7 @@ def synth_finefood(
     Fp = padded_width(num_features)
     Xp = np.zeros((rows, Fp), dtype=np.float32)
     Xp[:, :num_features] = X
-    Xb = torch.from_numpy(Xp).to(torch.bfloat16)
+    Xb = torch.from_numpy(Xp) if dtype == "fp32" else torch.from_numpy(Xp).to(torch.bfloat16)
     return Dataset(Xb, torch.from_numpy(y.astype(np.int32)), num_features, [str(i) for i in range(num_features)] + ["Score"])
 
 

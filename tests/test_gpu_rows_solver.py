@@ -116,3 +116,57 @@ def test_rows_mode_engine_large_buffer(cuda):
     accs = [r[3] for r in eng.log.book.server]
     assert accs[-1] > 0.35, accs
     assert _native.hip_loaded_path() is not None
+
+
+@pytest.mark.parametrize("B,start,F", [(1024, 1000, 1024), (700, 3, 300), (20000, 77, 1024)])
+def test_fp32_rows_match_reference(cuda, B, start, F):
+    """--dtype fp32: fp32 ring rows (hi + lo bf16 MFMA operands) against the float64
+    oracle on the SAME fp32 rows, tighter than the bf16 path's tolerance."""
+    spec = ModelSpec(F, 6)
+    ds = synth_finefood(B, F, seed=21, dtype="fp32")
+    assert ds.X.dtype == torch.float32
+    cap = max(1024, B)
+    ring = DeviceRing(cap, spec.Fp, cuda, dtype="fp32")
+    assert ring.rows_mode and ring.X.dtype == torch.float32
+    ring.place(ds.X[:B], ds.y[:B], start)
+    opts = SolverOptions(iters=2)
+    op = LocalSolveOp(spec, ring.cap, cuda, opts)
+    w_old = _rand_w(spec, 8)
+    op.run(ring, B, start, w_old.to(cuda))
+    torch.cuda.synchronize()
+    assert op._native.rows_mode
+    _check(op, ds, spec, w_old, opts, tol=5e-3)
+
+
+def test_fp32_rows_differ_from_bf16_rows(cuda):
+    """The fp32 path really consumes the fp32 bits: on rows that bf16 cannot
+    represent its result is closer to the fp32 oracle than the bf16 path's."""
+    spec = ModelSpec(1024, 6)
+    ds32 = synth_finefood(2048, seed=22, dtype="fp32")
+    ds16 = ds32.as_dtype("bf16")
+    w_old = _rand_w(spec, 9)
+    opts = SolverOptions(iters=2)
+    ref = local_solve_reference(ds32.float_features(), ds32.y.long(), spec.coef(w_old), spec.intercept(w_old),
+                                iters=2, hist=opts.hist, ls_max=opts.ls_max, nslots=opts.nslots)
+    errs = {}
+    for name, ds in (("fp32", ds32), ("bf16", ds16)):
+        ring = DeviceRing(2048, spec.Fp, cuda, dtype=name)
+        ring.place(ds.X, ds.y, 0)
+        op = LocalSolveOp(spec, ring.cap, cuda, opts)
+        op.run(ring, 2048, 0, w_old.to(cuda))
+        torch.cuda.synchronize()
+        errs[name] = (spec.coef(op.delta.cpu()) - ref.delta_coef).abs().max().item()
+    assert errs["fp32"] < 0.5 * errs["bf16"], errs
+
+
+def test_fp32_engine_bench_path(cuda):
+    from psx.runtime.config import PSConfig
+    from psx.runtime.engine import LocalEngine
+
+    train, test = synth_finefood(20000, seed=0, dtype="fp32"), synth_finefood(1000, seed=1)
+    cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=128, epochs=100, max_iters=30, dtype="fp32")
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    out = eng.run()
+    assert out["rounds"] == 30 and eng.workers[0].ring.X.dtype == torch.float32
+    assert eng.log.book.server[-1][3] > 0.3

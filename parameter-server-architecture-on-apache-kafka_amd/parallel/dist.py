@@ -404,7 +404,10 @@ class DistEngine:
                     mine = wfull[lo:lo + shard]
                     if comm is not None:
                         comm.reduce_scatter(myd, pad)
-                        mine.add_(myd, alpha=lr)
+                        # this rank's key range of the master weights (KeyRange.java:11-49):
+                        # w[lo:lo+shard] += lr * sum(delta) on the psx update kernel
+                        _native.hip().axpy(mine.data_ptr(), myd.data_ptr(), float(lr), int(shard),
+                                           torch.cuda.current_stream(self.device).cuda_stream)
                         comm.all_gather(wfull, mine)  # in place: srv.w is a view of wfull
                     else:
                         dist.reduce_scatter_tensor(myd, pad, op=dist.ReduceOp.SUM)

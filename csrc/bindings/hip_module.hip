@@ -407,6 +407,16 @@ PYBIND11_MODULE(_psx_hip, m) {
                              P<const float>(dloc), lr, umax, S(stream));
     hip_check(hipGetLastError(), "wide_apply_sparse launch");
   });
+  m.def("log_append", [](uintptr_t uniq, uintptr_t dloc, int U, int64_t F, int KP, uintptr_t lids, uintptr_t lvals,
+                         int64_t pos, int64_t cap, uintptr_t stream) {
+    launch_log_append(P<const int32_t>(uniq), P<const float>(dloc), U, F, KP, P<int32_t>(lids), P<float>(lvals), pos,
+                      cap, S(stream));
+    hip_check(hipGetLastError(), "log_append launch");
+  });
+  m.def("log_apply", [](uintptr_t w, uintptr_t ids, uintptr_t vals, int64_t n, int KP, float lr, uintptr_t stream) {
+    launch_log_apply(P<float>(w), P<const int32_t>(ids), P<const float>(vals), n, KP, lr, S(stream));
+    hip_check(hipGetLastError(), "log_apply launch");
+  });
   m.def("axpy", [](uintptr_t w, uintptr_t x, float a, int64_t n, uintptr_t stream) {
     launch_axpy(P<float>(w), P<const float>(x), a, n, S(stream));
     hip_check(hipGetLastError(), "axpy launch");
@@ -423,10 +433,12 @@ PYBIND11_MODULE(_psx_hip, m) {
            py::arg("nworkers"), py::arg("out_f32"), py::arg("out_i32"), py::arg("inbox"))
       .def("released", &LocalP2P::released);
   py::class_<LocalFeeder>(m, "LocalFeeder")
-      .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double, const std::vector<int64_t>&>(),
+      .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double, const std::vector<int64_t>&,
+                    const std::vector<uintptr_t>&>(),
            py::arg("api"), py::arg("ctrl"), py::arg("p2p"), py::arg("nworkers"), py::arg("iters"),
            py::arg("token_n") = 0, py::arg("timeout_s") = 60.0, py::arg("vc0") = std::vector<int64_t>{},
-           py::keep_alive<1, 4>())
+           py::arg("replies") = std::vector<uintptr_t>{}, py::keep_alive<1, 4>())
+      .def_property_readonly("sparse_pulls", &LocalFeeder::sparse_pulls)
       .def("start", &LocalFeeder::start)
       .def("join", &LocalFeeder::join, py::call_guard<py::gil_scoped_release>());
   py::class_<AsyncServer>(m, "AsyncServer")
@@ -468,6 +480,12 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.ctrl = U("ctrl");
              c.sink = U("sink");
              c.worker_timeout_s = d.contains("worker_timeout_s") ? d["worker_timeout_s"].cast<double>() : 600.0;
+             c.sparse_pull = (int)I("sparse_pull", 0);
+             c.lids = P<int32_t>(U("lids"));
+             c.lvals = P<float>(U("lvals"));
+             c.logcap = I("logcap", 0);
+             c.dense_every = (int)I("dense_every", 64);
+             if (d.contains("replies")) c.replies = d["replies"].cast<std::vector<uintptr_t>>();
              if (c.model == kAsyncDense || c.sink) prepare_kernels();
              return std::make_unique<AsyncServer>(&comm, c, S(stream));
            }),
@@ -489,7 +507,10 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property("updates", &AsyncServer::updates, &AsyncServer::set_updates)
       .def_property_readonly("tokens", &AsyncServer::tokens)
       .def_property_readonly("host_us_per_update", &AsyncServer::host_us_per_update)
-      .def_property_readonly("failed", &AsyncServer::failed);
+      .def_property_readonly("failed", &AsyncServer::failed)
+      .def_property_readonly("sparse_pulls", &AsyncServer::sparse_pulls)
+      .def_property_readonly("dense_pulls", &AsyncServer::dense_pulls)
+      .def_property_readonly("pull_floats", &AsyncServer::pull_floats);
   m.attr("ASYNC_DONE") = (int)kAsyncDone;
   m.attr("ASYNC_ERROR_TOKEN") = (int)kAsyncErrorToken;
   m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;

@@ -142,6 +142,11 @@ void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const i
 // l < *U (device count) or U_host when U_dev is null, and the intercepts.
 void launch_wide_apply_sparse(float* w, int64_t F, int KP, const unsigned* U_dev, int U_host, const int32_t* uniq,
                               const float* dloc, float lr, int umax, hipStream_t s);
+// Sparse pull: append a push (uniq[U], dloc[(U+1)*KP]) to the server's ring log
+// at id position pos (mod cap); a worker applies n received log ids / values.
+void launch_log_append(const int32_t* uniq, const float* dloc, int U, int64_t F, int KP, int32_t* lids, float* lvals,
+                       int64_t pos, int64_t cap, hipStream_t s);
+void launch_log_apply(float* w, const int32_t* ids, const float* vals, int64_t n, int KP, float lr, hipStream_t s);
 // Dense: w += lr * delta over n floats.
 void launch_axpy(float* w, const float* delta, float lr, int64_t n, hipStream_t s);
 

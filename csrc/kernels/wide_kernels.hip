@@ -1131,6 +1131,48 @@ __global__ __launch_bounds__(256) void axpy_kernel(float* __restrict__ w, const 
   for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) w[i] += a * x[i];
 }
 
+// ---------------------------------------------------------------------------
+// Sparse pull (asynchronous wide model): the server keeps the applied deltas in
+// a ring log -- entry = ids [F (the intercepts' pseudo-feature), uniq[0..U)] and
+// the push payload dloc [(U+1) * KP] unchanged, value block l <-> id l -- and a
+// released worker receives the log entries since its previous pull instead of
+// the dense weight vector (KeyRange-addressed payloads, BaseMessage.java:24-27).
+__global__ __launch_bounds__(256) void log_append_kernel(const int32_t* __restrict__ uniq,
+                                                         const float* __restrict__ dloc, int U, int64_t F, int KP,
+                                                         int32_t* lids, float* lvals, int64_t pos, int64_t cap) {
+  const int64_t nid = (int64_t)U + 1, nv = nid * KP;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < nv; p += (int64_t)gridDim.x * 256) {
+    const int64_t l = p / KP, k = p - l * KP;
+    const int64_t slot = (pos + l) % cap;
+    lvals[slot * KP + k] = dloc[p];
+    if (k == 0) lids[slot] = l == 0 ? (int32_t)F : uniq[l - 1];
+  }
+}
+
+void launch_log_append(const int32_t* uniq, const float* dloc, int U, int64_t F, int KP, int32_t* lids, float* lvals,
+                       int64_t pos, int64_t cap, hipStream_t s) {
+  const int64_t nv = ((int64_t)U + 1) * KP;
+  log_append_kernel<<<grid_for(nv, 2048), 256, 0, s>>>(uniq, dloc, U, F, KP, lids, lvals, pos, cap);
+}
+
+// w[ids[l] * KP + k] += lr * vals[l * KP + k]: ids repeat across log entries, so
+// the adds are atomic (hardware fp32 atomics; the order of equal-id adds varies).
+__global__ __launch_bounds__(256) void log_apply_kernel(float* w, const int32_t* __restrict__ ids,
+                                                        const float* __restrict__ vals, int64_t n, int KP, float lr) {
+  const int64_t nv = n * KP;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < nv; p += (int64_t)gridDim.x * 256) {
+    const float v = vals[p];
+    if (v == 0.f) continue;
+    const int64_t l = p / KP, k = p - l * KP;
+    atomicAdd(w + (int64_t)ids[l] * KP + k, lr * v);
+  }
+}
+
+void launch_log_apply(float* w, const int32_t* ids, const float* vals, int64_t n, int KP, float lr, hipStream_t s) {
+  if (n <= 0) return;
+  log_apply_kernel<<<grid_for(n * KP, 4096), 256, 0, s>>>(w, ids, vals, n, KP, lr);
+}
+
 void launch_axpy(float* w, const float* delta, float lr, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   axpy_kernel<<<grid_for(n / 4 + 1, 4096), 256, 0, s>>>(w, delta, lr, n);

@@ -76,10 +76,14 @@ class LocalP2P : public P2P {
   int size() const override { return n_ + 1; }
   void send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) override;
   void recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) override;
+  void group_start() override;
+  void group_end() override;  // one release per peer that got sends in the group
   int64_t released(int k) const;
 
  private:
   int n_;
+  bool in_group_ = false;
+  std::vector<int> group_peers_;
   std::vector<uintptr_t> out_f32_, out_i32_, inbox_;
   std::unique_ptr<std::atomic<int64_t>[]> released_;
 };
@@ -115,6 +119,17 @@ struct AsyncServerCfg {
   // host runtime handles (capi.h); sink 0: no server rows
   uintptr_t api = 0, tracker = 0, ctrl = 0, sink = 0;
   double worker_timeout_s = 600.0;
+  // sparse pull (kAsyncWideSparse): the applied pushes go into a ring log
+  // (lids[logcap] ids, lvals[logcap * KP] values); a released worker receives
+  // the entries since its previous pull (sizes on its reply queue) unless the
+  // dense vector is cheaper, it fell behind the log, or dense_every sparse pulls
+  // passed (a dense refresh bounds the atomics' rounding drift)
+  int sparse_pull = 0;
+  int32_t* lids = nullptr;
+  float* lvals = nullptr;
+  int64_t logcap = 0;
+  std::vector<uintptr_t> replies;  // per-worker reply CtrlQueue handles
+  int dense_every = 64;
 };
 
 enum AsyncCode : int {
@@ -165,6 +180,15 @@ class AsyncServer {
   std::vector<double> busy_since_;  // < 0: not busy (weights not sent / delta back)
   std::vector<int> rel_k_;
   std::vector<int64_t> rel_v_;
+  int64_t log_pos_ = 0;                 // ids appended to the log so far
+  std::vector<int64_t> last_pos_;       // log position of each worker's last pull (-1: dense next)
+  std::vector<int> since_dense_;        // sparse pulls since the worker's last dense pull
+  int64_t sparse_pulls_ = 0, dense_pulls_ = 0, pull_floats_ = 0;
+
+ public:
+  int64_t sparse_pulls() const { return sparse_pulls_; }
+  int64_t dense_pulls() const { return dense_pulls_; }
+  int64_t pull_floats() const { return pull_floats_; }  // values + ids moved by pulls
   int64_t updates_ = 0, tokens_ = 0, updates_run_ = 0;
   double host_ns_ = 0.0;
 };
@@ -179,7 +203,8 @@ class LocalFeeder {
   // vc0[k]: worker k's clock at the start (the tracker's); the release counter's
   // value at construction is the baseline (construct before the server's begin())
   LocalFeeder(uintptr_t api, uintptr_t ctrl, LocalP2P* p2p, int nworkers, int64_t iters, int64_t token_n,
-              double timeout_s, const std::vector<int64_t>& vc0);
+              double timeout_s, const std::vector<int64_t>& vc0, const std::vector<uintptr_t>& replies = {});
+  int64_t sparse_pulls() const { return sparse_.load(); }
   ~LocalFeeder();
   void start();
   // true: every thread pushed all its tokens; false: a thread timed out waiting
@@ -194,6 +219,8 @@ class LocalFeeder {
   int64_t iters_, token_n_;
   double timeout_s_;
   std::vector<int64_t> vc0_, base_;
+  std::vector<uintptr_t> replies_;  // sparse pull: each release comes with a reply token
+  std::atomic<int64_t> sparse_{0};
   std::vector<std::thread> th_;
   std::atomic<int> failed_{0};
 };

@@ -1,6 +1,7 @@
 // Native asynchronous server loop (see async_server.h).
 #include "async_server.h"
 
+#include <algorithm>
 #include <chrono>
 #include <stdexcept>
 #include <string>
@@ -39,10 +40,26 @@ LocalP2P::LocalP2P(int nworkers, const std::vector<uintptr_t>& out_f32, const st
 }
 
 void LocalP2P::send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) {
-  if (peer < 1 || peer > n_ || dtype != RcclComm::kF32) throw std::invalid_argument("LocalP2P::send: weights only");
+  if (peer < 1 || peer > n_ || dtype == RcclComm::kU8) throw std::invalid_argument("LocalP2P::send: peer / dtype");
+  // the inbox is sized for the dense weights: every pull piece fits (stand-in
+  // workers read only the release counter); one release per group
   hip_check(hipMemcpyAsync(reinterpret_cast<void*>(inbox_[peer - 1]), buf, count * 4, hipMemcpyDeviceToDevice, s),
             "LocalP2P send copy");
-  released_[peer - 1].fetch_add(1, std::memory_order_release);
+  if (!in_group_) released_[peer - 1].fetch_add(1, std::memory_order_release);
+  else group_peers_.push_back(peer - 1);
+}
+
+void LocalP2P::group_start() {
+  in_group_ = true;
+  group_peers_.clear();
+}
+
+void LocalP2P::group_end() {
+  in_group_ = false;
+  std::sort(group_peers_.begin(), group_peers_.end());
+  group_peers_.erase(std::unique(group_peers_.begin(), group_peers_.end()), group_peers_.end());
+  for (int k : group_peers_) released_[k].fetch_add(1, std::memory_order_release);
+  group_peers_.clear();
 }
 
 void LocalP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) {
@@ -56,9 +73,11 @@ void LocalP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s)
 int64_t LocalP2P::released(int k) const { return released_[k].load(std::memory_order_acquire); }
 
 LocalFeeder::LocalFeeder(uintptr_t api, uintptr_t ctrl, LocalP2P* p2p, int nworkers, int64_t iters, int64_t token_n,
-                         double timeout_s, const std::vector<int64_t>& vc0)
+                         double timeout_s, const std::vector<int64_t>& vc0, const std::vector<uintptr_t>& replies)
     : api_(reinterpret_cast<const HostApi*>(api)), ctrl_(ctrl), p2p_(p2p), n_(nworkers), iters_(iters),
-      token_n_(token_n), timeout_s_(timeout_s), vc0_(vc0), base_(nworkers, 0) {
+      token_n_(token_n), timeout_s_(timeout_s), vc0_(vc0), base_(nworkers, 0), replies_(replies) {
+  if (!replies_.empty() && (int)replies_.size() != nworkers)
+    throw std::invalid_argument("LocalFeeder: one reply queue per worker");
   if (!api_ || api_->version != kHostApiVersion || !ctrl || !p2p || nworkers < 1 || iters < 1)
     throw std::invalid_argument("LocalFeeder: bad arguments");
   if (vc0_.empty()) vc0_.assign(nworkers, 0);
@@ -89,6 +108,14 @@ void LocalFeeder::run(int k) {
         return;
       }
       std::this_thread::yield();
+    }
+    if (!replies_.empty()) {  // sparse pull: consume the release's reply token
+      CtrlToken r{};
+      if (api_->ctrl_pop((void*)replies_[k], &r, timeout_s_) != 1) {
+        failed_.fetch_add(1);
+        return;
+      }
+      if (r.kind == 1) sparse_.fetch_add(1);
     }
     CtrlToken t{};
     t.worker = k;
@@ -122,6 +149,13 @@ AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t strea
   finished_.assign(cfg.nworkers, 0);
   failed_.assign(cfg.nworkers, 0);
   dead_.assign(cfg.nworkers, 0);
+  last_pos_.assign(cfg.nworkers, -1);
+  since_dense_.assign(cfg.nworkers, 0);
+  if (cfg.sparse_pull) {
+    if (cfg.model != kAsyncWideSparse) throw std::invalid_argument("AsyncServer: sparse pull needs sparse pushes");
+    if (!cfg.lids || !cfg.lvals || cfg.logcap < 1 || (int)cfg.replies.size() != cfg.nworkers)
+      throw std::invalid_argument("AsyncServer: sparse pull needs the ring log and one reply queue per worker");
+  }
   busy_since_.assign(cfg.nworkers, -1.0);
   rel_k_.resize(cfg.nworkers + 1);
   rel_v_.resize(cfg.nworkers + 1);
@@ -147,22 +181,63 @@ std::vector<int> AsyncServer::failed() const {
 }
 
 void AsyncServer::send_weights(const int* ks, const int64_t* vs, int n) {
-  (void)vs;
   bool any = false;
   for (int i = 0; i < n; ++i) any |= !finished_[ks[i]];
   if (!any) return;
   const double t = now_s();
+  const int KP = cfg_.KP;
   comm_->group_start();
   for (int i = 0; i < n; ++i) {
     const int j = ks[i];
     if (finished_[j]) continue;
-    comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
     busy_since_[j] = t;
+    if (!cfg_.sparse_pull) {
+      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
+      pull_floats_ += cfg_.P;
+      ++dense_pulls_;
+      continue;
+    }
+    // the entries [last_pos_[j], log_pos_) of the ring log, or the dense vector
+    const int64_t m = last_pos_[j] < 0 ? -1 : log_pos_ - last_pos_[j];
+    const bool sparse = m >= 0 && m <= cfg_.logcap && m * (KP + 1) * 2 < cfg_.P && since_dense_[j] < cfg_.dense_every;
+    CtrlToken r{};
+    r.worker = j;
+    r.vc = vs[i];
+    if (sparse) {
+      const int64_t start = last_pos_[j] % cfg_.logcap;
+      const int64_t len1 = m < cfg_.logcap - start ? m : cfg_.logcap - start, len2 = m - len1;
+      r.kind = 1;
+      r.n = m;
+      r.aux = len1;
+      if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
+        throw std::runtime_error("AsyncServer: reply queue of worker " + std::to_string(j) + " full");
+      if (len1) {
+        comm_->send(cfg_.lids + start, (size_t)len1, RcclComm::kI32, j + 1, stream_);
+        comm_->send(cfg_.lvals + start * KP, (size_t)(len1 * KP), RcclComm::kF32, j + 1, stream_);
+      }
+      if (len2) {
+        comm_->send(cfg_.lids, (size_t)len2, RcclComm::kI32, j + 1, stream_);
+        comm_->send(cfg_.lvals, (size_t)(len2 * KP), RcclComm::kF32, j + 1, stream_);
+      }
+      ++since_dense_[j];
+      ++sparse_pulls_;
+      pull_floats_ += m * (KP + 1);
+    } else {
+      r.kind = 0;
+      if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
+        throw std::runtime_error("AsyncServer: reply queue of worker " + std::to_string(j) + " full");
+      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
+      since_dense_[j] = 0;
+      ++dense_pulls_;
+      pull_floats_ += cfg_.P;
+    }
+    last_pos_[j] = log_pos_;
   }
   comm_->group_end();
 }
 
 void AsyncServer::begin() {
+  std::fill(last_pos_.begin(), last_pos_.end(), -1);  // every run starts with a dense pull
   std::fill(finished_.begin(), finished_.end(), 0);
   std::fill(failed_.begin(), failed_.end(), 0);
   std::fill(busy_since_.begin(), busy_since_.end(), -1.0);
@@ -198,6 +273,12 @@ void AsyncServer::apply_and_log(const CtrlToken& t) {
     comm_->recv(cfg_.dbuf, (size_t)(cfg_.KP + U * cfg_.KP), RcclComm::kF32, peer, stream_);
     launch_wide_apply_sparse(cfg_.w, cfg_.Fw, cfg_.KP, nullptr, (int)U, cfg_.ubuf, cfg_.dbuf, cfg_.lr, cfg_.umax,
                              stream_);
+    if (cfg_.sparse_pull) {  // stream-ordered after every send that reads the slots it overwrites
+      if (U + 1 > cfg_.logcap) throw std::runtime_error("AsyncServer: push larger than the pull log");
+      launch_log_append(cfg_.ubuf, cfg_.dbuf, (int)U, cfg_.Fw, cfg_.KP, cfg_.lids, cfg_.lvals,
+                        log_pos_ % cfg_.logcap, cfg_.logcap, stream_);
+      log_pos_ += U + 1;
+    }
   } else {
     comm_->recv(cfg_.buf, (size_t)cfg_.P, RcclComm::kF32, peer, stream_);
     if (cfg_.model == kAsyncDense)

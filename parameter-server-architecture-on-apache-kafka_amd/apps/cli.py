@@ -83,6 +83,8 @@ def server_parser() -> argparse.ArgumentParser:
                    help="wide model: skip Spark's 1/std feature scaling over the buffer")
     g.add_argument("--dense_push", action="store_true",
                    help="wide model, -c != 0: push the dense delta instead of (feature ids, values)")
+    g.add_argument("--dense_pull", action="store_true",
+                   help="wide model, -c != 0: pull the dense weights instead of the deltas applied since the last pull")
     g = ap.add_argument_group("run control")
     g.add_argument("--max_iters", type=int, default=0, help="iterations per worker (0 = until data exhausted)")
     g.add_argument("--max_wallclock_s", type=float, default=0.0)
@@ -163,7 +165,7 @@ def server_config(a) -> PSConfig:
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
         perf_log=a.perf_log, async_scheduler=a.async_scheduler,
-        model=a.model, dtype=a.dtype, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push,
+        model=a.model, dtype=a.dtype, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push, sparse_pull=not a.dense_pull,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         inject_worker_stop={k: int(v) for k, v in parse_worker_map(a.inject_worker_stop).items()},
         worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)

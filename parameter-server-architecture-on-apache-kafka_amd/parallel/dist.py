@@ -166,6 +166,65 @@ class StopVote:
             self._ring = 0
 
 
+class PullLog:
+    """Server-side ring log of the applied sparse pushes (the Python twin of the
+    native loop's, csrc/runtime/async_server.hip): entry = ids [F (the intercepts'
+    pseudo-feature), uniq...] + the push payload dloc [(U+1) * KP] unchanged.  A
+    released worker receives the entries since its previous pull -- a
+    KeyRange-addressed payload (BaseMessage.java:24-27) instead of the dense
+    weights -- unless the dense vector is cheaper, the worker fell behind the
+    log, or ``dense_every`` sparse pulls passed."""
+
+    def __init__(self, spec, cap_ids: int, num_workers: int, device, dense_every: int = 64):
+        self.spec, self.cap, self.dense_every = spec, int(cap_ids), int(dense_every)
+        KP = spec.KP
+        self.ids = torch.zeros(self.cap, dtype=torch.int32, device=device)
+        self.vals = torch.zeros(self.cap * KP, dtype=torch.float32, device=device)
+        self.pos = 0
+        self.last = [-1] * num_workers
+        self.since = [0] * num_workers
+        self.sparse = self.dense = 0
+
+    def append(self, ubuf: torch.Tensor, dbuf: torch.Tensor, U: int):
+        KP, dev = self.spec.KP, self.ids.device
+        if U + 1 > self.cap:
+            raise ValueError("push larger than the pull log")
+        slots = (torch.arange(U + 1, device=dev) + self.pos) % self.cap
+        ids = torch.empty(U + 1, dtype=torch.int32, device=dev)
+        ids[0] = self.spec.F
+        ids[1:] = ubuf[:U]
+        self.ids[slots] = ids
+        self.vals.view(self.cap, KP)[slots] = dbuf[: (U + 1) * KP].view(U + 1, KP)
+        self.pos += U + 1
+
+    def plan(self, j: int):
+        """(kind, m, len1) of worker j's next pull, and the sends: [(tensor slice), ...]."""
+        KP, P = self.spec.KP, self.spec.P
+        m = -1 if self.last[j] < 0 else self.pos - self.last[j]
+        sparse = 0 <= m <= self.cap and m * (KP + 1) * 2 < P and self.since[j] < self.dense_every
+        self.last[j] = self.pos
+        if not sparse:
+            self.since[j] = 0
+            self.dense += 1
+            return 0, 0, 0, None
+        start = (self.pos - m) % self.cap
+        len1 = min(m, self.cap - start)
+        len2 = m - len1
+        parts = []
+        if len1:
+            parts += [self.ids[start:start + len1], self.vals[start * KP:(start + len1) * KP]]
+        if len2:
+            parts += [self.ids[:len2], self.vals[: len2 * KP]]
+        self.since[j] += 1
+        self.sparse += 1
+        return 1, m, len1, parts
+
+
+def pull_log_capacity(umax: int) -> int:
+    """Ids the pull log keeps: ~16 pushes of the largest window subspace."""
+    return 16 * (int(umax) + 1)
+
+
 class DistEngine:
     def __init__(self, cfg: PSConfig, rank: int, world: int, device, train=None, test=None):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, torch.device(device)
@@ -181,6 +240,8 @@ class DistEngine:
         # wide model: collectives and dense p2p pushes need the dense delta;
         # SSP/ASP with sparse_push send (feature ids, values) instead
         self.sparse_push = self.wide and self.async_mode and cfg.sparse_push
+        # ... and released workers pull the log entries since their last pull (PullLog)
+        self.sparse_pull = self.sparse_push and cfg.sparse_pull
         if self.wide and not self.sparse_push:
             cfg.wide_dense_delta = True
         self._umax = 0
@@ -491,11 +552,17 @@ class DistEngine:
     # ------------------------------------------------------------------
     def _open_ctrl(self):
         name = ctrl_queue_name()
+        N = self.cfg.num_workers
         if self.rank == 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, True)
+            # sparse pull: one reply queue per worker tells it what its next pull carries
+            self._replies = ([_native.host.CtrlQueue(f"{name}_r{j}"[:250], 64, True) for j in range(N)]
+                             if self.sparse_pull else [])
         dist.barrier()
         if self.rank != 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, False)
+            self._reply = (_native.host.CtrlQueue(f"{name}_r{self.worker_id}"[:250], 64, False)
+                           if self.sparse_pull else None)
         dist.barrier()
 
     def _run_async(self) -> dict:
@@ -512,6 +579,8 @@ class DistEngine:
             dist.barrier()
             if self.rank == 0 and self._ctrl is not None:
                 self._ctrl.unlink()
+                for q in getattr(self, "_replies", []):
+                    q.unlink()
 
     def _server_loop(self) -> dict:
         cfg, srv = self.cfg, self.server
@@ -524,6 +593,30 @@ class DistEngine:
         dead = self.__dict__.setdefault("_dead_workers", set())  # failed in any run: stay retired
         finished = set(dead)
         failed = set(dead)
+        plog = None
+        if self.sparse_pull:
+            if getattr(self, "_pull_log", None) is None:
+                self._pull_log = PullLog(self.spec, pull_log_capacity(self._umax), N, self.device)
+            plog = self._pull_log
+            plog.last = [-1] * N  # every run starts with a dense pull
+
+        def release(j: int, u: int):
+            """Send worker j the weights of clock u: the dense vector, or (sparse pull)
+            the log entries since its previous pull, announced on its reply queue."""
+            if plog is None:
+                dist.send(srv.w, dst=j + 1)
+                return
+            kind, m, len1, parts = plog.plan(j)
+            r = _native.host.CtrlToken()
+            r.worker, r.kind, r.vc, r.n, r.aux = j, kind, u, m, len1
+            if not self._replies[j].push(r, 600.0):
+                raise TimeoutError(f"reply queue of worker {j} full")
+            if kind == 0:
+                dist.send(srv.w, dst=j + 1)
+            else:
+                for t in parts:
+                    dist.send(t.contiguous(), dst=j + 1)
+
         for j in range(N):  # bootstrap: vc 0 to every worker (tracker untouched)
             if j in dead:
                 continue
@@ -531,7 +624,7 @@ class DistEngine:
                 srv.tracker.revive(j)
             if srv.tracker.clock(j) > 0:  # a later run of this engine: resume at the tracked clocks
                 srv.tracker.sent(j, srv.tracker.clock(j))
-            dist.send(srv.w, dst=j + 1)
+            release(j, int(srv.tracker.clock(j)))
         t_start = time.time()
         busy_since = {j: t_start for j in range(N)}  # weights sent, delta not back yet (watchdog)
 
@@ -545,7 +638,7 @@ class DistEngine:
             busy_since.pop(k, None)
             for j, u in srv.tracker.retire(k):
                 if j not in finished:
-                    dist.send(srv.w, dst=j + 1)
+                    release(j, u)
                     busy_since[j] = time.time()
 
         while len(finished) < N:
@@ -577,6 +670,8 @@ class DistEngine:
                 srv.apply_and_log(delta, v, self.log)
             else:
                 srv.apply(delta)
+            if plog is not None:
+                plog.append(ubuf, dbuf, U)
             srv.updates += 1
             released = srv.tracker.on_delta(k, v)
             if tok.kind == KIND_FINAL:
@@ -587,7 +682,7 @@ class DistEngine:
             for j, u in released:
                 if j in finished:
                     continue
-                dist.send(srv.w, dst=j + 1)
+                release(j, u)
                 busy_since[j] = time.time()
             maybe_checkpoint(cfg, srv, srv.updates)
             if self.log is not None:
@@ -597,7 +692,8 @@ class DistEngine:
         elapsed = time.time() - t_start
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
-                "failed_workers": sorted(failed)}
+                "failed_workers": sorted(failed), "sparse_pulls": plog.sparse if plog else 0,
+                "dense_pulls": plog.dense if plog else 0}
 
     def _native_server(self):
         """The C++ server loop (csrc/runtime/async_server.h) bound to this engine's
@@ -619,6 +715,13 @@ class DistEngine:
                 dbuf = torch.zeros(KP + self._umax * KP, dtype=torch.float32, device=self.device)
                 keep += [ubuf, dbuf]
                 d.update(model=1, umax=int(self._umax), ubuf=ubuf.data_ptr(), dbuf=dbuf.data_ptr())
+                if self.sparse_pull:
+                    cap = pull_log_capacity(self._umax)
+                    lids = torch.zeros(cap, dtype=torch.int32, device=self.device)
+                    lvals = torch.zeros(cap * KP, dtype=torch.float32, device=self.device)
+                    keep += [lids, lvals]
+                    d.update(sparse_pull=1, lids=lids.data_ptr(), lvals=lvals.data_ptr(), logcap=cap,
+                             replies=[q.handle for q in self._replies])
             else:
                 buf = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
                 keep.append(buf)
@@ -681,7 +784,8 @@ class DistEngine:
         n = srv.updates - u0
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": n / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
-                "failed_workers": list(a.failed), "host_us_per_update": a.host_us_per_update, "native_server": True}
+                "failed_workers": list(a.failed), "host_us_per_update": a.host_us_per_update, "native_server": True,
+                "sparse_pulls": int(a.sparse_pulls), "dense_pulls": int(a.dense_pulls)}
 
     def _worker_loop(self) -> dict:
         cfg, wk = self.cfg, self.worker
@@ -697,7 +801,39 @@ class DistEngine:
         def recv(t):
             comm.recv(t, 0) if comm is not None else dist.recv(t, src=0)
 
-        recv(wk.w)
+        KP = self.spec.KP if self.wide else 0
+        if self.sparse_pull:  # receive buffers of the largest pull the log can send
+            cap = pull_log_capacity(self._umax)
+            pids = torch.zeros(cap, dtype=torch.int32, device=self.device)
+            pvals = torch.zeros(cap * KP, dtype=torch.float32, device=self.device)
+
+        def pull():
+            """The weights of the next clock: dense, or (sparse pull) the log entries
+            since the last pull applied to this worker's replica (w += lr * delta)."""
+            if not self.sparse_pull:
+                recv(wk.w)
+                return
+            r = self._reply.pop(600.0)
+            if r is None:
+                raise TimeoutError(f"worker {wk.k}: no release from the server for 600 s")
+            if r.kind == 0:
+                recv(wk.w)
+                return
+            n, l1 = int(r.n), int(r.aux)
+            if l1:
+                recv(pids[:l1])
+                recv(pvals[: l1 * KP])
+            if n > l1:
+                recv(pids[l1:n])
+                recv(pvals[l1 * KP: n * KP])
+            if gpu:
+                _native.hip().log_apply(wk.w.data_ptr(), pids.data_ptr(), pvals.data_ptr(), n, KP, float(cfg.lr),
+                                        torch.cuda.current_stream(self.device).cuda_stream)
+            else:
+                idx = (pids[:n].long() * KP).unsqueeze(1) + torch.arange(KP).unsqueeze(0)
+                wk.w.index_add_(0, idx.reshape(-1), pvals[: n * KP] * cfg.lr)
+
+        pull()
         if gpu and not wk.wide:
             from ..runtime.roles import SideStream
 
@@ -752,7 +888,7 @@ class DistEngine:
                 send(delta)
             if final:
                 break
-            recv(wk.w)  # stream-ordered: the next solve enqueued below waits for it on the device
+            pull()  # stream-ordered: the next solve enqueued below waits for it on the device
             wk.vc += 1
             if self.log is not None:
                 self.log.drain()

@@ -31,6 +31,7 @@ class PSConfig:
     ring_nz: int = 0  # wide model: non-zeros per ring row (0 = from the data)
     wide_dense_delta: bool = False  # wide model: also produce a dense delta (collective pushes)
     sparse_push: bool = True  # wide model, SSP/ASP across ranks: push (ids, values) instead of a dense delta
+    sparse_pull: bool = True  # ... and pull the log entries since the last pull instead of the dense weights
     # topology / consistency
     num_workers: int = 4
     consistency_model: int = 0  # 0 sequential, -1 eventual, D>0 bounded delay

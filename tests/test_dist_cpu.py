@@ -185,6 +185,25 @@ def test_wide_async_push(sparse_push):
     assert out["updates"] == 12 and torch.isfinite(w).all()
 
 
+def test_wide_sparse_pull_matches_dense_pull():
+    """One worker (deterministic order): pulling the logged deltas since the last
+    pull gives the same model as pulling the dense weights every time."""
+    kw = dict(BASE, consistency_model=-1, max_iters=8, _data="wide", max_buffer_size=256, min_buffer_size=64,
+              num_workers=1)
+    out_s, w_s = _run(2, dict(kw, sparse_pull=True))
+    out_d, w_d = _run(2, dict(kw, sparse_pull=False))
+    assert out_s["sparse_pulls"] >= 1 and out_d["sparse_pulls"] == 0  # (small test model: dense is often cheaper)
+    assert torch.allclose(w_s, w_d, atol=1e-6, rtol=1e-5), (w_s - w_d).abs().max()
+
+
+@pytest.mark.parametrize("c", [-1, 2])
+def test_wide_sparse_pull_multi_worker(c):
+    out, w = _run(3, dict(BASE, consistency_model=c, max_iters=6, _data="wide", max_buffer_size=256,
+                          min_buffer_size=64))
+    assert out["updates"] == 12 and torch.isfinite(w).all()
+    assert out["sparse_pulls"] > 0
+
+
 @pytest.mark.parametrize("c,bound", [(0, 1), (2, 3), (-1, None)])
 def test_log_derived_vc_gap(tmp_path, c, bound):
     """The reference validates its consistency models from the logs

@@ -72,11 +72,16 @@ def launch(a, tr, te):
     return {n: p.returncode for n, p in procs}
 
 
+def _log(prefix: str, kind: str) -> str:
+    p = prefix + f"logs-{kind}.csv"
+    return p if os.path.exists(p) else p + ".gz"  # committed logs are gzipped when large
+
+
 def metrics(prefix: str) -> dict:
     import pandas as pd
 
-    s = pd.read_csv(prefix + "logs-server.csv", sep=";")
-    w = pd.read_csv(prefix + "logs-worker.csv", sep=";")
+    s = pd.read_csv(_log(prefix, "server"), sep=";")
+    w = pd.read_csv(_log(prefix, "worker"), sep=";")
     t0 = min(s.timestamp.min(), w.timestamp.min())
     s = s.sort_values("timestamp")
     out = {"span_s": (max(s.timestamp.max(), w.timestamp.max()) - t0) / 1000.0}
@@ -104,7 +109,7 @@ def table(out_dir: str) -> str:
     res = {}
     for name, ref, n, p, c in RUNS:
         for who, prefix in (("reference", os.path.join(REF, ref + "_")), ("psx", os.path.join(out_dir, name) + "/")):
-            if not os.path.exists(prefix + "logs-server.csv"):
+            if not os.path.exists(_log(prefix, "server")):
                 continue
             m = metrics(prefix)
             res[f"{name}/{who}"] = m

@@ -124,6 +124,65 @@ PYBIND11_MODULE(_psx_hip, m) {
                             step, n, dst};
              s.run(B, start, S(stream), ing);
            })
+      // One solve with the optional extras of LocalSolver::run: fused ingest
+      // (n > 0), a riding evaluation pass (ride_Xt != 0) and a fused server
+      // update (ap_w != 0).
+      .def(
+          "run_full",
+          [](LocalSolver& s, int B, int start, uintptr_t stream, uintptr_t src, uintptr_t ysrc, int64_t first,
+             int64_t step, int n, int dst, uintptr_t ride_Xt, uintptr_t ride_yt, int ride_T, uintptr_t whi,
+             uintptr_t wlo, uintptr_t wb, int coff1, uintptr_t shi, uintptr_t slo, uintptr_t sb, int coff2,
+             uintptr_t acc, uintptr_t ticket, uintptr_t slot, uintptr_t loss, unsigned long long seq, uintptr_t slot2,
+             unsigned long long seq2, uintptr_t ap_w, float ap_lr, uintptr_t ap_hi, uintptr_t ap_lo, uintptr_t ap_b,
+             int ap_coff) {
+            RingIngest ing{};
+            if (n > 0)
+              ing = RingIngest{reinterpret_cast<const uint16_t*>(src), reinterpret_cast<const int32_t*>(ysrc), first,
+                               step, n, dst};
+            EvalRide r{};
+            if (ride_Xt) {
+              r.Xt = P<const uint16_t>(ride_Xt);
+              r.yt = P<const int32_t>(ride_yt);
+              r.T = ride_T;
+              r.K = s.cfg().K;
+              r.whi = P<const uint16_t>(whi);
+              r.wlo = P<const uint16_t>(wlo);
+              r.wb = P<const float>(wb);
+              r.shi = P<const uint16_t>(shi);
+              r.slo = P<const uint16_t>(slo);
+              r.sb = P<const float>(sb);
+              r.coff1 = coff1;
+              r.coff2 = coff2;
+              r.acc = P<int>(acc);
+              r.ticket = P<unsigned>(ticket);
+              r.slot = P<char>(slot);
+              r.loss = P<const float>(loss);
+              r.seq = seq;
+              r.slot2 = P<char>(slot2);
+              r.seq2 = seq2;
+              r.nticket = (unsigned)r.ntiles();
+              if (r.slot2 && (!r.shi || !r.slo || !r.sb))
+                throw std::invalid_argument("run_full: the second model needs its own fragment buffer");
+            }
+            FusedApply ap{};
+            if (ap_w) {
+              ap.w = P<float>(ap_w);
+              ap.lr = ap_lr;
+              ap.hi = P<uint16_t>(ap_hi);
+              ap.lo = P<uint16_t>(ap_lo);
+              ap.b = P<float>(ap_b);
+              ap.coff = ap_coff;
+            }
+            s.run(B, start, S(stream), ing, ride_Xt ? &r : nullptr, ap_w ? &ap : nullptr);
+          },
+          py::arg("B"), py::arg("start"), py::arg("stream"), py::arg("src") = 0, py::arg("ysrc") = 0,
+          py::arg("first") = 0, py::arg("step") = 1, py::arg("n") = 0, py::arg("dst") = 0, py::arg("ride_Xt") = 0,
+          py::arg("ride_yt") = 0, py::arg("ride_T") = 0, py::arg("whi") = 0, py::arg("wlo") = 0, py::arg("wb") = 0,
+          py::arg("coff1") = 0, py::arg("shi") = 0, py::arg("slo") = 0, py::arg("sb") = 0, py::arg("coff2") = 0,
+          py::arg("acc") = 0, py::arg("ticket") = 0, py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0,
+          py::arg("slot2") = 0, py::arg("seq2") = 0, py::arg("ap_w") = 0, py::arg("ap_lr") = 1.f,
+          py::arg("ap_hi") = 0, py::arg("ap_lo") = 0, py::arg("ap_b") = 0, py::arg("ap_coff") = 0)
+      .def_property_readonly("eager", &LocalSolver::eager)
       .def("read_ctrl",
            [](LocalSolver& s, uintptr_t stream) {
              Ctrl c;

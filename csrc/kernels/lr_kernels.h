@@ -44,6 +44,37 @@ struct EvalApply {
   int F;
   int tgrid;  // workgroups evaluating test tiles (set by the launcher); the rest update
 };
+// One evaluation pass described as data, so that it can run either as its own
+// launch (test_eval_kernel) or "ride" in spare workgroups of the worker's solve
+// launches (bwd_update_kernel, see LocalSolver::run): the solve's latency-bound
+// kernels leave >200 of the 256 CUs idle, and the test-set pass of the previous
+// round fits beside them instead of adding a launch to the round.
+//   * model 1: columns [coff1, coff1+K) of (whi, wlo, wb) -> counts acc[0..256)
+//   * model 2 (slot2 != nullptr): columns [coff2, coff2+K), from (shi, slo, sb)
+//     when shi != nullptr (else the same buffer) -> acc[256..512)
+//   * slot != nullptr: the last of `nticket` arriving workgroups (over every
+//     launch the pass spans) publishes the counts (+ *loss) to the pinned host
+//     slot(s) with the sequence numbers; slot == nullptr: counts stay in acc.
+struct EvalRide {
+  const uint16_t* Xt;
+  const int32_t* yt;
+  int T, K;
+  const uint16_t *whi, *wlo;
+  const float* wb;
+  const uint16_t *shi, *slo;
+  const float* sb;
+  int coff1, coff2;
+  int* acc;
+  unsigned* ticket;
+  char* slot;
+  const float* loss;
+  unsigned long long seq;
+  char* slot2;
+  unsigned long long seq2;
+  unsigned nticket;  // arriving workgroups that complete the pass
+  PSX_HD int ntiles() const { return (T + kTileRows - 1) / kTileRows; }
+};
+
 void launch_eval_apply(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* whi,
                        const uint16_t* wlo, const float* wb, int* conf, hipStream_t s, unsigned* ticket, void* slot,
                        const float* loss, unsigned long long seq, int coff1, int coff2, void* slot2,

@@ -15,6 +15,7 @@
 //              the B-operand fragment order of v_mfma_f32_16x16x32_bf16.
 #include <hip/hip_runtime.h>
 
+#include "eval_body.h"
 #include "lr_kernels.h"
 #include "solve_kernels.h"
 #include "tile.h"
@@ -46,138 +47,30 @@ bool fp_supported(int FP) { return FP == 128 || FP == 256 || FP == 512 || FP == 
 // the other buffer of the server's pair (see lr_kernels.h: EvalApply) -- one
 // launch per round for the worker row, the server row and the update.
 template <int FP>
-__global__ __launch_bounds__(256) void test_eval_kernel(int K, const uint16_t* __restrict__ Xt,
-                                                        const int32_t* __restrict__ yt, int T,
-                                                        const uint16_t* __restrict__ wf_hi,
-                                                        const uint16_t* __restrict__ wf_lo,
-                                                        const float* __restrict__ b, int* acc, unsigned* ticket,
-                                                        char* slot, const float* loss, unsigned long long seq,
-                                                        int coff1, int coff2, char* slot2, unsigned long long seq2,
-                                                        EvalApply ea) {
+__global__ __launch_bounds__(256) void test_eval_kernel(EvalRide r, EvalApply ea) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* red_base = lds + 32 * FP * 2;
-  int* cl = (int*)(red_base + 8192);  // [16][16]
-  int* last = cl + 256;
-  int* cl2 = last + 4;                // [16][16] (paired mode)
-  const int tid = threadIdx.x;
-  const bool pair = slot2 != nullptr;
-  cl[tid] = 0;
-  if (pair) cl2[tid] = 0;
   // workgroups [0, tgrid) evaluate test tiles; the extra workgroups [tgrid, grid)
   // perform the round's server update (independent of everything this launch
   // reads) on otherwise idle CUs, beside the evaluation
   const int tgrid = ea.tgrid > 0 ? ea.tgrid : gridDim.x;
+  const int K = r.K;
   if (ea.dl.n > 0 && (int)blockIdx.x >= tgrid) {
     const int P = K * FP + K, KF = K * FP;
-    for (int p = (blockIdx.x - tgrid) * 256 + tid; p < P; p += (gridDim.x - tgrid) * 256) {
+    for (int p = (blockIdx.x - tgrid) * 256 + threadIdx.x; p < P; p += (gridDim.x - tgrid) * 256) {
       float sum = 0.f;
       for (int i = 0; i < ea.dl.n; ++i) sum += ea.dl.p[i][p];
       const float v = ea.w[p] + ea.lr * sum;
       ea.w[p] = v;
       if (p < KF) {
         const int c = p / FP, f = p - c * FP;
-        write_frag(ea.ohi, ea.olo, coff2 + c, f, f < ea.F ? v : 0.f);
+        write_frag(ea.ohi, ea.olo, r.coff2 + c, f, f < ea.F ? v : 0.f);
       } else {
-        ea.ob[coff2 + p - KF] = v;
+        ea.ob[r.coff2 + p - KF] = v;
       }
     }
   }
-  // per-lane B-operand source: server columns from the server's own buffer
-  const bool split = ea.shi != nullptr;
-  const int lcls = tid & 15;
-  const uint16_t* fh = (split && lcls >= coff2) ? ea.shi : wf_hi;
-  const uint16_t* fl = (split && lcls >= coff2) ? ea.slo : wf_lo;
-  const float* b2 = split ? ea.sb : b;
-  const int ntiles = (int)blockIdx.x < tgrid ? (T + 31) / 32 : 0;
-  // The weight fragments are usually fresh (written by the solve / update just
-  // before, so not in this XCD's L2): fetch them into registers BEFORE staging
-  // the first tile so the two memory latencies overlap (as fwd_kernel does);
-  // only the columns of the evaluated models are fetched.
-  constexpr bool kPre = FP <= 1024;
-  WFrag<kPre ? FP : 128> wf;
-  if constexpr (kPre) {
-    if (ntiles > (int)blockIdx.x) {
-      const bool live = (lcls >= coff1 && lcls < coff1 + K) || (pair && lcls >= coff2 && lcls < coff2 + K);
-      load_wfrag<FP>(wf, fh, fl, live ? 16 : 0);
-    }
-  }
-  for (int tile = blockIdx.x; tile < ntiles; tile += tgrid) {
-    const int nrows = min(32, T - tile * 32);
-    stage_tile<FP>(lds, Xt, (int64_t)tile * 32, nrows, 0, false);
-    __syncthreads();
-    f32x4 a0, a1;
-    if constexpr (kPre)
-      forward_tile_pre<FP>(lds, wf, a0, a1);
-    else
-      forward_tile<FP>(lds, fh, fl, a0, a1);
-    store_partial_logits(red_base, a0, a1);
-    __syncthreads();
-    if (tid < nrows) {
-      int best = 0;
-      float bz = -INFINITY;
-      for (int c = 0; c < K; ++c) {
-        const float z = load_logit(red_base, tid, coff1 + c) + b[coff1 + c];
-        if (z > bz) {
-          bz = z;
-          best = c;
-        }
-      }
-      int yl = yt[(size_t)tile * 32 + tid];
-      yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
-      atomicAdd(&cl[yl * 16 + best], 1);
-      if (pair) {
-        int best2 = 0;
-        float bz2 = -INFINITY;
-        for (int c = 0; c < K; ++c) {
-          const float z = load_logit(red_base, tid, coff2 + c) + b2[coff2 + c];
-          if (z > bz2) {
-            bz2 = z;
-            best2 = c;
-          }
-        }
-        atomicAdd(&cl2[yl * 16 + best2], 1);
-      }
-    }
-    __syncthreads();
-  }
-  __syncthreads();
-  const int v = cl[tid];
-  // the private accumulator (slot mode) spreads its cells one per 128-B line, so
-  // the workgroups' atomics are not serialised on a few cache lines (kAccStride)
-  const int ast = slot ? kAccStride : 1;
-  if (v) atomicAdd(acc + tid * ast, v);
-  if (pair) {
-    const int v2 = cl2[tid];
-    if (v2) atomicAdd(acc + (256 + tid) * ast, v2);
-  }
-  if (slot == nullptr) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    *last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!*last) return;
-  // Publication into the pinned (fine-grained, uncached) host slot: the counts
-  // go out as system-scope relaxed stores, every wave drains them (vmcnt), and
-  // only then is the sequence number stored.  No release fence: it would write
-  // back this XCD's whole L2 (the solver's dirty lines included), and nothing
-  // cached is being published.
-  const int tot = __hip_atomic_exchange(acc + tid * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (pair) {
-    const int tot2 = __hip_atomic_exchange(acc + (256 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((int*)slot2 + tid, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid == 0) __hip_atomic_store((float*)(slot2 + 1024), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((unsigned long long*)(slot + 1032), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (pair)
-      __hip_atomic_store((unsigned long long*)(slot2 + 1032), seq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  const int ntiles = (int)blockIdx.x < tgrid ? r.ntiles() : 0;
+  eval_body<FP>(lds, r, blockIdx.x, tgrid, ntiles);  // every workgroup arrives at the ticket
 }
 
 void launch_test_eval(int FP, int K, const uint16_t* Xt, const int32_t* yt, int T, const uint16_t* wf_hi,
@@ -201,12 +94,30 @@ void launch_eval_apply(int FP, int K, const uint16_t* Xt, const int32_t* yt, int
   a.tgrid = tgrid;
   if (ea.dl.n > 0) grid += (K * FP + K + 255) / 256;  // update workgroups
   if (grid <= 0) return;
-  char* sl = static_cast<char*>(slot);
-  char* sl2 = static_cast<char*>(slot2);
-#define PSX_TE(FPV)                                                                                          \
-  case FPV:                                                                                                  \
-    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(K, Xt, yt, T, wf_hi, wf_lo, b, conf, ticket, sl, loss, seq, \
-                                                 coff1, coff2, sl2, seq2, a);                               \
+  EvalRide r{};
+  r.Xt = Xt;
+  r.yt = yt;
+  r.T = T;
+  r.K = K;
+  r.whi = wf_hi;
+  r.wlo = wf_lo;
+  r.wb = b;
+  r.shi = ea.shi;
+  r.slo = ea.slo;
+  r.sb = ea.sb;
+  r.coff1 = coff1;
+  r.coff2 = coff2;
+  r.acc = conf;
+  r.ticket = ticket;
+  r.slot = static_cast<char*>(slot);
+  r.loss = loss;
+  r.seq = seq;
+  r.slot2 = static_cast<char*>(slot2);
+  r.seq2 = seq2;
+  r.nticket = (unsigned)grid;
+#define PSX_TE(FPV)                                             \
+  case FPV:                                                     \
+    test_eval_kernel<FPV><<<grid, 256, lds, s>>>(r, a);         \
     break;
   switch (FP) {
     PSX_TE(128)

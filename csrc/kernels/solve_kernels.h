@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lr_kernels.h"
 #include "solver_ctrl.h"
 
 namespace psx {
@@ -39,6 +40,24 @@ struct SolveDev {
   double* spart;  // [G][2][FP] partial column sums / sums of squares
   float* gred;    // [KP][FPI] reduced gradient sums (bwd_update reads them when non-null)
   const float* Xf;  // fp32 ring rows [cap][Fp] (cfg.xf32; X is then unused)
+  // optional server update fused into the finalisation (a colocated server whose
+  // model is this worker's pulled w_old, e.g. BSP with one worker): ap_w (may be
+  // w_old itself) = w_old + ap_lr * delta, fragments at columns ap_coff of
+  // (ap_hi, ap_lo, ap_b).  ap_w == nullptr: no update.
+  float* ap_w;
+  uint16_t *ap_hi, *ap_lo;
+  float* ap_b;
+  float ap_lr;
+  int ap_coff;
+};
+
+// Server update fused into a solve (see SolveDev::ap_w).
+struct FusedApply {
+  float* w = nullptr;
+  float lr = 1.f;
+  uint16_t *hi = nullptr, *lo = nullptr;
+  float* b = nullptr;
+  int coff = 0;
 };
 
 int padded_classes(int K);
@@ -53,8 +72,10 @@ void launch_stats_prep(const SolverCfg& cfg, SolveParams* prm, const SolveDev& d
                        const RingIngest& ing, hipStream_t s);
 const void* stats_prep_symbol();
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
+// win.B > 0: the window as kernel arguments (eager launches); otherwise the
+// kernels read it from prm (graph replays).
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                 hipStream_t s);
+                 hipStream_t s, const SolveParams& win);
 // Line-search retry slots [slot_begin, slot_end) in one persistent launch.
 // with_finalize: the finalisation runs inside the tail launch (no separate finalize node).
 void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
@@ -78,7 +99,12 @@ void launch_fwdbwd_rows(const SolverCfg& cfg, const SolveParams* prm, const Ctrl
 void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* ctrl, const SolveDev& dv, int G,
                      hipStream_t s);
 void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
-                hipStream_t s);
+                hipStream_t s, const SolveParams& win);
+// One function-evaluation slot (fwd + bwd_update launches) with `nride` extra
+// workgroups in the bwd_update launch evaluating test tiles [ride_t0, ride_t0 +
+// nride) of `ride` (see EvalRide, lr_kernels.h); nride == 0: none.
+void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
+                      hipStream_t s, const SolveParams& win, const struct EvalRide& ride, int ride_t0, int nride);
 size_t stats_rows_lds_bytes();
 // fp32 ring rows: rows src_first + i*src_step -> slots (dst_first + i) % cap
 void launch_ring_ingest_f32(const float* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,

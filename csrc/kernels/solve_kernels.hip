@@ -38,6 +38,7 @@
 
 #include <cstdlib>
 
+#include "eval_body.h"
 #include "lr_kernels.h"
 #include "solve_kernels.h"
 #include "tile.h"
@@ -281,11 +282,12 @@ __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned sho
 // image right after the hi one), forward x_hi.(W_hi + W_lo) + x_lo.W_hi and
 // backward (R_hi + R_lo)^T x_hi + R_hi^T x_lo -- near-fp32 products on bf16 MFMA.
 template <int FP, bool kRows = false, bool kF32 = false>
-__device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams* prm, int slot, const SolveDev& dv,
-                                         char* lds, const int wg, const int G, f32x4* gacc = nullptr) {
+__device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams pr, int slot, const SolveDev& dv,
+                                         char* lds, const int wg, const int G, f32x4* gacc = nullptr,
+                                         const int entry_phase = -1) {
   static_assert(!kF32 || (kRows && FP <= 1024), "fp32 rows: rows mode, FP <= 1024 (two tile images in LDS)");
-  const int B = prm->B, K = cfg.K;
-  const WinTiles wt(prm->start, B, cfg.cap);
+  const int B = pr.B, K = cfg.K;
+  const WinTiles wt(pr.start, B, cfg.cap);
   const int ntiles = wt.nt;
   if (wg >= ntiles) return;
   if (wg == 0 && threadIdx.x == 0) stamp(dv, slot, 0);
@@ -293,11 +295,10 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   char* red_base = lds + (kF32 ? 2 : 1) * 32 * FP * 2;
   unsigned short* rt = (unsigned short*)(red_base + 8192);  // [2][16][32]
   int* ylds = (int*)(red_base + 8192 + 2048);
-  float* rsum = (float*)(ylds + 32);
-  float* lred = rsum + 16;
+  float* rsum = (float*)(ylds + 32);  // [4 waves][16] per-wave residual sums
+  float* lred = rsum + 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 
-  if (tid < 16) rsum[tid] = 0.f;
   float loss = 0.f;
   const int sr = tid >> 3, sc0 = (tid & 7) * 2;
   float rs0 = 0.f, rs1 = 0.f;
@@ -315,6 +316,9 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
       stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
     if (tid < 32) ylds[tid] = dv.y[row0 + tid];
     __syncthreads();
+    // converged in an earlier slot: exit (the phase word was loaded at kernel
+    // entry, so its latency overlapped the tile staging; nothing written yet)
+    if (entry_phase == kPhDone) return;
     if (wg == 0 && tid == 0) stamp(dv, slot, 9);
     f32x4 a0, a1;
     if constexpr (kPre)
@@ -372,23 +376,40 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
     }
     if (wg == 0 && tid == 0) stamp(dv, slot, 11);
   }
-  atomicAdd(&rsum[sc0], rs0);
-  atomicAdd(&rsum[sc0 + 1], rs1);
+  // per-class residual sums over the rows, in a fixed order (a butterfly over the
+  // lanes of one class pair, then the waves in order): the solve is bitwise
+  // reproducible -- LDS float atomics would sum in arrival order
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    rs0 += __shfl_xor(rs0, o, 64);
+    rs1 += __shfl_xor(rs1, o, 64);
+  }
+  if (lane < 8) {
+    rsum[w * 16 + sc0] = rs0;
+    rsum[w * 16 + sc0 + 1] = rs1;
+  }
   loss = wave_sum(loss);
   if (lane == 0) lred[w] = loss;
   __syncthreads();
   float* part = dv.part + (size_t)wg * kPartStride;
-  if (tid < 16) part[tid] = rsum[tid];
+  if (tid < 16) part[tid] = ((rsum[tid] + rsum[16 + tid]) + rsum[32 + tid]) + rsum[48 + tid];
   if (tid == 16) part[16] = lred[0] + lred[1] + lred[2] + lred[3];
   if (wg == 0 && tid == 0) stamp(dv, slot, 1);
 }
 
+// The window arrives as a kernel argument (win.B > 0; eager launches) or from
+// device memory (win.B <= 0: graph replays, whose arguments are fixed at capture)
+// -- the argument form takes one dependent load off the head of the chain.
+__device__ __forceinline__ SolveParams window_of(const SolveParams& win, const SolveParams* prm) {
+  return win.B > 0 ? win : *prm;
+}
+
 template <int FP>
 __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl, int slot,
-                                                  SolveDev dv) {
+                                                  SolveDev dv, SolveParams win) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (ctrl->phase == kPhDone) return;  // converged in an earlier slot: exit at once
-  fwd_body<FP>(cfg, prm, slot, dv, lds, blockIdx.x, gridDim.x);
+  const int phase = ctrl->phase;  // checked once the first tile is staged
+  fwd_body<FP>(cfg, window_of(win, prm), slot, dv, lds, blockIdx.x, gridDim.x, nullptr, phase);
 }
 
 // ---------------------------------------------------------------------------
@@ -398,6 +419,13 @@ __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolvePara
 // copy XT (feature x 8 consecutive rows = 16 B per lane), so no LDS staging.
 constexpr int kBwdBatch = 8;  // k-steps (32-row tiles) per wave whose loads are in flight together
 
+size_t bwd_lds_bytes();
+// a bwd_update launch with riding evaluation workgroups sizes its LDS for both bodies
+size_t bwd_ride_lds_bytes(int FP) {
+  const size_t a = bwd_lds_bytes(), b = eval_lds_bytes(FP);
+  return a > b ? a : b;
+}
+
 size_t bwd_lds_bytes() {
   return (size_t)4 * 16 * 32 * 4 + 2 * 512 * 2 + ctrl_lds_bytes() +
          (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) + sizeof(CtrlScratch);
@@ -405,8 +433,9 @@ size_t bwd_lds_bytes() {
 
 // Body shared by bwd_update_kernel and tail_kernel: slice `wg` of `NS`.
 template <int FP, int KP>
-__device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
-                                         const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS) {
+__device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
+                                         const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
+                                         const bool check_done = false) {
   constexpr int FPI = FP > 256 ? FP : 256;
   constexpr int IB = KP * FPI;              // internal intercept base
   constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
@@ -428,8 +457,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     for (int i = tid; i < CW; i += 256) ((unsigned long long*)cl)[i] = ((const unsigned long long*)gctrl)[i];
   }
 
-  const int B = prm->B, cap = cfg.cap, K = cfg.K, H = cfg.hist;
-  const WinTiles wt(prm->start, B, cap);
+  const int B = win.B, cap = cfg.cap, K = cfg.K, H = cfg.hist;
+  const WinTiles wt(win.start, B, cap);
   const size_t PI = dv.PI;
   const float invB = 1.f / (float)B;
   const int fs = wg * 32;
@@ -519,6 +548,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       }
   }
   __syncthreads();
+  // converged in an earlier slot (standalone launch): exit.  Checked here, on the
+  // LDS copy of the controller, so the phase load overlapped the backward's loads;
+  // nothing global has been written yet.
+  if (check_done && cl->phase == kPhDone) return;
   float g[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
@@ -786,10 +819,15 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
 
 template <int FP, int KP>
 __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
-                                                         SolveDev dv, int fwd_grid) {
+                                                         SolveDev dv, int fwd_grid, SolveParams win, int ns,
+                                                         EvalRide ride, int ride_t0) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (gctrl->phase == kPhDone) return;
-  bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, fwd_grid, lds, blockIdx.x, gridDim.x);
+  if ((int)blockIdx.x >= ns) {  // an evaluation workgroup riding in this launch: one test tile
+    const int t = ride_t0 + (int)blockIdx.x - ns;
+    eval_body<FP>(lds, ride, t, 1, t + 1);
+    return;
+  }
+  bwd_body<FP, KP>(cfg, window_of(win, prm), gctrl, slot, dv, fwd_grid, lds, blockIdx.x, ns, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -830,20 +868,33 @@ __device__ __forceinline__ void grid_barrier(unsigned long long* ctr, unsigned l
 // Finalisation (after the last slot): back to the unstandardised space,
 // multinomial centring across classes, delta = w_new - w_old, eval fragments,
 // loss and solver statistics.  One thread per feature (all classes).
+// Per-feature inputs of the finalisation, loadable ahead of the phase check.
 template <int KP>
-__device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk) {
-  const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
-  const int f = blk * 256 + threadIdx.x;
-  if (blk == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
-  if (f < FP) {
-    const float iv = dv.inv_std[f];
-    float xv[KP], fx[KP], wo[KP];
+struct FinIn {
+  float iv, xv[KP], fx[KP], wo[KP];
+  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
+    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
+    const int f = blk * 256 + threadIdx.x;
+    if (f >= FP) return;
+    iv = dv.inv_std[f];
 #pragma unroll
     for (int c = 0; c < KP; ++c) {
       xv[c] = dv.x[c * FPI + f];
       fx[c] = dv.wfix[c * FPI + f];
       wo[c] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
     }
+  }
+};
+
+template <int KP>
+__device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk,
+                                              const FinIn<KP>& in) {
+  const int FP = cfg.Fp, K = cfg.K;
+  const int f = blk * 256 + threadIdx.x;
+  if (blk == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
+  if (f < FP) {
+    const float iv = in.iv;
+    const float *xv = in.xv, *fx = in.fx, *wo = in.wo;
     float wv[KP];
     float mean = 0.f;
 #pragma unroll
@@ -857,13 +908,20 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
       const float v = c < K ? wv[c] - mean : 0.f;
       write_frag(dv.out_hi, dv.out_lo, c, f, v);
       if (c < K) {
-        dv.delta[c * FP + f] = v - wo[c];
+        const float dl = v - wo[c];
+        dv.delta[c * FP + f] = dl;
         if (dv.w_new) dv.w_new[c * FP + f] = v;
+        if (dv.ap_w) {  // fused server update: w += lr * delta (ServerProcessor.java:148-151)
+          // (ap_w may alias w_old: this thread alone reads and writes element (c, f))
+          const float nw = wo[c] + dv.ap_lr * dl;
+          dv.ap_w[c * FP + f] = nw;
+          write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
+        }
       }
     }
   }
   if (blk == 0 && threadIdx.x == 0) {
-    const int IB = dv.KP * FPI;
+    const int IB = dv.KP * dv.FPI;
     float bv[16];
     float mean = 0.f;
     for (int c = 0; c < K; ++c) {
@@ -874,9 +932,16 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
     const int KF = K * FP;
     for (int c = 0; c < K; ++c) {
       const float v = bv[c] - mean;
-      dv.delta[KF + c] = v - dv.w_old[KF + c];
+      const float wo = dv.w_old[KF + c];
+      const float dl = v - wo;
+      dv.delta[KF + c] = dl;
       if (dv.w_new) dv.w_new[KF + c] = v;
       dv.b_fin[c] = v;
+      if (dv.ap_w) {
+        const float nw = wo + dv.ap_lr * dl;
+        dv.ap_w[KF + c] = nw;
+        dv.ap_b[dv.ap_coff + c] = nw;
+      }
     }
     *dv.loss = (float)ctrl->f_c;
     *dv.prm_count += 1;  // run counter: makes the all-gather tags unique per run
@@ -899,7 +964,9 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
 
 template <int KP>
 __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl* ctrl, SolveDev dv) {
-  finalize_body<KP>(cfg, ctrl, dv, blockIdx.x);
+  FinIn<KP> in;
+  in.load(cfg, dv, blockIdx.x);
+  finalize_body<KP>(cfg, ctrl, dv, blockIdx.x, in);
 }
 
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s) {
@@ -918,9 +985,13 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
                                                    int nfin) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
+  // the finalisation's inputs are fetched before the phase word is known, so
+  // the two load latencies overlap (the common case is phase == done)
+  FinIn<KP> in;
+  if ((int)blockIdx.x < nfin) in.load(cfg, dv, blockIdx.x);
   if (gctrl->phase == kPhDone) {  // the common case: written by the previous launch
     // the finalisation is folded into this launch (one graph node less per solve)
-    if (blockIdx.x < nfin) finalize_body<KP>(cfg, gctrl, dv, blockIdx.x);
+    if ((int)blockIdx.x < nfin) finalize_body<KP>(cfg, gctrl, dv, blockIdx.x, in);
     return;
   }
   const int G = gridDim.x, wg = blockIdx.x;
@@ -932,13 +1003,16 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
       __syncthreads();
       if (phase_s == kPhDone) break;  // uniform: every workgroup read the same word after the barrier
     }
-    fwd_body<FP>(cfg, prm, slot, dv, lds, wg, G);
+    fwd_body<FP>(cfg, *prm, slot, dv, lds, wg, G);
     grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
-    if (wg < ns) bwd_body<FP, KP>(cfg, prm, gctrl, slot, dv, G, lds, wg, ns);
+    if (wg < ns) bwd_body<FP, KP>(cfg, *prm, gctrl, slot, dv, G, lds, wg, ns);
     grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
   }
   // every exit of the loop follows a grid barrier: all slots' updates are visible
-  if (wg < nfin) finalize_body<KP>(cfg, gctrl, dv, wg);
+  if (wg < nfin) {
+    in.load(cfg, dv, wg);  // re-read: the slots above moved x
+    finalize_body<KP>(cfg, gctrl, dv, wg, in);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -958,52 +1032,61 @@ int padded_stride(int FP) { return FP > 256 ? FP : 256; }
 int bwd_grid(int FP) { return FP / 32; }
 
 template <int FP>
-static void launch_slot_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
-                           int nwg, hipStream_t s) {
-  fwd_kernel<FP><<<nwg, 256, fwd_lds_bytes(FP), s>>>(cfg, prm, ctrl, slot, dv);
-  const int ng = bwd_grid(FP);
-  const size_t bl = bwd_lds_bytes();
+static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
+                          int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
+                          int ride_t0 = 0, int nride = 0) {
+  const int ns = bwd_grid(FP), ng = ns + nride;
+  const size_t bl = nride > 0 ? bwd_ride_lds_bytes(FP) : bwd_lds_bytes();
   switch (dv.KP) {
-    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    default: bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
+    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
+    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
+    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
+    default:
+      bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0);
+      break;
   }
 }
 
 template <int FP>
-static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
-                          int nwg, hipStream_t s) {
-  const int ng = bwd_grid(FP);
-  const size_t bl = bwd_lds_bytes();
-  switch (dv.KP) {
-    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-    default: bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg); break;
-  }
+static void launch_slot_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
+                           int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
+                           int ride_t0 = 0, int nride = 0) {
+  fwd_kernel<FP><<<nwg, 256, fwd_lds_bytes(FP), s>>>(cfg, prm, ctrl, slot, dv, win);
+  launch_bwd_fp<FP>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride);
 }
 
 void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
-                hipStream_t s) {
+                hipStream_t s, const SolveParams& win) {
   switch (cfg.Fp) {
-    case 128: launch_bwd_fp<128>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
-    case 256: launch_bwd_fp<256>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
-    case 512: launch_bwd_fp<512>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
-    case 1024: launch_bwd_fp<1024>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
-    case 2048: launch_bwd_fp<2048>(cfg, prm, ctrl, slot, dv, fwd_grid, s); break;
+    case 128: launch_bwd_fp<128>(cfg, prm, ctrl, slot, dv, fwd_grid, s, win); break;
+    case 256: launch_bwd_fp<256>(cfg, prm, ctrl, slot, dv, fwd_grid, s, win); break;
+    case 512: launch_bwd_fp<512>(cfg, prm, ctrl, slot, dv, fwd_grid, s, win); break;
+    case 1024: launch_bwd_fp<1024>(cfg, prm, ctrl, slot, dv, fwd_grid, s, win); break;
+    case 2048: launch_bwd_fp<2048>(cfg, prm, ctrl, slot, dv, fwd_grid, s, win); break;
+    default: break;
+  }
+}
+
+void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
+                      hipStream_t s, const SolveParams& win, const EvalRide& ride, int ride_t0, int nride) {
+  switch (cfg.Fp) {
+    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
+    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
+    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
+    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
+    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
     default: break;
   }
 }
 
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                 hipStream_t s) {
+                 hipStream_t s, const SolveParams& win) {
   switch (cfg.Fp) {
-    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s); break;
-    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s); break;
-    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s); break;
-    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s); break;
-    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s); break;
+    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
+    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
+    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
+    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
+    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
     default: break;
   }
 }
@@ -1191,7 +1274,7 @@ __global__ __launch_bounds__(256) void fwdbwd_rows_kernel(SolverCfg cfg, const S
   const int wg = blockIdx.x;
   const WinTiles wt(prm->start, prm->B, cfg.cap);
   if (wg >= wt.nt) return;
-  fwd_body<FP, true, kF32>(cfg, prm, slot, dv, lds, wg, gridDim.x, acc);
+  fwd_body<FP, true, kF32>(cfg, *prm, slot, dv, lds, wg, gridDim.x, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, KP = dv.KP;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -1339,7 +1422,7 @@ static void set_slot_attr() {
   if constexpr (FP <= 1024)
     (void)hipFuncSetAttribute((const void*)fwdbwd_rows_kernel<FP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)fwdbwd_rows_lds_bytes(FP, true));
-  const int b = (int)bwd_lds_bytes();
+  const int b = (int)bwd_ride_lds_bytes(FP);
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
   (void)hipFuncSetAttribute((const void*)bwd_update_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, b);

@@ -46,13 +46,19 @@ class LocalSolver {
   // Enqueue one local solve over window [start, start+B) of the ring on `stream`;
   // `ing` (n > 0): first ingest those new rows, the newest of the window, into
   // the ring inside the solve's first kernel.
-  void run(int B, int start, hipStream_t stream, const RingIngest& ing = RingIngest{});
+  // `ride` (optional): an evaluation pass (of models this solve does not write
+  // before its last slot) executed by extra workgroups of the slots' bwd_update
+  // launches.  `ap` (optional): a server update fused into the finalisation
+  // (SolveDev::ap_w).  Both: eager solver only; small windows only for `ride`.
+  void run(int B, int start, hipStream_t stream, const RingIngest& ing = RingIngest{}, const EvalRide* ride = nullptr,
+           const FusedApply* ap = nullptr);
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
   int kernels_per_solve() const {  // stats_prep + slots + (tail with finalize | finalize); rows: 3 per slot
     return rows_mode_ ? 3 + (dv_.gred ? 3 : 2) * cfg_.nslots : 2 + 2 * nfast_;
   }
   bool rows_mode() const { return rows_mode_; }
+  bool eager() const { return !use_graph_; }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):
@@ -60,7 +66,8 @@ class LocalSolver {
   std::vector<long long> read_stamps(hipStream_t stream);
 
  private:
-  void enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing);
+  void enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing, bool capturing, const EvalRide* ride);
+  int ride_split_ = 3;
   SolverCfg cfg_;
   SolveDev dv_{};
   int nwg_eval_;

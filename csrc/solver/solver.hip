@@ -1,4 +1,5 @@
 #include "solver.h"
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -102,11 +103,13 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   // small grids sum the partials inside bwd_update (one launch less per slot)
   dv_.gred = rows_mode_ && nwg_eval_ > kRowsReduceInBwd ? reinterpret_cast<float*>(b + o_gred) : nullptr;
 
+  // riding evaluation passes spread over this many slots' bwd_update launches
+  if (const char* e = std::getenv("PSX_RIDE_SPLIT")) ride_split_ = std::atoi(e) > 0 ? std::atoi(e) : 1;
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    enqueue_body(cap_stream_, cfg.cap, 0, RingIngest{});
+    enqueue_body(cap_stream_, cfg.cap, 0, RingIngest{}, /*capturing=*/true, nullptr);
     hip_check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
     hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
     size_t n = 0;
@@ -145,7 +148,8 @@ LocalSolver::~LocalSolver() {
   if (ws_) (void)hipFree(ws_);
 }
 
-void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing) {
+void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing, bool capturing,
+                               const EvalRide* ride) {
   if (rows_mode_) {
     const int G = nwg_eval_;
     launch_stats_rows(cfg_, prm_, dv_, B, start, G, s);
@@ -153,14 +157,28 @@ void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest
     for (int slot = 0; slot < cfg_.nslots; ++slot) {  // slots after convergence exit at once
       launch_fwdbwd_rows(cfg_, prm_, ctrl_, slot, dv_, G, s);
       if (dv_.gred) launch_reduce_g(cfg_, prm_, ctrl_, dv_, G, s);
-      launch_bwd(cfg_, prm_, ctrl_, slot, dv_, G, s);
+      launch_bwd(cfg_, prm_, ctrl_, slot, dv_, G, s, SolveParams{B, start, 0, 0});
     }
     launch_finalize(cfg_, ctrl_, dv_, s);
     hip_check(hipGetLastError(), "solver kernel launch (rows mode)");
     return;
   }
   launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, ing, s);
-  for (int slot = 0; slot < nfast_; ++slot) launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s);
+  // eager launches carry the window as arguments; a captured graph reads prm
+  const SolveParams win = capturing ? SolveParams{-1, 0, 0, 0} : SolveParams{B, start, 0, 0};
+  // a riding evaluation pass: its test tiles are dealt over the bwd_update
+  // launches of the first `nsplit` slots (extra workgroups beside the slices)
+  const int rt = ride ? ride->ntiles() : 0;
+  const int nsplit = ride ? (ride_split_ < nfast_ ? ride_split_ : nfast_) : 1;
+  int t0 = 0;
+  for (int slot = 0; slot < nfast_; ++slot) {
+    const int n = slot < nsplit ? (rt - t0 + (nsplit - slot) - 1) / (nsplit - slot) : 0;
+    if (n > 0)
+      launch_slot_ride(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win, *ride, t0, n);
+    else
+      launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win);
+    t0 += n;
+  }
   if (cfg_.nslots > nfast_)
     launch_tail(cfg_, prm_, ctrl_, nfast_, cfg_.nslots, dv_, nwg_eval_, s, /*with_finalize=*/1);
   else
@@ -168,8 +186,33 @@ void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest
   hip_check(hipGetLastError(), "solver kernel launch");
 }
 
-void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& ing) {
+void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& ing, const EvalRide* ride,
+                      const FusedApply* ap) {
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
+  if ((ride || ap) && use_graph_) throw std::invalid_argument("riding evaluation / fused update: eager solver only");
+  if (ride) {
+    if (rows_mode_) throw std::invalid_argument("riding evaluation: small-window solver only");
+    if (!ride->Xt || !ride->yt || ride->T <= 0 || !ride->whi || !ride->wlo || !ride->wb || !ride->acc ||
+        !ride->ticket || !ride->slot)
+      throw std::invalid_argument("riding evaluation: incomplete descriptor");
+    if (ride->K != cfg_.K || ride->coff1 < 0 || ride->coff1 + ride->K > 16 ||
+        (ride->slot2 && (ride->coff2 < ride->coff1 + ride->K || ride->coff2 + ride->K > 16)))
+      throw std::invalid_argument("riding evaluation: class columns out of range");
+    if ((unsigned)ride->ntiles() != ride->nticket) throw std::invalid_argument("riding evaluation: ticket count");
+    // (the pass may read the fragments this solve's finalisation -- and a fused
+    // update -- rewrite: every riding workgroup belongs to a bwd_update launch,
+    // and those all precede the finalisation in stream order)
+  }
+  if (ap) {
+    if (!ap->w || !ap->hi || !ap->lo || !ap->b || ap->coff < 0 || ap->coff + cfg_.K > 16)
+      throw std::invalid_argument("fused update: bad output buffers");
+    dv_.ap_w = ap->w;
+    dv_.ap_hi = ap->hi;
+    dv_.ap_lo = ap->lo;
+    dv_.ap_b = ap->b;
+    dv_.ap_lr = ap->lr;
+    dv_.ap_coff = ap->coff;
+  }
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
   if (ing.n < 0 || ing.n > kMaxFusedIngest || ing.n > cfg_.cap) throw std::invalid_argument("fused ingest: bad row count");
   if (ing.n > 0 && rows_mode_) throw std::invalid_argument("fused ingest is not available for large windows");
@@ -186,8 +229,9 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
     hip_check(hipGraphExecKernelNodeSetParams(exec_, stats_node_, &stats_params_), "hipGraphExecKernelNodeSetParams");
     hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
   } else {
-    enqueue_body(stream, B, start, ing);
+    enqueue_body(stream, B, start, ing, false, ride);
   }
+  dv_.ap_w = nullptr;  // the launches above took their copy of dv_
 }
 
 std::vector<long long> LocalSolver::read_stamps(hipStream_t stream) {

@@ -135,6 +135,30 @@ def test_paired_eval_rows_match_unpaired(cuda, N):
     assert max(abs(a[2] - b[2]) for a, b in zip(w0, w1)) < 0.05
 
 
+@pytest.mark.parametrize("N", [1, 2])
+def test_riding_eval_matches_separate_launches(cuda, monkeypatch, N):
+    """Evaluation rows riding in the next solve's bwd_update launches (and, for one
+    worker, the server update fused into the solve's finalisation) log exactly the
+    rows of the separate evaluation / update launches, and end at the same model."""
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    kw = dict(num_workers=N, max_iters=10, init="random", min_buffer_size=512, max_buffer_size=512)
+    res = []
+    for ride in ("1", "0"):
+        monkeypatch.setenv("PSX_EVAL_RIDE", ride)
+        eng = LocalEngine(_cfg(**kw), cuda, train=train, test=test)
+        if ride == "1":
+            assert eng.workers[0].solver.can_ride(eng.workers[0].ring, eng.workers[0].w)
+        eng.run()
+        torch.cuda.synchronize()
+        book = eng.log.book
+        res.append((eng.server.w.cpu(), sorted((r[1], r[2], r[3]) for r in book.server),
+                    sorted((r[1], r[2], r[3], r[4], r[5], r[6]) for r in book.worker)))
+    assert torch.equal(res[0][0], res[1][0])
+    assert [r[0] for r in res[0][1]] == list(range(10))
+    assert res[0][1] == res[1][1]
+    assert len(res[0][2]) == 10 * N and res[0][2] == res[1][2]
+
+
 def test_concurrent_worker_lanes_match_sequential(cuda):
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     ws, books = [], []

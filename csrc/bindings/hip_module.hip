@@ -12,6 +12,7 @@
 
 #include "../comm/rccl_comm.h"
 #include "../runtime/async_server.h"
+#include "../runtime/bsp_loop.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
 #include "../solver/wide_solver.h"
@@ -570,6 +571,64 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("sparse_pulls", &AsyncServer::sparse_pulls)
       .def_property_readonly("dense_pulls", &AsyncServer::dense_pulls)
       .def_property_readonly("pull_floats", &AsyncServer::pull_floats);
+  py::class_<BspLoop>(m, "BspLoop")
+      .def(py::init([](LocalSolver& solver, RcclComm* comm, py::dict d) {
+             auto I = [&](const char* k, int64_t def) { return d.contains(k) ? d[k].cast<int64_t>() : def; };
+             auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
+             auto D = [&](const char* k, double def) { return d.contains(k) ? d[k].cast<double>() : def; };
+             BspLoopCfg c;
+             c.dsX = P<const uint16_t>(U("dsX"));
+             c.dsy = P<const int32_t>(U("dsy"));
+             c.ds_rows = I("ds_rows", 0);
+             c.k = (int)I("k", 0);
+             c.N = (int)I("N", 1);
+             c.per_iter_rows = (int)I("per_iter_rows", 0);
+             c.p_ms = D("p_ms", 0.0);
+             c.epochs = I("epochs", 1);
+             c.t0_ms = D("t0_ms", 0.0);
+             c.X = P<uint16_t>(U("X"));
+             c.XT = P<uint16_t>(U("XT"));
+             c.y = P<int32_t>(U("y"));
+             c.cap = I("cap", 0);
+             c.Fp = (int)I("Fp", 0);
+             c.K = (int)I("K", 0);
+             c.F = (int)I("F", 0);
+             c.window = U("window");
+             c.whi = P<const uint16_t>(U("whi"));
+             c.wlo = P<const uint16_t>(U("wlo"));
+             c.wb = P<const float>(U("wb"));
+             c.loss = P<const float>(U("loss"));
+             c.delta = P<float>(U("delta"));
+             c.w = P<float>(U("w"));
+             c.shi = P<uint16_t>(U("shi"));
+             c.slo = P<uint16_t>(U("slo"));
+             c.sb = P<float>(U("sb"));
+             c.scoff = (int)I("scoff", 0);
+             c.lr = (float)D("lr", 1.0);
+             c.tracker = U("tracker");
+             c.Xt = P<const uint16_t>(U("Xt"));
+             c.yt = P<const int32_t>(U("yt"));
+             c.T = (int)I("T", 0);
+             c.acc = P<int>(U("acc"));
+             c.ticket = P<unsigned>(U("ticket"));
+             c.sink = U("sink");
+             c.log_server = I("log_server", 1) != 0;
+             c.api = U("api");
+             prepare_kernels();
+             return std::make_unique<BspLoop>(&solver, comm, c);
+           }),
+           py::arg("solver"), py::arg("comm"), py::arg("cfg"), py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def(
+          "run",
+          [](BspLoop& b, int64_t rounds, int64_t r0, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            return b.run(rounds, r0, S(stream));
+          },
+          py::arg("rounds"), py::arg("r0"), py::arg("stream"))
+      .def("flush", [](BspLoop& b, uintptr_t stream) { b.flush(S(stream)); })
+      .def_property("next_local", &BspLoop::next_local, &BspLoop::set_next_local)
+      .def_property_readonly("exhausted", &BspLoop::exhausted)
+      .def_property_readonly("host_us_per_round", &BspLoop::host_us_per_round);
   m.attr("ASYNC_DONE") = (int)kAsyncDone;
   m.attr("ASYNC_ERROR_TOKEN") = (int)kAsyncErrorToken;
   m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;

@@ -81,6 +81,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def_property_readonly("head", &SlidingWindow::head)
       .def_property_readonly("start", &SlidingWindow::start)
       .def_property_readonly("tuples_seen", &SlidingWindow::tuples_seen)
+      .def_property_readonly("handle", [](SlidingWindow& w) { return reinterpret_cast<uintptr_t>(&w); })
       .def("mean_interarrival_ms", &SlidingWindow::mean_interarrival_ms);
 
   py::class_<CsvInfo>(m, "CsvInfo")

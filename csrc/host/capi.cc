@@ -4,7 +4,9 @@
 #include <exception>
 #include <string>
 
+#include "dataset.h"
 #include "metrics_sink.h"
+#include "sampling.h"
 #include "tracker.h"
 
 namespace psx {
@@ -94,8 +96,49 @@ void c_submit(void* s, int slot, uint64_t seq, int kind, int64_t ts, int64_t par
 }
 const char* c_last_error() { return g_err.c_str(); }
 
-const HostApi kApi{kHostApiVersion, c_on_delta, c_retire, c_is_live, c_revive,  c_clock,
-                   c_sent,          c_pop,      c_push,   c_acquire, c_submit,  c_last_error};
+int64_t c_window_insert_many(void* w, const double* t, int64_t n) {
+  try {
+    g_err.clear();
+    return static_cast<SlidingWindow*>(w)->insert_many(t, n, nullptr);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  }
+  return -1;
+}
+int c_window_state(void* w, int64_t* size, int64_t* start, int64_t* seen) {
+  return guarded(
+      [&] {
+        auto* win = static_cast<SlidingWindow*>(w);
+        *size = win->size();
+        *start = win->size() > 0 ? win->start() : 0;
+        *seen = win->tuples_seen();
+        return 0;
+      },
+      -1);
+}
+int64_t c_due_rows(int k, int n, double p_ms, int64_t total, int64_t next_local, double now_ms, int64_t max_rows,
+                   double* times) {
+  try {
+    g_err.clear();
+    return due_rows(k, n, p_ms, total, next_local, now_ms, max_rows, times);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  }
+  return -1;
+}
+int c_bsp_round(void* t, int64_t v) {
+  return guarded(
+      [&] {
+        static_cast<VectorClockTracker*>(t)->bsp_round(v);
+        return 0;
+      },
+      -1);
+}
+
+const HostApi kApi{kHostApiVersion, c_on_delta,   c_retire,         c_is_live,       c_revive,
+                   c_clock,         c_sent,       c_pop,            c_push,          c_acquire,
+                   c_submit,        c_last_error, c_window_insert_many, c_window_state, c_due_rows,
+                   c_bsp_round};
 
 }  // namespace
 

@@ -13,7 +13,7 @@
 
 namespace psx {
 
-constexpr int kHostApiVersion = 1;
+constexpr int kHostApiVersion = 2;
 
 struct HostApi {
   int version;
@@ -36,6 +36,17 @@ struct HostApi {
   // Exceptions thrown by the functions above are caught at this boundary: the
   // message of the last failure on this thread (empty: none).
   const char* (*last_error)();
+  // ---- version 2: the native BSP round loop (csrc/runtime/bsp_loop.h) ----
+  // SlidingWindow (sampling.h): n arrivals -> slot of the first (the n slots are
+  // consecutive modulo the ring), -1 on error; the window after it.
+  int64_t (*window_insert_many)(void* window, const double* times_ms, int64_t n);
+  int (*window_state)(void* window, int64_t* size, int64_t* start, int64_t* seen);
+  // producer schedule (dataset.h due_rows): rows of worker k due by now_ms
+  int64_t (*due_rows)(int k, int num_workers, double p_ms, int64_t total_rows, int64_t next_local, double now_ms,
+                      int64_t max_rows, double* times_out);
+  // VectorClockTracker::bsp_round: every live worker's delta of round v received,
+  // the weights of v + 1 sent
+  int (*tracker_bsp_round)(void* tracker, int64_t v);
 };
 
 const HostApi* host_api();

@@ -72,3 +72,31 @@ def test_dist_engine_native_vs_torch_collectives(cuda, pg, monkeypatch):
     base = ws[("0", "allreduce")]
     for k, w in ws.items():
         assert torch.allclose(w, base, atol=1e-4 * max(1.0, base.abs().max().item())), k
+
+
+def test_dist_engine_native_bsp_loop_world1(cuda, pg, monkeypatch):
+    """The allreduce rank body in the native BSP loop (RCCL all-reduce + update
+    launch per round, rows riding in the solves) == the Python rank loop: same
+    model, same rows."""
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
+    res = []
+    for native in ("1", "0"):
+        monkeypatch.setenv("PSX_NATIVE_BSP", native)
+        cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                       rows_per_iter=64, epochs=100, max_iters=12, init="random", bsp_schedule="allreduce",
+                       min_buffer_size=256, max_buffer_size=256)
+        eng = DistEngine(cfg, 0, 1, cuda, train=train, test=test)
+        out = eng.run()
+        assert out["rounds"] == 12
+        assert hasattr(eng, "native_host_us_per_round") == (native == "1")
+        torch.cuda.synchronize()
+        book = eng.log.book
+        res.append((eng.server.w.cpu(), sorted((r[1], r[2], r[3]) for r in book.server),
+                    sorted((r[1], r[2], r[3], r[4], r[5], r[6]) for r in book.worker), eng.server.updates))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and [r[0] for r in res[0][1]] == list(range(12))
+    assert res[0][2] == res[1][2] and res[0][3] == res[1][3]

@@ -159,6 +159,46 @@ def test_riding_eval_matches_separate_launches(cuda, monkeypatch, N):
     assert len(res[0][2]) == 10 * N and res[0][2] == res[1][2]
 
 
+def test_native_bsp_loop_matches_python_loop(cuda, monkeypatch):
+    """The native BSP round loop (csrc/runtime/bsp_loop.h) logs exactly the rows of
+    the Python loop, ends at the same model, producer cursor, window and tracker."""
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    kw = dict(num_workers=1, max_iters=25, init="random", min_buffer_size=256, max_buffer_size=256,
+              rows_per_iter=96)
+    res = []
+    for native in ("1", "0"):
+        monkeypatch.setenv("PSX_NATIVE_BSP", native)
+        eng = LocalEngine(_cfg(**kw), cuda, train=train, test=test)
+        assert eng._native_bsp_ok() == (native == "1")
+        out = eng.run()
+        assert out.get("native_loop", False) == (native == "1")
+        torch.cuda.synchronize()
+        wk = eng.workers[0]
+        book = eng.log.book
+        res.append((eng.server.w.cpu(), sorted((r[1], r[2], r[3]) for r in book.server),
+                    sorted((r[1], r[2], r[3], r[4], r[5], r[6]) for r in book.worker),
+                    (wk.source.next_local, wk.window.size, wk.window.start, wk.tuples_seen, wk.vc, wk.iters,
+                     eng.server.updates, eng.server.tracker.min_clock())))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and [r[0] for r in res[0][1]] == list(range(25))
+    assert res[0][2] == res[1][2] and len(res[0][2]) == 25
+    assert res[0][3] == res[1][3]
+
+
+def test_native_bsp_loop_producer_clock(cuda):
+    """The native loop on the reference producer clock (-p): rows arrive by the
+    schedule, every round logs a worker and a server row."""
+    train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
+    eng = LocalEngine(_cfg(stream_mode="schedule", producer_time_per_event=2.0, max_iters=40, init="random"), cuda,
+                      train=train, test=test)
+    assert eng._native_bsp_ok()
+    out = eng.run()
+    assert out["native_loop"] and out["rounds"] == 40
+    book = eng.log.book
+    assert [r[1] for r in book.server] == list(range(40))
+    assert len(book.worker) == 40 and eng.workers[0].tuples_seen >= 128
+
+
 def test_concurrent_worker_lanes_match_sequential(cuda):
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     ws, books = [], []

@@ -43,6 +43,25 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Copy N 8-byte words global -> LDS with all of a thread's loads in flight
+// before its first store (a load -> wait -> store loop pays one memory round
+// trip per word).  NTHR threads take words tid, tid + NTHR, ...
+template <int N, int NTHR>
+__device__ __forceinline__ void copy_words_to_lds(unsigned long long* dst, const unsigned long long* src) {
+  constexpr int PER = (N + NTHR - 1) / NTHR;
+  unsigned long long v[PER];
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {
+    const int i = (int)threadIdx.x + NTHR * c;
+    v[c] = i < N ? src[i] : 0ull;
+  }
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {
+    const int i = (int)threadIdx.x + NTHR * c;
+    if (i < N) dst[i] = v[c];
+  }
+}
+
 // Dual-use LDS image of a [rows][128 x bf16] sub-tile with 256-B rows: row
 // reads (ds_read_b128) and transposed reads (ds_read_b64_tr_b16) share one
 // copy.  Byte offset of 16-B chunk `ch` (0..15) of `row`:

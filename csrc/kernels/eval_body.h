@@ -50,6 +50,8 @@ __device__ __forceinline__ void eval_body(char* lds, const EvalRide& r, int tile
   }
   for (int tile = tile0; tile < tend; tile += tstep) {
     const int nrows = min(32, T - tile * 32);
+    // the labels travel with the tile's loads (one memory round trip, not two)
+    const int ylab = tid < nrows ? r.yt[(size_t)tile * 32 + tid] : 0;
     stage_tile<FP>(lds, r.Xt, (int64_t)tile * 32, nrows, 0, false);
     __syncthreads();
     f32x4 a0, a1;
@@ -69,8 +71,7 @@ __device__ __forceinline__ void eval_body(char* lds, const EvalRide& r, int tile
           best = c;
         }
       }
-      int yl = r.yt[(size_t)tile * 32 + tid];
-      yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
+      const int yl = ylab < 0 ? 0 : (ylab > 15 ? 15 : ylab);
       atomicAdd(&cl[yl * 16 + best], 1);
       if (pair) {
         int best2 = 0;

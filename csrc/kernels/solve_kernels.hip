@@ -186,6 +186,21 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
     if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
   }
   if (blockIdx.x == 0 && t < 16 && t < cfg.K) b_pre = dv.w_old[cfg.K * FP + t];
+  // the first batch of the window read is issued before the ingest copy (which
+  // waits on its own loads): the old rows' XT pieces do not depend on it
+  const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
+  const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
+  constexpr int U = 4;       // pieces per lane in flight
+  u16x8 v[U];
+  auto load_pieces = [&](int q0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qq = q0 + kStatL * u;
+      const int qc = qq < nq ? qq : nq - 1;
+      v[u] = *(const u16x8*)(xt + wt.ring_tile(qc >> 2) * 32 + (qc & 3) * 8);
+    }
+  };
+  load_pieces(j);
   for (int i = t; i < nin; i += 256) {  // fused ingest: one 16-B chunk of each new row
     const long long sr = ing.first + (long long)i * ing.step;
     int dr = ing.dst + i;
@@ -199,18 +214,9 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   }
   // the newest min(nin, B) window rows are the fused ones: counted from LDS
   const int bold = B - (nin < B ? nin : B);
-  const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
-  const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
   float s = 0.f, q = 0.f;
-  constexpr int U = 4;  // pieces per lane in flight
   for (int q0 = j; q0 < nq; q0 += kStatL * U) {
-    u16x8 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int qq = q0 + kStatL * u;
-      const int qc = qq < nq ? qq : nq - 1;
-      v[u] = *(const u16x8*)(xt + wt.ring_tile(qc >> 2) * 32 + (qc & 3) * 8);
-    }
+    if (q0 != j) load_pieces(q0);  // (the first batch was issued at entry)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int qq = q0 + kStatL * u;
@@ -310,11 +316,12 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
   for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
+    const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads (one round trip)
     if constexpr (kF32)
       stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
     else
       stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
-    if (tid < 32) ylds[tid] = dv.y[row0 + tid];
+    if (tid < 32) ylds[tid] = yv;
     __syncthreads();
     // converged in an earlier slot: exit (the phase word was loaded at kernel
     // entry, so its latency overlapped the tile staging; nothing written yet)
@@ -452,10 +459,6 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   float* pr = (float*)(gat + kMaxSlices * kNDX);           // [15][17] fwd-partial stripes
   CtrlScratch* csw = (CtrlScratch*)(pr + 256);
   unsigned long long* xch = dv.xch;
-  {  // every workgroup runs the (deterministic) controller on its own LDS copy
-    constexpr int CW = sizeof(Ctrl) / 8;
-    for (int i = tid; i < CW; i += 256) ((unsigned long long*)cl)[i] = ((const unsigned long long*)gctrl)[i];
-  }
 
   const int B = win.B, cap = cfg.cap, K = cfg.K, H = cfg.hist;
   const WinTiles wt(win.start, B, cap);
@@ -465,6 +468,37 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   const int fl = tid & 31, cgp = tid >> 5;
   const int f = fs + fl;
   const bool wg0 = wg == 0;
+  const int ntiles = wt.nt;
+
+  // ---- the backward's operands first: the residual tiles R (fwd output) and
+  // the feature-major window XT of this slice, kBwdBatch k-steps per wave in
+  // flight -- issued ahead of every other load so that one memory round trip
+  // covers them, the controller copy and the per-element state together ----
+  const bool gred = dv.gpart != nullptr;
+  const int m16 = lane & 15, kg = (lane >> 4) * 8;
+  const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
+  const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
+  const unsigned short* rp0 = dv.R + m16 * 32 + kg;
+  const bool live = m16 < K;  // padding-class rows of R are neither written nor read
+  u16x8 ah[kBwdBatch], al[kBwdBatch], b0[kBwdBatch], b1[kBwdBatch];
+  auto load_batch = [&](int kb) {
+#pragma unroll
+    for (int u = 0; u < kBwdBatch; ++u) {  // every load of the batch in flight together
+      const int i = kb + w + 4 * u;
+      const int ic = i < ntiles ? i : ntiles - 1;
+      const size_t ro = (size_t)wt.ring_tile(ic) * 32;
+      ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (live) {
+        ah[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024);
+        al[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024 + 512);
+      }
+      b0[u] = *(const u16x8*)(xt0 + ro);
+      b1[u] = *(const u16x8*)(xt1 + ro);
+    }
+  };
+  if (!gred) load_batch(0);
+  // every workgroup runs the (deterministic) controller on its own LDS copy
+  copy_words_to_lds<sizeof(Ctrl) / 8, 256>((unsigned long long*)cl, (const unsigned long long*)gctrl);
 
   // ---- per-element state first (independent of the backward) ----
   float DD[NE], GC[NE], XO[NE], FX[NE];
@@ -481,7 +515,6 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     FX[e] = dv.wfix[idx[e]];
   }
   const float iv = dv.inv_std[f];
-  const int ntiles = wt.nt;
   const int nfw = ntiles < fwd_grid ? ntiles : fwd_grid;
   float db0 = 0.f, gcb0 = 0.f, xb0 = 0.f;
   if (wg0 && tid < 255) {  // intercept gradient / loss partials: 15 stripes x 17 values, fixed order
@@ -501,29 +534,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // ---- backward G[c][slice] = sum_r R[r][c] X[r][slice] ----
   // (rows mode: partial sums of the fwdbwd_rows workgroups, already reduced by
   // reduce_g into dv.gred for large grids, summed here in a fixed order otherwise)
-  const bool gred = dv.gpart != nullptr;
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
   if (!gred) {
-    const int m16 = lane & 15, kg = (lane >> 4) * 8;
-    const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
-    const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
-    const unsigned short* rp0 = dv.R + m16 * 32 + kg;
-    const bool live = m16 < K;
     for (int kb = 0; kb < ntiles; kb += 4 * kBwdBatch) {
-      u16x8 ah[kBwdBatch], al[kBwdBatch], b0[kBwdBatch], b1[kBwdBatch];
-#pragma unroll
-      for (int u = 0; u < kBwdBatch; ++u) {  // every load of the batch in flight together
-        const int i = kb + w + 4 * u;
-        const int ic = i < ntiles ? i : ntiles - 1;
-        const size_t ro = (size_t)wt.ring_tile(ic) * 32;
-        ah[u] = al[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (live) {  // padding-class rows of R are neither written nor read
-          ah[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024);
-          al[u] = *(const u16x8*)(rp0 + (size_t)ic * 1024 + 512);
-        }
-        b0[u] = *(const u16x8*)(xt0 + ro);
-        b1[u] = *(const u16x8*)(xt1 + ro);
-      }
+      if (kb > 0) load_batch(kb);  // (batch 0 was issued at entry)
 #pragma unroll
       for (int u = 0; u < kBwdBatch; ++u) {
         const int i = kb + w + 4 * u;

@@ -507,7 +507,20 @@ __device__ __forceinline__ void wide_dots_body(const WideCfg& c, const WideDev& 
   constexpr int kCW = (int)(sizeof(Ctrl) / 8);
   unsigned long long* cg = reinterpret_cast<unsigned long long*>(ctrl);
   unsigned long long* cs = reinterpret_cast<unsigned long long*>(&sh.ctrl);
-  for (int i = threadIdx.x; i < kCW; i += nthr) cs[i] = cg[i];
+  {  // all of a thread's words in flight before its first store (nthr >= 256)
+    constexpr int kPer = (kCW + 255) / 256;
+    unsigned long long cv[kPer];
+#pragma unroll
+    for (int c2 = 0; c2 < kPer; ++c2) {
+      const int i = (int)threadIdx.x + nthr * c2;
+      cv[c2] = i < kCW ? cg[i] : 0ull;
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < kPer; ++c2) {
+      const int i = (int)threadIdx.x + nthr * c2;
+      if (i < kCW) cs[i] = cv[c2];
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (stp) stp[3] = (long long)__builtin_amdgcn_s_memrealtime();

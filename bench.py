@@ -79,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
+    ap.add_argument("--persist", action="store_true",
+                    help="dense: each local solve as ONE persistent launch (tile-resident, in-launch hand-offs)")
     ap.add_argument("--async-scheduler", default="auto", choices=["auto", "events", "threads"],
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--rccl-trace", action="store_true",
@@ -122,7 +124,7 @@ def build_cfg(a, n_workers):
         dtype=a.dtype,
         sigmoid=a.model == "sharded100m",
         solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
-                             zero_const=not wide),
+                             zero_const=not wide, persist=True if a.persist else None),
         bsp_schedule=a.schedule,
         server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,

@@ -90,7 +90,8 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("nslots", &SolverCfg::nslots)
       .def_readwrite("gd_lr", &SolverCfg::gd_lr)
       .def_readwrite("tol", &SolverCfg::tol)
-      .def_readwrite("xf32", &SolverCfg::xf32);
+      .def_readwrite("xf32", &SolverCfg::xf32)
+      .def_readwrite("persist", &SolverCfg::persist);
 
   py::class_<LocalSolver>(m, "LocalSolver")
       .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t XT, uintptr_t y, uintptr_t w_old,
@@ -184,6 +185,7 @@ PYBIND11_MODULE(_psx_hip, m) {
           py::arg("slot2") = 0, py::arg("seq2") = 0, py::arg("ap_w") = 0, py::arg("ap_lr") = 1.f,
           py::arg("ap_hi") = 0, py::arg("ap_lo") = 0, py::arg("ap_b") = 0, py::arg("ap_coff") = 0)
       .def_property_readonly("eager", &LocalSolver::eager)
+      .def_property_readonly("persistent", &LocalSolver::persistent)
       .def("read_ctrl",
            [](LocalSolver& s, uintptr_t stream) {
              Ctrl c;

@@ -14,6 +14,7 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double double2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ unsigned short f2bf(float f) {
   unsigned u = __float_as_uint(f);
@@ -60,6 +61,47 @@ __device__ __forceinline__ void copy_words_to_lds(unsigned long long* dst, const
     const int i = (int)threadIdx.x + NTHR * c;
     if (i < N) dst[i] = v[c];
   }
+}
+
+// ---- in-launch hand-offs between workgroups (persistent solve) ----------
+// Write-through (sc1) stores and L1-bypassing (sc1) loads: the R1 form of the
+// CDNA4 playbook's hand-off -- every handed-off byte is stored sc1 and drained
+// (s_waitcnt vmcnt(0)) before the arrival that publishes it, and EVERY load of
+// it is an sc1 load, so no release / acquire fence (buffer_wbl2 / buffer_inv)
+// is needed.  4- and 8-byte accesses: agent-scope relaxed atomics on global
+// pointers; 16 bytes: raw buffer ops with aux = sc1.
+typedef __attribute__((address_space(1))) float g_f32;
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAuxSc1 = 16;
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load((g_f32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store((g_f32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((g_u64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u16x8 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, kAuxSc1));
+}
+__device__ __forceinline__ void st_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned byte_off, u16x8 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)byte_off, 0, kAuxSc1);
+}
+__device__ __forceinline__ void st_sc1_f32(__amdgpu_buffer_rsrc_t r, unsigned byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)byte_off, 0, kAuxSc1);
+}
+__device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, kAuxSc1));
 }
 
 // Dual-use LDS image of a [rows][128 x bf16] sub-tile with 256-B rows: row

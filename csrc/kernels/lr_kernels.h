@@ -9,7 +9,7 @@ namespace psx {
 
 // Row tile and dynamic LDS footprint of the tile kernels for a padded width FP.
 constexpr int kTileRows = 32;
-inline size_t eval_lds_bytes(int FP) { return (size_t)kTileRows * FP * 2 + 8192 + 2048 + 1024 + 512; }
+PSX_HD constexpr size_t eval_lds_bytes(int FP) { return (size_t)kTileRows * FP * 2 + 8192 + 2048 + 1024 + 512; }
 bool fp_supported(int FP);
 // Raise dynamic-LDS limits for the wide tile kernels (call before capture).
 void prepare_kernels();

@@ -40,6 +40,10 @@ struct SolveDev {
   double* spart;  // [G][2][FP] partial column sums / sums of squares
   float* gred;    // [KP][FPI] reduced gradient sums (bwd_update reads them when non-null)
   const float* Xf;  // fp32 ring rows [cap][Fp] (cfg.xf32; X is then unused)
+  // feature-major gradient partials [fwd workgroup][FP][KP] (the "gpf" backward of
+  // the small-window solve: each forward workgroup's R^T X of its LDS tile; the
+  // slice owners reduce them with 16-B loads).  nullptr: the XT backward.
+  float* gpf;
   // optional server update fused into the finalisation (a colocated server whose
   // model is this worker's pulled w_old, e.g. BSP with one worker): ap_w (may be
   // w_old itself) = w_old + ap_lr * delta, fragments at columns ap_coff of
@@ -106,6 +110,15 @@ void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int sl
 void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
                       hipStream_t s, const SolveParams& win, const struct EvalRide& ride, int ride_t0, int nride);
 size_t stats_rows_lds_bytes();
+
+// ---- persistent small-window solve: the whole solve in ONE launch (see
+// solve_kernels.hip); G = persist_grid(FP, window tiles) co-resident
+// workgroups + `nride` evaluation workgroups of `ride` (tiles [0, nride)) ----
+bool persist_supported(int FP, int KP);
+int persist_grid(int FP, int ntiles);
+size_t persist_lds_bytes(int FP);
+void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
+                    const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s);
 // fp32 ring rows: rows src_first + i*src_step -> slots (dst_first + i) % cap
 void launch_ring_ingest_f32(const float* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
                             float* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s);

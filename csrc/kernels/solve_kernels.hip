@@ -70,7 +70,10 @@ constexpr int kNDX = kND + 1;          // + loss
 constexpr int kMaxSlices = 2048 / 32;
 constexpr int kXchBar = kMaxSlices * 2 * kNDX;  // [slices][2*kNDX] dot granules, then the tail barrier counter
 constexpr int kXchErr = kXchBar + 1;
-int xch_words() { return kXchErr + 1; }
+constexpr int kXchPhase = kXchErr + 1;  // persistent solve: the controller phase after a slot (wg 0 -> row-only wgs)
+constexpr int kXchGen = kXchPhase + 1;  // persistent solve: the barrier counters of even / odd runs
+constexpr int kXchRide = kXchGen + 2;   // persistent solve: riding workgroups done, even / odd runs
+int xch_words() { return kXchRide + 2; }
 constexpr int kPartStride = 32;  // fwd partials per workgroup: rsum[16], loss
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -287,7 +290,10 @@ __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned sho
 // kF32 (rows mode only): fp32 ring rows staged as hi + lo bf16 images (the lo
 // image right after the hi one), forward x_hi.(W_hi + W_lo) + x_lo.W_hi and
 // backward (R_hi + R_lo)^T x_hi + R_hi^T x_lo -- near-fp32 products on bf16 MFMA.
-template <int FP, bool kRows = false, bool kF32 = false>
+// kP (persistent solve): the tile and its labels are already resident in LDS,
+// and the trial point (fragments, intercepts) is read / the partials written
+// with sc1 accesses (an in-launch hand-off, see common.h).
+template <int FP, bool kRows = false, bool kF32 = false, bool kP = false>
 __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams pr, int slot, const SolveDev& dv,
                                          char* lds, const int wg, const int G, f32x4* gacc = nullptr,
                                          const int entry_phase = -1) {
@@ -308,20 +314,29 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   float loss = 0.f;
   const int sr = tid >> 3, sc0 = (tid & 7) * 2;
   float rs0 = 0.f, rs1 = 0.f;
-  const float bz0 = dv.b_eff[sc0], bz1 = dv.b_eff[sc0 + 1];
+  static_assert(!kP || (FP <= 1024 && kRows && !kF32), "persistent solve: rows-form bodies, FP <= 1024");
+  const float bz0 = kP ? ld_sc1(dv.b_eff + sc0) : dv.b_eff[sc0];
+  const float bz1 = kP ? ld_sc1(dv.b_eff + sc0 + 1) : dv.b_eff[sc0 + 1];
   // the trial weights do not depend on the tile: fetch them before staging so
   // the two memory latencies overlap (register budget allows it up to FP 1024)
   constexpr bool kPre = FP <= 1024;
   WFrag<kPre ? FP : 128> wf;
-  if constexpr (kPre) load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
+  if constexpr (kPre) {
+    if constexpr (kP)
+      load_wfrag_sc1<FP>(wf, dv.whi, dv.wlo, K);
+    else
+      load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
+  }
   for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-    const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads (one round trip)
-    if constexpr (kF32)
-      stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
-    else
-      stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
-    if (tid < 32) ylds[tid] = yv;
+    if constexpr (!kP) {  // (persistent: staged once, at the start of the solve)
+      const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads (one round trip)
+      if constexpr (kF32)
+        stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
+      else
+        stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
+      if (tid < 32) ylds[tid] = yv;
+    }
     __syncthreads();
     // converged in an earlier slot: exit (the phase word was loaded at kernel
     // entry, so its latency overlapped the tile staging; nothing written yet)
@@ -399,8 +414,15 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   if (lane == 0) lred[w] = loss;
   __syncthreads();
   float* part = dv.part + (size_t)wg * kPartStride;
-  if (tid < 16) part[tid] = ((rsum[tid] + rsum[16 + tid]) + rsum[32 + tid]) + rsum[48 + tid];
-  if (tid == 16) part[16] = lred[0] + lred[1] + lred[2] + lred[3];
+  float pv = 0.f;
+  if (tid < 16) pv = ((rsum[tid] + rsum[16 + tid]) + rsum[32 + tid]) + rsum[48 + tid];
+  if (tid == 16) pv = lred[0] + lred[1] + lred[2] + lred[3];
+  if (tid < 17) {
+    if constexpr (kP)
+      st_sc1(part + tid, pv);
+    else
+      part[tid] = pv;
+  }
   if (wg == 0 && tid == 0) stamp(dv, slot, 1);
 }
 
@@ -411,12 +433,70 @@ __device__ __forceinline__ SolveParams window_of(const SolveParams& win, const S
   return win.B > 0 ? win : *prm;
 }
 
+// A forward workgroup's partial gradient sums R^T X (classes < KP) -> gpf[wg][f][KP]:
+// a lane's 4 classes of one feature are contiguous -> one 16-B store (sc1 inside
+// the persistent solve, plain behind a kernel boundary).
+template <int FP, bool kSc1>
+__device__ __forceinline__ void store_gpf(const SolveDev& dv, int wg, int G, const f32x4* acc) {
+  constexpr int NT = FP / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, KP = dv.KP;
+  const int c0 = (lane >> 4) * 4;
+  const auto rg = rsrc_of(dv.gpf, (unsigned)((size_t)G * KP * FP * 4));
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int f = (w * NT + n) * 16 + (lane & 15);
+    const size_t eo = ((size_t)wg * FP + f) * KP + c0;
+    if (KP >= 4) {
+      if (c0 < KP) {
+        if constexpr (kSc1)
+          st_sc1_b128(rg, (unsigned)(eo * 4), __builtin_bit_cast(u16x8, acc[n]));
+        else
+          *(f32x4*)(dv.gpf + eo) = acc[n];
+      }
+    } else if (c0 == 0) {
+      if constexpr (kSc1) {
+        st_sc1_f32(rg, (unsigned)(eo * 4), acc[n][0]);
+        st_sc1_f32(rg, (unsigned)(eo * 4) + 4, acc[n][1]);
+      } else {
+        dv.gpf[eo] = acc[n][0];
+        dv.gpf[eo + 1] = acc[n][1];
+      }
+    }
+  }
+}
+
+// Forward of the slot's trial point; with dv.gpf also the backward's partial
+// sums R^T X of the workgroup's tile, while the tile is in LDS.
+template <int FP, bool kGpf>
+__device__ __forceinline__ void fwd_slot(const SolverCfg& cfg, const SolveParams pr, int slot, const SolveDev& dv,
+                                         char* lds, const int wg, const int G, const int entry_phase) {
+  if constexpr (kGpf) {
+    constexpr int NT = FP / 64;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
+    const WinTiles wt(pr.start, pr.B, cfg.cap);
+    if (wg >= wt.nt) return;
+    fwd_body<FP, true>(cfg, pr, slot, dv, lds, wg, G, acc, entry_phase);
+    if (entry_phase == kPhDone) return;  // (converged earlier: fwd_body left after staging)
+    store_gpf<FP, false>(dv, wg, G, acc);
+  } else {
+    fwd_body<FP>(cfg, pr, slot, dv, lds, wg, G, nullptr, entry_phase);
+  }
+}
+
 template <int FP>
 __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolveParams* prm, const Ctrl* ctrl, int slot,
                                                   SolveDev dv, SolveParams win) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int phase = ctrl->phase;  // checked once the first tile is staged
-  fwd_body<FP>(cfg, window_of(win, prm), slot, dv, lds, blockIdx.x, gridDim.x, nullptr, phase);
+  if constexpr (FP <= 1024) {
+    if (dv.gpf) {
+      fwd_slot<FP, true>(cfg, window_of(win, prm), slot, dv, lds, blockIdx.x, gridDim.x, phase);
+      return;
+    }
+  }
+  fwd_slot<FP, false>(cfg, window_of(win, prm), slot, dv, lds, blockIdx.x, gridDim.x, phase);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,8 +518,12 @@ size_t bwd_lds_bytes() {
          (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) + sizeof(CtrlScratch);
 }
 
-// Body shared by bwd_update_kernel and tail_kernel: slice `wg` of `NS`.
-template <int FP, int KP>
+// Body shared by bwd_update_kernel, tail_kernel and the persistent solve: slice
+// `wg` of `NS`.  kP (persistent solve): the controller copy in LDS persists
+// across slots (no copy-in / write-back), the partials written by other
+// workgroups of the launch are read with sc1 loads and the next trial point is
+// published with sc1 stores (common.h).
+template <int FP, int KP, bool kP = false>
 __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
                                          const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
                                          const bool check_done = false) {
@@ -474,7 +558,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // the feature-major window XT of this slice, kBwdBatch k-steps per wave in
   // flight -- issued ahead of every other load so that one memory round trip
   // covers them, the controller copy and the per-element state together ----
-  const bool gred = dv.gpart != nullptr;
+  const bool gpf = dv.gpf != nullptr;                // partials of the forward workgroups, [g][f][KP]
+  const bool gred = !gpf && dv.gpart != nullptr;     // rows mode: partials [g][KP][FP]
   const int m16 = lane & 15, kg = (lane >> 4) * 8;
   const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
   const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
@@ -496,9 +581,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       b1[u] = *(const u16x8*)(xt1 + ro);
     }
   };
-  if (!gred) load_batch(0);
+  if (!gred && !gpf) load_batch(0);
   // every workgroup runs the (deterministic) controller on its own LDS copy
-  copy_words_to_lds<sizeof(Ctrl) / 8, 256>((unsigned long long*)cl, (const unsigned long long*)gctrl);
+  if constexpr (!kP)
+    copy_words_to_lds<sizeof(Ctrl) / 8, 256>((unsigned long long*)cl, (const unsigned long long*)gctrl);
 
   // ---- per-element state first (independent of the backward) ----
   float DD[NE], GC[NE], XO[NE], FX[NE];
@@ -521,7 +607,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     const int k = tid % 17, g0 = tid / 17;
     float a = 0.f;
 #pragma unroll 4
-    for (int s = g0; s < nfw; s += 15) a += dv.part[(size_t)s * kPartStride + k];
+    for (int s = g0; s < nfw; s += 15) {
+      const float* pp = dv.part + (size_t)s * kPartStride + k;
+      a += kP ? ld_sc1(pp) : *pp;
+    }
     pr[g0 * 17 + k] = a;
   }
   if (wg0 && tid < 16) {
@@ -535,7 +624,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // (rows mode: partial sums of the fwdbwd_rows workgroups, already reduced by
   // reduce_g into dv.gred for large grids, summed here in a fixed order otherwise)
   f32x4 acc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  if (!gred) {
+  if (!gred && !gpf) {
     for (int kb = 0; kb < ntiles; kb += 4 * kBwdBatch) {
       if (kb > 0) load_batch(kb);  // (batch 0 was issued at entry)
 #pragma unroll
@@ -549,10 +638,51 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       }
     }
   }
+  if (gpf) {
+    // the slice's [32 f][KP c] partials of every tile are contiguous (1 KB for KP 8):
+    // thread = (16-B piece p, tile group q of 4); all its tiles' loads in flight,
+    // summed in tile order, then the 4 groups in order -> gw[c][f]
+    constexpr int NP = 32 * KP / 4;  // 16-B pieces of a slice (KP >= 4); KP 2: 8-B pieces
+    const int nfw_g = wt.nt < fwd_grid ? wt.nt : fwd_grid;
+    const int p = tid % 64, q = tid / 64;
+    float* red = (float*)(gw + 16 * 32);  // [4 groups][64 pieces][4] (gw's other waves' rows)
+    f32x4 a = f32x4{0, 0, 0, 0};
+    if (p < NP && KP >= 4) {
+      // (persistent solve: sc1 loads of the in-launch hand-off; chain: plain loads
+      // behind the kernel boundary)
+      const auto rg = rsrc_of(dv.gpf, (unsigned)((size_t)fwd_grid * KP * FP * 4));
+      constexpr int UG = 17;
+      for (int g0 = q; g0 < nfw_g; g0 += 4 * UG) {
+        u16x8 v[UG];
+#pragma unroll
+        for (int u = 0; u < UG; ++u) {
+          const int g = g0 + 4 * u;
+          const size_t eo = ((size_t)g * FP + fs) * KP + p * 4;
+          v[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+          if (g < nfw_g) v[u] = kP ? ld_sc1_b128(rg, (unsigned)(eo * 4)) : *(const u16x8*)(dv.gpf + eo);
+        }
+#pragma unroll
+        for (int u = 0; u < UG; ++u) a += __builtin_bit_cast(f32x4, v[u]);
+      }
+    } else if (p < 16 && KP == 2) {  // 32 features x 2 classes = 16 x 16 B as well
+      for (int g = q; g < nfw_g; g += 4) {
+        const float* src = dv.gpf + ((size_t)g * FP + fs) * KP + p * 4;
+        a += kP ? f32x4{ld_sc1(src), ld_sc1(src + 1), ld_sc1(src + 2), ld_sc1(src + 3)} : *(const f32x4*)src;
+      }
+    }
+    *(f32x4*)(red + (q * 64 + p) * 4) = a;
+    __syncthreads();
+    // thread (cgp = class, fl = feature): element (f, c) sits in piece (fl * KP + c) / 4
+    if (cgp < KP && cgp < 8) {
+      const int pc = fl * KP + cgp, pp = pc >> 2, lanei = pc & 3;
+      gw[cgp * 32 + fl] = ((red[(0 * 64 + pp) * 4 + lanei] + red[(1 * 64 + pp) * 4 + lanei]) +
+                           red[(2 * 64 + pp) * 4 + lanei]) + red[(3 * 64 + pp) * 4 + lanei];
+    }
+  }
   if (wg0 && tid == 0) stamp(dv, slot, 3);
   wg_stamp(dv, slot, 1, wg);
   // cross-wave reduction of the accumulators (D[class][feature])
-  if (!gred) {
+  if (!gred && !gpf) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -571,7 +701,9 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   for (int e = 0; e < NE; ++e) {
     const int c = (cgp + 8 * e) & 15;
     float s;
-    if (!gred) {
+    if (gpf) {  // reduced from the forward partials above
+      s = own[e] ? gw[c * 32 + fl] : 0.f;
+    } else if (!gred) {
       s = gw[c * 32 + fl] + gw[(16 + c) * 32 + fl] + gw[(32 + c) * 32 + fl] + gw[(48 + c) * 32 + fl];
     } else if (dv.gred) {
       s = own[e] ? dv.gred[idx[e]] : 0.f;
@@ -585,7 +717,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
         for (int g0 = 0; g0 < nfw_g; g0 += U) {
           float v[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) v[u] = g0 + u < nfw_g ? src[(size_t)(g0 + u) * stride] : 0.f;
+          for (int u = 0; u < U; ++u) {
+            const float* q = src + (size_t)(g0 + u) * stride;
+            v[u] = g0 + u < nfw_g ? (kP ? ld_sc1(q) : *q) : 0.f;
+          }
 #pragma unroll
           for (int u = 0; u < U; ++u) s += v[u];
         }
@@ -725,7 +860,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     if (wg0) stamp(dv, slot, 6);
   }
   __syncthreads();
-  if (wg0) {  // the next launches read the controller from global memory
+  if (!kP && wg0) {  // the next launches read the controller from global memory
     constexpr int CW = sizeof(Ctrl) / 8;
     for (int i = tid; i < CW; i += 256) ((unsigned long long*)gctrl)[i] = ((const unsigned long long*)cl)[i];
   }
@@ -820,12 +955,24 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
         frl[512 + o] = l;
       }
     }
-    if (ib) dv.b_eff[tid] = xbv + t_next * dbv;
+    if (ib) {
+      if constexpr (kP)
+        st_sc1(dv.b_eff + tid, xbv + t_next * dbv);
+      else
+        dv.b_eff[tid] = xbv + t_next * dbv;
+    }
     __syncthreads();
     if (tid < 128) {
       const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
       uint16_t* dst = tid < 64 ? dv.whi : dv.wlo;
-      *(u16x8*)(dst + go) = *(const u16x8*)(frl + tid * 8);
+      if constexpr (kP) {  // (wave-uniform buffer: wave 0 the hi, wave 1 the lo fragments)
+        const u16x8 v = *(const u16x8*)(frl + tid * 8);
+        if (tid < 64)
+          st_sc1_b128(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), v);
+        else
+          st_sc1_b128(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), v);
+      } else
+        *(u16x8*)(dst + go) = *(const u16x8*)(frl + tid * 8);
     }
   }
   if (wg0 && tid == 0) stamp(dv, slot, 8);
@@ -887,8 +1034,10 @@ template <int KP>
 struct FinIn {
   float iv, xv[KP], fx[KP], wo[KP];
   __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
+    load_f(cfg, dv, blk * 256 + threadIdx.x);
+  }
+  __device__ __forceinline__ void load_f(const SolverCfg& cfg, const SolveDev& dv, int f) {
     const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
-    const int f = blk * 256 + threadIdx.x;
     if (f >= FP) return;
     iv = dv.inv_std[f];
 #pragma unroll
@@ -901,11 +1050,8 @@ struct FinIn {
 };
 
 template <int KP>
-__device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk,
-                                              const FinIn<KP>& in) {
+__device__ __forceinline__ void finalize_feature(const SolverCfg& cfg, const SolveDev& dv, int f, const FinIn<KP>& in) {
   const int FP = cfg.Fp, K = cfg.K;
-  const int f = blk * 256 + threadIdx.x;
-  if (blk == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
   if (f < FP) {
     const float iv = in.iv;
     const float *xv = in.xv, *fx = in.fx, *wo = in.wo;
@@ -934,7 +1080,13 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
       }
     }
   }
-  if (blk == 0 && threadIdx.x == 0) {
+}
+
+// The intercepts, the loss and the solver statistics (one thread).
+template <int KP>
+__device__ __forceinline__ void finalize_scalars(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv) {
+  const int FP = cfg.Fp, K = cfg.K;
+  {
     const int IB = dv.KP * dv.FPI;
     float bv[16];
     float mean = 0.f;
@@ -974,6 +1126,14 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
       }
     }
   }
+}
+
+template <int KP>
+__device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk,
+                                              const FinIn<KP>& in) {
+  if (blk == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
+  finalize_feature<KP>(cfg, dv, blk * 256 + threadIdx.x, in);
+  if (blk == 0 && threadIdx.x == 0) finalize_scalars<KP>(cfg, ctrl, dv);
 }
 
 template <int KP>
@@ -1017,7 +1177,14 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
       __syncthreads();
       if (phase_s == kPhDone) break;  // uniform: every workgroup read the same word after the barrier
     }
-    fwd_body<FP>(cfg, *prm, slot, dv, lds, wg, G);
+    if constexpr (FP <= 1024) {
+      if (dv.gpf)
+        fwd_slot<FP, true>(cfg, *prm, slot, dv, lds, wg, G, -1);
+      else
+        fwd_slot<FP, false>(cfg, *prm, slot, dv, lds, wg, G, -1);
+    } else {
+      fwd_body<FP>(cfg, *prm, slot, dv, lds, wg, G);
+    }
     grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
     if (wg < ns) bwd_body<FP, KP>(cfg, *prm, gctrl, slot, dv, G, lds, wg, ns);
     grid_barrier(bar, (unsigned long long)G * ++nb, dv.xch + kXchErr);
@@ -1422,6 +1589,370 @@ void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* c
   reduce_g_kernel<<<(n + 63) / 64, 256, 0, s>>>(cfg, prm, ctrl, dv, G);
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent small-window solve: the WHOLE local solve in ONE launch.
+//
+// The launch chain above (stats_prep, 2 launches per slot, tail) pays a kernel
+// boundary (~1.5-2 us) per phase, and every launch re-reads its operands from
+// memory: each kernel start meets cold caches, so the per-slot chain is bounded
+// by memory round trips, not by work (profiles/r02_v3).  Here G = max(window
+// tiles, FP/32) co-resident workgroups keep their 32-row window tile (and its
+// labels) resident in LDS for the whole solve, and run
+//   S  stage the tile (new stream rows straight from the dataset: the fused
+//      ingest), per-tile column sums                     -> spart[wg]
+//   P  slice owners: window statistics of their 32 features, x0, the first
+//      trial point's fragments, the controller (every workgroup its own copy)
+//   per slot:  row role   forward + softmax + R^T X of the resident tile -> gpart[wg]
+//              slice role  G = sum of the partials (fixed order), the dots
+//                          all-gather, controller step, update, next fragments
+//   F  slice owners finalise their features (+ the fused server update)
+// with a grid-wide arrival counter between the phases.  Every hand-off between
+// workgroups is the R1 form of the CDNA4 playbook: sc1 (write-through) stores,
+// each storing wave drained before the arrival, sc1 loads on the consumer side
+// -- no release / acquire fences.  The counters are monotone within a run; the
+// two generations alternate between runs and the finalisation re-arms the next
+// one.  Spins are bounded (a timeout sets the sticky error word).  Workgroups
+// >= G evaluate test tiles (a riding evaluation pass) and never wait.
+__device__ __forceinline__ void p_barrier(unsigned long long* ctr, unsigned long long target, unsigned long long* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    (void)__hip_atomic_fetch_add((g_u64*)ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (xload(ctr) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 22)) {  // never expected: record and fall through rather than hang
+        xstore(err, 3ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+PSX_HD constexpr size_t persist_fwd_bytes(int FP) { return (eval_lds_bytes(FP) + 15) / 16 * 16; }
+size_t persist_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (bwd_lds_bytes() + 15) / 16 * 16; }
+int persist_grid(int FP, int ntiles) { return ntiles > FP / 32 ? ntiles : FP / 32; }
+
+// Phase S (row role): stage ring tile `tile` of the window into the LDS image
+// (rows that arrived since the last solve come straight from the dataset and
+// are also written into the ring X / XT / y), then the tile's column sums and
+// sums of squares over its window rows -> spart[tile][2][FP] (sc1).
+template <int FP>
+__device__ __forceinline__ void persist_stage(const SolverCfg& cfg, const SolveDev& dv, char* lds, char* scratch,
+                                              const WinTiles& wt, int tile, int B, const RingIngest& ing) {
+  constexpr int CPR = FP / 8;            // 16-B chunks per row
+  constexpr int PER_T = 32 * CPR / 256;  // chunks per thread
+  constexpr int L = 256 / CPR;           // row groups of the column sums
+  static_assert(CPR * L == 256, "FP in {128..1024}");
+  const int tid = threadIdx.x;
+  const int64_t cap = cfg.cap;
+  const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
+  int* ylds = (int*)(lds + 32 * FP * 2 + 8192 + 2048);
+  auto new_row = [&](int64_t slot) -> int {  // index of `slot` among the new rows, -1 if old
+    if (ing.n <= 0) return -1;
+    int64_t i = slot - ing.dst;
+    if (i < 0) i += cap;
+    return i < ing.n ? (int)i : -1;
+  };
+  int yv = 0, yi = -1;
+  if (tid < 32) {
+    yi = new_row(row0 + tid);
+    yv = yi >= 0 ? ing.ysrc[ing.first + (int64_t)yi * ing.step] : dv.y[row0 + tid];
+  }
+  u16x8 v[PER_T];
+  int ni[PER_T];
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {  // every load of the tile in flight together
+    const int q = tid + 256 * j, row = q / CPR, cg = q - row * CPR;
+    ni[j] = new_row(row0 + row);
+    const uint16_t* src = ni[j] >= 0 ? ing.src + (ing.first + (int64_t)ni[j] * ing.step) * FP
+                                     : dv.X + (row0 + row) * FP;
+    v[j] = *(const u16x8*)(src + cg * 8);
+  }
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int q = tid + 256 * j, row = q / CPR, cg = q - row * CPR;
+    *(u16x8*)(lds + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+    if (ni[j] >= 0) {  // a new row: into the ring for the later solves (row-major + feature-major)
+      const int64_t slot = row0 + row;
+      *(u16x8*)(const_cast<uint16_t*>(dv.X) + slot * FP + cg * 8) = v[j];
+      if (dv.XT) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(int64_t)(cg * 8 + e) * cap + slot] = v[j][e];
+      }
+    }
+  }
+  if (tid < 32) {
+    ylds[tid] = yv;
+    if (yi >= 0) const_cast<int32_t*>(dv.y)[row0 + tid] = yv;
+  }
+  __syncthreads();
+  // column sums of the tile's window rows: thread = (8-feature chunk, row group)
+  const int ch = tid % CPR, rl = tid / CPR;
+  float fs[8], fq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) fs[e] = fq[e] = 0.f;
+  for (int r = rl; r < 32; r += L) {
+    const int o = tile * 32 + r - wt.s0;
+    if (o < 0 || o >= B) continue;
+    const u16x8 x = *(const u16x8*)(lds + (ch >> 4) * 8192 + lds_off(r, ch & 15));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xf = bf2f(x[e]);
+      fs[e] += xf;
+      fq[e] += xf * xf;
+    }
+  }
+  float* red = (float*)scratch;  // [L][CPR][16]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(rl * CPR + ch) * 16 + e] = fs[e];
+    red[(rl * CPR + ch) * 16 + 8 + e] = fq[e];
+  }
+  __syncthreads();
+  if (tid < CPR * 2) {  // thread = (chunk, sums | squares): 8 features, row groups in order
+    const int c = tid >> 1, kind = tid & 1;
+    double a[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] = 0.0;
+      for (int g = 0; g < L; ++g) a[e] += (double)red[(g * CPR + c) * 16 + kind * 8 + e];
+    }
+    const auto rs = rsrc_of(dv.spart, (unsigned)((size_t)(tile + 1) * 2 * FP * 8));
+    const unsigned off = (unsigned)((((size_t)tile * 2 + kind) * FP + c * 8) * 8);
+#pragma unroll
+    for (int e = 0; e < 8; e += 2)
+      st_sc1_b128(rs, off + e * 8, __builtin_bit_cast(u16x8, double2v{a[e], a[e + 1]}));
+  }
+}
+
+// Phase P (slice owner `wg`, features [32 wg, 32 wg + 32)): the window
+// statistics from the tiles' partial sums (fixed order), std / 1/std, the
+// initial point x0 = w_old * std (Spark standardisation), the solver vectors
+// and the first trial point's fragments (sc1; intercepts by wg 0).
+template <int FP, int KP>
+__device__ __forceinline__ void persist_prep(const SolverCfg& cfg, const SolveDev& dv, char* scratch,
+                                             unsigned short* frl, int wg, int ntiles, int B, float wo_pre,
+                                             float b_pre) {
+  static_assert(KP <= 8, "one (class, feature) element per thread");
+  constexpr int FPI = FP > 256 ? FP : 256;
+  const int tid = threadIdx.x, K = cfg.K, F = cfg.F;
+  const int fs = wg * 32;
+  double* part = (double*)scratch;   // [4 lanes][64]
+  double* rs = part + 4 * 64;        // [32] sums, [32] sums of squares
+  float* sdl = (float*)(rs + 64);    // [32]
+  float* ivl = sdl + 32;             // [32]
+  {  // thread = (value: 32 features x {sum, square}, lane of 4 over the tiles)
+    const int val = tid & 63, ln = tid >> 6, fl = val & 31, kind = val >> 5;
+    constexpr int UG = 17;  // tiles per lane with every load in flight (windows of <= 68 tiles per pass)
+    double a = 0.0;
+    for (int g0 = ln; g0 < ntiles; g0 += 4 * UG) {
+      double v[UG];
+#pragma unroll
+      for (int u = 0; u < UG; ++u) {
+        const int g = g0 + 4 * u;
+        v[u] = g < ntiles ? ld_sc1(dv.spart + ((size_t)g * 2 + kind) * FP + fs + fl) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < UG; ++u) a += v[u];
+    }
+    part[ln * 64 + val] = a;
+  }
+  if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+  if (tid < 64) rs[tid] = ((part[tid] + part[64 + tid]) + part[128 + tid]) + part[192 + tid];
+  __syncthreads();
+  if (tid < 32) {
+    const int f = fs + tid;
+    const double a = rs[tid], b = rs[32 + tid], n = (double)B;
+    double sd = 0.0;
+    if (f < F && n > 1.0) {
+      const double mean = a / n;
+      const double var = (b - n * mean * mean) / (n - 1.0);
+      sd = var > 0.0 ? sqrt(var) : 0.0;
+    }
+    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
+    sdl[tid] = sdf;
+    ivl[tid] = inv;
+    dv.std_[f] = sdf;
+    dv.inv_std[f] = inv;
+  }
+  __syncthreads();
+  if (tid < 32 * KP) {
+    const int e = tid;
+    const int c = e >> 5, fl = e & 31, f = fs + fl;
+    const int pi = c * FPI + f;
+    const float wo = wo_pre;
+    const float xv = wo * sdl[fl];
+    dv.x[pi] = xv;
+    dv.d[pi] = 0.f;
+    dv.g_c[pi] = 0.f;
+    const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo;
+    dv.wfix[pi] = fix;
+    unsigned short h, l;
+    split_bf16(xv * ivl[fl] + fix, h, l);
+    const int o = (fl >> 3) * 128 + c * 8 + (fl & 7);
+    frl[o] = h;
+    frl[512 + o] = l;
+  }
+  if (wg == 0 && tid < 16) {
+    const int pi = KP * FPI + tid;
+    const float b = b_pre;
+    dv.x[pi] = b;
+    dv.d[pi] = 0.f;
+    dv.g_c[pi] = 0.f;
+    st_sc1(dv.b_eff + tid, b);
+  }
+  __syncthreads();
+  if (tid < 128) {  // wave 0: hi, wave 1: lo fragments of this slice
+    const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
+    const u16x8 v = *(const u16x8*)(frl + tid * 8);
+    if (tid < 64)
+      st_sc1_b128(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), v);
+    else
+      st_sc1_b128(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), v);
+  }
+}
+
+template <int FP, int KP>
+__global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, SolveDev dv, Ctrl* gctrl, SolveParams win,
+                                                            RingIngest ing, int G, EvalRide ride, int nride) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int wg = blockIdx.x, tid = threadIdx.x;
+  if (wg >= G) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
+    const int t = wg - G;
+    eval_body<FP>(lds, ride, t, 1, t + 1);
+    // arrival once this workgroup's loads (the models' fragments) are complete: the
+    // finalisation rewrites those fragments only after every riding workgroup arrived
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      (void)__hip_atomic_fetch_add((g_u64*)(dv.xch + kXchRide + (*dv.prm_count & 1u)), 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  constexpr int NS = FP / 32;  // feature slices
+  char* lf = lds;                          // row role: the resident tile + forward scratch
+  char* lb = lds + persist_fwd_bytes(FP);  // slice role: bwd_body's region
+  unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);
+  Ctrl* cl = (Ctrl*)(frl + 1024);          // bwd_body's controller copy (persists across slots)
+  const int B = win.B;
+  const WinTiles wt(win.start, B, cfg.cap);
+  const int ntiles = wt.nt;
+  const unsigned run = *dv.prm_count;
+  unsigned long long* xch = dv.xch;
+  unsigned long long* bar = xch + kXchGen + (run & 1u);
+  unsigned long long* err = xch + kXchErr;
+  unsigned long long nb = 0;
+  const bool row = wg < ntiles, owner = wg < NS;
+  if (wg == 0 && tid == 0) stamp(dv, 30, 0);
+  // the pulled weights of this slice, fetched now: their latency overlaps phase S
+  float wo_pre = 0.f, b_pre = 0.f;
+  if (owner && tid < 32 * KP) {
+    const int c = tid >> 5, f = wg * 32 + (tid & 31);
+    if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
+  }
+  if (wg == 0 && tid < 16 && tid < cfg.K) b_pre = dv.w_old[cfg.K * FP + tid];
+  // ---- S ----
+  if (row) persist_stage<FP>(cfg, dv, lf, lb, wt, wg, B, ing);
+  if (wg == 0 && tid == 0) stamp(dv, 30, 3);
+  p_barrier(bar, (unsigned long long)G * ++nb, err);
+  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
+  // ---- P ----
+  if (owner) {
+    persist_prep<FP, KP>(cfg, dv, lf + 32 * FP * 2, frl, wg, ntiles, B, wo_pre, b_pre);
+    if (tid == 0) ctrl_init(*cl);
+  }
+  if (wg == 0 && tid == 0) stamp(dv, 30, 1);
+  p_barrier(bar, (unsigned long long)G * ++nb, err);
+  // ---- slots ----
+  int phase = kPhInit;
+  for (int slot = 0; slot < cfg.nslots; ++slot) {
+    if (phase == kPhDone) break;  // uniform: every workgroup holds the same phase
+    if (row) {
+      constexpr int NT = FP / 64;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
+      fwd_body<FP, true, false, true>(cfg, win, slot, dv, lf, wg, G, acc);
+      store_gpf<FP, true>(dv, wg, G, acc);  // this tile's R^T X partials (sc1)
+    }
+    p_barrier(bar, (unsigned long long)G * ++nb, err);
+    if (owner) bwd_body<FP, KP, true>(cfg, win, gctrl, slot, dv, G, lb, wg, NS);
+    if (wg == 0 && tid == 0) xstore(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
+    p_barrier(bar, (unsigned long long)G * ++nb, err);
+    phase = owner ? cl->phase : (int)(unsigned)xload(xch + kXchPhase);
+  }
+  // ---- F: slice owners finalise their features ----
+  if (owner) {
+    if (nride > 0) {  // the riding evaluation still reads the fragments written below
+      if (tid == 0) {
+        unsigned long long* rc = xch + kXchRide + (run & 1u);
+        int spins = 0;
+        while (xload(rc) < (unsigned long long)nride) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > (1 << 22)) {
+            xstore(err, 4ull);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    FinIn<KP> in;
+    const int f = wg * 32 + tid;
+    if (tid < 32) in.load_f(cfg, dv, f);
+    if (wg == 0 && tid == 0) stamp(dv, 30, 2);
+    if (tid < 32) finalize_feature<KP>(cfg, dv, f, in);
+    if (wg == 0) {
+      __syncthreads();  // (the intercept entries of x were written by this workgroup's threads)
+      if (tid == 0) {
+        finalize_scalars<KP>(cfg, cl, dv);
+        xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counters
+        xstore(xch + kXchRide + ((run + 1u) & 1u), 0ull);
+      }
+      // the controller state for the host / later launches
+      constexpr int CW = sizeof(Ctrl) / 8;
+      for (int i = tid; i < CW; i += 256) ((unsigned long long*)gctrl)[i] = ((const unsigned long long*)cl)[i];
+    }
+  }
+}
+
+template <int FP>
+static void launch_persist_fp(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
+                              const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+  const size_t lb = persist_lds_bytes(FP);
+  const int grid = G + nride;
+  switch (dv.KP) {
+    case 2: solve_persist_kernel<FP, 2><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+    case 4: solve_persist_kernel<FP, 4><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+    default: solve_persist_kernel<FP, 8><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+  }
+}
+
+bool persist_supported(int FP, int KP) { return FP >= 128 && FP <= 1024 && KP <= 8; }
+
+void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
+                    const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+  switch (cfg.Fp) {
+    case 128: launch_persist_fp<128>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
+    case 256: launch_persist_fp<256>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
+    case 512: launch_persist_fp<512>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
+    case 1024: launch_persist_fp<1024>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
+    default: break;
+  }
+}
+
+template <int FP>
+static void set_persist_attr() {
+  const int b = (int)persist_lds_bytes(FP);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+}
+
 template <int FP>
 static void set_slot_attr() {
   const int tb = (int)tail_lds_bytes(FP);
@@ -1451,6 +1982,10 @@ void prepare_solve_kernels() {
   set_slot_attr<512>();
   set_slot_attr<1024>();
   set_slot_attr<2048>();
+  set_persist_attr<128>();
+  set_persist_attr<256>();
+  set_persist_attr<512>();
+  set_persist_attr<1024>();
   done = true;
 }
 

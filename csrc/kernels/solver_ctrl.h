@@ -69,6 +69,10 @@ struct SolverCfg {
   float gd_lr; // step for mode GD
   float tol;   // convergence tolerance (Spark default 1e-6)
   int xf32 = 0;  // fp32 feature rows (--dtype fp32): row-parallel solver with hi+lo bf16 MFMA operands
+  // the whole small-window solve as ONE persistent launch (solve_kernels.hip:
+  // solve_persist_kernel); needs its G workgroups co-resident, so only for a
+  // solver that has the device to itself (one worker per process)
+  int persist = 0;
 };
 
 // New stream rows a solve ingests into its ring before reading the window

@@ -153,6 +153,25 @@ __device__ __forceinline__ void load_wfrag(WFrag<FP>& wf, const uint16_t* __rest
   }
 }
 
+// The same with sc1 loads (fragments handed off inside a persistent launch).
+template <int FP>
+__device__ __forceinline__ void load_wfrag_sc1(WFrag<FP>& wf, const uint16_t* wf_hi, const uint16_t* wf_lo, int K = 16) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool live = (lane & 15) < K;
+  const auto rh = rsrc_of(wf_hi, 16u * FP * 2u), rl = rsrc_of(wf_lo, 16u * FP * 2u);
+#pragma unroll
+  for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+    const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
+    const unsigned fo = (unsigned)((cg * 16 + (lane & 15)) * 8) * 2u;
+    wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      wf.h[kk] = ld_sc1_b128(rh, fo);
+      wf.l[kk] = ld_sc1_b128(rl, fo);
+    }
+  }
+}
+
 template <int FP>
 __device__ __forceinline__ void forward_tile_pre(const char* lds, const WFrag<FP>& wf, f32x4& acc0, f32x4& acc1) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

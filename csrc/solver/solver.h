@@ -55,10 +55,12 @@ class LocalSolver {
   const SolverCfg& cfg() const { return cfg_; }
   int eval_wg() const { return nwg_eval_; }
   int kernels_per_solve() const {  // stats_prep + slots + (tail with finalize | finalize); rows: 3 per slot
+    if (persist_) return 1;
     return rows_mode_ ? 3 + (dv_.gred ? 3 : 2) * cfg_.nslots : 2 + 2 * nfast_;
   }
   bool rows_mode() const { return rows_mode_; }
   bool eager() const { return !use_graph_; }
+  bool persistent() const { return persist_; }
   // Debug access to the device controller (synchronous copy).
   void read_ctrl(Ctrl* out, hipStream_t stream);
   // Phase timeline of the last solve (PSX_SOLVER_STAMPS=1 at construction):
@@ -73,6 +75,9 @@ class LocalSolver {
   int nwg_eval_;
   int nfast_;
   bool rows_mode_ = false;  // large window: row-parallel fused passes (solve_kernels.h)
+  bool persist_ = false;    // small window: the whole solve in one persistent launch
+  bool gpf_ = false;        // small window: backward from the forward's feature-major partials
+  SolveDev dvp_{};          // the persistent launch's view (tile / statistics partials)
   bool use_graph_;
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;

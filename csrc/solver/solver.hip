@@ -31,6 +31,12 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
     // two workgroups per CU keep >= 128 KB of each CU's window tiles in flight
     nwg_eval_ = tiles < 512 ? tiles : 512;
   }
+  {  // persistent small-window solve (PSX_SOLVER_PERSIST=0 disables it)
+    const char* e = std::getenv("PSX_SOLVER_PERSIST");
+    const bool env_ok = !(e && *e && e[0] == '0');
+    persist_ = cfg.persist && env_ok && !rows_mode_ && !use_graph_ && persist_supported(cfg.Fp, padded_classes(cfg.K)) &&
+               cfg.cap <= 2048;
+  }
   // slots launched one by one: the initial evaluation + one trial per iteration
   // (what a solve whose line searches accept their first trial uses); the
   // remaining budget runs in the persistent tail launch
@@ -54,9 +60,21 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   const size_t o_std = take(FPI * 4), o_istd = take(FPI * 4), o_wfix = take(PI * 4), o_beff = take(16 * 4);
   const size_t o_whi = take(16 * FP * 2), o_wlo = take(16 * FP * 2);
   const size_t o_R = take(rows_mode_ ? 256 : (size_t)tiles * 1024 * 2);  // rows mode keeps no residual tiles
-  const size_t G = (size_t)nwg_eval_;
-  const size_t o_gpart = rows_mode_ ? take(G * dv_.KP * FP * 4) : 0;
-  const size_t o_spart = rows_mode_ ? take(G * 2 * FP * 8) : 0;
+  // PSX_SOLVER_GPF=1: the small-window chain's backward from the forward
+  // workgroups' feature-major partials (gpf) instead of the feature-major ring
+  // copy XT.  Measured equal on MI355X (profiles/r02_v3: the forward launch's
+  // 1 MB of partials costs at the boundary what the backward saves on loads),
+  // so the XT backward stays the default.
+  {
+    const char* e = std::getenv("PSX_SOLVER_GPF");
+    gpf_ = !rows_mode_ && cfg.Fp <= 1024 && e && e[0] == '1';
+  }
+  const size_t Gp = persist_ ? (size_t)persist_grid(cfg.Fp, tiles) : 0;
+  const size_t Gc = gpf_ ? (size_t)(nwg_eval_ > tail_grid(cfg.Fp, nwg_eval_) ? nwg_eval_ : tail_grid(cfg.Fp, nwg_eval_))
+                         : 0;
+  const size_t G = rows_mode_ ? (size_t)nwg_eval_ : (Gp > Gc ? Gp : Gc);
+  const size_t o_gpart = (rows_mode_ || persist_ || gpf_) ? take(G * dv_.KP * FP * 4) : 0;
+  const size_t o_spart = (rows_mode_ || persist_) ? take(G * 2 * FP * 8) : 0;
   const size_t o_gred = rows_mode_ ? take((size_t)dv_.KP * FPI * 4) : 0;
   const int npart = nwg_eval_ > tail_grid(cfg.Fp, nwg_eval_) ? nwg_eval_ : tail_grid(cfg.Fp, nwg_eval_);
   const size_t o_part = take((size_t)npart * 32 * 4);
@@ -102,6 +120,13 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   dv_.spart = rows_mode_ ? reinterpret_cast<double*>(b + o_spart) : nullptr;
   // small grids sum the partials inside bwd_update (one launch less per slot)
   dv_.gred = rows_mode_ && nwg_eval_ > kRowsReduceInBwd ? reinterpret_cast<float*>(b + o_gred) : nullptr;
+  if (gpf_) dv_.gpf = reinterpret_cast<float*>(b + o_gpart);
+  if (persist_) {  // the persistent launch reads the partials; the launch chain keeps XT / R
+    dvp_ = dv_;
+    dvp_.gpf = reinterpret_cast<float*>(b + o_gpart);
+    dvp_.spart = reinterpret_cast<double*>(b + o_spart);
+    dvp_.gred = nullptr;
+  }
 
   // riding evaluation passes spread over this many slots' bwd_update launches
   if (const char* e = std::getenv("PSX_RIDE_SPLIT")) ride_split_ = std::atoi(e) > 0 ? std::atoi(e) : 1;
@@ -221,6 +246,28 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
       throw std::invalid_argument("fused ingest: bad source / destination");
     if ((ing.dst + ing.n - 1) % cfg_.cap != (start + B - 1) % cfg_.cap)
       throw std::invalid_argument("fused ingest: the new rows must end the window");
+  }
+  if (persist_) {
+    RingIngest pin = ing;
+    if (pin.n > B) {  // new rows beyond the window: copied by their own launch (ring X, XT, y)
+      launch_ring_ingest(pin.src, pin.ysrc, pin.first, pin.step, pin.n, const_cast<uint16_t*>(dv_.X),
+                         const_cast<uint16_t*>(dv_.XT), const_cast<int32_t*>(dv_.y), pin.dst, cfg_.cap, cfg_.Fp, stream);
+      pin = RingIngest{};
+    }
+    const int nt = ((start & 31) + B + 31) >> 5;
+    const int G = persist_grid(cfg_.Fp, nt);
+    SolveDev d = dvp_;
+    d.ap_w = dv_.ap_w;
+    d.ap_hi = dv_.ap_hi;
+    d.ap_lo = dv_.ap_lo;
+    d.ap_b = dv_.ap_b;
+    d.ap_lr = dv_.ap_lr;
+    d.ap_coff = dv_.ap_coff;
+    launch_persist(cfg_, d, ctrl_, SolveParams{B, start, 0, 0}, pin, G, ride ? *ride : EvalRide{},
+                   ride ? ride->ntiles() : 0, stream);
+    hip_check(hipGetLastError(), "persistent solve launch");
+    dv_.ap_w = nullptr;
+    return;
   }
   if (use_graph_) {
     stats_args_.B = B;

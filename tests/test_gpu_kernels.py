@@ -56,7 +56,8 @@ def _ring_with(ds, cap, start, B, device):
     [("lbfgs", 2, 700, 900, 1024), ("lbfgs", 6, 1024, 0, 1024), ("gd", 3, 333, 10, 1024), ("lbfgs", 2, 50, 0, 99),
      ("lbfgs", 2, 1024, 1000, 1024)],  # full wrapped window: its first ring tile is visited twice
 )
-def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
+@pytest.mark.parametrize("persist", [False, True])  # launch chain / one persistent launch
+def test_local_solve_matches_reference(cuda, mode, iters, B, start, F, persist):
     cap = 1024
     if F == 99:
         ds = synth_binary(B, F, seed=3)
@@ -66,11 +67,12 @@ def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
         spec = ModelSpec(F, 6)
     ring = _ring_with(ds, cap, start, B, cuda)
     w_old = _rand_w(spec, 7, scale=0.05)
-    opts = SolverOptions(iters=iters, mode=mode, gd_lr=0.5, ls_max=6)
+    opts = SolverOptions(iters=iters, mode=mode, gd_lr=0.5, ls_max=6, persist=persist)
     op = LocalSolveOp(spec, cap, cuda, opts)
     wd = w_old.to(cuda)
     op.run(ring, B, start, wd)
     torch.cuda.synchronize()
+    assert bool(op._native.persistent) == persist
     ref = local_solve_reference(ds.float_features(), ds.y.long(), spec.coef(w_old), spec.intercept(w_old),
                                 iters=iters, hist=opts.hist, ls_max=opts.ls_max, nslots=opts.nslots, mode=mode,
                                 gd_lr=opts.gd_lr)
@@ -86,14 +88,15 @@ def test_local_solve_matches_reference(cuda, mode, iters, B, start, F):
 
 
 @pytest.mark.parametrize("seed,iters", [(4, 2), (5, 6)])
-def test_line_search_retries_run_in_tail(cuda, seed, iters):
+@pytest.mark.parametrize("persist", [False, True])
+def test_line_search_retries_run_in_tail(cuda, seed, iters, persist):
     """Large initial weights make some line searches need several evaluations:
     those run in the persistent tail launch and must match the reference."""
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(512, 1024, seed=seed)
     g = torch.Generator().manual_seed(seed + 100)
     w_old = torch.randn(spec.P, generator=g) * 8.0
-    opts = SolverOptions(iters=iters, ls_max=6)
+    opts = SolverOptions(iters=iters, ls_max=6, persist=persist)
     ring = _ring_with(ds, 1024, 37, 512, cuda)
     op = LocalSolveOp(spec, 1024, cuda, opts)
     op.run(ring, 512, 37, w_old.to(cuda))
@@ -338,3 +341,40 @@ def test_deferred_ingest_not_ending_window_is_flushed(cuda):
     op.run(ring, 32, 0, torch.zeros(spec.P, device=cuda))  # window [0,32) does not end at slot 63
     torch.cuda.synchronize()
     assert ring.pending is None and torch.equal(ring.X.cpu()[:64], ds.X.cpu()[:64])
+
+
+@pytest.mark.parametrize("n,B,pre", [(64, 512, 900), (200, 128, 300), (256, 1024, 1000), (1, 1, 0)])
+def test_persistent_solve_matches_chain(cuda, n, B, pre):
+    """The one-launch persistent solve (tile-resident, sc1 hand-offs) == the launch
+    chain: same ring contents after the fused ingest (bitwise), same solve up to
+    summation order; repeated runs are bitwise reproducible."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(4000, seed=7).to(cuda)
+    w = _rand_w(spec, 3, 0.02).to(cuda)
+    cap = 1024
+    dst = (pre + 37) % cap
+    start = (dst + n - B) % cap
+    outs, rings, stats = [], [], []
+    for persist in (True, False):
+        ring = DeviceRing(cap, ds.Fp, cuda, defer=True)
+        ring.ingest(ds.X, ds.y, 0, 1, min(cap, pre + 37), 0)
+        ring.flush()
+        ring.ingest(ds.X, ds.y, 2000, 3, n, dst)
+        op = LocalSolveOp(spec, cap, cuda, SolverOptions(use_graph=False, persist=persist))
+        op.run(ring, B, start, w)
+        torch.cuda.synchronize()
+        assert bool(op._native.persistent) == persist
+        outs.append((op.delta.clone(), op.loss.item()))
+        stats.append(op.stats.cpu().tolist())
+        rings.append((ring.X.cpu(), ring.XT.cpu(), ring.y.cpu()))
+        if persist:  # replays: bitwise identical
+            for _ in range(3):
+                op.run(ring, B, start, w)
+            torch.cuda.synchronize()
+            assert torch.equal(op.delta, outs[0][0])
+    for a, b in zip(*rings):
+        assert torch.equal(a, b)
+    assert stats[0][:4] == stats[1][:4] and stats[0][4] == 0, stats
+    scale = outs[1][0].abs().max().item()
+    assert (outs[0][0] - outs[1][0]).abs().max().item() <= 2e-3 * scale
+    assert abs(outs[0][1] - outs[1][1]) <= 1e-4 * max(1.0, abs(outs[1][1]))

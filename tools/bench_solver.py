@@ -53,9 +53,12 @@ def stamps(B=1024, opts=None):
     order = [0, 9, 10, 11, 1, 2, 3, 4, 5, 6, 7, 8]
     print(f"--- stamps B={B} (us, relative to slot 0 start; 100 MHz) ---")
     base = st[0]
-    sv = st[30 * 16: 30 * 16 + 3]
+    sv = st[30 * 16: 30 * 16 + 5]
+    extra = ""
+    if sv[3] >= base - 10 ** 6 and sv[3] > 0 and sv[4] > 0:  # persistent solve: staged / first barrier
+        extra = f" (persistent: staged={(sv[3] - base) / 100.0:.2f} barrier={(sv[4] - base) / 100.0:.2f})"
     print(f"stats_prep start={(sv[0] - base) / 100.0:.2f} end={(sv[1] - base) / 100.0:.2f}  "
-          f"finalize start={(sv[2] - base) / 100.0:.2f}")
+          f"finalize start={(sv[2] - base) / 100.0:.2f}{extra}")
     ph = ["start", "mfma", "publish", "gathered"]
     rows = []
     for p_ in range(4):
@@ -78,6 +81,10 @@ def main():
         stamps(1024)
         stamps(32)
         return
+    if "--stamps-persist" in sys.argv:
+        stamps(1024, SolverOptions(persist=True))
+        stamps(32, SolverOptions(persist=True))
+        return
     dev = "cuda:0"
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(1024, seed=0)
@@ -94,6 +101,9 @@ def main():
         ("default, B=32 (1 tile)", SolverOptions(), 32),
         ("init only, B=32", SolverOptions(iters=1, ls_max=0), 32),
         ("default, hipGraph replay", SolverOptions(use_graph=True), 1024),
+        ("persistent (one launch)", SolverOptions(persist=True), 1024),
+        ("persistent, B=32", SolverOptions(persist=True), 32),
+        ("persistent, ls_max=2", SolverOptions(persist=True, ls_max=2), 1024),
     ]:
         op = LocalSolveOp(spec, 1024, dev, opts)
         us = time_solve(op, ring, B, w)
@@ -109,6 +119,15 @@ def main():
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     print(f"host enqueue per solve: {(t1 - t0) / 200 * 1e6:.1f} us")
+    op = LocalSolveOp(spec, 1024, dev, SolverOptions(persist=True))
+    op.run(ring, 1024, 0, w)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        op.run(ring, 1024, 0, w)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f"host enqueue per solve (persistent): {(t1 - t0) / 200 * 1e6:.1f} us")
 
 
 if __name__ == "__main__":

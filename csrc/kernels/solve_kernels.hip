@@ -1128,6 +1128,68 @@ __device__ __forceinline__ void finalize_scalars(const SolverCfg& cfg, const Ctr
   }
 }
 
+// Finalisation over 32-feature slices (FP/32 workgroups, one (class, feature)
+// element per thread): the scattered fragment / delta stores spread over 32 CUs
+// instead of 4.  Same arithmetic (and class order of the centring mean) as
+// finalize_feature.
+template <int KP>
+struct FinSl {
+  static constexpr int NE = KP > 8 ? KP / 8 : 1;
+  float iv, xv[NE], fx[NE], wo[NE];
+  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
+    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
+    const int f = blk * 32 + (threadIdx.x & 31), cg = threadIdx.x >> 5;
+    iv = dv.inv_std[f];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int c = cg + 8 * e;
+      xv[e] = fx[e] = wo[e] = 0.f;
+      if (c < KP) {
+        xv[e] = dv.x[c * FPI + f];
+        fx[e] = dv.wfix[c * FPI + f];
+        wo[e] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
+      }
+    }
+  }
+};
+
+template <int KP>
+__device__ __forceinline__ void finalize_slice(const SolverCfg& cfg, const SolveDev& dv, int blk, const FinSl<KP>& in,
+                                               float* wvl /* LDS [16][32] */) {
+  constexpr int NE = FinSl<KP>::NE;
+  const int FP = cfg.Fp, K = cfg.K;
+  const int fl = threadIdx.x & 31, cg = threadIdx.x >> 5, f = blk * 32 + fl;
+  float wv[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cg + 8 * e;
+    wv[e] = (c < KP && f < cfg.F) ? (in.iv > 0.f ? in.xv[e] * in.iv : in.fx[e]) : 0.f;
+    if (c < KP) wvl[c * 32 + fl] = wv[e];
+  }
+  __syncthreads();
+  float mean = 0.f;
+#pragma unroll
+  for (int c = 0; c < KP; ++c) mean += wvl[c * 32 + fl];  // class order: as finalize_feature
+  mean = (cfg.center && f < cfg.F) ? mean / (float)K : 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cg + 8 * e;
+    if (c >= KP) continue;
+    const float v = c < K ? wv[e] - mean : 0.f;
+    write_frag(dv.out_hi, dv.out_lo, c, f, v);
+    if (c < K) {
+      const float dl = v - in.wo[e];
+      dv.delta[c * FP + f] = dl;
+      if (dv.w_new) dv.w_new[c * FP + f] = v;
+      if (dv.ap_w) {  // fused server update (see finalize_feature)
+        const float nw = in.wo[e] + dv.ap_lr * dl;
+        dv.ap_w[c * FP + f] = nw;
+        write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
+      }
+    }
+  }
+}
+
 template <int KP>
 __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk,
                                               const FinIn<KP>& in) {
@@ -1161,11 +1223,16 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
   int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
   // the finalisation's inputs are fetched before the phase word is known, so
   // the two load latencies overlap (the common case is phase == done)
-  FinIn<KP> in;
+  FinSl<KP> in;
+  float* wvl = (float*)lds;  // finalisation scratch (the slots' LDS is dead by then)
   if ((int)blockIdx.x < nfin) in.load(cfg, dv, blockIdx.x);
   if (gctrl->phase == kPhDone) {  // the common case: written by the previous launch
     // the finalisation is folded into this launch (one graph node less per solve)
-    if ((int)blockIdx.x < nfin) finalize_body<KP>(cfg, gctrl, dv, blockIdx.x, in);
+    if ((int)blockIdx.x < nfin) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
+      finalize_slice<KP>(cfg, dv, blockIdx.x, in, wvl);
+      if (blockIdx.x == 0 && threadIdx.x == 0) finalize_scalars<KP>(cfg, gctrl, dv);
+    }
     return;
   }
   const int G = gridDim.x, wg = blockIdx.x;
@@ -1192,7 +1259,9 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
   // every exit of the loop follows a grid barrier: all slots' updates are visible
   if (wg < nfin) {
     in.load(cfg, dv, wg);  // re-read: the slots above moved x
-    finalize_body<KP>(cfg, gctrl, dv, wg, in);
+    __syncthreads();       // (wvl overlaps the slots' LDS)
+    finalize_slice<KP>(cfg, dv, wg, in, wvl);
+    if (wg == 0 && threadIdx.x == 0) finalize_scalars<KP>(cfg, gctrl, dv);
   }
 }
 
@@ -1287,7 +1356,7 @@ static void launch_tail_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* c
   const int G = tail_grid(FP, nwg), ns = bwd_grid(FP);
   const size_t lb = tail_lds_bytes(FP);
   const int flag = (int)(lb - 16);
-  const int nfin = fin ? (cfg.Fp + 255) / 256 : 0;  // <= G: G >= FP/32 workgroups
+  const int nfin = fin ? cfg.Fp / 32 : 0;  // 32-feature slices; <= G: G >= FP/32 workgroups
   switch (dv.KP) {
     case 2: tail_kernel<FP, 2><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;
     case 4: tail_kernel<FP, 4><<<G, 256, lb, s>>>(cfg, prm, ctrl, s0, s1, dv, ns, flag, nfin); break;

@@ -54,6 +54,11 @@ class SolverOptions:
     use_graph: bool | None = None
     max_eval_wg: int = 512
     fused_ingest: bool = True  # GPU: new stream rows are copied into the ring by the solve's first kernel
+    # the whole small-window solve as ONE persistent launch (its workgroups must be
+    # co-resident: only for a solver that has the GPU to itself; the engines turn it
+    # off otherwise).  Host enqueue 3.8 us instead of ~23 us per solve, device time
+    # 68-72 us instead of ~63 us on MI355X (profiles/r02_v3): off by default.
+    persist: bool | None = None
 
     @property
     def nslots(self) -> int:
@@ -118,6 +123,7 @@ class LocalSolveOp:
         cfg.center, cfg.zero_const = int(o.center), int(o.zero_const)
         cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
         cfg.xf32 = int(ring.X.dtype == torch.float32)
+        cfg.persist = int(bool(o.persist))
         self._native = h.LocalSolver(
             cfg, ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),
@@ -130,8 +136,24 @@ class LocalSolveOp:
         the device (a stream sync): the engines check it at the end of a run."""
         return int(self.stats[4].item()) if self.frag is not None else 0
 
-    def run(self, ring, B: int, start: int, w_old: torch.Tensor):
-        """Enqueue a solve over the window [start, start+B) (mod cap) of ``ring`` (a DeviceRing)."""
+    def can_ride(self, ring, w_old: torch.Tensor) -> bool:
+        """True when this solver can carry a riding evaluation pass (GPU, eager
+        launches, small-window kernels): see :meth:`run`."""
+        if self.frag is None:
+            return False
+        self._bind(ring, w_old)
+        return bool(self._native.eager) and not bool(self._native.rows_mode)
+
+    def run(self, ring, B: int, start: int, w_old: torch.Tensor, ride: dict | None = None,
+            apply: tuple | None = None):
+        """Enqueue a solve over the window [start, start+B) (mod cap) of ``ring`` (a DeviceRing).
+
+        GPU extras (eager solver): ``ride`` = keyword arguments of an evaluation
+        pass executed by spare workgroups of the solve's bwd_update launches
+        (:class:`EvalRide`, csrc/kernels/lr_kernels.h); ``apply`` = (w, lr,
+        Fragments): the colocated server's update ``w = w_old + lr * delta`` fused
+        into the solve's finalisation, with that model's fragments written to the
+        given buffer."""
         if B <= 0:
             raise ValueError("local solve on an empty buffer")
         if ring.cap != self.cap:
@@ -140,13 +162,27 @@ class LocalSolveOp:
         if self.frag is not None:  # GPU
             self._bind(ring, w_old)
             pend = ring.take_pending(B, start) if hasattr(ring, "take_pending") else None
-            if pend is None:
-                self._native.run(int(B), int(start), stream_handle(self.device))
-            else:
+            if ride is None and apply is None:
+                if pend is None:
+                    self._native.run(int(B), int(start), stream_handle(self.device))
+                else:
+                    sX, sy, first, step, n, dst = pend
+                    self._native.run_ingest(int(B), int(start), stream_handle(self.device), sX.data_ptr(),
+                                            sy.data_ptr(), first, step, n, dst)
+                return
+            kw = dict(ride or {})
+            if pend is not None:
                 sX, sy, first, step, n, dst = pend
-                self._native.run_ingest(int(B), int(start), stream_handle(self.device), sX.data_ptr(), sy.data_ptr(),
-                                        first, step, n, dst)
+                kw.update(src=sX.data_ptr(), ysrc=sy.data_ptr(), first=int(first), step=int(step), n=int(n),
+                          dst=int(dst))
+            if apply is not None:
+                w, lr, fo = apply
+                kw.update(ap_w=w.data_ptr(), ap_lr=float(lr), ap_hi=fo.hi.data_ptr(), ap_lo=fo.lo.data_ptr(),
+                          ap_b=fo.b.data_ptr(), ap_coff=fo.coff)
+            self._native.run_full(int(B), int(start), stream_handle(self.device), **kw)
             return
+        if ride is not None:
+            raise ValueError("riding evaluation: GPU solver only")
         s, o = self.spec, self.opts
         idx = (torch.arange(B) + start) % self.cap
         Xw = X[idx, : s.F].float()
@@ -156,6 +192,9 @@ class LocalSolveOp:
             nslots=o.nslots, mode=o.mode, gd_lr=o.gd_lr, center=o.center, zero_const=o.zero_const, tol=o.tol)
         self.w_new.copy_(s.pack(res.coef, res.intercept))
         self.delta.copy_(self.w_new - w_old)
+        if apply is not None:  # the fused server update, same arithmetic as the kernel
+            w, lr, _ = apply
+            w.copy_(w_old + lr * self.delta)
         self.loss.fill_(res.loss)
         self.stats.copy_(torch.tensor([res.evals, res.accepted, res.ls_fail, 0, 0, 0, 0, 0], dtype=torch.int32))
 
@@ -207,6 +246,22 @@ class EvalSet:
         conf = torch.zeros(256, dtype=torch.int32)
         self.confusion_async(None, w, conf)
         _write_slot_cpu(slot_addr, conf, float(loss.item()) if loss is not None else 0.0, seq)
+
+    def ride_args(self, frag_a: "Fragments", frag_b: "Fragments | None", scratch: "EvalScratch", slot_a: int,
+                  seq_a: int, loss_a, slot_b: int, seq_b: int) -> dict:
+        """Keyword arguments of a riding evaluation pass (LocalSolveOp.run): model a
+        (columns frag_a.coff..) -> slot_a with ``loss_a``; model b (its own buffer,
+        columns frag_b.coff..; slot_b = 0: none) -> slot_b."""
+        kw = dict(ride_Xt=self.X.data_ptr(), ride_yt=self.y.data_ptr(), ride_T=self.T, whi=frag_a.hi.data_ptr(),
+                  wlo=frag_a.lo.data_ptr(), wb=frag_a.b.data_ptr(), coff1=frag_a.coff, acc=scratch.acc.data_ptr(),
+                  ticket=scratch.ticket.data_ptr(), slot=int(slot_a), seq=int(seq_a),
+                  loss=loss_a.data_ptr() if loss_a is not None else 0)
+        if slot_b:
+            if frag_b.coff < frag_a.coff + self.spec.K:
+                raise ValueError("riding evaluation: model a's columns must precede model b's")
+            kw.update(shi=frag_b.hi.data_ptr(), slo=frag_b.lo.data_ptr(), sb=frag_b.b.data_ptr(), coff2=frag_b.coff,
+                      slot2=int(slot_b), seq2=int(seq_b))
+        return kw
 
     def eval_pair_to_slots(self, frag_a: Fragments | None, w_a: torch.Tensor, frag_b: Fragments | None,
                            w_b: torch.Tensor, scratch: "EvalScratch", slot_a: int, seq_a: int, loss_a, slot_b: int,

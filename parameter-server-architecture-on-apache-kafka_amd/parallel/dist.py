@@ -235,6 +235,13 @@ class DistEngine:
             raise ValueError("need at least one worker rank (world size >= 2 with a dedicated server)")
         if cfg.num_workers != n_workers:
             cfg.num_workers = n_workers
+        if cfg.solver.persist and not (dist.is_initialized() and dist.get_backend() == "nccl"):
+            # the persistent solve needs its workgroups co-resident on the rank's GPU:
+            # one rank per GPU (the nccl = RCCL backend refuses two ranks on a device;
+            # gloo runs may share one)
+            import dataclasses
+
+            cfg.solver = dataclasses.replace(cfg.solver, persist=False)
         self.spec, train, test = load_datasets(cfg, train, test)
         self.wide = is_wide(self.spec)
         # wide model: collectives and dense p2p pushes need the dense delta;
@@ -353,6 +360,10 @@ class DistEngine:
                 wk.solver._bound = None
         if wk is not None and srv is None:
             wk.w.zero_()
+        if srv is not None and srv.pair is not None:
+            # the deferred evaluation rows ride in the next solve's launches (the
+            # update is a plain launch: it applies the reduced sum, not this delta)
+            srv.pair.set_ride(True, fuse_update=False)
         # bootstrap pull (vc 0): everybody starts from rank 0's weights
         boot = srv.w if srv is not None else (wk.w if wk is not None else zeros)
         dist.broadcast(boot, src=0)
@@ -386,6 +397,13 @@ class DistEngine:
             else:
                 vote = StopVote(self.device, torch.zeros(1, dtype=torch.float32, device=self.device), r)
         ingested_ahead = False
+        if vote is None and self._native_bsp_ok(sched, comm):
+            # every round of this rank enqueued by the native loop: solve (with the
+            # previous rows riding in it) -> RCCL all-reduce -> update, no Python per round
+            n = self._run_bsp_native(comm, cfg.max_iters)
+            r += n  # (rank 0's tracker advanced natively)
+            srv.updates += N * n
+            wk.vc = r
         while True:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
@@ -502,6 +520,8 @@ class DistEngine:
                 self.log.drain()
         if srv is not None:
             srv.flush_deferred(self.log)  # the last round's server row (rank 0)
+            if srv.pair is not None:
+                srv.pair.set_ride(False)
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         if vote is not None:
@@ -511,6 +531,55 @@ class DistEngine:
         return {"rounds": r, "updates": r * N, "elapsed_s": elapsed,
                 "updates_per_s": r * N / elapsed if elapsed > 0 else 0.0,
                 "max_vc_gap": int(srv.tracker.max_gap) if (srv is not None and self.rank == 0) else 0}
+
+    def _native_bsp_ok(self, sched: str, comm) -> bool:
+        """The native BSP loop (csrc/runtime/bsp_loop.h) runs this rank: allreduce
+        schedule over the native RCCL communicator, a colocated replica whose rows
+        ride in the solves, a bounded run and nothing that needs Python per round."""
+        c, wk, srv = self.cfg, self.worker, self.server
+        if os.environ.get("PSX_NATIVE_BSP", "1") == "0" or sched != "allreduce" or comm is None:
+            return False
+        if wk is None or srv is None or srv.pair is None or not srv.pair.ride_ok or not srv.pair.shared:
+            return False
+        if wk.wide or wk.evalset is None or self.tracer.enabled or not c.max_iters or c.max_wallclock_s:
+            return False
+        if c.iter_new_rows or c.checkpoint_dir or c.inject_worker_delay_ms or c.inject_worker_crash \
+                or c.inject_worker_stop:
+            return False
+        src = wk.source
+        if (src.mode == "per_iter" and src.rows_per_iter <= 0) or (src.mode != "per_iter" and not src.p_ms > 0):
+            return False
+        ring = wk.ring
+        if ring.f32 or ring.XT is None or src.ds.X.dtype != torch.bfloat16:
+            return False
+        return wk.solver.can_ride(ring, srv.w)
+
+    def _run_bsp_native(self, comm, rounds: int) -> int:
+        cfg, wk, srv, sp = self.cfg, self.worker, self.server, self.spec
+        wk.ring.flush()
+        srv.pair.flush(self.log)
+        src, ring, ev = wk.source, wk.ring, wk.evalset
+        d = dict(dsX=src.ds.X.data_ptr(), dsy=src.ds.y.data_ptr(), ds_rows=int(src.ds.rows), k=wk.k, N=src.N,
+                 per_iter_rows=src.rows_per_iter if src.mode == "per_iter" else 0, p_ms=float(src.p_ms),
+                 epochs=int(src.epochs), t0_ms=float(src.t0) * 1000.0, X=ring.X.data_ptr(), XT=ring.XT.data_ptr(),
+                 y=ring.y.data_ptr(), cap=ring.cap, Fp=sp.Fp, K=sp.K, F=sp.F, window=wk.window.handle,
+                 whi=wk.solver.frag.hi.data_ptr(), wlo=wk.solver.frag.lo.data_ptr(), wb=wk.solver.frag.b.data_ptr(),
+                 loss=wk.solver.loss.data_ptr(), delta=wk.solver.delta.data_ptr(), w=srv.w.data_ptr(),
+                 shi=srv.frag.hi.data_ptr(), slo=srv.frag.lo.data_ptr(), sb=srv.frag.b.data_ptr(),
+                 scoff=srv.frag.coff, lr=float(cfg.lr), tracker=srv.tracker.handle if self.rank == 0 else 0,
+                 Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T, acc=wk.scratch.acc.data_ptr(),
+                 ticket=wk.scratch.ticket.data_ptr(), sink=self.log.native.handle if self.log is not None else 0,
+                 log_server=1 if self.rank == 0 else 0, api=_native.host.capi())
+        loop = _native.hip().BspLoop(wk.solver._native, comm.c, d)
+        loop.next_local = int(src.next_local)
+        stream = comm.compute_stream()
+        n = int(loop.run(int(rounds), int(self.rounds), stream))
+        loop.flush(stream)
+        src.next_local = int(loop.next_local)
+        wk.iters += n
+        wk._seen_at_solve = wk.tuples_seen
+        self.native_host_us_per_round = float(loop.host_us_per_round)
+        return n
 
     def _vote_payload(self) -> torch.Tensor:
         """[P + 1] all-reduce payload: the solver writes its delta into the first P

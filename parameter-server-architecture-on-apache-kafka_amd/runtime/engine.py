@@ -18,15 +18,17 @@ and logging code as the distributed engine.
 from __future__ import annotations
 
 import dataclasses
+import os
 import queue
 import threading
 import time
 
 import torch
 
+from .. import _native
 from ..models.logreg import ModelSpec
 from ..models.wide import WideSpec
-from ..ops.lr import is_gpu
+from ..ops.lr import is_gpu, stream_handle
 from ..utils import data as data_mod
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
@@ -104,6 +106,10 @@ class LocalEngine:
         self.log = log
         self.tracer = Tracer(cfg.trace_path, 0, self.device,
                              f"{cfg.log_dir}/logs-perf.csv" if cfg.perf_log else None)
+        if cfg.solver.persist and cfg.num_workers > 1:
+            # the persistent solve needs its workgroups co-resident: one worker only
+            # (several in-process workers run their solves side by side)
+            cfg.solver = dataclasses.replace(cfg.solver, persist=False)
         if cfg.solver.use_graph is None and cfg.num_workers > 2:
             # many in-process workers share this process's launch thread: one graph
             # replay per solve beats 8 eager launches there (bench.py --workers 8:
@@ -168,7 +174,80 @@ class LocalEngine:
         return released
 
     # ------------------------------------------------------------------
+    def _native_bsp_ok(self) -> bool:
+        """The native round loop (csrc/runtime/bsp_loop.h) runs this BSP run: one
+        dense GPU worker whose rows ride in its solves, a bounded run, and nothing
+        that needs Python between rounds (tracing, checkpoints, injected faults,
+        a wall-clock or stream-driven cadence)."""
+        c = self.cfg
+        if os.environ.get("PSX_NATIVE_BSP", "1") == "0" or not is_gpu(self.device):
+            return False
+        if len(self.workers) != 1 or self.failed or self.server.pair is None or not self.server.pair.ride_ok:
+            return False
+        wk, srv = self.workers[0], self.server
+        if wk.wide or not srv.pair.shared or wk.evalset is None or self.tracer.enabled:
+            return False
+        if not c.max_iters or c.max_wallclock_s or c.iter_new_rows or c.checkpoint_dir or c.inject_worker_delay_ms \
+                or c.inject_worker_crash or c.inject_worker_stop:
+            return False
+        if c.stream_mode == "per_iter":
+            if wk.source.rows_per_iter <= 0:
+                return False
+        elif not wk.source.p_ms > 0:
+            return False
+        ring = wk.ring
+        if ring.f32 or ring.XT is None or wk.source.ds.X.dtype != torch.bfloat16:
+            return False
+        return wk.solver.can_ride(ring, srv.w)
+
+    def _run_bsp_native(self) -> dict:
+        """BSP rounds in the native loop: every round enqueued from C++ (producer,
+        window, fused ingest, solve with the previous rows riding in it, the
+        update fused into the solve, log records, tracker) -- no Python per round."""
+        cfg, srv = self.cfg, self.server
+        wk = self.workers[0]
+        wk.w = srv.w
+        wk.vc = self.rounds
+        wk.ring.flush()
+        srv.pair.flush(self.log)  # nothing may be pending from an earlier run
+        src, ring, sp = wk.source, wk.ring, self.spec
+        ev = wk.evalset
+        d = dict(dsX=src.ds.X.data_ptr(), dsy=src.ds.y.data_ptr(), ds_rows=int(src.ds.rows), k=wk.k, N=src.N,
+                 per_iter_rows=src.rows_per_iter if src.mode == "per_iter" else 0, p_ms=float(src.p_ms),
+                 epochs=int(src.epochs), t0_ms=float(src.t0) * 1000.0, X=ring.X.data_ptr(), XT=ring.XT.data_ptr(),
+                 y=ring.y.data_ptr(), cap=ring.cap, Fp=sp.Fp, K=sp.K, F=sp.F, window=wk.window.handle,
+                 whi=wk.solver.frag.hi.data_ptr(), wlo=wk.solver.frag.lo.data_ptr(), wb=wk.solver.frag.b.data_ptr(),
+                 loss=wk.solver.loss.data_ptr(), delta=wk.solver.delta.data_ptr(), w=srv.w.data_ptr(),
+                 shi=srv.frag.hi.data_ptr(), slo=srv.frag.lo.data_ptr(), sb=srv.frag.b.data_ptr(),
+                 scoff=srv.frag.coff, lr=float(cfg.lr), tracker=srv.tracker.handle, Xt=ev.X.data_ptr(),
+                 yt=ev.y.data_ptr(), T=ev.T, acc=wk.scratch.acc.data_ptr(), ticket=wk.scratch.ticket.data_ptr(),
+                 sink=self.log.native.handle, log_server=1, api=_native.host.capi())
+        h = _native.hip()
+        loop = h.BspLoop(wk.solver._native, None, d)
+        loop.next_local = int(src.next_local)
+        stream = stream_handle(self.device)
+        t_start = time.time()
+        r0 = self.rounds
+        u0 = srv.updates
+        n = int(loop.run(int(cfg.max_iters), int(r0), stream))
+        loop.flush(stream)
+        src.next_local = int(loop.next_local)
+        r = r0 + n
+        srv.updates += n
+        wk.vc = r
+        wk.iters += n
+        wk._seen_at_solve = wk.tuples_seen
+        self.native_host_us_per_round = float(loop.host_us_per_round)
+        self.log.drain()
+        torch.cuda.synchronize(self.device)
+        elapsed = time.time() - t_start
+        self.rounds = r
+        return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True}
+
     def _run_bsp(self) -> dict:
+        if self._native_bsp_ok():
+            return self._run_bsp_native()
         cfg, srv = self.cfg, self.server
         # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87).  Under BSP every
         # worker pulls the same version right after the server update, and all
@@ -183,6 +262,10 @@ class LocalEngine:
         u_start = srv.updates
         lanes = (_WorkerLanes(self.device, self.workers)
                  if is_gpu(self.device) and len(self.workers) > 1 and cfg.concurrent_workers else None)
+        if srv.pair is not None and lanes is None:
+            # the deferred evaluation rows ride in the next solve; one worker: the
+            # server update is fused into that worker's solve as well
+            srv.pair.set_ride(True, fuse_update=len(self.workers) == 1)
         while not self._stop(r - self.rounds, t_start, exhausted_since):
             W = [w for w in self.workers if w.k not in self.failed]
             if not W:
@@ -225,6 +308,8 @@ class LocalEngine:
             maybe_checkpoint(cfg, srv, r, W)
             self.log.drain()
         srv.flush_deferred(self.log)  # the last round's server row
+        if srv.pair is not None:
+            srv.pair.set_ride(False)
         if is_gpu(self.device):
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start

@@ -142,10 +142,18 @@ class WorkerRole:
             time.sleep(self.delay_s)
         B, start = int(self.window.size), int(self.window.start)
         self._seen_at_solve = self.tuples_seen
+        ride = ap = None
         if self.pair is not None:
-            self.pair.flush_worker()  # a deferred row reads the model this solve overwrites
+            # the deferred rows ride in this solve's launches, or (no ride) a deferred
+            # row reads the model this solve overwrites: evaluated first
+            ride, ap = self.pair.before_solve()
         self.side.fence()  # the last evaluation read the solver outputs this solve overwrites
-        self.solver.run(self.ring, B, start, self.w)
+        if ride is None and ap is None:
+            self.solver.run(self.ring, B, start, self.w)
+        else:
+            self.solver.run(self.ring, B, start, self.w, ride=ride[0] if ride else None, apply=ap)
+        if self.pair is not None:
+            self.pair.after_solve(ride, ap)
         self.iters += 1
         if self.wide and not self.solver.dense_delta:
             return self.solver.sparse_delta()
@@ -206,7 +214,7 @@ class ServerRole:
         """Every reader of the current global model is enqueued before w / the
         fragments are rewritten (a deferred paired row, a side-stream evaluation)."""
         if self.pair is not None:
-            self.pair.flush_worker()
+            self.pair.before_server_update()
         self.side.fence()
 
     def apply_round(self, deltas, vc: int, log, lr: float | None = None):
@@ -281,6 +289,16 @@ class EvalPair:
         self.pending = None  # (log, vc, ts) of a deferred server row
         self.pending_worker = None  # (log, vc, nseen, ts) of a deferred worker row
         self.fuse = os.environ.get("PSX_FUSED_APPLY", "1") != "0"
+        # Ride mode (GPU, dense, eager small-window solver): the deferred rows are
+        # evaluated by spare workgroups of the worker's NEXT solve (EvalRide,
+        # csrc/kernels/lr_kernels.h) instead of by a launch of their own; the
+        # server update is then a plain update launch, or -- when the engine sets
+        # ``fuse_update`` (the server's update of a round is exactly this worker's
+        # delta: one in-process BSP worker) -- part of the solve's finalisation.
+        self.ride_ok = os.environ.get("PSX_EVAL_RIDE", "1") != "0"
+        self.ride = False  # enabled by an engine loop whose solves and updates share one stream
+        self.fuse_update = False
+        self._applied = False  # this round's update already ran inside the solve
         spec = server.spec
         self.shared = (is_gpu(server.device) and not server.wide and server.evalset is worker.evalset
                        and server.evalset is not None and _solver_padded_classes(spec.K) + spec.K <= 16)
@@ -292,6 +310,84 @@ class EvalPair:
             server.frag_next = Fragments(spec, server.device, coff=16 - spec.K)
         server.pair = self
         worker.pair = self
+
+    # ---- ride mode ------------------------------------------------------
+    def set_ride(self, on: bool, fuse_update: bool = False):
+        """Engine hook: ride mode for the loop that follows (its worker solves and
+        server updates are enqueued in order on one stream); ``fuse_update``: the
+        server's update of every round is exactly this worker's delta."""
+        self.ride = bool(on) and self.ride_ok
+        self.fuse_update = self.ride and bool(fuse_update)
+        self._applied = False
+
+    def _riding(self) -> bool:
+        wk = self.worker
+        return self.ride and self.shared and not wk.wide and wk.solver.can_ride(wk.ring, wk.w)
+
+    def before_solve(self):
+        """(ride, apply) for the worker's next solve: the deferred rows to evaluate
+        inside it ((kwargs, submit) or None) and the fused server update (or None).
+        Without ride mode: the deferred worker row is evaluated now (the solve
+        overwrites its model) and both are None."""
+        if not self._riding():
+            self.flush_worker()
+            return None, None
+        ride = self._take_ride()
+        ap = None
+        if self.fuse_update and self.fuse:
+            srv = self.server
+            srv.side.fence()
+            ap = (srv.w, float(srv.cfg.lr), srv.frag_next)
+        return ride, ap
+
+    def after_solve(self, ride, ap):
+        if ride is not None:
+            ride[1]()  # the rows' records: submitted once their pass is enqueued
+        if ap is not None:
+            srv = self.server
+            srv.frag, srv.frag_next = srv.frag_next, srv.frag
+            self._applied = True
+
+    def _take_ride(self):
+        pw, pend = self.pending_worker, self.pending
+        if pw is None and pend is None:
+            return None
+        log = pw[0] if pw is not None else pend[0]
+        if pend is not None and pend[0] is not log:  # a different sink: evaluated on its own
+            self.pending = None
+            self._server_only(pend)
+            pend = None
+        self.pending_worker = self.pending = None
+        wk, srv = self.worker, self.server
+        nat = log.native
+        if pw is not None:
+            _, vc_w, nseen, ts_w = pw
+            slot_w, seq_w, addr_w = nat.acquire()
+            slot_s = seq_s = addr_s = 0
+            if pend is not None:
+                slot_s, seq_s, addr_s = nat.acquire()
+            kw = wk.evalset.ride_args(wk.solver.frag, srv.frag, wk.scratch, addr_w, seq_w, wk.solver.loss, addr_s,
+                                      seq_s)
+        else:  # a server row alone: the global model as the pass's only model
+            slot_s, seq_s, addr_s = nat.acquire()
+            kw = wk.evalset.ride_args(srv.frag, None, wk.scratch, addr_s, seq_s, None, 0, 0)
+
+        def submit():
+            if pend is not None:
+                nat.submit(slot_s, seq_s, 1, int(pend[2]), -1, int(pend[1]), 0)
+            if pw is not None:
+                nat.submit(slot_w, seq_w, 0, int(ts_w), int(wk.k), int(vc_w), int(nseen))
+
+        return kw, submit
+
+    def before_server_update(self):
+        """The server's w / fragments are about to be rewritten: a deferred row that
+        reads them is evaluated first."""
+        if self.ride and self.shared:
+            if self.pending is not None:  # a deferred server row reads the current global model
+                self.flush(self.pending[0])
+            return
+        self.flush_worker()
 
     def defer_server_row(self, log, vc: int, ts: int | None):
         if self.pending is not None:
@@ -321,6 +417,11 @@ class EvalPair:
         """The server update of this round in the launch that evaluates the
         deferred worker row (and the pending server row).  False: nothing to fuse
         with (the caller applies on its own)."""
+        if self.ride and self.shared and self._riding():
+            # ride mode: the rows wait for the next solve; the update ran inside the
+            # solve (fuse_update) or is a plain update launch (False)
+            applied, self._applied = self._applied, False
+            return applied
         pw = self.pending_worker
         if pw is None or not self.shared or not self.fuse or not (1 <= len(deltas) <= 16):
             return False

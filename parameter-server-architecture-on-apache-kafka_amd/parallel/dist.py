@@ -543,7 +543,7 @@ class DistEngine:
             return False
         if wk.wide or wk.evalset is None or self.tracer.enabled or not c.max_iters or c.max_wallclock_s:
             return False
-        if c.iter_new_rows or c.checkpoint_dir or c.inject_worker_delay_ms or c.inject_worker_crash \
+        if c.iter_new_rows or c.iter_new_frac or c.checkpoint_dir or c.inject_worker_delay_ms or c.inject_worker_crash \
                 or c.inject_worker_stop:
             return False
         src = wk.source

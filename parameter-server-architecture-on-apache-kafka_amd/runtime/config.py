@@ -41,6 +41,10 @@ class PSConfig:
     rows_per_iter: int = 0
     epochs: int = 1
     iter_new_rows: int = 0  # a worker iterates once this many new tuples arrived (0: continuously)
+    # ... or once this fraction of its current window is new (0: off).  At matched
+    # producer rates a fast worker otherwise re-fits an almost unchanged window
+    # many times over, which over-fits it (evaluation/README.md)
+    iter_new_frac: float = 0.0
     # buffer
     min_buffer_size: int = 128
     max_buffer_size: int = 1024

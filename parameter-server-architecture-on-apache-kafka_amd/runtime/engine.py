@@ -187,7 +187,7 @@ class LocalEngine:
         wk, srv = self.workers[0], self.server
         if wk.wide or not srv.pair.shared or wk.evalset is None or self.tracer.enabled:
             return False
-        if not c.max_iters or c.max_wallclock_s or c.iter_new_rows or c.checkpoint_dir or c.inject_worker_delay_ms \
+        if not c.max_iters or c.max_wallclock_s or c.iter_new_rows or c.iter_new_frac or c.checkpoint_dir or c.inject_worker_delay_ms \
                 or c.inject_worker_crash or c.inject_worker_stop:
             return False
         if c.stream_mode == "per_iter":

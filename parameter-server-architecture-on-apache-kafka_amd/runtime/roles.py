@@ -11,6 +11,7 @@ delta / weight tensors; roles only enqueue device work on the current stream.
 """
 from __future__ import annotations
 
+import math
 import os
 import time
 from contextlib import contextmanager
@@ -118,7 +119,7 @@ class WorkerRole:
         window only re-fits the same rows)."""
         if self.window.size <= 0:
             return False
-        K = self.cfg.iter_new_rows
+        K = max(self.cfg.iter_new_rows, math.ceil(self.cfg.iter_new_frac * int(self.window.size)))
         return K <= 0 or self.tuples_seen - self._seen_at_solve >= K or self.source.exhausted
 
     def compute(self, log=None) -> torch.Tensor:

@@ -121,9 +121,23 @@ def load_any(path: str, dtype: str = "bf16", **kw) -> Dataset:
 # synthetic data
 FINEFOOD_LABEL_MIX = np.array([20000, 14800, 20000, 20000, 20000], dtype=np.float64)
 FINEFOOD_TEST_ROWS = 4877
-# signal strength calibrated (tools/calibrate_synth.py) so that full-batch LR
-# reaches ~0.47 held-out accuracy, the reference's offline ground truth.
-FINEFOOD_SIGNAL = 0.074
+# Generator calibration (tools/stream_sim.py, tools/learning_curve.py; see
+# evaluation/README.md).  Two targets from the reference's real-data runs:
+#  * the offline ceiling: full-batch LR on the whole train set reaches ~0.47-0.50
+#    test accuracy (the reference's datawig ground truth is 0.47);
+#  * the streaming curve: the reference's own algorithm (128-row window, 2 L-BFGS
+#    iterations per update, ~7 new rows per update at 5 rows/s) reaches
+#    0.303 / 0.322 / 0.339 / 0.348 test accuracy after 60 / 120 / 300 / 600 s
+#    (evaluation/logs/single-worker_5tps).
+# Real review text learns fast and saturates early: a few frequent, strongly
+# indicative words (Zipf-ranked class words, ``class_zipf``) plus ratings whose
+# text reads like another rating (``text_noise``) that cap the ceiling.  The
+# round-1 generator (uniform class words, no text noise, signal 0.074) hit the
+# ceiling but learned far slower than the real data from a few hundred rows
+# (0.25 where the reference's curve is at 0.30-0.35).
+FINEFOOD_SIGNAL = 0.06
+FINEFOOD_CLASS_ZIPF = 1.3
+FINEFOOD_TEXT_NOISE = 0.47
 
 
 def synth_finefood(
@@ -135,8 +149,13 @@ def synth_finefood(
     words_per_row: float = 45.0,
     class_vocab: int = 400,
     dtype: str = "bf16",
+    class_zipf: float = FINEFOOD_CLASS_ZIPF,
+    text_noise: float = FINEFOOD_TEXT_NOISE,
 ) -> Dataset:
-    """Fine-food-reviews-shaped synthetic rows (labels 1..5, hashed L2-normalised text)."""
+    """Fine-food-reviews-shaped synthetic rows (labels 1..5, hashed L2-normalised text).
+
+    ``class_zipf = 0, text_noise = 0, signal = 0.074`` reproduces the round-1
+    generator (uniform class words)."""
     rng = np.random.default_rng(seed)
     mix = FINEFOOD_LABEL_MIX / FINEFOOD_LABEL_MIX.sum()
     y = rng.choice(5, size=rows, p=mix) + 1
@@ -159,8 +178,16 @@ def synth_finefood(
     row_of = np.repeat(np.arange(rows), nw)
     generic = rng.choice(vocab, size=total, p=zipf)
     use_cls = rng.random(total) < signal
-    cls_pick = rng.integers(0, class_vocab, size=total)
-    lab = y[row_of] - 1
+    if class_zipf > 0:  # a few frequent, strongly indicative words per class
+        cz = 1.0 / np.arange(1, class_vocab + 1) ** class_zipf
+        cls_pick = rng.choice(class_vocab, size=total, p=cz / cz.sum())
+    else:
+        cls_pick = rng.integers(0, class_vocab, size=total)
+    ty = y - 1
+    if text_noise > 0:  # rows whose text was written as if for another rating
+        flip = rng.random(rows) < text_noise
+        ty = np.where(flip, rng.integers(0, 5, size=rows), ty)
+    lab = ty[row_of]
     cls_word = np.stack(cls_words)[lab, cls_pick]
     words = np.where(use_cls, cls_word, generic)
     np.add.at(X, (row_of, w_idx[words]), w_sign[words])

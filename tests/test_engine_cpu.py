@@ -197,3 +197,28 @@ def test_cli_async_scheduler_and_rccl_trace(tmp_path):
     env = rccl_trace_env(str(tmp_path))
     assert env["NCCL_DEBUG"] == "INFO" and "COLL" in env["NCCL_DEBUG_SUBSYS"]
     assert env["NCCL_DEBUG_FILE"].startswith(str(tmp_path)) and "%p" in env["NCCL_DEBUG_FILE"]
+
+
+def test_fresh_window_cadence(tmp_path):
+    """--iter_new_frac 0.5: a worker iterates only once half of its window is new
+    tuples (evaluation/README.md §3), so consecutive solves are >= 64 tuples apart
+    for the 128-row minimum window."""
+    train, test = synth_finefood(3000, num_features=128, seed=0), synth_finefood(200, num_features=128, seed=1)
+    cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=2.0, max_wallclock_s=3.5,
+                   min_buffer_size=128, max_buffer_size=128, iter_new_frac=0.5, logging=True, log_dir=str(tmp_path))
+    LocalEngine(cfg, "cpu", train=train, test=test).run()
+    rows = [r.split(";") for r in (tmp_path / "logs-worker.csv").read_text().splitlines()[1:]]
+    seen = [int(r[6]) for r in rows]
+    assert len(seen) >= 3
+    gaps = [b - a for a, b in zip(seen, seen[1:])]
+    assert min(gaps[:-1]) >= 64, gaps  # the last solve may run on an exhausted stream
+
+
+def test_synth_finefood_round1_generator():
+    """class_zipf = 0, text_noise = 0 keeps the round-1 generator (uniform class words)."""
+    a = synth_finefood(64, num_features=128, seed=3, class_zipf=0.0, text_noise=0.0, signal=0.074)
+    b = synth_finefood(64, num_features=128, seed=3)
+    assert torch.equal(a.y, b.y)  # the labels come first from the same stream
+    assert not torch.equal(a.X, b.X)
+    n = a.float_features().norm(dim=1)
+    assert torch.allclose(n, torch.ones_like(n), atol=1e-2)

@@ -62,7 +62,7 @@ def launch(a, tr, te):
         cmd = [sys.executable, "-m", "psx.apps.server_app_runner", "--inprocess", "--device", a.device,
                "-training", tr, "-test", te, "-p", str(p), "-c", str(c), "--num_workers", str(n), "-l",
                "--log_dir", d, "--max_wallclock_s", str(a.seconds), "--async_scheduler", "threads",
-               "--iter_new_rows", str(a.iter_new_rows)]
+               "--iter_new_rows", str(a.iter_new_rows), "--iter_new_frac", str(a.iter_new_frac)]
         procs.append((name, subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(os.path.join(d, "run.out"), "w"),
                                              stderr=subprocess.STDOUT)))
     t0 = time.time()
@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--out", default="evaluation/psx_logs")
     ap.add_argument("--table-only", action="store_true")
+    ap.add_argument("--iter_new_frac", type=float, default=0.0,
+                    help="worker cadence: iterate once this fraction of the window is new (0: off)")
     ap.add_argument("--iter_new_rows", type=int, default=0,
                     help="worker cadence: iterate after this many new tuples (0: continuously, the reference's way)")
     a = ap.parse_args()

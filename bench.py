@@ -66,7 +66,12 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 200 dense, 30 wide)")
     ap.add_argument("--model", default="dense", choices=sorted(MODELS))
     ap.add_argument("--consistency", type=int, default=None)
-    ap.add_argument("--rows-per-step", type=int, default=64, help="new stream rows per worker per step")
+    ap.add_argument("--rows-per-step", type=int, default=None,
+                    help="new stream rows per worker per step (dense default: the whole window, as with the "
+                         "reference's unthrottled producer every local solve sees fresh rows; wide default: 64)")
+    ap.add_argument("--server-lr", type=float, default=None,
+                    help="server step on each delta (dense default 1/max(workers, 4): the reference's 1/N "
+                         "(ServerProcessor.java:148-151) with at least 4 workers' worth of averaging; wide: 1/N)")
     ap.add_argument("--train-rows", type=int, default=None)
     ap.add_argument("--test-rows", type=int, default=None)
     ap.add_argument("--features", type=int, default=None)
@@ -94,6 +99,8 @@ def parse(argv=None):
     for k in ("features", "train_rows", "test_rows", "consistency", "schedule"):
         if getattr(a, k) is None:
             setattr(a, k, m[k])
+    if a.rows_per_step is None:
+        a.rows_per_step = 64 if wide else a.buffer
     if a.steps is None:
         a.steps = 300 if wide else 2000
     if a.warmup is None:
@@ -128,6 +135,9 @@ def build_cfg(a, n_workers):
         bsp_schedule=a.schedule,
         server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,
+        # below 4 workers the step stays 1/4: one worker's fresh-window solve is a
+        # noisy estimate (evaluation/README.md; tools/stream_sim.py --lr)
+        server_lr=a.server_lr if a.server_lr is not None else (None if wide else 1.0 / max(n_workers, 4)),
     )
 
 
@@ -206,6 +216,7 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
             "consistency": a.consistency,
             "workers": n_workers,
             "rows_per_step_per_worker": a.rows_per_step,
+            "server_lr": cfg.lr,
             "bench_model": a.model,
         },
         "test_accuracy": summ.get("final_server_acc"),

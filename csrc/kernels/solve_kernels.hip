@@ -178,7 +178,13 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   const int t = threadIdx.x, j = t % kStatL, fl0 = t / kStatL;
   if (blockIdx.x == 0 && t == 0) *prm = pr;  // the later launches read it from device memory
   if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 0);
-  const int fs = blockIdx.x * kStatW;
+  // XCD-aware slice order: workgroups are dealt round-robin over the 8 XCDs, so
+  // workgroup b takes slice (b % 8) * (G / 8) + b / 8 -- each XCD owns a
+  // contiguous feature range and fetches every 128-B line of the new rows
+  // once, instead of all 8 XCDs fetching each line for their 8-feature pieces
+  const int G = gridDim.x;
+  const int sl = (G & 7) == 0 ? (int)(blockIdx.x & 7) * (G >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int fs = sl * kStatW;
   const int nin = ing.n;
   // the pulled weights were just written by the server update: fetch them now so
   // their latency overlaps the window read (one element per thread: kStatW*KP <= 256)
@@ -189,11 +195,13 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
     if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
   }
   if (blockIdx.x == 0 && t < 16 && t < cfg.K) b_pre = dv.w_old[cfg.K * FP + t];
-  // the first batch of the window read is issued before the ingest copy (which
-  // waits on its own loads): the old rows' XT pieces do not depend on it
+  // the newest min(nin, B) window rows are the fused ones (counted from LDS);
+  // only the pieces holding older rows are read from XT
+  const int bold = B - (nin < B ? nin : B);
   const unsigned short* xt = dv.XT + (size_t)(fs + fl0) * cap;
-  const int nq = wt.nt * 4;  // 8-row pieces of the window tiles
-  constexpr int U = 4;       // pieces per lane in flight
+  const int nq_all = wt.nt * 4;  // 8-row pieces of the window tiles (piece qq starts at window row qq*8 - s0)
+  const int nq = min(nq_all, (bold + wt.s0 + 7) >> 3);
+  constexpr int U = 4;  // pieces per lane in flight
   u16x8 v[U];
   auto load_pieces = [&](int q0) {
 #pragma unroll
@@ -203,20 +211,36 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
       v[u] = *(const u16x8*)(xt + wt.ring_tile(qc >> 2) * 32 + (qc & 3) * 8);
     }
   };
-  load_pieces(j);
-  for (int i = t; i < nin; i += 256) {  // fused ingest: one 16-B chunk of each new row
-    const long long sr = ing.first + (long long)i * ing.step;
-    int dr = ing.dst + i;
-    dr = dr >= cap ? dr - cap : dr;
-    const u16x8 v = *(const u16x8*)(ing.src + sr * FP + fs);
-    *(u16x8*)(const_cast<uint16_t*>(dv.X) + (size_t)dr * FP + fs) = v;
-    *(u16x8*)(nv + i * kStatW) = v;
+  // the first batch of the window read is issued before the ingest copy: the
+  // old rows' XT pieces do not depend on it
+  if (nq > 0) load_pieces(j);
+  // fused ingest: one 16-B chunk (this slice) of each new row; every chunk's
+  // load is issued before the first store
+  constexpr int kIU = kMaxFusedIngest / 256;
+  u16x8 iv[kIU];
+  int iy[kIU];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(size_t)(fs + e) * cap + dr] = v[e];
-    if (blockIdx.x == 0) const_cast<int32_t*>(dv.y)[dr] = ing.ysrc[sr];
+  for (int u = 0; u < kIU; ++u) {
+    const int i = t + 256 * u;
+    if (i < nin) {
+      const long long sr = ing.first + (long long)i * ing.step;
+      iv[u] = *(const u16x8*)(ing.src + sr * FP + fs);
+      if (blockIdx.x == 0) iy[u] = ing.ysrc[sr];
+    }
   }
-  // the newest min(nin, B) window rows are the fused ones: counted from LDS
-  const int bold = B - (nin < B ? nin : B);
+#pragma unroll
+  for (int u = 0; u < kIU; ++u) {
+    const int i = t + 256 * u;
+    if (i < nin) {
+      int dr = ing.dst + i;
+      dr = dr >= cap ? dr - cap : dr;
+      *(u16x8*)(const_cast<uint16_t*>(dv.X) + (size_t)dr * FP + fs) = iv[u];
+      *(u16x8*)(nv + i * kStatW) = iv[u];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(size_t)(fs + e) * cap + dr] = iv[u][e];
+      if (blockIdx.x == 0) const_cast<int32_t*>(dv.y)[dr] = iy[u];
+    }
+  }
   float s = 0.f, q = 0.f;
   for (int q0 = j; q0 < nq; q0 += kStatL * U) {
     if (q0 != j) load_pieces(q0);  // (the first batch was issued at entry)

@@ -79,7 +79,7 @@ struct SolverCfg {
 // (fused into the first kernel of the solve): rows src_first + i*src_step
 // (i < n) of the resident dataset go to ring slots (dst + i) % cap, and must be
 // the newest n rows of the window.  n == 0: nothing to ingest.
-constexpr int kMaxFusedIngest = 256;
+constexpr int kMaxFusedIngest = 1024;
 struct RingIngest {
   const uint16_t* src;   // dataset rows [*][Fp] bf16
   const int32_t* ysrc;   // dataset labels

@@ -34,7 +34,7 @@ class DeviceRing:  # dense rows; the sparse (ELL) ring is psx.ops.sparse.SparseR
     every 32-feature slice of a window contiguously."""
 
     TILE = 32
-    MAX_DEFERRED = 256  # kMaxFusedIngest (csrc/kernels/solver_ctrl.h)
+    MAX_DEFERRED = 1024  # kMaxFusedIngest (csrc/kernels/solver_ctrl.h)
 
     def __init__(self, cap: int, Fp: int, device, defer: bool = False, dtype: str = "bf16"):
         self.requested = int(cap)

@@ -260,3 +260,30 @@ def test_stream_handle_follows_current_stream(cuda):
     with torch.cuda.stream(side):
         assert stream_handle(cuda) == side.cuda_stream
     assert stream_handle(dev) == main.cuda_stream
+
+
+@pytest.mark.parametrize("rows", [96, 600, 1024])
+def test_fused_ingest_matches_ring_copy(cuda, monkeypatch, rows):
+    """New rows copied into the ring by the solve's first kernel (fused ingest, up to
+    kMaxFusedIngest = 1024 rows per solve, a fully fresh window included) end at the
+    same model and log the same rows as the separate ring-ingest launch (Python
+    loop), and as the native loop (which always fuses)."""
+    train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
+    res = []
+    for fused, native in ((True, "0"), (False, "0"), (True, "1")):
+        monkeypatch.setenv("PSX_NATIVE_BSP", native)
+        cfg = _cfg(max_iters=12, init="random", min_buffer_size=1024, max_buffer_size=1024, rows_per_iter=rows,
+                   solver=SolverOptions(fused_ingest=fused))
+        eng = LocalEngine(cfg, cuda, train=train, test=test)
+        eng.run()
+        torch.cuda.synchronize()
+        book = eng.log.book
+        res.append((eng.server.w.cpu(), sorted((r[1], r[2], r[3], r[4], r[5], r[6]) for r in book.worker)))
+    # fused vs ring copy: the window statistics add the same values in another order
+    w0, w1 = res[0][0], res[1][0]
+    assert torch.allclose(w0, w1, rtol=0, atol=1e-4 * w1.abs().max().item())
+    assert [r[:2] + r[5:] for r in res[0][1]] == [r[:2] + r[5:] for r in res[1][1]]
+    assert max(abs(a[2] - b[2]) for a, b in zip(res[0][1], res[1][1])) < 1e-3
+    # native loop vs Python loop, both fused: bit for bit
+    assert torch.equal(res[0][0], res[2][0])
+    assert res[0][1] == res[2][1] and len(res[0][1]) == 12

@@ -27,7 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def simulate(tr, te, window=128, rows_per_iter=7, marks=(300, 600, 1500, 3000, 5449), workers=1):
+def simulate(tr, te, window=128, rows_per_iter=7, marks=(300, 600, 1500, 3000, 5449), workers=1,
+             lr: float | None = None):
     """Returns [(tuples, test accuracy)] at each mark.  With workers > 1 every
     worker solves over its own partition's window from the same global model
     (sequential consistency: the server adds each delta with lr = 1/N,
@@ -52,7 +53,8 @@ def simulate(tr, te, window=128, rows_per_iter=7, marks=(300, 600, 1500, 3000, 5
             r = local_solve_reference(X[part], y[part], coef, inter, iters=2)
             dc += r.coef - coef
             di += r.intercept - inter
-        coef, inter = coef + dc / workers, inter + di / workers
+        step = 1.0 / workers if lr is None else lr
+        coef, inter = coef + step * dc, inter + step * di
         seen += rows_per_iter * workers
         while mi < len(marks) and seen >= marks[mi]:
             pred = (Xt @ coef.t() + inter).argmax(1)
@@ -66,6 +68,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows-per-iter", type=int, default=7)
     ap.add_argument("--workers", type=int, default=1)
+    ap.add_argument("--window", type=int, default=128)
+    ap.add_argument("--lr", type=float, default=None, help="server step (default 1/workers)")
     ap.add_argument("--marks", default="300,600,1500,3000,5449")
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--train-rows", type=int, default=12000)
@@ -78,7 +82,7 @@ def main():
     tr = synth_finefood(a.train_rows, seed=0, **kw)
     te = synth_finefood(FINEFOOD_TEST_ROWS, seed=1, **kw)
     t = time.time()
-    res = simulate(tr, te, rows_per_iter=a.rows_per_iter, workers=a.workers,
+    res = simulate(tr, te, window=a.window, rows_per_iter=a.rows_per_iter, workers=a.workers, lr=a.lr,
                    marks=tuple(int(m) for m in a.marks.split(",")))
     print(json.dumps({"kw": kw, "workers": a.workers, "curve": res, "s": round(time.time() - t, 1)}), flush=True)
 

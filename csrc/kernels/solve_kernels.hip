@@ -228,6 +228,10 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
       if (blockIdx.x == 0) iy[u] = ing.ysrc[sr];
     }
   }
+  if (nin > 0 && blockIdx.x == 0 && t == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(dv, 30, 5);  // this thread's ingest loads arrived
+  }
 #pragma unroll
   for (int u = 0; u < kIU; ++u) {
     const int i = t + 256 * u;
@@ -259,6 +263,7 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   }
   if (nin > 0) {
     __syncthreads();
+    if (blockIdx.x == 0 && t == 0) stamp(dv, 30, 6);  // copies issued, old-row sums done
     for (int i = nin - (B - bold) + j; i < nin; i += kStatL) {
       const float x = bf2f(nv[i * kStatW + fl0]);
       s += x;

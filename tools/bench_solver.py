@@ -76,7 +76,55 @@ def stamps(B=1024, opts=None):
                                           if row[k] >= base))
 
 
+def ingest_variants():
+    """Solve + fused ingest of n new rows per solve (the window's newest n rows come
+    from a device-resident data set, as in the engines): device time per solve and
+    the stats_prep kernel's span from the device stamps."""
+    import os
+
+    os.environ["PSX_SOLVER_STAMPS"] = "1"
+    dev = "cuda:0"
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(8192, seed=0)
+    sX, sy = ds.X.to(dev), ds.y.to(dev)
+    ring = DeviceRing(1024, spec.Fp, dev)
+    ring.place(ds.X[:1024], ds.y[:1024])
+    w = spec.init("random", seed=1).to(dev)
+    h = torch.cuda.current_stream().cuda_stream
+    for n in (0, 64, 256, 1024):
+        op = LocalSolveOp(spec, 1024, dev, SolverOptions())
+        op.run(ring, 1024, 0, w)
+        k = [0]
+
+        def one():
+            if n == 0:
+                op.run(ring, 1024, 0, w)
+            else:
+                first = (k[0] * n) % (8192 - n)
+                op._native.run_ingest(1024, 0, h, sX.data_ptr(), sy.data_ptr(), first, 1, n, 1024 - n)
+            k[0] += 1
+
+        for _ in range(10):
+            one()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            one()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1000.0 / 200
+        st = op._native.read_stamps(h)
+        sv = st[30 * 16: 30 * 16 + 7]
+        ph = "" if n == 0 else f" (loads in {(sv[5] - sv[0]) / 100.0:.2f}, copies+sums {(sv[6] - sv[0]) / 100.0:.2f})"
+        print(f"ingest {n:5d} rows: {us:8.2f} us/solve  stats_prep span {(sv[1] - sv[0]) / 100.0:.2f} us{ph} "
+              f"evals={op.stats.cpu().tolist()[0]}", flush=True)
+
+
 def main():
+    if "--ingest" in sys.argv:
+        ingest_variants()
+        return
     if "--stamps" in sys.argv:
         stamps(1024)
         stamps(32)

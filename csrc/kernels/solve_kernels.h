@@ -78,8 +78,11 @@ const void* stats_prep_symbol();
 void launch_finalize(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, hipStream_t s);
 // win.B > 0: the window as kernel arguments (eager launches); otherwise the
 // kernels read it from prm (graph replays).
+// fin_slot: a bwd_update launch of slot >= fin_slot that ends the solve finalises
+// its slice in place (the tail / finalize launch then writes the scalars only);
+// riding evaluation workgroups must all be in launches of earlier slots.
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                 hipStream_t s, const SolveParams& win);
+                 hipStream_t s, const SolveParams& win, int fin_slot = kNoFinSlot);
 // Line-search retry slots [slot_begin, slot_end) in one persistent launch.
 // with_finalize: the finalisation runs inside the tail launch (no separate finalize node).
 void launch_tail(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot_begin, int slot_end,
@@ -108,7 +111,8 @@ void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int sl
 // workgroups in the bwd_update launch evaluating test tiles [ride_t0, ride_t0 +
 // nride) of `ride` (see EvalRide, lr_kernels.h); nride == 0: none.
 void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                      hipStream_t s, const SolveParams& win, const struct EvalRide& ride, int ride_t0, int nride);
+                      hipStream_t s, const SolveParams& win, const struct EvalRide& ride, int ride_t0, int nride,
+                      int fin_slot = kNoFinSlot);
 size_t stats_rows_lds_bytes();
 
 // ---- persistent small-window solve: the whole solve in ONE launch (see

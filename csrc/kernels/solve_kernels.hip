@@ -529,6 +529,195 @@ __global__ __launch_bounds__(256) void fwd_kernel(SolverCfg cfg, const SolvePara
 }
 
 // ---------------------------------------------------------------------------
+// Finalisation (after the last slot): back to the unstandardised space,
+// multinomial centring across classes, delta = w_new - w_old, eval fragments,
+// loss and solver statistics.  One thread per feature (all classes).
+// Per-feature inputs of the finalisation, loadable ahead of the phase check.
+template <int KP>
+struct FinIn {
+  float iv, xv[KP], fx[KP], wo[KP];
+  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
+    load_f(cfg, dv, blk * 256 + threadIdx.x);
+  }
+  __device__ __forceinline__ void load_f(const SolverCfg& cfg, const SolveDev& dv, int f) {
+    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
+    if (f >= FP) return;
+    iv = dv.inv_std[f];
+#pragma unroll
+    for (int c = 0; c < KP; ++c) {
+      xv[c] = dv.x[c * FPI + f];
+      fx[c] = dv.wfix[c * FPI + f];
+      wo[c] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
+    }
+  }
+};
+
+template <int KP>
+__device__ __forceinline__ void finalize_feature(const SolverCfg& cfg, const SolveDev& dv, int f, const FinIn<KP>& in) {
+  const int FP = cfg.Fp, K = cfg.K;
+  if (f < FP) {
+    const float iv = in.iv;
+    const float *xv = in.xv, *fx = in.fx, *wo = in.wo;
+    float wv[KP];
+    float mean = 0.f;
+#pragma unroll
+    for (int c = 0; c < KP; ++c) {
+      wv[c] = f < cfg.F ? (iv > 0.f ? xv[c] * iv : fx[c]) : 0.f;
+      mean += wv[c];
+    }
+    mean = (cfg.center && f < cfg.F) ? mean / (float)K : 0.f;
+#pragma unroll
+    for (int c = 0; c < KP; ++c) {
+      const float v = c < K ? wv[c] - mean : 0.f;
+      write_frag(dv.out_hi, dv.out_lo, c, f, v);
+      if (c < K) {
+        const float dl = v - wo[c];
+        dv.delta[c * FP + f] = dl;
+        if (dv.w_new) dv.w_new[c * FP + f] = v;
+        if (dv.ap_w) {  // fused server update: w += lr * delta (ServerProcessor.java:148-151)
+          // (ap_w may alias w_old: this thread alone reads and writes element (c, f))
+          const float nw = wo[c] + dv.ap_lr * dl;
+          dv.ap_w[c * FP + f] = nw;
+          write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
+        }
+      }
+    }
+  }
+}
+
+// The intercepts, the loss and the solver statistics (one thread).  Every load
+// is issued before the first store (they are independent): one memory round
+// trip instead of a chain of them -- this is most of the tail launch's time
+// when the last bwd_update launch finalised the features.
+struct FinScal {
+  float bv[16], wo[16];
+  double f_c;
+  int evals, nacc, ls_fail, dir_reset, st4;
+  unsigned run;
+  unsigned long long err;
+  __device__ __forceinline__ void load(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv) {
+    const int K = cfg.K, IB = dv.KP * dv.FPI, KF = K * cfg.Fp;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      bv[c] = c < K ? dv.x[IB + c] : 0.f;
+      wo[c] = c < K ? dv.w_old[KF + c] : 0.f;
+    }
+    f_c = ctrl->f_c;
+    evals = ctrl->evals;
+    nacc = ctrl->nacc;
+    ls_fail = ctrl->ls_fail;
+    dir_reset = ctrl->dir_reset;
+    run = *dv.prm_count;
+    // a cross-workgroup wait that timed out (a workgroup was not co-resident):
+    // this solve's result is garbage -- sticky flag for the host, NaN loss in the logs
+    err = dv.stats ? xload(dv.xch + kXchErr) : 0ull;
+    st4 = dv.stats ? dv.stats[4] : 0;
+  }
+  __device__ __forceinline__ void store(const SolverCfg& cfg, const SolveDev& dv) const {
+    const int K = cfg.K, KF = K * cfg.Fp;
+    float mean = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) mean += c < K ? bv[c] : 0.f;
+    mean = cfg.center ? mean / (float)K : 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if (c >= K) continue;
+      const float v = bv[c] - mean;
+      const float dl = v - wo[c];
+      dv.delta[KF + c] = dl;
+      if (dv.w_new) dv.w_new[KF + c] = v;
+      dv.b_fin[c] = v;
+      if (dv.ap_w) {
+        const float nw = wo[c] + dv.ap_lr * dl;
+        dv.ap_w[KF + c] = nw;
+        dv.ap_b[dv.ap_coff + c] = nw;
+      }
+    }
+    *dv.loss = err ? __builtin_nanf("") : (float)f_c;
+    *dv.prm_count = run + 1;  // run counter: makes the all-gather tags unique per run
+    if (dv.stats) {
+      dv.stats[0] = evals;
+      dv.stats[1] = nacc;
+      dv.stats[2] = ls_fail;
+      dv.stats[3] = dir_reset;
+      if (err) {
+        dv.stats[4] = st4 | (int)err;
+        xstore(dv.xch + kXchErr, 0ull);
+      }
+    }
+  }
+};
+
+template <int KP>
+__device__ __forceinline__ void finalize_scalars(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv) {
+  FinScal sc;
+  sc.load(cfg, ctrl, dv);
+  sc.store(cfg, dv);
+}
+
+// Finalisation over 32-feature slices (FP/32 workgroups, one (class, feature)
+// element per thread): the scattered fragment / delta stores spread over 32 CUs
+// instead of 4.  Same arithmetic (and class order of the centring mean) as
+// finalize_feature.
+template <int KP>
+struct FinSl {
+  static constexpr int NE = KP > 8 ? KP / 8 : 1;
+  float iv, xv[NE], fx[NE], wo[NE];
+  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
+    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
+    const int f = blk * 32 + (threadIdx.x & 31), cg = threadIdx.x >> 5;
+    iv = dv.inv_std[f];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const int c = cg + 8 * e;
+      xv[e] = fx[e] = wo[e] = 0.f;
+      if (c < KP) {
+        xv[e] = dv.x[c * FPI + f];
+        fx[e] = dv.wfix[c * FPI + f];
+        wo[e] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
+      }
+    }
+  }
+};
+
+template <int KP>
+__device__ __forceinline__ void finalize_slice(const SolverCfg& cfg, const SolveDev& dv, int blk, const FinSl<KP>& in,
+                                               float* wvl /* LDS [16][32] */) {
+  constexpr int NE = FinSl<KP>::NE;
+  const int FP = cfg.Fp, K = cfg.K;
+  const int fl = threadIdx.x & 31, cg = threadIdx.x >> 5, f = blk * 32 + fl;
+  float wv[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cg + 8 * e;
+    wv[e] = (c < KP && f < cfg.F) ? (in.iv > 0.f ? in.xv[e] * in.iv : in.fx[e]) : 0.f;
+    if (c < KP) wvl[c * 32 + fl] = wv[e];
+  }
+  __syncthreads();
+  float mean = 0.f;
+#pragma unroll
+  for (int c = 0; c < KP; ++c) mean += wvl[c * 32 + fl];  // class order: as finalize_feature
+  mean = (cfg.center && f < cfg.F) ? mean / (float)K : 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cg + 8 * e;
+    if (c >= KP) continue;
+    const float v = c < K ? wv[e] - mean : 0.f;
+    write_frag(dv.out_hi, dv.out_lo, c, f, v);
+    if (c < K) {
+      const float dl = v - in.wo[e];
+      dv.delta[c * FP + f] = dl;
+      if (dv.w_new) dv.w_new[c * FP + f] = v;
+      if (dv.ap_w) {  // fused server update (see finalize_feature)
+        const float nw = in.wo[e] + dv.ap_lr * dl;
+        dv.ap_w[c * FP + f] = nw;
+        write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // bwd_update_kernel: gradient of a 32-feature slice, controller step, update.
 // Both MFMA operands come straight from global memory in fragment shape: the
 // residual tiles R (class x 8 rows = 16 B per lane) and the feature-major ring
@@ -555,7 +744,7 @@ size_t bwd_lds_bytes() {
 template <int FP, int KP, bool kP = false>
 __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
                                          const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
-                                         const bool check_done = false) {
+                                         const bool check_done = false, const int fin_slot = kNoFinSlot) {
   constexpr int FPI = FP > 256 ? FP : 256;
   constexpr int IB = KP * FPI;              // internal intercept base
   constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
@@ -630,6 +819,15 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     FX[e] = dv.wfix[idx[e]];
   }
   const float iv = dv.inv_std[f];
+  // a launch that may finish the solve finalises its slice in place (below):
+  // its w_old elements travel with the per-element state
+  const bool may_fin = slot >= fin_slot;
+  float WO[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int c = cgp + 8 * e;
+    WO[e] = (may_fin && c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
+  }
   const int nfw = ntiles < fwd_grid ? ntiles : fwd_grid;
   float db0 = 0.f, gcb0 = 0.f, xb0 = 0.f;
   if (wg0 && tid < 255) {  // intercept gradient / loss partials: 15 stripes x 17 values, fixed order
@@ -886,6 +1084,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (tid == 0) {
     if (wg0) stamp(dv, slot, 5);
     ctrl_step(*cl, cfg, dots[kND] / (double)B, dots, slot, *csw);
+    cl->fin = (may_fin && cl->phase == kPhDone) ? 1 : 0;  // finalised by this launch (tail: scalars only)
     if (wg0) stamp(dv, slot, 6);
   }
   __syncthreads();
@@ -971,6 +1170,21 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       if (own[e]) dv.d[idx[e]] = dn[e];
     if (ib) dv.d[IB + tid] = dbv;
   }
+  // ---- the solve ended in this launch: finalise this slice in place (no
+  // launch reads the fragments it rewrites: the riding evaluation workgroups
+  // are all in launches before fin_slot) ----
+  if (done && may_fin) {
+    FinSl<KP> in;
+    in.iv = iv;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      in.xv[e] = own[e] ? XO[e] : 0.f;
+      in.fx[e] = own[e] ? FX[e] : 0.f;
+      in.wo[e] = WO[e];
+    }
+    __syncthreads();  // gw (the gradient's LDS) is free: its last reads preceded the dots
+    finalize_slice<KP>(cfg, dv, wg, in, gw);
+  }
   // ---- next trial point: this slice of the MFMA weight fragments (16-B stores) ----
   if (!done) {
 #pragma unroll
@@ -1010,14 +1224,14 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
 template <int FP, int KP>
 __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
                                                          SolveDev dv, int fwd_grid, SolveParams win, int ns,
-                                                         EvalRide ride, int ride_t0) {
+                                                         EvalRide ride, int ride_t0, int fin_slot) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   if ((int)blockIdx.x >= ns) {  // an evaluation workgroup riding in this launch: one test tile
     const int t = ride_t0 + (int)blockIdx.x - ns;
     eval_body<FP>(lds, ride, t, 1, t + 1);
     return;
   }
-  bwd_body<FP, KP>(cfg, window_of(win, prm), gctrl, slot, dv, fwd_grid, lds, blockIdx.x, ns, true);
+  bwd_body<FP, KP>(cfg, window_of(win, prm), gctrl, slot, dv, fwd_grid, lds, blockIdx.x, ns, true, fin_slot);
 }
 
 // ---------------------------------------------------------------------------
@@ -1054,171 +1268,6 @@ __device__ __forceinline__ void grid_barrier(unsigned long long* ctr, unsigned l
   __syncthreads();
 }
 
-// ---------------------------------------------------------------------------
-// Finalisation (after the last slot): back to the unstandardised space,
-// multinomial centring across classes, delta = w_new - w_old, eval fragments,
-// loss and solver statistics.  One thread per feature (all classes).
-// Per-feature inputs of the finalisation, loadable ahead of the phase check.
-template <int KP>
-struct FinIn {
-  float iv, xv[KP], fx[KP], wo[KP];
-  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
-    load_f(cfg, dv, blk * 256 + threadIdx.x);
-  }
-  __device__ __forceinline__ void load_f(const SolverCfg& cfg, const SolveDev& dv, int f) {
-    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
-    if (f >= FP) return;
-    iv = dv.inv_std[f];
-#pragma unroll
-    for (int c = 0; c < KP; ++c) {
-      xv[c] = dv.x[c * FPI + f];
-      fx[c] = dv.wfix[c * FPI + f];
-      wo[c] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
-    }
-  }
-};
-
-template <int KP>
-__device__ __forceinline__ void finalize_feature(const SolverCfg& cfg, const SolveDev& dv, int f, const FinIn<KP>& in) {
-  const int FP = cfg.Fp, K = cfg.K;
-  if (f < FP) {
-    const float iv = in.iv;
-    const float *xv = in.xv, *fx = in.fx, *wo = in.wo;
-    float wv[KP];
-    float mean = 0.f;
-#pragma unroll
-    for (int c = 0; c < KP; ++c) {
-      wv[c] = f < cfg.F ? (iv > 0.f ? xv[c] * iv : fx[c]) : 0.f;
-      mean += wv[c];
-    }
-    mean = (cfg.center && f < cfg.F) ? mean / (float)K : 0.f;
-#pragma unroll
-    for (int c = 0; c < KP; ++c) {
-      const float v = c < K ? wv[c] - mean : 0.f;
-      write_frag(dv.out_hi, dv.out_lo, c, f, v);
-      if (c < K) {
-        const float dl = v - wo[c];
-        dv.delta[c * FP + f] = dl;
-        if (dv.w_new) dv.w_new[c * FP + f] = v;
-        if (dv.ap_w) {  // fused server update: w += lr * delta (ServerProcessor.java:148-151)
-          // (ap_w may alias w_old: this thread alone reads and writes element (c, f))
-          const float nw = wo[c] + dv.ap_lr * dl;
-          dv.ap_w[c * FP + f] = nw;
-          write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
-        }
-      }
-    }
-  }
-}
-
-// The intercepts, the loss and the solver statistics (one thread).
-template <int KP>
-__device__ __forceinline__ void finalize_scalars(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv) {
-  const int FP = cfg.Fp, K = cfg.K;
-  {
-    const int IB = dv.KP * dv.FPI;
-    float bv[16];
-    float mean = 0.f;
-    for (int c = 0; c < K; ++c) {
-      bv[c] = dv.x[IB + c];
-      mean += bv[c];
-    }
-    mean = cfg.center ? mean / (float)K : 0.f;
-    const int KF = K * FP;
-    for (int c = 0; c < K; ++c) {
-      const float v = bv[c] - mean;
-      const float wo = dv.w_old[KF + c];
-      const float dl = v - wo;
-      dv.delta[KF + c] = dl;
-      if (dv.w_new) dv.w_new[KF + c] = v;
-      dv.b_fin[c] = v;
-      if (dv.ap_w) {
-        const float nw = wo + dv.ap_lr * dl;
-        dv.ap_w[KF + c] = nw;
-        dv.ap_b[dv.ap_coff + c] = nw;
-      }
-    }
-    *dv.loss = (float)ctrl->f_c;
-    *dv.prm_count += 1;  // run counter: makes the all-gather tags unique per run
-    if (dv.stats) {
-      dv.stats[0] = ctrl->evals;
-      dv.stats[1] = ctrl->nacc;
-      dv.stats[2] = ctrl->ls_fail;
-      dv.stats[3] = ctrl->dir_reset;
-      // a cross-workgroup wait that timed out (a workgroup was not co-resident):
-      // this solve's result is garbage -- sticky flag for the host, NaN loss in the logs
-      const unsigned long long err = xload(dv.xch + kXchErr);
-      if (err) {
-        dv.stats[4] |= (int)err;
-        xstore(dv.xch + kXchErr, 0ull);
-        *dv.loss = __builtin_nanf("");
-      }
-    }
-  }
-}
-
-// Finalisation over 32-feature slices (FP/32 workgroups, one (class, feature)
-// element per thread): the scattered fragment / delta stores spread over 32 CUs
-// instead of 4.  Same arithmetic (and class order of the centring mean) as
-// finalize_feature.
-template <int KP>
-struct FinSl {
-  static constexpr int NE = KP > 8 ? KP / 8 : 1;
-  float iv, xv[NE], fx[NE], wo[NE];
-  __device__ __forceinline__ void load(const SolverCfg& cfg, const SolveDev& dv, int blk) {
-    const int FP = cfg.Fp, FPI = dv.FPI, K = cfg.K;
-    const int f = blk * 32 + (threadIdx.x & 31), cg = threadIdx.x >> 5;
-    iv = dv.inv_std[f];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-      const int c = cg + 8 * e;
-      xv[e] = fx[e] = wo[e] = 0.f;
-      if (c < KP) {
-        xv[e] = dv.x[c * FPI + f];
-        fx[e] = dv.wfix[c * FPI + f];
-        wo[e] = (c < K && f < cfg.F) ? dv.w_old[c * FP + f] : 0.f;
-      }
-    }
-  }
-};
-
-template <int KP>
-__device__ __forceinline__ void finalize_slice(const SolverCfg& cfg, const SolveDev& dv, int blk, const FinSl<KP>& in,
-                                               float* wvl /* LDS [16][32] */) {
-  constexpr int NE = FinSl<KP>::NE;
-  const int FP = cfg.Fp, K = cfg.K;
-  const int fl = threadIdx.x & 31, cg = threadIdx.x >> 5, f = blk * 32 + fl;
-  float wv[NE];
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const int c = cg + 8 * e;
-    wv[e] = (c < KP && f < cfg.F) ? (in.iv > 0.f ? in.xv[e] * in.iv : in.fx[e]) : 0.f;
-    if (c < KP) wvl[c * 32 + fl] = wv[e];
-  }
-  __syncthreads();
-  float mean = 0.f;
-#pragma unroll
-  for (int c = 0; c < KP; ++c) mean += wvl[c * 32 + fl];  // class order: as finalize_feature
-  mean = (cfg.center && f < cfg.F) ? mean / (float)K : 0.f;
-#pragma unroll
-  for (int e = 0; e < NE; ++e) {
-    const int c = cg + 8 * e;
-    if (c >= KP) continue;
-    const float v = c < K ? wv[e] - mean : 0.f;
-    write_frag(dv.out_hi, dv.out_lo, c, f, v);
-    if (c < K) {
-      const float dl = v - in.wo[e];
-      dv.delta[c * FP + f] = dl;
-      if (dv.w_new) dv.w_new[c * FP + f] = v;
-      if (dv.ap_w) {  // fused server update (see finalize_feature)
-        const float nw = in.wo[e] + dv.ap_lr * dl;
-        dv.ap_w[c * FP + f] = nw;
-        write_frag(dv.ap_hi, dv.ap_lo, dv.ap_coff + c, f, f < cfg.F ? nw : 0.f);
-      }
-    }
-  }
-}
-
 template <int KP>
 __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* ctrl, const SolveDev& dv, int blk,
                                               const FinIn<KP>& in) {
@@ -1229,6 +1278,10 @@ __device__ __forceinline__ void finalize_body(const SolverCfg& cfg, const Ctrl* 
 
 template <int KP>
 __global__ __launch_bounds__(256) void finalize_kernel(SolverCfg cfg, const Ctrl* ctrl, SolveDev dv) {
+  if (ctrl->fin) {  // the last bwd_update launch finalised the features
+    if (blockIdx.x == 0 && threadIdx.x == 0) finalize_scalars<KP>(cfg, ctrl, dv);
+    return;
+  }
   FinIn<KP> in;
   in.load(cfg, dv, blockIdx.x);
   finalize_body<KP>(cfg, ctrl, dv, blockIdx.x, in);
@@ -1252,10 +1305,22 @@ __global__ __launch_bounds__(256) void tail_kernel(SolverCfg cfg, const SolvePar
   int& phase_s = *(int*)(lds + lds_flag);  // past both bodies' LDS (no static __shared__: keeps the base aligned)
   // the finalisation's inputs are fetched before the phase word is known, so
   // the two load latencies overlap (the common case is phase == done)
+  // the scalars' inputs travel with the phase words (one round trip); they are
+  // re-read below when slots run here
+  FinScal sc;
+  const bool t0 = blockIdx.x == 0 && threadIdx.x == 0;
+  if (t0 && nfin > 0) sc.load(cfg, gctrl, dv);
+  if (gctrl->fin) {  // the common case: the last bwd_update launch finished and finalised the solve
+    if (t0) {
+      stamp(dv, 30, 2);
+      if (nfin > 0) sc.store(cfg, dv);
+    }
+    return;
+  }
   FinSl<KP> in;
   float* wvl = (float*)lds;  // finalisation scratch (the slots' LDS is dead by then)
   if ((int)blockIdx.x < nfin) in.load(cfg, dv, blockIdx.x);
-  if (gctrl->phase == kPhDone) {  // the common case: written by the previous launch
+  if (gctrl->phase == kPhDone) {  // written by the previous launch
     // the finalisation is folded into this launch (one graph node less per solve)
     if ((int)blockIdx.x < nfin) {
       if (blockIdx.x == 0 && threadIdx.x == 0) stamp(dv, 30, 2);
@@ -1313,25 +1378,25 @@ int bwd_grid(int FP) { return FP / 32; }
 template <int FP>
 static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
                           int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
-                          int ride_t0 = 0, int nride = 0) {
+                          int ride_t0 = 0, int nride = 0, int fin_slot = kNoFinSlot) {
   const int ns = bwd_grid(FP), ng = ns + nride;
   const size_t bl = nride > 0 ? bwd_ride_lds_bytes(FP) : bwd_lds_bytes();
   switch (dv.KP) {
-    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
-    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
-    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0); break;
+    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
+    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
+    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
     default:
-      bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0);
+      bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot);
       break;
   }
 }
 
 template <int FP>
 static void launch_slot_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
-                           int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
-                           int ride_t0 = 0, int nride = 0) {
+                           int nwg, hipStream_t s, const SolveParams& win, int fin_slot,
+                           const EvalRide& ride = EvalRide{}, int ride_t0 = 0, int nride = 0) {
   fwd_kernel<FP><<<nwg, 256, fwd_lds_bytes(FP), s>>>(cfg, prm, ctrl, slot, dv, win);
-  launch_bwd_fp<FP>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride);
+  launch_bwd_fp<FP>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride, fin_slot);
 }
 
 void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int fwd_grid,
@@ -1347,25 +1412,26 @@ void launch_bwd(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int sl
 }
 
 void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                      hipStream_t s, const SolveParams& win, const EvalRide& ride, int ride_t0, int nride) {
+                      hipStream_t s, const SolveParams& win, const EvalRide& ride, int ride_t0, int nride,
+                      int fin_slot) {
   switch (cfg.Fp) {
-    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
-    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
-    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
-    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
-    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win, ride, ride_t0, nride); break;
+    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot, ride, ride_t0, nride); break;
+    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot, ride, ride_t0, nride); break;
+    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot, ride, ride_t0, nride); break;
+    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot, ride, ride_t0, nride); break;
+    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot, ride, ride_t0, nride); break;
     default: break;
   }
 }
 
 void launch_slot(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv, int nwg,
-                 hipStream_t s, const SolveParams& win) {
+                 hipStream_t s, const SolveParams& win, int fin_slot) {
   switch (cfg.Fp) {
-    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
-    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
-    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
-    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
-    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win); break;
+    case 128: launch_slot_fp<128>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot); break;
+    case 256: launch_slot_fp<256>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot); break;
+    case 512: launch_slot_fp<512>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot); break;
+    case 1024: launch_slot_fp<1024>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot); break;
+    case 2048: launch_slot_fp<2048>(cfg, prm, ctrl, slot, dv, nwg, s, win, fin_slot); break;
     default: break;
   }
 }

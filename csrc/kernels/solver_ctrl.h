@@ -80,6 +80,8 @@ struct SolverCfg {
 // (i < n) of the resident dataset go to ring slots (dst + i) % cap, and must be
 // the newest n rows of the window.  n == 0: nothing to ingest.
 constexpr int kMaxFusedIngest = 1024;
+// fin_slot of a launch chain that never finalises inside bwd_update
+constexpr int kNoFinSlot = 1 << 30;
 struct RingIngest {
   const uint16_t* src;   // dataset rows [*][Fp] bf16
   const int32_t* ysrc;   // dataset labels
@@ -97,7 +99,7 @@ struct Ctrl {
   int phase, action, action_slot, iter;
   int ls_i, zoom, evals, m;
   int head, push_slot, nacc, ls_fail;
-  int dir_reset, pad0, pad1, pad2;
+  int dir_reset, fin, pad1, pad2;  // fin: features finalised by the last bwd_update launch
   double t;      // next trial step (consumed by the update kernel)
   double t_acc;  // accepted step (consumed by the update kernel)
   double f_c, dg0, gg_c, f_init;
@@ -124,6 +126,7 @@ PSX_HD inline void ctrl_init(Ctrl& c) {
   c.head = -1;
   c.push_slot = -1;
   c.nacc = c.ls_fail = c.dir_reset = 0;
+  c.fin = 0;
   c.t = 0.0;
   c.t_acc = 0.0;
   c.f_c = c.dg0 = c.gg_c = c.f_init = 0.0;

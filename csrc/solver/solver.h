@@ -69,7 +69,8 @@ class LocalSolver {
 
  private:
   void enqueue_body(hipStream_t s, int B, int start, const RingIngest& ing, bool capturing, const EvalRide* ride);
-  int ride_split_ = 3;
+  int ride_split_ = 2;       // riding evaluation tiles over the first 2 bwd_update launches
+  bool fin_inplace_ = true;  // the last bwd_update launch finalises (PSX_FIN_INPLACE=0: the tail does)
   SolverCfg cfg_;
   SolveDev dv_{};
   int nwg_eval_;

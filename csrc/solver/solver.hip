@@ -130,6 +130,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
 
   // riding evaluation passes spread over this many slots' bwd_update launches
   if (const char* e = std::getenv("PSX_RIDE_SPLIT")) ride_split_ = std::atoi(e) > 0 ? std::atoi(e) : 1;
+  if (const char* e = std::getenv("PSX_FIN_INPLACE")) fin_inplace_ = std::atoi(e) != 0;
   prepare_kernels();  // >64 KiB dynamic LDS for the wide tiles (gfx950: 160 KiB per CU)
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
@@ -195,13 +196,18 @@ void LocalSolver::enqueue_body(hipStream_t s, int B, int start, const RingIngest
   // launches of the first `nsplit` slots (extra workgroups beside the slices)
   const int rt = ride ? ride->ntiles() : 0;
   const int nsplit = ride ? (ride_split_ < nfast_ ? ride_split_ : nfast_) : 1;
+  // the bwd_update launch that ends the solve finalises the features in place
+  // (the tail / finalize launch then writes only the scalars), from the first
+  // slot after the riding workgroups: none of them may read the model fragments
+  // that finalisation rewrites
+  const int fin_slot = fin_inplace_ ? (ride ? nsplit : 0) : kNoFinSlot;
   int t0 = 0;
   for (int slot = 0; slot < nfast_; ++slot) {
     const int n = slot < nsplit ? (rt - t0 + (nsplit - slot) - 1) / (nsplit - slot) : 0;
     if (n > 0)
-      launch_slot_ride(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win, *ride, t0, n);
+      launch_slot_ride(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win, *ride, t0, n, fin_slot);
     else
-      launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win);
+      launch_slot(cfg_, prm_, ctrl_, slot, dv_, nwg_eval_, s, win, fin_slot);
     t0 += n;
   }
   if (cfg_.nslots > nfast_)

@@ -378,3 +378,33 @@ def test_persistent_solve_matches_chain(cuda, n, B, pre):
     scale = outs[1][0].abs().max().item()
     assert (outs[0][0] - outs[1][0]).abs().max().item() <= 2e-3 * scale
     assert abs(outs[0][1] - outs[1][1]) <= 1e-4 * max(1.0, abs(outs[1][1]))
+
+
+@pytest.mark.parametrize("ls_max,iters", [(4, 2), (1, 3), (4, 1)])
+def test_inplace_finalisation_matches_tail(cuda, monkeypatch, ls_max, iters):
+    """The bwd_update launch that ends the solve finalises its feature slice in
+    place (PSX_FIN_INPLACE, default on); the tail launch then writes only the
+    scalars.  Bitwise the same delta, loss, model fragments and statistics as the
+    tail's finalisation -- also when the line search needs the tail's extra slots
+    (ls_max 1 / several iterations exercise both exits)."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(2048, seed=21).to(cuda)
+    cap = 1024
+    outs = []
+    for fin in ("1", "0"):
+        monkeypatch.setenv("PSX_FIN_INPLACE", fin)
+        ring = DeviceRing(cap, ds.Fp, cuda)
+        ring.place(ds.X[:cap], ds.y[:cap])
+        runs = []
+        for seed, sc in ((3, 0.05), (4, 0.05), (5, 8.0)):  # large weights: line-search retries in the tail
+            w = _rand_w(spec, seed, sc).to(cuda)
+            op = LocalSolveOp(spec, cap, cuda, SolverOptions(use_graph=False, iters=iters, ls_max=ls_max))
+            op.run(ring, cap, 0, w)
+            torch.cuda.synchronize()
+            runs.append((op.delta.clone(), op.loss.item(), op.stats.cpu().tolist(), op.frag.hi.clone(),
+                         op.frag.lo.clone(), op.frag.b.clone()))
+        outs.append(runs)
+    for a, b in zip(*outs):
+        assert torch.equal(a[0], b[0])
+        assert a[1] == b[1] and a[2] == b[2] and a[2][4] == 0
+        assert torch.equal(a[3], b[3]) and torch.equal(a[4], b[4]) and torch.equal(a[5], b[5])

@@ -93,6 +93,9 @@ def parse(argv=None):
     ap.add_argument("--dedicated-server", action="store_true",
                     help="multi-GPU BSP with a dedicated server rank (BASELINE config 2: reduce + broadcast)")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
+    ap.add_argument("--no-accuracy-run", dest="accuracy_run", action="store_false",
+                    help="with --steps < 2000: skip the untimed continuation to 2000 rounds that reports the "
+                         "accuracy half of the metric (accuracy_run in the JSON)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
     wide = a.model != "dense"
@@ -271,8 +274,34 @@ def main(argv=None):
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res.update(_accuracy_fields(eng.log.book.server))
+    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense":
+        rows = list(eng.log.book.server)
+        eng.cfg.max_iters = ACC_ROUNDS - a.steps
+        eng.log = _fresh_log(eng)
+        eng.run()
+        res["accuracy_run"] = _accuracy_run(rows, list(eng.log.book.server), a.steps)
     print(json.dumps(res))
     return res
+
+
+ACC_ROUNDS = 2000  # the default --steps: the accuracy half of the metric is quoted at this many rounds
+
+
+def _accuracy_run(timed_rows, extra_rows, steps):
+    """Accuracy half of the metric when the timed region is shorter than
+    ACC_ROUNDS (the driver's short runs): the same engine keeps training, UNTIMED,
+    until ACC_ROUNDS rounds past the warm-up, and the server's test-set rows of
+    the timed region plus that continuation give the curve.  updates/s is never
+    taken from the continuation."""
+    rows = timed_rows + extra_rows
+    out = {"rounds_after_warmup": ACC_ROUNDS, "timed_rounds": steps, "untimed_continuation_rounds": ACC_ROUNDS - steps}
+    out.update(_accuracy_fields(rows))
+    if rows:
+        out["best_test_f1"] = round(max(r[2] for r in rows), 4)
+        out["test_f1"] = round(rows[-1][2], 4)
+        out["test_accuracy"] = round(rows[-1][3], 4)
+        out["wallclock_s"] = round((rows[-1][0] - rows[0][0]) / 1000.0, 4)
+    return out
 
 
 def _free_port() -> int:
@@ -373,6 +402,19 @@ def bench_distributed(a):
         res.update(_accuracy_fields(book.server))
         if rccl is not None and rccl != world:
             raise SystemExit(f"bench.py: RCCL communicator has {rccl} ranks, world is {world}")
+    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not async_mode:
+        # untimed continuation for the accuracy half (see _accuracy_run); every rank runs it
+        timed_rows = list(eng.log.book.server) if rank == 0 else []
+        if eng.log is not None:
+            if rank != 0:
+                eng.log.close()
+            eng.log = LogSink(eng.spec.eval_classes, eng.device, keep_records=(rank == 0))
+        cfg.max_iters = ACC_ROUNDS - a.steps
+        eng._run_bsp()
+        if rank == 0:
+            eng.log.close()
+            res["accuracy_run"] = _accuracy_run(timed_rows, list(eng.log.book.server), a.steps)
+    if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()
     dist.barrier()

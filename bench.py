@@ -95,7 +95,7 @@ def parse(argv=None):
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     ap.add_argument("--no-accuracy-run", dest="accuracy_run", action="store_false",
                     help="with --steps < 2000: skip the untimed continuation to 2000 rounds that reports the "
-                         "accuracy half of the metric (accuracy_run in the JSON)")
+                         "accuracy half of the metric (accuracy_run in the JSON; GPU runs only)")
     a = ap.parse_args(argv)
     m = MODELS[a.model]
     wide = a.model != "dense"
@@ -274,7 +274,7 @@ def main(argv=None):
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res.update(_accuracy_fields(eng.log.book.server))
-    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense":
+    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not a.cpu:
         rows = list(eng.log.book.server)
         eng.cfg.max_iters = ACC_ROUNDS - a.steps
         eng.log = _fresh_log(eng)
@@ -402,7 +402,7 @@ def bench_distributed(a):
         res.update(_accuracy_fields(book.server))
         if rccl is not None and rccl != world:
             raise SystemExit(f"bench.py: RCCL communicator has {rccl} ranks, world is {world}")
-    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not async_mode:
+    if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not async_mode and not a.cpu:
         # untimed continuation for the accuracy half (see _accuracy_run); every rank runs it
         timed_rows = list(eng.log.book.server) if rank == 0 else []
         if eng.log is not None:

@@ -104,6 +104,54 @@ __device__ __forceinline__ float ld_sc1_f32(__amdgpu_buffer_rsrc_t r, unsigned b
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)byte_off, 0, kAuxSc1));
 }
 
+// Hand-off accessors by the parties' scope.  S = 1: the workgroups are spread
+// over the XCDs -- sc1 accesses as above.  S = 2: every party runs on ONE XCD
+// (blockIdx % 8 == XCC_ID on MI355X) and so shares one L2: a plain store reaches
+// that L2 through the write-through vector L1, an nt load misses the L1 and
+// reads it.  Measured (tools/xcd_probe.hip, profiles/r02_v5/): a 32-workgroup
+// hand-off costs 0.64 us that way, 1.7 us with sc1 flags and 2.7 us with sc1 + an
+// atomic arrival counter (sc0 loads and L2-executed counters do NOT work: device
+// memory's atomics are performed past the L2).
+constexpr int kAuxNt = 2;
+template <int S>
+__device__ __forceinline__ float ld_h(const float* p) {
+  if constexpr (S == 2) return __builtin_nontemporal_load(p);
+  else return ld_sc1(p);
+}
+template <int S>
+__device__ __forceinline__ double ld_h(const double* p) {
+  if constexpr (S == 2) return __builtin_nontemporal_load(p);
+  else return ld_sc1(p);
+}
+template <int S>
+__device__ __forceinline__ void st_h(float* p, float v) {
+  if constexpr (S == 2) *p = v;
+  else st_sc1(p, v);
+}
+template <int S>
+__device__ __forceinline__ u16x8 ld_h_b128(__amdgpu_buffer_rsrc_t r, unsigned byte_off) {
+  return __builtin_bit_cast(u16x8,
+                            __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, S == 2 ? kAuxNt : kAuxSc1));
+}
+template <int S>
+__device__ __forceinline__ void st_h_b128(__amdgpu_buffer_rsrc_t r, unsigned byte_off, u16x8 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)byte_off, 0, S == 2 ? 0 : kAuxSc1);
+}
+template <int S>
+__device__ __forceinline__ unsigned long long ld_h64(unsigned long long* p) {
+  if constexpr (S == 2) {
+    asm volatile("" ::: "memory");  // a spin re-reads: never fold the load out of the loop
+    return __builtin_nontemporal_load(p);
+  } else {
+    return __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+template <int S>
+__device__ __forceinline__ void st_h64(unsigned long long* p, unsigned long long v) {
+  if constexpr (S == 2) *(volatile unsigned long long*)p = v;
+  else __hip_atomic_store((g_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Dual-use LDS image of a [rows][128 x bf16] sub-tile with 256-B rows: row
 // reads (ds_read_b128) and transposed reads (ds_read_b64_tr_b16) share one
 // copy.  Byte offset of 16-B chunk `ch` (0..15) of `row`:

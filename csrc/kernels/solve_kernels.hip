@@ -73,7 +73,10 @@ constexpr int kXchErr = kXchBar + 1;
 constexpr int kXchPhase = kXchErr + 1;  // persistent solve: the controller phase after a slot (wg 0 -> row-only wgs)
 constexpr int kXchGen = kXchPhase + 1;  // persistent solve: the barrier counters of even / odd runs
 constexpr int kXchRide = kXchGen + 2;   // persistent solve: riding workgroups done, even / odd runs
-int xch_words() { return kXchRide + 2; }
+// one-XCD persistent solve: workgroup i's arrival word at kXchFlags + 32 i (own 256-B line)
+constexpr int kXchFlags = (kXchRide + 2 + 31) / 32 * 32;
+constexpr int kMaxXcdWg = 32;  // CUs of one MI355X XCD
+int xch_words() { return kXchFlags + 32 * kMaxXcdWg; }
 constexpr int kPartStride = 32;  // fwd partials per workgroup: rsum[16], loss
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -92,6 +95,16 @@ struct WinTiles {
       : s0(start & 31), t0(start >> 5), T(cap >> 5), nt(((start & 31) + B + 31) >> 5) {}
   __device__ __forceinline__ int ring_tile(int i) const { return t0 + i >= T ? t0 + i - T : t0 + i; }
 };
+// Physical history slot i holds one of the m stored pairs (ring head = newest);
+// no integer modulo (H is a runtime value: each % costs ~40 instructions).
+__device__ __forceinline__ bool pair_valid(int i, int m, int head, int H) {
+  if (i >= H || m <= 0) return false;
+  if (m >= H) return true;
+  int d = i - (head - m + 1);  // in [-(H-1), 2H-3]: (d mod H) < m
+  if (d < 0) d += H;
+  if (d >= H) d -= H;
+  return d < m;
+}
 __device__ __forceinline__ unsigned long long d2u(double v) { return __builtin_bit_cast(unsigned long long, v); }
 __device__ __forceinline__ double u2d(unsigned long long v) { return __builtin_bit_cast(double, v); }
 
@@ -322,7 +335,7 @@ __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned sho
 // kP (persistent solve): the tile and its labels are already resident in LDS,
 // and the trial point (fragments, intercepts) is read / the partials written
 // with sc1 accesses (an in-launch hand-off, see common.h).
-template <int FP, bool kRows = false, bool kF32 = false, bool kP = false>
+template <int FP, bool kRows = false, bool kF32 = false, int kP = 0>
 __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams pr, int slot, const SolveDev& dv,
                                          char* lds, const int wg, const int G, f32x4* gacc = nullptr,
                                          const int entry_phase = -1) {
@@ -344,21 +357,27 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   const int sr = tid >> 3, sc0 = (tid & 7) * 2;
   float rs0 = 0.f, rs1 = 0.f;
   static_assert(!kP || (FP <= 1024 && kRows && !kF32), "persistent solve: rows-form bodies, FP <= 1024");
-  const float bz0 = kP ? ld_sc1(dv.b_eff + sc0) : dv.b_eff[sc0];
-  const float bz1 = kP ? ld_sc1(dv.b_eff + sc0 + 1) : dv.b_eff[sc0 + 1];
+  float bz0, bz1;
+  if constexpr (kP != 0) {
+    bz0 = ld_h<kP>(dv.b_eff + sc0);
+    bz1 = ld_h<kP>(dv.b_eff + sc0 + 1);
+  } else {
+    bz0 = dv.b_eff[sc0];
+    bz1 = dv.b_eff[sc0 + 1];
+  }
   // the trial weights do not depend on the tile: fetch them before staging so
   // the two memory latencies overlap (register budget allows it up to FP 1024)
   constexpr bool kPre = FP <= 1024;
   WFrag<kPre ? FP : 128> wf;
   if constexpr (kPre) {
-    if constexpr (kP)
-      load_wfrag_sc1<FP>(wf, dv.whi, dv.wlo, K);
+    if constexpr (kP != 0)
+      load_wfrag_sc1<FP, kP>(wf, dv.whi, dv.wlo, K);
     else
       load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
   }
   for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-    if constexpr (!kP) {  // (persistent: staged once, at the start of the solve)
+    if constexpr (kP == 0) {  // (persistent: staged once, at the start of the solve)
       const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads (one round trip)
       if constexpr (kF32)
         stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
@@ -447,8 +466,8 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   if (tid < 16) pv = ((rsum[tid] + rsum[16 + tid]) + rsum[32 + tid]) + rsum[48 + tid];
   if (tid == 16) pv = lred[0] + lred[1] + lred[2] + lred[3];
   if (tid < 17) {
-    if constexpr (kP)
-      st_sc1(part + tid, pv);
+    if constexpr (kP != 0)
+      st_h<kP>(part + tid, pv);
     else
       part[tid] = pv;
   }
@@ -741,7 +760,7 @@ size_t bwd_lds_bytes() {
 // across slots (no copy-in / write-back), the partials written by other
 // workgroups of the launch are read with sc1 loads and the next trial point is
 // published with sc1 stores (common.h).
-template <int FP, int KP, bool kP = false>
+template <int FP, int KP, int kP = 0>
 __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
                                          const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
                                          const bool check_done = false, const int fin_slot = kNoFinSlot) {
@@ -776,8 +795,9 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // the feature-major window XT of this slice, kBwdBatch k-steps per wave in
   // flight -- issued ahead of every other load so that one memory round trip
   // covers them, the controller copy and the per-element state together ----
-  const bool gpf = dv.gpf != nullptr;                // partials of the forward workgroups, [g][f][KP]
-  const bool gred = !gpf && dv.gpart != nullptr;     // rows mode: partials [g][KP][FP]
+  // partials of the forward workgroups [g][f][KP] (always, in the persistent solve)
+  const bool gpf = kP != 0 || dv.gpf != nullptr;
+  const bool gred = kP == 0 && !gpf && dv.gpart != nullptr;  // rows mode: partials [g][KP][FP]
   const int m16 = lane & 15, kg = (lane >> 4) * 8;
   const unsigned short* xt0 = dv.XT + (size_t)(fs + m16) * cap + kg;  // N-tile 0 (features fs..fs+15)
   const unsigned short* xt1 = xt0 + (size_t)16 * cap;                  // N-tile 1
@@ -801,7 +821,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   };
   if (!gred && !gpf) load_batch(0);
   // every workgroup runs the (deterministic) controller on its own LDS copy
-  if constexpr (!kP)
+  if constexpr (kP == 0)
     copy_words_to_lds<sizeof(Ctrl) / 8, 256>((unsigned long long*)cl, (const unsigned long long*)gctrl);
 
   // ---- per-element state first (independent of the backward) ----
@@ -819,6 +839,14 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     FX[e] = dv.wfix[idx[e]];
   }
   const float iv = dv.inv_std[f];
+  const bool ib0 = wg0 && tid < 16;
+  // stored curvature pairs of this slice (measured: prefetching them with the
+  // backward's operands lengthens the load phase by ~1 us and saves nothing
+  // later -- profiles/r02_v5/README.md -- so they are read where needed)
+  auto s_at = [&](int i, int e) { return dv.S[(size_t)i * PI + idx[e]]; };
+  auto y_at = [&](int i, int e) { return dv.Y[(size_t)i * PI + idx[e]]; };
+  auto sb_at = [&](int i) { return dv.S[(size_t)i * PI + IB + tid]; };
+  auto yb_at = [&](int i) { return dv.Y[(size_t)i * PI + IB + tid]; };
   // a launch that may finish the solve finalises its slice in place (below):
   // its w_old elements travel with the per-element state
   const bool may_fin = slot >= fin_slot;
@@ -836,7 +864,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
 #pragma unroll 4
     for (int s = g0; s < nfw; s += 15) {
       const float* pp = dv.part + (size_t)s * kPartStride + k;
-      a += kP ? ld_sc1(pp) : *pp;
+      if constexpr (kP != 0)
+        a += ld_h<kP>(pp);
+      else
+        a += *pp;
     }
     pr[g0 * 17 + k] = a;
   }
@@ -886,7 +917,12 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
           const int g = g0 + 4 * u;
           const size_t eo = ((size_t)g * FP + fs) * KP + p * 4;
           v[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-          if (g < nfw_g) v[u] = kP ? ld_sc1_b128(rg, (unsigned)(eo * 4)) : *(const u16x8*)(dv.gpf + eo);
+          if (g < nfw_g) {
+            if constexpr (kP != 0)
+              v[u] = ld_h_b128<kP>(rg, (unsigned)(eo * 4));
+            else
+              v[u] = *(const u16x8*)(dv.gpf + eo);
+          }
         }
 #pragma unroll
         for (int u = 0; u < UG; ++u) a += __builtin_bit_cast(f32x4, v[u]);
@@ -894,7 +930,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     } else if (p < 16 && KP == 2) {  // 32 features x 2 classes = 16 x 16 B as well
       for (int g = q; g < nfw_g; g += 4) {
         const float* src = dv.gpf + ((size_t)g * FP + fs) * KP + p * 4;
-        a += kP ? f32x4{ld_sc1(src), ld_sc1(src + 1), ld_sc1(src + 2), ld_sc1(src + 3)} : *(const f32x4*)src;
+        if constexpr (kP != 0)
+          a += f32x4{ld_h<kP>(src), ld_h<kP>(src + 1), ld_h<kP>(src + 2), ld_h<kP>(src + 3)};
+        else
+          a += *(const f32x4*)src;
       }
     }
     *(f32x4*)(red + (q * 64 + p) * 4) = a;
@@ -946,7 +985,10 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const float* q = src + (size_t)(g0 + u) * stride;
-            v[u] = g0 + u < nfw_g ? (kP ? ld_sc1(q) : *q) : 0.f;
+            if constexpr (kP != 0)
+              v[u] = g0 + u < nfw_g ? ld_h<kP>(q) : 0.f;
+            else
+              v[u] = g0 + u < nfw_g ? *q : 0.f;
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) s += v[u];
@@ -983,19 +1025,17 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     sdot[w * kNDX + kND] = ls;
   }
   for (int i = 0; i < H; ++i) {  // wave-uniform loop over stored pairs
-    const bool valid = m > 0 && (m == H || (((i - (head - m + 1)) % H + H) % H) < m);
+    const bool valid = pair_valid(i, m, head, H);
     double si = 0.0, yi = 0.0;
     if (valid) {
-      const float* Si = dv.S + (size_t)i * PI;
-      const float* Yi = dv.Y + (size_t)i * PI;
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
-        si += (double)Si[idx[e]] * g[e];
-        yi += (double)Yi[idx[e]] * g[e];
+        si += (double)s_at(i, e) * g[e];
+        yi += (double)y_at(i, e) * g[e];
       }
-      if (wg0 && tid < 16) {
-        si += (double)Si[IB + tid] * gb;
-        yi += (double)Yi[IB + tid] * gb;
+      if (ib0) {
+        si += (double)sb_at(i) * gb;
+        yi += (double)yb_at(i) * gb;
       }
       si = wave_sum(si);
       yi = wave_sum(yi);
@@ -1025,7 +1065,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     const unsigned long long u = d2u(v);
     const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
     if (ns > 1)
-      xstore(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
+      st_h64<kP == 2 ? 2 : 1>(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
     else
       gat32[tid] = half;
   }
@@ -1045,7 +1085,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
           const int i = i0 + st + 192 * j;
           if (i < total) {
             const int b = i / (2 * nv), r = i - b * (2 * nv);
-            x[j] = xload(xch + (size_t)b * (2 * kNDX) + r);
+            x[j] = ld_h64<kP == 2 ? 2 : 1>(xch + (size_t)b * (2 * kNDX) + r);
             ok &= (unsigned)(x[j] >> 32) == tag;
           }
         }
@@ -1088,7 +1128,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     if (wg0) stamp(dv, slot, 6);
   }
   __syncthreads();
-  if (!kP && wg0) {  // the next launches read the controller from global memory
+  if (kP == 0 && wg0) {  // the next launches read the controller from global memory
     constexpr int CW = sizeof(Ctrl) / 8;
     for (int i = tid; i < CW; i += 256) ((unsigned long long*)gctrl)[i] = ((const unsigned long long*)cl)[i];
   }
@@ -1159,11 +1199,9 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
         if (ib) dbv += cs * (t_acc * db0) + cy * (gb - gcb0);
         continue;
       }
-      const float* Si = dv.S + (size_t)i * PI;
-      const float* Yi = dv.Y + (size_t)i * PI;
 #pragma unroll
-      for (int e = 0; e < NE; ++e) dn[e] += cs * Si[idx[e]] + cy * Yi[idx[e]];
-      if (ib) dbv += cs * Si[IB + tid] + cy * Yi[IB + tid];
+      for (int e = 0; e < NE; ++e) dn[e] += cs * s_at(i, e) + cy * y_at(i, e);
+      if (ib) dbv += cs * sb_at(i) + cy * yb_at(i);
     }
 #pragma unroll
     for (int e = 0; e < NE; ++e)
@@ -1199,8 +1237,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       }
     }
     if (ib) {
-      if constexpr (kP)
-        st_sc1(dv.b_eff + tid, xbv + t_next * dbv);
+      if constexpr (kP != 0)
+        st_h<kP>(dv.b_eff + tid, xbv + t_next * dbv);
       else
         dv.b_eff[tid] = xbv + t_next * dbv;
     }
@@ -1208,12 +1246,12 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     if (tid < 128) {
       const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
       uint16_t* dst = tid < 64 ? dv.whi : dv.wlo;
-      if constexpr (kP) {  // (wave-uniform buffer: wave 0 the hi, wave 1 the lo fragments)
+      if constexpr (kP != 0) {  // (wave-uniform buffer: wave 0 the hi, wave 1 the lo fragments)
         const u16x8 v = *(const u16x8*)(frl + tid * 8);
         if (tid < 64)
-          st_sc1_b128(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), v);
+          st_h_b128<kP>(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), v);
         else
-          st_sc1_b128(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), v);
+          st_h_b128<kP>(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), v);
       } else
         *(u16x8*)(dst + go) = *(const u16x8*)(frl + tid * 8);
     }
@@ -1760,24 +1798,24 @@ void launch_reduce_g(const SolverCfg& cfg, const SolveParams* prm, const Ctrl* c
 // The launch chain above (stats_prep, 2 launches per slot, tail) pays a kernel
 // boundary (~1.5-2 us) per phase, and every launch re-reads its operands from
 // memory: each kernel start meets cold caches, so the per-slot chain is bounded
-// by memory round trips, not by work (profiles/r02_v3).  Here G = max(window
-// tiles, FP/32) co-resident workgroups keep their 32-row window tile (and its
-// labels) resident in LDS for the whole solve, and run
-//   S  stage the tile (new stream rows straight from the dataset: the fused
-//      ingest), per-tile column sums                     -> spart[wg]
-//   P  slice owners: window statistics of their 32 features, x0, the first
-//      trial point's fragments, the controller (every workgroup its own copy)
-//   per slot:  row role   forward + softmax + R^T X of the resident tile -> gpart[wg]
+// by memory round trips, not by work (profiles/r02_v3).  The persistent solve is
+// TWO launches: stats_prep_kernel (the fused ingest, window statistics, x0, the
+// first trial point, the controller -- as in the chain), then one launch in
+// which G = max(window tiles, FP/32) co-resident workgroups keep their 32-row
+// window tile (and its labels) resident in LDS for the whole solve and run
+//   per slot:  row role   forward + softmax + R^T X of the resident tile -> gpf[wg]
 //              slice role  G = sum of the partials (fixed order), the dots
 //                          all-gather, controller step, update, next fragments
 //   F  slice owners finalise their features (+ the fused server update)
-// with a grid-wide arrival counter between the phases.  Every hand-off between
-// workgroups is the R1 form of the CDNA4 playbook: sc1 (write-through) stores,
-// each storing wave drained before the arrival, sc1 loads on the consumer side
-// -- no release / acquire fences.  The counters are monotone within a run; the
-// two generations alternate between runs and the finalisation re-arms the next
-// one.  Spins are bounded (a timeout sets the sticky error word).  Workgroups
-// >= G evaluate test tiles (a riding evaluation pass) and never wait.
+// with a grid-wide arrival between the phases.  When G <= 32 (every window of
+// <= 1024 rows that starts on a 32-row boundary) all solve workgroups run on
+// ONE XCD and every hand-off goes through its L2 (S = 2 below: plain stores, nt
+// loads, a flag-line barrier; 0.64 us per hand-off, tools/xcd_probe.hip);
+// otherwise they spread over the XCDs with the R1 form of the CDNA4 playbook
+// (S = 1: sc1 write-through stores, each storing wave drained before the
+// arrival on a monotone counter, sc1 loads; 1.7-2.7 us per hand-off).  Spins
+// are bounded (a timeout sets the sticky error word).  The riding evaluation's
+// workgroups (one test tile each) never wait.
 __device__ __forceinline__ void p_barrier(unsigned long long* ctr, unsigned long long target, unsigned long long* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
@@ -1795,198 +1833,64 @@ __device__ __forceinline__ void p_barrier(unsigned long long* ctr, unsigned long
   __syncthreads();
 }
 
+// The one-XCD form (S = 2): no read-modify-write (device memory's atomics run
+// past the L2, 2 us at 32 workgroups): workgroup wg stores the arrival word
+// (run << 8 | n) into its own 256-B flag line, and thread i of every workgroup
+// polls workgroup i's line with nt loads (the L2 of the shared XCD), so all
+// arrivals are observed in one round trip.  The words only grow over the runs
+// (the run counter advances per solve): nothing is reset.
+__device__ __forceinline__ void x_barrier(unsigned long long* flags, int wg, int G, unsigned long long word,
+                                          unsigned long long* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores reached the L2
+  __syncthreads();
+  if (threadIdx.x == 0) st_h64<2>(flags + (size_t)wg * 32, word);
+  if ((int)threadIdx.x < G) {
+    int spins = 0;
+    while (ld_h64<2>(flags + (size_t)threadIdx.x * 32) < word) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 22)) {  // never expected: record and fall through rather than hang
+        xstore(err, 5ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 PSX_HD constexpr size_t persist_fwd_bytes(int FP) { return (eval_lds_bytes(FP) + 15) / 16 * 16; }
 size_t persist_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (bwd_lds_bytes() + 15) / 16 * 16; }
 int persist_grid(int FP, int ntiles) { return ntiles > FP / 32 ? ntiles : FP / 32; }
 
-// Phase S (row role): stage ring tile `tile` of the window into the LDS image
-// (rows that arrived since the last solve come straight from the dataset and
-// are also written into the ring X / XT / y), then the tile's column sums and
-// sums of squares over its window rows -> spart[tile][2][FP] (sc1).
-template <int FP>
-__device__ __forceinline__ void persist_stage(const SolverCfg& cfg, const SolveDev& dv, char* lds, char* scratch,
-                                              const WinTiles& wt, int tile, int B, const RingIngest& ing) {
-  constexpr int CPR = FP / 8;            // 16-B chunks per row
-  constexpr int PER_T = 32 * CPR / 256;  // chunks per thread
-  constexpr int L = 256 / CPR;           // row groups of the column sums
-  static_assert(CPR * L == 256, "FP in {128..1024}");
-  const int tid = threadIdx.x;
-  const int64_t cap = cfg.cap;
-  const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-  int* ylds = (int*)(lds + 32 * FP * 2 + 8192 + 2048);
-  auto new_row = [&](int64_t slot) -> int {  // index of `slot` among the new rows, -1 if old
-    if (ing.n <= 0) return -1;
-    int64_t i = slot - ing.dst;
-    if (i < 0) i += cap;
-    return i < ing.n ? (int)i : -1;
-  };
-  int yv = 0, yi = -1;
-  if (tid < 32) {
-    yi = new_row(row0 + tid);
-    yv = yi >= 0 ? ing.ysrc[ing.first + (int64_t)yi * ing.step] : dv.y[row0 + tid];
-  }
-  u16x8 v[PER_T];
-  int ni[PER_T];
-#pragma unroll
-  for (int j = 0; j < PER_T; ++j) {  // every load of the tile in flight together
-    const int q = tid + 256 * j, row = q / CPR, cg = q - row * CPR;
-    ni[j] = new_row(row0 + row);
-    const uint16_t* src = ni[j] >= 0 ? ing.src + (ing.first + (int64_t)ni[j] * ing.step) * FP
-                                     : dv.X + (row0 + row) * FP;
-    v[j] = *(const u16x8*)(src + cg * 8);
-  }
-#pragma unroll
-  for (int j = 0; j < PER_T; ++j) {
-    const int q = tid + 256 * j, row = q / CPR, cg = q - row * CPR;
-    *(u16x8*)(lds + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
-    if (ni[j] >= 0) {  // a new row: into the ring for the later solves (row-major + feature-major)
-      const int64_t slot = row0 + row;
-      *(u16x8*)(const_cast<uint16_t*>(dv.X) + slot * FP + cg * 8) = v[j];
-      if (dv.XT) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) const_cast<uint16_t*>(dv.XT)[(int64_t)(cg * 8 + e) * cap + slot] = v[j][e];
-      }
-    }
-  }
-  if (tid < 32) {
-    ylds[tid] = yv;
-    if (yi >= 0) const_cast<int32_t*>(dv.y)[row0 + tid] = yv;
-  }
-  __syncthreads();
-  // column sums of the tile's window rows: thread = (8-feature chunk, row group)
-  const int ch = tid % CPR, rl = tid / CPR;
-  float fs[8], fq[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) fs[e] = fq[e] = 0.f;
-  for (int r = rl; r < 32; r += L) {
-    const int o = tile * 32 + r - wt.s0;
-    if (o < 0 || o >= B) continue;
-    const u16x8 x = *(const u16x8*)(lds + (ch >> 4) * 8192 + lds_off(r, ch & 15));
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float xf = bf2f(x[e]);
-      fs[e] += xf;
-      fq[e] += xf * xf;
-    }
-  }
-  float* red = (float*)scratch;  // [L][CPR][16]
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    red[(rl * CPR + ch) * 16 + e] = fs[e];
-    red[(rl * CPR + ch) * 16 + 8 + e] = fq[e];
-  }
-  __syncthreads();
-  if (tid < CPR * 2) {  // thread = (chunk, sums | squares): 8 features, row groups in order
-    const int c = tid >> 1, kind = tid & 1;
-    double a[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      a[e] = 0.0;
-      for (int g = 0; g < L; ++g) a[e] += (double)red[(g * CPR + c) * 16 + kind * 8 + e];
-    }
-    const auto rs = rsrc_of(dv.spart, (unsigned)((size_t)(tile + 1) * 2 * FP * 8));
-    const unsigned off = (unsigned)((((size_t)tile * 2 + kind) * FP + c * 8) * 8);
-#pragma unroll
-    for (int e = 0; e < 8; e += 2)
-      st_sc1_b128(rs, off + e * 8, __builtin_bit_cast(u16x8, double2v{a[e], a[e + 1]}));
+// S = 2 (one XCD): the G <= 32 solve workgroups are blockIdx 0, 8, .., 8 (G - 1)
+// -- all on XCD 0, whose L2 carries every in-launch hand-off (x_barrier, the
+// dots all-gather, partials, fragments) -- and the riding evaluation
+// workgroups fill the other blockIdx, i.e. XCDs 1..7: they never compete with
+// the solve for XCD 0's CUs.  S = 1: solve workgroups 0..G-1 spread over the
+// XCDs (sc1 hand-offs, atomic arrival counter), riding workgroups after them.
+template <int S>
+__device__ __forceinline__ int persist_role(int b, int G) {  // >= 0: solve workgroup; < 0: -(ride index) - 1
+  if constexpr (S == 2) {
+    if ((b & 7) == 0 && (b >> 3) < G) return b >> 3;
+    const int before = (b >> 3) + 1 < G ? (b >> 3) + 1 : G;  // solve workgroups with blockIdx <= b
+    return -(b - before) - 1;
+  } else {
+    return b < G ? b : -(b - G) - 1;
   }
 }
-
-// Phase P (slice owner `wg`, features [32 wg, 32 wg + 32)): the window
-// statistics from the tiles' partial sums (fixed order), std / 1/std, the
-// initial point x0 = w_old * std (Spark standardisation), the solver vectors
-// and the first trial point's fragments (sc1; intercepts by wg 0).
-template <int FP, int KP>
-__device__ __forceinline__ void persist_prep(const SolverCfg& cfg, const SolveDev& dv, char* scratch,
-                                             unsigned short* frl, int wg, int ntiles, int B, float wo_pre,
-                                             float b_pre) {
-  static_assert(KP <= 8, "one (class, feature) element per thread");
-  constexpr int FPI = FP > 256 ? FP : 256;
-  const int tid = threadIdx.x, K = cfg.K, F = cfg.F;
-  const int fs = wg * 32;
-  double* part = (double*)scratch;   // [4 lanes][64]
-  double* rs = part + 4 * 64;        // [32] sums, [32] sums of squares
-  float* sdl = (float*)(rs + 64);    // [32]
-  float* ivl = sdl + 32;             // [32]
-  {  // thread = (value: 32 features x {sum, square}, lane of 4 over the tiles)
-    const int val = tid & 63, ln = tid >> 6, fl = val & 31, kind = val >> 5;
-    constexpr int UG = 17;  // tiles per lane with every load in flight (windows of <= 68 tiles per pass)
-    double a = 0.0;
-    for (int g0 = ln; g0 < ntiles; g0 += 4 * UG) {
-      double v[UG];
-#pragma unroll
-      for (int u = 0; u < UG; ++u) {
-        const int g = g0 + 4 * u;
-        v[u] = g < ntiles ? ld_sc1(dv.spart + ((size_t)g * 2 + kind) * FP + fs + fl) : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < UG; ++u) a += v[u];
-    }
-    part[ln * 64 + val] = a;
-  }
-  if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  __syncthreads();
-  if (tid < 64) rs[tid] = ((part[tid] + part[64 + tid]) + part[128 + tid]) + part[192 + tid];
-  __syncthreads();
-  if (tid < 32) {
-    const int f = fs + tid;
-    const double a = rs[tid], b = rs[32 + tid], n = (double)B;
-    double sd = 0.0;
-    if (f < F && n > 1.0) {
-      const double mean = a / n;
-      const double var = (b - n * mean * mean) / (n - 1.0);
-      sd = var > 0.0 ? sqrt(var) : 0.0;
-    }
-    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
-    sdl[tid] = sdf;
-    ivl[tid] = inv;
-    dv.std_[f] = sdf;
-    dv.inv_std[f] = inv;
-  }
-  __syncthreads();
-  if (tid < 32 * KP) {
-    const int e = tid;
-    const int c = e >> 5, fl = e & 31, f = fs + fl;
-    const int pi = c * FPI + f;
-    const float wo = wo_pre;
-    const float xv = wo * sdl[fl];
-    dv.x[pi] = xv;
-    dv.d[pi] = 0.f;
-    dv.g_c[pi] = 0.f;
-    const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo;
-    dv.wfix[pi] = fix;
-    unsigned short h, l;
-    split_bf16(xv * ivl[fl] + fix, h, l);
-    const int o = (fl >> 3) * 128 + c * 8 + (fl & 7);
-    frl[o] = h;
-    frl[512 + o] = l;
-  }
-  if (wg == 0 && tid < 16) {
-    const int pi = KP * FPI + tid;
-    const float b = b_pre;
-    dv.x[pi] = b;
-    dv.d[pi] = 0.f;
-    dv.g_c[pi] = 0.f;
-    st_sc1(dv.b_eff + tid, b);
-  }
-  __syncthreads();
-  if (tid < 128) {  // wave 0: hi, wave 1: lo fragments of this slice
-    const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
-    const u16x8 v = *(const u16x8*)(frl + tid * 8);
-    if (tid < 64)
-      st_sc1_b128(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), v);
-    else
-      st_sc1_b128(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), v);
-  }
+int persist_launch_grid(int G, int nride, bool one_xcd) {
+  if (!one_xcd) return G + nride;
+  const int a = 8 * (G - 1) + 1, b = G + nride;
+  return a > b ? a : b;
 }
 
-template <int FP, int KP>
+template <int FP, int KP, int S>
 __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, SolveDev dv, Ctrl* gctrl, SolveParams win,
                                                             RingIngest ing, int G, EvalRide ride, int nride) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int wg = blockIdx.x, tid = threadIdx.x;
-  if (wg >= G) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
-    const int t = wg - G;
+  const int role = persist_role<S>((int)blockIdx.x, G), tid = threadIdx.x;
+  if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
+    const int t = -role - 1;
+    if (t >= nride) return;
     eval_body<FP>(lds, ride, t, 1, t + 1);
     // arrival once this workgroup's loads (the models' fragments) are complete: the
     // finalisation rewrites those fragments only after every riding workgroup arrived
@@ -1997,6 +1901,7 @@ __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, Solve
                                    __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  const int wg = role;
   constexpr int NS = FP / 32;  // feature slices
   char* lf = lds;                          // row role: the resident tile + forward scratch
   char* lb = lds + persist_fwd_bytes(FP);  // slice role: bwd_body's region
@@ -2010,27 +1915,27 @@ __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, Solve
   unsigned long long* bar = xch + kXchGen + (run & 1u);
   unsigned long long* err = xch + kXchErr;
   unsigned long long nb = 0;
+  auto barrier = [&]() {
+    ++nb;
+    if constexpr (S == 2)
+      x_barrier(xch + kXchFlags, wg, G, ((unsigned long long)run << 8) | nb, err);
+    else
+      p_barrier(bar, (unsigned long long)G * nb, err);
+  };
   const bool row = wg < ntiles, owner = wg < NS;
-  if (wg == 0 && tid == 0) stamp(dv, 30, 0);
-  // the pulled weights of this slice, fetched now: their latency overlaps phase S
-  float wo_pre = 0.f, b_pre = 0.f;
-  if (owner && tid < 32 * KP) {
-    const int c = tid >> 5, f = wg * 32 + (tid & 31);
-    if (c < cfg.K && f < cfg.F) wo_pre = dv.w_old[c * FP + f];
-  }
-  if (wg == 0 && tid < 16 && tid < cfg.K) b_pre = dv.w_old[cfg.K * FP + tid];
-  // ---- S ----
-  if (row) persist_stage<FP>(cfg, dv, lf, lb, wt, wg, B, ing);
   if (wg == 0 && tid == 0) stamp(dv, 30, 3);
-  p_barrier(bar, (unsigned long long)G * ++nb, err);
-  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
-  // ---- P ----
-  if (owner) {
-    persist_prep<FP, KP>(cfg, dv, lf + 32 * FP * 2, frl, wg, ntiles, B, wo_pre, b_pre);
-    if (tid == 0) ctrl_init(*cl);
+  // ---- the window statistics, x0, the first trial point's fragments and the
+  // controller come from stats_prep_kernel, the launch before (with the fused
+  // ingest of the new rows): here the tile is staged once and stays resident ----
+  if (row) {
+    const int64_t row0 = (int64_t)wt.ring_tile(wg) * 32;
+    const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads
+    stage_tile<FP>(lf, dv.X, row0, 32, cfg.cap, false);
+    if (tid < 32) ((int*)(lf + 32 * FP * 2 + 8192 + 2048))[tid] = yv;  // fwd_body's label slots
   }
-  if (wg == 0 && tid == 0) stamp(dv, 30, 1);
-  p_barrier(bar, (unsigned long long)G * ++nb, err);
+  if (owner) copy_words_to_lds<sizeof(Ctrl) / 8, 256>((unsigned long long*)cl, (const unsigned long long*)gctrl);
+  __syncthreads();
+  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
   // ---- slots ----
   int phase = kPhInit;
   for (int slot = 0; slot < cfg.nslots; ++slot) {
@@ -2040,14 +1945,14 @@ __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, Solve
       f32x4 acc[NT];
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
-      fwd_body<FP, true, false, true>(cfg, win, slot, dv, lf, wg, G, acc);
-      store_gpf<FP, true>(dv, wg, G, acc);  // this tile's R^T X partials (sc1)
+      fwd_body<FP, true, false, S>(cfg, win, slot, dv, lf, wg, G, acc);
+      store_gpf<FP, S == 1>(dv, wg, G, acc);  // this tile's R^T X partials (sc1 | plain: in-XCD)
     }
-    p_barrier(bar, (unsigned long long)G * ++nb, err);
-    if (owner) bwd_body<FP, KP, true>(cfg, win, gctrl, slot, dv, G, lb, wg, NS);
-    if (wg == 0 && tid == 0) xstore(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
-    p_barrier(bar, (unsigned long long)G * ++nb, err);
-    phase = owner ? cl->phase : (int)(unsigned)xload(xch + kXchPhase);
+    barrier();
+    if (owner) bwd_body<FP, KP, S>(cfg, win, gctrl, slot, dv, G, lb, wg, NS);
+    if (wg == 0 && tid == 0) st_h64<S>(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
+    barrier();
+    phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
   }
   // ---- F: slice owners finalise their features ----
   if (owner) {
@@ -2084,16 +1989,30 @@ __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, Solve
   }
 }
 
+template <int FP, int S>
+static void launch_persist_fps(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
+                               const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+  const size_t lb = persist_lds_bytes(FP);
+  const int grid = persist_launch_grid(G, nride, S == 2);
+  switch (dv.KP) {
+    case 2: solve_persist_kernel<FP, 2, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+    case 4: solve_persist_kernel<FP, 4, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+    default: solve_persist_kernel<FP, 8, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+  }
+}
+
 template <int FP>
 static void launch_persist_fp(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
                               const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
-  const size_t lb = persist_lds_bytes(FP);
-  const int grid = G + nride;
-  switch (dv.KP) {
-    case 2: solve_persist_kernel<FP, 2><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
-    case 4: solve_persist_kernel<FP, 4><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
-    default: solve_persist_kernel<FP, 8><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
-  }
+  // one XCD when the solve workgroups fit its CUs (PSX_PERSIST_XCD=0: always spread)
+  static const bool xcd_ok = [] {
+    const char* e = std::getenv("PSX_PERSIST_XCD");
+    return !(e && e[0] == '0');
+  }();
+  if (xcd_ok && G <= kMaxXcdWg)
+    launch_persist_fps<FP, 2>(cfg, dv, ctrl, win, ing, G, ride, nride, s);
+  else
+    launch_persist_fps<FP, 1>(cfg, dv, ctrl, win, ing, G, ride, nride, s);
 }
 
 bool persist_supported(int FP, int KP) { return FP >= 128 && FP <= 1024 && KP <= 8; }
@@ -2112,9 +2031,12 @@ void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const 
 template <int FP>
 static void set_persist_attr() {
   const int b = (int)persist_lds_bytes(FP);
-  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
-  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
+  (void)hipFuncSetAttribute((const void*)solve_persist_kernel<FP, 8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, b);
 }
 
 template <int FP>

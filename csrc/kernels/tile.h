@@ -153,8 +153,9 @@ __device__ __forceinline__ void load_wfrag(WFrag<FP>& wf, const uint16_t* __rest
   }
 }
 
-// The same with sc1 loads (fragments handed off inside a persistent launch).
-template <int FP>
+// The same with hand-off loads (fragments handed off inside a persistent launch;
+// S: the hand-off scope of common.h's ld_h_b128).
+template <int FP, int S = 1>
 __device__ __forceinline__ void load_wfrag_sc1(WFrag<FP>& wf, const uint16_t* wf_hi, const uint16_t* wf_lo, int K = 16) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool live = (lane & 15) < K;
@@ -166,8 +167,8 @@ __device__ __forceinline__ void load_wfrag_sc1(WFrag<FP>& wf, const uint16_t* wf
     wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (live) {
-      wf.h[kk] = ld_sc1_b128(rh, fo);
-      wf.l[kk] = ld_sc1_b128(rl, fo);
+      wf.h[kk] = ld_h_b128<S>(rh, fo);
+      wf.l[kk] = ld_h_b128<S>(rl, fo);
     }
   }
 }

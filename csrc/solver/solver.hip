@@ -74,7 +74,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
                          : 0;
   const size_t G = rows_mode_ ? (size_t)nwg_eval_ : (Gp > Gc ? Gp : Gc);
   const size_t o_gpart = (rows_mode_ || persist_ || gpf_) ? take(G * dv_.KP * FP * 4) : 0;
-  const size_t o_spart = (rows_mode_ || persist_) ? take(G * 2 * FP * 8) : 0;
+  const size_t o_spart = rows_mode_ ? take(G * 2 * FP * 8) : 0;
   const size_t o_gred = rows_mode_ ? take((size_t)dv_.KP * FPI * 4) : 0;
   const int npart = nwg_eval_ > tail_grid(cfg.Fp, nwg_eval_) ? nwg_eval_ : tail_grid(cfg.Fp, nwg_eval_);
   const size_t o_part = take((size_t)npart * 32 * 4);
@@ -124,7 +124,6 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   if (persist_) {  // the persistent launch reads the partials; the launch chain keeps XT / R
     dvp_ = dv_;
     dvp_.gpf = reinterpret_cast<float*>(b + o_gpart);
-    dvp_.spart = reinterpret_cast<double*>(b + o_spart);
     dvp_.gred = nullptr;
   }
 
@@ -254,14 +253,11 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
       throw std::invalid_argument("fused ingest: the new rows must end the window");
   }
   if (persist_) {
-    RingIngest pin = ing;
-    if (pin.n > B) {  // new rows beyond the window: copied by their own launch (ring X, XT, y)
-      launch_ring_ingest(pin.src, pin.ysrc, pin.first, pin.step, pin.n, const_cast<uint16_t*>(dv_.X),
-                         const_cast<uint16_t*>(dv_.XT), const_cast<int32_t*>(dv_.y), pin.dst, cfg_.cap, cfg_.Fp, stream);
-      pin = RingIngest{};
-    }
+    // stats_prep (fused ingest, window statistics, x0, the first trial point, the
+    // controller), then ONE persistent launch for every slot and the finalisation
     const int nt = ((start & 31) + B + 31) >> 5;
     const int G = persist_grid(cfg_.Fp, nt);
+    launch_stats_prep(cfg_, prm_, dv_, ctrl_, B, start, ing, stream);
     SolveDev d = dvp_;
     d.ap_w = dv_.ap_w;
     d.ap_hi = dv_.ap_hi;
@@ -269,7 +265,7 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
     d.ap_b = dv_.ap_b;
     d.ap_lr = dv_.ap_lr;
     d.ap_coff = dv_.ap_coff;
-    launch_persist(cfg_, d, ctrl_, SolveParams{B, start, 0, 0}, pin, G, ride ? *ride : EvalRide{},
+    launch_persist(cfg_, d, ctrl_, SolveParams{B, start, 0, 0}, RingIngest{}, G, ride ? *ride : EvalRide{},
                    ride ? ride->ntiles() : 0, stream);
     hip_check(hipGetLastError(), "persistent solve launch");
     dv_.ap_w = nullptr;

@@ -54,10 +54,13 @@ class SolverOptions:
     use_graph: bool | None = None
     max_eval_wg: int = 512
     fused_ingest: bool = True  # GPU: new stream rows are copied into the ring by the solve's first kernel
-    # the whole small-window solve as ONE persistent launch (its workgroups must be
-    # co-resident: only for a solver that has the GPU to itself; the engines turn it
-    # off otherwise).  Host enqueue 3.8 us instead of ~23 us per solve, device time
-    # 68-72 us instead of ~63 us on MI355X (profiles/r02_v3): off by default.
+    # the small-window solve as stats_prep + ONE persistent launch (its workgroups must
+    # be co-resident: only for a solver that has the GPU to itself).  With <= 32 solve
+    # workgroups they all run on one XCD and hand off through its L2: 57.6 us per
+    # solve against 62.5 us for the 8-launch chain (profiles/r02_v5).  None = the
+    # engine decides: LocalEngine turns it on for a lone GPU worker; DistEngine and
+    # several in-process workers keep the chain (kernels of other streams -- RCCL,
+    # other workers -- could hold the XCD's CUs the persistent workgroups wait for).
     persist: bool | None = None
 
     @property

@@ -110,6 +110,11 @@ class LocalEngine:
             # the persistent solve needs its workgroups co-resident: one worker only
             # (several in-process workers run their solves side by side)
             cfg.solver = dataclasses.replace(cfg.solver, persist=False)
+        if cfg.solver.persist is None and cfg.num_workers == 1 and is_gpu(self.device):
+            # a lone worker has the GPU to itself: the persistent solve (one XCD) is the
+            # fastest small-window solve on MI355X (profiles/r02_v5); unsupported shapes
+            # (rows mode, fp32 rows, > 1024 features) keep the chain inside the solver
+            cfg.solver = dataclasses.replace(cfg.solver, persist=True)
         if cfg.solver.use_graph is None and cfg.num_workers > 2:
             # many in-process workers share this process's launch thread: one graph
             # replay per solve beats 8 eager launches there (bench.py --workers 8:

@@ -55,8 +55,8 @@ def stamps(B=1024, opts=None):
     base = st[0]
     sv = st[30 * 16: 30 * 16 + 5]
     extra = ""
-    if sv[3] >= base - 10 ** 6 and sv[3] > 0 and sv[4] > 0:  # persistent solve: staged / first barrier
-        extra = f" (persistent: staged={(sv[3] - base) / 100.0:.2f} barrier={(sv[4] - base) / 100.0:.2f})"
+    if sv[3] >= base - 10 ** 6 and sv[3] > 0 and sv[4] > 0:  # persistent solve: its start / tile staged
+        extra = f" (persistent: start={(sv[3] - base) / 100.0:.2f} staged={(sv[4] - base) / 100.0:.2f})"
     print(f"stats_prep start={(sv[0] - base) / 100.0:.2f} end={(sv[1] - base) / 100.0:.2f}  "
           f"finalize start={(sv[2] - base) / 100.0:.2f}{extra}")
     ph = ["start", "mfma", "publish", "gathered"]

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r02v5
+OUT=gpurun_out/${TAG:-r02v5}
 mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest_gpu.log
@@ -17,7 +17,7 @@ rc=$?; echo "bench short rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python - <<'PY'
 import json
 for f in ("bench.json", "bench_short.json"):
-    d = json.loads(open("gpurun_out/r02v5/" + f).read().strip().splitlines()[-1])
+    d = json.loads(open("gpurun_out/" + __import__("os").environ.get("TAG", "r02v5") + "/" + f).read().strip().splitlines()[-1])
     print(f, d["value"], d["ms_per_step"], d["best_test_f1"], d.get("accuracy_run", {}).get("best_test_f1"))
 PY
 if [ -n "${PROF:-}" ]; then

@@ -85,7 +85,10 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--persist", action="store_true",
-                    help="dense: each local solve as ONE persistent launch (tile-resident, in-launch hand-offs)")
+                    help="dense: stats_prep + ONE persistent launch per local solve (the default for a lone GPU "
+                         "worker in one process; forces it elsewhere)")
+    ap.add_argument("--chain", action="store_true",
+                    help="dense: the 8-launch chain per local solve instead of the persistent launch")
     ap.add_argument("--async-scheduler", default="auto", choices=["auto", "events", "threads"],
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--rccl-trace", action="store_true",
@@ -134,7 +137,7 @@ def build_cfg(a, n_workers):
         dtype=a.dtype,
         sigmoid=a.model == "sharded100m",
         solver=SolverOptions(iters=a.iters, use_graph=False if a.no_graph else (True if a.graph else None),
-                             zero_const=not wide, persist=True if a.persist else None),
+                             zero_const=not wide, persist=True if a.persist else (False if a.chain else None)),
         bsp_schedule=a.schedule,
         server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,

@@ -297,6 +297,28 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
   prep_epilogue(cfg, dv, ctrl, B, fs, rs, rq, sdl, ivl, wo_pre, b_pre);
 }
 
+// Launch geometry of a grid whose G <= 32 cooperating workgroups hand off
+// through one L2 (S = 2): they are blockIdx 0, 8, .., 8 (G - 1) -- all on XCD 0
+// (blockIdx % 8 == XCC_ID on MI355X) -- and the riding evaluation workgroups
+// fill the other blockIdx, i.e. XCDs 1..7: they never compete with the
+// cooperating ones for XCD 0's CUs.  S = 1: workgroups 0..G-1 spread over the
+// XCDs (sc1 hand-offs), riding workgroups after them.
+template <int S>
+__device__ __forceinline__ int xcd_role(int b, int G) {  // >= 0: solve workgroup; < 0: -(ride index) - 1
+  if constexpr (S == 2) {
+    if ((b & 7) == 0 && (b >> 3) < G) return b >> 3;
+    const int before = (b >> 3) + 1 < G ? (b >> 3) + 1 : G;  // solve workgroups with blockIdx <= b
+    return -(b - before) - 1;
+  } else {
+    return b < G ? b : -(b - G) - 1;
+  }
+}
+int xcd_grid(int G, int nride, bool one_xcd) {
+  if (!one_xcd) return G + nride;
+  const int a = 8 * (G - 1) + 1, b = G + nride;
+  return a > b ? a : b;
+}
+
 // ---------------------------------------------------------------------------
 // fwd_kernel: loss and residuals at the trial point (row-parallel).
 // Body shared by fwd_kernel and tail_kernel: workgroup `wg` of `G` takes the
@@ -760,7 +782,7 @@ size_t bwd_lds_bytes() {
 // across slots (no copy-in / write-back), the partials written by other
 // workgroups of the launch are read with sc1 loads and the next trial point is
 // published with sc1 stores (common.h).
-template <int FP, int KP, int kP = 0>
+template <int FP, int KP, int kP = 0, int kXs = (kP == 2 ? 2 : 1)>
 __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
                                          const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
                                          const bool check_done = false, const int fin_slot = kNoFinSlot) {
@@ -1065,7 +1087,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     const unsigned long long u = d2u(v);
     const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
     if (ns > 1)
-      st_h64<kP == 2 ? 2 : 1>(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
+      st_h64<kXs>(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
     else
       gat32[tid] = half;
   }
@@ -1085,7 +1107,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
           const int i = i0 + st + 192 * j;
           if (i < total) {
             const int b = i / (2 * nv), r = i - b * (2 * nv);
-            x[j] = ld_h64<kP == 2 ? 2 : 1>(xch + (size_t)b * (2 * kNDX) + r);
+            x[j] = ld_h64<kXs>(xch + (size_t)b * (2 * kNDX) + r);
             ok &= (unsigned)(x[j] >> 32) == tag;
           }
         }
@@ -1259,17 +1281,25 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (wg0 && tid == 0) stamp(dv, slot, 8);
 }
 
+// The ns = FP/32 slice workgroups all-gather their dots: for FP <= 1024 (ns <=
+// 32) they run on one XCD and the all-gather goes through its L2 (xcd_role).
+template <int FP>
+constexpr int bwd_scope() { return FP <= 1024 ? 2 : 1; }
+
 template <int FP, int KP>
 __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const SolveParams* prm, Ctrl* gctrl, int slot,
                                                          SolveDev dv, int fwd_grid, SolveParams win, int ns,
-                                                         EvalRide ride, int ride_t0, int fin_slot) {
+                                                         EvalRide ride, int ride_t0, int nride, int fin_slot) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if ((int)blockIdx.x >= ns) {  // an evaluation workgroup riding in this launch: one test tile
-    const int t = ride_t0 + (int)blockIdx.x - ns;
+  constexpr int S = bwd_scope<FP>();
+  const int role = xcd_role<S>((int)blockIdx.x, ns);
+  if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile
+    if (-role - 1 >= nride) return;  // (a gap of the one-XCD geometry)
+    const int t = ride_t0 - role - 1;
     eval_body<FP>(lds, ride, t, 1, t + 1);
     return;
   }
-  bwd_body<FP, KP>(cfg, window_of(win, prm), gctrl, slot, dv, fwd_grid, lds, blockIdx.x, ns, true, fin_slot);
+  bwd_body<FP, KP, 0, S>(cfg, window_of(win, prm), gctrl, slot, dv, fwd_grid, lds, role, ns, true, fin_slot);
 }
 
 // ---------------------------------------------------------------------------
@@ -1417,14 +1447,20 @@ template <int FP>
 static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
                           int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
                           int ride_t0 = 0, int nride = 0, int fin_slot = kNoFinSlot) {
-  const int ns = bwd_grid(FP), ng = ns + nride;
+  const int ns = bwd_grid(FP), ng = xcd_grid(ns, nride, bwd_scope<FP>() == 2);
   const size_t bl = nride > 0 ? bwd_ride_lds_bytes(FP) : bwd_lds_bytes();
   switch (dv.KP) {
-    case 2: bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
-    case 4: bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
-    case 8: bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot); break;
+    case 2:
+      bwd_update_kernel<FP, 2><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, nride, fin_slot);
+      break;
+    case 4:
+      bwd_update_kernel<FP, 4><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, nride, fin_slot);
+      break;
+    case 8:
+      bwd_update_kernel<FP, 8><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, nride, fin_slot);
+      break;
     default:
-      bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, fin_slot);
+      bwd_update_kernel<FP, 16><<<ng, 256, bl, s>>>(cfg, prm, ctrl, slot, dv, nwg, win, ns, ride, ride_t0, nride, fin_slot);
       break;
   }
 }
@@ -1861,33 +1897,11 @@ PSX_HD constexpr size_t persist_fwd_bytes(int FP) { return (eval_lds_bytes(FP) +
 size_t persist_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (bwd_lds_bytes() + 15) / 16 * 16; }
 int persist_grid(int FP, int ntiles) { return ntiles > FP / 32 ? ntiles : FP / 32; }
 
-// S = 2 (one XCD): the G <= 32 solve workgroups are blockIdx 0, 8, .., 8 (G - 1)
-// -- all on XCD 0, whose L2 carries every in-launch hand-off (x_barrier, the
-// dots all-gather, partials, fragments) -- and the riding evaluation
-// workgroups fill the other blockIdx, i.e. XCDs 1..7: they never compete with
-// the solve for XCD 0's CUs.  S = 1: solve workgroups 0..G-1 spread over the
-// XCDs (sc1 hand-offs, atomic arrival counter), riding workgroups after them.
-template <int S>
-__device__ __forceinline__ int persist_role(int b, int G) {  // >= 0: solve workgroup; < 0: -(ride index) - 1
-  if constexpr (S == 2) {
-    if ((b & 7) == 0 && (b >> 3) < G) return b >> 3;
-    const int before = (b >> 3) + 1 < G ? (b >> 3) + 1 : G;  // solve workgroups with blockIdx <= b
-    return -(b - before) - 1;
-  } else {
-    return b < G ? b : -(b - G) - 1;
-  }
-}
-int persist_launch_grid(int G, int nride, bool one_xcd) {
-  if (!one_xcd) return G + nride;
-  const int a = 8 * (G - 1) + 1, b = G + nride;
-  return a > b ? a : b;
-}
-
 template <int FP, int KP, int S>
 __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, SolveDev dv, Ctrl* gctrl, SolveParams win,
                                                             RingIngest ing, int G, EvalRide ride, int nride) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int role = persist_role<S>((int)blockIdx.x, G), tid = threadIdx.x;
+  const int role = xcd_role<S>((int)blockIdx.x, G), tid = threadIdx.x;
   if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
     const int t = -role - 1;
     if (t >= nride) return;
@@ -1993,7 +2007,7 @@ template <int FP, int S>
 static void launch_persist_fps(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
                                const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
   const size_t lb = persist_lds_bytes(FP);
-  const int grid = persist_launch_grid(G, nride, S == 2);
+  const int grid = xcd_grid(G, nride, S == 2);
   switch (dv.KP) {
     case 2: solve_persist_kernel<FP, 2, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
     case 4: solve_persist_kernel<FP, 4, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;

@@ -242,6 +242,16 @@ class DistEngine:
             import dataclasses
 
             cfg.solver = dataclasses.replace(cfg.solver, persist=False)
+        if (cfg.solver.persist is None and not self.async_mode and not self.dedicated and cfg.bsp_schedule == "allreduce"
+                and dist.is_initialized() and dist.get_backend() == "nccl"):
+            # every rank is one worker whose round is solve -> all-reduce -> update on ONE
+            # stream: nothing else runs on the GPU beside the solve, so the persistent
+            # solve (one XCD, profiles/r02_v5) is safe and faster.  The asynchronous and
+            # dedicated-server schedules overlap RCCL kernels of other streams with the
+            # solve and keep the launch chain.
+            import dataclasses
+
+            cfg.solver = dataclasses.replace(cfg.solver, persist=True)
         self.spec, train, test = load_datasets(cfg, train, test)
         self.wide = is_wide(self.spec)
         # wide model: collectives and dense p2p pushes need the dense delta;

@@ -91,7 +91,9 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("gd_lr", &SolverCfg::gd_lr)
       .def_readwrite("tol", &SolverCfg::tol)
       .def_readwrite("xf32", &SolverCfg::xf32)
-      .def_readwrite("persist", &SolverCfg::persist);
+      .def_readwrite("persist", &SolverCfg::persist)
+      .def_readwrite("xcd", &SolverCfg::xcd)
+      .def_readwrite("tail", &SolverCfg::tail);
 
   py::class_<LocalSolver>(m, "LocalSolver")
       .def(py::init([](const SolverCfg& cfg, uintptr_t X, uintptr_t XT, uintptr_t y, uintptr_t w_old,

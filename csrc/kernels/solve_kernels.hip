@@ -304,18 +304,19 @@ __global__ __launch_bounds__(256) void stats_prep_kernel(SolverCfg cfg, SolvePar
 // cooperating ones for XCD 0's CUs.  S = 1: workgroups 0..G-1 spread over the
 // XCDs (sc1 hand-offs), riding workgroups after them.
 template <int S>
-__device__ __forceinline__ int xcd_role(int b, int G) {  // >= 0: solve workgroup; < 0: -(ride index) - 1
-  if constexpr (S == 2) {
-    if ((b & 7) == 0 && (b >> 3) < G) return b >> 3;
-    const int before = (b >> 3) + 1 < G ? (b >> 3) + 1 : G;  // solve workgroups with blockIdx <= b
+__device__ __forceinline__ int xcd_role(int b, int G, int x) {  // >= 0: cooperating workgroup; < 0: -(ride index) - 1
+  if constexpr (S == 2) {  // cooperating workgroup i is blockIdx 8 i + x (XCD x)
+    if ((b & 7) == x && (b >> 3) < G) return b >> 3;
+    int before = b > x ? (b - x + 7) >> 3 : 0;  // cooperating workgroups with blockIdx < b
+    before = before < G ? before : G;
     return -(b - before) - 1;
   } else {
     return b < G ? b : -(b - G) - 1;
   }
 }
-int xcd_grid(int G, int nride, bool one_xcd) {
+int xcd_grid(int G, int nride, bool one_xcd, int x) {
   if (!one_xcd) return G + nride;
-  const int a = 8 * (G - 1) + 1, b = G + nride;
+  const int a = 8 * (G - 1) + x + 1, b = G + nride;
   return a > b ? a : b;
 }
 
@@ -1074,6 +1075,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // stores; every workgroup sweeps all slices' words with sc1 loads until each
   // carries this (run, slot)'s tag, which never repeats (no reset needed) ----
   const int ns = NS;
+  // the slices share one XCD (one L2) unless the solver spreads them (cfg.xcd < 0)
+  const bool xs2 = kXs == 2 && (kP == 2 || cfg.xcd >= 0);
   // only the m stored pairs' dots travel (ring slots (head - m + 1 + j) mod H)
   const int nv = 4 + 2 * m;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (m), Y_i.gt (m)
   const int hbase = ((head - m + 1) % H + H) % H;
@@ -1086,8 +1089,14 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     const double v = sdot[si] + sdot[kNDX + si] + sdot[2 * kNDX + si] + sdot[3 * kNDX + si];
     const unsigned long long u = d2u(v);
     const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
-    if (ns > 1)
-      st_h64<kXs>(xch + (size_t)wg * (2 * kNDX) + tid, ((unsigned long long)tag << 32) | half);
+    if (ns > 1) {
+      unsigned long long* dst = xch + (size_t)wg * (2 * kNDX) + tid;
+      const unsigned long long v = ((unsigned long long)tag << 32) | half;
+      if (xs2)
+        st_h64<2>(dst, v);
+      else
+        st_h64<1>(dst, v);
+    }
     else
       gat32[tid] = half;
   }
@@ -1107,7 +1116,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
           const int i = i0 + st + 192 * j;
           if (i < total) {
             const int b = i / (2 * nv), r = i - b * (2 * nv);
-            x[j] = ld_h64<kXs>(xch + (size_t)b * (2 * kNDX) + r);
+            x[j] = xs2 ? ld_h64<2>(xch + (size_t)b * (2 * kNDX) + r) : ld_h64<1>(xch + (size_t)b * (2 * kNDX) + r);
             ok &= (unsigned)(x[j] >> 32) == tag;
           }
         }
@@ -1292,7 +1301,8 @@ __global__ __launch_bounds__(256) void bwd_update_kernel(SolverCfg cfg, const So
                                                          EvalRide ride, int ride_t0, int nride, int fin_slot) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int S = bwd_scope<FP>();
-  const int role = xcd_role<S>((int)blockIdx.x, ns);
+  const int role = (S == 2 && cfg.xcd >= 0) ? xcd_role<2>((int)blockIdx.x, ns, cfg.xcd & 7)
+                                            : xcd_role<1>((int)blockIdx.x, ns, 0);
   if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile
     if (-role - 1 >= nride) return;  // (a gap of the one-XCD geometry)
     const int t = ride_t0 - role - 1;
@@ -1447,7 +1457,7 @@ template <int FP>
 static void launch_bwd_fp(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, int slot, const SolveDev& dv,
                           int nwg, hipStream_t s, const SolveParams& win, const EvalRide& ride = EvalRide{},
                           int ride_t0 = 0, int nride = 0, int fin_slot = kNoFinSlot) {
-  const int ns = bwd_grid(FP), ng = xcd_grid(ns, nride, bwd_scope<FP>() == 2);
+  const int ns = bwd_grid(FP), ng = xcd_grid(ns, nride, bwd_scope<FP>() == 2 && cfg.xcd >= 0, cfg.xcd & 7);
   const size_t bl = nride > 0 ? bwd_ride_lds_bytes(FP) : bwd_lds_bytes();
   switch (dv.KP) {
     case 2:
@@ -1901,7 +1911,7 @@ template <int FP, int KP, int S>
 __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, SolveDev dv, Ctrl* gctrl, SolveParams win,
                                                             RingIngest ing, int G, EvalRide ride, int nride) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int role = xcd_role<S>((int)blockIdx.x, G), tid = threadIdx.x;
+  const int role = xcd_role<S>((int)blockIdx.x, G, cfg.xcd & 7), tid = threadIdx.x;
   if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
     const int t = -role - 1;
     if (t >= nride) return;
@@ -2007,7 +2017,7 @@ template <int FP, int S>
 static void launch_persist_fps(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
                                const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
   const size_t lb = persist_lds_bytes(FP);
-  const int grid = xcd_grid(G, nride, S == 2);
+  const int grid = xcd_grid(G, nride, S == 2, cfg.xcd & 7);
   switch (dv.KP) {
     case 2: solve_persist_kernel<FP, 2, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
     case 4: solve_persist_kernel<FP, 4, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
@@ -2023,7 +2033,7 @@ static void launch_persist_fp(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ct
     const char* e = std::getenv("PSX_PERSIST_XCD");
     return !(e && e[0] == '0');
   }();
-  if (xcd_ok && G <= kMaxXcdWg)
+  if (xcd_ok && G <= kMaxXcdWg && cfg.xcd >= 0)
     launch_persist_fps<FP, 2>(cfg, dv, ctrl, win, ing, G, ride, nride, s);
   else
     launch_persist_fps<FP, 1>(cfg, dv, ctrl, win, ing, G, ride, nride, s);

@@ -73,6 +73,16 @@ struct SolverCfg {
   // solve_persist_kernel); needs its G workgroups co-resident, so only for a
   // solver that has the device to itself (one worker per process)
   int persist = 0;
+  // XCD (0..7) that hosts the persistent solve's workgroups and the chain's
+  // bwd_update slices (their hand-offs through that XCD's L2); -1: the chain's
+  // slices spread over the XCDs (sc1 hand-offs) -- a solver that shares the GPU
+  // with other solvers' concurrent launches
+  int xcd = 0;
+  // 1: the line-search retry slots run in ONE tail launch with grid barriers (its
+  // workgroups must be co-resident); 0: every budgeted slot is its own fwd /
+  // bwd_update launch pair (no cross-launch co-residency: in-process workers that
+  // solve concurrently)
+  int tail = 1;
 };
 
 // New stream rows a solve ingests into its ring before reading the window

@@ -40,7 +40,7 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   // slots launched one by one: the initial evaluation + one trial per iteration
   // (what a solve whose line searches accept their first trial uses); the
   // remaining budget runs in the persistent tail launch
-  nfast_ = cfg.mode == 1 ? cfg.nslots : (1 + cfg.iters < cfg.nslots ? 1 + cfg.iters : cfg.nslots);
+  nfast_ = (cfg.mode == 1 || !cfg.tail) ? cfg.nslots : (1 + cfg.iters < cfg.nslots ? 1 + cfg.iters : cfg.nslots);
 
   // solver-private vectors use the padded layout of solve_kernels.hip
   dv_.KP = padded_classes(cfg.K);

@@ -62,6 +62,13 @@ class SolverOptions:
     # several in-process workers keep the chain (kernels of other streams -- RCCL,
     # other workers -- could hold the XCD's CUs the persistent workgroups wait for).
     persist: bool | None = None
+    # XCD (0..7) of the persistent solve's workgroups / the chain's backward slices
+    # (in-L2 hand-offs); -1: spread over the XCDs (sc1 hand-offs) -- for a solver
+    # whose GPU runs other solvers' launches concurrently
+    xcd: int = 0
+    # False: no tail launch (its grid barriers need co-resident workgroups); every
+    # budgeted line-search slot is its own launch pair -- for concurrent in-process workers
+    tail: bool = True
 
     @property
     def nslots(self) -> int:
@@ -127,6 +134,8 @@ class LocalSolveOp:
         cfg.nslots, cfg.gd_lr, cfg.tol = o.nslots, o.gd_lr, o.tol
         cfg.xf32 = int(ring.X.dtype == torch.float32)
         cfg.persist = int(bool(o.persist))
+        cfg.xcd = int(o.xcd) if o.xcd < 0 else int(o.xcd) % 8
+        cfg.tail = int(bool(o.tail))
         self._native = h.LocalSolver(
             cfg, ring.X.data_ptr(), xt, ring.y.data_ptr(), w_old.data_ptr(), self.delta.data_ptr(),
             self.w_new.data_ptr(), self.frag.hi.data_ptr(), self.frag.lo.data_ptr(), self.frag.b.data_ptr(),

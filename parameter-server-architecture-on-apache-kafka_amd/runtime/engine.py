@@ -107,14 +107,24 @@ class LocalEngine:
         self.tracer = Tracer(cfg.trace_path, 0, self.device,
                              f"{cfg.log_dir}/logs-perf.csv" if cfg.perf_log else None)
         if cfg.solver.persist and cfg.num_workers > 1:
-            # the persistent solve needs its workgroups co-resident: one worker only
-            # (several in-process workers run their solves side by side)
+            # the persistent solve needs its workgroups co-resident: one worker only.
+            # Measured: two workers' persistent launches on their own XCDs deadlock (each
+            # launch's gap / riding workgroups wait for CUs of the other's XCD, and the
+            # dispatcher places a launch's workgroups in order) -- profiles/r02_v5
             cfg.solver = dataclasses.replace(cfg.solver, persist=False)
         if cfg.solver.persist is None and cfg.num_workers == 1 and is_gpu(self.device):
             # a lone worker has the GPU to itself: the persistent solve (one XCD) is the
             # fastest small-window solve on MI355X (profiles/r02_v5); unsupported shapes
             # (rows mode, fp32 rows, > 1024 features) keep the chain inside the solver
             cfg.solver = dataclasses.replace(cfg.solver, persist=True)
+        if cfg.num_workers > 4 and is_gpu(self.device) and cfg.solver.tail:
+            # many concurrent workers' solves share the CUs: no launch may wait for
+            # workgroups of its own that other workers' launches keep from being placed
+            # (8 workers' tail launches, 33 one-CU workgroups each, did -- fresh windows
+            # need many line-search retries).  Up to 4 workers (132 tail workgroups) keep
+            # the tail: 14.4k / 20.2k updates/s with it against 9.2k / 15.2k without
+            # (profiles/r02_v5/workers_*.jsonl)
+            cfg.solver = dataclasses.replace(cfg.solver, tail=False)
         if cfg.solver.use_graph is None and cfg.num_workers > 2:
             # many in-process workers share this process's launch thread: one graph
             # replay per solve beats 8 eager launches there (bench.py --workers 8:
@@ -123,7 +133,11 @@ class LocalEngine:
         w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0)
         self.t0 = time.time()
-        self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0)
+        # one worker: its solve's cooperating workgroups on XCD 0 (in-L2 hand-offs); several
+        # concurrent workers: spread over the XCDs (a one-XCD launch's gap workgroups would
+        # wait for CUs the other workers' solves hold -- the ASP runs timed out that way)
+        xcd = 0 if cfg.num_workers == 1 else -1
+        self.workers = [WorkerRole(k, self.spec, cfg, self.device, self.train, self.evalset, t0=self.t0, xcd=xcd)
                         for k in range(cfg.num_workers)]
         self.rounds = 0
         # worker 0's rows and the server rows: one eval pass (sequential consistency,

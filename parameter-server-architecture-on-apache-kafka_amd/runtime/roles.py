@@ -11,6 +11,8 @@ delta / weight tensors; roles only enqueue device work on the current stream.
 """
 from __future__ import annotations
 
+import dataclasses
+
 import math
 import os
 import time
@@ -75,7 +77,8 @@ def make_evalset(spec, test, device):
 
 
 class WorkerRole:
-    def __init__(self, k: int, spec, cfg: PSConfig, device, train, evalset, t0: float | None = None):
+    def __init__(self, k: int, spec, cfg: PSConfig, device, train, evalset, t0: float | None = None,
+                 xcd: int = 0):
         self.k, self.spec, self.cfg, self.device = k, spec, cfg, torch.device(device)
         self.wide = is_wide(spec)
         if self.wide:
@@ -93,7 +96,9 @@ class WorkerRole:
             self.solver = WideSolveOp(spec, self.ring.cap, self.ring.NZ, self.device, cfg.solver,
                                       dense_delta=cfg.wide_dense_delta)
         else:
-            self.solver = LocalSolveOp(spec, self.ring.cap, self.device, cfg.solver)
+            # xcd: the XCD of the solve's cooperating workgroups (-1: spread over the XCDs,
+            # for workers that share the GPU with other workers' concurrent solves)
+            self.solver = LocalSolveOp(spec, self.ring.cap, self.device, dataclasses.replace(cfg.solver, xcd=xcd))
         self.evalset = evalset
         self.w = torch.zeros(spec.P, dtype=torch.float32, device=self.device)  # pulled weights
         self.scratch = EvalScratch(self.device)

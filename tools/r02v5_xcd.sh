@@ -13,7 +13,7 @@ PSX_PERSIST_XCD=0 timeout -k 10 200 python tools/bench_solver.py > $OUT/bench_so
 rc=$?; echo "bench_solver spread rc=$rc"; grep -E "persistent" $OUT/bench_solver_spread.txt; [ $rc -eq 0 ] || exit $rc
 PSX_SOLVER_STAMPS=1 timeout -k 10 120 python tools/bench_solver.py --stamps-persist > $OUT/stamps_persist_xcd.txt 2>&1 && PSX_SOLVER_STAMPS=1 timeout -k 10 120 python tools/bench_solver.py --stamps > $OUT/stamps_chain.txt 2>&1
 rc=$?; echo "stamps rc=$rc"; [ $rc -eq 0 ] || exit $rc
-for v in "--chain" "" "--workers 4"; do
+for v in ${VARIANTS:-"--chain" "" "--workers 4"}; do
   timeout -k 10 300 python bench.py $v >> $OUT/bench_variants.jsonl 2>> $OUT/bench_err.log
   rc=$?; echo "bench [$v] rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done

@@ -13,7 +13,7 @@ STEPS="${PMC_STEPS:-150}"
 run_pass() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o $name -- \
-    python3 bench.py --steps $STEPS --warmup 20 > $OUT/$name.log 2>&1
+    python3 bench.py --steps $STEPS --warmup 20 --no-accuracy-run > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   return $rc

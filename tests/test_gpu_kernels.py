@@ -408,3 +408,34 @@ def test_inplace_finalisation_matches_tail(cuda, monkeypatch, ls_max, iters):
         assert torch.equal(a[0], b[0])
         assert a[1] == b[1] and a[2] == b[2] and a[2][4] == 0
         assert torch.equal(a[3], b[3]) and torch.equal(a[4], b[4]) and torch.equal(a[5], b[5])
+
+
+@pytest.mark.parametrize("B,start", [(1024, 0), (700, 96), (1020, 40)])  # (1020, 40): 33 tiles -> spread form
+def test_solve_placement_variants_agree(cuda, B, start):
+    """Where the cooperating workgroups run must not change the result: the
+    persistent solve on XCD 0, on XCD 3 and spread over the XCDs (xcd = -1), and
+    the chain with its backward slices on one XCD or spread, are each bitwise
+    identical (fixed-order reductions everywhere); persistent vs chain agree up to
+    summation order.  Placement: blockIdx % 8 == XCD (tools/xcd_probe.hip)."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(B, seed=11)
+    cap = 1024
+    ring = _ring_with(ds, cap, start, B, cuda)
+    w = _rand_w(spec, 5, 0.03).to(cuda)
+    outs = {}
+    for persist in (True, False):
+        for xcd in (0, 3, -1):
+            op = LocalSolveOp(spec, cap, cuda, SolverOptions(use_graph=False, persist=persist, xcd=xcd))
+            for _ in range(2):  # a replay on the same solver as well
+                op.run(ring, B, start, w)
+            torch.cuda.synchronize()
+            assert bool(op._native.persistent) == persist
+            assert op.barrier_errors() == 0
+            outs[(persist, xcd)] = (op.delta.clone(), op.loss.item())
+    for persist in (True, False):
+        ref = outs[(persist, 0)]
+        for xcd in (3, -1):
+            assert torch.equal(outs[(persist, xcd)][0], ref[0]), (persist, xcd)
+            assert outs[(persist, xcd)][1] == ref[1]
+    a, b = outs[(True, 0)][0], outs[(False, 0)][0]
+    assert (a - b).abs().max().item() <= 2e-3 * b.abs().max().item()

@@ -252,7 +252,9 @@ def main(argv=None):
     world = int(world_env or "1")
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
-    if world > 1:
+    if world > 1 or os.environ.get("PSX_BENCH_DIST") == "1":
+        # PSX_BENCH_DIST=1 with one rank: the multi-rank code path (DistEngine, RCCL
+        # communicator, all-reduce + update launch per round) rehearsed on one GPU
         return bench_distributed(a)
 
     device = "cpu" if a.cpu else "cuda:0"

@@ -115,14 +115,15 @@ void launch_slot_ride(const SolverCfg& cfg, const SolveParams* prm, Ctrl* ctrl, 
                       int fin_slot = kNoFinSlot);
 size_t stats_rows_lds_bytes();
 
-// ---- persistent small-window solve: the whole solve in ONE launch (see
-// solve_kernels.hip); G = persist_grid(FP, window tiles) co-resident
-// workgroups + `nride` evaluation workgroups of `ride` (tiles [0, nride)) ----
+// ---- persistent small-window solve: every slot and the finalisation in ONE
+// launch after launch_stats_prep (see solve_kernels.hip); G = persist_grid(FP,
+// window tiles) co-resident workgroups (on XCD cfg.xcd when G <= 32) + `nride`
+// evaluation workgroups of `ride` (tiles [0, nride)) ----
 bool persist_supported(int FP, int KP);
 int persist_grid(int FP, int ntiles);
 size_t persist_lds_bytes(int FP);
-void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
-                    const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s);
+void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win, int G,
+                    const EvalRide& ride, int nride, hipStream_t s);
 // fp32 ring rows: rows src_first + i*src_step -> slots (dst_first + i) % cap
 void launch_ring_ingest_f32(const float* src, const int32_t* ysrc, int64_t src_first, int64_t src_step, int64_t n,
                             float* ring, int32_t* yring, int64_t dst_first, int64_t cap, int FP, hipStream_t s);

@@ -1909,7 +1909,7 @@ int persist_grid(int FP, int ntiles) { return ntiles > FP / 32 ? ntiles : FP / 3
 
 template <int FP, int KP, int S>
 __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, SolveDev dv, Ctrl* gctrl, SolveParams win,
-                                                            RingIngest ing, int G, EvalRide ride, int nride) {
+                                                            int G, EvalRide ride, int nride) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int role = xcd_role<S>((int)blockIdx.x, G, cfg.xcd & 7), tid = threadIdx.x;
   if (role < 0) {  // an evaluation workgroup riding in this launch: one test tile, no waiting
@@ -2014,40 +2014,40 @@ __global__ __launch_bounds__(256) void solve_persist_kernel(SolverCfg cfg, Solve
 }
 
 template <int FP, int S>
-static void launch_persist_fps(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
-                               const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+static void launch_persist_fps(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win, int G,
+                               const EvalRide& ride, int nride, hipStream_t s) {
   const size_t lb = persist_lds_bytes(FP);
   const int grid = xcd_grid(G, nride, S == 2, cfg.xcd & 7);
   switch (dv.KP) {
-    case 2: solve_persist_kernel<FP, 2, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
-    case 4: solve_persist_kernel<FP, 4, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
-    default: solve_persist_kernel<FP, 8, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, ing, G, ride, nride); break;
+    case 2: solve_persist_kernel<FP, 2, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, G, ride, nride); break;
+    case 4: solve_persist_kernel<FP, 4, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, G, ride, nride); break;
+    default: solve_persist_kernel<FP, 8, S><<<grid, 256, lb, s>>>(cfg, dv, ctrl, win, G, ride, nride); break;
   }
 }
 
 template <int FP>
-static void launch_persist_fp(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
-                              const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+static void launch_persist_fp(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win, int G,
+                              const EvalRide& ride, int nride, hipStream_t s) {
   // one XCD when the solve workgroups fit its CUs (PSX_PERSIST_XCD=0: always spread)
   static const bool xcd_ok = [] {
     const char* e = std::getenv("PSX_PERSIST_XCD");
     return !(e && e[0] == '0');
   }();
   if (xcd_ok && G <= kMaxXcdWg && cfg.xcd >= 0)
-    launch_persist_fps<FP, 2>(cfg, dv, ctrl, win, ing, G, ride, nride, s);
+    launch_persist_fps<FP, 2>(cfg, dv, ctrl, win, G, ride, nride, s);
   else
-    launch_persist_fps<FP, 1>(cfg, dv, ctrl, win, ing, G, ride, nride, s);
+    launch_persist_fps<FP, 1>(cfg, dv, ctrl, win, G, ride, nride, s);
 }
 
 bool persist_supported(int FP, int KP) { return FP >= 128 && FP <= 1024 && KP <= 8; }
 
-void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win,
-                    const RingIngest& ing, int G, const EvalRide& ride, int nride, hipStream_t s) {
+void launch_persist(const SolverCfg& cfg, const SolveDev& dv, Ctrl* ctrl, const SolveParams& win, int G,
+                    const EvalRide& ride, int nride, hipStream_t s) {
   switch (cfg.Fp) {
-    case 128: launch_persist_fp<128>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
-    case 256: launch_persist_fp<256>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
-    case 512: launch_persist_fp<512>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
-    case 1024: launch_persist_fp<1024>(cfg, dv, ctrl, win, ing, G, ride, nride, s); break;
+    case 128: launch_persist_fp<128>(cfg, dv, ctrl, win, G, ride, nride, s); break;
+    case 256: launch_persist_fp<256>(cfg, dv, ctrl, win, G, ride, nride, s); break;
+    case 512: launch_persist_fp<512>(cfg, dv, ctrl, win, G, ride, nride, s); break;
+    case 1024: launch_persist_fp<1024>(cfg, dv, ctrl, win, G, ride, nride, s); break;
     default: break;
   }
 }

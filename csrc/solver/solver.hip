@@ -265,8 +265,8 @@ void LocalSolver::run(int B, int start, hipStream_t stream, const RingIngest& in
     d.ap_b = dv_.ap_b;
     d.ap_lr = dv_.ap_lr;
     d.ap_coff = dv_.ap_coff;
-    launch_persist(cfg_, d, ctrl_, SolveParams{B, start, 0, 0}, RingIngest{}, G, ride ? *ride : EvalRide{},
-                   ride ? ride->ntiles() : 0, stream);
+    launch_persist(cfg_, d, ctrl_, SolveParams{B, start, 0, 0}, G, ride ? *ride : EvalRide{}, ride ? ride->ntiles() : 0,
+                   stream);
     hip_check(hipGetLastError(), "persistent solve launch");
     dv_.ap_w = nullptr;
     return;

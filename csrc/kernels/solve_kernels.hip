@@ -773,10 +773,13 @@ size_t bwd_ride_lds_bytes(int FP) {
   return a > b ? a : b;
 }
 
-size_t bwd_lds_bytes() {
-  return (size_t)4 * 16 * 32 * 4 + 2 * 512 * 2 + ctrl_lds_bytes() +
-         (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) + sizeof(CtrlScratch);
-}
+// persistent solve: the slice's curvature pairs in LDS, [kMaxHist][S | Y][KP <= 8 classes x 32 features + 16 intercepts]
+constexpr int kSyStride = 8 * 32 + 16;
+constexpr size_t kSyBytes = (size_t)kMaxHist * 2 * kSyStride * sizeof(float);
+constexpr size_t kBwdLdsBytes = (size_t)4 * 16 * 32 * 4 + 2 * 512 * 2 + ctrl_lds_bytes() +
+                                (4 * kNDX + kNDX + kMaxSlices * kNDX) * sizeof(double) + 256 * sizeof(float) +
+                                sizeof(CtrlScratch);
+size_t bwd_lds_bytes() { return kBwdLdsBytes; }
 
 // Body shared by bwd_update_kernel, tail_kernel and the persistent solve: slice
 // `wg` of `NS`.  kP (persistent solve): the controller copy in LDS persists
@@ -866,10 +869,20 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   // stored curvature pairs of this slice (measured: prefetching them with the
   // backward's operands lengthens the load phase by ~1 us and saves nothing
   // later -- profiles/r02_v5/README.md -- so they are read where needed)
-  auto s_at = [&](int i, int e) { return dv.S[(size_t)i * PI + idx[e]]; };
-  auto y_at = [&](int i, int e) { return dv.Y[(size_t)i * PI + idx[e]]; };
-  auto sb_at = [&](int i) { return dv.S[(size_t)i * PI + IB + tid]; };
-  auto yb_at = [&](int i) { return dv.Y[(size_t)i * PI + IB + tid]; };
+  // (persistent solve: the slice's pairs stay in LDS for the whole solve -- each
+  // element is written and read by the same thread -- at lsy[(2 i + {0: S, 1: Y})
+  // * kSyStride + c * 32 + fl], intercepts at [... + 256 + tid])
+  float* lsy = kP != 0 ? (float*)(lds + (kBwdLdsBytes + 15) / 16 * 16) : nullptr;
+  auto s_at = [&](int i, int e) {
+    return kP != 0 ? lsy[2 * i * kSyStride + (cgp + 8 * e) * 32 + fl] : dv.S[(size_t)i * PI + idx[e]];
+  };
+  auto y_at = [&](int i, int e) {
+    return kP != 0 ? lsy[(2 * i + 1) * kSyStride + (cgp + 8 * e) * 32 + fl] : dv.Y[(size_t)i * PI + idx[e]];
+  };
+  auto sb_at = [&](int i) { return kP != 0 ? lsy[2 * i * kSyStride + 256 + tid] : dv.S[(size_t)i * PI + IB + tid]; };
+  auto yb_at = [&](int i) {
+    return kP != 0 ? lsy[(2 * i + 1) * kSyStride + 256 + tid] : dv.Y[(size_t)i * PI + IB + tid];
+  };
   // a launch that may finish the solve finalises its slice in place (below):
   // its w_old elements travel with the per-element state
   const bool may_fin = slot >= fin_slot;
@@ -1199,8 +1212,13 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
         dv.x[idx[e]] = XO[e];
         if (more) {
           if (ps >= 0) {
-            dv.S[(size_t)ps * PI + idx[e]] = t_acc * DD[e];
-            dv.Y[(size_t)ps * PI + idx[e]] = g[e] - GC[e];
+            if constexpr (kP != 0) {
+              lsy[2 * ps * kSyStride + (cgp + 8 * e) * 32 + fl] = t_acc * DD[e];
+              lsy[(2 * ps + 1) * kSyStride + (cgp + 8 * e) * 32 + fl] = g[e] - GC[e];
+            } else {
+              dv.S[(size_t)ps * PI + idx[e]] = t_acc * DD[e];
+              dv.Y[(size_t)ps * PI + idx[e]] = g[e] - GC[e];
+            }
           }
           dv.g_c[idx[e]] = g[e];
         }
@@ -1212,8 +1230,13 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       dv.x[IB + tid] = xbv;
       if (more) {
         if (ps >= 0) {
-          dv.S[(size_t)ps * PI + IB + tid] = t_acc * db0;
-          dv.Y[(size_t)ps * PI + IB + tid] = gb - gcb0;
+          if constexpr (kP != 0) {
+            lsy[2 * ps * kSyStride + 256 + tid] = t_acc * db0;
+            lsy[(2 * ps + 1) * kSyStride + 256 + tid] = gb - gcb0;
+          } else {
+            dv.S[(size_t)ps * PI + IB + tid] = t_acc * db0;
+            dv.Y[(size_t)ps * PI + IB + tid] = gb - gcb0;
+          }
         }
         dv.g_c[IB + tid] = gb;
         dbv = cg * gb;
@@ -1904,7 +1927,7 @@ __device__ __forceinline__ void x_barrier(unsigned long long* flags, int wg, int
 }
 
 PSX_HD constexpr size_t persist_fwd_bytes(int FP) { return (eval_lds_bytes(FP) + 15) / 16 * 16; }
-size_t persist_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (bwd_lds_bytes() + 15) / 16 * 16; }
+size_t persist_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (bwd_lds_bytes() + 15) / 16 * 16 + kSyBytes; }
 int persist_grid(int FP, int ntiles) { return ntiles > FP / 32 ? ntiles : FP / 32; }
 
 template <int FP, int KP, int S>

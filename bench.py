@@ -264,27 +264,34 @@ def main(argv=None):
     cfg = build_cfg(a, a.workers)
     cfg.max_iters = a.warmup
     eng = LocalEngine(cfg, device, train=train, test=test)
-    eng.run() if a.warmup > 0 else None
-    # timed region: exactly `steps` rounds, synchronised on both sides
+    # ONE log sink for the whole run: the accuracy half's t = 0 is the run's first
+    # server row, warm-up included
+    if a.warmup > 0:
+        eng.run(close_log=False)
     eng.cfg.max_iters = a.steps
-    eng.log = _fresh_log(eng)
+    n_warm = len(eng.log.book.server) if eng.log.book is not None else 0
     u0 = eng.server.updates  # the server's counter includes the warmup rounds
     if device != "cpu":
         torch.cuda.synchronize()
+    # timed region: exactly `steps` rounds, synchronised on both sides (their rows
+    # logged inside it)
     t0 = time.perf_counter()
-    out = eng.run()
+    out = eng.run(close_log=False)
+    eng.log.drain(block=True)
     if device != "cpu":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
-    res.update(_accuracy_fields(eng.log.book.server))
+    res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),
+                     "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2)}
+    rows = list(eng.log.book.server)
+    res.update(_accuracy_fields(rows, timed_from=n_warm))
     if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not a.cpu:
-        rows = list(eng.log.book.server)
         eng.cfg.max_iters = ACC_ROUNDS - a.steps
-        eng.log = _fresh_log(eng)
-        eng.run()
-        res["accuracy_run"] = _accuracy_run(rows, list(eng.log.book.server), a.steps)
+        eng.run(close_log=False)
+        res["accuracy_run"] = _accuracy_run(list(eng.log.book.server), a.steps, n_warm)
+    eng.log.close()
     print(json.dumps(res))
     return res
 
@@ -292,20 +299,19 @@ def main(argv=None):
 ACC_ROUNDS = 2000  # the default --steps: the accuracy half of the metric is quoted at this many rounds
 
 
-def _accuracy_run(timed_rows, extra_rows, steps):
+def _accuracy_run(rows, steps, n_warm):
     """Accuracy half of the metric when the timed region is shorter than
     ACC_ROUNDS (the driver's short runs): the same engine keeps training, UNTIMED,
-    until ACC_ROUNDS rounds past the warm-up, and the server's test-set rows of
-    the timed region plus that continuation give the curve.  updates/s is never
-    taken from the continuation."""
-    rows = timed_rows + extra_rows
+    until ACC_ROUNDS rounds past the warm-up; the curve covers every server row of
+    the run (t = 0 at the first warm-up row).  updates/s is never taken from the
+    continuation."""
     out = {"rounds_after_warmup": ACC_ROUNDS, "timed_rounds": steps, "untimed_continuation_rounds": ACC_ROUNDS - steps}
-    out.update(_accuracy_fields(rows))
+    out.update(_accuracy_fields(rows, timed_from=n_warm))
     if rows:
         out["best_test_f1"] = round(max(r[2] for r in rows), 4)
         out["test_f1"] = round(rows[-1][2], 4)
         out["test_accuracy"] = round(rows[-1][3], 4)
-        out["wallclock_s"] = round((rows[-1][0] - rows[0][0]) / 1000.0, 4)
+        out["wallclock_s"] = round((rows[-1][0] - rows[0][0]) / 1000.0, 6)
     return out
 
 
@@ -418,7 +424,7 @@ def bench_distributed(a):
         eng._run_bsp()
         if rank == 0:
             eng.log.close()
-            res["accuracy_run"] = _accuracy_run(timed_rows, list(eng.log.book.server), a.steps)
+            res["accuracy_run"] = _accuracy_run(timed_rows + list(eng.log.book.server), a.steps, 0)
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()
@@ -427,26 +433,30 @@ def bench_distributed(a):
     return res
 
 
-def _accuracy_fields(server_rows, threshold=0.40):
-    """Accuracy half of the metric from the timed region's server rows (global
-    model on the test set, ServerProcessor.java:154-165): the curve, the best
-    weighted F1 and the time to reach F1 >= threshold (None: never)."""
+def _accuracy_fields(server_rows, threshold=0.40, timed_from=0):
+    """Accuracy half of the metric (global model on the test set, ServerProcessor.java:
+    154-165): the curve, the best weighted F1 and the time to reach F1 >= threshold,
+    all with t = 0 at the run's FIRST server row (warm-up included; SURVEY.md section
+    6).  Row timestamps are taken when each evaluation completed (us resolution)."""
     out = {"accuracy_vs_wallclock": _curve(server_rows)}
     if server_rows:
         ts0 = server_rows[0][0]
         hit = next((r for r in server_rows if r[2] >= threshold), None)
-        out["time_to_f1_0.40_s"] = round((hit[0] - ts0) / 1000.0, 4) if hit is not None else None
+        out["time_to_f1_0.40_s"] = round((hit[0] - ts0) / 1000.0, 6) if hit is not None else None
+        out["time_to_f1_0.40_rounds"] = (server_rows.index(hit) + 1) if hit is not None else None
         out["server_rows"] = len(server_rows)
+        out["timed_server_rows"] = len(server_rows) - timed_from
+        out["best_test_f1_all_rows"] = round(max(r[2] for r in server_rows), 4)
     return out
 
 
 def _curve(server_rows, points=10):
-    """[(seconds since the timed region started, test accuracy, weighted F1)] samples."""
+    """[(seconds since the run's first server row, test accuracy, weighted F1)] samples."""
     if not server_rows:
         return []
     ts0 = server_rows[0][0]
     idx = sorted({int(i * (len(server_rows) - 1) / max(1, points - 1)) for i in range(points)})
-    return [(round((server_rows[i][0] - ts0) / 1000.0, 4), round(server_rows[i][3], 4), round(server_rows[i][2], 4))
+    return [(round((server_rows[i][0] - ts0) / 1000.0, 6), round(server_rows[i][3], 4), round(server_rows[i][2], 4))
             for i in idx]
 
 

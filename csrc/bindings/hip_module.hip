@@ -13,6 +13,7 @@
 #include "../comm/rccl_comm.h"
 #include "../runtime/async_server.h"
 #include "../runtime/bsp_loop.h"
+#include "../runtime/lanes_loop.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
 #include "../solver/wide_solver.h"
@@ -633,6 +634,80 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property("next_local", &BspLoop::next_local, &BspLoop::set_next_local)
       .def_property_readonly("exhausted", &BspLoop::exhausted)
       .def_property_readonly("host_us_per_round", &BspLoop::host_us_per_round);
+  // Multi-lane BSP round loop (csrc/runtime/lanes_loop.h): `cfg` dict of ints /
+  // floats / lists; pointers are device addresses or host-runtime handles.
+  py::class_<LanesLoop>(m, "LanesLoop")
+      .def(py::init([](py::dict d, RcclComm* comm) {
+             auto I = [&](const char* k, int64_t def) { return d.contains(k) ? d[k].cast<int64_t>() : def; };
+             auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
+             auto D = [&](const char* k, double def) { return d.contains(k) ? d[k].cast<double>() : def; };
+             auto V = [&](const char* k) {
+               return d.contains(k) ? d[k].cast<std::vector<uintptr_t>>() : std::vector<uintptr_t>{};
+             };
+             LanesLoopCfg c;
+             c.scfg = d["scfg"].cast<SolverCfg>();
+             c.dsX = P<const uint16_t>(U("dsX"));
+             c.dsy = P<const int32_t>(U("dsy"));
+             c.ds_rows = I("ds_rows", 0);
+             c.N = (int)I("N", 1);
+             c.per_iter_rows = (int)I("per_iter_rows", 0);
+             c.p_ms = D("p_ms", 0.0);
+             c.epochs = I("epochs", 1);
+             c.t0_ms = D("t0_ms", 0.0);
+             c.k = d.contains("k") ? d["k"].cast<std::vector<int>>() : std::vector<int>{};
+             c.L = (int)c.k.size();
+             c.X = V("X");
+             c.XT = V("XT");
+             c.y = V("y");
+             c.window = V("window");
+             c.w = P<float>(U("w"));
+             c.lr = (float)D("lr", 1.0);
+             const auto shi = V("shi"), slo = V("slo"), sb = V("sb");
+             for (int i = 0; i < 2; ++i) {
+               c.shi[i] = i < (int)shi.size() ? P<uint16_t>(shi[i]) : nullptr;
+               c.slo[i] = i < (int)slo.size() ? P<uint16_t>(slo[i]) : nullptr;
+               c.sb[i] = i < (int)sb.size() ? P<float>(sb[i]) : nullptr;
+             }
+             c.scoff = (int)I("scoff", 0);
+             c.Xt = P<const uint16_t>(U("Xt"));
+             c.yt = P<const int32_t>(U("yt"));
+             c.T = (int)I("T", 0);
+             c.sink = U("sink");
+             c.log_server = I("log_server", 1) != 0;
+             c.log_workers = I("log_workers", 1) != 0;
+             c.tracker = U("tracker");
+             c.api = U("api");
+             c.server_rank = (int)I("server_rank", 0);
+             return std::make_unique<LanesLoop>(c, comm);
+           }),
+           py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
+      .def(
+          "run",
+          [](LanesLoop& l, int64_t rounds, int64_t r0, uintptr_t stream, double max_wait_s) {
+            py::gil_scoped_release nogil;
+            return l.run(rounds, r0, S(stream), max_wait_s);
+          },
+          py::arg("rounds"), py::arg("r0"), py::arg("stream"), py::arg("max_wait_s") = 600.0)
+      .def("flush", [](LanesLoop& l, uintptr_t stream) { l.flush(S(stream)); })
+      .def("set_sink", &LanesLoop::set_sink)
+      .def("set_lr", &LanesLoop::set_lr)
+      .def("next_local", &LanesLoop::next_local)
+      .def("set_next_local", &LanesLoop::set_next_local)
+      .def("exhausted", &LanesLoop::exhausted)
+      .def_property_readonly("all_exhausted", &LanesLoop::all_exhausted)
+      .def_property_readonly("hand_off_scope", &LanesLoop::hand_off_scope)
+      .def_property_readonly("host_us_per_round", &LanesLoop::host_us_per_round)
+      .def_property_readonly("rounds_run", &LanesLoop::rounds_run)
+      .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })
+      .def("loss", [](const LanesLoop& l, int lane, uintptr_t s) { return l.loss(lane, S(s)); })
+      .def("delta_ptr", &LanesLoop::delta_ptr)
+      .def("copy_out", [](const LanesLoop& l, int lane, uintptr_t loss, uintptr_t delta,
+                          uintptr_t s) { l.copy_out(lane, loss, delta, S(s)); },
+           py::arg("lane"), py::arg("loss") = 0, py::arg("delta") = 0, py::arg("stream") = 0)
+      .def("inject_spin_timeout", &LanesLoop::inject_spin_timeout)
+      .def("poll_errors", &LanesLoop::poll_errors)
+      .def_static("probe_placement", [](uintptr_t s) { return LanesLoop::probe_placement(S(s)); });
+  m.def("lanes_supported", &lanes_supported, py::arg("FP"), py::arg("K"), py::arg("cap"));
   m.attr("ASYNC_DONE") = (int)kAsyncDone;
   m.attr("ASYNC_ERROR_TOKEN") = (int)kAsyncErrorToken;
   m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;

@@ -61,16 +61,43 @@ def _run(cmd):
     return r.stdout
 
 
-def _compile_link(compiler, sources, out, cflags, ldflags, jobs, objdir):
+def _local_includes(src):
+    """src + every file it pulls in through #include "..." (recursively)."""
+    seen, todo = [], [os.path.abspath(src)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.append(f)
+        with open(f) as fh:
+            for line in fh:
+                line = line.strip()
+                if line.startswith("#include \""):
+                    todo.append(os.path.normpath(os.path.join(os.path.dirname(f), line.split('"')[1])))
+    return seen
+
+
+def _compile_link(compiler, sources, out, cflags, ldflags, jobs, objdir, headers=()):
+    """Compile every source whose object is stale (its own content, the shared
+    headers' and the flags hashed into <obj>.hash), then link."""
     os.makedirs(objdir, exist_ok=True)
     objs = []
     cmds = []
     for s in sources:
         o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
-        cmds.append([compiler] + cflags + ["-c", s, "-o", o])
+        dig = _hash(_local_includes(s), cflags)
+        if _up_to_date(o, dig):
+            continue
+        cmds.append(([compiler] + cflags + ["-c", s, "-o", o], o, dig))
+
+    def one(job):
+        cmd, o, dig = job
+        _run(cmd)
+        open(o + ".hash", "w").write(dig)
+
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        list(ex.map(_run, cmds))
+        list(ex.map(one, cmds))
     tmp = out + ".tmp"
     _run([compiler] + objs + ["-shared", "-o", tmp] + ldflags)
     os.replace(tmp, out)
@@ -89,7 +116,7 @@ def build_host(force=False, jobs=8):
     digest = _hash(sources + headers, cflags + ldflags)
     if not force and _up_to_date(out, digest):
         return out
-    _compile_link("g++", sources, out, cflags, ldflags, jobs, os.path.join(ROOT, "build", "host"))
+    _compile_link("g++", sources, out, cflags, ldflags, jobs, os.path.join(ROOT, "build", "host"), headers)
     open(out + ".hash", "w").write(digest)
     return out
 
@@ -117,7 +144,7 @@ def build_hip(force=False, jobs=8):
     digest = _hash(sources + headers, cflags + ldflags)
     if not force and _up_to_date(out, digest):
         return out
-    _compile_link(hipcc, sources, out, cflags, ldflags, jobs, os.path.join(ROOT, "build", "hip"))
+    _compile_link(hipcc, sources, out, cflags, ldflags, jobs, os.path.join(ROOT, "build", "hip"), headers)
     open(out + ".hash", "w").write(digest)
     return out
 

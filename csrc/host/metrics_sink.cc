@@ -93,21 +93,27 @@ void MetricsSink::run() {
       std::lock_guard<std::mutex> lk(mu_);
       if (stop_ && spins > 100000) break;  // closing with a producer that never ran: give up
     }
+    double ts = (double)p.ts;
+    if (p.ts < 0)  // stamped now: the evaluation just completed
+      ts = (double)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+               .count() /
+           1000.0;
     double f1 = 0.0, acc = 0.0;
     weighted_f1_accuracy(s.conf, K_, &f1, &acc);
     const double loss = s.loss;
     if (p.kind == 0) {
-      if (wlog_) wlog_->log_worker(p.ts, p.partition, p.vc, loss, f1, acc, p.nseen);
+      if (wlog_) wlog_->log_worker((int64_t)ts, p.partition, p.vc, loss, f1, acc, p.nseen);
     } else {
-      if (slog_) slog_->log_server(p.ts, p.vc, f1, acc);
+      if (slog_) slog_->log_server((int64_t)ts, p.vc, f1, acc);
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (keep_) {
         if (p.kind == 0)
-          wrows_.push_back(WorkerRow{p.ts, p.partition, p.vc, loss, f1, acc, p.nseen});
+          wrows_.push_back(WorkerRow{ts, p.partition, p.vc, loss, f1, acc, p.nseen});
         else
-          srows_.push_back(ServerRow{p.ts, p.vc, f1, acc});
+          srows_.push_back(ServerRow{ts, p.vc, f1, acc});
       }
       pending_.pop_front();
       free_.push_back(p.slot);

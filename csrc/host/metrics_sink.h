@@ -37,13 +37,18 @@ static_assert(sizeof(EvalSlot) == 1088, "EvalSlot layout is shared with the devi
 // (weighted F1, accuracy) of a [K][K] block of a 16x16 confusion matrix.
 void weighted_f1_accuracy(const int32_t* conf16, int K, double* f1, double* acc);
 
+// Row timestamps: epoch milliseconds.  A record submitted with ts < 0 is stamped
+// by the sink thread when it observes the record's evaluation complete (us
+// resolution; the CSV keeps the reference's integer milliseconds).
 struct WorkerRow {
-  int64_t ts, partition, vc;
+  double ts;
+  int64_t partition, vc;
   double loss, f1, acc;
   int64_t nseen;
 };
 struct ServerRow {
-  int64_t ts, vc;
+  double ts;
+  int64_t vc;
   double f1, acc;
 };
 

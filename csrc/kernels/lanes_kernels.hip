@@ -1,0 +1,537 @@
+// Multi-lane BSP round kernel (see lanes_kernels.h).
+#include "lanes_kernels.h"
+
+#include <cstdlib>
+
+#include "solve_body.h"
+
+namespace psx {
+
+bool lanes_supported(int FP, int K, int cap) {
+  return FP >= 128 && FP <= 1024 && (FP & (FP - 1)) == 0 && K >= 2 && K <= 8 && cap >= 32 && cap % 32 == 0 &&
+         cap <= 32 * kLaneWg;
+}
+size_t lanes_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (kBwdLdsBytes + 15) / 16 * 16 + kSyBytes; }
+int lanes_rider_base(int L) { return kLaneWg * (8 - L); }
+int lanes_grid(int L, int nride_total) {
+  const int extra = nride_total - lanes_rider_base(L);
+  return 8 * kLaneWg + (extra > 0 ? extra : 0);
+}
+
+namespace {
+
+// Element i of a kernel-argument array with a workgroup-uniform runtime index:
+// a switch over constant indices keeps every access a scalar load from the
+// kernarg segment (a dynamic index would copy the whole argument struct into
+// scratch memory, per lane, at kernel entry).
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&arr)[N], int i) {
+  T v = arr[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j)
+    if (i == j) v = arr[j];
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Riders: evaluation of up to kMaxEvalModels models (the previous round's
+// local models and global model) over the test tiles.  Work items = (model
+// pair, test tile), pair-major, dealt to the riders in contiguous chunks so that
+// a rider keeps one pair's fragments in registers across its tiles.  Every
+// rider arrives on the ticket once; the last one publishes every model's
+// counts (and its loss) into its pinned slot, then the sequence number.
+template <int FP>
+__device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel* ma, const EvalModel* mb, int K) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, c = col & 7;
+  const EvalModel* m = col < 8 ? ma : mb;
+  const bool live = m != nullptr && c < K;
+#pragma unroll
+  for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+    const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
+    const size_t fo = ((size_t)cg * 16 + (live ? m->coff + c : 0)) * 8;
+    wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      wf.h[kk] = *(const u16x8*)(m->hi + fo);
+      wf.l[kk] = *(const u16x8*)(m->lo + fo);
+    }
+  }
+}
+
+template <int FP>
+__device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, int rid, int nride) {
+  if (ev.nmodels <= 0 || rid >= nride) return;
+  char* red_base = lds + 32 * FP * 2;
+  int* cl = (int*)(red_base + 8192);  // [kMaxEvalModels][256]
+  int* lastp = cl + kMaxEvalModels * 256;
+  const int tid = threadIdx.x, K = ev.K, T = ev.T, M = ev.nmodels;
+  const int nT = (T + 31) / 32, npairs = (M + 1) / 2;
+  for (int m = 0; m < M; ++m) cl[m * 256 + tid] = 0;
+  const int items = npairs * nT, chunk = (items + nride - 1) / nride;
+  const int i0 = rid * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
+  int curp = -1;
+  WFrag<FP> wf;
+  __syncthreads();
+  for (int it = i0; it < i1; ++it) {
+    const int p = it / nT, tile = it - p * nT;
+    const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
+    const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
+    if (p != curp) {  // (workgroup-uniform)
+      load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
+      curp = p;
+    }
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+    const int ylab = tid < nrows ? ev.yt[(size_t)tile * 32 + tid] : 0;
+    stage_tile<FP>(lds, ev.Xt, (int64_t)tile * 32, nrows, 0, false);
+    __syncthreads();
+    f32x4 a0, a1;
+    forward_tile_pre<FP>(lds, wf, a0, a1);
+    store_partial_logits(red_base, a0, a1);
+    __syncthreads();
+    if (tid < nrows) {
+      const int yl = ylab < 0 ? 0 : (ylab > 15 ? 15 : ylab);
+      const float* ba = A.b + A.coff;
+      int best = 0;
+      float bz = -INFINITY;
+      for (int c = 0; c < K; ++c) {
+        const float z = load_logit(red_base, tid, c) + ba[c];
+        if (z > bz) {
+          bz = z;
+          best = c;
+        }
+      }
+      atomicAdd(&cl[ma * 256 + yl * 16 + best], 1);
+      if (mb >= 0) {
+        const float* bb = Bm.b + Bm.coff;
+        int best2 = 0;
+        float bz2 = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(red_base, tid, 8 + c) + bb[c];
+          if (z > bz2) {
+            bz2 = z;
+            best2 = c;
+          }
+        }
+        atomicAdd(&cl[mb * 256 + yl * 16 + best2], 1);
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int m = 0; m < M; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(ev.acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ev.nticket - 1;
+  __syncthreads();
+  if (!*lastp) return;
+  // publication into the pinned slots (see eval_body.h): counts, loss, drain, seq
+  for (int m = 0; m < M; ++m) {
+    const EvalModel E = pick(ev.m, m);
+    const int tot = __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((int*)E.slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0)
+      __hip_atomic_store((float*)(E.slot + 1024), E.loss ? *E.loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int m = 0; m < M; ++m) {
+      const EvalModel E = pick(ev.m, m);
+      __hip_atomic_store((unsigned long long*)(E.slot + 1032), E.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Phase I of a lane's solve, row role: stage ring tile `rt` into the LDS image,
+// the round's new rows straight from the dataset (also written into the ring),
+// and publish the tile's column sums / sums of squares over its window rows.
+// Thread t holds chunk cg = t % CPR (8 features) of rows g + NG j (g = t / CPR),
+// so the sums come from the staging registers; the NG row groups are combined
+// in LDS (fixed order).
+template <int FP, int S>
+__device__ __forceinline__ void lane_stage_stats(char* lf, float* scratch, const SolverCfg& cfg, const SolveDev& dv,
+                                                 const LaneRound& r, const uint16_t* dsX, const int32_t* dsy, int rt,
+                                                 float* spart_wg) {
+  constexpr int CPR = FP / 8, NG = 256 / CPR, PER_T = 32 * CPR / 256;
+  const int tid = threadIdx.x, cap = cfg.cap;
+  const int cg = tid % CPR, g = tid / CPR;
+  uint16_t* X = const_cast<uint16_t*>(dv.X);
+  int32_t* Y = const_cast<int32_t*>(dv.y);
+  // labels travel with the first loads
+  int yv = 0;
+  bool ynew = false;
+  if (tid < 32) {
+    const int s = rt * 32 + tid;
+    int dn = s - r.dst;
+    if (dn < 0) dn += cap;
+    ynew = dn < r.n;
+    yv = ynew ? dsy[r.first + (long long)dn * r.step] : dv.y[s];
+  }
+  u16x8 v[PER_T];
+  bool isnew[PER_T], valid[PER_T];
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int row = g + NG * j, s = rt * 32 + row;
+    int dn = s - r.dst;
+    if (dn < 0) dn += cap;
+    isnew[j] = dn < r.n;
+    int dw = s - r.start;
+    if (dw < 0) dw += cap;
+    valid[j] = dw < r.B;
+    const uint16_t* src = isnew[j] ? dsX + (size_t)(r.first + (long long)dn * r.step) * FP : dv.X + (size_t)s * FP;
+    v[j] = *(const u16x8*)(src + cg * 8);
+  }
+  float sm[8], sq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sm[e] = sq[e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int row = g + NG * j, s = rt * 32 + row;
+    *(u16x8*)(lf + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+    if (isnew[j]) *(u16x8*)(X + (size_t)s * FP + cg * 8) = v[j];  // the ring keeps the new row
+    if (valid[j]) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = bf2f(v[j][e]);
+        sm[e] += x;
+        sq[e] += x * x;
+      }
+    }
+  }
+  if (tid < 32) {
+    ((int*)(lf + 32 * FP * 2 + 8192 + 2048))[tid] = yv;  // fwd_body's label slots
+    if (ynew) Y[rt * 32 + tid] = yv;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    scratch[(g * CPR + cg) * 16 + e] = sm[e];
+    scratch[(g * CPR + cg) * 16 + 8 + e] = sq[e];
+  }
+  __syncthreads();
+  if (tid < CPR) {
+    float a[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) a[e] = 0.f;
+    for (int gg = 0; gg < NG; ++gg)  // fixed order
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a[e] += scratch[(gg * CPR + tid) * 16 + e];
+    // 8 features x (sum, sum of squares) = 64 contiguous bytes of spart[wg][f][2]
+    const auto rs = rsrc_of(spart_wg, (unsigned)(FP * 2 * 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 o = f32x4{a[2 * q], a[8 + 2 * q], a[2 * q + 1], a[8 + 2 * q + 1]};
+      st_h_b128<S>(rs, (unsigned)((tid * 8 + 2 * q) * 2 * 4), __builtin_bit_cast(u16x8, o));
+    }
+  }
+}
+
+// Phase I, slice role: the window statistics of features [fs, fs + 32) from the
+// row workgroups' partials, then x0 = w_old * std (Spark standardisation), the
+// solver vectors and the first trial point's fragments (as prep_epilogue).
+template <int FP, int KP, int S>
+__device__ __forceinline__ void lane_prep(char* lb, const SolverCfg& cfg, const SolveDev& dv, const float* spart,
+                                          int ntr, int B, int wg, float wo_pre, float b_pre) {
+  constexpr int FPI = FP > 256 ? FP : 256;
+  const int tid = threadIdx.x, fl = tid & 31, grp = tid >> 5, fs = wg * 32, K = cfg.K;
+  double* red = (double*)lb;                  // [8 groups][32][2]
+  float* sdl = (float*)(red + 8 * 32 * 2);    // [32]
+  float* ivl = sdl + 32;                      // [32]
+  unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);  // [2][512] (bwd_body's staging)
+  double s = 0.0, q = 0.0;
+  for (int gg = grp; gg < ntr; gg += 8) {
+    const double pv = ld_h<S>((const double*)(spart + ((size_t)gg * FP + fs + fl) * 2));
+    const float2 u = __builtin_bit_cast(float2, pv);
+    s += (double)u.x;
+    q += (double)u.y;
+  }
+  red[(grp * 32 + fl) * 2] = s;
+  red[(grp * 32 + fl) * 2 + 1] = q;
+  if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+  if (tid < 32) {
+    double a = 0.0, b = 0.0;
+    for (int gg = 0; gg < 8; ++gg) {
+      a += red[(gg * 32 + tid) * 2];
+      b += red[(gg * 32 + tid) * 2 + 1];
+    }
+    const int f = fs + tid;
+    const double n = (double)B;
+    double sd = 0.0;
+    if (f < cfg.F && n > 1.0) {
+      const double mean = a / n;
+      const double var = (b - n * mean * mean) / (n - 1.0);
+      sd = var > 0.0 ? sqrt(var) : 0.0;
+    }
+    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
+    sdl[tid] = sdf;
+    ivl[tid] = inv;
+    dv.std_[f] = sdf;
+    dv.inv_std[f] = inv;
+  }
+  __syncthreads();
+  {  // element (c = tid / 32, feature fs + fl): x0, d, g_c, wfix, trial fragment
+    const int c = grp;
+    if (c < KP) {
+      const int f = fs + fl, pi = c * FPI + f;
+      const float xv = wo_pre * sdl[fl];
+      dv.x[pi] = xv;
+      dv.d[pi] = 0.f;
+      dv.g_c[pi] = 0.f;
+      const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo_pre;
+      dv.wfix[pi] = fix;
+      unsigned short h, l;
+      split_bf16(xv * ivl[fl] + fix, h, l);
+      const int o = (fl >> 3) * 128 + c * 8 + (fl & 7);
+      frl[o] = h;
+      frl[512 + o] = l;
+    }
+  }
+  if (wg == 0 && tid < 16) {  // intercepts: x0 = the pulled intercepts (not standardised)
+    const int pi = KP * FPI + tid;
+    dv.x[pi] = b_pre;
+    dv.d[pi] = 0.f;
+    dv.g_c[pi] = 0.f;
+    st_h<S>(dv.b_eff + tid, b_pre);
+  }
+  (void)K;
+  __syncthreads();
+  if (tid < 128) {  // this slice of the trial fragments: 16-B hand-off stores (wave 0 hi, wave 1 lo)
+    const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
+    const u16x8 vv = *(const u16x8*)(frl + tid * 8);
+    if (tid < 64)
+      st_h_b128<S>(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), vv);
+    else
+      st_h_b128<S>(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), vv);
+  }
+}
+
+// The BSP update of one slice by the last lane to finish it: w += lr * (sum of
+// the lanes' deltas, lane order) and the server's evaluation fragments, or the
+// plain sum into dsum (multi-rank).  A lane whose solve reported a timed-out
+// wait (sticky error word) contributes nothing.
+template <int FP>
+__device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a,
+                                                 int wg, int NS) {
+  const int tid = threadIdx.x, K = cfg.K, L = a.L;
+  unsigned ok = 0;
+  for (int l = 0; l < L; ++l) ok |= (xload(lanes[l].dv.xch + kXchErr) == 0ull ? 1u : 0u) << l;
+  if (wg < NS) {
+    const int c = tid >> 5, f = wg * 32 + (tid & 31);
+    if (c < K) {
+      const size_t e = (size_t)c * FP + f;
+      float sum = 0.f;
+      for (int l = 0; l < L; ++l)
+        if (ok >> l & 1u) sum += ld_sc1(lanes[l].dv.delta + e);
+      if (a.dsum) {
+        a.dsum[e] = sum;
+      } else {
+        const float nw = a.w[e] + a.lr * sum;
+        a.w[e] = nw;
+        write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
+      }
+    }
+  } else if (tid < K) {  // intercepts
+    const size_t e = (size_t)K * FP + tid;
+    float sum = 0.f;
+    for (int l = 0; l < L; ++l)
+      if (ok >> l & 1u) sum += ld_sc1(lanes[l].dv.delta + e);
+    if (a.dsum) {
+      a.dsum[e] = sum;
+    } else {
+      const float nw = a.w[e] + a.lr * sum;
+      a.w[e] = nw;
+      a.sb[a.scoff + tid] = nw;
+    }
+  }
+}
+
+// Arrive on slice `idx`'s lane counter (every store of this workgroup drained
+// first); true for the last lane, which resets the counter for the next launch.
+__device__ __forceinline__ bool lane_arrive(unsigned* arrive, int idx, int L, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(arrive + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == (unsigned)L - 1u;
+    if (last) __hip_atomic_store(arrive + idx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+template <int FP, int KP, int S>
+__global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const LaneDev* __restrict__ lanes,
+                                                          LanesArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = (int)blockIdx.x, tid = threadIdx.x, L = a.L;
+  const int x = b & 7, i = b >> 3;
+  if (b >= 8 * kLaneWg || x >= L) {  // a rider: the previous round's evaluation
+    const int rid = b < 8 * kLaneWg ? i * (8 - L) + (x - L) : kLaneWg * (8 - L) + (b - 8 * kLaneWg);
+    eval_multi_body<FP>(lds, a.ev, rid, a.nride);
+    return;
+  }
+  const int l = x, wg = i;
+  constexpr int NS = FP / 32;
+  const LaneRound rr = pick(a.r, l);
+  const SolveParams win{rr.B, rr.start, 0, 0};
+  const WinTiles wt(win.start, win.B, cfg.cap);
+  const int ntr = wt.nt < wt.T ? wt.nt : wt.T;  // row workgroups (ring tiles of the window)
+  const int G = ntr > NS ? ntr : NS;
+  if (wg >= G) return;
+  SolveDev dv = lanes[l].dv;
+  dv.out_hi = lanes[l].ohi[a.par];
+  dv.out_lo = lanes[l].olo[a.par];
+  dv.b_fin = lanes[l].ob[a.par];
+  dv.loss = lanes[l].loss2 + a.par;
+  dv.w_old = a.w;
+  dv.w_new = nullptr;
+  dv.ap_w = nullptr;
+  dv.spin_max = a.spin_max;
+  char* lf = lds;                          // row role: the resident tile + forward scratch
+  char* lb = lds + persist_fwd_bytes(FP);  // slice role: bwd_body's region
+  float* lsy = (float*)(lb + (kBwdLdsBytes + 15) / 16 * 16);  // curvature pairs (phase I: scratch)
+  unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);
+  Ctrl* cl = (Ctrl*)(frl + 1024);  // bwd_body's controller copy (persists across slots)
+  int* flag = (int*)(lsy + 8192);
+  const unsigned run = *dv.prm_count;
+  unsigned long long* xch = dv.xch;
+  unsigned long long* bar = xch + kXchGen + (run & 1u);
+  unsigned long long* err = xch + kXchErr;
+  const int spin = spin_limit(dv);
+  unsigned long long nb = 0;
+  auto barrier = [&]() {
+    ++nb;
+    if constexpr (S == 2)
+      x_barrier(xch + kXchFlags, wg, G, ((unsigned long long)run << 16) | nb, err, spin);
+    else
+      p_barrier(bar, (unsigned long long)G * nb, err, spin);
+  };
+  const bool row = wg < ntr, owner = wg < NS;
+  const int K = cfg.K, FPr = FP;
+  // the pulled weights of this slice, fetched first (their latency overlaps the staging)
+  float wo_pre = 0.f, b_pre = 0.f;
+  if (owner) {
+    const int c = tid >> 5, f = wg * 32 + (tid & 31);
+    if (c < K && f < cfg.F) wo_pre = a.w[(size_t)c * FPr + f];
+    if (wg == 0 && tid < K) b_pre = a.w[(size_t)K * FPr + tid];
+  }
+  if (wg == 0 && tid == 0) {
+    xstore(err, 0ull);  // this round's sticky error word (set by any timed-out wait below)
+    if constexpr (S == 1) xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counter
+  }
+  // ---- phase I: stage + ingest + window statistics, then x0 / first trial point ----
+  if (row) {
+    const int rt = wt.ring_tile(wg);
+    lane_stage_stats<FP, S>(lf, lsy, cfg, dv, rr, a.dsX, a.dsy, rt, lanes[l].spart + (size_t)wg * FP * 2);
+  }
+  barrier();
+  if (owner) {
+    lane_prep<FP, KP, S>(lb, cfg, dv, lanes[l].spart, ntr, win.B, wg, wo_pre, b_pre);
+    if (tid == 0) ctrl_init(*cl);
+  }
+  barrier();
+  // ---- slots (as solve_persist_kernel) ----
+  int phase = kPhInit;
+  for (int slot = 0; slot < cfg.nslots; ++slot) {
+    if (phase == kPhDone) break;  // uniform: every workgroup holds the same phase
+    if (row) {
+      constexpr int NT = FP / 64;
+      f32x4 acc[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
+      fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
+      store_gpf<FP, S == 1>(dv, wg, G, acc);
+    }
+    barrier();
+    if (owner) bwd_body<FP, KP, S>(cfg, win, lanes[l].ctrl, slot, dv, G, lb, wg, NS);
+    if (wg == 0 && tid == 0) st_h64<S>(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
+    barrier();
+    phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
+  }
+  if (!owner) return;
+  // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
+  {
+    FinIn<KP> in;
+    const int f = wg * 32 + tid;
+    if (tid < 32) {
+      in.load_f(cfg, dv, f);
+      finalize_feature<KP>(cfg, dv, f, in, /*sc1_delta=*/true);
+    }
+  }
+  if (wg == 0) {
+    __syncthreads();  // (the intercept entries of x were written by this workgroup's threads)
+    if (tid == 0) {
+      FinScal sc;
+      sc.load(cfg, cl, dv);
+      sc.store(cfg, dv, /*sc1_delta=*/true, /*clear_err=*/false);
+    }
+    constexpr int CW = sizeof(Ctrl) / 8;
+    for (int k = tid; k < CW; k += 256) ((unsigned long long*)lanes[l].ctrl)[k] = ((const unsigned long long*)cl)[k];
+  }
+  // ---- the BSP update: the last lane to finish a slice applies the sum ----
+  if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg, NS);
+  if (wg == 0 && lane_arrive(a.arrive, NS, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, NS, NS);
+}
+
+__global__ void xcc_probe_kernel(int* ids, int n) {
+  if (threadIdx.x == 0 && (int)blockIdx.x < n)
+    ids[blockIdx.x] = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
+}
+
+template <int FP, int KP, int S>
+void set_lanes_attr() {
+  (void)hipFuncSetAttribute((const void*)lanes_round_kernel<FP, KP, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lanes_lds_bytes(FP));
+}
+
+template <int FP, int KP, int S>
+void launch_fks(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a, hipStream_t s) {
+  static const bool prepared = (set_lanes_attr<FP, KP, S>(), true);
+  (void)prepared;
+  const int grid = lanes_grid(a.L, a.nride);
+  lanes_round_kernel<FP, KP, S><<<grid, 256, lanes_lds_bytes(FP), s>>>(cfg, lanes, a);
+}
+
+template <int FP, int KP>
+void launch_fk(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a, int S, hipStream_t s) {
+  if (S == 2)
+    launch_fks<FP, KP, 2>(cfg, lanes, a, s);
+  else
+    launch_fks<FP, KP, 1>(cfg, lanes, a, s);
+}
+
+template <int FP>
+void launch_f(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a, int S, hipStream_t s) {
+  const int KP = padded_classes(cfg.K);
+  if (KP <= 2)
+    launch_fk<FP, 2>(cfg, lanes, a, S, s);
+  else if (KP <= 4)
+    launch_fk<FP, 4>(cfg, lanes, a, S, s);
+  else
+    launch_fk<FP, 8>(cfg, lanes, a, S, s);
+}
+
+}  // namespace
+
+void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const LanesArgs& a, int S, hipStream_t s) {
+  switch (cfg.Fp) {
+    case 128: launch_f<128>(cfg, lanes_dev, a, S, s); break;
+    case 256: launch_f<256>(cfg, lanes_dev, a, S, s); break;
+    case 512: launch_f<512>(cfg, lanes_dev, a, S, s); break;
+    case 1024: launch_f<1024>(cfg, lanes_dev, a, S, s); break;
+    default: break;
+  }
+}
+
+void launch_xcc_probe(int* ids, int n, hipStream_t s) { xcc_probe_kernel<<<n, 64, 0, s>>>(ids, n); }
+
+}  // namespace psx

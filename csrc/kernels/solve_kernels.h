@@ -53,6 +53,11 @@ struct SolveDev {
   float* ap_b;
   float ap_lr;
   int ap_coff;
+  // pinned host word (nullptr: none): a solve whose cross-workgroup wait timed
+  // out stores ((run + 1) << 8 | code) there, so host loops notice without a sync
+  unsigned long long* err_host;
+  int spin_max;  // cross-workgroup wait budget in polls (0: 2^22)
+  int pad_sd;
 };
 
 // Server update fused into a solve (see SolveDev::ap_w).

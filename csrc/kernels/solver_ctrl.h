@@ -33,6 +33,10 @@
 namespace psx {
 
 constexpr int kMaxHist = 16;
+// Evaluation slots per solve are < kMaxSlots: the persistent solve's all-gather
+// tags (run * kMaxSlots + slot + 1) and barrier words (run << 16 | n) must not
+// repeat between consecutive solves.
+constexpr int kMaxSlots = 64;
 
 // Workspace of the compact L-BFGS algebra.  On the device it lives in LDS (a
 // stack array would be scratch memory: each access an L1/L2 round trip for

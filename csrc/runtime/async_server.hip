@@ -300,7 +300,7 @@ void AsyncServer::apply_and_log(const CtrlToken& t) {
     else
       launch_wide_eval(cfg_.K, cfg_.KP, cfg_.Fw, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, cfg_.w,
                        nullptr, nullptr, cfg_.acc, cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, stream_);
-    api().sink_submit((void*)cfg_.sink, slot, seq, 1, epoch_ms(), -1, v, 0);
+    api().sink_submit((void*)cfg_.sink, slot, seq, 1, -1, -1, v, 0);  // stamped when the evaluation lands
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("AsyncServer launch: ") + hipGetErrorString(e));

@@ -173,7 +173,7 @@ int64_t BspLoop::run(int64_t rounds, int64_t r0, hipStream_t stream) {
       pend_w_ = BspRow{};
       pend_s_ = BspRow{};
     }
-    const int64_t ts_w = (int64_t)epoch_ms();
+    const int64_t ts_w = -1;  // the sink stamps the row when its evaluation lands
     if (comm_) {  // the round's deltas summed over the ranks (xGMI), then the update
       comm_->all_reduce(cfg_.delta, cfg_.delta, (size_t)P, RcclComm::kF32, stream);
       launch_server_apply(cfg_.K, cfg_.F, cfg_.Fp, cfg_.w, cfg_.delta, cfg_.lr, cfg_.shi, cfg_.slo, cfg_.sb, stream,
@@ -182,7 +182,7 @@ int64_t BspLoop::run(int64_t rounds, int64_t r0, hipStream_t stream) {
     }
     if (sink) {
       pend_w_ = BspRow{r, seen, ts_w};
-      if (cfg_.log_server) pend_s_ = BspRow{r, 0, (int64_t)epoch_ms()};
+      if (cfg_.log_server) pend_s_ = BspRow{r, 0, -1};
     }
     if (cfg_.tracker) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
   }

@@ -1,0 +1,156 @@
+// Native BSP round loop of up to 8 in-process workers sharing one MI355X
+// ("lanes", csrc/kernels/lanes_kernels.h): ONE launch per round.
+//
+// Reference: the worker JVM hosts every logical worker (BaseKafkaApp.java:25,70,
+// WorkerApp.java:31-43); under sequential consistency the server answers once
+// every worker's gradient of the round arrived (ServerProcessor.java:111-120)
+// with w += (1/N) delta_k applied per gradient (ServerProcessor.java:148-151).
+//
+// Per round, from C++ with no host synchronisation:
+//   * every lane's producer delivers its due rows (per-round rows or the
+//     reference producer clock) into its adaptive window (SlidingWindow, host
+//     runtime C ABI); the rows themselves are copied into the lane's HBM ring by
+//     the round kernel (a delivery that wraps its shard's epoch: the first part
+//     by a ring-ingest launch);
+//   * one lanes_round launch: every lane's solve on its own XCD, the cross-lane
+//     update (the last lane to finish a slice applies the lane sum), and rider
+//     workgroups evaluating the previous round's local + global models into the
+//     metrics sink's pinned slots (worker rows, server row);
+//   * multi-rank (comm != nullptr): the kernel writes the lane sum instead; the
+//     rank reduces it to the server rank over RCCL and receives the new weights
+//     by broadcast (BASELINE config 2/3 topology); on the server rank the update
+//     and its fragments follow the reduce;
+//   * the vector-clock tracker advances one round; the device error word (pinned)
+//     is polled: a timed-out cross-workgroup wait surfaces as an exception naming
+//     the round.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../comm/rccl_comm.h"
+#include "../host/capi.h"
+#include "../kernels/lanes_kernels.h"
+
+namespace psx {
+
+struct LanesLoopCfg {
+  SolverCfg scfg;  // K, F, Fp, P, cap, iters, hist, ls_max, mode, center, zero_const, nslots, gd_lr, tol
+  // producer: worker k of N reads dataset rows k, k + N, ... (`epochs` passes)
+  const uint16_t* dsX = nullptr;
+  const int32_t* dsy = nullptr;
+  int64_t ds_rows = 0;
+  int N = 1;              // logical workers in the whole job
+  int per_iter_rows = 0;  // > 0: rows per round; 0: the producer clock p_ms
+  double p_ms = 0.0;
+  int64_t epochs = 1;
+  double t0_ms = 0.0;
+  // lanes of this process
+  int L = 0;
+  std::vector<int> k;             // worker ids
+  std::vector<uintptr_t> X, XT, y;  // rings [cap][Fp] bf16 (+ optional feature-major copy, kept in step), labels
+  std::vector<uintptr_t> window;  // SlidingWindow*
+  // server state (replica): w [P], its evaluation fragments (two buffers, columns scoff..)
+  float* w = nullptr;
+  float lr = 1.f;
+  uint16_t* shi[2] = {nullptr, nullptr};
+  uint16_t* slo[2] = {nullptr, nullptr};
+  float* sb[2] = {nullptr, nullptr};
+  int scoff = 0;
+  // evaluation
+  const uint16_t* Xt = nullptr;
+  const int32_t* yt = nullptr;
+  int T = 0;
+  uintptr_t sink = 0;       // MetricsSink* (0: no rows)
+  bool log_server = true;   // server rows on this rank
+  bool log_workers = true;  // worker rows on this rank
+  uintptr_t tracker = 0;    // VectorClockTracker* (0: none)
+  uintptr_t api = 0;        // HostApi*
+  int server_rank = 0;      // multi-rank: the rank that applies the update
+};
+
+class LanesLoop {
+ public:
+  // comm: RCCL communicator of a multi-rank job (nullptr: one rank).  A rank with
+  // L == 0 is a dedicated server rank.
+  LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm);
+  ~LanesLoop();
+  LanesLoop(const LanesLoop&) = delete;
+  LanesLoop& operator=(const LanesLoop&) = delete;
+  // Run `rounds` rounds from round r0; returns the rounds run (fewer when every
+  // lane's stream is exhausted and its window empty).  max_wait_s: how long a
+  // round may wait for a lane's first rows.
+  int64_t run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s = 600.0);
+  // Evaluate the last round's rows (one launch of riders only).
+  void flush(hipStream_t stream);
+  void set_sink(uintptr_t sink) { cfg_.sink = sink; }
+  void set_lr(float lr) { cfg_.lr = lr; }
+  int64_t next_local(int lane) const { return next_local_.at(lane); }
+  void set_next_local(int lane, int64_t v) { next_local_.at(lane) = v; }
+  bool exhausted(int lane) const { return next_local_[lane] >= local_total_[lane] * cfg_.epochs; }
+  bool all_exhausted() const;
+  int hand_off_scope() const { return S_; }  // 2: one-XCD hand-offs, 1: sc1 (placement check failed)
+  double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
+  int64_t rounds_run() const { return rounds_run_; }
+  // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
+  std::vector<int> stats(int lane, hipStream_t stream) const;
+  float loss(int lane, hipStream_t stream) const;
+  // the lane's last delta [P] (device pointer)
+  uintptr_t delta_ptr(int lane) const;
+  // stream-ordered copies of lane `lane`'s last loss (1 float) and delta (P floats);
+  // a null destination is skipped
+  void copy_out(int lane, uintptr_t loss_dst, uintptr_t delta_dst, hipStream_t stream) const;
+  // fault injection (tests): round r runs with a wait budget of `spin` polls
+  void inject_spin_timeout(int64_t round, int spin) {
+    inject_round_ = round;
+    inject_spin_ = spin;
+  }
+  // Raise if a lane's solve reported a timed-out cross-workgroup wait (the pinned
+  // error words; no synchronisation: call after one to cover every enqueued round).
+  void poll_errors() { check_errors(-1); }
+  // placement probe: blockIdx % 8 == XCC_ID for every workgroup of a large launch
+  static bool probe_placement(hipStream_t stream);
+
+ private:
+  struct Pending {  // deferred evaluation rows of the previous round
+    bool valid = false;
+    int64_t vc = 0;
+    int par = 0;
+    std::vector<int64_t> nseen;
+  };
+  const HostApi& api() const { return *api_; }
+  void check(int64_t rc, const char* what) const;
+  int64_t poll(int lane, double now_ms, LaneRound* r, hipStream_t stream);
+  void fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slots, std::vector<uint64_t>* seqs,
+                 std::vector<int>* kinds);
+  void submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
+                   const std::vector<int>& kinds);
+  void check_errors(int64_t round);
+  int rider_count(int nmodels, int L) const;
+
+  LanesLoopCfg cfg_;
+  RcclComm* comm_;
+  const HostApi* api_;
+  int S_ = 2;
+  int P_ = 0;
+  std::vector<int64_t> local_total_, next_local_;
+  std::vector<double> times_;
+  void* ws_ = nullptr;  // device workspace of every lane + shared buffers
+  LaneDev* lanes_dev_ = nullptr;
+  std::vector<LaneDev> lanes_;
+  unsigned* arrive_ = nullptr;
+  int* acc_ = nullptr;
+  unsigned* ticket_ = nullptr;
+  float* dsum_ = nullptr;
+  unsigned long long* err_host_ = nullptr;  // pinned [kMaxLanes]
+  Pending pend_;
+  int last_par_ = 0;  // parity of the last round run
+  int64_t inject_round_ = -1;
+  int inject_spin_ = 0;
+  int64_t rounds_run_ = 0;
+  double host_ns_ = 0.0;
+};
+
+}  // namespace psx

@@ -1,0 +1,471 @@
+// Native multi-lane BSP round loop (see lanes_loop.h).
+#include "lanes_loop.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "../kernels/common.h"
+#include "../kernels/lr_kernels.h"
+#include "../solver/solver.h"
+
+namespace psx {
+
+namespace {
+double epoch_ms() {
+  using namespace std::chrono;
+  return (double)duration_cast<microseconds>(system_clock::now().time_since_epoch()).count() / 1000.0;
+}
+int64_t steady_ns() {
+  using namespace std::chrono;
+  return duration_cast<nanoseconds>(steady_clock::now().time_since_epoch()).count();
+}
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+bool LanesLoop::probe_placement(hipStream_t stream) {
+  static int cached = -1;  // one probe per process
+  if (const char* e = std::getenv("PSX_FAKE_XCD_MISMATCH"))
+    if (e[0] == '1') return false;
+  if (cached >= 0) return cached == 1;
+  constexpr int n = 2048;
+  int* ids = nullptr;
+  hip_check(hipMalloc(&ids, n * sizeof(int)), "hipMalloc(xcc probe)");
+  launch_xcc_probe(ids, n, stream);
+  hip_check(hipGetLastError(), "xcc probe launch");
+  std::vector<int> h(n);
+  hip_check(hipMemcpyAsync(h.data(), ids, n * sizeof(int), hipMemcpyDeviceToHost, stream), "xcc probe copy");
+  hip_check(hipStreamSynchronize(stream), "xcc probe sync");
+  (void)hipFree(ids);
+  bool ok = true;
+  for (int b = 0; b < n; ++b) ok &= h[b] == (b & 7);
+  cached = ok ? 1 : 0;
+  return ok;
+}
+
+LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
+    : cfg_(cfg), comm_(comm), api_(reinterpret_cast<const HostApi*>(cfg.api)) {
+  const SolverCfg& s = cfg_.scfg;
+  if (!api_ || api_->version != kHostApiVersion) throw std::invalid_argument("LanesLoop: host runtime API mismatch");
+  if (cfg_.L < 0 || cfg_.L > kMaxLanes) throw std::invalid_argument("LanesLoop: 0..8 lanes per process");
+  if (cfg_.L == 0 && !comm_) throw std::invalid_argument("LanesLoop: a rank without lanes needs a communicator");
+  if (!lanes_supported(s.Fp, s.K, s.cap)) throw std::invalid_argument("LanesLoop: unsupported model / ring shape");
+  if (s.P != s.K * s.Fp + s.K) throw std::invalid_argument("LanesLoop: P mismatch");
+  if (s.nslots < 1 || s.nslots >= kMaxSlots || s.hist < 1 || s.hist > kMaxHist)
+    throw std::invalid_argument("LanesLoop: slots / history out of range");
+  if ((int)cfg_.k.size() != cfg_.L || (int)cfg_.X.size() != cfg_.L || (int)cfg_.y.size() != cfg_.L ||
+      (int)cfg_.window.size() != cfg_.L)
+    throw std::invalid_argument("LanesLoop: one worker id / ring / window per lane");
+  if (cfg_.XT.empty()) cfg_.XT.assign(cfg_.L, 0);
+  if (cfg_.L > 0 && (!cfg_.dsX || !cfg_.dsy || cfg_.ds_rows <= 0 || cfg_.N < cfg_.L))
+    throw std::invalid_argument("LanesLoop: bad dataset / worker count");
+  if (cfg_.per_iter_rows <= 0 && !(cfg_.p_ms > 0.0) && cfg_.L > 0)
+    throw std::invalid_argument("LanesLoop: need rows per round or a producer period");
+  if (!cfg_.w) throw std::invalid_argument("LanesLoop: no server weights");
+  const bool evaluates = cfg_.sink && (cfg_.log_server || cfg_.log_workers);
+  if (evaluates && (!cfg_.Xt || !cfg_.yt || cfg_.T <= 0)) throw std::invalid_argument("LanesLoop: no test set");
+  if (cfg_.log_server && evaluates && (!cfg_.shi[0] || !cfg_.shi[1] || !cfg_.slo[0] || !cfg_.slo[1] || !cfg_.sb[0] ||
+                                       !cfg_.sb[1] || cfg_.scoff < 0 || cfg_.scoff + s.K > 16))
+    throw std::invalid_argument("LanesLoop: server evaluation fragments");
+  if (comm_ && comm_->rank() == cfg_.server_rank && (!cfg_.shi[0] || !cfg_.shi[1]))
+    throw std::invalid_argument("LanesLoop: the server rank needs its fragments");
+  P_ = s.P;
+  for (int l = 0; l < cfg_.L; ++l) {
+    const int k = cfg_.k[l];
+    if (k < 0 || k >= cfg_.N || !cfg_.X[l] || !cfg_.y[l] || !cfg_.window[l])
+      throw std::invalid_argument("LanesLoop: bad lane " + std::to_string(l));
+    const int64_t tot = cfg_.ds_rows > k ? (cfg_.ds_rows - k + cfg_.N - 1) / cfg_.N : 0;
+    if (tot == 0) throw std::invalid_argument("LanesLoop: worker " + std::to_string(k) + " has no rows");
+    local_total_.push_back(tot);
+    next_local_.push_back(0);
+  }
+  prepare_kernels();
+  hipStream_t s0 = nullptr;
+  S_ = probe_placement(s0) ? 2 : 1;
+
+  // ---- device workspace: per lane + shared ----
+  const int KP = padded_classes(s.K), FPI = padded_stride(s.Fp), PI = KP * FPI + 16, FP = s.Fp;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  struct Offs {
+    size_t x, d, gc, wfix, std_, istd, beff, whi, wlo, part, xch, gpf, spart, delta, ohi[2], olo[2], ob[2], loss2,
+        stats, cnt, ctrl;
+  };
+  std::vector<Offs> o(cfg_.L);
+  for (int l = 0; l < cfg_.L; ++l) {
+    Offs& q = o[l];
+    q.x = take(PI * 4);
+    q.d = take(PI * 4);
+    q.gc = take(PI * 4);
+    q.wfix = take(PI * 4);
+    q.std_ = take(FPI * 4);
+    q.istd = take(FPI * 4);
+    q.beff = take(16 * 4);
+    q.whi = take(16 * FP * 2);
+    q.wlo = take(16 * FP * 2);
+    q.part = take(kLaneWg * 32 * 4);
+    q.xch = take((size_t)xch_words() * 8);
+    q.gpf = take((size_t)kLaneWg * KP * FP * 4);
+    q.spart = take((size_t)kLaneWg * FP * 2 * 4);
+    q.delta = take((size_t)P_ * 4);
+    for (int p = 0; p < 2; ++p) {
+      q.ohi[p] = take(16 * FP * 2);
+      q.olo[p] = take(16 * FP * 2);
+      q.ob[p] = take(16 * 4);
+    }
+    q.loss2 = take(2 * 4);
+    q.stats = take(8 * 4);
+    q.cnt = take(16);
+    q.ctrl = take(sizeof(Ctrl));
+  }
+  const size_t o_tab = take(sizeof(LaneDev) * (cfg_.L > 0 ? cfg_.L : 1));
+  const size_t o_arr = take((FP / 32 + 1) * sizeof(unsigned));
+  const size_t o_acc = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
+  const size_t o_tic = take(8 * sizeof(unsigned));
+  const size_t o_dsum = take((size_t)P_ * 4);
+  hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
+  hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
+  char* b = static_cast<char*>(ws_);
+  hip_check(hipHostMalloc((void**)&err_host_, kMaxLanes * sizeof(unsigned long long),
+                          hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(error words)");
+  std::memset(err_host_, 0, kMaxLanes * sizeof(unsigned long long));
+  lanes_.resize(cfg_.L);
+  for (int l = 0; l < cfg_.L; ++l) {
+    const Offs& q = o[l];
+    LaneDev& ld = lanes_[l];
+    std::memset(&ld, 0, sizeof(ld));
+    SolveDev& dv = ld.dv;
+    dv.X = reinterpret_cast<const uint16_t*>(cfg_.X[l]);
+    dv.XT = reinterpret_cast<const uint16_t*>(cfg_.XT[l]);
+    dv.y = reinterpret_cast<const int32_t*>(cfg_.y[l]);
+    dv.w_old = cfg_.w;
+    dv.x = reinterpret_cast<float*>(b + q.x);
+    dv.d = reinterpret_cast<float*>(b + q.d);
+    dv.g_c = reinterpret_cast<float*>(b + q.gc);
+    dv.wfix = reinterpret_cast<float*>(b + q.wfix);
+    dv.std_ = reinterpret_cast<float*>(b + q.std_);
+    dv.inv_std = reinterpret_cast<float*>(b + q.istd);
+    dv.b_eff = reinterpret_cast<float*>(b + q.beff);
+    dv.whi = reinterpret_cast<uint16_t*>(b + q.whi);
+    dv.wlo = reinterpret_cast<uint16_t*>(b + q.wlo);
+    dv.part = reinterpret_cast<float*>(b + q.part);
+    dv.xch = reinterpret_cast<unsigned long long*>(b + q.xch);
+    dv.gpf = reinterpret_cast<float*>(b + q.gpf);
+    dv.delta = reinterpret_cast<float*>(b + q.delta);
+    dv.out_hi = reinterpret_cast<uint16_t*>(b + q.ohi[0]);
+    dv.out_lo = reinterpret_cast<uint16_t*>(b + q.olo[0]);
+    dv.b_fin = reinterpret_cast<float*>(b + q.ob[0]);
+    dv.loss = reinterpret_cast<float*>(b + q.loss2);
+    dv.stats = reinterpret_cast<int*>(b + q.stats);
+    dv.prm_count = reinterpret_cast<unsigned*>(b + q.cnt);
+    dv.KP = KP;
+    dv.FPI = FPI;
+    dv.PI = PI;
+    dv.err_host = err_host_ + l;
+    ld.spart = reinterpret_cast<float*>(b + q.spart);
+    for (int p = 0; p < 2; ++p) {
+      ld.ohi[p] = reinterpret_cast<uint16_t*>(b + q.ohi[p]);
+      ld.olo[p] = reinterpret_cast<uint16_t*>(b + q.olo[p]);
+      ld.ob[p] = reinterpret_cast<float*>(b + q.ob[p]);
+    }
+    ld.loss2 = reinterpret_cast<float*>(b + q.loss2);
+    ld.ctrl = reinterpret_cast<Ctrl*>(b + q.ctrl);
+  }
+  lanes_dev_ = reinterpret_cast<LaneDev*>(b + o_tab);
+  arrive_ = reinterpret_cast<unsigned*>(b + o_arr);
+  acc_ = reinterpret_cast<int*>(b + o_acc);
+  ticket_ = reinterpret_cast<unsigned*>(b + o_tic);
+  dsum_ = reinterpret_cast<float*>(b + o_dsum);
+  if (cfg_.L > 0)
+    hip_check(hipMemcpy(lanes_dev_, lanes_.data(), sizeof(LaneDev) * cfg_.L, hipMemcpyHostToDevice),
+              "lanes table upload");
+}
+
+LanesLoop::~LanesLoop() {
+  if (ws_) (void)hipFree(ws_);
+  if (err_host_) (void)hipHostFree(err_host_);
+}
+
+void LanesLoop::check(int64_t rc, const char* what) const {
+  if (rc < 0) throw std::runtime_error(std::string("LanesLoop: ") + what + ": " + api().last_error());
+}
+
+bool LanesLoop::all_exhausted() const {
+  for (int l = 0; l < cfg_.L; ++l)
+    if (!exhausted(l)) return false;
+  return true;
+}
+
+// Deliver lane `lane`'s due rows into its window (WorkerSamplingProcessor.java:
+// 50-113 through the host runtime's SlidingWindow); the rows of the last
+// contiguous run go to the round kernel (r->n, dst, first, step), earlier runs
+// (a delivery that wraps the shard's epoch) to a ring-ingest launch.
+int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t stream) {
+  if (exhausted(lane)) return 0;
+  const int k = cfg_.k[lane];
+  const int64_t lt = local_total_[lane];
+  int64_t& nl = next_local_[lane];
+  const int64_t limit = lt * cfg_.epochs - nl;
+  int64_t n;
+  if (cfg_.per_iter_rows > 0) {
+    n = cfg_.per_iter_rows < limit ? cfg_.per_iter_rows : limit;
+    times_.assign((size_t)n, now_ms);
+  } else {
+    const int64_t epoch = nl / lt, cur = nl - epoch * lt;
+    int64_t mx = limit < lt - cur ? limit : lt - cur;
+    if (mx > (int64_t(1) << 22)) mx = int64_t(1) << 22;
+    times_.resize(mx > 0 ? (size_t)mx : 1);
+    n = api().due_rows(k, cfg_.N, cfg_.p_ms, cfg_.ds_rows, cur, now_ms, mx, times_.data());
+    check(n, "due_rows");
+  }
+  if (n <= 0) return 0;
+  const int64_t first = api().window_insert_many(reinterpret_cast<void*>(cfg_.window[lane]), times_.data(), n);
+  check(first, "window insert");
+  const int64_t cap = cfg_.scfg.cap;
+  if (r->n > 0) {  // an earlier delivery of this round still pending for the kernel: launch it now
+    launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]), nullptr,
+                       reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
+    r->n = 0;
+  }
+  const int64_t keep = n < cap ? n : cap, skip = n - keep;
+  int64_t slot = (first + skip) % cap, pos = nl + skip, remaining = keep;
+  while (remaining > 0) {  // split at the shard's epoch boundaries
+    const int64_t cur = pos % lt;
+    const int64_t run = remaining < lt - cur ? remaining : lt - cur;
+    const int64_t src_first = k + cur * (int64_t)cfg_.N;
+    if (run == remaining) {
+      r->first = src_first;
+      r->step = cfg_.N;
+      r->n = (int)run;
+      r->dst = (int)slot;
+    } else {
+      launch_ring_ingest(cfg_.dsX, cfg_.dsy, src_first, cfg_.N, run, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
+                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), slot, cap, cfg_.scfg.Fp, stream);
+    }
+    slot = (slot + run) % cap;
+    pos += run;
+    remaining -= run;
+  }
+  nl += n;
+  return n;
+}
+
+int LanesLoop::rider_count(int nmodels, int L) const {
+  if (nmodels <= 0) return 0;
+  const int nT = (cfg_.T + 31) / 32, items = (nmodels + 1) / 2 * nT;
+  const int slots = lanes_rider_base(L);
+  if (slots > 0) return slots < items ? slots : items;
+  return items < 256 ? items : 256;  // every XCD solves: riders after the lanes
+}
+
+// The previous round's rows as models of one evaluation pass: the lanes' local
+// models (worker rows, LogisticRegressionTaskSpark.java:186), then the global
+// model (server row, ServerProcessor.java:154-165).
+void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slots, std::vector<uint64_t>* seqs,
+                          std::vector<int>* kinds) {
+  std::memset(ev, 0, sizeof(*ev));
+  slots->clear();
+  seqs->clear();
+  kinds->clear();
+  if (!p.valid || !cfg_.sink) return;
+  ev->Xt = cfg_.Xt;
+  ev->yt = cfg_.yt;
+  ev->T = cfg_.T;
+  ev->K = cfg_.scfg.K;
+  ev->acc = acc_;
+  ev->ticket = ticket_;
+  void* sink = reinterpret_cast<void*>(cfg_.sink);
+  auto add = [&](const uint16_t* hi, const uint16_t* lo, const float* bb, int coff, const float* loss, int kind) {
+    uint64_t seq = 0;
+    uintptr_t addr = 0;
+    const int slot = api().sink_acquire(sink, &seq, &addr);
+    check(slot, "metrics sink acquire");
+    EvalModel& m = ev->m[ev->nmodels++];
+    m.hi = hi;
+    m.lo = lo;
+    m.b = bb;
+    m.coff = coff;
+    m.loss = loss;
+    m.slot = reinterpret_cast<char*>(addr);
+    m.seq = seq;
+    slots->push_back(slot);
+    seqs->push_back(seq);
+    kinds->push_back(kind);
+  };
+  if (cfg_.log_workers)
+    for (int l = 0; l < cfg_.L; ++l)
+      add(lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
+  if (cfg_.log_server)
+    add(cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
+  ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);
+}
+
+void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
+                            const std::vector<int>& kinds) {
+  void* sink = reinterpret_cast<void*>(cfg_.sink);
+  // the reference's order: the server row, then the worker rows; timestamps are
+  // taken by the sink when the evaluation lands (ts = -1)
+  for (size_t i = 0; i < slots.size(); ++i)
+    if (kinds[i] == 1) api().sink_submit(sink, slots[i], seqs[i], 1, -1, -1, p.vc, 0);
+  int l = 0;
+  for (size_t i = 0; i < slots.size(); ++i)
+    if (kinds[i] == 0) {
+      api().sink_submit(sink, slots[i], seqs[i], 0, -1, cfg_.k[l], p.vc, p.nseen[l]);
+      ++l;
+    }
+}
+
+void LanesLoop::check_errors(int64_t round) {
+  for (int l = 0; l < cfg_.L; ++l) {
+    const unsigned long long e = __atomic_load_n(err_host_ + l, __ATOMIC_ACQUIRE);
+    if (e) {
+      __atomic_store_n(err_host_ + l, 0ull, __ATOMIC_RELAXED);
+      throw std::runtime_error("LanesLoop: worker " + std::to_string(cfg_.k[l]) +
+                               ": device solver: a cross-workgroup wait timed out (solve " +
+                               std::to_string((long long)(e >> 8) - 1) + ", code " + std::to_string((int)(e & 0xff)) +
+                               ", noticed at round " + std::to_string((long long)round) + ")");
+    }
+  }
+}
+
+int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s) {
+  const int64_t t_begin = steady_ns();
+  const int L = cfg_.L;
+  const int KF = cfg_.scfg.K * cfg_.scfg.Fp;
+  std::vector<int> slots, kinds;
+  std::vector<uint64_t> seqs;
+  const bool is_server = !comm_ || comm_->rank() == cfg_.server_rank;
+  int64_t done = 0;
+  for (; done < rounds; ++done) {
+    const int64_t r = r0 + done;
+    const int par = (int)(r & 1);
+    LanesArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.L = L;
+    a.par = par;
+    // ---- deliveries, then every lane's window (BSP: wait until all have rows) ----
+    std::vector<int64_t> seen(L, 0);
+    const double wait0 = epoch_ms();
+    for (;;) {
+      const double now = epoch_ms() - cfg_.t0_ms;
+      for (int l = 0; l < L; ++l) poll(l, now, &a.r[l], stream);
+      bool ready = true;
+      for (int l = 0; l < L; ++l) {
+        int64_t size = 0, start = 0, sn = 0;
+        check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
+        a.r[l].B = (int)size;
+        a.r[l].start = (int)start;
+        seen[l] = sn;
+        ready &= size > 0;
+      }
+      if (ready) break;
+      for (int l = 0; l < L; ++l)  // a lane with an empty window and nothing left to come: the run ends
+        if (a.r[l].B <= 0 && exhausted(l)) {
+          rounds_run_ += done;
+          host_ns_ += (double)(steady_ns() - t_begin);
+          return done;
+        }
+      if (epoch_ms() - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+    // ---- the round kernel: solves + update + riding evaluation of the last round ----
+    fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
+    a.nride = (int)a.ev.nticket;
+    a.dsX = cfg_.dsX;
+    a.dsy = cfg_.dsy;
+    a.w = cfg_.w;
+    a.lr = cfg_.lr;
+    a.dsum = comm_ ? dsum_ : nullptr;
+    a.shi = cfg_.shi[par];
+    a.slo = cfg_.slo[par];
+    a.sb = cfg_.sb[par];
+    a.scoff = cfg_.scoff;
+    a.arrive = arrive_;
+    a.spin_max = r == inject_round_ ? inject_spin_ : 0;
+    if (L > 0 || a.ev.nmodels > 0) {
+      launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
+      hip_check(hipGetLastError(), "lanes round launch");
+    }
+    if (!slots.empty()) submit_rows(pend_, slots, seqs, kinds);
+    // ---- multi-rank: lane sums -> server (reduce), update, weights -> every rank ----
+    if (comm_) {
+      if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
+      comm_->reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+      if (is_server)
+        launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr, cfg_.shi[par],
+                            cfg_.slo[par], cfg_.sb[par], stream, cfg_.scoff);
+      comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+      hip_check(hipGetLastError(), "server update launch");
+    }
+    (void)KF;
+    // ---- this round's rows are evaluated by the next launch ----
+    last_par_ = par;
+    pend_.valid = cfg_.sink != 0;
+    pend_.vc = r;
+    pend_.par = par;
+    pend_.nseen = seen;
+    if (cfg_.tracker && is_server) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
+    check_errors(r);
+  }
+  rounds_run_ += done;
+  host_ns_ += (double)(steady_ns() - t_begin);
+  return done;
+}
+
+void LanesLoop::flush(hipStream_t stream) {
+  if (!pend_.valid || !cfg_.sink) return;
+  std::vector<int> slots, kinds;
+  std::vector<uint64_t> seqs;
+  LanesArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.L = 0;
+  fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
+  a.ev.nticket = (unsigned)rider_count(a.ev.nmodels, 0);
+  a.nride = (int)a.ev.nticket;
+  a.w = cfg_.w;
+  a.arrive = arrive_;
+  if (a.ev.nmodels > 0) {
+    launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
+    hip_check(hipGetLastError(), "lanes evaluation launch");
+  }
+  submit_rows(pend_, slots, seqs, kinds);
+  pend_ = Pending{};
+}
+
+std::vector<int> LanesLoop::stats(int lane, hipStream_t stream) const {
+  std::vector<int> v(8, 0);
+  hip_check(hipMemcpyAsync(v.data(), lanes_.at(lane).dv.stats, 8 * sizeof(int), hipMemcpyDeviceToHost, stream),
+            "lane stats");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v;
+}
+
+float LanesLoop::loss(int lane, hipStream_t stream) const {
+  float v[2] = {0.f, 0.f};
+  hip_check(hipMemcpyAsync(v, lanes_.at(lane).loss2, 2 * sizeof(float), hipMemcpyDeviceToHost, stream), "lane loss");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v[last_par_];
+}
+
+uintptr_t LanesLoop::delta_ptr(int lane) const { return reinterpret_cast<uintptr_t>(lanes_.at(lane).dv.delta); }
+
+void LanesLoop::copy_out(int lane, uintptr_t loss_dst, uintptr_t delta_dst, hipStream_t stream) const {
+  const LaneDev& ld = lanes_.at(lane);
+  if (loss_dst)
+    hip_check(hipMemcpyAsync(reinterpret_cast<void*>(loss_dst), ld.loss2 + last_par_, sizeof(float),
+                             hipMemcpyDeviceToDevice, stream),
+              "lane loss copy");
+  if (delta_dst)
+    hip_check(hipMemcpyAsync(reinterpret_cast<void*>(delta_dst), ld.dv.delta, (size_t)P_ * sizeof(float),
+                             hipMemcpyDeviceToDevice, stream),
+              "lane delta copy");
+}
+
+}  // namespace psx

@@ -17,7 +17,8 @@ LocalSolver::LocalSolver(const SolverCfg& cfg, const SolverBuffers& buf, int max
   if (cfg.K < 2 || cfg.K > 16) throw std::invalid_argument("num classes (incl. phantom) must be in [2,16]");
   if (cfg.P != cfg.K * cfg.Fp + cfg.K) throw std::invalid_argument("P mismatch");
   if (cfg.hist < 1 || cfg.hist > kMaxHist) throw std::invalid_argument("history must be in [1,16]");
-  if (cfg.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
+  if (cfg.nslots < 1 || cfg.nslots >= kMaxSlots)
+    throw std::invalid_argument("nslots must be in [1, " + std::to_string(kMaxSlots - 1) + "]");
   if (cfg.cap < 32 || cfg.cap % 32 != 0) throw std::invalid_argument("ring capacity must be a positive multiple of 32");
   rows_mode_ = cfg.xf32 || rows_mode_for(cfg.cap);  // fp32 rows: only the row-parallel solver reads them
   if (cfg.xf32 && (!buf.Xf || cfg.Fp > 1024))

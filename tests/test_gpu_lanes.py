@@ -1,0 +1,188 @@
+"""Multi-lane BSP round kernel (csrc/kernels/lanes_kernels.hip, csrc/runtime/lanes_loop.h)
+on one MI355X: every in-process worker's solve on its own XCD, the cross-lane update
+and the riding evaluation in ONE launch per round."""
+import os
+
+import pytest
+import torch
+
+from psx import _native
+from psx.models.logreg import ModelSpec
+from psx.models.reference import local_solve_reference
+from psx.ops.lr import Fragments, SolverOptions, stream_handle
+from psx.runtime.config import PSConfig
+from psx.runtime.engine import LocalEngine
+from psx.utils.data import synth_finefood
+from psx.utils.logsink import LogSink
+
+pytestmark = pytest.mark.gpu
+
+
+def _loop(spec, ks, N, train, test, w, dev, rows=1024, cap=1024, sink=None, lr=None, frags=None, opts=None):
+    """A LanesLoop over worker ids `ks` (of N) with fresh rings / windows."""
+    h, host = _native.hip(), _native.host
+    o = opts or SolverOptions()
+    sc = h.SolverCfg()
+    sc.K, sc.F, sc.Fp, sc.P, sc.cap = spec.K, spec.F, spec.Fp, spec.P, cap
+    sc.iters, sc.hist, sc.ls_max, sc.mode = o.iters, o.hist, o.ls_max, 0
+    sc.center, sc.zero_const, sc.nslots, sc.gd_lr, sc.tol = 1, 1, o.nslots, o.gd_lr, o.tol
+    rings = [(torch.zeros(cap, spec.Fp, dtype=torch.bfloat16, device=dev),
+              torch.zeros(cap, dtype=torch.int32, device=dev)) for _ in ks]
+    wins = [host.SlidingWindow(cap, cap, 0.3, 500, cap) for _ in ks]
+    frags = frags or [Fragments(spec, dev), Fragments(spec, dev)]
+    d = dict(scfg=sc, dsX=train.X.data_ptr(), dsy=train.y.data_ptr(), ds_rows=int(train.rows), N=N,
+             per_iter_rows=rows, k=list(ks), X=[r[0].data_ptr() for r in rings], y=[r[1].data_ptr() for r in rings],
+             window=[wn.handle for wn in wins], w=w.data_ptr(), lr=float(lr if lr is not None else 1.0 / N),
+             shi=[f.hi.data_ptr() for f in frags], slo=[f.lo.data_ptr() for f in frags],
+             sb=[f.b.data_ptr() for f in frags], scoff=0, Xt=test.X.data_ptr(), yt=test.y.data_ptr(), T=test.T,
+             sink=sink.native.handle if sink is not None else 0, api=host.capi())
+    lp = h.LanesLoop(d, None)
+    return lp, (rings, wins, frags)
+
+
+def _data(dev, rows=20000):
+    spec = ModelSpec(1024, 6)
+    train = synth_finefood(rows, seed=0).to(dev)
+    from psx.ops.lr import EvalSet
+
+    te = synth_finefood(4877, seed=1)
+    return spec, train, EvalSet(spec, te.X, te.y, dev)
+
+
+def _deltas(lp, L, spec, dev):
+    out = []
+    for l in range(L):
+        d = torch.empty(spec.P, dtype=torch.float32, device=dev)
+        lp.copy_out(l, 0, d.data_ptr(), stream_handle(dev))
+        out.append(d)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("L", [8, 3])
+def test_lanes_equal_separate_solves_bitwise(cuda, L):
+    """Lane l of an L-lane round == worker l's round run alone on the GPU (bitwise)."""
+    spec, train, ev = _data(cuda)
+    w0 = spec.init("random", seed=3, device=cuda)
+    w = w0.clone()
+    lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda)
+    assert lp.run(1, 0, stream_handle(cuda)) == 1
+    multi = _deltas(lp, L, spec, cuda)
+    for l in range(L):
+        wl = w0.clone()
+        lp1, keep1 = _loop(spec, [l], L, train, ev, wl, cuda)
+        lp1.run(1, 0, stream_handle(cuda))
+        alone = _deltas(lp1, 1, spec, cuda)[0]
+        assert torch.equal(alone, multi[l]), (l, (alone - multi[l]).abs().max().item())
+        assert torch.allclose(wl, w0 + multi[l] / L, atol=1e-6)  # alone: w += (1/N) * delta
+
+
+def test_lanes_solve_matches_reference_and_update(cuda):
+    """One lane's delta against the float64 oracle of the reference solve; the
+    update is w + lr * (sum of the lane deltas)."""
+    spec, train, ev = _data(cuda)
+    L = 4
+    w0 = spec.init("random", seed=5, device=cuda)
+    w = w0.clone()
+    lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, lr=0.25)
+    lp.run(1, 0, stream_handle(cuda))
+    ds = _deltas(lp, L, spec, cuda)
+    ref_w = w0 + 0.25 * (((ds[0] + ds[1]) + ds[2]) + ds[3])
+    assert torch.allclose(w, ref_w, atol=2e-6, rtol=1e-5)
+    # worker 2's window: its first 1024 shard rows (rows 2, 6, 10, ...)
+    Xw = train.X[2::L][:1024, : spec.F].float().cpu()
+    yw = train.y[2::L][:1024].long().cpu()
+    res = local_solve_reference(Xw, yw, spec.coef(w0.cpu()), spec.intercept(w0.cpu()))
+    ref = spec.pack(res.coef, res.intercept) - w0.cpu()
+    got = ds[2].cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 2e-2 * scale + 1e-4, (err, scale)
+
+
+def test_lanes_engine_rows_and_learning(cuda):
+    """LocalEngine with 4 workers runs the lanes loop: one worker row per worker and
+    one server row per round, vector clocks in order, the model learns."""
+    train, test = synth_finefood(40000, seed=0), synth_finefood(2000, seed=1)
+    cfg = PSConfig(num_workers=4, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=256, epochs=100, max_iters=60, min_buffer_size=128, max_buffer_size=1024,
+                   init="random")
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    out = eng.run()
+    assert out.get("lanes") == 4 and out["rounds"] == 60 and out["updates"] == 240
+    book = eng.log.book
+    assert [r[1] for r in book.server] == list(range(60))
+    assert len(book.worker) == 240 and {r[1] for r in book.worker} == {0, 1, 2, 3}
+    assert all(b[0] >= a[0] for a, b in zip(book.server, book.server[1:]))  # sink-stamped, in order
+    assert book.server[-1][3] > 0.33, book.server[-5:]
+    assert eng.server.tracker.min_clock() == 60
+    loss = eng.workers[0].solver.loss.item()
+    assert loss == loss and loss > 0
+
+
+def test_lanes_server_rows_match_standalone_eval(cuda):
+    """The riding evaluation of the global model == a standalone evaluation of it."""
+    spec, train, ev = _data(cuda)
+    w = spec.init("random", seed=9, device=cuda)
+    log = LogSink(spec.K, cuda)
+    lp, keep = _loop(spec, [0, 1], 2, train, ev, w, cuda, sink=log)
+    lp.run(3, 0, stream_handle(cuda))
+    lp.flush(stream_handle(cuda))
+    torch.cuda.synchronize()
+    book = log.book
+    assert [r[1] for r in book.server] == [0, 1, 2]
+    fr = Fragments(spec, cuda)
+    fr.refresh(w)
+    log2 = LogSink(spec.K, cuda)
+    from psx.ops.lr import EvalScratch
+
+    log2.server_eval(ev, fr, w, EvalScratch(cuda), 2)
+    b2 = log2.book
+    assert abs(book.server[-1][2] - b2.server[0][2]) < 1e-12 and abs(book.server[-1][3] - b2.server[0][3]) < 1e-12
+    assert len(book.worker) == 6 and all(r[3] > 0 for r in book.worker)  # worker rows carry the loss
+    log.close()
+    log2.close()
+
+
+def test_lanes_placement_fallback_same_result(cuda, monkeypatch):
+    """A failed placement check (faked) runs the sc1 hand-off form: same deltas bitwise."""
+    spec, train, ev = _data(cuda)
+    w0 = spec.init("random", seed=4, device=cuda)
+    wa, wb = w0.clone(), w0.clone()
+    lpa, ka = _loop(spec, [0, 1], 2, train, ev, wa, cuda)
+    assert lpa.hand_off_scope == 2
+    lpa.run(2, 0, stream_handle(cuda))
+    monkeypatch.setenv("PSX_FAKE_XCD_MISMATCH", "1")
+    lpb, kb = _loop(spec, [0, 1], 2, train, ev, wb, cuda)
+    assert lpb.hand_off_scope == 1
+    lpb.run(2, 0, stream_handle(cuda))
+    da, db = _deltas(lpa, 2, spec, cuda), _deltas(lpb, 2, spec, cuda)
+    assert all(torch.equal(x, y) for x, y in zip(da, db))
+    assert torch.equal(wa, wb)
+
+
+def test_lanes_spin_timeout_is_reported(cuda):
+    """A cross-workgroup wait that times out (forced: a 1-poll budget in round 3)
+    surfaces as an error naming that solve, without a host synchronisation."""
+    spec, train, ev = _data(cuda)
+    w = spec.init("random", seed=4, device=cuda)
+    lp, keep = _loop(spec, [0, 1], 2, train, ev, w, cuda)
+    lp.inject_spin_timeout(3, 1)
+    with pytest.raises(RuntimeError, match=r"timed out \(solve 3"):
+        lp.run(40, 0, stream_handle(cuda))  # (raises here if the device got there first)
+        torch.cuda.synchronize()
+        lp.poll_errors()
+    torch.cuda.synchronize()
+
+
+def test_engine_lanes_fault_maps_to_worker_failure(cuda, monkeypatch):
+    from psx.runtime.faults import WorkerFailure
+
+    monkeypatch.setenv("PSX_INJECT_SPIN_TIMEOUT", "2:1")
+    train, test = synth_finefood(8000, seed=0), synth_finefood(500, seed=1)
+    cfg = PSConfig(num_workers=2, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=256, epochs=100, max_iters=30, min_buffer_size=128, max_buffer_size=512)
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    with pytest.raises(WorkerFailure):
+        eng.run()
+    torch.cuda.synchronize()

@@ -497,6 +497,21 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def(py::init<int, const std::vector<uintptr_t>&, const std::vector<uintptr_t>&, const std::vector<uintptr_t>&>(),
            py::arg("nworkers"), py::arg("out_f32"), py::arg("out_i32"), py::arg("inbox"))
       .def("released", &LocalP2P::released);
+  py::class_<HostP2P, P2P>(m, "HostP2P")
+      .def(py::init<const std::string&, int, int, bool, bool, size_t, double>(), py::arg("name"), py::arg("nworkers"),
+           py::arg("rank"), py::arg("create"), py::arg("device") = false, py::arg("cap_bytes") = (size_t)8 << 20,
+           py::arg("timeout_s") = 600.0)
+      .def("send",
+           [](HostP2P& p, uintptr_t buf, size_t n, int dt, int peer, uintptr_t s) {
+             py::gil_scoped_release nogil;
+             p.send(reinterpret_cast<const void*>(buf), n, dt, peer, S(s));
+           })
+      .def("recv",
+           [](HostP2P& p, uintptr_t buf, size_t n, int dt, int peer, uintptr_t s) {
+             py::gil_scoped_release nogil;
+             p.recv(reinterpret_cast<void*>(buf), n, dt, peer, S(s));
+           })
+      .def("unlink", &HostP2P::unlink);
   py::class_<LocalFeeder>(m, "LocalFeeder")
       .def(py::init<uintptr_t, uintptr_t, LocalP2P*, int, int64_t, int64_t, double, const std::vector<int64_t>&,
                     const std::vector<uintptr_t>&>(),
@@ -550,8 +565,9 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.lvals = P<float>(U("lvals"));
              c.logcap = I("logcap", 0);
              c.dense_every = (int)I("dense_every", 64);
+             c.cpu = (int)I("cpu", 0);
              if (d.contains("replies")) c.replies = d["replies"].cast<std::vector<uintptr_t>>();
-             if (c.model == kAsyncDense || c.sink) prepare_kernels();
+             if (!c.cpu && (c.model == kAsyncDense || c.sink)) prepare_kernels();
              return std::make_unique<AsyncServer>(&comm, c, S(stream));
            }),
            py::arg("p2p"), py::arg("cfg"), py::arg("stream"), py::keep_alive<1, 2>())

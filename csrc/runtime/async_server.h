@@ -23,6 +23,7 @@
 #include <atomic>
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -88,6 +89,39 @@ class LocalP2P : public P2P {
   std::unique_ptr<std::atomic<int64_t>[]> released_;
 };
 
+// Host shared-memory transport between processes (one host, no GPU transport):
+// a byte FIFO per direction per worker in one POSIX shm segment, messages in the
+// order they are sent (RCCL's per-peer send / recv order).  It carries the same
+// server loop across processes on the CPU (tests, the plumbing config) and on a
+// GPU whose ranks cannot open an RCCL communicator (several ranks per device):
+// device buffers are staged through the host after a stream synchronisation.
+// rank 0 = the server (creates the segment), rank k + 1 = worker k.
+class HostP2P : public P2P {
+ public:
+  HostP2P(const std::string& name, int nworkers, int rank, bool create, bool device, size_t cap_bytes,
+          double timeout_s);
+  ~HostP2P() override;
+  int size() const override { return n_ + 1; }
+  void send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) override;
+  void recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) override;
+  void unlink();
+
+ private:
+  struct Chan;
+  Chan* chan(int idx) const;
+  int out_chan(int peer) const;
+  int in_chan(int peer) const;
+  void write(Chan* c, const char* src, size_t n);
+  void read(Chan* c, char* dst, size_t n);
+  std::string name_;
+  int n_, rank_;
+  bool owner_, device_;
+  size_t cap_, map_bytes_ = 0;
+  double timeout_s_;
+  char* base_ = nullptr;
+  std::vector<char> bounce_;
+};
+
 struct AsyncServerCfg {
   int nworkers = 0;
   int model = kAsyncDense;
@@ -130,6 +164,9 @@ struct AsyncServerCfg {
   int64_t logcap = 0;
   std::vector<uintptr_t> replies;  // per-worker reply CtrlQueue handles
   int dense_every = 64;
+  // host memory server (CPU ranks): the update / log / evaluation run on the host
+  // (same arithmetic as the kernels; no evaluation fragments)
+  int cpu = 0;
 };
 
 enum AsyncCode : int {
@@ -169,6 +206,8 @@ class AsyncServer {
   void check_api(int rc, const char* what) const;
   void send_weights(const int* ks, const int64_t* vs, int n);
   void apply_and_log(const CtrlToken& t);
+  void apply_cpu(const CtrlToken& t);
+  void eval_cpu(char* slot, uint64_t seq);
   int log_worker() const;
 
   P2P* comm_;

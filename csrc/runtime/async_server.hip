@@ -1,10 +1,18 @@
 // Native asynchronous server loop (see async_server.h).
 #include "async_server.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "../kernels/lr_kernels.h"
 #include "../kernels/wide_kernels.h"
@@ -23,6 +31,180 @@ int64_t epoch_ms() {
 constexpr int kKindDelta = 0, kKindFinal = 1, kKindError = 2;
 
 }  // namespace
+
+// ---- HostP2P: byte FIFOs in one POSIX shared-memory segment ----------------
+namespace {
+constexpr uint64_t kShmMagic = 0x70737832703270ull;  // "psx2p2p"
+constexpr size_t kSegHdr = 256, kChanHdr = 256;
+size_t dtype_bytes(int dtype) { return dtype == RcclComm::kU8 ? 1 : 4; }
+}  // namespace
+
+struct HostP2P::Chan {
+  alignas(128) std::atomic<uint64_t> head;  // bytes written (the producer's)
+  alignas(128) std::atomic<uint64_t> tail;  // bytes read (the consumer's)
+};
+static_assert(sizeof(std::atomic<uint64_t>) == 8, "lock-free 64-bit counters");
+
+HostP2P::HostP2P(const std::string& name, int nworkers, int rank, bool create, bool device, size_t cap_bytes,
+                 double timeout_s)
+    : name_(name), n_(nworkers), rank_(rank), owner_(create), device_(device), cap_(cap_bytes),
+      timeout_s_(timeout_s) {
+  if (nworkers < 1 || rank < 0 || rank > nworkers || cap_bytes < 4096 || name.empty() || name[0] != '/')
+    throw std::invalid_argument("HostP2P: bad arguments");
+  map_bytes_ = kSegHdr + (size_t)2 * nworkers * (kChanHdr + cap_);
+  int fd;
+  if (create) {
+    fd = shm_open(name.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0600);
+    if (fd < 0) throw std::runtime_error("HostP2P: shm_open(create) " + name);
+    if (ftruncate(fd, (off_t)map_bytes_) != 0) {
+      close(fd);
+      throw std::runtime_error("HostP2P: ftruncate");
+    }
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {  // the server creates the segment before the rendezvous barrier; tolerate a race
+      fd = shm_open(name.c_str(), O_RDWR, 0600);
+      struct stat st {};
+      if (fd >= 0 && fstat(fd, &st) == 0 && (size_t)st.st_size >= map_bytes_) break;
+      if (fd >= 0) close(fd);
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+        throw std::runtime_error("HostP2P: no segment " + name);
+      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    }
+  }
+  void* p = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("HostP2P: mmap");
+  base_ = static_cast<char*>(p);
+  auto* magic = reinterpret_cast<std::atomic<uint64_t>*>(base_);
+  if (create) {
+    for (int i = 0; i < 2 * n_; ++i) {
+      new (&chan(i)->head) std::atomic<uint64_t>(0);
+      new (&chan(i)->tail) std::atomic<uint64_t>(0);
+    }
+    reinterpret_cast<uint64_t*>(base_)[1] = (uint64_t)n_;
+    reinterpret_cast<uint64_t*>(base_)[2] = (uint64_t)cap_;
+    magic->store(kShmMagic, std::memory_order_release);
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (magic->load(std::memory_order_acquire) != kShmMagic) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+        throw std::runtime_error("HostP2P: segment never initialised");
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (reinterpret_cast<uint64_t*>(base_)[1] != (uint64_t)n_ || reinterpret_cast<uint64_t*>(base_)[2] != cap_)
+      throw std::runtime_error("HostP2P: segment shape differs");
+  }
+}
+
+HostP2P::~HostP2P() {
+  if (base_) munmap(base_, map_bytes_);
+  if (owner_) shm_unlink(name_.c_str());
+}
+
+void HostP2P::unlink() {
+  if (owner_) shm_unlink(name_.c_str());
+  owner_ = false;
+}
+
+HostP2P::Chan* HostP2P::chan(int idx) const {
+  return reinterpret_cast<Chan*>(base_ + kSegHdr + (size_t)idx * (kChanHdr + cap_));
+}
+// channel 2k: worker k -> server, 2k + 1: server -> worker k
+int HostP2P::out_chan(int peer) const {
+  if (rank_ == 0) {
+    if (peer < 1 || peer > n_) throw std::invalid_argument("HostP2P::send: peer");
+    return 2 * (peer - 1) + 1;
+  }
+  if (peer != 0) throw std::invalid_argument("HostP2P: workers talk to the server only");
+  return 2 * (rank_ - 1);
+}
+int HostP2P::in_chan(int peer) const {
+  if (rank_ == 0) {
+    if (peer < 1 || peer > n_) throw std::invalid_argument("HostP2P::recv: peer");
+    return 2 * (peer - 1);
+  }
+  if (peer != 0) throw std::invalid_argument("HostP2P: workers talk to the server only");
+  return 2 * (rank_ - 1) + 1;
+}
+
+void HostP2P::write(Chan* c, const char* src, size_t n) {
+  char* data = reinterpret_cast<char*>(c) + kChanHdr;
+  uint64_t head = c->head.load(std::memory_order_relaxed);
+  auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  while (n > 0) {
+    const uint64_t tail = c->tail.load(std::memory_order_acquire);
+    const size_t room = cap_ - (size_t)(head - tail);
+    if (room == 0) {
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins < 4096 ? 2 : 100));
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+        throw std::runtime_error("HostP2P: send timed out (peer not receiving)");
+      continue;
+    }
+    const size_t off = (size_t)(head % cap_);
+    const size_t m = std::min({n, room, cap_ - off});
+    std::memcpy(data + off, src, m);
+    head += m;
+    src += m;
+    n -= m;
+    c->head.store(head, std::memory_order_release);
+    spins = 0;
+    t0 = std::chrono::steady_clock::now();
+  }
+}
+
+void HostP2P::read(Chan* c, char* dst, size_t n) {
+  const char* data = reinterpret_cast<const char*>(c) + kChanHdr;
+  uint64_t tail = c->tail.load(std::memory_order_relaxed);
+  auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  while (n > 0) {
+    const uint64_t head = c->head.load(std::memory_order_acquire);
+    const size_t avail = (size_t)(head - tail);
+    if (avail == 0) {
+      if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins < 4096 ? 2 : 100));
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+        throw std::runtime_error("HostP2P: recv timed out (peer not sending)");
+      continue;
+    }
+    const size_t off = (size_t)(tail % cap_);
+    const size_t m = std::min({n, avail, cap_ - off});
+    std::memcpy(dst, data + off, m);
+    tail += m;
+    dst += m;
+    n -= m;
+    c->tail.store(tail, std::memory_order_release);
+    spins = 0;
+    t0 = std::chrono::steady_clock::now();
+  }
+}
+
+void HostP2P::send(const void* buf, size_t count, int dtype, int peer, hipStream_t s) {
+  const size_t bytes = count * dtype_bytes(dtype);
+  Chan* c = chan(out_chan(peer));
+  if (!device_) {
+    write(c, static_cast<const char*>(buf), bytes);
+    return;
+  }
+  bounce_.resize(bytes);  // stream order: the producer of buf first
+  hip_check(hipStreamSynchronize(s), "HostP2P send sync");
+  hip_check(hipMemcpy(bounce_.data(), buf, bytes, hipMemcpyDeviceToHost), "HostP2P send staging");
+  write(c, bounce_.data(), bytes);
+}
+
+void HostP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) {
+  const size_t bytes = count * dtype_bytes(dtype);
+  Chan* c = chan(in_chan(peer));
+  if (!device_) {
+    read(c, static_cast<char*>(buf), bytes);
+    return;
+  }
+  bounce_.resize(bytes);
+  read(c, bounce_.data(), bytes);
+  hip_check(hipMemcpyAsync(buf, bounce_.data(), bytes, hipMemcpyHostToDevice, s), "HostP2P recv staging");
+  hip_check(hipStreamSynchronize(s), "HostP2P recv sync");
+}
 
 RcclP2P::RcclP2P(RcclComm* c) : c_(c) {
   if (!c_) throw std::invalid_argument("RcclP2P: null communicator");
@@ -143,7 +325,7 @@ AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t strea
   } else if (!cfg.buf) {
     throw std::invalid_argument("AsyncServer: no receive buffer");
   }
-  if (cfg.model == kAsyncDense && cfg.sink && (!cfg.fhi || !cfg.flo || !cfg.fb || !cfg.Xt || !cfg.yt))
+  if (cfg.model == kAsyncDense && cfg.sink && !cfg.cpu && (!cfg.fhi || !cfg.flo || !cfg.fb || !cfg.Xt || !cfg.yt))
     throw std::invalid_argument("AsyncServer: dense evaluation needs fragments and a test set");
   if (cfg.sink && (!cfg.acc || !cfg.ticket)) throw std::invalid_argument("AsyncServer: evaluation scratch");
   finished_.assign(cfg.nworkers, 0);
@@ -262,10 +444,121 @@ void AsyncServer::begin() {
   send_weights(rel_k_.data(), rel_v_.data(), n);  // the bootstrap (ServerProcessor.java:75-87)
 }
 
+// Host-memory update (CPU ranks): the same arithmetic as the update kernels
+// (server_apply / axpy: w += lr * delta; wide_apply_sparse: the pushed ids'
+// values and the intercepts; the pull log), without evaluation fragments.
+void AsyncServer::apply_cpu(const CtrlToken& t) {
+  const int peer = t.worker + 1;
+  float* w = cfg_.w;
+  const float lr = cfg_.lr;
+  if (cfg_.model == kAsyncWideSparse) {
+    const int64_t U = t.n, KP = cfg_.KP;
+    if (U < 0 || U > cfg_.umax) throw std::runtime_error("AsyncServer: sparse push larger than the buffer");
+    if (U) comm_->recv(cfg_.ubuf, (size_t)U, RcclComm::kI32, peer, stream_);
+    comm_->recv(cfg_.dbuf, (size_t)(KP + U * KP), RcclComm::kF32, peer, stream_);
+    for (int64_t p = 0; p < KP + U * KP; ++p) {
+      const float v = cfg_.dbuf[p];
+      if (v == 0.f) continue;
+      if (p < KP)
+        w[cfg_.Fw * KP + p] += lr * v;
+      else
+        w[(int64_t)cfg_.ubuf[(p - KP) / KP] * KP + (p - KP) % KP] += lr * v;
+    }
+    if (cfg_.sparse_pull) {
+      if (U + 1 > cfg_.logcap) throw std::runtime_error("AsyncServer: push larger than the pull log");
+      for (int64_t l = 0; l <= U; ++l) {
+        const int64_t slot = (log_pos_ + l) % cfg_.logcap;
+        cfg_.lids[slot] = l == 0 ? (int32_t)cfg_.Fw : cfg_.ubuf[l - 1];
+        for (int64_t c = 0; c < KP; ++c) cfg_.lvals[slot * KP + c] = cfg_.dbuf[l * KP + c];
+      }
+      log_pos_ += U + 1;
+    }
+    return;
+  }
+  comm_->recv(cfg_.buf, (size_t)cfg_.P, RcclComm::kF32, peer, stream_);
+  for (int64_t i = 0; i < cfg_.P; ++i) w[i] += lr * cfg_.buf[i];
+}
+
+// Host-memory evaluation of the global model on the test set (CPU ranks): the
+// argmax confusion counts published into the metrics slot like the kernels do.
+void AsyncServer::eval_cpu(char* slot, uint64_t seq) {
+  int32_t conf[256] = {0};
+  const float* w = cfg_.w;
+  if (cfg_.model == kAsyncDense) {
+    const int K = cfg_.K, FP = cfg_.FP;
+    for (int t = 0; t < cfg_.T; ++t) {
+      int best = 0;
+      float bz = -INFINITY;
+      for (int c = 0; c < K; ++c) {
+        float z = w[(int64_t)K * FP + c];
+        const uint16_t* x = cfg_.Xt + (int64_t)t * FP;
+        const float* wc = w + (int64_t)c * FP;
+        for (int f = 0; f < cfg_.F; ++f) {
+          uint32_t u = (uint32_t)x[f] << 16;
+          float xf;
+          std::memcpy(&xf, &u, 4);
+          z += xf * wc[f];
+        }
+        if (z > bz) {
+          bz = z;
+          best = c;
+        }
+      }
+      const int y = std::min(15, std::max(0, (int)cfg_.yt[t]));
+      ++conf[y * 16 + best];
+    }
+  } else {
+    const int K = cfg_.K, KP = cfg_.KP;
+    std::vector<float> z(KP);
+    for (int t = 0; t < cfg_.T; ++t) {
+      for (int k = 0; k < KP; ++k) z[k] = w[cfg_.Fw * KP + k];
+      for (int64_t e = cfg_.t_indptr[t]; e < cfg_.t_indptr[t + 1]; ++e) {
+        uint32_t u = (uint32_t)cfg_.t_val[e] << 16;
+        float v;
+        std::memcpy(&v, &u, 4);
+        for (int k = 0; k < KP; ++k) z[k] += v * w[(int64_t)cfg_.t_idx[e] * KP + k];
+      }
+      int best = 0;
+      if (K == 1) {
+        best = z[0] > 0.f ? 1 : 0;
+      } else {
+        float bz = -INFINITY;
+        for (int k = 0; k < K; ++k)
+          if (z[k] > bz) {
+            bz = z[k];
+            best = k;
+          }
+      }
+      int y = cfg_.t_y[t];
+      if (K == 1) y = y > 0 ? 1 : 0;
+      y = std::min(15, std::max(0, y));
+      ++conf[y * 16 + best];
+    }
+  }
+  std::memcpy(slot, conf, sizeof(conf));
+  const float zero = 0.f;
+  std::memcpy(slot + 1024, &zero, 4);
+  __atomic_store_n(reinterpret_cast<uint64_t*>(slot + 1032), (uint64_t)seq, __ATOMIC_RELEASE);
+}
+
 void AsyncServer::apply_and_log(const CtrlToken& t) {
   const int k = t.worker;
   const int peer = k + 1;
   const int64_t v = t.vc;
+  if (cfg_.cpu) {
+    apply_cpu(t);
+    ++updates_;
+    ++updates_run_;
+    if (cfg_.sink && k == log_worker()) {
+      uint64_t seq = 0;
+      uintptr_t addr = 0;
+      const int slot = api().sink_acquire((void*)cfg_.sink, &seq, &addr);
+      check_api(slot, "metrics sink acquire");
+      eval_cpu(reinterpret_cast<char*>(addr), seq);
+      api().sink_submit((void*)cfg_.sink, slot, seq, 1, -1, -1, v, 0);
+    }
+    return;
+  }
   if (cfg_.model == kAsyncWideSparse) {
     const int64_t U = t.n;
     if (U < 0 || U > cfg_.umax) throw std::runtime_error("AsyncServer: sparse push larger than the buffer");

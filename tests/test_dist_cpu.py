@@ -117,10 +117,13 @@ def test_bsp_dedicated_server():
     assert out["updates"] == 10  # 2 worker ranks x 5 rounds
 
 
-@pytest.mark.parametrize("c", [-1, 2])
+@pytest.mark.parametrize("c", [-1, 2, 10])
 def test_async_dedicated_server(c):
+    """SSP / ASP across processes through the ONE native server loop
+    (csrc/runtime/async_server.h) over the host shared-memory transport."""
     out, w = _run(3, dict(BASE, consistency_model=c, max_iters=6))
-    assert out["updates"] == 12
+    assert out["updates"] == 12 and out.get("native_server") is True
+    assert out["host_us_per_update"] > 0
     if c > 0:
         assert out["max_vc_gap"] <= c + 1
 
@@ -204,7 +207,7 @@ def test_wide_sparse_pull_multi_worker(c):
     assert out["sparse_pulls"] > 0
 
 
-@pytest.mark.parametrize("c,bound", [(0, 1), (2, 3), (-1, None)])
+@pytest.mark.parametrize("c,bound", [(0, 1), (2, 3), (10, 11), (-1, None)])
 def test_log_derived_vc_gap(tmp_path, c, bound):
     """The reference validates its consistency models from the logs
     (iteration-vs-time plots, README.md:299-321); automated here: with a

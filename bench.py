@@ -70,8 +70,8 @@ def parse(argv=None):
                     help="new stream rows per worker per step (dense default: the whole window, as with the "
                          "reference's unthrottled producer every local solve sees fresh rows; wide default: 64)")
     ap.add_argument("--server-lr", type=float, default=None,
-                    help="server step on each delta (dense default 1/max(workers, 4): the reference's 1/N "
-                         "(ServerProcessor.java:148-151) with at least 4 workers' worth of averaging; wide: 1/N)")
+                    help="server step on each delta (default 1/N, N = all logical workers: the reference's "
+                         "learningRate = 1/numWorkers, ServerProcessor.java:36,148-151)")
     ap.add_argument("--train-rows", type=int, default=None)
     ap.add_argument("--test-rows", type=int, default=None)
     ap.add_argument("--features", type=int, default=None)
@@ -79,8 +79,9 @@ def parse(argv=None):
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="dense model feature rows (fp32: row-parallel solver with hi+lo MFMA operands)")
-    ap.add_argument("--workers", type=int, default=1,
-                    help="single-GPU run: in-process workers sharing the GPU (one HIP stream each); default 1")
+    ap.add_argument("--workers", type=int, default=None,
+                    help="logical workers per worker GPU, one XCD each in one launch per round (default 4: the "
+                         "reference's numWorkers = 4, all hosted in one process, BaseKafkaApp.java:25,70)")
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
@@ -93,8 +94,12 @@ def parse(argv=None):
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--rccl-trace", action="store_true",
                     help="RCCL collective/p2p trace into ./rccl-trace.<host>.<pid>.log (multi-GPU runs)")
-    ap.add_argument("--dedicated-server", action="store_true",
-                    help="multi-GPU BSP with a dedicated server rank (BASELINE config 2: reduce + broadcast)")
+    ap.add_argument("--dedicated-server", action="store_true", default=True,
+                    help="multi-GPU BSP: rank 0 is the server, ranks 1..N-1 the worker ranks, RCCL reduce (push) "
+                         "+ broadcast (pull) -- BASELINE config 2/3 topology (the default)")
+    ap.add_argument("--colocated-server", dest="dedicated_server", action="store_false",
+                    help="multi-GPU BSP: every rank hosts workers and a server replica, one RCCL all-reduce per "
+                         "round (data-parallel variant)")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check only)")
     ap.add_argument("--no-accuracy-run", dest="accuracy_run", action="store_false",
                     help="with --steps < 2000: skip the untimed continuation to 2000 rounds that reports the "
@@ -102,17 +107,21 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     m = MODELS[a.model]
     wide = a.model != "dense"
-    for k in ("features", "train_rows", "test_rows", "consistency", "schedule"):
+    for k in ("features", "train_rows", "test_rows", "consistency"):
         if getattr(a, k) is None:
             setattr(a, k, m[k])
+    if a.schedule is None and m["schedule"] == "sharded":
+        a.schedule = "sharded"
     if a.rows_per_step is None:
         a.rows_per_step = 64 if wide else a.buffer
     if a.steps is None:
         a.steps = 300 if wide else 2000
     if a.warmup is None:
         a.warmup = 30 if wide else 200
-    if a.dedicated_server and a.schedule == "allreduce":
-        a.schedule = "reduce_bcast"
+    if a.schedule is None:
+        a.schedule = "reduce_bcast" if a.dedicated_server else "allreduce"
+    if a.workers is None:  # the wide configs keep one worker per GPU
+        a.workers = 1 if wide else 4
     return a
 
 
@@ -143,7 +152,8 @@ def build_cfg(a, n_workers):
         async_scheduler=a.async_scheduler,
         # below 4 workers the step stays 1/4: one worker's fresh-window solve is a
         # noisy estimate (evaluation/README.md; tools/stream_sim.py --lr)
-        server_lr=a.server_lr if a.server_lr is not None else (None if wide else 1.0 / max(n_workers, 4)),
+        server_lr=a.server_lr,  # None: 1/N, the reference's update rule
+        workers_per_rank=1 if (wide or a.consistency != 0) else a.workers,
     )
 
 
@@ -168,9 +178,10 @@ def _backend_label() -> str:
     return "RCCL" if dist.get_backend() == "nccl" else dist.get_backend()
 
 
-def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
+def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, topo=None):
     async_mode = a.consistency != 0
     n_workers = cfg.num_workers
+    wpr = max(1, int(cfg.workers_per_rank))
     if a.model == "dense":
         model = f"multinomial-logreg F={a.features} K=6 (P={6 * a.features + 6}), local solver L-BFGS x2 + strong-Wolfe"
         data = (f"synthetic (fine-food-reviews-shaped, {a.train_rows} train / {a.test_rows} test rows, "
@@ -188,14 +199,16 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
         vs = None  # the reference never ran this configuration
     mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
     backend = _backend_label()
+    lanes = f"{wpr} workers/GPU, one XCD each" if wpr > 1 else "1 worker/GPU"
     if world == 1:
-        par = f"ps-{mode} w{n_workers} (server colocated{', workers share the GPU' if n_workers > 1 else ''})"
+        par = f"ps-{mode} w{n_workers} (server colocated, {lanes if n_workers > 1 else '1 worker'})"
     elif async_mode:
-        par = f"ps-{mode} 1 server + {n_workers} workers ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
+        par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
     elif not cfg.server_colocated:
-        par = f"ps-{mode} 1 server + {n_workers} workers ({cfg.bsp_schedule}, {backend})"
+        par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers "
+               f"({backend} reduce + broadcast, {cfg.bsp_schedule})")
     else:
-        par = f"ps-{mode} dp{world} ({cfg.bsp_schedule}, {backend})"
+        par = f"ps-{mode} dp{world} x {wpr} workers ({cfg.bsp_schedule}, {backend})"
     res = {
         "metric": "server_updates_per_s (PS push/pull rounds, logistic regression; test accuracy reported alongside)",
         "value": round(ups, 2),
@@ -221,14 +234,24 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None):
             "parallelism": par,
             "consistency": a.consistency,
             "workers": n_workers,
+            "workers_per_gpu": wpr,
             "rows_per_step_per_worker": a.rows_per_step,
             "server_lr": cfg.lr,
             "bench_model": a.model,
         },
+        # where the protocol differs from the reference's (ServerProcessor.java:36,
+        # WorkerTrainingProcessor.java:63-98): the update rule is the reference's
+        # w += (1/N) delta; the producer is unthrottled (-p 0) and every local solve
+        # fits a whole fresh window
+        "protocol": {"server_lr": cfg.lr, "reference_server_lr": 1.0 / n_workers,
+                     "rows_per_step_per_worker": a.rows_per_step, "window_rows": a.buffer,
+                     "producer": "unthrottled (-p 0), fresh rows every round"},
         "test_accuracy": summ.get("final_server_acc"),
         "test_f1": summ.get("final_server_f1"),
         "best_test_f1": summ.get("best_server_f1"),
     }
+    if topo is not None:
+        res["topology"] = topo
     if rccl_ranks is not None:
         res["rccl_ranks"] = rccl_ranks
     if tuples_seen is not None:
@@ -361,13 +384,16 @@ def _spawn_ranks(n: int, argv) -> int:
 
 
 def bench_distributed(a):
-    """N > 1 GPUs: one rank per GPU (torchrun or _spawn_ranks), RCCL over xGMI."""
+    """N > 1 GPUs: one rank per GPU (torchrun or _spawn_ranks), RCCL over xGMI.
+    Default topology (BASELINE config 2/3): rank 0 is the server, ranks 1..N-1 are
+    worker ranks with --workers workers each; every round the worker ranks' lane
+    sums are reduced to the server (push), updated there, and broadcast (pull)."""
     import torch
     import torch.distributed as dist
 
     from psx.ops.lr import is_gpu
     from psx.parallel.dist import DistEngine, init_from_env, rccl_trace_env
-    from psx.utils.logsink import LogSink, summarize
+    from psx.utils.logsink import summarize
 
     if a.rccl_trace:
         os.environ.update(rccl_trace_env("."))
@@ -376,21 +402,30 @@ def bench_distributed(a):
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
     async_mode = a.consistency != 0
     dedicated = async_mode or a.dedicated_server
-    cfg = build_cfg(a, world - 1 if dedicated else world)
+    wpr = 1 if (async_mode or a.model != "dense" or a.cpu) else a.workers
+    worker_ranks = world - 1 if dedicated else world
+    cfg = build_cfg(a, worker_ranks * wpr)
+    cfg.workers_per_rank = wpr
+    cfg.server_colocated = not dedicated
+    if not async_mode:
+        cfg.bsp_schedule = a.schedule if a.schedule != "reduce_bcast" or dedicated else "allreduce"
+        if dedicated and cfg.bsp_schedule == "allreduce":
+            cfg.bsp_schedule = "reduce_bcast"
     train, test = make_data(a, device)
     cfg.max_iters = a.warmup
     eng = DistEngine(cfg, rank, world, device, train=train, test=test)
+    run = eng._run_async if async_mode else eng._run_bsp
     if a.warmup:
-        eng._run_async() if async_mode else eng._run_bsp()
-    if eng.log is not None:
-        eng.log.close()
-        eng.log = LogSink(eng.spec.eval_classes, eng.device, keep_records=(rank == 0))
+        run()
+    n_warm = len(eng.log.book.server) if (rank == 0 and eng.log is not None and eng.log.book is not None) else 0
     cfg.max_iters = a.steps
     dist.barrier()
     if is_gpu(device):
         torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    out = eng._run_async() if async_mode else eng._run_bsp()
+    out = run()
+    if eng.log is not None:
+        eng.log.drain(block=True)
     dist.barrier()
     if is_gpu(device):
         torch.cuda.synchronize(device)
@@ -403,30 +438,28 @@ def bench_distributed(a):
     # collectives) or torch.distributed's (nccl backend = RCCL); None on gloo
     rccl = comm.c.size if comm is not None else (dist.get_world_size() if dist.get_backend() == "nccl" else None)
     res = None
+    topo = {"server_rank": 0 if dedicated else None, "worker_ranks": worker_ranks, "workers_per_rank": wpr,
+            "workers": cfg.num_workers, "schedule": cfg.bsp_schedule if not async_mode else "p2p",
+            "native_lanes_loop": getattr(eng, "_lanes", None) is not None}
     if rank == 0:
-        eng.log.close()
         book = eng.log.book
         summ = summarize(book)
         ups = a.steps * cfg.num_workers / dt
-        res = describe(a, world, cfg, ups, dt, summ, rccl_ranks=rccl)
+        res = describe(a, world, cfg, ups, dt, summ, rccl_ranks=rccl, topo=topo)
         res["max_vc_gap"] = out.get("max_vc_gap")
-        res.update(_accuracy_fields(book.server))
+        res.update(_accuracy_fields(list(book.server), timed_from=n_warm))
         if rccl is not None and rccl != world:
             raise SystemExit(f"bench.py: RCCL communicator has {rccl} ranks, world is {world}")
     if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not async_mode and not a.cpu:
         # untimed continuation for the accuracy half (see _accuracy_run); every rank runs it
-        timed_rows = list(eng.log.book.server) if rank == 0 else []
-        if eng.log is not None:
-            if rank != 0:
-                eng.log.close()
-            eng.log = LogSink(eng.spec.eval_classes, eng.device, keep_records=(rank == 0))
         cfg.max_iters = ACC_ROUNDS - a.steps
         eng._run_bsp()
         if rank == 0:
-            eng.log.close()
-            res["accuracy_run"] = _accuracy_run(timed_rows + list(eng.log.book.server), a.steps, 0)
+            res["accuracy_run"] = _accuracy_run(list(eng.log.book.server), a.steps, n_warm)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if eng.log is not None:
+        eng.log.close()
     eng.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -694,6 +694,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.tracker = U("tracker");
              c.api = U("api");
              c.server_rank = (int)I("server_rank", 0);
+             c.allreduce = I("allreduce", 0) != 0;
              return std::make_unique<LanesLoop>(c, comm);
            }),
            py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
@@ -722,8 +723,20 @@ PYBIND11_MODULE(_psx_hip, m) {
            py::arg("lane"), py::arg("loss") = 0, py::arg("delta") = 0, py::arg("stream") = 0)
       .def("inject_spin_timeout", &LanesLoop::inject_spin_timeout)
       .def("poll_errors", &LanesLoop::poll_errors)
+      .def("read_stamps", [](const LanesLoop& l, int lane, uintptr_t s) { return l.read_stamps(lane, S(s)); })
       .def_static("probe_placement", [](uintptr_t s) { return LanesLoop::probe_placement(S(s)); });
   m.def("lanes_supported", &lanes_supported, py::arg("FP"), py::arg("K"), py::arg("cap"));
+  // XCC_ID of every workgroup of an n-workgroup launch (placement diagnostics)
+  m.def("xcc_map", [](int n, uintptr_t stream) {
+    int* ids = nullptr;
+    hip_check(hipMalloc(&ids, n * sizeof(int)), "hipMalloc");
+    launch_xcc_probe(ids, n, S(stream));
+    std::vector<int> h(n);
+    hip_check(hipMemcpyAsync(h.data(), ids, n * sizeof(int), hipMemcpyDeviceToHost, S(stream)), "copy");
+    hip_check(hipStreamSynchronize(S(stream)), "sync");
+    (void)hipFree(ids);
+    return h;
+  });
   m.attr("ASYNC_DONE") = (int)kAsyncDone;
   m.attr("ASYNC_ERROR_TOKEN") = (int)kAsyncErrorToken;
   m.attr("ASYNC_WATCHDOG") = (int)kAsyncWatchdog;

@@ -95,6 +95,13 @@ struct LanesArgs {
   float* sb;
   int scoff;
   unsigned* arrive;     // [FP/32 + 1] per-slice lane arrival counters (zero between launches)
+  // workgroup roles are CLAIMED at run time: a workgroup reads its XCC_ID and takes
+  // the next slot of that XCD's lane (< kLaneWg of them), else the next rider id,
+  // so a lane's workgroups share one L2 whatever order the dispatcher deals the
+  // workgroups to the XCDs in.  claim: [2 launch parities][16] counters (XCD
+  // lane slots 0..7, riders at 8); this launch uses parity cpar and clears the other.
+  unsigned* claim;
+  int cpar;
   int spin_max;         // cross-workgroup wait budget (0: default)
   int nride;            // rider workgroups
   EvalMulti ev;
@@ -102,9 +109,9 @@ struct LanesArgs {
 
 bool lanes_supported(int FP, int K, int cap);
 size_t lanes_lds_bytes(int FP);
-// Grid of a round: 8 * kLaneWg lane slots + extra riders.
-int lanes_grid(int L, int nride_total);
-int lanes_rider_base(int L);  // riders on the lane slots of unused XCDs
+// Grid of a round with L lanes and at least `min_riders` riders (>= 8 * kLaneWg);
+// its riders are grid - L * kLaneWg.
+int lanes_grid(int L, int min_riders);
 // S = 2: one-XCD hand-offs (blockIdx % 8 == XCC_ID verified); S = 1: sc1 hand-offs.
 void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const LanesArgs& a, int S, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).

@@ -12,10 +12,9 @@ bool lanes_supported(int FP, int K, int cap) {
          cap <= 32 * kLaneWg;
 }
 size_t lanes_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (kBwdLdsBytes + 15) / 16 * 16 + kSyBytes; }
-int lanes_rider_base(int L) { return kLaneWg * (8 - L); }
-int lanes_grid(int L, int nride_total) {
-  const int extra = nride_total - lanes_rider_base(L);
-  return 8 * kLaneWg + (extra > 0 ? extra : 0);
+int lanes_grid(int L, int min_riders) {
+  const int g = L * kLaneWg + min_riders;
+  return g > 8 * kLaneWg ? g : 8 * kLaneWg;
 }
 
 namespace {
@@ -373,13 +372,37 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
                                                           LanesArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = (int)blockIdx.x, tid = threadIdx.x, L = a.L;
-  const int x = b & 7, i = b >> 3;
-  if (b >= 8 * kLaneWg || x >= L) {  // a rider: the previous round's evaluation
-    const int rid = b < 8 * kLaneWg ? i * (8 - L) + (x - L) : kLaneWg * (8 - L) + (b - 8 * kLaneWg);
-    eval_multi_body<FP>(lds, a.ev, rid, a.nride);
-    return;
+  int l, wg;
+  {
+    __shared__ int role;
+    if (tid == 0) {
+      unsigned* c = a.claim + 16 * a.cpar;
+      int r = -1;
+      if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
+        if ((int)xcc < L) {
+          const unsigned k = __hip_atomic_fetch_add(c + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (k < (unsigned)kLaneWg) r = (int)(xcc * kLaneWg + k);
+        }
+      } else if (b < 8 * kLaneWg && (b & 7) < L) {  // spread hand-offs: any placement works
+        r = (b & 7) * kLaneWg + (b >> 3);
+      }
+      if (r < 0) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
+      if (b == 0)  // the other parity's counters (the previous launch is complete) for the next launch
+        for (int j = 0; j < 16; ++j)
+          __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      role = r;
+    }
+    __syncthreads();
+    const int r = role;
+    __syncthreads();
+    if (r < 0) {  // a rider: the previous round's evaluation
+      eval_multi_body<FP>(lds, a.ev, -r - 1, a.nride);
+      return;
+    }
+    l = r / kLaneWg;
+    wg = r - l * kLaneWg;
   }
-  const int l = x, wg = i;
   constexpr int NS = FP / 32;
   const LaneRound rr = pick(a.r, l);
   const SolveParams win{rr.B, rr.start, 0, 0};
@@ -429,16 +452,20 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     if constexpr (S == 1) xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counter
   }
   // ---- phase I: stage + ingest + window statistics, then x0 / first trial point ----
+  if (wg == 0 && tid == 0) stamp(dv, 30, 0);
   if (row) {
     const int rt = wt.ring_tile(wg);
     lane_stage_stats<FP, S>(lf, lsy, cfg, dv, rr, a.dsX, a.dsy, rt, lanes[l].spart + (size_t)wg * FP * 2);
   }
+  if (wg == 0 && tid == 0) stamp(dv, 30, 1);
   barrier();
+  if (wg == 0 && tid == 0) stamp(dv, 30, 2);
   if (owner) {
     lane_prep<FP, KP, S>(lb, cfg, dv, lanes[l].spart, ntr, win.B, wg, wo_pre, b_pre);
     if (tid == 0) ctrl_init(*cl);
   }
   barrier();
+  if (wg == 0 && tid == 0) stamp(dv, 30, 3);
   // ---- slots (as solve_persist_kernel) ----
   int phase = kPhInit;
   for (int slot = 0; slot < cfg.nslots; ++slot) {
@@ -458,6 +485,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
   }
   if (!owner) return;
+  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
   // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
   {
     FinIn<KP> in;
@@ -478,8 +506,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     for (int k = tid; k < CW; k += 256) ((unsigned long long*)lanes[l].ctrl)[k] = ((const unsigned long long*)cl)[k];
   }
   // ---- the BSP update: the last lane to finish a slice applies the sum ----
+  if (wg == 0 && tid == 0) stamp(dv, 30, 5);
   if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg, NS);
   if (wg == 0 && lane_arrive(a.arrive, NS, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, NS, NS);
+  if (wg == 0 && tid == 0) stamp(dv, 30, 6);
 }
 
 __global__ void xcc_probe_kernel(int* ids, int n) {

@@ -69,6 +69,10 @@ struct LanesLoopCfg {
   uintptr_t tracker = 0;    // VectorClockTracker* (0: none)
   uintptr_t api = 0;        // HostApi*
   int server_rank = 0;      // multi-rank: the rank that applies the update
+  // multi-rank schedule: false = reduce to the server rank, update there, broadcast
+  // the weights (the PS push / pull); true = all-reduce of the lane sums, every rank
+  // applies the same update to its replica (one collective per round)
+  bool allreduce = false;
 };
 
 class LanesLoop {
@@ -110,6 +114,9 @@ class LanesLoop {
   // Raise if a lane's solve reported a timed-out cross-workgroup wait (the pinned
   // error words; no synchronisation: call after one to cover every enqueued round).
   void poll_errors() { check_errors(-1); }
+  // phase timeline of lane `lane`'s last solve (PSX_LANES_STAMPS=1 at construction):
+  // [slot][k] s_memrealtime ticks (100 MHz), row 30 = the round's own phases
+  std::vector<long long> read_stamps(int lane, hipStream_t stream) const;
   // placement probe: blockIdx % 8 == XCC_ID for every workgroup of a large launch
   static bool probe_placement(hipStream_t stream);
 
@@ -143,7 +150,11 @@ class LanesLoop {
   unsigned* arrive_ = nullptr;
   int* acc_ = nullptr;
   unsigned* ticket_ = nullptr;
+  unsigned* claim_ = nullptr;
+  int64_t launches_ = 0;
   float* dsum_ = nullptr;
+  uint16_t *upd_hi_ = nullptr, *upd_lo_ = nullptr;  // fragments of an update nobody evaluates
+  float* upd_b_ = nullptr;
   unsigned long long* err_host_ = nullptr;  // pinned [kMaxLanes]
   Pending pend_;
   int last_par_ = 0;  // parity of the last round run

@@ -82,8 +82,11 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
     next_local_.push_back(0);
   }
   prepare_kernels();
-  hipStream_t s0 = nullptr;
-  S_ = probe_placement(s0) ? 2 : 1;
+  // the lanes claim their XCD at run time (LanesArgs::claim), so placement needs no
+  // assumption; PSX_FAKE_XCD_MISMATCH=1 / PSX_LANES_SPREAD=1 select the spread form
+  const char* sp = std::getenv("PSX_LANES_SPREAD");
+  const char* fk = std::getenv("PSX_FAKE_XCD_MISMATCH");
+  S_ = ((sp && sp[0] == '1') || (fk && fk[0] == '1')) ? 1 : 2;
 
   // ---- device workspace: per lane + shared ----
   const int KP = padded_classes(s.K), FPI = padded_stride(s.Fp), PI = KP * FPI + 16, FP = s.Fp;
@@ -95,8 +98,9 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   };
   struct Offs {
     size_t x, d, gc, wfix, std_, istd, beff, whi, wlo, part, xch, gpf, spart, delta, ohi[2], olo[2], ob[2], loss2,
-        stats, cnt, ctrl;
+        stats, cnt, ctrl, dbg;
   };
+  const bool stamps = std::getenv("PSX_LANES_STAMPS") != nullptr;
   std::vector<Offs> o(cfg_.L);
   for (int l = 0; l < cfg_.L; ++l) {
     Offs& q = o[l];
@@ -123,12 +127,15 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
     q.stats = take(8 * 4);
     q.cnt = take(16);
     q.ctrl = take(sizeof(Ctrl));
+    q.dbg = stamps ? take(32 * 16 * sizeof(long long)) : 0;
   }
   const size_t o_tab = take(sizeof(LaneDev) * (cfg_.L > 0 ? cfg_.L : 1));
   const size_t o_arr = take((FP / 32 + 1) * sizeof(unsigned));
   const size_t o_acc = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
   const size_t o_tic = take(8 * sizeof(unsigned));
+  const size_t o_claim = take(32 * sizeof(unsigned));
   const size_t o_dsum = take((size_t)P_ * 4);
+  const size_t o_uhi = take((size_t)16 * FP * 2), o_ulo = take((size_t)16 * FP * 2), o_ub = take(16 * 4);
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
   char* b = static_cast<char*>(ws_);
@@ -169,6 +176,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
     dv.FPI = FPI;
     dv.PI = PI;
     dv.err_host = err_host_ + l;
+    dv.dbg = stamps ? reinterpret_cast<long long*>(b + q.dbg) : nullptr;
     ld.spart = reinterpret_cast<float*>(b + q.spart);
     for (int p = 0; p < 2; ++p) {
       ld.ohi[p] = reinterpret_cast<uint16_t*>(b + q.ohi[p]);
@@ -182,7 +190,11 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   arrive_ = reinterpret_cast<unsigned*>(b + o_arr);
   acc_ = reinterpret_cast<int*>(b + o_acc);
   ticket_ = reinterpret_cast<unsigned*>(b + o_tic);
+  claim_ = reinterpret_cast<unsigned*>(b + o_claim);
   dsum_ = reinterpret_cast<float*>(b + o_dsum);
+  upd_hi_ = reinterpret_cast<uint16_t*>(b + o_uhi);
+  upd_lo_ = reinterpret_cast<uint16_t*>(b + o_ulo);
+  upd_b_ = reinterpret_cast<float*>(b + o_ub);
   if (cfg_.L > 0)
     hip_check(hipMemcpy(lanes_dev_, lanes_.data(), sizeof(LaneDev) * cfg_.L, hipMemcpyHostToDevice),
               "lanes table upload");
@@ -258,11 +270,14 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
 }
 
 int LanesLoop::rider_count(int nmodels, int L) const {
-  if (nmodels <= 0) return 0;
-  const int nT = (cfg_.T + 31) / 32, items = (nmodels + 1) / 2 * nT;
-  const int slots = lanes_rider_base(L);
-  if (slots > 0) return slots < items ? slots : items;
-  return items < 256 ? items : 256;  // every XCD solves: riders after the lanes
+  // the riders of the launch: the CUs of the XCDs no lane uses, or (every XCD
+  // solves) enough riders to run after the lanes; a launch has grid - L * 32
+  int extra = 0;
+  if (nmodels > 0 && L == 8) {
+    const int nT = (cfg_.T + 31) / 32, items = (nmodels + 1) / 2 * nT;
+    extra = items < 256 ? items : 256;
+  }
+  return lanes_grid(L, extra) - L * kLaneWg;
 }
 
 // The previous round's rows as models of one evaluation pass: the lanes' local
@@ -304,7 +319,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
       add(lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
   if (cfg_.log_server)
     add(cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
-  ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);
+  ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
 }
 
 void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
@@ -388,20 +403,31 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.sb = cfg_.sb[par];
     a.scoff = cfg_.scoff;
     a.arrive = arrive_;
+    a.claim = claim_;
+    a.cpar = (int)(launches_ & 1);
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
+      if (a.nride == 0) a.nride = rider_count(0, L);
       launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
       hip_check(hipGetLastError(), "lanes round launch");
+      ++launches_;
     }
     if (!slots.empty()) submit_rows(pend_, slots, seqs, kinds);
     // ---- multi-rank: lane sums -> server (reduce), update, weights -> every rank ----
     if (comm_) {
       if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
-      comm_->reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
-      if (is_server)
-        launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr, cfg_.shi[par],
-                            cfg_.slo[par], cfg_.sb[par], stream, cfg_.scoff);
-      comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+      if (cfg_.allreduce) {  // every replica applies the same summed update
+        comm_->all_reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, stream);
+        launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr,
+                            cfg_.shi[par] ? cfg_.shi[par] : upd_hi_, cfg_.shi[par] ? cfg_.slo[par] : upd_lo_,
+                            cfg_.shi[par] ? cfg_.sb[par] : upd_b_, stream, cfg_.scoff);
+      } else {  // push: reduce to the server rank; update there; pull: broadcast
+        comm_->reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+        if (is_server)
+          launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr, cfg_.shi[par],
+                              cfg_.slo[par], cfg_.sb[par], stream, cfg_.scoff);
+        comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+      }
       hip_check(hipGetLastError(), "server update launch");
     }
     (void)KF;
@@ -431,9 +457,12 @@ void LanesLoop::flush(hipStream_t stream) {
   a.nride = (int)a.ev.nticket;
   a.w = cfg_.w;
   a.arrive = arrive_;
+  a.claim = claim_;
+  a.cpar = (int)(launches_ & 1);
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
     hip_check(hipGetLastError(), "lanes evaluation launch");
+    ++launches_;
   }
   submit_rows(pend_, slots, seqs, kinds);
   pend_ = Pending{};
@@ -452,6 +481,16 @@ float LanesLoop::loss(int lane, hipStream_t stream) const {
   hip_check(hipMemcpyAsync(v, lanes_.at(lane).loss2, 2 * sizeof(float), hipMemcpyDeviceToHost, stream), "lane loss");
   hip_check(hipStreamSynchronize(stream), "sync");
   return v[last_par_];
+}
+
+std::vector<long long> LanesLoop::read_stamps(int lane, hipStream_t stream) const {
+  std::vector<long long> v;
+  const long long* d = lanes_.at(lane).dv.dbg;
+  if (!d) return v;
+  v.resize(32 * 16);
+  hip_check(hipMemcpyAsync(v.data(), d, v.size() * sizeof(long long), hipMemcpyDeviceToHost, stream), "stamps");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v;
 }
 
 uintptr_t LanesLoop::delta_ptr(int lane) const { return reinterpret_cast<uintptr_t>(lanes_.at(lane).dv.delta); }

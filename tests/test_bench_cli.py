@@ -27,17 +27,30 @@ def _run(args, env=None):
 
 @pytest.mark.parametrize("n", [2, 4])
 def test_bench_spawns_n_ranks(n):
+    """Default topology for N >= 2 (BASELINE config 2/3, the north star): rank 0 is
+    the server, ranks 1..N-1 the worker ranks (RCCL reduce + broadcast on GPUs)."""
     p, lines = _run(["--gpus", str(n)] + SMALL)
     assert p.returncode == 0, p.stderr[-2000:]
     assert len(lines) == 1, p.stdout  # rank 0 only
     d = json.loads(lines[0])
     assert d["n_gpus"] == n
     assert d["steps"] == 4 and d["warmup"] == 1
-    assert d["config"]["workers"] == n  # allreduce schedule: every rank is a worker
-    assert d["config"]["parallelism"].startswith(f"ps-bsp dp{n}")
-    assert d["config"]["features"] == 1024 and d["config"]["window_rows_total"] == 1024 * n
+    assert d["config"]["workers"] == n - 1  # (one worker per rank on the CPU)
+    assert d["config"]["parallelism"].startswith(f"ps-bsp 1 server rank + {n - 1} worker ranks")
+    assert d["topology"]["server_rank"] == 0 and d["topology"]["worker_ranks"] == n - 1
+    assert d["topology"]["schedule"] == "reduce_bcast"
+    assert d["config"]["features"] == 1024 and d["config"]["window_rows_total"] == 1024 * (n - 1)
     assert "3000 train / 400 test" in d["data"]
     assert "time_to_f1_0.40_s" in d and d["best_test_f1"] is not None
+    assert d["protocol"]["server_lr"] == d["protocol"]["reference_server_lr"]
+
+
+def test_bench_colocated_server_variant():
+    p, lines = _run(["--gpus", "2", "--colocated-server"] + SMALL)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["config"]["workers"] == 2 and d["config"]["parallelism"].startswith("ps-bsp dp2")
+    assert d["topology"]["server_rank"] is None and d["topology"]["schedule"] == "allreduce"
 
 
 def test_bench_dedicated_server_config2():
@@ -45,7 +58,7 @@ def test_bench_dedicated_server_config2():
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["workers"] == 1
-    assert "1 server + 1 workers" in d["config"]["parallelism"]
+    assert "1 server rank + 1 worker ranks" in d["config"]["parallelism"]
 
 
 def test_bench_world_mismatch_is_an_error():
@@ -54,11 +67,15 @@ def test_bench_world_mismatch_is_an_error():
     assert "--gpus 2" in (p.stderr + p.stdout)
 
 
-def test_bench_single_gpu_default_unchanged():
+def test_bench_single_gpu_default():
+    """One GPU: the server and the reference's numWorkers = 4 workers in one process
+    (BaseKafkaApp.java:25,70), server step 1/N (ServerProcessor.java:36)."""
     p, lines = _run(SMALL)
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w1")
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w4")
+    assert d["config"]["workers"] == 4 and d["config"]["server_lr"] == 0.25
+    assert d["time_to_f1_0.40_s"] is None or d["time_to_f1_0.40_s"] > 0
 
 
 @pytest.mark.parametrize("c", [2, -1])

@@ -84,6 +84,7 @@ def test_dist_engine_native_bsp_loop_world1(cuda, pg, monkeypatch):
 
     train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
     res = []
+    monkeypatch.setenv("PSX_NATIVE_LANES", "0")  # (the single-worker BspLoop against the Python loop)
     for native in ("1", "0"):
         monkeypatch.setenv("PSX_NATIVE_BSP", native)
         cfg = PSConfig(num_workers=1, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
@@ -100,3 +101,55 @@ def test_dist_engine_native_bsp_loop_world1(cuda, pg, monkeypatch):
     assert torch.equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1] and [r[0] for r in res[0][1]] == list(range(12))
     assert res[0][2] == res[1][2] and res[0][3] == res[1][3]
+
+
+def test_rccl_p2p_self_world1(cuda, pg):
+    """RcclComm send / recv to self inside group_start / group_end for every piece
+    shape the native SSP/ASP server sends (dense weights; sparse pull: ids int32 +
+    values f32, split in two ring-log halves)."""
+    from psx.parallel.comm import make_comm
+
+    comm = make_comm(0, 1, cuda)
+    c, s = comm.c, torch.cuda.current_stream().cuda_stream
+    w = torch.randn(6150, device=cuda)
+    ids = torch.randint(0, 1 << 20, (700,), dtype=torch.int32, device=cuda)
+    vals = torch.randn(700 * 8, device=cuda)
+    pieces = [w, ids[:300], vals[:300 * 8], ids[300:], vals[300 * 8:]]
+    outs = [torch.zeros_like(t) for t in pieces]
+    c.group_start()
+    for t, o in zip(pieces, outs):
+        dt = 1 if t.dtype == torch.int32 else 0
+        c.send(t.data_ptr(), t.numel(), dt, 0, s)
+        c.recv(o.data_ptr(), o.numel(), dt, 0, s)
+    c.group_end()
+    torch.cuda.synchronize()
+    assert all(torch.equal(t, o) for t, o in zip(pieces, outs))
+    comm.close()
+
+
+@pytest.mark.parametrize("sched", ["reduce_bcast", "allreduce"])
+def test_dist_lanes_world1_matches_local(cuda, pg, sched):
+    """A rank of the multi-lane loop with RCCL (4 workers per rank: lane sum -> reduce
+    to the server -> update -> broadcast, or all-reduce into every replica) gives the
+    in-process engine's model and server rows."""
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(20000, seed=0), synth_finefood(1000, seed=1)
+    kw = dict(consistency_model=0, producer_time_per_event=0, stream_mode="per_iter", rows_per_iter=512,
+              epochs=100, max_iters=10, init="random", min_buffer_size=512, max_buffer_size=512)
+    cfg = PSConfig(num_workers=4, workers_per_rank=4, bsp_schedule=sched, **kw)
+    eng = DistEngine(cfg, 0, 1, cuda, train=train, test=test)
+    out = eng.run()
+    assert out["rounds"] == 10 and getattr(eng, "_lanes", None) is not None
+    ref = LocalEngine(PSConfig(num_workers=4, **kw), cuda, train=train, test=test)
+    ref.run()
+    torch.cuda.synchronize()
+    scale = ref.server.w.abs().max().item()
+    assert torch.allclose(eng.server.w, ref.server.w, atol=1e-5 * scale), (eng.server.w - ref.server.w).abs().max()
+    a = [(r[1], round(r[2], 6)) for r in eng.log.book.server]
+    b = [(r[1], round(r[2], 6)) for r in ref.log.book.server]
+    assert [r[0] for r in a] == list(range(10)) and len(eng.log.book.worker) == 40
+    assert sum(x != y for x, y in zip(a, b)) <= 2  # (argmax ties may flip with last-bit differences)

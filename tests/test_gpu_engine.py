@@ -162,6 +162,7 @@ def test_riding_eval_matches_separate_launches(cuda, monkeypatch, N):
 def test_native_bsp_loop_matches_python_loop(cuda, monkeypatch):
     """The native BSP round loop (csrc/runtime/bsp_loop.h) logs exactly the rows of
     the Python loop, ends at the same model, producer cursor, window and tracker."""
+    monkeypatch.setenv("PSX_NATIVE_LANES", "0")  # (the single-worker loop; the lanes loop has its own tests)
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     kw = dict(num_workers=1, max_iters=25, init="random", min_buffer_size=256, max_buffer_size=256,
               rows_per_iter=96)

@@ -58,6 +58,7 @@ def test_dist_engine_native_vs_torch_collectives(cuda, pg, monkeypatch):
     from psx.utils.data import synth_finefood
 
     train, test = synth_finefood(4000, seed=0), synth_finefood(500, seed=1)
+    monkeypatch.setenv("PSX_NATIVE_LANES", "0")  # (one worker per rank: the collectives' own comparison)
     ws = {}
     for native in ("1", "0"):
         for sched in ("allreduce", "reduce_bcast", "sharded"):

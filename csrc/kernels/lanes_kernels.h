@@ -53,11 +53,14 @@ struct LaneDev {
   Ctrl* ctrl;         // the lane's controller after the round (host diagnostics)
 };
 
-// Per-round arguments of one lane: the window and the new rows of this round
-// (dataset rows first + i * step, i < n, into ring slots (dst + i) % cap).
+// Per-round arguments of one lane: the window and the new rows of this round:
+// dataset rows first + i * step (i < n) into ring slots (dst + i) % cap, then (a
+// delivery that wraps the worker's shard) first2 + i * step (i < n2) into slots
+// (dst + n + i) % cap.
 struct LaneRound {
   int B, start, n, dst;
-  long long first, step;
+  long long first, step, first2;
+  int n2, pad;
 };
 
 struct EvalModel {

@@ -167,25 +167,31 @@ __device__ __forceinline__ void lane_stage_stats(char* lf, float* scratch, const
   // labels travel with the first loads
   int yv = 0;
   bool ynew = false;
-  if (tid < 32) {
-    const int s = rt * 32 + tid;
+  // the dataset row of ring slot s when it holds one of this round's new rows, else -1
+  auto new_src = [&](int s) -> long long {
     int dn = s - r.dst;
     if (dn < 0) dn += cap;
-    ynew = dn < r.n;
-    yv = ynew ? dsy[r.first + (long long)dn * r.step] : dv.y[s];
+    if (dn < r.n) return r.first + (long long)dn * r.step;
+    if (dn - r.n < r.n2) return r.first2 + (long long)(dn - r.n) * r.step;
+    return -1;
+  };
+  if (tid < 32) {
+    const int s = rt * 32 + tid;
+    const long long src = new_src(s);
+    ynew = src >= 0;
+    yv = ynew ? dsy[src] : dv.y[s];
   }
   u16x8 v[PER_T];
   bool isnew[PER_T], valid[PER_T];
 #pragma unroll
   for (int j = 0; j < PER_T; ++j) {
     const int row = g + NG * j, s = rt * 32 + row;
-    int dn = s - r.dst;
-    if (dn < 0) dn += cap;
-    isnew[j] = dn < r.n;
+    const long long sr = new_src(s);
+    isnew[j] = sr >= 0;
     int dw = s - r.start;
     if (dw < 0) dw += cap;
     valid[j] = dw < r.B;
-    const uint16_t* src = isnew[j] ? dsX + (size_t)(r.first + (long long)dn * r.step) * FP : dv.X + (size_t)s * FP;
+    const uint16_t* src = isnew[j] ? dsX + (size_t)sr * FP : dv.X + (size_t)s * FP;
     v[j] = *(const u16x8*)(src + cg * 8);
   }
   float sm[8], sq[8];

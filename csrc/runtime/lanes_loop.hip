@@ -241,25 +241,41 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
   const int64_t first = api().window_insert_many(reinterpret_cast<void*>(cfg_.window[lane]), times_.data(), n);
   check(first, "window insert");
   const int64_t cap = cfg_.scfg.cap;
-  if (r->n > 0) {  // an earlier delivery of this round still pending for the kernel: launch it now
-    launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]), nullptr,
-                       reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
-    r->n = 0;
-  }
+  // rows already pending for the kernel from an earlier delivery of this round: into
+  // the ring now (the kernel carries at most the last two contiguous runs)
+  auto flush_pending = [&]() {
+    if (r->n > 0)
+      launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
+                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
+    if (r->n2 > 0)
+      launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first2, r->step, r->n2, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
+                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), (r->dst + r->n) % cap, cap, cfg_.scfg.Fp,
+                         stream);
+    r->n = r->n2 = 0;
+  };
+  flush_pending();
   const int64_t keep = n < cap ? n : cap, skip = n - keep;
   int64_t slot = (first + skip) % cap, pos = nl + skip, remaining = keep;
   while (remaining > 0) {  // split at the shard's epoch boundaries
     const int64_t cur = pos % lt;
     const int64_t run = remaining < lt - cur ? remaining : lt - cur;
     const int64_t src_first = k + cur * (int64_t)cfg_.N;
-    if (run == remaining) {
+    if (r->n2 > 0) {  // a third run: the oldest goes to a launch of its own
+      launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
+                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
+      r->dst = (int)((r->dst + r->n) % cap);
+      r->first = r->first2;
+      r->n = r->n2;
+      r->n2 = 0;
+    }
+    if (r->n == 0) {
       r->first = src_first;
       r->step = cfg_.N;
       r->n = (int)run;
       r->dst = (int)slot;
     } else {
-      launch_ring_ingest(cfg_.dsX, cfg_.dsy, src_first, cfg_.N, run, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
-                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), slot, cap, cfg_.scfg.Fp, stream);
+      r->first2 = src_first;
+      r->n2 = (int)run;
     }
     slot = (slot + run) % cap;
     pos += run;

@@ -172,6 +172,9 @@ class LocalSolveOp:
             raise ValueError(f"ring capacity {ring.cap} != solver capacity {self.cap}")
         X, y = ring.X, ring.y
         if self.frag is not None:  # GPU
+            if getattr(ring, "xt_stale", False):  # rows written by the multi-lane round kernel
+                ring.sync_transposed()
+                ring.xt_stale = False
             self._bind(ring, w_old)
             pend = ring.take_pending(B, start) if hasattr(ring, "take_pending") else None
             if ride is None and apply is None:

@@ -26,12 +26,15 @@ instead of ~30 us through torch.distributed, which otherwise bounds the round.
 
 Bounded-delay (SSP, c = D > 0) and eventual (ASP, c = -1) need a dedicated
 server rank 0 (workers are ranks 1..N).  A worker pushes a (worker, vc) token
-into the shm control queue and ncclSend's its delta; the server pops tokens in
-arrival order (= the single GRADIENTS_TOPIC partition), ncclRecv's from that
-worker, applies, and ncclSend's the new weights to every worker the tracker
-releases.  A worker always posts its recv right after its send and the server
-only receives from workers whose token it has seen, so the send/recv graph is
-acyclic (deadlock free).
+into the shm control queue and sends its delta; the ONE server loop -- the native
+AsyncServer (csrc/runtime/async_server.h) -- pops tokens in arrival order (= the
+single GRADIENTS_TOPIC partition), receives from that worker, applies, and sends
+the new weights to every worker the tracker releases.  The data plane is RCCL
+point-to-point over xGMI (one rank per GPU) or, for ranks without an RCCL
+communicator (CPU / gloo runs), the host shared-memory transport HostP2P with
+the same per-peer message order.  A worker always posts its recv right after
+its send and the server only receives from workers whose token it has seen, so
+the send/recv graph is acyclic (deadlock free).
 """
 from __future__ import annotations
 
@@ -166,60 +169,6 @@ class StopVote:
             self._ring = 0
 
 
-class PullLog:
-    """Server-side ring log of the applied sparse pushes (the Python twin of the
-    native loop's, csrc/runtime/async_server.hip): entry = ids [F (the intercepts'
-    pseudo-feature), uniq...] + the push payload dloc [(U+1) * KP] unchanged.  A
-    released worker receives the entries since its previous pull -- a
-    KeyRange-addressed payload (BaseMessage.java:24-27) instead of the dense
-    weights -- unless the dense vector is cheaper, the worker fell behind the
-    log, or ``dense_every`` sparse pulls passed."""
-
-    def __init__(self, spec, cap_ids: int, num_workers: int, device, dense_every: int = 64):
-        self.spec, self.cap, self.dense_every = spec, int(cap_ids), int(dense_every)
-        KP = spec.KP
-        self.ids = torch.zeros(self.cap, dtype=torch.int32, device=device)
-        self.vals = torch.zeros(self.cap * KP, dtype=torch.float32, device=device)
-        self.pos = 0
-        self.last = [-1] * num_workers
-        self.since = [0] * num_workers
-        self.sparse = self.dense = 0
-
-    def append(self, ubuf: torch.Tensor, dbuf: torch.Tensor, U: int):
-        KP, dev = self.spec.KP, self.ids.device
-        if U + 1 > self.cap:
-            raise ValueError("push larger than the pull log")
-        slots = (torch.arange(U + 1, device=dev) + self.pos) % self.cap
-        ids = torch.empty(U + 1, dtype=torch.int32, device=dev)
-        ids[0] = self.spec.F
-        ids[1:] = ubuf[:U]
-        self.ids[slots] = ids
-        self.vals.view(self.cap, KP)[slots] = dbuf[: (U + 1) * KP].view(U + 1, KP)
-        self.pos += U + 1
-
-    def plan(self, j: int):
-        """(kind, m, len1) of worker j's next pull, and the sends: [(tensor slice), ...]."""
-        KP, P = self.spec.KP, self.spec.P
-        m = -1 if self.last[j] < 0 else self.pos - self.last[j]
-        sparse = 0 <= m <= self.cap and m * (KP + 1) * 2 < P and self.since[j] < self.dense_every
-        self.last[j] = self.pos
-        if not sparse:
-            self.since[j] = 0
-            self.dense += 1
-            return 0, 0, 0, None
-        start = (self.pos - m) % self.cap
-        len1 = min(m, self.cap - start)
-        len2 = m - len1
-        parts = []
-        if len1:
-            parts += [self.ids[start:start + len1], self.vals[start * KP:(start + len1) * KP]]
-        if len2:
-            parts += [self.ids[:len2], self.vals[: len2 * KP]]
-        self.since[j] += 1
-        self.sparse += 1
-        return 1, m, len1, parts
-
-
 def pull_log_capacity(umax: int) -> int:
     """Ids the pull log keeps: ~16 pushes of the largest window subspace."""
     return 16 * (int(umax) + 1)
@@ -230,9 +179,14 @@ class DistEngine:
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, torch.device(device)
         self.async_mode = cfg.consistency_model != 0
         self.dedicated = self.async_mode or not cfg.server_colocated
-        n_workers = world - 1 if self.dedicated else world
-        if n_workers < 1:
+        wpr = max(1, int(cfg.workers_per_rank))
+        n_worker_ranks = world - 1 if self.dedicated else world
+        n_workers = n_worker_ranks * wpr
+        if n_worker_ranks < 1:
             raise ValueError("need at least one worker rank (world size >= 2 with a dedicated server)")
+        if wpr > 1 and (self.async_mode or cfg.bsp_schedule == "sharded" or torch.device(device).type != "cuda"):
+            raise ValueError("several workers per rank: BSP (allreduce / reduce_bcast) on GPUs only "
+                             "(the multi-lane round loop, csrc/runtime/lanes_loop.h)")
         if cfg.num_workers != n_workers:
             cfg.num_workers = n_workers
         if cfg.solver.persist and not (dist.is_initialized() and dist.get_backend() == "nccl"):
@@ -257,7 +211,8 @@ class DistEngine:
         # wide model: collectives and dense p2p pushes need the dense delta;
         # SSP/ASP with sparse_push send (feature ids, values) instead
         self.sparse_push = self.wide and self.async_mode and cfg.sparse_push
-        # ... and released workers pull the log entries since their last pull (PullLog)
+        # ... and released workers pull the log entries since their last pull (the native
+        # server's ring log, csrc/runtime/async_server.h)
         self.sparse_pull = self.sparse_push and cfg.sparse_pull
         if self.wide and not self.sparse_push:
             cfg.wide_dense_delta = True
@@ -296,9 +251,12 @@ class DistEngine:
         self.server = ServerRole(self.spec, cfg, self.device, self.evalset, w0) if (self.is_server or replicated) else None
         self.t0 = time.time()
         self.worker = None
+        self.workers = []
         if self.is_worker:
-            self.worker = WorkerRole(self.worker_id, self.spec, cfg, self.device, train.to(self.device), self.evalset,
-                                     t0=self.t0)
+            tr = train.to(self.device)
+            self.workers = [WorkerRole(self.worker_id * wpr + l, self.spec, cfg, self.device, tr, self.evalset,
+                                       t0=self.t0) for l in range(wpr)]
+            self.worker = self.workers[0]
         self.rounds = 0
         self._ctrl = None
         self._next_vc = 0
@@ -324,6 +282,7 @@ class DistEngine:
 
     # ------------------------------------------------------------------
     def run(self) -> dict:
+        self.mark_start()
         try:
             out = self._run_async() if self.async_mode else self._run_bsp()
         except BaseException:
@@ -341,6 +300,10 @@ class DistEngine:
                 out.update(summarize(self.log.book))
         self.tracer.close()
         return out
+
+    def mark_start(self):
+        if getattr(self, "train_start_ms", None) is None:  # epoch ms when training first began
+            self.train_start_ms = time.time() * 1000.0
 
     def close(self):
         """Release the native communicator (collective: every rank calls it)."""
@@ -381,8 +344,12 @@ class DistEngine:
             srv.frag.refresh(srv.w)
         if wk is not None:
             wk.w.copy_(boot)
-        # wait until every worker has data
-        while True:
+        if not hasattr(self, "comm"):  # created once per engine (init is ~0.1-0.5 s), closed by close()
+            self.comm = make_comm(self.rank, self.world, self.device)  # None: torch.distributed collectives
+        comm = self.comm
+        lanes = self._lanes_ok(sched, comm)
+        # wait until every worker has data (the multi-lane loop waits for its lanes itself)
+        while not lanes:
             if wk is not None:
                 wk.ingest()
             if self._all_ready():
@@ -391,9 +358,6 @@ class DistEngine:
         shard = (P + self.world - 1) // self.world
         if sched == "sharded":
             wfull, pad, myd = self._sharded_buffers(shard)
-        if not hasattr(self, "comm"):  # created once per engine (init is ~0.1-0.5 s), closed by close()
-            self.comm = make_comm(self.rank, self.world, self.device)  # None: torch.distributed collectives
-        comm = self.comm
         overlap = os.environ.get("PSX_COMM_OVERLAP", "0") == "1"
         N = cfg.num_workers
         lr = cfg.lr
@@ -407,7 +371,19 @@ class DistEngine:
             else:
                 vote = StopVote(self.device, torch.zeros(1, dtype=torch.float32, device=self.device), r)
         ingested_ahead = False
-        if vote is None and self._native_bsp_ok(sched, comm):
+        if vote is None and lanes:
+            # every round of this rank in the multi-lane loop: its workers' solves on their
+            # XCDs (one launch), the lane sum reduced to the server over RCCL, the update,
+            # the weights broadcast back (or all-reduced into every replica)
+            n = self._run_bsp_lanes(comm, cfg.max_iters)
+            r += n
+            if srv is not None:
+                srv.updates += N * n
+            for w in self.workers:
+                w.vc = r
+        elif len(self.workers) > 1:
+            raise RuntimeError("several workers per rank need the multi-lane loop (bounded BSP over RCCL)")
+        elif vote is None and self._native_bsp_ok(sched, comm):
             # every round of this rank enqueued by the native loop: solve (with the
             # previous rows riding in it) -> RCCL all-reduce -> update, no Python per round
             n = self._run_bsp_native(comm, cfg.max_iters)
@@ -542,6 +518,93 @@ class DistEngine:
                 "updates_per_s": r * N / elapsed if elapsed > 0 else 0.0,
                 "max_vc_gap": int(srv.tracker.max_gap) if (srv is not None and self.rank == 0) else 0}
 
+    def _lanes_ok(self, sched: str, comm) -> bool:
+        """The multi-lane round loop runs this rank's BSP rounds.  Decided from the
+        configuration alone, so every rank (the dedicated server has no workers)
+        reaches the same answer."""
+        c = self.cfg
+        if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or comm is None or not is_gpu(self.device):
+            return False
+        if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
+            return False
+        if not c.max_iters or c.max_wallclock_s or c.checkpoint_dir or c.iter_new_rows or c.iter_new_frac:
+            return False
+        if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop or c.dtype != "bf16":
+            return False
+        if c.stream_mode == "per_iter" and c.rows_per_iter <= 0 or (c.stream_mode != "per_iter"
+                                                                    and not c.producer_time_per_event > 0):
+            return False
+        o = c.solver
+        if o.nslots >= 64 or o.hist > 16:
+            return False
+        cap = -(-int(c.max_buffer_size) // 32) * 32
+        return bool(_native.hip().lanes_supported(self.spec.Fp, self.spec.K, cap))
+
+    def _run_bsp_lanes(self, comm, rounds: int) -> int:
+        from ..ops.lr import Fragments
+
+        cfg, srv, sp, W = self.cfg, self.server, self.spec, self.workers
+        w_main = srv.w if srv is not None else W[0].w
+        for w in W:
+            w.w = w_main
+            w.ring.flush()
+        if srv is not None and srv.pair is not None:
+            srv.pair.flush(self.log)
+        lp = getattr(self, "_lanes", None)
+        if lp is None:
+            h = _native.hip()
+            o = cfg.solver
+            sc = h.SolverCfg()
+            sc.K, sc.F, sc.Fp, sc.P, sc.cap = sp.K, sp.F, sp.Fp, sp.P, -(-int(cfg.max_buffer_size) // 32) * 32
+            sc.iters, sc.hist, sc.ls_max = o.iters, o.hist, o.ls_max
+            sc.mode = 1 if o.mode == "gd" else 0
+            sc.center, sc.zero_const = int(o.center), int(o.zero_const)
+            sc.nslots, sc.gd_lr, sc.tol = o.nslots, o.gd_lr, o.tol
+            d = dict(scfg=sc, N=int(cfg.num_workers), per_iter_rows=cfg.rows_per_iter if cfg.stream_mode == "per_iter"
+                     else 0, p_ms=float(cfg.producer_time_per_event), epochs=int(cfg.epochs), t0_ms=self.t0 * 1000.0,
+                     k=[w.k for w in W], X=[w.ring.X.data_ptr() for w in W], y=[w.ring.y.data_ptr() for w in W],
+                     window=[w.window.handle for w in W], w=w_main.data_ptr(), lr=float(cfg.lr),
+                     api=_native.host.capi(), server_rank=0, allreduce=int(cfg.bsp_schedule == "allreduce"),
+                     log_server=int(self.rank == 0), log_workers=int(bool(W)),
+                     sink=self.log.native.handle if self.log is not None else 0,
+                     tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0)
+            if W:
+                ds = W[0].source.ds
+                d.update(dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows))
+            if srv is not None:
+                self._lane_frags = [Fragments(sp, self.device), Fragments(sp, self.device)]
+                d.update(shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
+                         sb=[f.b.data_ptr() for f in self._lane_frags])
+            ev = self.evalset
+            d.update(Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T)
+            lp = h.LanesLoop(d, comm.c)
+            self._lanes = lp
+        elif self.log is not None:
+            lp.set_sink(self.log.native.handle)
+        for i, w in enumerate(W):
+            lp.set_next_local(i, int(w.source.next_local))
+        stream = comm.compute_stream()
+        try:
+            n = int(lp.run(int(rounds), int(self.rounds), stream))
+            lp.flush(stream)
+            torch.cuda.synchronize(self.device)
+            lp.poll_errors()
+        except RuntimeError as e:
+            if "cross-workgroup wait timed out" in str(e):
+                raise WorkerFailure(W[0].k if W else -1, str(e)) from e
+            raise
+        for i, w in enumerate(W):
+            w.source.next_local = int(lp.next_local(i))
+            w.iters += n
+            w._seen_at_solve = w.tuples_seen
+            lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+            if w.ring.XT is not None:
+                w.ring.xt_stale = True
+        if srv is not None and srv.frag is not None:
+            srv.frag.refresh(srv.w)
+        self.native_host_us_per_round = float(lp.host_us_per_round)
+        return n
+
     def _native_bsp_ok(self, sched: str, comm) -> bool:
         """The native BSP loop (csrc/runtime/bsp_loop.h) runs this rank: allreduce
         schedule over the native RCCL communicator, a colocated replica whose rows
@@ -629,30 +692,42 @@ class DistEngine:
         return self._shard_bufs
 
     # ------------------------------------------------------------------
-    def _open_ctrl(self):
+    def _open_ctrl(self, host_p2p: bool):
+        """The control plane (token queue, sparse-pull reply queues) and, for ranks
+        without an RCCL communicator (CPU / gloo), the host shared-memory data
+        plane (HostP2P): rank 0 creates, the workers attach after the barrier."""
         name = ctrl_queue_name()
         N = self.cfg.num_workers
+        h = _native.hip()
+        gpu = is_gpu(self.device)
+        self._hp2p = None
         if self.rank == 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, True)
             # sparse pull: one reply queue per worker tells it what its next pull carries
             self._replies = ([_native.host.CtrlQueue(f"{name}_r{j}"[:250], 64, True) for j in range(N)]
                              if self.sparse_pull else [])
+            if host_p2p:
+                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], N, 0, True, gpu, self._p2p_cap())
         dist.barrier()
         if self.rank != 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, False)
             self._reply = (_native.host.CtrlQueue(f"{name}_r{self.worker_id}"[:250], 64, False)
                            if self.sparse_pull else None)
+            if host_p2p:
+                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], N, self.rank, False, gpu, self._p2p_cap())
         dist.barrier()
 
+    def _p2p_cap(self) -> int:
+        """Bytes per HostP2P direction: a few of the largest messages (dense weights)."""
+        return max(1 << 20, 4 * 4 * int(self.spec.P))
+
     def _run_async(self) -> dict:
-        self._open_ctrl()
         if not hasattr(self, "comm"):  # collective: every rank creates it (None on gloo / CPU)
             self.comm = make_comm(self.rank, self.world, self.device)
+        self._open_ctrl(host_p2p=self.comm is None)
         try:
-            if self.is_server:
-                if self.comm is not None and os.environ.get("PSX_NATIVE_ASYNC", "1") != "0":
-                    return self._server_loop_native()
-                return self._server_loop()
+            if self.is_server:  # ONE server loop: the native one (RCCL p2p, or HostP2P without RCCL)
+                return self._server_loop_native()
             return self._worker_loop()
         finally:
             dist.barrier()
@@ -660,131 +735,22 @@ class DistEngine:
                 self._ctrl.unlink()
                 for q in getattr(self, "_replies", []):
                     q.unlink()
-
-    def _server_loop(self) -> dict:
-        cfg, srv = self.cfg, self.server
-        N = cfg.num_workers
-        buf = torch.zeros(self.spec.P, dtype=torch.float32, device=self.device) if not self.sparse_push else None
-        if self.sparse_push:
-            KP = self.spec.KP
-            ubuf = torch.zeros(self._umax, dtype=torch.int32, device=self.device)
-            dbuf = torch.zeros(KP + self._umax * KP, dtype=torch.float32, device=self.device)
-        dead = self.__dict__.setdefault("_dead_workers", set())  # failed in any run: stay retired
-        finished = set(dead)
-        failed = set(dead)
-        plog = None
-        if self.sparse_pull:
-            if getattr(self, "_pull_log", None) is None:
-                self._pull_log = PullLog(self.spec, pull_log_capacity(self._umax), N, self.device)
-            plog = self._pull_log
-            plog.last = [-1] * N  # every run starts with a dense pull
-
-        def release(j: int, u: int):
-            """Send worker j the weights of clock u: the dense vector, or (sparse pull)
-            the log entries since its previous pull, announced on its reply queue."""
-            if plog is None:
-                dist.send(srv.w, dst=j + 1)
-                return
-            kind, m, len1, parts = plog.plan(j)
-            r = _native.host.CtrlToken()
-            r.worker, r.kind, r.vc, r.n, r.aux = j, kind, u, m, len1
-            if not self._replies[j].push(r, 600.0):
-                raise TimeoutError(f"reply queue of worker {j} full")
-            if kind == 0:
-                dist.send(srv.w, dst=j + 1)
-            else:
-                for t in parts:
-                    dist.send(t.contiguous(), dst=j + 1)
-
-        for j in range(N):  # bootstrap: vc 0 to every worker (tracker untouched)
-            if j in dead:
-                continue
-            if not srv.tracker.is_live(j):  # finished the previous run of this engine: rejoins
-                srv.tracker.revive(j)
-            if srv.tracker.clock(j) > 0:  # a later run of this engine: resume at the tracked clocks
-                srv.tracker.sent(j, srv.tracker.clock(j))
-            release(j, int(srv.tracker.clock(j)))
-        t_start = time.time()
-        busy_since = {j: t_start for j in range(N)}  # weights sent, delta not back yet (watchdog)
-
-        def fail(k: int, reason: str):
-            if not drop_on_failure(cfg):
-                raise WorkerFailure(k, reason)
-            print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
-            failed.add(k)
-            finished.add(k)
-            dead.add(k)
-            busy_since.pop(k, None)
-            for j, u in srv.tracker.retire(k):
-                if j not in finished:
-                    release(j, u)
-                    busy_since[j] = time.time()
-
-        while len(finished) < N:
-            tok = self._ctrl.pop(min(1.0, cfg.worker_timeout_s))
-            if tok is None:
-                now = time.time()
-                for j, since in list(busy_since.items()):
-                    if j not in finished and now - since > cfg.worker_timeout_s:
-                        fail(j, f"silent for {now - since:.0f} s while busy (watchdog)")
-                continue
-            if tok.kind == KIND_ERROR:
-                fail(int(tok.worker), "reported an error")
-                continue
-            k, v = int(tok.worker), int(tok.vc)
-            with self.tracer.span("recv", worker=k, vc=v):
-                if self.sparse_push:
-                    U = int(tok.n)
-                    if U:
-                        dist.recv(ubuf[:U], src=k + 1)
-                    dist.recv(dbuf[: KP + U * KP], src=k + 1)
-                    delta = SparseDelta(self.spec, ubuf, dbuf, U)
-                else:
-                    dist.recv(buf, src=k + 1)
-                    delta = buf
-            busy_since.pop(k, None)
-            # server eval rows follow the deltas of worker 0 (ServerProcessor.java:154-165),
-            # or of the lowest surviving worker once 0 has failed
-            if k == min(j for j in range(N) if j not in failed):
-                srv.apply_and_log(delta, v, self.log)
-            else:
-                srv.apply(delta)
-            if plog is not None:
-                plog.append(ubuf, dbuf, U)
-            srv.updates += 1
-            released = srv.tracker.on_delta(k, v)
-            if tok.kind == KIND_FINAL:
-                # a finished worker no longer holds the others back (its clock would
-                # freeze min_clock: an SSP worker D ahead would wait forever)
-                finished.add(k)
-                released = list(released) + list(srv.tracker.retire(k))
-            for j, u in released:
-                if j in finished:
-                    continue
-                release(j, u)
-                busy_since[j] = time.time()
-            maybe_checkpoint(cfg, srv, srv.updates)
-            if self.log is not None:
-                self.log.drain()
-        if is_gpu(self.device):
-            torch.cuda.synchronize(self.device)
-        elapsed = time.time() - t_start
-        return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
-                "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
-                "failed_workers": sorted(failed), "sparse_pulls": plog.sparse if plog else 0,
-                "dense_pulls": plog.dense if plog else 0}
+            if self._hp2p is not None:
+                self._hp2p.unlink()
+                self._hp2p = None
 
     def _native_server(self):
         """The C++ server loop (csrc/runtime/async_server.h) bound to this engine's
         tensors, token queue, tracker and metrics sink (created once per engine)."""
         a = getattr(self, "_aserver", None)
-        if a is not None:
+        if a is not None and getattr(self, "_aserver_p2p", None) is (self._hp2p or self.comm):
             return a
         cfg, srv, spec = self.cfg, self.server, self.spec
         h = _native.hip()
+        gpu = is_gpu(self.device)
         d = dict(nworkers=cfg.num_workers, lr=float(cfg.lr), P=int(spec.P), w=srv.w.data_ptr(),
                  api=_native.host.capi(), tracker=srv.tracker.handle, ctrl=self._ctrl.handle,
-                 worker_timeout_s=float(cfg.worker_timeout_s))
+                 worker_timeout_s=float(cfg.worker_timeout_s), cpu=0 if gpu else 1)
         keep = []
         if self.wide:
             d.update(KP=spec.KP, K=spec.K, Fw=int(spec.F))
@@ -808,9 +774,10 @@ class DistEngine:
         else:
             buf = torch.zeros(spec.P, dtype=torch.float32, device=self.device)
             keep.append(buf)
+            d.update(model=0, buf=buf.data_ptr(), K=spec.K, F=spec.F, FP=spec.Fp)
             fr = srv.frag
-            d.update(model=0, buf=buf.data_ptr(), K=spec.K, F=spec.F, FP=spec.Fp, coff=fr.coff, fhi=fr.hi.data_ptr(),
-                     flo=fr.lo.data_ptr(), fb=fr.b.data_ptr())
+            if fr is not None:  # (GPU: the evaluation reads the model's MFMA fragments)
+                d.update(coff=fr.coff, fhi=fr.hi.data_ptr(), flo=fr.lo.data_ptr(), fb=fr.b.data_ptr())
         ev = self.evalset
         if self.log is not None and ev is not None:
             d.update(sink=self.log.native.handle, acc=srv.scratch.acc.data_ptr(), ticket=srv.scratch.ticket.data_ptr(),
@@ -821,9 +788,9 @@ class DistEngine:
                          t_y=ds.y.data_ptr())
             else:
                 d.update(Xt=ev.X.data_ptr(), yt=ev.y.data_ptr())
-        p2p = h.RcclP2P(self.comm.c)
-        a = h.AsyncServer(p2p, d, torch.cuda.current_stream(self.device).cuda_stream)
-        self._aserver, self._aserver_keep = a, keep + [p2p]
+        p2p = self._hp2p if self._hp2p is not None else h.RcclP2P(self.comm.c)
+        a = h.AsyncServer(p2p, d, torch.cuda.current_stream(self.device).cuda_stream if gpu else 0)
+        self._aserver, self._aserver_keep, self._aserver_p2p = a, keep + [p2p], (self._hp2p or self.comm)
         return a
 
     def _server_loop_native(self) -> dict:
@@ -840,7 +807,8 @@ class DistEngine:
                 self._aserver = None
                 a = self._native_server()
             self._aserver_sink = self.log.native.handle
-        a.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        gpu = is_gpu(self.device)
+        a.set_stream(torch.cuda.current_stream(self.device).cuda_stream if gpu else 0)
         a.updates = srv.updates
         t_start = time.time()
         u0 = srv.updates
@@ -858,7 +826,8 @@ class DistEngine:
                 raise WorkerFailure(int(k), reason)
             print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
             a.fail(int(k))
-        torch.cuda.synchronize(self.device)
+        if gpu:
+            torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start
         n = srv.updates - u0
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
@@ -874,11 +843,22 @@ class DistEngine:
         gpu = is_gpu(self.device)
         done = torch.cuda.Event() if gpu else None
 
+        hp = self._hp2p  # no RCCL communicator: the host shared-memory data plane
+
+        def _stream():
+            return torch.cuda.current_stream(self.device).cuda_stream if gpu else 0
+
         def send(t):
-            comm.send(t, 0) if comm is not None else dist.send(t, dst=0)
+            if comm is not None:
+                comm.send(t, 0)
+            else:
+                hp.send(t.data_ptr(), t.numel(), _p2p_dtype(t), 0, _stream())
 
         def recv(t):
-            comm.recv(t, 0) if comm is not None else dist.recv(t, src=0)
+            if comm is not None:
+                comm.recv(t, 0)
+            else:
+                hp.recv(t.data_ptr(), t.numel(), _p2p_dtype(t), 0, _stream())
 
         KP = self.spec.KP if self.wide else 0
         if self.sparse_pull:  # receive buffers of the largest pull the log can send
@@ -963,7 +943,7 @@ class DistEngine:
                 if U:
                     send(delta.uniq[:U])
                 send(delta.dloc[: KP + U * KP])
-            elif not early:  # gloo sends block until received: only after the token
+            elif not early:  # (host transport: written after the token, read when the server serves it)
                 send(delta)
             if final:
                 break
@@ -976,6 +956,12 @@ class DistEngine:
             torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start
         return {"rounds": it, "updates": it, "elapsed_s": elapsed}
+
+
+def _p2p_dtype(t: torch.Tensor) -> int:
+    from .comm import _dtype
+
+    return _dtype(t)
 
 
 def run_distributed(cfg: PSConfig, cpu: bool = False, train=None, test=None) -> dict:

@@ -65,6 +65,9 @@ class PSConfig:
     # distributed
     bsp_schedule: str = "allreduce"  # allreduce | reduce_bcast | sharded
     server_colocated: bool = True
+    # logical workers per worker rank (one XCD each: the multi-lane round loop);
+    # the reference hosts all of its workers in one process (BaseKafkaApp.java:25,70)
+    workers_per_rank: int = 1
     # checkpoint
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0

@@ -160,7 +160,11 @@ class LocalEngine:
             return True
         return False
 
-    def run(self) -> dict:
+    def run(self, close_log: bool = True) -> dict:
+        """Run until the configured stop (max_iters / wall clock / data).  close_log
+        False: the log sink stays open for a later run (its rows are flushed)."""
+        if getattr(self, "train_start_ms", None) is None:  # epoch ms when training first began
+            self.train_start_ms = time.time() * 1000.0
         live = [w for w in self.workers if w.k not in self.failed]
         if self.cfg.consistency_model == 0 or len(live) == 1:
             # with a single worker every consistency model releases that worker right
@@ -172,11 +176,13 @@ class LocalEngine:
         else:
             out = self._run_async()
         flush_checkpoints(self.cfg)
-        for w in self.workers:
-            if w.k not in self.failed:
-                w.check_device_health()
-        self.log.close()
-        self.tracer.close()
+        if not out.get("lanes"):  # (the multi-lane loop raises on a device error itself)
+            for w in self.workers:
+                if w.k not in self.failed:
+                    w.check_device_health()
+        if close_log:
+            self.log.close()
+            self.tracer.close()
         if self.log.book is not None:
             out.update(summarize(self.log.book))
         out["max_vc_gap"] = int(self.server.tracker.max_gap)
@@ -218,6 +224,133 @@ class LocalEngine:
         if ring.f32 or ring.XT is None or wk.source.ds.X.dtype != torch.bfloat16:
             return False
         return wk.solver.can_ride(ring, srv.w)
+
+    def _lanes_ok(self) -> bool:
+        """The multi-lane round loop (csrc/runtime/lanes_loop.h) runs this BSP run:
+        1..8 dense GPU workers with bf16 rings of <= 1024 rows, ONE launch per round
+        (every worker's solve on its own XCD, the update, the previous round's
+        evaluation rows).  Runs that need Python between rounds (tracing, injected
+        faults, a tuple-driven cadence) use the loops below."""
+        c = self.cfg
+        if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
+            return False
+        W = [w for w in self.workers if w.k not in self.failed]
+        if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
+            return False
+        if c.iter_new_rows or c.iter_new_frac or c.inject_worker_delay_ms or c.inject_worker_crash \
+                or c.inject_worker_stop:
+            return False
+        sp = self.spec
+        for w in W:
+            if w.wide or w.ring.f32 or w.source.ds.X.dtype != torch.bfloat16:
+                return False
+            if (w.source.mode == "per_iter" and w.source.rows_per_iter <= 0) or (
+                    w.source.mode != "per_iter" and not w.source.p_ms > 0):
+                return False
+        if w.solver.opts.nslots >= 64 or w.solver.opts.hist > 16:
+            return False
+        return bool(_native.hip().lanes_supported(sp.Fp, sp.K, W[0].ring.cap))
+
+    def _lanes_loop(self, W):
+        """The native loop bound to this engine's rings / windows / server (built
+        once per set of workers; the metrics sink is rebound per run)."""
+        key = tuple(w.k for w in W)
+        lp = getattr(self, "_lanes", None)
+        if lp is not None and self._lanes_key == key:
+            lp.set_sink(self.log.native.handle)
+            lp.set_lr(float(self.cfg.lr))
+            return lp
+        from ..ops.lr import Fragments
+
+        h, sp, cfg, srv = _native.hip(), self.spec, self.cfg, self.server
+        o = W[0].solver.opts
+        sc = h.SolverCfg()
+        sc.K, sc.F, sc.Fp, sc.P, sc.cap = sp.K, sp.F, sp.Fp, sp.P, W[0].ring.cap
+        sc.iters, sc.hist, sc.ls_max = o.iters, o.hist, o.ls_max
+        sc.mode = 1 if o.mode == "gd" else 0
+        sc.center, sc.zero_const = int(o.center), int(o.zero_const)
+        sc.nslots, sc.gd_lr, sc.tol = o.nslots, o.gd_lr, o.tol
+        self._lane_frags = [Fragments(sp, self.device), Fragments(sp, self.device)]
+        src0, ev = W[0].source, self.evalset
+        d = dict(scfg=sc, dsX=src0.ds.X.data_ptr(), dsy=src0.ds.y.data_ptr(), ds_rows=int(src0.ds.rows),
+                 N=int(cfg.num_workers), per_iter_rows=src0.rows_per_iter if src0.mode == "per_iter" else 0,
+                 p_ms=float(src0.p_ms), epochs=int(src0.epochs), t0_ms=float(src0.t0) * 1000.0,
+                 k=[w.k for w in W], X=[w.ring.X.data_ptr() for w in W], y=[w.ring.y.data_ptr() for w in W],
+                 window=[w.window.handle for w in W], w=srv.w.data_ptr(), lr=float(cfg.lr),
+                 shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
+                 sb=[f.b.data_ptr() for f in self._lane_frags], scoff=0, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(),
+                 T=ev.T, sink=self.log.native.handle, tracker=srv.tracker.handle, api=_native.host.capi())
+        lp = h.LanesLoop(d, None)
+        if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
+            rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
+            lp.inject_spin_timeout(int(rr), int(sp_))
+        self._lanes, self._lanes_key = lp, key
+        return lp
+
+    def _run_bsp_lanes(self) -> dict:
+        """BSP rounds of every live worker in the native multi-lane loop: one launch
+        per round, no Python per round.  An unbounded run (max_iters 0: until the
+        data or the wall clock says stop) and checkpoints run in chunks of rounds."""
+        cfg, srv = self.cfg, self.server
+        W = [w for w in self.workers if w.k not in self.failed]
+        for w in W:
+            w.w = srv.w
+            w.ring.flush()
+        if srv.pair is not None:
+            srv.pair.flush(self.log)  # nothing may be pending from an earlier run
+        lp = self._lanes_loop(W)
+        for i, w in enumerate(W):
+            lp.set_next_local(i, int(w.source.next_local))
+        stream = stream_handle(self.device)
+        t_start = time.time()
+        r0 = r = self.rounds
+        u0 = srv.updates
+        chunk = 256
+        if cfg.checkpoint_dir and cfg.checkpoint_every:
+            chunk = max(1, int(cfg.checkpoint_every))
+        try:
+            while True:
+                todo = chunk
+                if cfg.max_iters:
+                    todo = min(todo, cfg.max_iters - (r - r0))
+                    if todo <= 0:
+                        break
+                if cfg.max_wallclock_s and time.time() - t_start >= cfg.max_wallclock_s:
+                    break
+                n = int(lp.run(int(todo), int(r), stream))
+                r += n
+                for i, w in enumerate(W):
+                    w.source.next_local = int(lp.next_local(i))
+                if n:
+                    maybe_checkpoint(cfg, srv, r, W)
+                if n < todo:  # a worker's stream is exhausted and its window empty
+                    break
+            lp.flush(stream)
+            torch.cuda.synchronize(self.device)
+            lp.poll_errors()  # a device error of the last rounds (the loop polls without syncs)
+        except RuntimeError as e:
+            if "cross-workgroup wait timed out" in str(e):
+                raise WorkerFailure(W[0].k, str(e)) from e
+            raise
+        n = r - r0
+        srv.updates += n * len(W)
+        for i, w in enumerate(W):  # the last local solve's loss / delta, for code that reads the roles
+            lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+        for w in W:
+            w.vc = r
+            w.iters += n
+            w._seen_at_solve = w.tuples_seen
+            if w.ring.XT is not None:
+                w.ring.xt_stale = True  # the round kernel writes the row-major ring only
+        if srv.frag is not None:
+            srv.frag.refresh(srv.w)  # the Python-side evaluation fragments follow the native update
+        self.native_host_us_per_round = float(lp.host_us_per_round)
+        torch.cuda.synchronize(self.device)
+        elapsed = time.time() - t_start
+        self.rounds = r
+        return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True,
+                "lanes": len(W), "hand_off_scope": int(lp.hand_off_scope)}
 
     def _run_bsp_native(self) -> dict:
         """BSP rounds in the native loop: every round enqueued from C++ (producer,
@@ -265,6 +398,8 @@ class LocalEngine:
                 "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True}
 
     def _run_bsp(self) -> dict:
+        if self._lanes_ok():
+            return self._run_bsp_lanes()
         if self._native_bsp_ok():
             return self._run_bsp_native()
         cfg, srv = self.cfg, self.server

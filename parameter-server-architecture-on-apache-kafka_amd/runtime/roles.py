@@ -398,7 +398,7 @@ class EvalPair:
     def defer_server_row(self, log, vc: int, ts: int | None):
         if self.pending is not None:
             self.flush(self.pending[0])
-        self.pending = (log, int(vc), int(ts) if ts is not None else int(time.time() * 1000))
+        self.pending = (log, int(vc), int(ts) if ts is not None else -1)  # -1: stamped when evaluated
 
     def worker_row(self, log):
         wk = self.worker
@@ -406,7 +406,7 @@ class EvalPair:
             return
         self.flush_worker()
         if self.shared:  # evaluated together with the server update that follows
-            self.pending_worker = (log, int(wk.vc), int(wk.tuples_seen), int(time.time() * 1000))
+            self.pending_worker = (log, int(wk.vc), int(wk.tuples_seen), -1)
             return
         pend, srv = self.pending, self.server
         if (pend is not None and pend[0] is log and self.wide_pair and wk.w.data_ptr() == srv.w.data_ptr()):

@@ -26,7 +26,9 @@ def now_ms() -> int:
 
 
 class RecordBook:
-    """In-memory copy of every logged row (tests, benchmarks, plots)."""
+    """In-memory copy of every logged row (tests, benchmarks, plots).  Row
+    timestamps are epoch milliseconds as floats: rows submitted without one are
+    stamped (us resolution) when their evaluation completed."""
 
     def __init__(self, worker=None, server=None):
         self.worker = worker if worker is not None else []  # (ts, partition, vc, loss, f1, acc, nseen)
@@ -75,14 +77,14 @@ class LogSink:
                     ts: int | None = None):
         """Evaluate the worker's local model ``w`` and log a worker row."""
         slot, seq, addr = self.native.acquire()
-        ts = ts or now_ms()
+        ts = -1 if ts is None else ts  # -1: stamped by the sink when the evaluation lands
         evalset.eval_to_slot(frag, w, scratch, addr, seq, loss_dev)
         self.native.submit(slot, seq, 0, ts, int(partition), int(vc), int(nseen))
 
     def server_eval(self, evalset, frag, w, scratch, vc: int, ts: int | None = None):
         """Evaluate the global model ``w`` and log a server row."""
         slot, seq, addr = self.native.acquire()
-        ts = ts or now_ms()
+        ts = -1 if ts is None else ts
         evalset.eval_to_slot(frag, w, scratch, addr, seq, None)
         self.native.submit(slot, seq, 1, ts, -1, int(vc), 0)
 
@@ -94,7 +96,7 @@ class LogSink:
         slot_s = seq_s = addr_s = 0
         if vc_s is not None:
             slot_s, seq_s, addr_s = self.native.acquire()
-        ts_w = now_ms() if ts_w is None else int(ts_w)
+        ts_w = -1 if ts_w is None else int(ts_w)
         evalset.eval_pair_to_slots(frag_w, w_w, frag_s, w_s, scratch, addr_w, seq_w, loss_dev, addr_s, seq_s, apply)
         if vc_s is not None:
             self.native.submit(slot_s, seq_s, 1, int(ts_s), -1, int(vc_s), 0)

@@ -186,3 +186,21 @@ def test_engine_lanes_fault_maps_to_worker_failure(cuda, monkeypatch):
     with pytest.raises(WorkerFailure):
         eng.run()
     torch.cuda.synchronize()
+
+
+def test_lanes_ring_rows_across_epoch_wrap(cuda):
+    """Deliveries that wrap a worker's shard (the producer's next epoch) land in the
+    ring inside the round kernel: slot s after round r holds the worker's tuple
+    1024 r + s, i.e. dataset row k + ((1024 r + s) mod shard) * N."""
+    spec, train, ev = _data(cuda, rows=3000)  # 1500 rows per worker: round 1 wraps
+    w = spec.init("random", seed=2, device=cuda)
+    lp, (rings, wins, frags) = _loop(spec, [0, 1], 2, train, ev, w, cuda)
+    for rnd in range(3):
+        lp.run(1, rnd, stream_handle(cuda))
+        torch.cuda.synchronize()
+        for k in (0, 1):
+            j = torch.arange(1024) + 1024 * rnd
+            rows = k + (j % 1500) * 2
+            X, y = rings[k]
+            assert torch.equal(X.cpu(), train.X[rows.to(cuda)].cpu()), (rnd, k)
+            assert torch.equal(y.cpu(), train.y[rows.to(cuda)].cpu()), (rnd, k)

@@ -21,7 +21,8 @@ push on arrival).  Nothing is skipped inside the timed region.
     1..5, ASP with a dedicated server rank (world >= 2; one GPU: in-process).
 --model sharded100m  (config 5): 10M rows x 10^8 hashed features, binary
     sigmoid model, P = 10^8 + 1 dense fp32 weights, BSP key-range sharded
-    server (reduce-scatter of the dense delta + all-gather of the weights).
+    server: every rank stores only its key range; a round pulls / pushes only
+    the ids the windows touch (psx/parallel/keyrange.py).
 
 value = server-applied updates per second over ALL workers.
 vs_baseline = value / reference updates/s (dense: 0.76 for 1 worker, 1.85 for
@@ -55,7 +56,7 @@ MODELS = {
     "dense": dict(features=1024, train_rows=90000, test_rows=4877, consistency=0, schedule="allreduce"),
     "sparse1m": dict(features=1 << 20, train_rows=10_000_000, test_rows=20000, consistency=-1, schedule="allreduce"),
     "sharded100m": dict(features=100_000_000, train_rows=10_000_000, test_rows=20000, consistency=0,
-                        schedule="sharded"),
+                        schedule="keyrange"),
 }
 
 
@@ -82,7 +83,7 @@ def parse(argv=None):
     ap.add_argument("--workers", type=int, default=None,
                     help="logical workers per worker GPU, one XCD each in one launch per round (default 4: the "
                          "reference's numWorkers = 4, all hosted in one process, BaseKafkaApp.java:25,70)")
-    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded"])
+    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded", "keyrange"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--persist", action="store_true",
@@ -110,8 +111,10 @@ def parse(argv=None):
     for k in ("features", "train_rows", "test_rows", "consistency"):
         if getattr(a, k) is None:
             setattr(a, k, m[k])
-    if a.schedule is None and m["schedule"] == "sharded":
-        a.schedule = "sharded"
+    if a.schedule is None and m["schedule"] == "keyrange":
+        a.schedule = "keyrange"
+    if a.schedule == "sharded" and wide:
+        a.schedule = "keyrange"  # the wide model's sharded server is the key-range one
     if a.rows_per_step is None:
         a.rows_per_step = 64 if wide else a.buffer
     if a.steps is None:
@@ -200,7 +203,10 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
     mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
     backend = _backend_label()
     lanes = f"{wpr} workers/GPU, one XCD each" if wpr > 1 else "1 worker/GPU"
-    if world == 1:
+    if cfg.bsp_schedule == "keyrange":
+        par = (f"ps-{mode} key-range sharded server x{world} (every rank: 1 worker + the shard of its key "
+               f"range; pull/push of the window's ids over {backend if world > 1 else 'local copies'})")
+    elif world == 1:
         par = f"ps-{mode} w{n_workers} (server colocated, {lanes if n_workers > 1 else '1 worker'})"
     elif async_mode:
         par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
@@ -275,7 +281,7 @@ def main(argv=None):
     world = int(world_env or "1")
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} ranks")
-    if world > 1 or os.environ.get("PSX_BENCH_DIST") == "1":
+    if world > 1 or os.environ.get("PSX_BENCH_DIST") == "1" or a.schedule == "keyrange":
         # PSX_BENCH_DIST=1 with one rank: the multi-rank code path (DistEngine, RCCL
         # communicator, all-reduce + update launch per round) rehearsed on one GPU
         return bench_distributed(a)
@@ -401,7 +407,8 @@ def bench_distributed(a):
     if dist.get_world_size() != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
     async_mode = a.consistency != 0
-    dedicated = async_mode or a.dedicated_server
+    keyrange = a.schedule == "keyrange"
+    dedicated = (async_mode or a.dedicated_server) and not keyrange  # key-range: every rank holds a shard
     wpr = 1 if (async_mode or a.model != "dense" or a.cpu) else a.workers
     worker_ranks = world - 1 if dedicated else world
     cfg = build_cfg(a, worker_ranks * wpr)
@@ -411,6 +418,8 @@ def bench_distributed(a):
         cfg.bsp_schedule = a.schedule if a.schedule != "reduce_bcast" or dedicated else "allreduce"
         if dedicated and cfg.bsp_schedule == "allreduce":
             cfg.bsp_schedule = "reduce_bcast"
+    if keyrange:
+        cfg.bsp_schedule = "keyrange"
     train, test = make_data(a, device)
     cfg.max_iters = a.warmup
     eng = DistEngine(cfg, rank, world, device, train=train, test=test)
@@ -448,6 +457,10 @@ def bench_distributed(a):
         ups = a.steps * cfg.num_workers / dt
         res = describe(a, world, cfg, ups, dt, summ, rccl_ranks=rccl, topo=topo)
         res["max_vc_gap"] = out.get("max_vc_gap")
+        if "keyrange" in out:
+            k = out["keyrange"]
+            res["keyrange"] = dict(k, model_bytes_per_round=round(k["model_bytes"] / max(1, a.steps + a.warmup), 1),
+                                   dense_vector_bytes=(a.features + 1) * 4)
         res.update(_accuracy_fields(list(book.server), timed_from=n_warm, start_ms=eng.train_start_ms))
         if rccl is not None and rccl != world:
             raise SystemExit(f"bench.py: RCCL communicator has {rccl} ranks, world is {world}")

@@ -14,6 +14,7 @@
 #include "../runtime/async_server.h"
 #include "../runtime/bsp_loop.h"
 #include "../runtime/lanes_loop.h"
+#include "../runtime/keyrange_loop.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
 #include "../solver/wide_solver.h"
@@ -351,7 +352,10 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("standardize", &WideCfg::standardize)
       .def_readwrite("center", &WideCfg::center)
       .def_readwrite("zero_const", &WideCfg::zero_const)
-      .def_readwrite("dense_delta", &WideCfg::dense_delta);
+      .def_readwrite("dense_delta", &WideCfg::dense_delta)
+      .def_readwrite("pulled", &WideCfg::pulled)
+      .def_readwrite("own_W", &WideCfg::own_W)
+      .def_readwrite("own_S", &WideCfg::own_S);
 
   py::class_<RcclComm>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
@@ -399,8 +403,10 @@ PYBIND11_MODULE(_psx_hip, m) {
   py::class_<WideSolver>(m, "WideSolver")
       .def(py::init([](const WideCfg& cfg, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz, uintptr_t ry,
                        uintptr_t w_old, uintptr_t dloc, uintptr_t wloc, uintptr_t loss, uintptr_t stats,
-                       uintptr_t uniq, uintptr_t delta_dense, bool use_graph) {
+                       uintptr_t uniq, uintptr_t delta_dense, bool use_graph, uintptr_t w_pull, uintptr_t w_pull_b) {
              WideBuffers b;
+             b.w_pull = P<const float>(w_pull);
+             b.w_pull_b = P<const float>(w_pull_b);
              b.uniq = P<int32_t>(uniq);
              b.ridx = P<const int32_t>(ridx);
              b.rval = P<const uint16_t>(rval);
@@ -416,8 +422,23 @@ PYBIND11_MODULE(_psx_hip, m) {
            }),
            py::arg("cfg"), py::arg("ridx"), py::arg("rval"), py::arg("rnnz"), py::arg("ry"), py::arg("w_old"),
            py::arg("dloc"), py::arg("wloc"), py::arg("loss"), py::arg("stats"), py::arg("uniq"), py::arg("delta_dense") = 0,
-           py::arg("use_graph") = true)
+           py::arg("use_graph") = true, py::arg("w_pull") = 0, py::arg("w_pull_b") = 0)
       .def("run", [](WideSolver& s, int B, int start, uintptr_t stream) { s.run(B, start, S(stream)); })
+      .def("plan", [](WideSolver& s, int B, int start, uintptr_t stream) { s.plan(B, start, S(stream)); })
+      .def("finish", [](WideSolver& s, uintptr_t stream) { s.finish(S(stream)); })
+      .def_property_readonly("owner_counts_ptr",
+                             [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.owner_counts_dev()); })
+      // (tests) U of the last plan and the per-owner counts, read after a sync
+      .def("read_plan",
+           [](const WideSolver& s, uintptr_t stream) {
+             std::vector<unsigned> v(1 + kMaxOwners);
+             hip_check(hipMemcpyAsync(v.data(), s.ucount_dev(), 4, hipMemcpyDeviceToHost, S(stream)), "read U");
+             hip_check(hipMemcpyAsync(v.data() + 1, s.owner_counts_dev(), kMaxOwners * 4, hipMemcpyDeviceToHost,
+                                      S(stream)),
+                       "read owner counts");
+             hip_check(hipStreamSynchronize(S(stream)), "sync");
+             return v;
+           })
       .def("read_ctrl",
            [](WideSolver& s, uintptr_t stream) {
              Ctrl c;
@@ -427,7 +448,8 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("read_stamps", [](WideSolver& s, uintptr_t stream) { return s.read_stamps(S(stream)); })
       .def_property_readonly("plmax", &WideSolver::plmax)
       .def_property_readonly("umax", [](const WideSolver& s) { return s.cfg().umax; })
-      .def_property_readonly("map_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.map()); })
+      .def_property_readonly("table_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.table()); })
+      .def_property_readonly("table_mask", &WideSolver::table_mask)
       .def_property_readonly("uniq_ptr", [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.uniq()); })
       .def_property_readonly("ucount_ptr",
                              [](const WideSolver& s) { return reinterpret_cast<uintptr_t>(s.ucount_dev()); })
@@ -446,20 +468,24 @@ PYBIND11_MODULE(_psx_hip, m) {
   m.def(
       "wide_eval",
       [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int T, uintptr_t w,
-         uintptr_t map, uintptr_t wloc, uintptr_t acc, uintptr_t ticket, uintptr_t slot, uintptr_t loss,
-         unsigned long long seq, uintptr_t stream, uintptr_t slot2, unsigned long long seq2) {
-        if (slot2 && (!slot || !map || !wloc))
-          throw std::invalid_argument("wide_eval: the paired row needs a slot and the overlay");
+         uintptr_t table, unsigned mask, uintptr_t wloc, uintptr_t acc, uintptr_t ticket, uintptr_t slot,
+         uintptr_t loss, unsigned long long seq, uintptr_t stream, uintptr_t slot2, unsigned long long seq2,
+         uintptr_t zbase, uintptr_t bias) {
+        if (slot2 && (!slot || !table || !wloc || !w))
+          throw std::invalid_argument("wide_eval: the paired row needs a slot, the dense model and the overlay");
+        if (!w && !zbase) throw std::invalid_argument("wide_eval: need the model or the margins base");
+        if (!w && !bias && !table) throw std::invalid_argument("wide_eval: key-range form needs the intercepts");
+        if (table && !wloc) throw std::invalid_argument("wide_eval: overlay table without values");
         launch_wide_eval(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val),
-                         P<const int32_t>(y), T, P<const float>(w), P<const int32_t>(map), P<const float>(wloc),
+                         P<const int32_t>(y), T, P<const float>(w), P<const int2>(table), mask, P<const float>(wloc),
                          P<int>(acc), P<unsigned>(ticket), P<void>(slot), P<const float>(loss), seq, S(stream),
-                         P<void>(slot2), seq2);
+                         P<void>(slot2), seq2, P<const float>(zbase), P<const float>(bias));
         hip_check(hipGetLastError(), "wide_eval launch");
       },
       py::arg("K"), py::arg("KP"), py::arg("F"), py::arg("indptr"), py::arg("idx"), py::arg("val"), py::arg("y"),
-      py::arg("T"), py::arg("w"), py::arg("map"), py::arg("wloc"), py::arg("acc"), py::arg("ticket") = 0,
-      py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0, py::arg("stream") = 0, py::arg("slot2") = 0,
-      py::arg("seq2") = 0);
+      py::arg("T"), py::arg("w"), py::arg("table"), py::arg("mask"), py::arg("wloc"), py::arg("acc"),
+      py::arg("ticket") = 0, py::arg("slot") = 0, py::arg("loss") = 0, py::arg("seq") = 0, py::arg("stream") = 0,
+      py::arg("slot2") = 0, py::arg("seq2") = 0, py::arg("zbase") = 0, py::arg("bias") = 0);
   m.def("wide_logits", [](int K, int KP, int64_t F, uintptr_t indptr, uintptr_t idx, uintptr_t val, int T,
                           uintptr_t w, uintptr_t out, uintptr_t stream) {
     launch_wide_logits(K, KP, F, P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val), T,
@@ -726,6 +752,76 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("read_stamps", [](const LanesLoop& l, int lane, uintptr_t s) { return l.read_stamps(lane, S(s)); })
       .def_static("probe_placement", [](uintptr_t s) { return LanesLoop::probe_placement(S(s)); });
   m.def("lanes_supported", &lanes_supported, py::arg("FP"), py::arg("K"), py::arg("cap"));
+
+  py::class_<KeyRangeLoop>(m, "KeyRangeLoop")
+      .def(py::init([](py::dict d, RcclComm* comm) {
+             auto I = [&](const char* k, int64_t def) { return d.contains(k) ? d[k].cast<int64_t>() : def; };
+             auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
+             auto D = [&](const char* k, double def) { return d.contains(k) ? d[k].cast<double>() : def; };
+             KeyRangeLoopCfg c;
+             c.wcfg = d["wcfg"].cast<WideCfg>();
+             c.use_graph = I("use_graph", 1) != 0;
+             c.indptr = P<const int64_t>(U("indptr"));
+             c.idx = P<const int32_t>(U("idx"));
+             c.val = P<const uint16_t>(U("val"));
+             c.y = P<const int32_t>(U("y"));
+             c.ds_rows = I("ds_rows", 0);
+             c.k = (int)I("k", 0);
+             c.N = (int)I("N", 1);
+             c.per_iter_rows = (int)I("per_iter_rows", 0);
+             c.p_ms = D("p_ms", 0.0);
+             c.epochs = I("epochs", 1);
+             c.t0_ms = D("t0_ms", 0.0);
+             c.ridx = P<int32_t>(U("ridx"));
+             c.rval = P<uint16_t>(U("rval"));
+             c.rnnz = P<int32_t>(U("rnnz"));
+             c.ry = P<int32_t>(U("ry"));
+             c.trunc = P<int>(U("trunc"));
+             c.window = U("window");
+             c.shard = P<float>(U("shard"));
+             c.b = P<float>(U("b"));
+             c.lr = (float)D("lr", 1.0);
+             c.dloc = P<float>(U("dloc"));
+             c.wloc = P<float>(U("wloc"));
+             c.loss = P<float>(U("loss"));
+             c.stats = P<int>(U("stats"));
+             c.uniq = P<int32_t>(U("uniq"));
+             c.t_indptr = P<const int64_t>(U("t_indptr"));
+             c.t_idx = P<const int32_t>(U("t_idx"));
+             c.t_val = P<const uint16_t>(U("t_val"));
+             c.t_y = P<const int32_t>(U("t_y"));
+             c.T = (int)I("T", 0);
+             c.s_indptr = P<const int64_t>(U("s_indptr"));
+             c.s_idx = P<const int32_t>(U("s_idx"));
+             c.s_val = P<const uint16_t>(U("s_val"));
+             c.sink = U("sink");
+             c.log_server = I("log_server", 1) != 0;
+             c.log_workers = I("log_workers", 1) != 0;
+             c.tracker = U("tracker");
+             c.api = U("api");
+             return std::make_unique<KeyRangeLoop>(c, comm);
+           }),
+           py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
+      .def(
+          "run",
+          [](KeyRangeLoop& l, int64_t rounds, int64_t r0, uintptr_t stream, double max_wait_s) {
+            py::gil_scoped_release nogil;
+            return l.run(rounds, r0, S(stream), max_wait_s);
+          },
+          py::arg("rounds"), py::arg("r0"), py::arg("stream"), py::arg("max_wait_s") = 600.0)
+      .def_property_readonly("lo", &KeyRangeLoop::lo)
+      .def_property_readonly("hi", &KeyRangeLoop::hi)
+      .def_property_readonly("shard_size", &KeyRangeLoop::shard_size)
+      .def_property_readonly("model_bytes", &KeyRangeLoop::model_bytes)
+      .def_property_readonly("eval_bytes", &KeyRangeLoop::eval_bytes)
+      .def_property_readonly("last_round_bytes", &KeyRangeLoop::last_round_bytes)
+      .def_property_readonly("last_u", &KeyRangeLoop::last_u)
+      .def_property_readonly("device_bytes", &KeyRangeLoop::device_bytes)
+      .def_property_readonly("host_us_per_round", &KeyRangeLoop::host_us_per_round)
+      .def_property_readonly("rounds_run", &KeyRangeLoop::rounds_run)
+      .def("next_local", &KeyRangeLoop::next_local)
+      .def("set_next_local", &KeyRangeLoop::set_next_local)
+      .def_property_readonly("exhausted", &KeyRangeLoop::exhausted);
   // XCC_ID of every workgroup of an n-workgroup launch (placement diagnostics)
   m.def("xcc_map", [](int n, uintptr_t stream) {
     int* ids = nullptr;

@@ -42,20 +42,32 @@ std::string java_double(double v) {
   return neg ? "-" + out : out;
 }
 
+static const char* header(bool worker_schema) {
+  return worker_schema ? "timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen\n"
+                       : "timestamp;partition;vectorClock;loss;fMeasure;accuracy\n";
+}
+
 CsvLogger::CsvLogger(const std::string& path, bool worker_schema, bool write_header, bool append) {
   if (path.empty()) {
     f_ = stdout;
   } else {
     // append mode: several worker processes share one file; every write() is
     // a run of whole lines on an O_APPEND descriptor, so lines never interleave
+    // A creating logger truncates, writes the header at once and continues on an
+    // O_APPEND descriptor too: ranks that open the file later append after the
+    // header, and nobody's lines overwrite another's.
     f_ = std::fopen(path.c_str(), append ? "a" : "w");
     if (!f_) throw std::runtime_error("cannot open log file " + path);
     own_ = true;
+    if (!append) {
+      if (write_header) std::fputs(header(worker_schema), f_);
+      std::fclose(f_);
+      f_ = std::fopen(path.c_str(), "a");
+      if (!f_) throw std::runtime_error("cannot reopen log file " + path);
+      write_header = false;
+    }
   }
-  if (write_header) {
-    pending_ = worker_schema ? "timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen\n"
-                             : "timestamp;partition;vectorClock;loss;fMeasure;accuracy\n";
-  }
+  if (write_header) pending_ = header(worker_schema);
   th_ = std::thread(&CsvLogger::run, this);
 }
 

@@ -54,7 +54,38 @@ struct WideCfg {
   int center;         // multinomial centring (Spark, regParam == 0)
   int zero_const;     // zero-std features get coefficient 0 (Spark) instead of keeping w_old
   int dense_delta;    // also scatter the delta into a dense [F*KP + KP] vector
+  // key-range pull mode (csrc/runtime/keyrange_loop.h): the old weights of the
+  // window's features arrive as w_pull [U][KP] in local-id order, and the local
+  // ids are grouped by owner rank min(f / own_S, own_W - 1) (own_W > 1)
+  int pulled;
+  int own_W;
+  int64_t own_S;
 };
+
+constexpr int kMaxOwners = 64;
+
+// Feature -> local id of the window: open-addressing table of H = pow2 >=
+// 2*umax int2 entries {feature, local id} (key -1 = empty).  Sized by the
+// window, not by F, so a 10^8-feature model carries no F-sized index.
+__device__ __forceinline__ unsigned wide_gslot(int f, unsigned mask) {
+  unsigned x = (unsigned)f;
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x & mask;
+}
+
+__device__ __forceinline__ int wide_find(const int2* __restrict__ tab, unsigned mask, int f) {
+  unsigned h = wide_gslot(f, mask);
+  while (true) {
+    const int2 e = tab[h];
+    if (e.x == f) return e.y;
+    if (e.x == -1) return -1;
+    h = (h + 1) & mask;
+  }
+}
 
 struct WideParams {
   int B, start, pad0, pad1;
@@ -67,13 +98,19 @@ struct WideDev {
   const uint16_t* rval;
   const int32_t* rnnz;
   const int32_t* ry;
-  const float* w_old;  // dense pulled weights [F*KP + KP]
+  const float* w_old;  // dense pulled weights [F*KP + KP] (null in pull mode)
+  const float* w_pull;    // pull mode: [umax][KP] old weights of local id i
+  const float* w_pull_b;  // pull mode: [KP] old intercepts
   // workspace
   WideParams* prm;
   Ctrl* ctrl;
   unsigned* cnt;       // [0] U, [1] dots ticket, [2] U of the previous solve, [3] tail barrier error
-  int32_t* map;        // [F] local id or -1 (-2 transiently)
+  int2* htab;          // [H] {feature, local id} (see wide_find)
+  unsigned hmask;      // H - 1
+  int32_t* hslot;      // [umax] table slot of local id i (cleared by the next solve's begin)
   int32_t* uniq;       // [umax] local id -> feature
+  int32_t* uniq_alt;   // [umax] owner-order scratch (pull mode with own_W > 1)
+  unsigned* own;       // [2 * kMaxOwners] per-owner counts, then cursors
   int32_t* lid;        // [cap*NZ] window entry -> local id
   // block plan (built once per solve): window rows are processed in groups of
   // RB rows; every group dedups its entries' features in LDS so that hot
@@ -111,7 +148,10 @@ int wide_rows_per_group(int NZ, int KP);
 
 // Launchers (stream order; the solver captures them into one hipGraph).
 void wide_launch_begin(const WideCfg& c, const WideDev& d, int B, int start, hipStream_t s);  // cleanup + params
-void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s);  // remap, assign, stats, prep
+// plan: window features -> local ids (+ owner order in pull mode); the old
+// weights are read from here on (prepare: assign, stats, prep)
+void wide_launch_plan(const WideCfg& c, const WideDev& d, hipStream_t s);
+void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s);
 void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dots, hipStream_t s);
 // Line-search retry slots [s0, s1) in one persistent launch (grid barriers).
 void wide_launch_tail(const WideCfg& c, const WideDev& d, int s0, int s1, hipStream_t s);
@@ -128,12 +168,15 @@ void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const 
                                hipStream_t s);
 
 // Test-set evaluation of a dense wide model (optionally overlaid with a
-// worker's local solution: features with map[f] >= 0 read wloc).  Same
-// EvalSlot protocol as launch_test_eval.
+// worker's local solution: features the solver's table htab maps to a local id
+// l read wloc[KP + l*KP]).  Same EvalSlot protocol as launch_test_eval.
+// Key-range form (w == nullptr): margins = zbase[r] (the reduced partial
+// margins of the sharded model) + the overlay's entries + bias[0..KP).
 void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
-                      const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
-                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
-                      void* slot2 = nullptr, unsigned long long seq2 = 0);
+                      const int32_t* y, int T, const float* w, const int2* htab, unsigned hmask, const float* wloc,
+                      int* acc, unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
+                      void* slot2 = nullptr, unsigned long long seq2 = 0, const float* zbase = nullptr,
+                      const float* bias = nullptr);
 // Margins of T rows (tests): out[T][KP].
 void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
                         int T, const float* w, float* out, hipStream_t s);

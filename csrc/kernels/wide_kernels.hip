@@ -89,14 +89,17 @@ __global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int s
     d.cnt[1] = 0u;
     *d.gbar = 0ull;  // grid-barrier counter of this solve's tail launch
   }
-  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256) d.map[d.uniq[i]] = -1;
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256)
+    d.htab[d.hslot[i]] = make_int2(-1, -1);
+  if (blockIdx.x == 0 && threadIdx.x < 2 * kMaxOwners) d.own[threadIdx.x] = 0u;
 }
 
 // plan: per group of RB window rows, dedup the entries' features in an LDS
 // hash table (linear probing), give every entry its group slot, and give every
-// feature new to the window a compact id (first CAS on map[f] wins; winners of
-// a wave take consecutive ids with ONE atomic per wave).  A hot feature thus
-// costs one global CAS per group instead of one per row.
+// feature new to the window a compact id (first CAS of its key into the
+// window table htab wins; winners of a wave take consecutive ids with ONE
+// atomic per wave).  A hot feature thus costs one global CAS per group instead
+// of one per row.
 __device__ __forceinline__ unsigned wide_hash(int f) { return (unsigned)f * 2654435761u; }
 
 __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
@@ -157,7 +160,16 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
     if (si < n) {
       f = bf[si];
       gfeat[si] = f;
-      win = atomicCAS(&d.map[f], -1, -2) == -1;
+      unsigned h = wide_gslot(f, d.hmask);
+      while (true) {
+        const int old = atomicCAS(&d.htab[h].x, -1, f);
+        if (old == -1) {
+          win = true;
+          break;
+        }
+        if (old == f) break;
+        h = (h + 1) & d.hmask;
+      }
     }
     const unsigned long long mask = __ballot(win);
     if (mask) {
@@ -171,20 +183,67 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
   if (t == 0) d.bcount[b] = n;
 }
 
-// assign: map[f] = id, gather the old weights of the window's features.
+// owner order (pull mode, own_W > 1): per-owner counts of the window's
+// features, then every feature scattered to its owner's segment of uniq_alt
+// (assign copies it back): the pull and push segments of owner j are then the
+// contiguous local ids [off_j, off_j + cnt_j).
+__device__ __forceinline__ int wide_owner(const WideCfg& c, int f) {
+  const int64_t o = (int64_t)f / c.own_S;
+  return o < c.own_W - 1 ? (int)o : c.own_W - 1;
+}
+
+__global__ __launch_bounds__(256) void wide_owner_count_kernel(WideCfg c, WideDev d) {
+  __shared__ unsigned cnt_s[kMaxOwners];
+  const unsigned U = d.cnt[0];
+  if (threadIdx.x < kMaxOwners) cnt_s[threadIdx.x] = 0u;
+  __syncthreads();
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+    const int f = d.uniq[i];
+    atomicAdd(&cnt_s[wide_owner(c, f)], 1u);
+    d.uniq_alt[i] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x < c.own_W && cnt_s[threadIdx.x]) atomicAdd(&d.own[threadIdx.x], cnt_s[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void wide_owner_scatter_kernel(WideCfg c, WideDev d) {
+  __shared__ unsigned base_s[kMaxOwners];
+  const unsigned U = d.cnt[0];
+  if (threadIdx.x == 0) {
+    unsigned o = 0;
+    for (int j = 0; j < c.own_W; ++j) {
+      base_s[j] = o;
+      o += d.own[j];
+    }
+  }
+  __syncthreads();
+  unsigned* cur = d.own + kMaxOwners;
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+    const int f = d.uniq_alt[i];
+    const int j = wide_owner(c, f);
+    d.uniq[base_s[j] + atomicAdd(&cur[j], 1u)] = f;
+  }
+}
+
+// assign: table entry of every local id, gather the old weights of the
+// window's features (the dense pulled vector, or the pulled values in pull mode).
 __global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) {
   const unsigned U = d.cnt[0];
   const int KP = c.KP;
   for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
     const int f = d.uniq[i];
-    d.map[f] = (int)i;
-    const float* src = d.w_old + (int64_t)f * KP;
+    unsigned h = wide_gslot(f, d.hmask);
+    while (d.htab[h].x != f) h = (h + 1) & d.hmask;
+    d.htab[h].y = (int)i;
+    d.hslot[i] = (int)h;
+    const float* src = c.pulled ? d.w_pull + (int64_t)i * KP : d.w_old + (int64_t)f * KP;
     float* dst = d.w0 + KP + (int64_t)i * KP;
     for (int k = 0; k < KP; ++k) dst[k] = src[k];
     d.s1[i] = 0.f;
     d.s2[i] = 0.f;
   }
-  if (blockIdx.x == 0 && threadIdx.x < KP) d.w0[threadIdx.x] = d.w_old[c.F * KP + threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x < KP)
+    d.w0[threadIdx.x] = c.pulled ? d.w_pull_b[threadIdx.x] : d.w_old[c.F * KP + threadIdx.x];
 }
 
 // stats: local ids of the group's features, every entry's local id, and the
@@ -204,7 +263,7 @@ __global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
   const int32_t* gfeat = d.bfeat + (int64_t)b * EB;
   int32_t* glid = d.blid + (int64_t)b * EB;
   for (int si = t; si < n; si += 256) {
-    const int l = d.map[gfeat[si]];
+    const int l = wide_find(d.htab, d.hmask, gfeat[si]);
     lid_s[si] = l;
     glid[si] = l;
     s1l[si] = 0.f;
@@ -714,9 +773,16 @@ int wide_rows_per_group(int NZ, int KP) {
 
 static int ngroups(const WideCfg& c, const WideDev& d) { return (c.cap + d.RB - 1) / d.RB; }
 
+void wide_launch_plan(const WideCfg& c, const WideDev& d, hipStream_t s) {
+  wide_plan_kernel<<<ngroups(c, d), 256, (size_t)(2 * d.TS + d.EB) * 4, s>>>(c, d);
+  if (c.pulled && c.own_W > 1) {
+    wide_owner_count_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(c, d);
+    wide_owner_scatter_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(c, d);
+  }
+}
+
 void wide_launch_prepare(const WideCfg& c, const WideDev& d, hipStream_t s) {
   const int G = ngroups(c, d);
-  wide_plan_kernel<<<G, 256, (size_t)(2 * d.TS + d.EB) * 4, s>>>(c, d);
   wide_assign_kernel<<<grid_for(c.umax, 1024), 256, 0, s>>>(c, d);
   wide_stats_kernel<<<G, 256, (size_t)d.EB * 12, s>>>(c, d);
   wide_prep_kernel<<<grid_for(d.PLmax, 1024), 256, 0, s>>>(c, d);
@@ -852,9 +918,7 @@ void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const 
 template <int KP>
 __device__ __forceinline__ void wide_row_margins(int64_t F, const int64_t* __restrict__ indptr,
                                                  const int32_t* __restrict__ idx, const uint16_t* __restrict__ val,
-                                                 int64_t row, const float* __restrict__ w,
-                                                 const int32_t* __restrict__ map, const float* __restrict__ wloc,
-                                                 float (&z)[KP]) {
+                                                 int64_t row, const float* __restrict__ w, float (&z)[KP]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] = 0.f;
@@ -862,20 +926,15 @@ __device__ __forceinline__ void wide_row_margins(int64_t F, const int64_t* __res
   for (int64_t e = a + lane; e < b; e += 64) {
     const int f = idx[e];
     const float v = bf2f(val[e]);
-    const float* src = w + (int64_t)f * KP;
-    if (map) {
-      const int l = map[f];
-      if (l >= 0) src = wloc + KP + (int64_t)l * KP;
-    }
     float wv[KP];
-    ldk<KP>(src, wv);
+    ldk<KP>(w + (int64_t)f * KP, wv);
 #pragma unroll
     for (int k = 0; k < KP; ++k) z[k] += v * wv[k];
   }
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] = wave_sum(z[k]);
   float bv[KP];
-  ldk<KP>(map ? wloc : w + F * KP, bv);
+  ldk<KP>(w + F * KP, bv);
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] += bv[k];
 }
@@ -887,16 +946,19 @@ __device__ __forceinline__ void wide_row_margins(int64_t F, const int64_t* __res
 // PAIR: also the margins zb of the plain model w (no overlay) from the same
 // gathers -- the worker's local model and the global model it was trained from
 // differ only on the window's features.
+// Key-range form (w == nullptr): only overlay entries contribute, on top of
+// zbase[row] (the caller adds it), with the intercepts from `bias`.
 template <int KP, bool PAIR>
 __device__ __forceinline__ void wide_rows4_margins(int64_t F, const int64_t* __restrict__ indptr,
                                                   const int32_t* __restrict__ idx,
                                                   const uint16_t* __restrict__ val, int64_t row, bool valid,
-                                                  const float* __restrict__ w, const int32_t* __restrict__ map,
-                                                  const float* __restrict__ wloc, float (&z)[KP], float (&zb)[KP]) {
+                                                  const float* __restrict__ w, const int2* __restrict__ htab,
+                                                  unsigned hmask, const float* __restrict__ wloc,
+                                                  const float* __restrict__ bias, float (&z)[KP], float (&zb)[KP]) {
   const int l = threadIdx.x & 15;
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] = zb[k] = 0.f;
-  if (valid) {
+  if (valid && (w || htab)) {  // (key-range server row: margins base + intercepts only)
     const int64_t a = indptr[row], b = indptr[row + 1];
     for (int64_t e0 = a + l; e0 < b; e0 += 64) {
       int f[4];
@@ -912,10 +974,10 @@ __device__ __forceinline__ void wide_rows4_margins(int64_t F, const int64_t* __r
       bool ov[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        src[u] = f[u] >= 0 ? w + (int64_t)f[u] * KP : nullptr;
+        src[u] = f[u] >= 0 && w ? w + (int64_t)f[u] * KP : nullptr;
         ov[u] = false;
-        if (map && f[u] >= 0) {
-          const int li = map[f[u]];
+        if (htab && f[u] >= 0) {
+          const int li = wide_find(htab, hmask, f[u]);
           if (li >= 0) {
             src[u] = wloc + KP + (int64_t)li * KP;
             ov[u] = true;
@@ -947,7 +1009,7 @@ __device__ __forceinline__ void wide_rows4_margins(int64_t F, const int64_t* __r
     }
   }
   float bv[KP];
-  ldk<KP>(map ? wloc : w + F * KP, bv);
+  ldk<KP>(bias ? bias : (htab ? wloc : w + F * KP), bv);
 #pragma unroll
   for (int k = 0; k < KP; ++k) z[k] += bv[k];
   if constexpr (PAIR) {
@@ -979,10 +1041,12 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
                                                         const int32_t* __restrict__ idx,
                                                         const uint16_t* __restrict__ val,
                                                         const int32_t* __restrict__ y, int T,
-                                                        const float* __restrict__ w, const int32_t* __restrict__ map,
-                                                        const float* __restrict__ wloc, int* acc, unsigned* ticket,
-                                                        char* slot, const float* loss, unsigned long long seq,
-                                                        char* slot2, unsigned long long seq2) {
+                                                        const float* __restrict__ w, const int2* __restrict__ htab,
+                                                        unsigned hmask, const float* __restrict__ wloc, int* acc,
+                                                        unsigned* ticket, char* slot, const float* loss,
+                                                        unsigned long long seq, char* slot2, unsigned long long seq2,
+                                                        const float* __restrict__ zbase,
+                                                        const float* __restrict__ bias) {
   __shared__ int cl[2][256];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -993,7 +1057,11 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
   for (int64_t r0 = (int64_t)blockIdx.x * 16; r0 < T; r0 += (int64_t)gridDim.x * 16) {
     const int64_t r = r0 + (tid >> 4);
     float z[KP], zb[KP];
-    wide_rows4_margins<KP, PAIR>(F, indptr, idx, val, r, r < T, w, map, wloc, z, zb);
+    wide_rows4_margins<KP, PAIR>(F, indptr, idx, val, r, r < T, w, htab, hmask, wloc, bias, z, zb);
+    if (zbase && r < T) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) z[k] += zbase[r * KP + k];
+    }
     if ((lane & 15) == 0 && r < T) {
       int yl = y[r];
       if (K == 1) yl = yl > 0 ? 1 : 0;
@@ -1045,7 +1113,7 @@ __global__ __launch_bounds__(256) void wide_logits_kernel(int64_t F, const int64
   const int lane = threadIdx.x & 63;
   for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < T; r += (int64_t)gridDim.x * 4) {
     float z[KP];
-    wide_row_margins<KP>(F, indptr, idx, val, r, w, nullptr, nullptr, z);
+    wide_row_margins<KP>(F, indptr, idx, val, r, w, z);
     if (lane < KP) {
       float o = 0.f;
 #pragma unroll
@@ -1057,9 +1125,9 @@ __global__ __launch_bounds__(256) void wide_logits_kernel(int64_t F, const int64
 }
 
 void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
-                      const int32_t* y, int T, const float* w, const int32_t* map, const float* wloc, int* acc,
-                      unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
-                      void* slot2, unsigned long long seq2) {
+                      const int32_t* y, int T, const float* w, const int2* htab, unsigned hmask, const float* wloc,
+                      int* acc, unsigned* ticket, void* slot, const float* loss, unsigned long long seq, hipStream_t s,
+                      void* slot2, unsigned long long seq2, const float* zbase, const float* bias) {
   if (T <= 0) return;
   const int grid = grid_for((int64_t)T * 16, 1024);  // 16 rows per workgroup pass
   char* sl = static_cast<char*>(slot);
@@ -1068,11 +1136,11 @@ void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int
 #define PSX_WE(KV)                                                                                             \
   case KV:                                                                                                     \
     if (pair)                                                                                                  \
-      wide_eval_kernel<KV, true><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc, ticket, \
-                                                      sl, loss, seq, sl2, seq2);                              \
-    else                                                                                                       \
-      wide_eval_kernel<KV, false><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, map, wloc, acc,       \
-                                                       ticket, sl, loss, seq, nullptr, 0);                    \
+      wide_eval_kernel<KV, true><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, htab, hmask, wloc, acc, \
+                                                      ticket, sl, loss, seq, sl2, seq2, nullptr, nullptr);     \
+    else                                                                                                        \
+      wide_eval_kernel<KV, false><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, htab, hmask, wloc, acc, \
+                                                       ticket, sl, loss, seq, nullptr, 0, zbase, bias);        \
     break;
   switch (KP) {
     PSX_WE(1)

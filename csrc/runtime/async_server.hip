@@ -592,7 +592,7 @@ void AsyncServer::apply_and_log(const CtrlToken& t) {
                        cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, cfg_.coff);
     else
       launch_wide_eval(cfg_.K, cfg_.KP, cfg_.Fw, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, cfg_.w,
-                       nullptr, nullptr, cfg_.acc, cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, stream_);
+                       nullptr, 0u, nullptr, cfg_.acc, cfg_.ticket, reinterpret_cast<void*>(addr), nullptr, seq, stream_);
     api().sink_submit((void*)cfg_.sink, slot, seq, 1, -1, -1, v, 0);  // stamped when the evaluation lands
   }
   const hipError_t e = hipGetLastError();

@@ -2,7 +2,7 @@
 //
 // Same role as LocalSolver (solver.h) for rows that are sparse and models too
 // wide for the dense MFMA tiles (BASELINE.json configs 4 and 5):
-//   begin -> remap -> assign -> lid/stats -> prep -> (fwdbwd, dots+ctrl, apply) x nslots
+//   begin -> plan [-> owner order] | assign -> lid/stats -> prep -> (fwdbwd, dots+ctrl, apply) x nslots
 //         -> [memset dense delta] -> finalize
 // is captured once into a hipGraph; per run only the first node's kernel
 // arguments (the window) change.
@@ -29,6 +29,10 @@ struct WideBuffers {
   int* stats = nullptr;           // [4] out
   float* delta_dense = nullptr;   // [F*KP + KP] out (cfg.dense_delta)
   int32_t* uniq = nullptr;        // [min(F, cap*NZ)] out: local id -> feature
+  // pull mode (cfg.pulled): the caller fills w_pull [umax][KP] (old weights of
+  // local id i) and w_pull_b [KP] between plan() and finish(); w_old is unused
+  const float* w_pull = nullptr;
+  const float* w_pull_b = nullptr;
 };
 
 class WideSolver {
@@ -39,10 +43,18 @@ class WideSolver {
   WideSolver& operator=(const WideSolver&) = delete;
 
   void run(int B, int start, hipStream_t stream);
+  // pull mode: phase 1 (window features -> local ids, grouped by owner when
+  // cfg.own_W > 1), then -- once w_pull holds the old weights of uniq[0..U) --
+  // phase 2 (the solve).  Each phase is one hipGraph replay.
+  void plan(int B, int start, hipStream_t stream);
+  void finish(hipStream_t stream);
+  // [kMaxOwners] per-owner feature counts of the last plan (pull mode, own_W > 1)
+  const unsigned* owner_counts_dev() const { return dv_.own; }
   const WideCfg& cfg() const { return cfg_; }
   int64_t plmax() const { return dv_.PLmax; }
   // Device arrays valid after a run (until the next run's first kernel):
-  const int32_t* map() const { return dv_.map; }
+  const int2* table() const { return dv_.htab; }
+  unsigned table_mask() const { return dv_.hmask; }
   const int32_t* uniq() const { return dv_.uniq; }
   const unsigned* ucount_dev() const { return dv_.cnt; }
   // U of the last finished run (pinned host mirror; valid after the stream synced).
@@ -58,7 +70,9 @@ class WideSolver {
   }
 
  private:
-  void enqueue_body(hipStream_t s, int B, int start);
+  void enqueue_plan(hipStream_t s, int B, int start);
+  void enqueue_rest(hipStream_t s);
+  void check_window(int B, int start) const;
   WideCfg cfg_;
   WideDev dv_{};
   bool use_graph_;
@@ -74,8 +88,10 @@ class WideSolver {
   void* begin_kp_[3] = {};
   hipKernelNodeParams begin_params_{};
   hipStream_t cap_stream_ = nullptr;
-  hipGraph_t graph_ = nullptr;
+  hipGraph_t graph_ = nullptr;  // whole solve, or phase 1 in pull mode
   hipGraphExec_t exec_ = nullptr;
+  hipGraph_t graph2_ = nullptr;  // pull mode: phase 2
+  hipGraphExec_t exec2_ = nullptr;
 };
 
 const void* wide_begin_symbol();

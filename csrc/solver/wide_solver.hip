@@ -21,6 +21,11 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   if (cfg.sc.nslots < 1) throw std::invalid_argument("nslots must be >= 1");
   if (cfg.dense_delta && !buf.delta_dense) throw std::invalid_argument("dense_delta needs a dense output buffer");
   if (!buf.uniq || !buf.dloc || !buf.wloc || !buf.loss || !buf.stats) throw std::invalid_argument("missing output buffer");
+  if (cfg.pulled && (!buf.w_pull || !buf.w_pull_b)) throw std::invalid_argument("pull mode needs w_pull / w_pull_b");
+  if (!cfg.pulled && !buf.w_old) throw std::invalid_argument("missing w_old");
+  if (cfg.pulled && (cfg.own_W < 1 || cfg.own_W > kMaxOwners || (cfg.own_W > 1 && cfg.own_S < 1)))
+    throw std::invalid_argument("owner split: 1 <= own_W <= 64 and own_S >= 1");
+  if (cfg.pulled && cfg.dense_delta) throw std::invalid_argument("pull mode has no dense delta");
   const int64_t E = (int64_t)cfg.cap * cfg.NZ;
   const int64_t umax = cfg.F < E ? cfg.F : E;
   if (umax > 0x7fffffff / 2) throw std::invalid_argument("window too large");
@@ -36,7 +41,10 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
     return o;
   };
   const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16), o_gbar = take(8);
-  const size_t o_map = take((size_t)cfg.F * 4), o_lid = take((size_t)E * 4);
+  unsigned HT = 1;
+  while (HT < 2 * (unsigned)umax) HT <<= 1;
+  const size_t o_tab = take((size_t)HT * 8), o_hslot = take(umax * 4), o_alt = take(umax * 4),
+               o_own = take(2 * kMaxOwners * 4), o_lid = take((size_t)E * 4);
   const int RB = wide_rows_per_group(cfg.NZ, KP), EB = RB * cfg.NZ;
   int TS = 1;
   while (TS < 2 * EB) TS <<= 1;
@@ -57,7 +65,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   hip_check(hipMalloc(&ws_, ws_bytes_), "hipMalloc(wide solver workspace)");
   hip_check(hipMemset(ws_, 0, ws_bytes_), "hipMemset(wide solver workspace)");
   char* b = static_cast<char*>(ws_);
-  hip_check(hipMemset(b + o_map, 0xff, (size_t)cfg.F * 4), "hipMemset(map)");  // all -1
+  hip_check(hipMemset(b + o_tab, 0xff, (size_t)HT * 8), "hipMemset(table)");  // all keys -1
   hip_check(hipHostMalloc((void**)&host_u_, 64, hipHostMallocCoherent | hipHostMallocMapped), "hipHostMalloc");
   *host_u_ = 0;
 
@@ -66,11 +74,17 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.rnnz = buf.rnnz;
   dv_.ry = buf.ry;
   dv_.w_old = buf.w_old;
+  dv_.w_pull = buf.w_pull;
+  dv_.w_pull_b = buf.w_pull_b;
   dv_.prm = reinterpret_cast<WideParams*>(b + o_prm);
   dv_.ctrl = reinterpret_cast<Ctrl*>(b + o_ctrl);
   dv_.cnt = reinterpret_cast<unsigned*>(b + o_cnt);
   dv_.gbar = reinterpret_cast<unsigned long long*>(b + o_gbar);
-  dv_.map = reinterpret_cast<int32_t*>(b + o_map);
+  dv_.htab = reinterpret_cast<int2*>(b + o_tab);
+  dv_.hmask = HT - 1;
+  dv_.hslot = reinterpret_cast<int32_t*>(b + o_hslot);
+  dv_.uniq_alt = reinterpret_cast<int32_t*>(b + o_alt);
+  dv_.own = reinterpret_cast<unsigned*>(b + o_own);
   dv_.uniq = buf.uniq;
   dv_.lid = reinterpret_cast<int32_t*>(b + o_lid);
   dv_.pslot = reinterpret_cast<uint16_t*>(b + o_pslot);
@@ -106,9 +120,16 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-    enqueue_body(cap_stream_, 1, 0);
+    enqueue_plan(cap_stream_, 1, 0);
+    if (!cfg_.pulled) enqueue_rest(cap_stream_);
     hip_check(hipStreamEndCapture(cap_stream_, &graph_), "hipStreamEndCapture");
     hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+    if (cfg_.pulled) {
+      hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+      enqueue_rest(cap_stream_);
+      hip_check(hipStreamEndCapture(cap_stream_, &graph2_), "hipStreamEndCapture");
+      hip_check(hipGraphInstantiate(&exec2_, graph2_, nullptr, nullptr, 0), "hipGraphInstantiate");
+    }
     size_t n = 0;
     hip_check(hipGraphGetNodes(graph_, nullptr, &n), "hipGraphGetNodes");
     std::vector<hipGraphNode_t> nodes(n);
@@ -137,13 +158,20 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
 WideSolver::~WideSolver() {
   if (exec_) (void)hipGraphExecDestroy(exec_);
   if (graph_) (void)hipGraphDestroy(graph_);
+  if (exec2_) (void)hipGraphExecDestroy(exec2_);
+  if (graph2_) (void)hipGraphDestroy(graph2_);
   if (cap_stream_) (void)hipStreamDestroy(cap_stream_);
   if (ws_) (void)hipFree(ws_);
   if (host_u_) (void)hipHostFree(host_u_);
 }
 
-void WideSolver::enqueue_body(hipStream_t s, int B, int start) {
+void WideSolver::enqueue_plan(hipStream_t s, int B, int start) {
   wide_launch_begin(cfg_, dv_, B, start, s);
+  wide_launch_plan(cfg_, dv_, s);
+  hip_check(hipGetLastError(), "wide solver launch");
+}
+
+void WideSolver::enqueue_rest(hipStream_t s) {
   wide_launch_prepare(cfg_, dv_, s);
   // slots launched one by one: the initial evaluation + one trial per iteration
   // (a solve whose line searches accept their first trial); the retry budget
@@ -158,17 +186,44 @@ void WideSolver::enqueue_body(hipStream_t s, int B, int start) {
   hip_check(hipGetLastError(), "wide solver launch");
 }
 
-void WideSolver::run(int B, int start, hipStream_t stream) {
+void WideSolver::check_window(int B, int start) const {
   if (B <= 0) throw std::invalid_argument("local solve on an empty buffer");
   if (B > cfg_.cap || start < 0 || start >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
+}
+
+void WideSolver::run(int B, int start, hipStream_t stream) {
+  if (cfg_.pulled) throw std::logic_error("pull mode: plan() + finish()");
+  check_window(B, start);
   if (use_graph_) {
     begin_args_.B = B;
     begin_args_.start = start;
     hip_check(hipGraphExecKernelNodeSetParams(exec_, begin_node_, &begin_params_), "hipGraphExecKernelNodeSetParams");
     hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
   } else {
-    enqueue_body(stream, B, start);
+    enqueue_plan(stream, B, start);
+    enqueue_rest(stream);
   }
+}
+
+void WideSolver::plan(int B, int start, hipStream_t stream) {
+  if (!cfg_.pulled) throw std::logic_error("plan() is the pull mode's first phase");
+  check_window(B, start);
+  if (use_graph_) {
+    begin_args_.B = B;
+    begin_args_.start = start;
+    hip_check(hipGraphExecKernelNodeSetParams(exec_, begin_node_, &begin_params_), "hipGraphExecKernelNodeSetParams");
+    hip_check(hipGraphLaunch(exec_, stream), "hipGraphLaunch");
+  } else {
+    enqueue_plan(stream, B, start);
+  }
+}
+
+void WideSolver::finish(hipStream_t stream) {
+  if (!cfg_.pulled) throw std::logic_error("finish() is the pull mode's second phase");
+  if (use_graph_)
+    hip_check(hipGraphLaunch(exec2_, stream), "hipGraphLaunch");
+  else
+    enqueue_rest(stream);
 }
 
 std::vector<long long> WideSolver::read_stamps(hipStream_t stream) {

@@ -103,7 +103,7 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--async_scheduler", default="auto", choices=["auto", "events", "threads"],
                    help="--inprocess SSP/ASP: one host thread polling the workers' HIP events, or a thread "
                         "per worker (auto: events on a GPU unless a delay is injected)")
-    g.add_argument("--bsp_schedule", default="reduce_bcast", choices=["allreduce", "reduce_bcast", "sharded"])
+    g.add_argument("--bsp_schedule", default="reduce_bcast", choices=["allreduce", "reduce_bcast", "sharded", "keyrange"])
     g.add_argument("--checkpoint_dir", default=None)
     g.add_argument("--checkpoint_every", type=int, default=0)
     g.add_argument("--resume", action="store_true")

@@ -74,19 +74,32 @@ class WideSpec:
         w[self.F * self.KP : self.F * self.KP + self.K] = intercept.to(dev, torch.float32)
         return w
 
+    INIT_CHUNK = 1 << 22  # features per generator chunk of the random init
+
     def init(self, kind: str = "zeros", seed: int = 0, scale: float = 0.01, device=None) -> torch.Tensor:
         """Zeros (reference quirk Q6) or N(0, scale^2) coefficients.  Random
-        init is drawn by a CPU generator (identical on every device and rank)
-        in chunks and streamed to the target device (10^8 x KP floats)."""
+        init is drawn by CPU generators (identical on every device and rank), one
+        per chunk of INIT_CHUNK features, and streamed to the target device
+        (10^8 x KP floats)."""
+        return self.init_range(kind, seed, 0, self.F, scale, device)
+
+    def init_range(self, kind: str, seed: int, lo: int, hi: int, scale: float = 0.01, device=None) -> torch.Tensor:
+        """The coefficients of features [lo, hi) of :meth:`init` followed by KP
+        zero intercepts: ``[(hi - lo)*KP + KP]`` (a key-range shard, or with
+        lo = 0, hi = F the whole vector).  Only the chunks overlapping the range
+        are generated, so a rank draws its own shard alone."""
         dev = torch.device(device) if device is not None else torch.device("cpu")
-        w = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        n = hi - lo
+        w = torch.zeros(n * self.KP + self.KP, dtype=torch.float32, device=dev)
         if kind == "random":
-            g = torch.Generator().manual_seed(seed)
-            view = w[: self.F * self.KP].view(self.F, self.KP)
-            step = 1 << 22
-            for f0 in range(0, self.F, step):
-                f1 = min(self.F, f0 + step)
-                view[f0:f1, : self.K] = (torch.randn(f1 - f0, self.K, generator=g) * scale).to(dev)
+            view = w[: n * self.KP].view(n, self.KP)
+            step = self.INIT_CHUNK
+            for c in range(lo // step, -(-hi // step)):
+                f0, f1 = c * step, min(self.F, (c + 1) * step)
+                g = torch.Generator().manual_seed(seed * 1_000_003 + c)
+                blk = torch.randn(f1 - f0, self.K, generator=g) * scale
+                a, b = max(f0, lo), min(f1, hi)
+                view[a - lo:b - lo, : self.K] = blk[a - f0:b - f0].to(dev)
         elif kind != "zeros":
             raise ValueError(f"unknown init {kind!r}")
         return w

@@ -170,8 +170,11 @@ class WideSolveOp:
         self._bound = key
 
     @property
-    def map_ptr(self) -> int:
-        return self._native.map_ptr if self._native is not None else 0
+    def table(self) -> tuple[int, int]:
+        """(device pointer, mask) of the feature -> local id table of the last solve."""
+        if self._native is None:
+            return 0, 0
+        return self._native.table_ptr, self._native.table_mask
 
     def run(self, ring: SparseRing, B: int, start: int, w_old: torch.Tensor):
         if B <= 0:
@@ -201,12 +204,27 @@ class WideSolveOp:
 
     # -- CPU oracle path ---------------------------------------------------------
     def _run_cpu(self, ring: SparseRing, B: int, start: int, w_old: torch.Tensor):
-        s, o = self.spec, self.opts
+        s = self.spec
+        uniq = self.plan_cpu(ring, B, start)
+        W = w_old[: s.F * s.KP].view(s.F, s.KP)
+        self.finish_cpu(W[uniq.long()], w_old[s.F * s.KP:])
+
+    def plan_cpu(self, ring: SparseRing, B: int, start: int) -> torch.Tensor:
+        """Phase 1 of a pulled solve (CPU): the window's distinct features, sorted
+        (= grouped by key-range owner).  The caller pulls their coefficients and
+        calls :meth:`finish_cpu`."""
         slots = ((torch.arange(B) + start) % self.cap).tolist()
-        feats = []
-        for sl in slots:
-            feats.append(ring.idx[sl, : int(ring.nnz[sl])])
+        feats = [ring.idx[sl, : int(ring.nnz[sl])] for sl in slots]
         uniq = torch.unique(torch.cat(feats)) if feats else torch.zeros(0, dtype=torch.int32)
+        self._plan = (slots, uniq.to(torch.int32), ring)
+        return self._plan[1]
+
+    def finish_cpu(self, w_pull: torch.Tensor, b_old: torch.Tensor):
+        """Phase 2 (CPU): the local solve from the pulled coefficients ``w_pull``
+        [U, KP] of the planned features and the intercepts ``b_old`` [KP]."""
+        s, o = self.spec, self.opts
+        slots, uniq, ring = self._plan
+        B = len(slots)
         U = int(uniq.numel())
         pos = {int(f): i for i, f in enumerate(uniq.tolist())}
         X = torch.zeros(B, U, dtype=torch.float64)
@@ -215,9 +233,8 @@ class WideSolveOp:
             for f, v in zip(ring.idx[sl, :k].tolist(), ring.val[sl, :k].float().tolist()):
                 X[r, pos[f]] += v
         y = ring.y[slots].long()
-        W = w_old[: s.F * s.KP].view(s.F, s.KP)
-        coef_old = W[uniq.long(), : s.K].t().double() if U else torch.zeros(s.K, 0, dtype=torch.float64)
-        b_old = w_old[s.F * s.KP: s.F * s.KP + s.K].double()
+        coef_old = w_pull[:, : s.K].t().double() if U else torch.zeros(s.K, 0, dtype=torch.float64)
+        b_old = b_old[: s.K].double()
         res = local_solve_reference(X, y, coef_old, b_old, iters=o.iters, hist=o.hist, ls_max=o.ls_max,
                                     nslots=o.nslots, mode=o.mode, gd_lr=o.gd_lr, center=o.center,
                                     zero_const=o.zero_const, tol=o.tol, standardize=o.standardize)
@@ -228,7 +245,7 @@ class WideSolveOp:
         if U:
             self.dloc[s.KP: s.KP + U * s.KP].view(U, s.KP)[:, : s.K] = res.delta_coef.t()
             self.wloc[s.KP: s.KP + U * s.KP].view(U, s.KP)[:, : s.K] = res.coef.t()
-            self.uniq[:U] = uniq.to(torch.int32)
+            self.uniq[:U] = uniq
         self._count_cpu = U
         self._map_cpu = pos
         self.loss.fill_(res.loss)
@@ -284,10 +301,10 @@ class WideEvalSet:
         ``overlay`` is a :class:`WideSolveOp`) into the host EvalSlot at ``slot_addr``."""
         s = self.spec
         if is_gpu(self.device):
-            map_ptr = overlay.map_ptr if overlay is not None else 0
+            tab, mask = overlay.table if overlay is not None else (0, 0)
             wloc_ptr = overlay.wloc.data_ptr() if overlay is not None else 0
             _native.hip().wide_eval(s.K, s.KP, s.F, self.ds.indptr.data_ptr(), self.ds.idx.data_ptr(),
-                                    self.ds.val.data_ptr(), self.ds.y.data_ptr(), self.T, w.data_ptr(), map_ptr,
+                                    self.ds.val.data_ptr(), self.ds.y.data_ptr(), self.T, w.data_ptr(), tab, mask,
                                     wloc_ptr, scratch.acc.data_ptr(), scratch.ticket.data_ptr(), int(slot_addr),
                                     loss.data_ptr() if loss is not None else 0, int(seq), stream_handle(self.device))
             return
@@ -306,7 +323,7 @@ class WideEvalSet:
             s = self.spec
             _native.hip().wide_eval(s.K, s.KP, s.F, self.ds.indptr.data_ptr(), self.ds.idx.data_ptr(),
                                     self.ds.val.data_ptr(), self.ds.y.data_ptr(), self.T, w_a.data_ptr(),
-                                    overlay.map_ptr, overlay.wloc.data_ptr(), scratch.acc.data_ptr(),
+                                    *overlay.table, overlay.wloc.data_ptr(), scratch.acc.data_ptr(),
                                     scratch.ticket.data_ptr(), int(slot_a),
                                     loss_a.data_ptr() if loss_a is not None else 0, int(seq_a),
                                     stream_handle(self.device), int(slot_b), int(seq_b))

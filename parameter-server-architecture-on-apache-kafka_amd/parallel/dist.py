@@ -17,9 +17,11 @@ Sequential (BSP, c = 0) schedules, chosen with ``--bsp_schedule``:
   reduce_bcast  the textbook PS: ncclReduce(delta -> server) then
                 ncclBroadcast(w <- server).  Works with a dedicated server rank
                 (contributes zeros) or a colocated one.
-  sharded       key-range sharded server (new capability): every
-                rank owns P/world of the master weights; ncclReduceScatter(delta)
-                -> shard update -> ncclAllGather(w).
+  sharded       dense model: every rank owns P/world of the master weights;
+                ncclReduceScatter(delta) -> shard update -> ncclAllGather(w).
+                Wide model (or ``keyrange``): the key-range sharded server of
+                keyrange.py -- each rank stores ONLY its key range and a round moves
+                the window's ids and values (pull / push by owner), never P floats.
 On GPUs the BSP collectives are issued through a native RCCL communicator
 (psx.parallel.comm, csrc/comm/rccl_comm.h): a few us of host time per call
 instead of ~30 us through torch.distributed, which otherwise bounds the round.
@@ -174,7 +176,20 @@ def pull_log_capacity(umax: int) -> int:
     return 16 * (int(umax) + 1)
 
 
+def uses_keyrange(cfg: PSConfig) -> bool:
+    """The wide model's sharded schedule is the key-range server (keyrange.py):
+    each rank stores only its key range and moves only the window's ids / values."""
+    return cfg.bsp_schedule == "keyrange" or (cfg.bsp_schedule == "sharded" and cfg.model == "wide")
+
+
 class DistEngine:
+    def __new__(cls, cfg: PSConfig, *args, **kwargs):
+        if cls is DistEngine and uses_keyrange(cfg):
+            from .keyrange import KeyRangeEngine
+
+            return KeyRangeEngine(cfg, *args, **kwargs)
+        return super().__new__(cls)
+
     def __init__(self, cfg: PSConfig, rank: int, world: int, device, train=None, test=None):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, torch.device(device)
         self.async_mode = cfg.consistency_model != 0
@@ -239,10 +254,16 @@ class DistEngine:
                         fh.write("timestamp;partition;vectorClock;loss;fMeasure;accuracy;numTuplesSeen\n")
             elif self.is_worker:
                 wp, append = wpath, True
-            dist.barrier()
         # every rank evaluates (workers log their local model each iteration, as the
-        # reference does); only files requested with -l are written
-        self.log = LogSink(self.spec.eval_classes, self.device, wp, sp, keep_records=(rank == 0), worker_append=append)
+        # reference does); only files requested with -l are written.  Rank 0 creates
+        # the files (headers written at once) before the others open them to append.
+        mk = lambda: LogSink(self.spec.eval_classes, self.device, wp, sp, keep_records=(rank == 0),
+                             worker_append=append)
+        self.log = mk() if rank == 0 else None
+        if cfg.logging:
+            dist.barrier()
+        if self.log is None:
+            self.log = mk()
         self.tracer = Tracer(cfg.trace_path.replace(".json", f".rank{rank}.json") if cfg.trace_path else None, rank,
                              self.device, f"{cfg.log_dir}/logs-perf.rank{rank}.csv" if cfg.perf_log else None)
         w0 = self.spec.init(cfg.init, seed=cfg.seed, device=self.device)

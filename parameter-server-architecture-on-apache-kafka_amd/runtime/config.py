@@ -28,6 +28,7 @@ class PSConfig:
     model: str = "auto"
     dtype: str = "bf16"  # feature rows of the dense model: bf16 or fp32 (the reference fits in fp64)
     sigmoid: bool = False  # wide model: one logit + sigmoid (binary labels)
+    log_workers: bool = True  # worker rows (the reference logs one per local iteration)
     ring_nz: int = 0  # wide model: non-zeros per ring row (0 = from the data)
     wide_dense_delta: bool = False  # wide model: also produce a dense delta (collective pushes)
     sparse_push: bool = True  # wide model, SSP/ASP across ranks: push (ids, values) instead of a dense delta
@@ -63,7 +64,7 @@ class PSConfig:
     log_dir: str = "."
     verbose: bool = False
     # distributed
-    bsp_schedule: str = "allreduce"  # allreduce | reduce_bcast | sharded
+    bsp_schedule: str = "allreduce"  # allreduce | reduce_bcast | sharded | keyrange (wide: sharded == keyrange)
     server_colocated: bool = True
     # logical workers per worker rank (one XCD each: the multi-lane round loop);
     # the reference hosts all of its workers in one process (BaseKafkaApp.java:25,70)

@@ -18,7 +18,8 @@ from psx.utils.logsink import LogSink
 pytestmark = pytest.mark.gpu
 
 
-def _loop(spec, ks, N, train, test, w, dev, rows=1024, cap=1024, sink=None, lr=None, frags=None, opts=None):
+def _loop(spec, ks, N, train, test, w, dev, rows=1024, cap=1024, sink=None, lr=None, frags=None, opts=None,
+          **extra):
     """A LanesLoop over worker ids `ks` (of N) with fresh rings / windows."""
     h, host = _native.hip(), _native.host
     o = opts or SolverOptions()
@@ -35,7 +36,7 @@ def _loop(spec, ks, N, train, test, w, dev, rows=1024, cap=1024, sink=None, lr=N
              window=[wn.handle for wn in wins], w=w.data_ptr(), lr=float(lr if lr is not None else 1.0 / N),
              shi=[f.hi.data_ptr() for f in frags], slo=[f.lo.data_ptr() for f in frags],
              sb=[f.b.data_ptr() for f in frags], scoff=0, Xt=test.X.data_ptr(), yt=test.y.data_ptr(), T=test.T,
-             sink=sink.native.handle if sink is not None else 0, api=host.capi())
+             sink=sink.native.handle if sink is not None else 0, api=host.capi(), **extra)
     lp = h.LanesLoop(d, None)
     return lp, (rings, wins, frags)
 
@@ -194,7 +195,7 @@ def test_lanes_ring_rows_across_epoch_wrap(cuda):
     1024 r + s, i.e. dataset row k + ((1024 r + s) mod shard) * N."""
     spec, train, ev = _data(cuda, rows=3000)  # 1500 rows per worker: round 1 wraps
     w = spec.init("random", seed=2, device=cuda)
-    lp, (rings, wins, frags) = _loop(spec, [0, 1], 2, train, ev, w, cuda)
+    lp, (rings, wins, frags) = _loop(spec, [0, 1], 2, train, ev, w, cuda, epochs=10)
     for rnd in range(3):
         lp.run(1, rnd, stream_handle(cuda))
         torch.cuda.synchronize()

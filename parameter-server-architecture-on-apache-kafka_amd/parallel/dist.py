@@ -385,17 +385,18 @@ class DistEngine:
         t_start = time.time()
         r = self.rounds
         vote = None
-        if not cfg.max_iters:  # run until the data / the wall clock says stop: agreed without host syncs
+        if not cfg.max_iters and not lanes:  # run until the data / the wall clock says stop: agreed without host syncs
             if sched == "allreduce" and wk is not None:
                 payload = self._vote_payload()
                 vote = StopVote(self.device, payload[P:], r)
             else:
                 vote = StopVote(self.device, torch.zeros(1, dtype=torch.float32, device=self.device), r)
         ingested_ahead = False
-        if vote is None and lanes:
+        if lanes:
             # every round of this rank in the multi-lane loop: its workers' solves on their
             # XCDs (one launch), the lane sum reduced to the server over RCCL, the update,
-            # the weights broadcast back (or all-reduced into every replica)
+            # the weights broadcast back (or all-reduced into every replica); an unbounded
+            # run stops by a collective vote between chunks of rounds
             n = self._run_bsp_lanes(comm, cfg.max_iters)
             r += n
             if srv is not None:
@@ -411,7 +412,7 @@ class DistEngine:
             r += n  # (rank 0's tracker advanced natively)
             srv.updates += N * n
             wk.vc = r
-        while True:
+        while not lanes:
             if cfg.max_iters and r - self.rounds >= cfg.max_iters:
                 break
             if vote is not None:
@@ -548,7 +549,7 @@ class DistEngine:
             return False
         if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
             return False
-        if not c.max_iters or c.max_wallclock_s or c.checkpoint_dir or c.iter_new_rows or c.iter_new_frac:
+        if c.checkpoint_dir or c.iter_new_rows or c.iter_new_frac:
             return False
         if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop or c.dtype != "bf16":
             return False
@@ -606,7 +607,7 @@ class DistEngine:
             lp.set_next_local(i, int(w.source.next_local))
         stream = comm.compute_stream()
         try:
-            n = int(lp.run(int(rounds), int(self.rounds), stream))
+            n = self._lanes_chunks(lp, comm, stream, int(rounds), W)
             lp.flush(stream)
             torch.cuda.synchronize(self.device)
             lp.poll_errors()
@@ -625,6 +626,32 @@ class DistEngine:
             srv.frag.refresh(srv.w)
         self.native_host_us_per_round = float(lp.host_us_per_round)
         return n
+
+    def _lanes_chunks(self, lp, comm, stream, rounds: int, W) -> int:
+        """Rounds of the native lanes loop: a bounded run in one call; an unbounded
+        one (max_iters 0: ServerAppRunner's default) in chunks of 256 rounds with a
+        collective stop vote after each -- stop when any rank's wall clock is up or
+        every worker rank's stream has been exhausted for idle_exit_s (the dedicated
+        server rank has no say on data)."""
+        cfg = self.cfg
+        if rounds:
+            return int(lp.run(rounds, int(self.rounds), stream))
+        t_start = time.time()
+        exhausted_since = None
+        flag = torch.zeros(2, dtype=torch.float32, device=self.device)
+        n = 0
+        while True:
+            n += int(lp.run(256, int(self.rounds) + n, stream))
+            now = time.time()
+            if W and all(lp.exhausted(i) for i in range(len(W))):
+                exhausted_since = exhausted_since or now
+            done_data = not W or (exhausted_since is not None and now - exhausted_since >= cfg.idle_exit_s)
+            flag[0] = 1.0 if (cfg.max_wallclock_s and now - t_start >= cfg.max_wallclock_s) else 0.0
+            flag[1] = 0.0 if done_data else 1.0
+            comm.all_reduce(flag)
+            f = flag.tolist()
+            if f[0] > 0 or f[1] == 0:
+                return n
 
     def _native_bsp_ok(self, sched: str, comm) -> bool:
         """The native BSP loop (csrc/runtime/bsp_loop.h) runs this rank: allreduce

@@ -308,6 +308,7 @@ class LocalEngine:
         chunk = 256
         if cfg.checkpoint_dir and cfg.checkpoint_every:
             chunk = max(1, int(cfg.checkpoint_every))
+        exhausted_since = None
         try:
             while True:
                 todo = chunk
@@ -315,7 +316,9 @@ class LocalEngine:
                     todo = min(todo, cfg.max_iters - (r - r0))
                     if todo <= 0:
                         break
-                if cfg.max_wallclock_s and time.time() - t_start >= cfg.max_wallclock_s:
+                if lp.all_exhausted:  # the streams ended: stale windows for idle_exit_s more
+                    exhausted_since = exhausted_since or time.time()
+                if self._stop(r - r0, t_start, exhausted_since):
                     break
                 n = int(lp.run(int(todo), int(r), stream))
                 r += n

@@ -154,3 +154,40 @@ def test_dist_lanes_world1_matches_local(cuda, pg, sched):
     b = [(r[1], round(r[2], 6)) for r in ref.log.book.server]
     assert [r[0] for r in a] == list(range(10)) and len(eng.log.book.worker) == 40
     assert sum(x != y for x, y in zip(a, b)) <= 2  # (argmax ties may flip with last-bit differences)
+
+
+def test_dist_lanes_unbounded_run_stops_by_vote(cuda, pg):
+    """max_iters 0 (the CLI default) runs natively too: chunks of the lanes loop with
+    a collective stop vote -- by the wall clock, or when the data is exhausted."""
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(8000, seed=0), synth_finefood(500, seed=1)
+    kw = dict(consistency_model=0, producer_time_per_event=0, stream_mode="per_iter", rows_per_iter=256,
+              init="random", min_buffer_size=256, max_buffer_size=512, max_iters=0, num_workers=2,
+              workers_per_rank=2, bsp_schedule="allreduce")
+    eng = DistEngine(PSConfig(epochs=1000, max_wallclock_s=1.0, **kw), 0, 1, cuda, train=train, test=test)
+    out = eng.run()
+    assert getattr(eng, "_lanes", None) is not None and out["rounds"] >= 256 and out["rounds"] % 256 == 0
+    assert [r[1] for r in eng.log.book.server] == list(range(out["rounds"]))
+    # data exhausted (1 epoch = 4000 rows per worker = 16 rounds of deliveries), then idle_exit_s
+    eng = DistEngine(PSConfig(epochs=1, idle_exit_s=0.3, **kw), 0, 1, cuda, train=train, test=test)
+    out = eng.run()
+    assert getattr(eng, "_lanes", None) is not None and out["rounds"] >= 256
+    assert eng.workers[0].source.exhausted
+
+
+def test_local_lanes_unbounded_run_stops_when_data_is_exhausted(cuda):
+    from psx.runtime.config import PSConfig
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(8000, seed=0), synth_finefood(500, seed=1)
+    cfg = PSConfig(consistency_model=0, producer_time_per_event=0, stream_mode="per_iter", rows_per_iter=256,
+                   init="random", min_buffer_size=256, max_buffer_size=512, max_iters=0, num_workers=2, epochs=1,
+                   idle_exit_s=0.3)
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    out = eng.run()
+    assert out.get("lanes") == 2 and out["rounds"] >= 16
+    assert all(w.source.exhausted for w in eng.workers)

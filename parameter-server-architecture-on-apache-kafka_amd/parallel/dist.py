@@ -50,7 +50,7 @@ import torch.distributed as dist
 from .. import _native
 from ..models.logreg import ModelSpec
 from ..ops.lr import is_gpu
-from ..runtime.config import PSConfig
+from ..runtime.config import PSConfig, cadence_free
 from ..runtime.engine import load_datasets
 from ..runtime.faults import WorkerFailure, drop_on_failure
 from ..ops.sparse import SparseDelta, nz_capacity
@@ -549,7 +549,7 @@ class DistEngine:
             return False
         if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
             return False
-        if c.checkpoint_dir or c.iter_new_rows or c.iter_new_frac:
+        if c.checkpoint_dir or not cadence_free(c):
             return False
         if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop or c.dtype != "bf16":
             return False
@@ -664,7 +664,7 @@ class DistEngine:
             return False
         if wk.wide or wk.evalset is None or self.tracer.enabled or not c.max_iters or c.max_wallclock_s:
             return False
-        if c.iter_new_rows or c.iter_new_frac or c.checkpoint_dir or c.inject_worker_delay_ms or c.inject_worker_crash \
+        if not cadence_free(c) or c.checkpoint_dir or c.inject_worker_delay_ms or c.inject_worker_crash \
                 or c.inject_worker_stop:
             return False
         src = wk.source

@@ -94,3 +94,18 @@ class PSConfig:
 
     def to_dict(self) -> dict:
         return asdict(self)
+
+
+def cadence_free(c: "PSConfig") -> bool:
+    """True when the tuple-driven cadence (iter_new_rows / iter_new_frac) never
+    holds a worker back: no cadence, or per-round deliveries (stream_mode
+    per_iter) that always bring at least the required new tuples -- the native
+    round loops (which solve every round) then run the same schedule."""
+    import math
+
+    if not c.iter_new_rows and not c.iter_new_frac:
+        return True
+    if c.stream_mode != "per_iter" or c.rows_per_iter <= 0:
+        return False
+    return c.rows_per_iter >= max(c.iter_new_rows, math.ceil(c.iter_new_frac * c.max_buffer_size))
+

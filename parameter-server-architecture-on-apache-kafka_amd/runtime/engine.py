@@ -33,7 +33,7 @@ from ..utils import data as data_mod
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
-from .config import PSConfig
+from .config import PSConfig, cadence_free
 from .faults import WorkerFailure, drop_on_failure
 from .roles import EvalPair, ServerRole, WorkerRole, make_evalset
 
@@ -212,7 +212,7 @@ class LocalEngine:
         wk, srv = self.workers[0], self.server
         if wk.wide or not srv.pair.shared or wk.evalset is None or self.tracer.enabled:
             return False
-        if not c.max_iters or c.max_wallclock_s or c.iter_new_rows or c.iter_new_frac or c.checkpoint_dir or c.inject_worker_delay_ms \
+        if not c.max_iters or c.max_wallclock_s or not cadence_free(c) or c.checkpoint_dir or c.inject_worker_delay_ms \
                 or c.inject_worker_crash or c.inject_worker_stop:
             return False
         if c.stream_mode == "per_iter":
@@ -237,7 +237,7 @@ class LocalEngine:
         W = [w for w in self.workers if w.k not in self.failed]
         if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
             return False
-        if c.iter_new_rows or c.iter_new_frac or c.inject_worker_delay_ms or c.inject_worker_crash \
+        if not cadence_free(c) or c.inject_worker_delay_ms or c.inject_worker_crash \
                 or c.inject_worker_stop:
             return False
         sp = self.spec

@@ -129,8 +129,9 @@ def main():
     ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--out", default="evaluation/psx_logs")
     ap.add_argument("--table-only", action="store_true")
-    ap.add_argument("--iter_new_frac", type=float, default=0.0,
-                    help="worker cadence: iterate once this fraction of the window is new (0: off)")
+    ap.add_argument("--iter_new_frac", type=float, default=0.5,
+                    help="worker cadence: iterate once this fraction of the window is new (the CLI default 0.5; "
+                         "0: continuously)")
     ap.add_argument("--iter_new_rows", type=int, default=0,
                     help="worker cadence: iterate after this many new tuples (0: continuously, the reference's way)")
     a = ap.parse_args()

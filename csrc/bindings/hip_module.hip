@@ -355,7 +355,8 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("dense_delta", &WideCfg::dense_delta)
       .def_readwrite("pulled", &WideCfg::pulled)
       .def_readwrite("own_W", &WideCfg::own_W)
-      .def_readwrite("own_S", &WideCfg::own_S);
+      .def_readwrite("own_S", &WideCfg::own_S)
+      .def_readwrite("persist", &WideCfg::persist);
 
   py::class_<RcclComm>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
@@ -739,6 +740,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("exhausted", &LanesLoop::exhausted)
       .def_property_readonly("all_exhausted", &LanesLoop::all_exhausted)
       .def_property_readonly("hand_off_scope", &LanesLoop::hand_off_scope)
+      .def_property_readonly("side_eval", &LanesLoop::side_eval)
       .def_property_readonly("host_us_per_round", &LanesLoop::host_us_per_round)
       .def_property_readonly("rounds_run", &LanesLoop::rounds_run)
       .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })
@@ -799,6 +801,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.log_workers = I("log_workers", 1) != 0;
              c.tracker = U("tracker");
              c.api = U("api");
+             c.margin_refresh = (int)I("margin_refresh", 256);
              return std::make_unique<KeyRangeLoop>(c, comm);
            }),
            py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())

@@ -21,4 +21,19 @@ void launch_kr_gather(const float* shard, int64_t lo, int KP, const int32_t* ids
 void launch_kr_apply(float* shard, int64_t lo, int KP, const int32_t* ids, const unsigned* n_dev, int n_host,
                      const float* vals, float lr, float* b, const float* db, int nmax, hipStream_t s);
 
+// The round's evaluation rows from maintained margins (no pass over the
+// sharded model):
+//  * worker row: zw = z[r] + sum over the row's window features of
+//    v * dloc[KP + l*KP] (the solver's table maps f -> l) + wloc_b -> confusion
+//    into `slot` with the solver's loss; dz[r] = that window sum (this worker's
+//    share of the global margin update).  htab == nullptr: no worker row, dz = 0.
+void launch_kr_worker_rows(int K, int KP, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                           const int32_t* y, int T, const float* z, const int2* htab, unsigned hmask,
+                           const float* dloc, const float* wloc_b, float* dz, int* acc, unsigned* ticket, void* slot,
+                           const float* loss, unsigned long long seq, hipStream_t s);
+//  * server row: z += lr * dz (dz all-reduced over the ranks: every worker's
+//    delta), then the confusion of z + b into `slot` (null: the update only).
+void launch_kr_server_rows(int K, int KP, const int32_t* y, int T, float* z, const float* dz, float lr, const float* b,
+                           int* acc, unsigned* ticket, void* slot, unsigned long long seq, hipStream_t s);
+
 }  // namespace psx

@@ -119,5 +119,10 @@ int lanes_grid(int L, int min_riders);
 void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const LanesArgs& a, int S, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).
 void launch_xcc_probe(int* ids, int n, hipStream_t s);
+// Evaluation of ev's models as a launch of its own that co-runs with a lanes
+// round (side stream; 8.6 KB LDS per workgroup, lanes_eval_grid() workgroups,
+// ev.nticket must equal that grid).  Same EvalSlot publication.
+int lanes_eval_grid();
+void launch_lanes_eval(const SolverCfg& cfg, const EvalMulti& ev, hipStream_t s);
 
 }  // namespace psx

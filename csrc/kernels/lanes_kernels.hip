@@ -570,4 +570,123 @@ void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const La
 
 void launch_xcc_probe(int* ids, int n, hipStream_t s) { xcc_probe_kernel<<<n, 64, 0, s>>>(ids, n); }
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// Side-stream evaluation (8 lanes: every XCD solves, so in-launch riders could
+// only start once the solves have freed their CUs).  The same models and
+// EvalSlot protocol as eval_multi_body, in a launch sized to CO-RUN with the
+// next round's kernel: a lane workgroup leaves ~14.5 KB of LDS and ~150 VGPRs
+// per SIMD lane free on its CU, and this kernel needs 8.6 KB of LDS and no LDS
+// staging -- each wave streams its 256-feature slice of a 16-row test tile from
+// global memory straight into the MFMA A operand, against the pair's weight
+// fragments held in registers.  Items = (model pair, 16-row tile), pair-major
+// contiguous chunks per workgroup.
+template <int FP>
+__global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
+  __shared__ f32x4 red[4][64];
+  __shared__ int cl[kMaxEvalModels][16][8];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int K = ev.K, T = ev.T, M = ev.nmodels;
+  if (M <= 0) return;
+  const int nT = (T + 15) / 16, npairs = (M + 1) / 2;
+  for (int i = tid; i < kMaxEvalModels * 128; i += 256) (&cl[0][0][0])[i] = 0;
+  const int items = npairs * nT, chunk = (items + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
+  const int r = lane & 15, kq = lane >> 4;
+  int curp = -1;
+  WFrag<FP> wf;
+  __syncthreads();
+  for (int it = i0; it < i1; ++it) {
+    const int p = it / nT, tile = it - p * nT;
+    const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
+    const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
+    if (p != curp) {  // (workgroup-uniform)
+      load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
+      curp = p;
+    }
+    const int64_t row = (int64_t)tile * 16 + r;
+    u16x8 a[WFrag<FP>::KS];
+#pragma unroll
+    for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {  // the slice's loads all in flight
+      const int cg = (w * WFrag<FP>::KS + kk) * 4 + kq;
+      a[kk] = row < T ? *(const u16x8*)(ev.Xt + row * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    f32x4 acc = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+      acc = mfma16x16x32(as_bf16x8(a[kk]), as_bf16x8(wf.h[kk]), acc);
+      acc = mfma16x16x32(as_bf16x8(a[kk]), as_bf16x8(wf.l[kk]), acc);
+    }
+    red[w][lane] = acc;
+    __syncthreads();
+    if (tid < 32) {  // (row, model) of the tile: rows 0..15 x models {a, b}
+      const int rr = tid & 15, which = tid >> 4;
+      const int m = which == 0 ? ma : mb;
+      const int64_t grow = (int64_t)tile * 16 + rr;
+      if (m >= 0 && grow < T) {
+        const float* bb = which == 0 ? A.b + A.coff : Bm.b + Bm.coff;
+        int best = 0;
+        float bz = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const int ln = (rr >> 2) * 16 + which * 8 + c, reg = rr & 3;
+          const float z = red[0][ln][reg] + red[1][ln][reg] + red[2][ln][reg] + red[3][ln][reg] + bb[c];
+          if (z > bz) {
+            bz = z;
+            best = c;
+          }
+        }
+        const int y = ev.yt[grow];
+        atomicAdd(&cl[m][y < 0 ? 0 : (y > 15 ? 15 : y)][best], 1);
+      }
+    }
+    __syncthreads();
+  }
+  for (int m = 0; m < M; ++m)
+    if (tid < 128) {
+      const int v = cl[m][tid >> 3][tid & 7];
+      if (v) atomicAdd(ev.acc + (m * 256 + (tid >> 3) * 16 + (tid & 7)) * kAccStride, v);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int m = 0; m < M; ++m) {
+    const EvalModel E = pick(ev.m, m);
+    const int tot = __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((int*)E.slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0)
+      __hip_atomic_store((float*)(E.slot + 1024), E.loss ? *E.loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int m = 0; m < M; ++m) {
+      const EvalModel E = pick(ev.m, m);
+      __hip_atomic_store((unsigned long long*)(E.slot + 1032), E.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+}  // namespace
+
+int lanes_eval_grid() { return 256; }
+
+void launch_lanes_eval(const SolverCfg& cfg, const EvalMulti& ev, hipStream_t s) {
+  if (ev.nmodels <= 0) return;
+  const int g = lanes_eval_grid();
+  switch (cfg.Fp) {
+    case 128: lanes_eval_kernel<128><<<g, 256, 0, s>>>(ev); break;
+    case 256: lanes_eval_kernel<256><<<g, 256, 0, s>>>(ev); break;
+    case 512: lanes_eval_kernel<512><<<g, 256, 0, s>>>(ev); break;
+    case 1024: lanes_eval_kernel<1024><<<g, 256, 0, s>>>(ev); break;
+    default: break;
+  }
+}
+
 }  // namespace psx

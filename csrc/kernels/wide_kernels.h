@@ -60,6 +60,9 @@ struct WideCfg {
   int pulled;
   int own_W;
   int64_t own_S;
+  // the whole solve in one persistent launch (wide_persist_kernel) instead of the
+  // launch chain; only for a solver alone on the GPU (its workgroups must be co-resident)
+  int persist;
 };
 
 constexpr int kMaxOwners = 64;
@@ -121,6 +124,7 @@ struct WideDev {
   int32_t* bcount;     // [ngroups] distinct features per group
   int RB, EB, TS;      // rows per group, EB = RB*NZ, LDS hash size (pow2 >= 2*EB)
   unsigned long long* gbar;  // grid-barrier counter of the tail launch (reset per solve)
+  unsigned* pbar;            // [2] self-resetting grid barrier of the persistent solve: count, generation
   float* s1;           // [umax] feature sums over the window
   float* s2;           // [umax] feature sums of squares
   float* scale;        // [umax] effective coefficient = scale * x
@@ -156,6 +160,10 @@ void wide_launch_slot(const WideCfg& c, const WideDev& d, int slot, int nblk_dot
 // Line-search retry slots [s0, s1) in one persistent launch (grid barriers).
 void wide_launch_tail(const WideCfg& c, const WideDev& d, int s0, int s1, hipStream_t s);
 void wide_prepare_kernels();  // LDS attributes of the tail kernels (call before capture)
+// The solve (phases 3) or one of its phases (1: begin + plan, 2: the rest) in one
+// persistent launch of wide_persist_grid() co-resident workgroups.
+void wide_launch_persist(const WideCfg& c, const WideDev& d, int B, int start, int phases, hipStream_t s);
+int wide_persist_grid();
 void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s);
 int wide_dots_blocks(int64_t PLmax);
 

@@ -80,18 +80,22 @@ __device__ __forceinline__ float row_residual(const float (&z)[KP], int K, int y
 
 // ---------------------------------------------------------------------------
 // begin: reset the previous solve's feature map entries, publish the window.
-__global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int start) {
+__device__ __forceinline__ void wide_begin_body(const WideDev& d, int B, int start, int blk, int nblk) {
   const unsigned prevU = d.cnt[2];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  const unsigned nthr = blockDim.x;
+  if (blk == 0 && threadIdx.x == 0) {
     d.prm->B = B;
     d.prm->start = start;
-    d.cnt[0] = 0u;  // not read by anybody else in this kernel
+    d.cnt[0] = 0u;  // not read by anybody else in this phase
     d.cnt[1] = 0u;
     *d.gbar = 0ull;  // grid-barrier counter of this solve's tail launch
   }
-  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < prevU; i += gridDim.x * 256)
-    d.htab[d.hslot[i]] = make_int2(-1, -1);
-  if (blockIdx.x == 0 && threadIdx.x < 2 * kMaxOwners) d.own[threadIdx.x] = 0u;
+  for (unsigned i = blk * nthr + threadIdx.x; i < prevU; i += nblk * nthr) d.htab[d.hslot[i]] = make_int2(-1, -1);
+  if (blk == 0 && threadIdx.x < 2 * kMaxOwners) d.own[threadIdx.x] = 0u;
+}
+
+__global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int start) {
+  wide_begin_body(d, B, start, blockIdx.x, gridDim.x);
 }
 
 // plan: per group of RB window rows, dedup the entries' features in an LDS
@@ -102,23 +106,24 @@ __global__ __launch_bounds__(256) void wide_begin_kernel(WideDev d, int B, int s
 // of one per row.
 __device__ __forceinline__ unsigned wide_hash(int f) { return (unsigned)f * 2654435761u; }
 
-__global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
-  extern __shared__ __attribute__((aligned(16))) int plan_lds[];
+// Group `b` of the window (any block size; LDS: (2 TS + EB) ints at plan_lds).
+__device__ __forceinline__ void wide_plan_body(const WideCfg& c, const WideDev& d, int b, int* plan_lds) {
   const int TS = d.TS, EB = d.EB, RB = d.RB, NZ = c.NZ, cap = c.cap;
+  const int nthr = blockDim.x;
   int* keys = plan_lds;        // [TS]
   int* sidx = keys + TS;       // [TS]
   int* bf = sidx + TS;         // [EB]
   __shared__ int nuq;
   const int B = d.prm->B, start = d.prm->start;
-  const int b = blockIdx.x, t = threadIdx.x, lane = __lane_id();
+  const int t = threadIdx.x, lane = __lane_id();
   const int r0 = b * RB;
   if (r0 >= B) return;
   const int rows = min(RB, B - r0);
-  for (int h = t; h < TS; h += 256) keys[h] = -1;
+  for (int h = t; h < TS; h += nthr) keys[h] = -1;
   if (t == 0) nuq = 0;
   __syncthreads();
   const int ne = rows * NZ;
-  for (int el = t; el < ne; el += 256) {
+  for (int el = t; el < ne; el += nthr) {
     const int r = el / NZ, j = el - r * NZ;
     int sl = start + r0 + r;
     if (sl >= cap) sl -= cap;
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
     }
   }
   __syncthreads();
-  for (int h = t; h < TS; h += 256) {
+  for (int h = t; h < TS; h += nthr) {
     const int k = keys[h];
     if (k != -1) {
       const int sidx_h = atomicAdd(&nuq, 1);
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
   }
   __syncthreads();
   const int n = nuq;
-  for (int el = t; el < ne; el += 256) {
+  for (int el = t; el < ne; el += nthr) {
     const int r = el / NZ, j = el - r * NZ;
     int sl = start + r0 + r;
     if (sl >= cap) sl -= cap;
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
     d.pslot[(int64_t)(r0 + r) * NZ + j] = (uint16_t)sidx[h];
   }
   int32_t* gfeat = d.bfeat + (int64_t)b * EB;
-  for (int base = 0; base < n; base += 256) {  // uniform trip count: every lane reaches the ballot
+  for (int base = 0; base < n; base += nthr) {  // uniform trip count: every lane reaches the ballot
     const int si = base + t;
     bool win = false;
     int f = 0;
@@ -181,6 +186,12 @@ __global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
     }
   }
   if (t == 0) d.bcount[b] = n;
+  __syncthreads();  // the LDS table is reused by the block's next group
+}
+
+__global__ __launch_bounds__(256) void wide_plan_kernel(WideCfg c, WideDev d) {
+  extern __shared__ __attribute__((aligned(16))) int plan_lds[];
+  wide_plan_body(c, d, blockIdx.x, plan_lds);
 }
 
 // owner order (pull mode, own_W > 1): per-owner counts of the window's
@@ -227,10 +238,11 @@ __global__ __launch_bounds__(256) void wide_owner_scatter_kernel(WideCfg c, Wide
 
 // assign: table entry of every local id, gather the old weights of the
 // window's features (the dense pulled vector, or the pulled values in pull mode).
-__global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) {
+__device__ __forceinline__ void wide_assign_body(const WideCfg& c, const WideDev& d, int blk, int nblk) {
   const unsigned U = d.cnt[0];
   const int KP = c.KP;
-  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+  const unsigned nthr = blockDim.x;
+  for (unsigned i = blk * nthr + threadIdx.x; i < U; i += nblk * nthr) {
     const int f = d.uniq[i];
     unsigned h = wide_gslot(f, d.hmask);
     while (d.htab[h].x != f) h = (h + 1) & d.hmask;
@@ -242,27 +254,31 @@ __global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) 
     d.s1[i] = 0.f;
     d.s2[i] = 0.f;
   }
-  if (blockIdx.x == 0 && threadIdx.x < KP)
-    d.w0[threadIdx.x] = c.pulled ? d.w_pull_b[threadIdx.x] : d.w_old[c.F * KP + threadIdx.x];
+  if (blk == 0 && threadIdx.x < KP)  // intercepts: kept apart (w_pull_b) or after the coefficients
+    d.w0[threadIdx.x] = d.w_pull_b ? d.w_pull_b[threadIdx.x] : d.w_old[c.F * KP + threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void wide_assign_kernel(WideCfg c, WideDev d) {
+  wide_assign_body(c, d, blockIdx.x, gridDim.x);
 }
 
 // stats: local ids of the group's features, every entry's local id, and the
 // feature sums for the 1/std scaling aggregated per group in LDS.
-__global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
-  extern __shared__ __attribute__((aligned(16))) int st_lds[];
+__device__ __forceinline__ void wide_stats_body(const WideCfg& c, const WideDev& d, int b, int* st_lds) {
   const int EB = d.EB, RB = d.RB, NZ = c.NZ, cap = c.cap;
+  const int nthr = blockDim.x;
   int* lid_s = st_lds;                  // [EB]
   float* s1l = (float*)(lid_s + EB);    // [EB]
   float* s2l = s1l + EB;                // [EB]
   const int B = d.prm->B, start = d.prm->start;
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   const int r0 = b * RB;
   if (r0 >= B) return;
   const int rows = min(RB, B - r0);
   const int n = d.bcount[b];
   const int32_t* gfeat = d.bfeat + (int64_t)b * EB;
   int32_t* glid = d.blid + (int64_t)b * EB;
-  for (int si = t; si < n; si += 256) {
+  for (int si = t; si < n; si += nthr) {
     const int l = wide_find(d.htab, d.hmask, gfeat[si]);
     lid_s[si] = l;
     glid[si] = l;
@@ -271,7 +287,7 @@ __global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
   }
   __syncthreads();
   const int ne = rows * NZ;
-  for (int el = t; el < ne; el += 256) {
+  for (int el = t; el < ne; el += nthr) {
     const int r = el / NZ, j = el - r * NZ;
     int sl = start + r0 + r;
     if (sl >= cap) sl -= cap;
@@ -285,22 +301,29 @@ __global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
       atomicAdd(&s2l[ps], v * v);
     }
   }
-  if (!c.standardize) return;
   __syncthreads();
-  for (int si = t; si < n; si += 256) {
-    atomicAdd(&d.s1[lid_s[si]], s1l[si]);
-    atomicAdd(&d.s2[lid_s[si]], s2l[si]);
+  if (c.standardize) {
+    for (int si = t; si < n; si += nthr) {
+      atomicAdd(&d.s1[lid_s[si]], s1l[si]);
+      atomicAdd(&d.s2[lid_s[si]], s2l[si]);
+    }
   }
+  __syncthreads();  // the block's next group reuses the LDS
+}
+
+__global__ __launch_bounds__(256) void wide_stats_kernel(WideCfg c, WideDev d) {
+  extern __shared__ __attribute__((aligned(16))) int st_lds[];
+  wide_stats_body(c, d, blockIdx.x, st_lds);
 }
 
 // prep: per-feature scaling, starting point x, zeroed direction / gradients,
 // controller init.
-__global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
+__device__ __forceinline__ void wide_prep_body(const WideCfg& c, const WideDev& d, int blk, int nblk) {
   const unsigned U = d.cnt[0];
   const int KP = c.KP, K = c.K;
   const int B = d.prm->B;
   const int64_t PL = KP + (int64_t)U * KP;
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+  const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x, gs = (int64_t)nblk * blockDim.x;
   for (int64_t i = gid; i < U; i += gs) {
     float sc = 1.f, gsc = 1.f, xs = 1.f;
     if (c.standardize) {
@@ -337,6 +360,10 @@ __global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
     d.ctrl->t = 0.0;
     for (int s = 0; s < c.sc.nslots; ++s) d.loss_acc[s] = 0.0;
   }
+}
+
+__global__ __launch_bounds__(256) void wide_prep_kernel(WideCfg c, WideDev d) {
+  wide_prep_body(c, d, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -703,11 +730,11 @@ __global__ __launch_bounds__(512) void wide_tail_kernel(WideCfg c, WideDev d, in
 }
 
 // finalize: effective coefficients, centring, local delta (+ dense scatter).
-__global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d) {
+__device__ __forceinline__ void wide_finalize_body(const WideCfg& c, const WideDev& d, int blk, int nblk) {
   const unsigned U = d.cnt[0];
   const int KP = c.KP, K = c.K;
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int64_t i = gid; i <= (int64_t)U; i += (int64_t)gridDim.x * 256) {
+  const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x;
+  for (int64_t i = gid; i <= (int64_t)U; i += (int64_t)nblk * blockDim.x) {
     // i < U: feature i ; i == U: the intercepts
     const bool icpt = i == (int64_t)U;
     const int64_t p0 = icpt ? 0 : KP + i * KP;
@@ -749,6 +776,84 @@ __global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d
     // read by the host after a stream synchronisation: no release (an L2 writeback) needed
     if (d.host_u) __hip_atomic_store(d.host_u, U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+__global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d) {
+  wide_finalize_body(c, d, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// wide_persist_kernel: the whole solve (or, in pull mode, its second phase) in
+// ONE launch of co-resident workgroups, the phases separated by a
+// self-resetting grid barrier (arrival count + generation word: the last
+// arriver zeroes the count and bumps the generation, the others poll the
+// generation).  On MI355X a kernel boundary of the launch chain costs ~4.5-5 us
+// of device time even for an empty phase (profiles/r03_v4), a barrier ~2-3 us.
+// phases: bit 0 = begin + plan, bit 1 = assign .. finalize.
+__device__ __forceinline__ void wide_gen_barrier(unsigned* bar, unsigned G, unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == G - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      (void)__hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int spins = 0;
+      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1 << 24)) {  // never expected: a workgroup was not co-resident
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int KP, int NQ>
+__global__ __launch_bounds__(512) void wide_persist_kernel(WideCfg c, WideDev d, int B, int start, int phases) {
+  extern __shared__ __attribute__((aligned(16))) int pl_lds[];
+  __shared__ WideFwdShared fsh;
+  __shared__ WideDotsShared dsh;
+  __shared__ int phase_s;
+  const int G = gridDim.x, blk = blockIdx.x;
+  const int ngr = (c.cap + d.RB - 1) / d.RB;
+  unsigned* err = d.cnt + 3;
+  if (phases & 1) {
+    wide_begin_body(d, B, start, blk, G);
+    wide_gen_barrier(d.pbar, G, err);
+    for (int grp = blk; grp < ngr; grp += G) wide_plan_body(c, d, grp, pl_lds);
+    wide_gen_barrier(d.pbar, G, err);
+  }
+  if (!(phases & 2)) return;
+  wide_assign_body(c, d, blk, G);
+  wide_gen_barrier(d.pbar, G, err);
+  for (int grp = blk; grp < ngr; grp += G) wide_stats_body(c, d, grp, pl_lds);
+  wide_gen_barrier(d.pbar, G, err);
+  wide_prep_body(c, d, blk, G);
+  wide_gen_barrier(d.pbar, G, err);
+  for (int slot = 0; slot < c.sc.nslots; ++slot) {
+    if (threadIdx.x == 0)
+      phase_s = __hip_atomic_load(&d.ctrl->phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (phase_s == kPhDone) break;  // uniform: every workgroup read the word after the last barrier
+    const int Bw = d.prm->B;
+    for (int grp = blk; grp * d.RB < Bw; grp += G) wide_fwdbwd_body<KP, NQ>(c, d, slot, grp, (float*)pl_lds, fsh);
+    wide_gen_barrier(d.pbar, G, err);
+    wide_dots_body(c, d, slot, blk, G, dsh);
+    wide_gen_barrier(d.pbar, G, err);
+    wide_apply_body(c, d, slot, blk, G);
+    wide_gen_barrier(d.pbar, G, err);
+  }
+  wide_finalize_body(c, d, blk, G);
 }
 
 // ---------------------------------------------------------------------------
@@ -851,12 +956,21 @@ static void set_tail_attr() {
   (void)hipFuncSetAttribute((const void*)wide_tail_kernel<KP, NQ>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             96 * 1024);
 }
+template <int KP, int NQ>
+static void set_persist_attr() {
+  (void)hipFuncSetAttribute((const void*)wide_persist_kernel<KP, NQ>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            96 * 1024);
+}
 template <int KP>
 static void set_tail_attr_kp() {
   set_tail_attr<KP, 1>();
   set_tail_attr<KP, 2>();
   set_tail_attr<KP, 4>();
   set_tail_attr<KP, 8>();
+  set_persist_attr<KP, 1>();
+  set_persist_attr<KP, 2>();
+  set_persist_attr<KP, 4>();
+  set_persist_attr<KP, 8>();
 }
 void wide_prepare_kernels() {
   static bool done = false;
@@ -867,6 +981,39 @@ void wide_prepare_kernels() {
   set_tail_attr_kp<8>();
   set_tail_attr_kp<16>();
   done = true;
+}
+
+size_t wide_persist_lds(const WideCfg& c, const WideDev& d) {
+  const size_t plan = (size_t)(2 * d.TS + d.EB) * 4, stats = (size_t)d.EB * 12, fb = (size_t)d.EB * c.KP * 4;
+  size_t m = plan > stats ? plan : stats;
+  return m > fb ? m : fb;
+}
+
+int wide_persist_grid() { return 256; }
+
+template <int KP>
+static void launch_persist_kp(const WideCfg& c, const WideDev& d, int B, int start, int phases, hipStream_t s) {
+  const int nq = (c.NZ + 63) / 64;
+  const size_t lds = wide_persist_lds(c, d);
+  const int G = wide_persist_grid();
+  if (nq <= 1)
+    wide_persist_kernel<KP, 1><<<G, 512, lds, s>>>(c, d, B, start, phases);
+  else if (nq <= 2)
+    wide_persist_kernel<KP, 2><<<G, 512, lds, s>>>(c, d, B, start, phases);
+  else if (nq <= 4)
+    wide_persist_kernel<KP, 4><<<G, 512, lds, s>>>(c, d, B, start, phases);
+  else
+    wide_persist_kernel<KP, 8><<<G, 512, lds, s>>>(c, d, B, start, phases);
+}
+
+void wide_launch_persist(const WideCfg& c, const WideDev& d, int B, int start, int phases, hipStream_t s) {
+  switch (c.KP) {
+    case 1: launch_persist_kp<1>(c, d, B, start, phases, s); break;
+    case 2: launch_persist_kp<2>(c, d, B, start, phases, s); break;
+    case 4: launch_persist_kp<4>(c, d, B, start, phases, s); break;
+    case 8: launch_persist_kp<8>(c, d, B, start, phases, s); break;
+    default: launch_persist_kp<16>(c, d, B, start, phases, s); break;
+  }
 }
 
 void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s) {

@@ -19,14 +19,18 @@
 //            already there from the pull); every owner applies w += lr * delta
 //            sender by sender in rank order (deterministic); the intercepts are
 //            replicated and all-reduced
-//   rows     partial test margins of each shard, all-reduced; the server row
-//            (rank 0) is the reduced margins + intercepts; every worker row is
-//            the previous round's margins + the window overlay of its delta
+//   rows     the test margins of the global model are maintained: each worker
+//            adds the window overlay of its delta to them (its worker row, one
+//            pass over the test rows), the per-row sums are all-reduced (T KP
+//            floats) into z += lr * sum, and the server row (rank 0) is z + the
+//            intercepts; every margin_refresh rounds z is recomputed from the
+//            shards (partial margins of each key range, all-reduced)
 //
 // Bytes on the wire per round: 4 W + 8 U + 8 U KP (+ KP intercepts + T KP
 // margins for the rows) with U the window's distinct features -- proportional
-// to the window, independent of F.  At world 1 every exchange is local and the
-// round needs no host synchronisation at all.
+// to the window, independent of F.  At world 1 every exchange is local, the
+// solve reads the shard in place (one hipGraph, no pull phase) and the round
+// needs no host synchronisation at all.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -88,6 +92,9 @@ struct KeyRangeLoopCfg {
   bool log_workers = true;
   uintptr_t tracker = 0;  // VectorClockTracker* (rank 0)
   uintptr_t api = 0;      // HostApi*
+  // the rows' margins are updated incrementally (z += lr * X_test * sum of the
+  // round's deltas) and recomputed from the shards every `margin_refresh` rounds
+  int margin_refresh = 256;
 };
 
 class KeyRangeLoop {
@@ -140,7 +147,8 @@ class KeyRangeLoop {
   int32_t* req_ids_ = nullptr; // [W * umax] ids requested from this owner
   float* req_vals_ = nullptr;  // [W * umax][KP] pulled answers, then pushed deltas
   float* db_ = nullptr;        // [KP] intercept deltas (all-reduced)
-  float* z_[2] = {nullptr, nullptr};  // [T][KP] reduced partial margins, by round parity
+  float* z_ = nullptr;   // [T][KP] test margins of the global model (coefficients only)
+  float* dz_ = nullptr;  // [T][KP] this round's margin update (all-reduced over the ranks)
   int* acc_ = nullptr;
   unsigned* ticket_ = nullptr;
   unsigned* cnt_dev_ = nullptr;  // [2W]: recv counts

@@ -2,6 +2,7 @@
 #include "keyrange_loop.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -50,10 +51,14 @@ KeyRangeLoop::KeyRangeLoop(const KeyRangeLoopCfg& cfg, RcclComm* comm)
     throw std::invalid_argument("KeyRangeLoop: no test set");
   local_total_ = cfg_.ds_rows > cfg_.k ? (cfg_.ds_rows - cfg_.k + cfg_.N - 1) / cfg_.N : 0;
   if (local_total_ == 0) throw std::invalid_argument("KeyRangeLoop: the worker has no rows");
-  c.pulled = 1;
+  c.pulled = W_ > 1 ? 1 : 0;  // world 1: the solve reads the (whole) shard in place
   c.own_W = W_;
   c.own_S = S_;
   c.dense_delta = 0;
+  // the solver is alone on the GPU: its whole solve (pull mode: its second phase)
+  // in one persistent launch (PSX_WIDE_PERSIST=0: the launch chain)
+  const char* wp = std::getenv("PSX_WIDE_PERSIST");
+  c.persist = wp ? (wp[0] == '1' ? 1 : 0) : 1;
   const int64_t E = (int64_t)c.cap * c.NZ;
   umax_ = (int)(c.F < E ? c.F : E);
 
@@ -69,6 +74,7 @@ KeyRangeLoop::KeyRangeLoop(const KeyRangeLoopCfg& cfg, RcclComm* comm)
   const size_t o_db = take(16 * 4);
   const size_t o_z0 = evaluates ? take((size_t)cfg_.T * KP_ * 4) : 0;
   const size_t o_z1 = evaluates ? take((size_t)cfg_.T * KP_ * 4) : 0;
+  if (cfg_.margin_refresh < 1) cfg_.margin_refresh = 1;
   const size_t o_acc = take((size_t)512 * kAccStride * 4);
   const size_t o_tic = take(64);
   const size_t o_cnt = take((size_t)2 * kMaxOwners * 4);
@@ -81,8 +87,8 @@ KeyRangeLoop::KeyRangeLoop(const KeyRangeLoopCfg& cfg, RcclComm* comm)
   req_vals_ = W_ > 1 ? reinterpret_cast<float*>(bp + o_rval) : nullptr;
   db_ = reinterpret_cast<float*>(bp + o_db);
   if (evaluates) {
-    z_[0] = reinterpret_cast<float*>(bp + o_z0);
-    z_[1] = reinterpret_cast<float*>(bp + o_z1);
+    z_ = reinterpret_cast<float*>(bp + o_z0);
+    dz_ = reinterpret_cast<float*>(bp + o_z1);
   }
   acc_ = reinterpret_cast<int*>(bp + o_acc);
   ticket_ = reinterpret_cast<unsigned*>(bp + o_tic);
@@ -96,7 +102,8 @@ KeyRangeLoop::KeyRangeLoop(const KeyRangeLoopCfg& cfg, RcclComm* comm)
   wb.rval = cfg_.rval;
   wb.rnnz = cfg_.rnnz;
   wb.ry = cfg_.ry;
-  wb.w_pull = w_pull_;
+  wb.w_pull = W_ > 1 ? w_pull_ : nullptr;
+  wb.w_old = W_ > 1 ? nullptr : cfg_.shard;
   wb.w_pull_b = cfg_.b;  // the replicated intercepts are read in place
   wb.dloc = cfg_.dloc;
   wb.wloc = cfg_.wloc;
@@ -198,7 +205,7 @@ int64_t KeyRangeLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double
   const bool evaluates = cfg_.sink && (cfg_.log_server || cfg_.log_workers);
   void* sink = reinterpret_cast<void*>(cfg_.sink);
   if (evaluates && !margins_ready_) {  // the margins the first worker row builds on
-    margins(z_[(r0 + 1) & 1], stream);
+    margins(z_, stream);
     margins_ready_ = true;
   }
   std::vector<int64_t> scnt(W_), rcnt(W_), soff(W_), roff(W_);
@@ -222,10 +229,10 @@ int64_t KeyRangeLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double
       if (epoch_ms() - wait0 > max_wait_s * 1000.0) throw std::runtime_error("KeyRangeLoop: no rows");
       std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
-    // ---- plan: the window's features, grouped by owner ----
-    solver_->plan((int)size, (int)start, stream);
     const int32_t* ids = cfg_.uniq;
     if (W_ > 1) {
+      // ---- plan: the window's features, grouped by owner ----
+      solver_->plan((int)size, (int)start, stream);
       // ---- pull: counts, ids to the owners, coefficients back ----
       const unsigned* own = solver_->owner_counts_dev();
       {
@@ -268,40 +275,49 @@ int64_t KeyRangeLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double
       for (int j = 0; j < W_; ++j)  // sender by sender, in rank order
         launch_kr_apply(cfg_.shard, lo_, KP_, req_ids_ + roff[j], nullptr, (int)rcnt[j], req_vals_ + roff[j] * KP_,
                         cfg_.lr, cfg_.b, j == 0 ? db_ : nullptr, 0, stream);
-    } else {
-      const unsigned* U = solver_->ucount_dev();
-      launch_kr_gather(cfg_.shard, lo_, KP_, ids, U, 0, w_pull_, umax_, stream);
-      hip_check(hipGetLastError(), "keyrange gather");
-      solver_->finish(stream);
-      launch_kr_apply(cfg_.shard, lo_, KP_, ids, U, 0, cfg_.dloc + KP_, cfg_.lr, cfg_.b, cfg_.dloc, umax_, stream);
+    } else {  // the whole key space is local: solve from the shard in place, apply
+      solver_->run((int)size, (int)start, stream);
+      launch_kr_apply(cfg_.shard, lo_, KP_, ids, solver_->ucount_dev(), 0, cfg_.dloc + KP_, cfg_.lr, cfg_.b,
+                      cfg_.dloc, umax_, stream);
     }
     hip_check(hipGetLastError(), "keyrange update");
     model_bytes_ += last_round_bytes_;
-    // ---- rows: the global model of round r (server), worker k's local model ----
+    // ---- rows: worker k's local model (the margins + its window delta), then the
+    // global model of round r (the margins + every worker's delta, all-reduced) ----
     if (evaluates) {
-      margins(z_[par], stream);
-      if (cfg_.log_server && rank_ == 0) {
-        uint64_t seq = 0;
-        uintptr_t addr = 0;
-        const int slot = api().sink_acquire(sink, &seq, &addr);
-        check(slot, "metrics sink acquire");
-        launch_wide_eval(c.K, KP_, c.F, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, nullptr, nullptr, 0u,
-                         nullptr, acc_, ticket_, reinterpret_cast<void*>(addr), nullptr, seq, stream, nullptr, 0,
-                         z_[par], cfg_.b);
-        hip_check(hipGetLastError(), "server row");
-        api().sink_submit(sink, slot, seq, 1, -1, -1, r, 0);
-      }
+      uint64_t seq = 0;
+      uintptr_t addr = 0;
+      int slot = -1;
       if (cfg_.log_workers) {
-        uint64_t seq = 0;
-        uintptr_t addr = 0;
-        const int slot = api().sink_acquire(sink, &seq, &addr);
+        slot = api().sink_acquire(sink, &seq, &addr);
         check(slot, "metrics sink acquire");
-        launch_wide_eval(c.K, KP_, c.F, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, nullptr,
-                         solver_->table(), solver_->table_mask(), cfg_.dloc, acc_, ticket_,
-                         reinterpret_cast<void*>(addr), cfg_.loss, seq, stream, nullptr, 0, z_[par ^ 1], cfg_.wloc);
-        hip_check(hipGetLastError(), "worker row");
-        api().sink_submit(sink, slot, seq, 0, -1, cfg_.k, r, seen);
       }
+      launch_kr_worker_rows(c.K, KP_, cfg_.t_indptr, cfg_.t_idx, cfg_.t_val, cfg_.t_y, cfg_.T, z_, solver_->table(),
+                            solver_->table_mask(), cfg_.dloc, cfg_.wloc, dz_, acc_, ticket_,
+                            reinterpret_cast<void*>(addr), cfg_.loss, seq, stream);
+      hip_check(hipGetLastError(), "worker row");
+      if (slot >= 0) api().sink_submit(sink, slot, seq, 0, -1, cfg_.k, r, seen);
+      if (W_ > 1) {
+        comm_->all_reduce(dz_, dz_, (size_t)cfg_.T * KP_, RcclComm::kF32, stream);
+        eval_bytes_ += (int64_t)cfg_.T * KP_ * 4;
+      }
+      const bool srow = cfg_.log_server && rank_ == 0;
+      const bool refresh = (r + 1) % cfg_.margin_refresh == 0;
+      seq = 0;
+      addr = 0;
+      slot = -1;
+      if (srow) {
+        slot = api().sink_acquire(sink, &seq, &addr);
+        check(slot, "metrics sink acquire");
+      }
+      if (refresh) {  // exact margins from the shards (bounds the drift of the updates)
+        margins(z_, stream);
+        hip_check(hipMemsetAsync(dz_, 0, (size_t)cfg_.T * KP_ * 4, stream), "zero margin update");
+      }
+      launch_kr_server_rows(c.K, KP_, cfg_.t_y, cfg_.T, z_, dz_, cfg_.lr, cfg_.b, acc_, ticket_,
+                            reinterpret_cast<void*>(addr), seq, stream);
+      hip_check(hipGetLastError(), "server row");
+      if (slot >= 0) api().sink_submit(sink, slot, seq, 1, -1, -1, r, 0);
     }
     if (cfg_.tracker && rank_ == 0) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
   }

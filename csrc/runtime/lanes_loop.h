@@ -96,6 +96,9 @@ class LanesLoop {
   bool exhausted(int lane) const { return next_local_[lane] >= local_total_[lane] * cfg_.epochs; }
   bool all_exhausted() const;
   int hand_off_scope() const { return S_; }  // 2: one-XCD hand-offs, 1: sc1 (placement check failed)
+  // true: a round's rows are evaluated by a launch of their own on a side stream
+  // that co-runs with the next round (8 lanes: no XCD left for riders)
+  bool side_eval() const { return side_eval_; }
   double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
   int64_t rounds_run() const { return rounds_run_; }
   // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
@@ -156,6 +159,19 @@ class LanesLoop {
   uint16_t *upd_hi_ = nullptr, *upd_lo_ = nullptr;  // fragments of an update nobody evaluates
   float* upd_b_ = nullptr;
   unsigned long long* err_host_ = nullptr;  // pinned [kMaxLanes]
+  // side-stream evaluation: events by round parity (round done -> evaluation;
+  // evaluation done -> the round that rewrites that parity's fragments)
+  bool side_eval_ = false;
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_round_[2] = {nullptr, nullptr}, ev_eval_[2] = {nullptr, nullptr};
+  bool eval_pending_[2] = {false, false};
+  int* acc2_ = nullptr;
+  unsigned* ticket2_ = nullptr;
+  // cross-stream ordering: 0 = HIP events, 1 = stream memory ops on device flags
+  // (PSX_SIDE_SYNC=value), 2 = none on the main stream (measurement only)
+  int side_sync_ = 0;
+  unsigned* sflags_ = nullptr;  // [0] last round done (main), [1] last evaluation done (side)
+  int64_t eval_round_[2] = {-1, -1};
   Pending pend_;
   int last_par_ = 0;  // parity of the last round run
   int64_t inject_round_ = -1;

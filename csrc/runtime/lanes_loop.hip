@@ -5,6 +5,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <string>
 #include <thread>
 
 #include "../kernels/common.h"
@@ -136,6 +137,9 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   const size_t o_claim = take(32 * sizeof(unsigned));
   const size_t o_dsum = take((size_t)P_ * 4);
   const size_t o_uhi = take((size_t)16 * FP * 2), o_ulo = take((size_t)16 * FP * 2), o_ub = take(16 * 4);
+  const size_t o_acc2 = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
+  const size_t o_tic2 = take(8 * sizeof(unsigned));
+  const size_t o_sfl = take(8 * sizeof(unsigned));
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
   char* b = static_cast<char*>(ws_);
@@ -195,12 +199,36 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   upd_hi_ = reinterpret_cast<uint16_t*>(b + o_uhi);
   upd_lo_ = reinterpret_cast<uint16_t*>(b + o_ulo);
   upd_b_ = reinterpret_cast<float*>(b + o_ub);
+  acc2_ = reinterpret_cast<int*>(b + o_acc2);
+  ticket2_ = reinterpret_cast<unsigned*>(b + o_tic2);
+  sflags_ = reinterpret_cast<unsigned*>(b + o_sfl);
+  if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
+    side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : 0);
+  // 8 lanes occupy every XCD: the rows go to a co-running side launch instead of
+  // riders that would wait for the solves (PSX_LANES_SIDE_EVAL=0/1 overrides)
+  const char* se = std::getenv("PSX_LANES_SIDE_EVAL");
+  side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : cfg_.L == kMaxLanes;
+  if (side_eval_) {
+    hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side eval)");
+    for (int p = 0; p < 2; ++p) {
+      hip_check(hipEventCreateWithFlags(&ev_round_[p], hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventCreateWithFlags(&ev_eval_[p], hipEventDisableTiming), "hipEventCreate");
+    }
+  }
   if (cfg_.L > 0)
     hip_check(hipMemcpy(lanes_dev_, lanes_.data(), sizeof(LaneDev) * cfg_.L, hipMemcpyHostToDevice),
               "lanes table upload");
 }
 
 LanesLoop::~LanesLoop() {
+  if (side_) {
+    (void)hipStreamSynchronize(side_);
+    (void)hipStreamDestroy(side_);
+  }
+  for (int p = 0; p < 2; ++p) {
+    if (ev_round_[p]) (void)hipEventDestroy(ev_round_[p]);
+    if (ev_eval_[p]) (void)hipEventDestroy(ev_eval_[p]);
+  }
   if (ws_) (void)hipFree(ws_);
   if (err_host_) (void)hipHostFree(err_host_);
 }
@@ -407,7 +435,20 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
     // ---- the round kernel: solves + update + riding evaluation of the last round ----
-    fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
+    if (side_eval_) {
+      // this round rewrites the fragments the evaluation of round r - 2 reads
+      if (eval_pending_[par]) {
+        if (side_sync_ == 0)
+          hip_check(hipStreamWaitEvent(stream, ev_eval_[par], 0), "wait evaluation");
+        else if (side_sync_ == 1)
+          hip_check(hipStreamWaitValue32(stream, sflags_ + 1, (uint32_t)(eval_round_[par] + 1), hipStreamWaitValueGte),
+                    "wait evaluation");
+      }
+      eval_pending_[par] = false;
+      slots.clear();
+    } else {
+      fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
+    }
     a.nride = (int)a.ev.nticket;
     a.dsX = cfg_.dsX;
     a.dsy = cfg_.dsy;
@@ -447,12 +488,37 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       hip_check(hipGetLastError(), "server update launch");
     }
     (void)KF;
-    // ---- this round's rows are evaluated by the next launch ----
+    // ---- this round's rows: evaluated by the next launch, or side launch now ----
     last_par_ = par;
     pend_.valid = cfg_.sink != 0;
     pend_.vc = r;
     pend_.par = par;
     pend_.nseen = seen;
+    if (side_eval_) {
+      EvalMulti ev;
+      fill_eval(&ev, pend_, &slots, &seqs, &kinds);
+      if (ev.nmodels > 0) {
+        ev.acc = acc2_;
+        ev.ticket = ticket2_;
+        ev.nticket = (unsigned)lanes_eval_grid();
+        if (side_sync_ == 1) {
+          hip_check(hipStreamWriteValue32(stream, sflags_, (uint32_t)(r + 1), 0), "round done");
+          hip_check(hipStreamWaitValue32(side_, sflags_, (uint32_t)(r + 1), hipStreamWaitValueGte), "side waits");
+        } else {
+          hip_check(hipEventRecord(ev_round_[par], stream), "record round");
+          hip_check(hipStreamWaitEvent(side_, ev_round_[par], 0), "side waits round");
+        }
+        launch_lanes_eval(cfg_.scfg, ev, side_);
+        hip_check(hipGetLastError(), "side evaluation launch");
+        if (side_sync_ == 1)
+          hip_check(hipStreamWriteValue32(side_, sflags_ + 1, (uint32_t)(r + 1), 0), "evaluation done");
+        hip_check(hipEventRecord(ev_eval_[par], side_), "record evaluation");
+        eval_pending_[par] = true;
+        eval_round_[par] = r;
+        submit_rows(pend_, slots, seqs, kinds);
+      }
+      pend_.valid = false;
+    }
     if (cfg_.tracker && is_server) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
     check_errors(r);
   }
@@ -462,6 +528,11 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
 }
 
 void LanesLoop::flush(hipStream_t stream) {
+  for (int p = 0; p < 2; ++p)  // side evaluations: ordered before the stream's later work
+    if (eval_pending_[p]) {
+      hip_check(hipStreamWaitEvent(stream, ev_eval_[p], 0), "wait evaluation");
+      eval_pending_[p] = false;
+    }
   if (!pend_.valid || !cfg_.sink) return;
   std::vector<int> slots, kinds;
   std::vector<uint64_t> seqs;

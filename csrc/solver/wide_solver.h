@@ -30,7 +30,8 @@ struct WideBuffers {
   float* delta_dense = nullptr;   // [F*KP + KP] out (cfg.dense_delta)
   int32_t* uniq = nullptr;        // [min(F, cap*NZ)] out: local id -> feature
   // pull mode (cfg.pulled): the caller fills w_pull [umax][KP] (old weights of
-  // local id i) and w_pull_b [KP] between plan() and finish(); w_old is unused
+  // local id i) and w_pull_b [KP] between plan() and finish(); w_old is unused.
+  // Without pull mode a given w_pull_b holds the intercepts (w_old's are not read).
   const float* w_pull = nullptr;
   const float* w_pull_b = nullptr;
 };
@@ -65,6 +66,7 @@ class WideSolver {
   std::vector<long long> read_stamps(hipStream_t stream);
   size_t workspace_bytes() const { return ws_bytes_; }
   int kernels_per_solve() const {
+    if (cfg_.persist) return 1;
     const int nf = cfg_.sc.mode == 1 ? cfg_.sc.nslots : std::min(cfg_.sc.nslots, 1 + cfg_.sc.iters);
     return 5 + 3 * nf + (cfg_.sc.nslots > nf ? 1 : 0) + 1;
   }

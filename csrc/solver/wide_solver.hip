@@ -40,7 +40,8 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
     off = align256(off + bytes);
     return o;
   };
-  const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16), o_gbar = take(8);
+  const size_t o_prm = take(sizeof(WideParams)), o_ctrl = take(sizeof(Ctrl)), o_cnt = take(16), o_gbar = take(8),
+               o_pbar = take(8);
   unsigned HT = 1;
   while (HT < 2 * (unsigned)umax) HT <<= 1;
   const size_t o_tab = take((size_t)HT * 8), o_hslot = take(umax * 4), o_alt = take(umax * 4),
@@ -80,6 +81,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   dv_.ctrl = reinterpret_cast<Ctrl*>(b + o_ctrl);
   dv_.cnt = reinterpret_cast<unsigned*>(b + o_cnt);
   dv_.gbar = reinterpret_cast<unsigned long long*>(b + o_gbar);
+  dv_.pbar = reinterpret_cast<unsigned*>(b + o_pbar);
   dv_.htab = reinterpret_cast<int2*>(b + o_tab);
   dv_.hmask = HT - 1;
   dv_.hslot = reinterpret_cast<int32_t*>(b + o_hslot);
@@ -118,6 +120,7 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
 
   wide_prepare_kernels();  // before any capture
   hip_check(hipStreamCreateWithFlags(&cap_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  if (cfg_.persist) use_graph_ = false;  // one launch per phase: nothing to replay
   if (use_graph_) {
     hip_check(hipStreamBeginCapture(cap_stream_, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     enqueue_plan(cap_stream_, 1, 0);
@@ -194,7 +197,12 @@ void WideSolver::check_window(int B, int start) const {
 void WideSolver::run(int B, int start, hipStream_t stream) {
   if (cfg_.pulled) throw std::logic_error("pull mode: plan() + finish()");
   check_window(B, start);
-  if (use_graph_) {
+  if (cfg_.persist) {
+    if (cfg_.dense_delta)
+      hip_check(hipMemsetAsync(dv_.delta_dense, 0, (size_t)(cfg_.F * cfg_.KP + cfg_.KP) * 4, stream), "memset delta");
+    wide_launch_persist(cfg_, dv_, B, start, 3, stream);
+    hip_check(hipGetLastError(), "wide persistent solve launch");
+  } else if (use_graph_) {
     begin_args_.B = B;
     begin_args_.start = start;
     hip_check(hipGraphExecKernelNodeSetParams(exec_, begin_node_, &begin_params_), "hipGraphExecKernelNodeSetParams");
@@ -220,7 +228,10 @@ void WideSolver::plan(int B, int start, hipStream_t stream) {
 
 void WideSolver::finish(hipStream_t stream) {
   if (!cfg_.pulled) throw std::logic_error("finish() is the pull mode's second phase");
-  if (use_graph_)
+  if (cfg_.persist) {
+    wide_launch_persist(cfg_, dv_, 0, 0, 2, stream);
+    hip_check(hipGetLastError(), "wide persistent solve launch");
+  } else if (use_graph_)
     hip_check(hipGraphLaunch(exec2_, stream), "hipGraphLaunch");
   else
     enqueue_rest(stream);

@@ -46,6 +46,7 @@ class PSConfig:
     # producer rates a fast worker otherwise re-fits an almost unchanged window
     # many times over, which over-fits it (evaluation/README.md)
     iter_new_frac: float = 0.0
+    iter_new_cap: int = 128  # ... but never more than this many new tuples per iteration (0: no cap)
     # buffer
     min_buffer_size: int = 128
     max_buffer_size: int = 1024
@@ -107,5 +108,18 @@ def cadence_free(c: "PSConfig") -> bool:
         return True
     if c.stream_mode != "per_iter" or c.rows_per_iter <= 0:
         return False
-    return c.rows_per_iter >= max(c.iter_new_rows, math.ceil(c.iter_new_frac * c.max_buffer_size))
+    return c.rows_per_iter >= new_tuples_needed(c, c.max_buffer_size)
+
+
+def new_tuples_needed(c: "PSConfig", window: int) -> int:
+    """New tuples a worker with a `window`-row buffer waits for before its next
+    local solve: iter_new_rows, or the iter_new_frac share of the window capped at
+    iter_new_cap (a large window at a high rate would otherwise wait for hundreds
+    of tuples between updates)."""
+    import math
+
+    k = math.ceil(c.iter_new_frac * int(window))
+    if c.iter_new_cap > 0:
+        k = min(k, c.iter_new_cap)
+    return max(c.iter_new_rows, k)
 

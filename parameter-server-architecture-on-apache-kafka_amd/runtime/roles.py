@@ -26,7 +26,7 @@ from ..models.wide import WideSpec
 from ..ops.lr import EvalScratch, EvalSet, Fragments, LocalSolveOp, is_gpu, server_apply, stream_handle
 from ..ops.sparse import SparseRing, WideEvalSet, WideSolveOp, nz_capacity, wide_server_apply
 from .buffer import DeviceRing, StreamSource
-from .config import PSConfig
+from .config import PSConfig, new_tuples_needed
 from .faults import WorkerFailure
 
 
@@ -124,7 +124,7 @@ class WorkerRole:
         window only re-fits the same rows)."""
         if self.window.size <= 0:
             return False
-        K = max(self.cfg.iter_new_rows, math.ceil(self.cfg.iter_new_frac * int(self.window.size)))
+        K = new_tuples_needed(self.cfg, int(self.window.size))
         return K <= 0 or self.tuples_seen - self._seen_at_solve >= K or self.source.exhausted
 
     def compute(self, log=None) -> torch.Tensor:

@@ -112,6 +112,29 @@ def test_line_search_retries_run_in_tail(cuda, seed, iters, persist):
     assert (spec.coef(delta) - ref.delta_coef).abs().max().item() / scale < 2e-2
 
 
+def test_persistent_consecutive_solves_with_many_slots(cuda):
+    """nslots = 37 (> 32) with forced line-search retries, two solves in a row on
+    one op: the second equals the same solve on a fresh op bitwise (the barrier
+    words and the all-gather tags of consecutive solves never alias)."""
+    spec = ModelSpec(1024, 6)
+    ds = synth_finefood(512, 1024, seed=5)
+    g = torch.Generator().manual_seed(105)
+    w1 = (torch.randn(spec.P, generator=g) * 8.0).to(cuda)
+    w2 = (torch.randn(spec.P, generator=g) * 8.0).to(cuda)
+    opts = SolverOptions(iters=6, ls_max=6, persist=True)
+    assert opts.nslots > 32
+    ring = _ring_with(ds, 1024, 37, 512, cuda)
+    op = LocalSolveOp(spec, 1024, cuda, opts)
+    op.run(ring, 512, 37, w1)
+    op.run(ring, 512, 37, w2)
+    fresh = LocalSolveOp(spec, 1024, cuda, opts)
+    fresh.run(ring, 512, 37, w2)
+    torch.cuda.synchronize()
+    assert bool(op._native.persistent)
+    assert op.stats.cpu().tolist()[0] > op.stats.cpu().tolist()[1] + 1  # retries happened
+    assert torch.equal(op.delta, fresh.delta) and op.loss.item() == fresh.loss.item()
+
+
 def test_graph_and_eager_agree(cuda):
     spec = ModelSpec(1024, 6)
     ds = synth_finefood(512, seed=5)

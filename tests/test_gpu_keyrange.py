@@ -84,6 +84,60 @@ def test_pulled_solve_equals_dense_solve(cuda, own_W):
     assert abs(b["loss"].item() - dense.loss.item()) <= 1e-5 * abs(dense.loss.item())
 
 
+def _wide_solver(spec, ring, dev, persist, pulled=0):
+    h = _native.hip()
+    o = SolverOptions()
+    c = h.WideCfg()
+    c.K, c.KP, c.F, c.cap, c.NZ = spec.K, spec.KP, spec.F, ring.cap, ring.NZ
+    c.iters, c.hist, c.ls_max, c.nslots, c.mode, c.gd_lr, c.tol = o.iters, o.hist, o.ls_max, o.nslots, 0, o.gd_lr, o.tol
+    c.standardize, c.center, c.zero_const = int(o.standardize), int(o.center), int(o.zero_const)
+    c.persist = int(persist)
+    umax = min(spec.F, ring.cap * ring.NZ)
+    pl = spec.KP + umax * spec.KP
+    bufs = dict(dloc=torch.zeros(pl, device=dev), wloc=torch.zeros(pl, device=dev),
+                loss=torch.zeros(1, device=dev), stats=torch.zeros(8, dtype=torch.int32, device=dev),
+                uniq=torch.zeros(umax, dtype=torch.int32, device=dev))
+    return bufs, c
+
+
+@pytest.mark.parametrize("K", [1, 6])
+def test_persistent_wide_solve_equals_chain(cuda, K):
+    """The one-launch persistent wide solve (grid barriers between the phases)
+    == the launch chain, over consecutive solves on different windows."""
+    F = 300_000
+    spec = WideSpec(F, K)
+    labels = "binary" if K == 1 else "finefood"
+    ds = synth_sparse(1200, num_features=F, labels=labels, nnz_mean=24, max_nnz=48, seed=3, vocab=50000,
+                      class_vocab=400, signal=0.3)
+    w = spec.init("random", seed=5, scale=0.2, device=cuda)
+    ring = SparseRing(1024, nz_capacity(ds.max_nnz), cuda)
+    ring.ingest_from(ds.to(cuda), 0, 1, 1024, 0)
+    h = _native.hip()
+    outs = []
+    for persist in (False, True):
+        bufs, c = _wide_solver(spec, ring, cuda, persist)
+        s = h.WideSolver(c, ring.idx.data_ptr(), ring.val.data_ptr(), ring.nnz.data_ptr(), ring.y.data_ptr(),
+                         w.data_ptr(), bufs["dloc"].data_ptr(), bufs["wloc"].data_ptr(), bufs["loss"].data_ptr(),
+                         bufs["stats"].data_ptr(), bufs["uniq"].data_ptr(), 0, True)
+        assert s.kernels_per_solve == 1 if persist else s.kernels_per_solve > 5
+        res = []
+        for B, start in ((1000, 5), (700, 300), (1024, 0)):
+            s.run(B, start, stream_handle(cuda))
+            torch.cuda.synchronize()
+            U = s.ucount_host
+            dense = torch.zeros(spec.P, device=cuda)
+            dense.view(-1)[spec.F * spec.KP:] = bufs["dloc"][:spec.KP]
+            dense[: spec.F * spec.KP].view(spec.F, spec.KP)[bufs["uniq"][:U].long()] = \
+                bufs["dloc"][spec.KP: spec.KP + U * spec.KP].view(U, spec.KP)
+            res.append((dense, bufs["loss"].item(), bufs["stats"][:4].tolist(), int(bufs["stats"][4].item())))
+        outs.append(res)
+    for (da, la, sa, ea), (db, lb, sb, eb) in zip(*outs):
+        assert ea == 0 and eb == 0 and sa == sb
+        scale = da.abs().max().item()
+        assert (da - db).abs().max().item() <= 1e-4 * scale + 1e-7
+        assert abs(la - lb) <= 1e-5 * abs(la)
+
+
 def _replicated_gpu(spec, train, cfg, rounds, dev):
     """Oracle: one worker, the whole vector, dense-mode solves, w += lr * delta."""
     ring = SparseRing(cfg.max_buffer_size, nz_capacity(train.max_nnz), dev)

@@ -205,3 +205,30 @@ def test_lanes_ring_rows_across_epoch_wrap(cuda):
             X, y = rings[k]
             assert torch.equal(X.cpu(), train.X[rows.to(cuda)].cpu()), (rnd, k)
             assert torch.equal(y.cpu(), train.y[rows.to(cuda)].cpu()), (rnd, k)
+
+
+@pytest.mark.parametrize("L", [2, 8])
+def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L):
+    """The co-running side-stream evaluation (the default at 8 lanes) logs the same
+    rows as the in-launch riders: every worker's local model and the global model,
+    identical confusion counts."""
+    spec, train, ev = _data(cuda)
+    books = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("PSX_LANES_SIDE_EVAL", side)
+        w = spec.init("random", seed=6, device=cuda)
+        log = LogSink(spec.K, cuda)
+        lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log)
+        assert lp.side_eval == (side == "1")
+        lp.run(4, 0, stream_handle(cuda))
+        lp.flush(stream_handle(cuda))
+        torch.cuda.synchronize()
+        books.append(log.book)
+        log.close()
+    a, b = books
+    assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 4
+    assert sorted(r[1:] for r in a.worker) == sorted(r[1:] for r in b.worker) and len(a.worker) == 4 * L
+    monkeypatch.delenv("PSX_LANES_SIDE_EVAL")
+    w = spec.init("random", seed=6, device=cuda)
+    lp8, keep8 = _loop(spec, list(range(8)), 8, train, ev, w, cuda)
+    assert lp8.side_eval  # the default at 8 lanes

@@ -54,19 +54,27 @@ def ensure_data(out_dir: str):
 
 
 def launch(a, tr, te):
+    """The selected runs as independent processes, at most a.max_concurrent at a time."""
+    todo = [r for r in RUNS if not a.runs or r[0] in a.runs.split(",")]
     procs = []
-    for name, _, n, p, c in RUNS:
+
+    def start(name, n, p, c):
         d = os.path.join(a.out, name)
         os.makedirs(d, exist_ok=True)
         env = dict(os.environ, OMP_NUM_THREADS=str(a.threads), PYTHONPATH=ROOT)
         cmd = [sys.executable, "-m", "psx.apps.server_app_runner", "--inprocess", "--device", a.device,
                "-training", tr, "-test", te, "-p", str(p), "-c", str(c), "--num_workers", str(n), "-l",
                "--log_dir", d, "--max_wallclock_s", str(a.seconds), "--async_scheduler", "threads",
-               "--iter_new_rows", str(a.iter_new_rows), "--iter_new_frac", str(a.iter_new_frac)]
+               "--iter_new_rows", str(a.iter_new_rows), "--iter_new_frac", str(a.iter_new_frac),
+               "--iter_new_cap", str(a.iter_new_cap)]
         procs.append((name, subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(os.path.join(d, "run.out"), "w"),
                                              stderr=subprocess.STDOUT)))
+
     t0 = time.time()
-    while any(p.poll() is None for _, p in procs):
+    while todo or any(p.poll() is None for _, p in procs):
+        while todo and sum(p.poll() is None for _, p in procs) < a.max_concurrent:
+            name, _, n, p, c = todo.pop(0)
+            start(name, n, p, c)
         time.sleep(15)
         print(f"[matrix] {time.time() - t0:.0f} s, running: {[n for n, p in procs if p.poll() is None]}", flush=True)
     return {n: p.returncode for n, p in procs}
@@ -132,6 +140,10 @@ def main():
     ap.add_argument("--iter_new_frac", type=float, default=0.5,
                     help="worker cadence: iterate once this fraction of the window is new (the CLI default 0.5; "
                          "0: continuously)")
+    ap.add_argument("--iter_new_cap", type=int, default=128, help="cap of the new tuples per iteration (CLI default)")
+    ap.add_argument("--runs", default="", help="comma-separated run names (default: all 8)")
+    ap.add_argument("--max-concurrent", dest="max_concurrent", type=int, default=8,
+                    help="engines running at once (on one GPU every one is a process of its own)")
     ap.add_argument("--iter_new_rows", type=int, default=0,
                     help="worker cadence: iterate after this many new tuples (0: continuously, the reference's way)")
     a = ap.parse_args()

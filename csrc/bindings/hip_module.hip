@@ -722,16 +722,23 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.api = U("api");
              c.server_rank = (int)I("server_rank", 0);
              c.allreduce = I("allreduce", 0) != 0;
+             c.new_rows = (int)I("new_rows", 0);
+             c.new_frac = D("new_frac", 0.0);
+             c.new_cap = (int)I("new_cap", 0);
              return std::make_unique<LanesLoop>(c, comm);
            }),
            py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
       .def(
           "run",
-          [](LanesLoop& l, int64_t rounds, int64_t r0, uintptr_t stream, double max_wait_s) {
+          [](LanesLoop& l, int64_t rounds, int64_t r0, uintptr_t stream, double max_wait_s, double deadline_ms) {
             py::gil_scoped_release nogil;
-            return l.run(rounds, r0, S(stream), max_wait_s);
+            return l.run(rounds, r0, S(stream), max_wait_s, deadline_ms);
           },
-          py::arg("rounds"), py::arg("r0"), py::arg("stream"), py::arg("max_wait_s") = 600.0)
+          py::arg("rounds"), py::arg("r0"), py::arg("stream"), py::arg("max_wait_s") = 600.0,
+          py::arg("deadline_ms") = 0.0)
+      .def("seen_at_solve", &LanesLoop::seen_at_solve)
+      .def("set_seen_at_solve", &LanesLoop::set_seen_at_solve)
+      .def("new_tuples_needed", &LanesLoop::new_tuples_needed)
       .def("flush", [](LanesLoop& l, uintptr_t stream) { l.flush(S(stream)); })
       .def("set_sink", &LanesLoop::set_sink)
       .def("set_lr", &LanesLoop::set_lr)

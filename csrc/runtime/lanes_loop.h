@@ -73,6 +73,13 @@ struct LanesLoopCfg {
   // the weights (the PS push / pull); true = all-reduce of the lane sums, every rank
   // applies the same update to its replica (one collective per round)
   bool allreduce = false;
+  // stream-driven cadence (the CLI's --iter_new_rows / --iter_new_frac / --iter_new_cap,
+  // psx/runtime/config.py:new_tuples_needed): a round starts once every lane saw at
+  // least max(new_rows, min(ceil(new_frac * window), new_cap)) new tuples since its
+  // last solve (or its stream ended); 0 / 0.0: every round solves at once
+  int new_rows = 0;
+  double new_frac = 0.0;
+  int new_cap = 0;
 };
 
 class LanesLoop {
@@ -85,14 +92,21 @@ class LanesLoop {
   LanesLoop& operator=(const LanesLoop&) = delete;
   // Run `rounds` rounds from round r0; returns the rounds run (fewer when every
   // lane's stream is exhausted and its window empty).  max_wait_s: how long a
-  // round may wait for a lane's first rows.
-  int64_t run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s = 600.0);
+  // round may wait for a lane's first rows.  deadline_ms > 0 (epoch ms): a round
+  // still waiting for rows or for the cadence at that time is not run (the call
+  // returns the rounds run so far) -- the wall-clock stop of a producer-clock run.
+  int64_t run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
   // Evaluate the last round's rows (one launch of riders only).
   void flush(hipStream_t stream);
   void set_sink(uintptr_t sink) { cfg_.sink = sink; }
   void set_lr(float lr) { cfg_.lr = lr; }
   int64_t next_local(int lane) const { return next_local_.at(lane); }
   void set_next_local(int lane, int64_t v) { next_local_.at(lane) = v; }
+  // tuples seen by lane `lane` when its last solve started (the cadence's origin)
+  int64_t seen_at_solve(int lane) const { return seen_at_solve_.at(lane); }
+  void set_seen_at_solve(int lane, int64_t v) { seen_at_solve_.at(lane) = v; }
+  // new tuples lane windows of `size` rows wait for (0: no cadence)
+  int64_t new_tuples_needed(int64_t size) const;
   bool exhausted(int lane) const { return next_local_[lane] >= local_total_[lane] * cfg_.epochs; }
   bool all_exhausted() const;
   int hand_off_scope() const { return S_; }  // 2: one-XCD hand-offs, 1: sc1 (placement check failed)
@@ -133,6 +147,8 @@ class LanesLoop {
   const HostApi& api() const { return *api_; }
   void check(int64_t rc, const char* what) const;
   int64_t poll(int lane, double now_ms, LaneRound* r, hipStream_t stream);
+  // the rows staged for the round kernel in `r`: into the lane's ring by ring-ingest launches
+  void flush_ingest(int lane, LaneRound* r, hipStream_t stream);
   void fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slots, std::vector<uint64_t>* seqs,
                  std::vector<int>* kinds);
   void submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
@@ -145,7 +161,7 @@ class LanesLoop {
   const HostApi* api_;
   int S_ = 2;
   int P_ = 0;
-  std::vector<int64_t> local_total_, next_local_;
+  std::vector<int64_t> local_total_, next_local_, seen_at_solve_;
   std::vector<double> times_;
   void* ws_ = nullptr;  // device workspace of every lane + shared buffers
   LaneDev* lanes_dev_ = nullptr;

@@ -2,6 +2,7 @@
 #include "lanes_loop.h"
 
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -65,6 +66,8 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   if (cfg_.per_iter_rows <= 0 && !(cfg_.p_ms > 0.0) && cfg_.L > 0)
     throw std::invalid_argument("LanesLoop: need rows per round or a producer period");
   if (!cfg_.w) throw std::invalid_argument("LanesLoop: no server weights");
+  if (cfg_.new_rows < 0 || cfg_.new_frac < 0.0 || cfg_.new_cap < 0)
+    throw std::invalid_argument("LanesLoop: negative cadence");
   const bool evaluates = cfg_.sink && (cfg_.log_server || cfg_.log_workers);
   if (evaluates && (!cfg_.Xt || !cfg_.yt || cfg_.T <= 0)) throw std::invalid_argument("LanesLoop: no test set");
   if (cfg_.log_server && evaluates && (!cfg_.shi[0] || !cfg_.shi[1] || !cfg_.slo[0] || !cfg_.slo[1] || !cfg_.sb[0] ||
@@ -81,6 +84,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
     if (tot == 0) throw std::invalid_argument("LanesLoop: worker " + std::to_string(k) + " has no rows");
     local_total_.push_back(tot);
     next_local_.push_back(0);
+    seen_at_solve_.push_back(0);
   }
   prepare_kernels();
   // the lanes claim their XCD at run time (LanesArgs::claim), so placement needs no
@@ -271,17 +275,7 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
   const int64_t cap = cfg_.scfg.cap;
   // rows already pending for the kernel from an earlier delivery of this round: into
   // the ring now (the kernel carries at most the last two contiguous runs)
-  auto flush_pending = [&]() {
-    if (r->n > 0)
-      launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
-                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
-    if (r->n2 > 0)
-      launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first2, r->step, r->n2, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
-                         nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), (r->dst + r->n) % cap, cap, cfg_.scfg.Fp,
-                         stream);
-    r->n = r->n2 = 0;
-  };
-  flush_pending();
+  flush_ingest(lane, r, stream);
   const int64_t keep = n < cap ? n : cap, skip = n - keep;
   int64_t slot = (first + skip) % cap, pos = nl + skip, remaining = keep;
   while (remaining > 0) {  // split at the shard's epoch boundaries
@@ -311,6 +305,18 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
   }
   nl += n;
   return n;
+}
+
+void LanesLoop::flush_ingest(int lane, LaneRound* r, hipStream_t stream) {
+  const int64_t cap = cfg_.scfg.cap;
+  if (r->n > 0)
+    launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]), nullptr,
+                       reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
+  if (r->n2 > 0)
+    launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first2, r->step, r->n2, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
+                       nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), (r->dst + r->n) % cap, cap, cfg_.scfg.Fp,
+                       stream);
+  r->n = r->n2 = 0;
 }
 
 int LanesLoop::rider_count(int nmodels, int L) const {
@@ -394,7 +400,14 @@ void LanesLoop::check_errors(int64_t round) {
   }
 }
 
-int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s) {
+int64_t LanesLoop::new_tuples_needed(int64_t size) const {
+  int64_t k = (int64_t)std::ceil(cfg_.new_frac * (double)size);  // as math.ceil in config.py
+  if (k < 0) k = 0;
+  if (cfg_.new_cap > 0 && k > cfg_.new_cap) k = cfg_.new_cap;
+  return k > cfg_.new_rows ? k : cfg_.new_rows;
+}
+
+int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s, double deadline_ms) {
   const int64_t t_begin = steady_ns();
   const int L = cfg_.L;
   const int KF = cfg_.scfg.K * cfg_.scfg.Fp;
@@ -409,31 +422,41 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     std::memset(&a, 0, sizeof(a));
     a.L = L;
     a.par = par;
-    // ---- deliveries, then every lane's window (BSP: wait until all have rows) ----
+    // ---- deliveries, then every lane's window (BSP: wait until all have rows, and
+    // with a cadence until all saw enough new tuples, WorkerTrainingProcessor.java:63-98
+    // runs on every new tuple; psx/runtime/roles.py:WorkerRole.ready) ----
     std::vector<int64_t> seen(L, 0);
     const double wait0 = epoch_ms();
     for (;;) {
       const double now = epoch_ms() - cfg_.t0_ms;
       for (int l = 0; l < L; ++l) poll(l, now, &a.r[l], stream);
-      bool ready = true;
+      bool ready = true, rows = true;
       for (int l = 0; l < L; ++l) {
         int64_t size = 0, start = 0, sn = 0;
         check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
         a.r[l].B = (int)size;
         a.r[l].start = (int)start;
         seen[l] = sn;
-        ready &= size > 0;
+        rows &= size > 0;
+        const int64_t need = new_tuples_needed(size);
+        ready &= size > 0 && (need <= 0 || sn - seen_at_solve_[l] >= need || exhausted(l));
       }
       if (ready) break;
+      bool end = false;
       for (int l = 0; l < L; ++l)  // a lane with an empty window and nothing left to come: the run ends
-        if (a.r[l].B <= 0 && exhausted(l)) {
-          rounds_run_ += done;
-          host_ns_ += (double)(steady_ns() - t_begin);
-          return done;
-        }
-      if (epoch_ms() - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
+        end |= a.r[l].B <= 0 && exhausted(l);
+      if (deadline_ms > 0.0 && epoch_ms() >= deadline_ms) end = true;
+      if (end) {
+        for (int l = 0; l < L; ++l)  // rows delivered meanwhile: into the ring now
+          if (a.r[l].n > 0 || a.r[l].n2 > 0) flush_ingest(l, &a.r[l], stream);
+        rounds_run_ += done;
+        host_ns_ += (double)(steady_ns() - t_begin);
+        return done;
+      }
+      if (!rows && epoch_ms() - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
       std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
+    for (int l = 0; l < L; ++l) seen_at_solve_[l] = seen[l];
     // ---- the round kernel: solves + update + riding evaluation of the last round ----
     if (side_eval_) {
       // this round rewrites the fragments the evaluation of round r - 2 reads

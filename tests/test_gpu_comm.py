@@ -191,3 +191,45 @@ def test_local_lanes_unbounded_run_stops_when_data_is_exhausted(cuda):
     out = eng.run()
     assert out.get("lanes") == 2 and out["rounds"] >= 16
     assert all(w.source.exhausted for w in eng.workers)
+
+
+def test_lanes_loop_dedicated_server_rank_world1(cuda, pg):
+    """The dedicated server rank's body of the lanes loop (no lanes: a zero
+    contribution reduced to itself, the update, the broadcast of the weights, the
+    global model's evaluation rows) through the native RCCL communicator."""
+    from psx import _native
+    from psx.models.logreg import ModelSpec
+    from psx.ops.lr import EvalSet, Fragments, SolverOptions, stream_handle
+    from psx.parallel.comm import make_comm
+    from psx.utils.data import synth_finefood
+    from psx.utils.logsink import LogSink
+
+    comm = make_comm(0, 1, cuda)
+    h, host = _native.hip(), _native.host
+    spec = ModelSpec(1024, 6)
+    te = synth_finefood(1000, seed=1)
+    ev = EvalSet(spec, te.X, te.y, cuda)
+    o = SolverOptions()
+    sc = h.SolverCfg()
+    sc.K, sc.F, sc.Fp, sc.P, sc.cap = spec.K, spec.F, spec.Fp, spec.P, 1024
+    sc.iters, sc.hist, sc.ls_max, sc.mode = o.iters, o.hist, o.ls_max, 0
+    sc.center, sc.zero_const, sc.nslots, sc.gd_lr, sc.tol = 1, 1, o.nslots, o.gd_lr, o.tol
+    w = spec.init("random", seed=2, device=cuda)
+    w0 = w.clone()
+    frags = [Fragments(spec, cuda), Fragments(spec, cuda)]
+    sink = LogSink(spec.eval_classes, cuda)
+    d = dict(scfg=sc, N=4, p_ms=1.0, k=[], w=w.data_ptr(), lr=0.25, api=host.capi(), server_rank=0,
+             shi=[f.hi.data_ptr() for f in frags], slo=[f.lo.data_ptr() for f in frags],
+             sb=[f.b.data_ptr() for f in frags], Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T,
+             sink=sink.native.handle, log_server=1, log_workers=0)
+    lp = h.LanesLoop(d, comm.c)
+    assert lp.run(5, 0, stream_handle(cuda)) == 5
+    lp.flush(stream_handle(cuda))
+    torch.cuda.synchronize()
+    sink.drain(block=True)
+    assert torch.equal(w, w0)  # nothing pushed: w += lr * 0
+    assert [r[1] for r in sink.book.server] == list(range(5)) and not sink.book.worker
+    f1 = [r[2] for r in sink.book.server]
+    assert max(f1) - min(f1) < 1e-9 and f1[0] > 0  # the same (unchanged) global model every round
+    del lp
+    comm.close()

@@ -232,3 +232,56 @@ def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L):
     w = spec.init("random", seed=6, device=cuda)
     lp8, keep8 = _loop(spec, list(range(8)), 8, train, ev, w, cuda)
     assert lp8.side_eval  # the default at 8 lanes
+
+
+def test_lanes_cadence_waits_for_new_tuples(cuda):
+    """--iter_new_rows in the native loop: a round starts only once every lane saw
+    the required new tuples since its last solve (per-round deliveries of 16 rows:
+    3 deliveries per round for 48 new tuples)."""
+    spec, train, ev = _data(cuda)
+    w = spec.init("random", seed=3, device=cuda)
+    lp, keep = _loop(spec, [0, 1], 2, train, ev, w, cuda, rows=16, new_rows=48)
+    assert lp.new_tuples_needed(1024) == 48
+    assert lp.run(4, 0, stream_handle(cuda)) == 4
+    for l in range(2):
+        assert lp.next_local(l) == 4 * 48 and lp.seen_at_solve(l) == 4 * 48
+    torch.cuda.synchronize()
+
+
+def test_lanes_cadence_fraction_and_cap(cuda):
+    """iter_new_frac share of the window, capped at iter_new_cap (config.new_tuples_needed)."""
+    from psx.runtime.config import new_tuples_needed
+
+    spec, train, ev = _data(cuda)
+    w = spec.init("zeros", device=cuda)
+    lp, keep = _loop(spec, [0], 1, train, ev, w, cuda, rows=16, new_frac=0.3, new_cap=100)
+    c = PSConfig(iter_new_frac=0.3, iter_new_cap=100)
+    for size in (1, 10, 16, 300, 333, 1024):
+        assert lp.new_tuples_needed(size) == new_tuples_needed(c, size), size
+
+
+def test_lanes_engine_producer_clock_cadence_and_deadline(cuda):
+    """The reference's producer clock (-p) with the fresh-window cadence runs on the
+    lanes loop: every worker row is >= the cadence's new tuples after the previous
+    one, and the wall-clock stop ends a round that waits for tuples."""
+    import time
+
+    from psx.runtime.config import new_tuples_needed
+
+    train, test = synth_finefood(40000, seed=0), synth_finefood(2000, seed=1)
+    cfg = PSConfig(num_workers=4, consistency_model=0, producer_time_per_event=2.0, max_wallclock_s=3.0,
+                   iter_new_frac=0.5, iter_new_cap=128, min_buffer_size=128, max_buffer_size=1024)
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    t0 = time.time()
+    out = eng.run()
+    took = time.time() - t0
+    assert out.get("lanes") == 4, out
+    assert out["rounds"] >= 3, out
+    assert took < 3.0 + 1.5, took
+    book = eng.log.book
+    rows = {k: [r for r in book.worker if r[1] == k] for k in range(4)}
+    for k, rs in rows.items():
+        assert len(rs) == out["rounds"], (k, len(rs))
+        seen = [r[-1] for r in rs]
+        for a, b in zip(seen, seen[1:]):
+            assert b - a >= min(new_tuples_needed(cfg, 128), 64), (k, seen)

@@ -56,9 +56,11 @@ WideSolver::WideSolver(const WideCfg& cfg, const WideBuffers& buf, bool use_grap
   const size_t o_x = take(PLmax * 4), o_d = take(PLmax * 4), o_gt = take(PLmax * 4), o_gc = take(PLmax * 4),
                o_w0 = take(PLmax * 4);
   const size_t o_S = take(H * PLmax * 4), o_Y = take(H * PLmax * 4);
-  // dot partials: one row per workgroup of the dots launches (nblk_dots_) AND of the
-  // persistent tail (up to 64 workgroups)
-  const int npart = nblk_dots_ > 64 ? nblk_dots_ : 64;
+  // dot partials: one row per workgroup of the dots launches (nblk_dots_), of the
+  // persistent tail (up to 64 workgroups) AND of the one-launch persistent solve
+  // (wide_persist_grid() workgroups run its dots phase)
+  int npart = nblk_dots_ > 64 ? nblk_dots_ : 64;
+  if (npart < wide_persist_grid()) npart = wide_persist_grid();
   const size_t o_part = take((size_t)npart * kWideND * 8), o_loss = take((size_t)cfg.sc.nslots * 8);
   const bool stamps = std::getenv("PSX_WIDE_STAMPS") != nullptr;
   const size_t o_dbg = stamps ? take((size_t)cfg.sc.nslots * 8 * 8) : 0;

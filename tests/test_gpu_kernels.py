@@ -125,10 +125,11 @@ def test_persistent_consecutive_solves_with_many_slots(cuda):
     assert opts.nslots > 32
     ring = _ring_with(ds, 1024, 37, 512, cuda)
     op = LocalSolveOp(spec, 1024, cuda, opts)
-    op.run(ring, 512, 37, w1)
+    # (w1 is test_line_search_retries_run_in_tail's seed-5 start: its solve retries)
     op.run(ring, 512, 37, w2)
+    op.run(ring, 512, 37, w1)
     fresh = LocalSolveOp(spec, 1024, cuda, opts)
-    fresh.run(ring, 512, 37, w2)
+    fresh.run(ring, 512, 37, w1)
     torch.cuda.synchronize()
     assert bool(op._native.persistent)
     assert op.stats.cpu().tolist()[0] > op.stats.cpu().tolist()[1] + 1  # retries happened

@@ -55,10 +55,13 @@ KeyRangeLoop::KeyRangeLoop(const KeyRangeLoopCfg& cfg, RcclComm* comm)
   c.own_W = W_;
   c.own_S = S_;
   c.dense_delta = 0;
-  // the solver is alone on the GPU: its whole solve (pull mode: its second phase)
-  // in one persistent launch (PSX_WIDE_PERSIST=0: the launch chain)
+  // the launch chain (graph replay) by default; PSX_WIDE_PERSIST=1: the whole solve
+  // (pull mode: its second phase) in one persistent launch.  Measured on MI355X
+  // (profiles/r03_v5): sharded100m 0.163 ms per round with the chain, 0.365 ms with
+  // the persistent launch -- its 256 workgroups x 512 threads pay a grid barrier per
+  // phase (~9 per solve + 3 per slot) where the chain's small launches overlap
   const char* wp = std::getenv("PSX_WIDE_PERSIST");
-  c.persist = wp ? (wp[0] == '1' ? 1 : 0) : 1;
+  c.persist = wp ? (wp[0] == '1' ? 1 : 0) : 0;
   const int64_t E = (int64_t)c.cap * c.NZ;
   umax_ = (int)(c.F < E ? c.F : E);
 

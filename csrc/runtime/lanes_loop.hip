@@ -208,10 +208,12 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   sflags_ = reinterpret_cast<unsigned*>(b + o_sfl);
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : 0);
-  // 8 lanes occupy every XCD: the rows go to a co-running side launch instead of
-  // riders that would wait for the solves (PSX_LANES_SIDE_EVAL=0/1 overrides)
+  // PSX_LANES_SIDE_EVAL=1: the rows go to a co-running side launch instead of riders
+  // of the round kernel.  Off by default: with 8 lanes (no XCD left for riders) the
+  // two forms measured the same, 69.4k vs 69.2k updates/s (profiles/r03_v5), and
+  // the riders keep a round at one launch
   const char* se = std::getenv("PSX_LANES_SIDE_EVAL");
-  side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : cfg_.L == kMaxLanes;
+  side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : false;
   if (side_eval_) {
     hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side eval)");
     for (int p = 0; p < 2; ++p) {

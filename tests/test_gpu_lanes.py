@@ -209,7 +209,7 @@ def test_lanes_ring_rows_across_epoch_wrap(cuda):
 
 @pytest.mark.parametrize("L", [2, 8])
 def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L):
-    """The co-running side-stream evaluation (the default at 8 lanes) logs the same
+    """The co-running side-stream evaluation (PSX_LANES_SIDE_EVAL=1) logs the same
     rows as the in-launch riders: every worker's local model and the global model,
     identical confusion counts."""
     spec, train, ev = _data(cuda)
@@ -231,7 +231,7 @@ def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L):
     monkeypatch.delenv("PSX_LANES_SIDE_EVAL")
     w = spec.init("random", seed=6, device=cuda)
     lp8, keep8 = _loop(spec, list(range(8)), 8, train, ev, w, cuda)
-    assert lp8.side_eval  # the default at 8 lanes
+    assert not lp8.side_eval  # riders by default, 8 lanes too
 
 
 def test_lanes_cadence_waits_for_new_tuples(cuda):

@@ -58,6 +58,63 @@ __device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel* 
   }
 }
 
+// The last arriving workgroup publishes every model's counts into its pinned slot
+// (see eval_body.h): all M accumulator exchanges (and the losses) are issued
+// before the first system-scope store, so they cost one L2 round trip instead of M
+// dependent ones; then the drain, the ticket reset and the sequence numbers.
+__device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid) {
+  int tot[kMaxEvalModels];
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)
+    tot[m] = m < M ? __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                   : 0;
+  float lv = 0.f;
+  if (tid < M) {
+    const EvalModel E = pick(ev.m, tid);
+    lv = E.loss ? *E.loss : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)
+    if (m < M) __hip_atomic_store((int*)pick(ev.m, m).slot + tid, tot[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < M) __hip_atomic_store((float*)(pick(ev.m, tid).slot + 1024), lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < M)
+    __hip_atomic_store((unsigned long long*)(pick(ev.m, tid).slot + 1032), pick(ev.m, tid).seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A 32-row test tile held in registers (stage_tile's loads, split from its LDS
+// stores so that the next tile's loads fly while the current one is evaluated).
+template <int FP>
+struct TileRegs {
+  static constexpr int CPR = FP / 8, PER_T = 32 * CPR / 256;
+  u16x8 v[PER_T];
+  int y;
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ X, const int32_t* __restrict__ yt, int tile,
+                                       int T) {
+    const int64_t row0 = (int64_t)tile * 32;
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int q = threadIdx.x + 256 * j;
+      const int row = q / CPR, cg = q - row * CPR;
+      v[j] = row < nrows ? *(const u16x8*)(X + (row0 + row) * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    y = (int)threadIdx.x < nrows ? yt[row0 + threadIdx.x] : 0;
+  }
+  __device__ __forceinline__ void store(char* lds) const {  // stage_tile's LDS layout
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int q = threadIdx.x + 256 * j;
+      const int row = q / CPR, cg = q - row * CPR;
+      *(u16x8*)(lds + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+    }
+  }
+};
+
 template <int FP>
 __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, int rid, int nride) {
   if (ev.nmodels <= 0 || rid >= nride) return;
@@ -71,6 +128,8 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   const int i0 = rid * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
   int curp = -1;
   WFrag<FP> wf;
+  TileRegs<FP> tr;  // the next item's tile, in flight during the current item
+  if (i0 < i1) tr.load(ev.Xt, ev.yt, i0 % nT, T);
   __syncthreads();
   for (int it = i0; it < i1; ++it) {
     const int p = it / nT, tile = it - p * nT;
@@ -81,8 +140,9 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
       curp = p;
     }
     const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
-    const int ylab = tid < nrows ? ev.yt[(size_t)tile * 32 + tid] : 0;
-    stage_tile<FP>(lds, ev.Xt, (int64_t)tile * 32, nrows, 0, false);
+    tr.store(lds);
+    const int ylab = tr.y;
+    if (it + 1 < i1) tr.load(ev.Xt, ev.yt, (it + 1) % nT, T);
     __syncthreads();
     f32x4 a0, a1;
     forward_tile_pre<FP>(lds, wf, a0, a1);
@@ -128,24 +188,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
     *lastp = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ev.nticket - 1;
   __syncthreads();
   if (!*lastp) return;
-  // publication into the pinned slots (see eval_body.h): counts, loss, drain, seq
-  for (int m = 0; m < M; ++m) {
-    const EvalModel E = pick(ev.m, m);
-    const int tot = __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((int*)E.slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid == 0)
-      __hip_atomic_store((float*)(E.slot + 1024), E.loss ? *E.loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int m = 0; m < M; ++m) {
-      const EvalModel E = pick(ev.m, m);
-      __hip_atomic_store((unsigned long long*)(E.slot + 1032), E.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  publish_counts(ev, M, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -654,23 +697,7 @@ __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
     last = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  for (int m = 0; m < M; ++m) {
-    const EvalModel E = pick(ev.m, m);
-    const int tot = __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((int*)E.slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid == 0)
-      __hip_atomic_store((float*)(E.slot + 1024), E.loss ? *E.loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int m = 0; m < M; ++m) {
-      const EvalModel E = pick(ev.m, m);
-      __hip_atomic_store((unsigned long long*)(E.slot + 1032), E.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  publish_counts(ev, M, tid);
 }
 
 }  // namespace

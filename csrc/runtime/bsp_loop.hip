@@ -4,6 +4,7 @@
 #include <chrono>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "../kernels/lr_kernels.h"
 
@@ -111,7 +112,17 @@ int64_t BspLoop::run(int64_t rounds, int64_t r0, hipStream_t stream) {
     poll(now - cfg_.t0_ms, &ing, stream);
     int64_t size = 0, start = 0, seen = 0;
     check(api().window_state(win, &size, &start, &seen), "window state");
-    if (size <= 0) break;  // nothing to train on (the stream has not delivered yet / is exhausted)
+    // no rows yet: wait for the producer as the Python loop does (a poll that
+    // delivers anything makes the window non-empty, so no staged run is lost);
+    // an exhausted stream with an empty window ends the run
+    const double wait0 = epoch_ms();
+    while (size <= 0 && !exhausted()) {
+      if (epoch_ms() - wait0 > 600e3) throw std::runtime_error("BspLoop: no rows for 600 s");
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
+      poll(epoch_ms() - cfg_.t0_ms, &ing, stream);
+      check(api().window_state(win, &size, &start, &seen), "window state");
+    }
+    if (size <= 0) break;
     // ---- the previous round's rows ride in this solve ----
     EvalRide ride{};
     bool riding = false;

@@ -70,7 +70,17 @@ def phases(st):
         if not T(s, 0):
             break
         slots.append({"fwd": us(T(s, 0), T(s, 2)), "bwd": us(T(s, 2), T(s, 8)),
-                      "fwd_start_us": us(base, T(s, 0))})
+                      "fwd_start_us": us(base, T(s, 0)),
+                      # lane 0's workgroup 0: trial-point fragments + staging wait, forward MFMA,
+                      # softmax + backward tile, row sums, partials store + barrier
+                      "f.wfrag": us(T(s, 0), T(s, 9)), "f.mfma": us(T(s, 9), T(s, 10)),
+                      "f.smax+bwd": us(T(s, 10), T(s, 11)), "f.sums": us(T(s, 11), T(s, 1)),
+                      "f.gpf+barrier": us(T(s, 1), T(s, 2)),
+                      # slice owner 0: partials reduce, gradient, dots + all-gather, controller,
+                      # controller copy, apply + next trial point
+                      "b.reduce": us(T(s, 2), T(s, 3)), "b.grad": us(T(s, 3), T(s, 4)),
+                      "b.dots+gather": us(T(s, 4), T(s, 5)), "b.ctrl": us(T(s, 5), T(s, 6)),
+                      "b.copy": us(T(s, 6), T(s, 7)), "b.apply+next": us(T(s, 7), T(s, 8))})
     out["slots"] = slots
     out["slots_total"] = us(T(30, 3), T(30, 4))
     out["finalize"] = us(T(30, 4), T(30, 5))

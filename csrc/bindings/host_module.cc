@@ -74,6 +74,12 @@ PYBIND11_MODULE(_psx_host, m) {
              w.insert_many(t.data(), n, slots.mutable_data());
              return slots;
            })
+      // the round loops' form (no per-row slots: equal-stamp runs take the bulk path);
+      // returns the slot of the first row
+      .def("insert_bulk",
+           [](SlidingWindow& w, py::array_t<double, py::array::c_style | py::array::forcecast> t) {
+             return w.insert_many(t.data(), t.size(), nullptr);
+           })
       .def("restore", &SlidingWindow::restore)
       .def_property_readonly("size", &SlidingWindow::size)
       .def_property_readonly("capacity", &SlidingWindow::capacity)

@@ -6,25 +6,6 @@
 
 namespace psx {
 
-void RateEstimator::arrival(double now_ms) {
-  if (have_last_) {
-    double d = now_ms - last_ms_;
-    deltas_.push_back(d);
-    sum_ += d;
-    if (static_cast<int>(deltas_.size()) > window_) {
-      sum_ -= deltas_.front();
-      deltas_.pop_front();
-    }
-  }
-  have_last_ = true;
-  last_ms_ = now_ms;
-}
-
-double RateEstimator::mean_interarrival_ms() const {
-  if (deltas_.empty()) return 1000.0;
-  return sum_ / static_cast<double>(deltas_.size());
-}
-
 SlidingWindow::SlidingWindow(int64_t min_size, int64_t max_size, double bc, int rate_window, int64_t ring_capacity)
     : min_(min_size), max_(max_size), cap_(ring_capacity > max_size ? ring_capacity : max_size), bc_(bc),
       rate_(rate_window) {
@@ -49,23 +30,43 @@ int64_t SlidingWindow::target_size() const {
 }
 
 SlotAssignment SlidingWindow::insert(double now_ms) {
+  // A zero inter-arrival time cannot raise the mean (the estimator gains a 0 and
+  // at most loses a non-negative delta), so a target already at max stays there:
+  // the rows of one delivery (equal stamps) skip the two fp64 divisions of
+  // target_size() -- 1,024 of them per lane and round in the lanes loop.
+  const bool zero_dt = rate_.has_last() && now_ms == rate_.last_ms();
   rate_.arrival(now_ms);
-  int64_t target = target_size();
+  const int64_t target = (zero_dt && last_target_ == max_) ? max_ : target_size();
+  last_target_ = target;
   if (size_ < target)
     size_ += 1;
   else
     size_ = target;
-  head_ = (head_ + 1) % cap_;
+  head_ = head_ + 1 == cap_ ? 0 : head_ + 1;  // (no 64-bit modulo on the per-row path)
   seen_ += 1;
   return SlotAssignment{head_, seen_, size_, target};
 }
 
 int64_t SlidingWindow::insert_many(const double* now_ms, int64_t n, int64_t* slots_out) {
   int64_t first = -1;
-  for (int64_t i = 0; i < n; ++i) {
+  for (int64_t i = 0; i < n;) {
+    if (!slots_out && i > 0 && last_target_ == max_ && now_ms[i] == now_ms[i - 1]) {
+      // a run of equal stamps with the target at max (see insert()): k rows at
+      // once -- k zero deltas into the estimator, the size grows by one per row
+      int64_t j = i + 1;
+      while (j < n && now_ms[j] == now_ms[i]) ++j;
+      const int64_t k = j - i;
+      rate_.zeros(k);
+      size_ = size_ + k < max_ ? size_ + k : max_;
+      head_ = (head_ + k) % cap_;
+      seen_ += k;
+      i = j;
+      continue;
+    }
     SlotAssignment a = insert(now_ms[i]);
     if (i == 0) first = a.slot;
     if (slots_out) slots_out[i] = a.slot;
+    ++i;
   }
   return first;
 }
@@ -80,6 +81,7 @@ void SlidingWindow::restore(int64_t head, int64_t size, int64_t seen) {
   head_ = head;
   size_ = size;
   seen_ = seen;
+  last_target_ = -1;
 }
 
 }  // namespace psx

@@ -15,25 +15,67 @@
 // slots ending at head.  No per-tuple scan.
 #pragma once
 #include <cstdint>
-#include <deque>
+#include <vector>
 
 namespace psx {
 
+// The last `window` inter-arrival times in a fixed ring (no allocation per
+// arrival: a window of 1,024 new rows per round is 1,024 arrivals, on the round
+// loop's critical host path for every lane).  The running sum is updated in the
+// same order as a FIFO would (+ newest, then - evicted), so the estimate is the
+// same to the last bit.
 class RateEstimator {
  public:
-  explicit RateEstimator(int window = 500) : window_(window) {}
+  explicit RateEstimator(int window = 500) : window_(window > 0 ? window : 0), buf_(window_ + 1, 0.0) {}
   // Record an arrival at wall-clock `now_ms`.
-  void arrival(double now_ms);
+  void arrival(double now_ms) {
+    if (have_last_) {
+      const double d = now_ms - last_ms_;
+      buf_[tail_] = d;
+      tail_ = tail_ + 1 == (int)buf_.size() ? 0 : tail_ + 1;
+      sum_ += d;
+      if (++n_ > window_) {
+        sum_ -= buf_[head_];
+        head_ = head_ + 1 == (int)buf_.size() ? 0 : head_ + 1;
+        --n_;
+      }
+    }
+    have_last_ = true;
+    last_ms_ = now_ms;
+  }
+  // k arrivals at the last stamp (k zero deltas): the same state as k arrival()
+  // calls -- adding 0.0 leaves the sum unchanged (it is never -0.0), evictions are
+  // subtracted in order.
+  void zeros(int64_t k) {
+    if (!have_last_) {  // the first of them only sets the stamp
+      if (k <= 0) return;
+      have_last_ = true;
+      --k;
+    }
+    const int B = (int)buf_.size();
+    for (int64_t i = 0; i < k; ++i) {
+      buf_[tail_] = 0.0;
+      tail_ = tail_ + 1 == B ? 0 : tail_ + 1;
+      if (++n_ > window_) {
+        sum_ -= buf_[head_];
+        head_ = head_ + 1 == B ? 0 : head_ + 1;
+        --n_;
+      }
+    }
+  }
   // Mean inter-arrival time in ms (1000 when fewer than two arrivals).
-  double mean_interarrival_ms() const;
-  int samples() const { return static_cast<int>(deltas_.size()); }
+  double mean_interarrival_ms() const { return n_ == 0 ? 1000.0 : sum_ / static_cast<double>(n_); }
+  int samples() const { return n_; }
+  bool has_last() const { return have_last_; }
+  double last_ms() const { return last_ms_; }
 
  private:
   int window_;
   bool have_last_ = false;
   double last_ms_ = 0.0;
   double sum_ = 0.0;
-  std::deque<double> deltas_;
+  std::vector<double> buf_;  // ring of window_ + 1 slots: [head_, tail_) holds n_ deltas
+  int head_ = 0, tail_ = 0, n_ = 0;
 };
 
 // Result of ingesting one tuple.
@@ -77,6 +119,7 @@ class SlidingWindow {
   int64_t head_ = -1;
   int64_t size_ = 0;
   int64_t seen_ = 0;
+  int64_t last_target_ = -1;  // target of the previous insert (-1: none)
 };
 
 }  // namespace psx

@@ -364,38 +364,52 @@ __device__ __forceinline__ void lane_prep(char* lb, const SolverCfg& cfg, const 
 // The BSP update of one slice by the last lane to finish it: w += lr * (sum of
 // the lanes' deltas, lane order) and the server's evaluation fragments, or the
 // plain sum into dsum (multi-rank).  A lane whose solve reported a timed-out
-// wait (sticky error word) contributes nothing.
+// wait (sticky error word) contributes nothing.  Slice 0 also carries the
+// intercepts (each lane's workgroup 0 stored them before arriving).  Every
+// lane's error word and delta element are loaded before the first is used: one
+// round trip to the other XCDs' data, not one per lane.
 template <int FP>
 __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a,
-                                                 int wg, int NS) {
+                                                 int wg) {
   const int tid = threadIdx.x, K = cfg.K, L = a.L;
-  unsigned ok = 0;
-  for (int l = 0; l < L; ++l) ok |= (xload(lanes[l].dv.xch + kXchErr) == 0ull ? 1u : 0u) << l;
-  if (wg < NS) {
-    const int c = tid >> 5, f = wg * 32 + (tid & 31);
-    if (c < K) {
-      const size_t e = (size_t)c * FP + f;
-      float sum = 0.f;
-      for (int l = 0; l < L; ++l)
-        if (ok >> l & 1u) sum += ld_sc1(lanes[l].dv.delta + e);
-      if (a.dsum) {
-        a.dsum[e] = sum;
-      } else {
-        const float nw = a.w[e] + a.lr * sum;
-        a.w[e] = nw;
-        write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
-      }
+  const int c = tid >> 5, f = wg * 32 + (tid & 31);
+  const bool coef = c < K;
+  const bool icpt = wg == 0 && tid < K;  // (threads 0..K-1 carry one intercept each as well)
+  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
+  unsigned long long er[kMaxLanes];
+  float dl[kMaxLanes], di[kMaxLanes];
+#pragma unroll
+  for (int l = 0; l < kMaxLanes; ++l) {
+    er[l] = 0ull;
+    dl[l] = di[l] = 0.f;
+    if (l < L) {
+      er[l] = xload(lanes[l].dv.xch + kXchErr);
+      if (coef) dl[l] = ld_sc1(lanes[l].dv.delta + e);
+      if (icpt) di[l] = ld_sc1(lanes[l].dv.delta + ei);
     }
-  } else if (tid < K) {  // intercepts
-    const size_t e = (size_t)K * FP + tid;
-    float sum = 0.f;
-    for (int l = 0; l < L; ++l)
-      if (ok >> l & 1u) sum += ld_sc1(lanes[l].dv.delta + e);
+  }
+  float sum = 0.f, sumi = 0.f;
+#pragma unroll
+  for (int l = 0; l < kMaxLanes; ++l)
+    if (l < L && er[l] == 0ull) {
+      sum += dl[l];
+      sumi += di[l];
+    }
+  if (coef) {
     if (a.dsum) {
       a.dsum[e] = sum;
     } else {
       const float nw = a.w[e] + a.lr * sum;
       a.w[e] = nw;
+      write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
+    }
+  }
+  if (icpt) {
+    if (a.dsum) {
+      a.dsum[ei] = sumi;
+    } else {
+      const float nw = a.w[ei] + a.lr * sumi;
+      a.w[ei] = nw;
       a.sb[a.scoff + tid] = nw;
     }
   }
@@ -556,8 +570,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   }
   // ---- the BSP update: the last lane to finish a slice applies the sum ----
   if (wg == 0 && tid == 0) stamp(dv, 30, 5);
-  if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg, NS);
-  if (wg == 0 && lane_arrive(a.arrive, NS, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, NS, NS);
+  if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
   if (wg == 0 && tid == 0) stamp(dv, 30, 6);
 }
 

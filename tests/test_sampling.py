@@ -117,3 +117,31 @@ def test_zero_mean_interarrival_policy():
     assert w.target_size() == 1024
     java_int_cast = ((2 ** 63 - 1) + 2 ** 31) % 2 ** 32 - 2 ** 31  # (int) Long.MAX_VALUE
     assert java_int_cast == -1 and max(128, min(1024, java_int_cast)) == 128
+
+
+def test_bulk_insert_equals_row_by_row():
+    """The round loops' bulk insert (equal-stamp runs at the max target in one step)
+    leaves the window and the rate estimator exactly as row-by-row inserts do."""
+    import numpy as np
+
+    rng = np.random.default_rng(7)
+    for trial in range(20):
+        a = host.SlidingWindow(128, 1024, 0.3, 500, 1024)
+        b = host.SlidingWindow(128, 1024, 0.3, 500, 1024)
+        now = 0.0
+        for _ in range(60):
+            k = int(rng.integers(1, 1500))
+            mode = rng.integers(0, 3)
+            if mode == 0:  # a burst (one poll of per-round deliveries)
+                t = np.full(k, now)
+            elif mode == 1:  # producer clock: distinct stamps
+                t = now + np.cumsum(rng.exponential(rng.choice([0.01, 5.0, 400.0]), k))
+            else:  # mixed: runs of equal stamps
+                t = np.repeat(now + np.cumsum(rng.exponential(2.0, k // 8 + 1)), 8)[:k]
+            now = float(t[-1]) + float(rng.choice([0.0, 0.5, 50.0]))
+            a.insert_many(t)
+            first = b.insert_bulk(t)
+            assert first == (b.head - k + 1) % b.capacity or k > b.capacity
+            assert (a.size, a.head, a.tuples_seen, a.start) == (b.size, b.head, b.tuples_seen, b.start), trial
+            assert a.mean_interarrival_ms() == b.mean_interarrival_ms(), trial
+            assert a.target_size() == b.target_size()

@@ -549,7 +549,7 @@ class DistEngine:
             return False
         if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
             return False
-        if c.checkpoint_dir or not cadence_free(c):
+        if c.checkpoint_dir:
             return False
         if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop or c.dtype != "bf16":
             return False
@@ -589,7 +589,8 @@ class DistEngine:
                      api=_native.host.capi(), server_rank=0, allreduce=int(cfg.bsp_schedule == "allreduce"),
                      log_server=int(self.rank == 0), log_workers=int(bool(W)),
                      sink=self.log.native.handle if self.log is not None else 0,
-                     tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0)
+                     tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0,
+                     new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap))
             if W:
                 ds = W[0].source.ds
                 d.update(dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows))
@@ -605,6 +606,7 @@ class DistEngine:
             lp.set_sink(self.log.native.handle)
         for i, w in enumerate(W):
             lp.set_next_local(i, int(w.source.next_local))
+            lp.set_seen_at_solve(i, int(w._seen_at_solve))
         stream = comm.compute_stream()
         try:
             n = self._lanes_chunks(lp, comm, stream, int(rounds), W)
@@ -618,7 +620,7 @@ class DistEngine:
         for i, w in enumerate(W):
             w.source.next_local = int(lp.next_local(i))
             w.iters += n
-            w._seen_at_solve = w.tuples_seen
+            w._seen_at_solve = int(lp.seen_at_solve(i))
             lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
             if w.ring.XT is not None:
                 w.ring.xt_stale = True
@@ -632,16 +634,22 @@ class DistEngine:
         one (max_iters 0: ServerAppRunner's default) in chunks of 256 rounds with a
         collective stop vote after each -- stop when any rank's wall clock is up or
         every worker rank's stream has been exhausted for idle_exit_s (the dedicated
-        server rank has no say on data)."""
+        server rank has no say on data).  Rounds paced by the stream (the producer
+        clock or a tuple cadence: a rank's round waits for its lanes' tuples) run in
+        chunks of 4 rounds, so the wall-clock stop lands within a few rounds; every
+        rank runs the same rounds per chunk (no deadline inside a chunk: the ranks'
+        collectives must pair up)."""
         cfg = self.cfg
         if rounds:
             return int(lp.run(rounds, int(self.rounds), stream))
         t_start = time.time()
         exhausted_since = None
         flag = torch.zeros(2, dtype=torch.float32, device=self.device)
+        paced = cfg.stream_mode != "per_iter" or not cadence_free(cfg)
+        chunk = 4 if paced else 256
         n = 0
         while True:
-            n += int(lp.run(256, int(self.rounds) + n, stream))
+            n += int(lp.run(chunk, int(self.rounds) + n, stream))
             now = time.time()
             if W and all(lp.exhausted(i) for i in range(len(W))):
                 exhausted_since = exhausted_since or now

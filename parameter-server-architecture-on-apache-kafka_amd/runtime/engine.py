@@ -230,15 +230,16 @@ class LocalEngine:
         1..8 dense GPU workers with bf16 rings of <= 1024 rows, ONE launch per round
         (every worker's solve on its own XCD, the update, the previous round's
         evaluation rows).  Runs that need Python between rounds (tracing, injected
-        faults, a tuple-driven cadence) use the loops below."""
+        faults) use the loops below.  The tuple-driven cadence (--iter_new_*) and
+        the producer clock run natively: a round waits until every lane saw its
+        new tuples."""
         c = self.cfg
         if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
         W = [w for w in self.workers if w.k not in self.failed]
         if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
             return False
-        if not cadence_free(c) or c.inject_worker_delay_ms or c.inject_worker_crash \
-                or c.inject_worker_stop:
+        if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop:
             return False
         sp = self.spec
         for w in W:
@@ -279,7 +280,8 @@ class LocalEngine:
                  window=[w.window.handle for w in W], w=srv.w.data_ptr(), lr=float(cfg.lr),
                  shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
                  sb=[f.b.data_ptr() for f in self._lane_frags], scoff=0, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(),
-                 T=ev.T, sink=self.log.native.handle, tracker=srv.tracker.handle, api=_native.host.capi())
+                 T=ev.T, sink=self.log.native.handle, tracker=srv.tracker.handle, api=_native.host.capi(),
+                 new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap))
         lp = h.LanesLoop(d, None)
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
@@ -301,8 +303,10 @@ class LocalEngine:
         lp = self._lanes_loop(W)
         for i, w in enumerate(W):
             lp.set_next_local(i, int(w.source.next_local))
+            lp.set_seen_at_solve(i, int(w._seen_at_solve))
         stream = stream_handle(self.device)
         t_start = time.time()
+        deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
         r0 = r = self.rounds
         u0 = srv.updates
         chunk = 256
@@ -320,13 +324,13 @@ class LocalEngine:
                     exhausted_since = exhausted_since or time.time()
                 if self._stop(r - r0, t_start, exhausted_since):
                     break
-                n = int(lp.run(int(todo), int(r), stream))
+                n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
                 r += n
                 for i, w in enumerate(W):
                     w.source.next_local = int(lp.next_local(i))
                 if n:
                     maybe_checkpoint(cfg, srv, r, W)
-                if n < todo:  # a worker's stream is exhausted and its window empty
+                if n < todo:  # a worker's stream is exhausted and its window empty, or the deadline
                     break
             lp.flush(stream)
             torch.cuda.synchronize(self.device)
@@ -339,10 +343,10 @@ class LocalEngine:
         srv.updates += n * len(W)
         for i, w in enumerate(W):  # the last local solve's loss / delta, for code that reads the roles
             lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
-        for w in W:
+        for i, w in enumerate(W):
             w.vc = r
             w.iters += n
-            w._seen_at_solve = w.tuples_seen
+            w._seen_at_solve = int(lp.seen_at_solve(i))
             if w.ring.XT is not None:
                 w.ring.xt_stale = True  # the round kernel writes the row-major ring only
         if srv.frag is not None:

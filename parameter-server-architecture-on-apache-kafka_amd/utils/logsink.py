@@ -77,16 +77,14 @@ class LogSink:
                     ts: int | None = None):
         """Evaluate the worker's local model ``w`` and log a worker row."""
         slot, seq, addr = self.native.acquire()
-        ts = -1 if ts is None else ts  # -1: stamped by the sink when the evaluation lands
         evalset.eval_to_slot(frag, w, scratch, addr, seq, loss_dev)
-        self.native.submit(slot, seq, 0, ts, int(partition), int(vc), int(nseen))
+        self.native.submit(slot, seq, 0, self._ts(ts), int(partition), int(vc), int(nseen))
 
     def server_eval(self, evalset, frag, w, scratch, vc: int, ts: int | None = None):
         """Evaluate the global model ``w`` and log a server row."""
         slot, seq, addr = self.native.acquire()
-        ts = -1 if ts is None else ts
         evalset.eval_to_slot(frag, w, scratch, addr, seq, None)
-        self.native.submit(slot, seq, 1, ts, -1, int(vc), 0)
+        self.native.submit(slot, seq, 1, self._ts(ts), -1, int(vc), 0)
 
     def pair_eval(self, evalset, frag_w, w_w, loss_dev, partition: int, vc_w: int, nseen: int, frag_s, w_s,
                   vc_s: int | None, ts_s: int, scratch, ts_w: int | None = None, apply=None):
@@ -96,11 +94,19 @@ class LogSink:
         slot_s = seq_s = addr_s = 0
         if vc_s is not None:
             slot_s, seq_s, addr_s = self.native.acquire()
-        ts_w = -1 if ts_w is None else int(ts_w)
         evalset.eval_pair_to_slots(frag_w, w_w, frag_s, w_s, scratch, addr_w, seq_w, loss_dev, addr_s, seq_s, apply)
         if vc_s is not None:
-            self.native.submit(slot_s, seq_s, 1, int(ts_s), -1, int(vc_s), 0)
-        self.native.submit(slot_w, seq_w, 0, ts_w, int(partition), int(vc_w), int(nseen))
+            self.native.submit(slot_s, seq_s, 1, self._ts(ts_s), -1, int(vc_s), 0)
+        self.native.submit(slot_w, seq_w, 0, self._ts(ts_w), int(partition), int(vc_w), int(nseen))
+
+    def _ts(self, ts) -> int:
+        """Row timestamp: the given one, else -1 on a GPU (the sink stamps the row when
+        the device's evaluation lands in its slot) or now on the CPU, where the
+        evaluation has completed before the submit (a sink thread starved on a busy
+        host would otherwise stamp it late and misorder the ranks' rows)."""
+        if ts is not None and int(ts) >= 0:
+            return int(ts)
+        return -1 if self.gpu else int(time.time() * 1000.0)
 
     # -- consumers ---------------------------------------------------------
     def drain(self, block: bool = False):

@@ -129,7 +129,8 @@ def build_hip(force=False, jobs=8):
         glob.glob(os.path.join(CSRC, "runtime", "*.hip"))) + [os.path.join(CSRC, "bindings", "hip_module.hip")]
     headers = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + glob.glob(os.path.join(CSRC, "solver", "*.h")) +
                      glob.glob(os.path.join(CSRC, "comm", "*.h")) + glob.glob(os.path.join(CSRC, "runtime", "*.h")) +
-                     [os.path.join(CSRC, "host", "capi.h"), os.path.join(CSRC, "host", "ctrl.h")])
+                     [os.path.join(CSRC, "host", "capi.h"), os.path.join(CSRC, "host", "ctrl.h"),
+                     os.path.join(CSRC, "host", "sink_record.h")])
     out = os.path.join(PKG, "_psx_hip" + _ext_suffix())
     cflags = [
         "-O3",

@@ -135,10 +135,29 @@ int c_bsp_round(void* t, int64_t v) {
       -1);
 }
 
+int c_acquire_many(void* s, int n, int* slots, uint64_t* seqs, uintptr_t* addrs) {
+  return guarded(
+      [&] {
+        auto* sink = static_cast<MetricsSink*>(s);
+        sink->acquire_many(n, slots, seqs);
+        for (int i = 0; i < n; ++i) addrs[i] = sink->slot_address(slots[i]);
+        return 0;
+      },
+      -1);
+}
+int c_submit_many(void* s, int n, const SinkRecord* recs) {
+  return guarded(
+      [&] {
+        static_cast<MetricsSink*>(s)->submit_many(n, recs);
+        return 0;
+      },
+      -1);
+}
+
 const HostApi kApi{kHostApiVersion, c_on_delta,   c_retire,         c_is_live,       c_revive,
                    c_clock,         c_sent,       c_pop,            c_push,          c_acquire,
                    c_submit,        c_last_error, c_window_insert_many, c_window_state, c_due_rows,
-                   c_bsp_round};
+                   c_bsp_round,     c_acquire_many, c_submit_many};
 
 }  // namespace
 

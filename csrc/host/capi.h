@@ -10,10 +10,11 @@
 #include <cstdint>
 
 #include "ctrl.h"
+#include "sink_record.h"
 
 namespace psx {
 
-constexpr int kHostApiVersion = 2;
+constexpr int kHostApiVersion = 3;
 
 struct HostApi {
   int version;
@@ -47,6 +48,10 @@ struct HostApi {
   // VectorClockTracker::bsp_round: every live worker's delta of round v received,
   // the weights of v + 1 sent
   int (*tracker_bsp_round)(void* tracker, int64_t v);
+  // ---- version 3: batched metrics-sink hand-over (the lanes loop: a round's rows
+  // under one lock and one wake-up).  addrs[i]: host address of slots[i]; 0 / -1 ----
+  int (*sink_acquire_many)(void* sink, int n, int* slots, uint64_t* seqs, uintptr_t* addrs);
+  int (*sink_submit_many)(void* sink, int n, const SinkRecord* recs);
 };
 
 const HostApi* host_api();

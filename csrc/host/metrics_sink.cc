@@ -59,6 +59,18 @@ int MetricsSink::acquire(uint64_t* seq) {
   return s;
 }
 
+void MetricsSink::acquire_many(int n, int* slots, uint64_t* seqs) {
+  if (n < 0 || n > nslots_) throw std::invalid_argument("MetricsSink: acquire_many beyond the slot pool");
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_free_.wait(lk, [&] { return (int)free_.size() >= n || stop_; });
+  if (stop_) throw std::runtime_error("MetricsSink is closed");
+  for (int i = 0; i < n; ++i) {
+    slots[i] = free_.back();
+    free_.pop_back();
+    seqs[i] = next_seq_++;
+  }
+}
+
 uintptr_t MetricsSink::slot_address(int slot) const {
   if (slot < 0 || slot >= nslots_) throw std::out_of_range("slot");
   return reinterpret_cast<uintptr_t>(&slots_[slot]);
@@ -73,6 +85,20 @@ void MetricsSink::submit(int slot, uint64_t seq, int kind, int64_t ts, int64_t p
     ++submitted_;
   }
   cv_work_.notify_one();
+}
+
+void MetricsSink::submit_many(int n, const SinkRecord* recs) {
+  for (int i = 0; i < n; ++i)
+    if (recs[i].slot < 0 || recs[i].slot >= nslots_) throw std::out_of_range("slot");
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < n; ++i) {
+      const SinkRecord& r = recs[i];
+      pending_.push_back(Pending{r.slot, r.seq, r.kind, r.ts, r.partition, r.vc, r.nseen});
+    }
+    submitted_ += n;
+  }
+  if (n > 0) cv_work_.notify_one();
 }
 
 void MetricsSink::run() {

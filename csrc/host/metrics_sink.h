@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "logger.h"
+#include "sink_record.h"
 
 namespace psx {
 
@@ -52,6 +53,7 @@ struct ServerRow {
   double f1, acc;
 };
 
+
 class MetricsSink {
  public:
   // slots: nslots EvalSlot records (host pointer).  Loggers may be null.
@@ -64,8 +66,13 @@ class MetricsSink {
   // and the sequence number the producer must publish.
   int acquire(uint64_t* seq);
   uintptr_t slot_address(int slot) const;
+  // n slots at once (one lock; blocks until n are free, n <= nslots).
+  void acquire_many(int n, int* slots, uint64_t* seqs);
   // kind 0 = worker row, 1 = server row.
   void submit(int slot, uint64_t seq, int kind, int64_t ts, int64_t partition, int64_t vc, int64_t nseen);
+  // n records in order, one lock and one wake-up of the logger thread (a round of
+  // the lanes loop hands over up to 9 rows)
+  void submit_many(int n, const SinkRecord* recs);
   // Wait until every submitted record has been processed (timeout_s <= 0: forever).
   bool flush(double timeout_s = 0.0);
   void close();

@@ -348,45 +348,48 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
   ev->K = cfg_.scfg.K;
   ev->acc = acc_;
   ev->ticket = ticket_;
-  void* sink = reinterpret_cast<void*>(cfg_.sink);
-  auto add = [&](const uint16_t* hi, const uint16_t* lo, const float* bb, int coff, const float* loss, int kind) {
-    uint64_t seq = 0;
-    uintptr_t addr = 0;
-    const int slot = api().sink_acquire(sink, &seq, &addr);
-    check(slot, "metrics sink acquire");
+  const int nw = cfg_.log_workers ? cfg_.L : 0, n = nw + (cfg_.log_server ? 1 : 0);
+  if (n == 0) return;
+  // the round's slots in one reservation (one lock of the sink)
+  int sl[kMaxEvalModels];
+  uint64_t sq[kMaxEvalModels];
+  uintptr_t ad[kMaxEvalModels];
+  check(api().sink_acquire_many(reinterpret_cast<void*>(cfg_.sink), n, sl, sq, ad), "metrics sink acquire");
+  auto add = [&](int i, const uint16_t* hi, const uint16_t* lo, const float* bb, int coff, const float* loss,
+                 int kind) {
     EvalModel& m = ev->m[ev->nmodels++];
     m.hi = hi;
     m.lo = lo;
     m.b = bb;
     m.coff = coff;
     m.loss = loss;
-    m.slot = reinterpret_cast<char*>(addr);
-    m.seq = seq;
-    slots->push_back(slot);
-    seqs->push_back(seq);
+    m.slot = reinterpret_cast<char*>(ad[i]);
+    m.seq = sq[i];
+    slots->push_back(sl[i]);
+    seqs->push_back(sq[i]);
     kinds->push_back(kind);
   };
-  if (cfg_.log_workers)
-    for (int l = 0; l < cfg_.L; ++l)
-      add(lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
-  if (cfg_.log_server)
-    add(cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
+  for (int l = 0; l < nw; ++l)
+    add(l, lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
+  if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
 }
 
 void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
                             const std::vector<int>& kinds) {
-  void* sink = reinterpret_cast<void*>(cfg_.sink);
   // the reference's order: the server row, then the worker rows; timestamps are
-  // taken by the sink when the evaluation lands (ts = -1)
+  // taken by the sink when the evaluation lands (ts = -1); one hand-over
+  SinkRecord rec[kMaxEvalModels];
+  int n = 0;
   for (size_t i = 0; i < slots.size(); ++i)
-    if (kinds[i] == 1) api().sink_submit(sink, slots[i], seqs[i], 1, -1, -1, p.vc, 0);
+    if (kinds[i] == 1) rec[n++] = SinkRecord{slots[i], 1, seqs[i], -1, -1, p.vc, 0};
   int l = 0;
   for (size_t i = 0; i < slots.size(); ++i)
     if (kinds[i] == 0) {
-      api().sink_submit(sink, slots[i], seqs[i], 0, -1, cfg_.k[l], p.vc, p.nseen[l]);
+      rec[n++] = SinkRecord{slots[i], 0, seqs[i], -1, cfg_.k[l], p.vc, p.nseen[l]};
       ++l;
     }
+  if (n) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), n, rec), "metrics sink submit");
 }
 
 void LanesLoop::check_errors(int64_t round) {

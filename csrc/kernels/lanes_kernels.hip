@@ -294,11 +294,21 @@ __device__ __forceinline__ void lane_prep(char* lb, const SolverCfg& cfg, const 
   float* ivl = sdl + 32;                      // [32]
   unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);  // [2][512] (bwd_body's staging)
   double s = 0.0, q = 0.0;
-  for (int gg = grp; gg < ntr; gg += 8) {
-    const double pv = ld_h<S>((const double*)(spart + ((size_t)gg * FP + fs + fl) * 2));
-    const float2 u = __builtin_bit_cast(float2, pv);
-    s += (double)u.x;
-    q += (double)u.y;
+  {  // the (<= 4) row tiles' partials of this thread all in flight, then summed in tile order
+    constexpr int NPT = (kLaneWg + 7) / 8;
+    double pv[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int gg = grp + 8 * i;
+      pv[i] = gg < ntr ? ld_h<S>((const double*)(spart + ((size_t)gg * FP + fs + fl) * 2)) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+      if (grp + 8 * i < ntr) {
+        const float2 u = __builtin_bit_cast(float2, pv[i]);
+        s += (double)u.x;
+        q += (double)u.y;
+      }
   }
   red[(grp * 32 + fl) * 2] = s;
   red[(grp * 32 + fl) * 2 + 1] = q;
@@ -530,6 +540,12 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   barrier();
   if (wg == 0 && tid == 0) stamp(dv, 30, 3);
   // ---- slots (as solve_persist_kernel) ----
+  // Every workgroup a slice owner (G == NS: the window has no more tiles than the
+  // model has 32-feature slices): the controller's phase is in every workgroup's
+  // LDS copy, so the slot that ends the solve finalises each slice in place, from
+  // the registers of its backward (delta written through for the cross-lane sum),
+  // and skips the last grid barrier -- no later forward reads its trial point.
+  const bool inplace = G == NS;
   int phase = kPhInit;
   for (int slot = 0; slot < cfg.nslots; ++slot) {
     if (phase == kPhDone) break;  // uniform: every workgroup holds the same phase
@@ -542,7 +558,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       store_gpf<FP, S == 1>(dv, wg, G, acc);
     }
     barrier();
-    if (owner) bwd_body<FP, KP, S>(cfg, win, lanes[l].ctrl, slot, dv, G, lb, wg, NS);
+    if (owner)
+      bwd_body<FP, KP, S>(cfg, win, lanes[l].ctrl, slot, dv, G, lb, wg, NS, false, inplace ? 0 : kNoFinSlot,
+                          /*fin_sc1=*/true);
+    if (inplace && cl->phase == kPhDone) {
+      phase = kPhDone;
+      break;
+    }
     if (wg == 0 && tid == 0) st_h64<S>(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
     barrier();
     phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
@@ -550,7 +572,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   if (!owner) return;
   if (wg == 0 && tid == 0) stamp(dv, 30, 4);
   // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
-  {
+  if (!inplace) {
     FinIn<KP> in;
     const int f = wg * 32 + tid;
     if (tid < 32) {

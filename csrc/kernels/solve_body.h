@@ -485,9 +485,11 @@ struct FinSl {
   }
 };
 
+// sc1_delta: the delta is stored write-through (agent scope) for readers on other
+// XCDs (the lanes kernel's cross-lane sum), as finalize_feature's flag.
 template <int KP>
 __device__ __forceinline__ void finalize_slice(const SolverCfg& cfg, const SolveDev& dv, int blk, const FinSl<KP>& in,
-                                               float* wvl /* LDS [16][32] */) {
+                                               float* wvl /* LDS [16][32] */, bool sc1_delta = false) {
   constexpr int NE = FinSl<KP>::NE;
   const int FP = cfg.Fp, K = cfg.K;
   const int fl = threadIdx.x & 31, cg = threadIdx.x >> 5, f = blk * 32 + fl;
@@ -511,7 +513,10 @@ __device__ __forceinline__ void finalize_slice(const SolverCfg& cfg, const Solve
     write_frag(dv.out_hi, dv.out_lo, c, f, v);
     if (c < K) {
       const float dl = v - in.wo[e];
-      dv.delta[c * FP + f] = dl;
+      if (sc1_delta)
+        st_sc1(dv.delta + c * FP + f, dl);
+      else
+        dv.delta[c * FP + f] = dl;
       if (dv.w_new) dv.w_new[c * FP + f] = v;
       if (dv.ap_w) {  // fused server update (see finalize_feature)
         const float nw = in.wo[e] + dv.ap_lr * dl;
@@ -544,7 +549,8 @@ constexpr size_t kBwdLdsBytes = (size_t)4 * 16 * 32 * 4 + 2 * 512 * 2 + ctrl_lds
 template <int FP, int KP, int kP = 0, int kXs = (kP == 2 ? 2 : 1)>
 __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams win, Ctrl* gctrl, int slot,
                                          const SolveDev& dv, int fwd_grid, char* lds, const int wg, const int NS,
-                                         const bool check_done = false, const int fin_slot = kNoFinSlot) {
+                                         const bool check_done = false, const int fin_slot = kNoFinSlot,
+                                         const bool fin_sc1 = false) {
   constexpr int FPI = FP > 256 ? FP : 256;
   constexpr int IB = KP * FPI;              // internal intercept base
   constexpr int NE = KP >= 8 ? KP / 8 : 1;  // elements per thread
@@ -1032,7 +1038,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       in.wo[e] = WO[e];
     }
     __syncthreads();  // gw (the gradient's LDS) is free: its last reads preceded the dots
-    finalize_slice<KP>(cfg, dv, wg, in, gw);
+    finalize_slice<KP>(cfg, dv, wg, in, gw, fin_sc1);
   }
   // ---- next trial point: this slice of the MFMA weight fragments (16-B stores) ----
   if (!done) {

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-3 GPU session R: full GPU suite, smoke, the driver's bench forms (4 / 8
+# workers), phase timeline, rocprofv3 kernel trace and the PMC passes of the
+# default bench (tools/pmc_profile.sh).
+set -o pipefail
+OUT=gpurun_out/r03r
+mkdir -p $OUT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+echo "pytest rc=$?" >> $OUT/pytest_gpu.log
+grep -q "Fatal\|core dumped\|HSA_STATUS" $OUT/pytest_gpu.log && exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
+timeout -k 10 120 python bench.py --steps 20 --warmup 5 > $OUT/bench_short.json 2> $OUT/bench_short.err || exit 1
+timeout -k 10 120 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1
+timeout -k 10 120 python bench.py --workers 8 > $OUT/bench_w8.json 2> $OUT/bench_w8.err || exit 1
+timeout -k 10 120 python bench.py --workers 1 > $OUT/bench_w1.json 2> $OUT/bench_w1.err || exit 1
+for L in 4 8; do
+  PSX_LANES_STAMPS=1 timeout -k 10 120 python tools/lanes_profile.py --lanes $L --rounds 400 >> $OUT/lanes_profile.jsonl 2> $OUT/lanes_profile.err || exit 1
+done
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o w4 -- python3 bench.py --steps 200 --warmup 20 --no-accuracy-run > $OUT/bench_prof.json 2> $OUT/prof.err || exit 1
+PMC_STEPS=200 bash tools/pmc_profile.sh > $OUT/pmc_passes.txt 2>&1
+echo "session done"

@@ -183,7 +183,7 @@ PSX_HD inline double ls_interp(double lt, double lf, double ld, double rt, doubl
 
 // Compact L-BFGS direction d = -H g for the current history.  Fills cg/cs/cy
 // and returns d . g.
-PSX_HD inline double ctrl_direction(Ctrl& c, int H, CtrlScratch& ws) {
+PSX_HD inline double ctrl_direction(Ctrl& __restrict__ c, int H, CtrlScratch& __restrict__ ws) {
   for (int i = 0; i < kMaxHist; ++i) c.cs[i] = c.cy[i] = 0.0;
   const int m = c.m;
   if (m == 0) {
@@ -231,8 +231,8 @@ PSX_HD inline double ctrl_direction(Ctrl& c, int H, CtrlScratch& ws) {
 
 // Accept the evaluated trial point (step t_eval): bookkeeping of the new
 // curvature pair and the next direction.  `dots` as produced by the reduction.
-PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot,
-                               CtrlScratch& ws) {
+PSX_HD inline void ctrl_accept(Ctrl& __restrict__ c, const SolverCfg& cfg, double f_t,
+                               const double* __restrict__ dots, int slot, CtrlScratch& __restrict__ ws) {
   const int H = cfg.hist;
   const double tt = dots[0], td = dots[1], tc = dots[2];
   const double t = c.t;
@@ -334,8 +334,11 @@ PSX_HD inline void ctrl_accept(Ctrl& c, const SolverCfg& cfg, double f_t, const 
 
 // Advance the state machine after the function evaluation of `slot`.
 // f_t = objective at the trial point, dots as documented above.
-PSX_HD inline void ctrl_step(Ctrl& c, const SolverCfg& cfg, double f_t, const double* dots, int slot,
-                             CtrlScratch& ws) {
+// (__restrict__: the state, the dots and the scratch never alias -- on the device
+// they are separate LDS blocks, so the single controller thread's loads need not
+// wait behind its own stores)
+PSX_HD inline void ctrl_step(Ctrl& __restrict__ c, const SolverCfg& cfg, double f_t, const double* __restrict__ dots,
+                             int slot, CtrlScratch& __restrict__ ws) {
   c.evals += 1;
   const double tt = dots[0], td = dots[1];
   const bool finite = f_t == f_t && fabs(f_t) < 1e300;

@@ -328,11 +328,19 @@ class LocalEngine:
                 r += n
                 for i, w in enumerate(W):
                     w.source.next_local = int(lp.next_local(i))
+                    w._seen_at_solve = int(lp.seen_at_solve(i))
                 if n:
                     maybe_checkpoint(cfg, srv, r, W)
                 if n < todo:  # a worker's stream is exhausted and its window empty, or the deadline
                     break
             lp.flush(stream)
+            # stream-ordered behind the rounds: the last local solve's loss / delta for code
+            # that reads the roles, and the Python-side evaluation fragments of the global
+            # model (the native update rewrote w); ONE synchronisation covers them all
+            for i, w in enumerate(W):
+                lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+            if srv.frag is not None:
+                srv.frag.refresh(srv.w)
             torch.cuda.synchronize(self.device)
             lp.poll_errors()  # a device error of the last rounds (the loop polls without syncs)
         except RuntimeError as e:
@@ -341,18 +349,13 @@ class LocalEngine:
             raise
         n = r - r0
         srv.updates += n * len(W)
-        for i, w in enumerate(W):  # the last local solve's loss / delta, for code that reads the roles
-            lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
         for i, w in enumerate(W):
             w.vc = r
             w.iters += n
             w._seen_at_solve = int(lp.seen_at_solve(i))
             if w.ring.XT is not None:
                 w.ring.xt_stale = True  # the round kernel writes the row-major ring only
-        if srv.frag is not None:
-            srv.frag.refresh(srv.w)  # the Python-side evaluation fragments follow the native update
         self.native_host_us_per_round = float(lp.host_us_per_round)
-        torch.cuda.synchronize(self.device)
         elapsed = time.time() - t_start
         self.rounds = r
         return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,

@@ -167,6 +167,7 @@ def worker_state(wk) -> dict:
         "window_head": int(wk.window.head),
         "window_size": int(wk.window.size),
         "tuples_seen": int(wk.window.tuples_seen),
+        "seen_at_solve": int(getattr(wk, "_seen_at_solve", 0)),  # the tuple cadence's origin
         **tensors,
     }
 
@@ -185,6 +186,7 @@ def restore_worker(wk, state: dict) -> None:
     wk.source.next_local = int(state["next_local"])
     wk.vc = int(state["vc"])
     wk.iters = int(state["iters"])
+    wk._seen_at_solve = int(state.get("seen_at_solve", 0))
 
 
 # ---- compatibility helpers (synchronous) -------------------------------------

@@ -737,7 +737,14 @@ __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
 
 }  // namespace
 
-int lanes_eval_grid() { return 256; }
+int lanes_eval_grid() {  // PSX_SIDE_GRID: workgroups of the evaluation launch (default 256)
+  static const int g = [] {
+    const char* e = std::getenv("PSX_SIDE_GRID");
+    const int v = e ? std::atoi(e) : 256;
+    return v >= 1 && v <= 4096 ? v : 256;
+  }();
+  return g;
+}
 
 void launch_lanes_eval(const SolverCfg& cfg, const EvalMulti& ev, hipStream_t s) {
   if (ev.nmodels <= 0) return;

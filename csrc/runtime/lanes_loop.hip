@@ -207,7 +207,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   ticket2_ = reinterpret_cast<unsigned*>(b + o_tic2);
   sflags_ = reinterpret_cast<unsigned*>(b + o_sfl);
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
-    side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : 0);
+    side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
   // PSX_LANES_SIDE_EVAL=1: the rows go to a co-running side launch instead of riders
   // of the round kernel.  Off by default: with 8 lanes (no XCD left for riders) the
   // two forms measured the same, 69.4k vs 69.2k updates/s (profiles/r03_v5), and
@@ -529,6 +529,16 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
         ev.acc = acc2_;
         ev.ticket = ticket2_;
         ev.nticket = (unsigned)lanes_eval_grid();
+        if (side_sync_ == 3) {  // stream order: the evaluation launch right behind the round
+          launch_lanes_eval(cfg_.scfg, ev, stream);
+          hip_check(hipGetLastError(), "evaluation launch");
+          submit_rows(pend_, slots, seqs, kinds);
+          pend_.valid = false;
+          if (cfg_.tracker && is_server)
+            check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
+          check_errors(r);
+          continue;
+        }
         if (side_sync_ == 1) {
           hip_check(hipStreamWriteValue32(stream, sflags_, (uint32_t)(r + 1), 0), "round done");
           hip_check(hipStreamWaitValue32(side_, sflags_, (uint32_t)(r + 1), hipStreamWaitValueGte), "side waits");

@@ -16,7 +16,9 @@ push on arrival).  Nothing is skipped inside the timed region.
     LR, F = 1024 hashed features, labels 1..5 (+ phantom class 0: K = 6,
     P = 6150), buffer min/max/bc = 128/1024/0.3, fine-food-reviews-shaped
     synthetic data (90k train / 4,877 test rows), random-init weights, bf16
-    features with fp32 master weights.  BSP, allreduce schedule.
+    features with fp32 master weights.  BSP; 8 workers per GPU by default, one per
+    XCD (BASELINE's 8-worker configuration; --workers 4 = the reference's numWorkers),
+    all solved in ONE launch per round (csrc/kernels/lanes_kernels.hip).
 --model sparse1m  (config 4): 10M rows x 2^20 hashed sparse features, labels
     1..5, ASP with a dedicated server rank (world >= 2; one GPU: in-process).
 --model sharded100m  (config 5): 10M rows x 10^8 hashed features, binary
@@ -81,7 +83,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="dense model feature rows (fp32: row-parallel solver with hi+lo MFMA operands)")
     ap.add_argument("--workers", type=int, default=None,
-                    help="logical workers per worker GPU, one XCD each in one launch per round (default 4: the "
+                    help="logical workers per worker GPU, one XCD each in one launch per round (default 8: one "
+                         "per XCD of the MI355X -- BASELINE's 8-worker configuration on one GPU; --workers 4 is the "
                          "reference's numWorkers = 4, all hosted in one process, BaseKafkaApp.java:25,70)")
     ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded", "keyrange"])
     ap.add_argument("--no-graph", action="store_true")
@@ -123,8 +126,8 @@ def parse(argv=None):
         a.warmup = 30 if wide else 200
     if a.schedule is None:
         a.schedule = "reduce_bcast" if a.dedicated_server else "allreduce"
-    if a.workers is None:  # the wide configs keep one worker per GPU
-        a.workers = 1 if wide else 4
+    if a.workers is None:  # the wide configs keep one worker per GPU; dense: one worker per XCD
+        a.workers = 1 if wide else 8
     return a
 
 

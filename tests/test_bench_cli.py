@@ -68,12 +68,18 @@ def test_bench_world_mismatch_is_an_error():
 
 
 def test_bench_single_gpu_default():
-    """One GPU: the server and the reference's numWorkers = 4 workers in one process
-    (BaseKafkaApp.java:25,70), server step 1/N (ServerProcessor.java:36)."""
+    """One GPU: the server and 8 workers in one process -- one per XCD of the MI355X
+    (all of the reference's workers share one process too, BaseKafkaApp.java:25,70),
+    server step 1/N (ServerProcessor.java:36); --workers 4 is the reference's numWorkers."""
     p, lines = _run(SMALL)
     assert p.returncode == 0, p.stderr[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w4")
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"].startswith("ps-bsp w8")
+    assert d["config"]["workers"] == 8 and d["config"]["server_lr"] == 0.125
+    assert d["config"]["workers_per_gpu"] == 8
+    p, lines = _run(SMALL + ["--workers", "4"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(lines[0])
     assert d["config"]["workers"] == 4 and d["config"]["server_lr"] == 0.25
     assert d["time_to_f1_0.40_s"] is None or d["time_to_f1_0.40_s"] > 0
 

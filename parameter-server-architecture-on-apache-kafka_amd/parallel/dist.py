@@ -437,6 +437,13 @@ class DistEngine:
                 with self.tracer.span("comm", schedule=sched):
                     # the stop vote rides in the payload's extra element (allreduce schedule)
                     payload = self._payload if (vote is not None and wk is not None) else delta
+                    row_first = comm is None and wk is not None
+                    if row_first:
+                        # torch.distributed (gloo): the worker row before the push, the
+                        # reference's order (WorkerTrainingProcessor.java:86-97) -- a row logged
+                        # after launching an asynchronous all-reduce can land after a faster
+                        # rank's next row, and the log-derived BSP gap would read 2
+                        wk.log_eval(self.log)
                     if comm is not None:
                         # in stream order; PSX_COMM_OVERLAP=1 runs it on the communicator's side
                         # stream beside the evaluations instead (the fork/join event pairs cost
@@ -448,7 +455,8 @@ class DistEngine:
                     else:
                         work = dist.all_reduce(payload, op=dist.ReduceOp.SUM, async_op=True)
                     if wk is not None:
-                        wk.log_eval(self.log)
+                        if not row_first:
+                            wk.log_eval(self.log)
                         # the next round's stream rows land in the ring while the collective
                         # is in flight (they overwrite only slots this round's solve has read)
                         if not (cfg.max_iters and r + 1 - self.rounds >= cfg.max_iters):

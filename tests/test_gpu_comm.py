@@ -233,3 +233,31 @@ def test_lanes_loop_dedicated_server_rank_world1(cuda, pg):
     assert max(f1) - min(f1) < 1e-9 and f1[0] > 0  # the same (unchanged) global model every round
     del lp
     comm.close()
+
+
+def test_dist_lanes_cli_defaults_producer_clock_and_cadence(cuda, pg):
+    """ServerAppRunner's defaults on the multi-rank engine: the producer clock (-p), the
+    fresh-window cadence (iter_new_frac 0.5) and an unbounded run that stops by the
+    wall clock -- all inside the native lanes loop (4-round chunks + stop vote)."""
+    import time
+
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig, new_tuples_needed
+    from psx.utils.data import synth_finefood
+
+    train, test = synth_finefood(40000, seed=0), synth_finefood(1000, seed=1)
+    cfg = PSConfig(consistency_model=0, producer_time_per_event=0.5, iter_new_frac=0.5, iter_new_cap=128,
+                   max_iters=0, max_wallclock_s=2.0, num_workers=2, workers_per_rank=2, bsp_schedule="allreduce",
+                   init="random")
+    eng = DistEngine(cfg, 0, 1, cuda, train=train, test=test)
+    t0 = time.time()
+    out = eng.run()
+    took = time.time() - t0
+    assert getattr(eng, "_lanes", None) is not None, "the lanes loop did not run"
+    assert out["rounds"] >= 3 and took < 2.0 + 3.0, (out["rounds"], took)
+    book = eng.log.book
+    assert [r[1] for r in book.server] == list(range(out["rounds"]))
+    for k in (0, 1):
+        seen = [r[-1] for r in book.worker if r[1] == k]
+        assert len(seen) == out["rounds"]
+        assert all(b - a >= min(new_tuples_needed(cfg, 128), 64) for a, b in zip(seen, seen[1:])), seen

@@ -121,6 +121,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [kMaxEvalModels][256]
   int* lastp = cl + kMaxEvalModels * 256;
+  float* bl = (float*)(lastp + 4);  // [16]: the current pair's intercepts (model A: 0..7, B: 8..15)
   const int tid = threadIdx.x, K = ev.K, T = ev.T, M = ev.nmodels;
   const int nT = (T + 31) / 32, npairs = (M + 1) / 2;
   for (int m = 0; m < M; ++m) cl[m * 256 + tid] = 0;
@@ -137,6 +138,11 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
     const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
     if (p != curp) {  // (workgroup-uniform)
       load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
+      if (tid < 16) {  // the intercepts into LDS once per pair, not a global load per class and row
+        const int h = tid >> 3, c = tid & 7;
+        const float* bp = h == 0 ? A.b + A.coff : Bm.b + Bm.coff;
+        bl[tid] = (c < K && (h == 0 || mb >= 0)) ? bp[c] : 0.f;
+      }
       curp = p;
     }
     const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
@@ -148,31 +154,21 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
     forward_tile_pre<FP>(lds, wf, a0, a1);
     store_partial_logits(red_base, a0, a1);
     __syncthreads();
-    if (tid < nrows) {
-      const int yl = ylab < 0 ? 0 : (ylab > 15 ? 15 : ylab);
-      const float* ba = A.b + A.coff;
-      int best = 0;
-      float bz = -INFINITY;
-      for (int c = 0; c < K; ++c) {
-        const float z = load_logit(red_base, tid, c) + ba[c];
-        if (z > bz) {
-          bz = z;
-          best = c;
-        }
-      }
-      atomicAdd(&cl[ma * 256 + yl * 16 + best], 1);
-      if (mb >= 0) {
-        const float* bb = Bm.b + Bm.coff;
-        int best2 = 0;
-        float bz2 = -INFINITY;
+    {  // thread (row, model): rows 0..31 x models {A, B} -- both models' argmax at once
+      const int row = tid & 31, h = (tid >> 5) & 1;
+      const int yrow = __shfl(ylab, row, 64);  // the row's label (held by thread `row` of wave 0)
+      if (tid < 64 && row < nrows && (h == 0 || mb >= 0)) {
+        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+        int best = 0;
+        float bz = -INFINITY;
         for (int c = 0; c < K; ++c) {
-          const float z = load_logit(red_base, tid, 8 + c) + bb[c];
-          if (z > bz2) {
-            bz2 = z;
-            best2 = c;
+          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
+          if (z > bz) {
+            bz = z;
+            best = c;
           }
         }
-        atomicAdd(&cl[mb * 256 + yl * 16 + best2], 1);
+        atomicAdd(&cl[(h == 0 ? ma : mb) * 256 + yl * 16 + best], 1);
       }
     }
     __syncthreads();

@@ -759,6 +759,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("inject_spin_timeout", &LanesLoop::inject_spin_timeout)
       .def("poll_errors", &LanesLoop::poll_errors)
       .def("read_stamps", [](const LanesLoop& l, int lane, uintptr_t s) { return l.read_stamps(lane, S(s)); })
+      .def("read_rider_stamps", [](const LanesLoop& l, uintptr_t s) { return l.read_rider_stamps(S(s)); })
       .def_static("probe_placement", [](uintptr_t s) { return LanesLoop::probe_placement(S(s)); });
   m.def("lanes_supported", &lanes_supported, py::arg("FP"), py::arg("K"), py::arg("cap"));
 

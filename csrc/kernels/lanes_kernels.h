@@ -83,6 +83,11 @@ struct EvalMulti {
   int* acc;          // [kMaxEvalModels][256] private accumulators (stride kAccStride), zero between passes
   unsigned* ticket;  // arrivals of the riders (reset by the last)
   unsigned nticket;
+  // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
+  // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the
+  // ticket, [10] the last rider is known, [11] its publication done, [12] / [13] the
+  // earliest / latest rider entry, [14] the latest ticket arrival
+  long long* dbg;
 };
 
 struct LanesArgs {

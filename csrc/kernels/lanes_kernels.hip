@@ -118,6 +118,16 @@ struct TileRegs {
 template <int FP>
 __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, int rid, int nride) {
   if (ev.nmodels <= 0 || rid >= nride) return;
+  long long* dbg = ev.dbg;
+  auto rstamp = [&](int k) {
+    if (dbg && threadIdx.x == 0) dbg[k] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  if (dbg && threadIdx.x == 0) {
+    const long long t = (long long)__builtin_amdgcn_s_memrealtime();
+    atomicMin((unsigned long long*)(dbg + 12), (unsigned long long)t);
+    atomicMax((unsigned long long*)(dbg + 13), (unsigned long long)t);
+  }
+  if (rid == 0) rstamp(0);
   char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [kMaxEvalModels][256]
   int* lastp = cl + kMaxEvalModels * 256;
@@ -150,6 +160,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
     const int ylab = tr.y;
     if (it + 1 < i1) tr.load(ev.Xt, ev.yt, (it + 1) % nT, T);
     __syncthreads();
+    if (rid == 0 && it == i0) rstamp(1);
     f32x4 a0, a1;
     forward_tile_pre<FP>(lds, wf, a0, a1);
     store_partial_logits(red_base, a0, a1);
@@ -172,6 +183,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
       }
     }
     __syncthreads();
+    if (rid == 0 && it - i0 < 4) rstamp(2 + (it - i0));
   }
   __syncthreads();
   for (int m = 0; m < M; ++m) {
@@ -180,11 +192,16 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (rid == 0) rstamp(8);
+  if (dbg && tid == 0)
+    atomicMax((unsigned long long*)(dbg + 14), (unsigned long long)__builtin_amdgcn_s_memrealtime());
   if (tid == 0)
     *lastp = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ev.nticket - 1;
   __syncthreads();
   if (!*lastp) return;
+  rstamp(10);
   publish_counts(ev, M, tid);
+  rstamp(11);
 }
 
 // ---------------------------------------------------------------------------

@@ -134,6 +134,9 @@ class LanesLoop {
   // phase timeline of lane `lane`'s last solve (PSX_LANES_STAMPS=1 at construction):
   // [slot][k] s_memrealtime ticks (100 MHz), row 30 = the round's own phases
   std::vector<long long> read_stamps(int lane, hipStream_t stream) const;
+  // the riders' timeline of the last launch that evaluated (PSX_LANES_STAMPS=1;
+  // EvalMulti::dbg layout)
+  std::vector<long long> read_rider_stamps(hipStream_t stream) const;
   // placement probe: blockIdx % 8 == XCC_ID for every workgroup of a large launch
   static bool probe_placement(hipStream_t stream);
 
@@ -187,6 +190,7 @@ class LanesLoop {
   // (PSX_SIDE_SYNC=value), 2 = none on the main stream (measurement only)
   int side_sync_ = 0;
   unsigned* sflags_ = nullptr;  // [0] last round done (main), [1] last evaluation done (side)
+  long long* rider_dbg_ = nullptr;  // PSX_LANES_STAMPS: the riders' stamps
   int64_t eval_round_[2] = {-1, -1};
   Pending pend_;
   int last_par_ = 0;  // parity of the last round run

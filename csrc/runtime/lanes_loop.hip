@@ -144,6 +144,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   const size_t o_acc2 = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
   const size_t o_tic2 = take(8 * sizeof(unsigned));
   const size_t o_sfl = take(8 * sizeof(unsigned));
+  const size_t o_rdbg = stamps ? take(64 * sizeof(long long)) : 0;
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
   char* b = static_cast<char*>(ws_);
@@ -206,6 +207,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
   acc2_ = reinterpret_cast<int*>(b + o_acc2);
   ticket2_ = reinterpret_cast<unsigned*>(b + o_tic2);
   sflags_ = reinterpret_cast<unsigned*>(b + o_sfl);
+  rider_dbg_ = stamps ? reinterpret_cast<long long*>(b + o_rdbg) : nullptr;
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
   // PSX_LANES_SIDE_EVAL=1: the rows go to a co-running side launch instead of riders
@@ -373,6 +375,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
     add(l, lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
+  ev->dbg = rider_dbg_;
 }
 
 void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
@@ -493,6 +496,10 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
+      if (rider_dbg_ && a.ev.nmodels > 0) {  // PSX_LANES_STAMPS: this launch's rider timeline
+        hip_check(hipMemsetAsync(rider_dbg_, 0, 64 * sizeof(long long), stream), "rider stamps");
+        hip_check(hipMemsetAsync(rider_dbg_ + 12, 0xff, sizeof(long long), stream), "rider stamps");
+      }
       launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
       hip_check(hipGetLastError(), "lanes round launch");
       ++launches_;
@@ -614,6 +621,16 @@ std::vector<long long> LanesLoop::read_stamps(int lane, hipStream_t stream) cons
   if (!d) return v;
   v.resize(32 * 16);
   hip_check(hipMemcpyAsync(v.data(), d, v.size() * sizeof(long long), hipMemcpyDeviceToHost, stream), "stamps");
+  hip_check(hipStreamSynchronize(stream), "sync");
+  return v;
+}
+
+std::vector<long long> LanesLoop::read_rider_stamps(hipStream_t stream) const {
+  std::vector<long long> v;
+  if (!rider_dbg_) return v;
+  v.resize(64);
+  hip_check(hipMemcpyAsync(v.data(), rider_dbg_, v.size() * sizeof(long long), hipMemcpyDeviceToHost, stream),
+            "rider stamps");
   hip_check(hipStreamSynchronize(stream), "sync");
   return v;
 }

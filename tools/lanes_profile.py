@@ -114,6 +114,14 @@ def main():
            "hand_off_scope": lp.hand_off_scope}
     if os.environ.get("PSX_LANES_STAMPS"):
         res["phases"] = [phases(lp.read_stamps(l, s)) for l in range(a.lanes)]
+        # the riders of the last round, us from lane 0's phase-I start (its stamp 30/0)
+        rs, base = lp.read_rider_stamps(s), lp.read_stamps(0, s)[30 * 16]
+        if rs and base:
+            rel = lambda t: round((t - base) / 100.0, 2) if 0 < t < (1 << 62) else None
+            res["riders"] = {"first_entry": rel(rs[12]), "last_entry": rel(rs[13]), "rider0_entry": rel(rs[0]),
+                             "rider0_first_tile": rel(rs[1]), "rider0_items": [rel(rs[2 + i]) for i in range(4)],
+                             "rider0_ticket": rel(rs[8]), "last_ticket": rel(rs[14]),
+                             "publisher_known": rel(rs[10]), "published": rel(rs[11])}
     print(json.dumps(res))
 
 

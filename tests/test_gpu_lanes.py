@@ -207,13 +207,16 @@ def test_lanes_ring_rows_across_epoch_wrap(cuda):
             assert torch.equal(y.cpu(), train.y[rows.to(cuda)].cpu()), (rnd, k)
 
 
+@pytest.mark.parametrize("sync", ["event", "inline"])
 @pytest.mark.parametrize("L", [2, 8])
-def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L):
+def test_side_stream_evaluation_rows_equal_riders(cuda, monkeypatch, L, sync):
     """The co-running side-stream evaluation (PSX_LANES_SIDE_EVAL=1) logs the same
     rows as the in-launch riders: every worker's local model and the global model,
     identical confusion counts."""
     spec, train, ev = _data(cuda)
     books = []
+    if sync == "inline":  # the evaluation launch right behind each round on the same stream
+        monkeypatch.setenv("PSX_SIDE_SYNC", "inline")
     for side in ("0", "1"):
         monkeypatch.setenv("PSX_LANES_SIDE_EVAL", side)
         w = spec.init("random", seed=6, device=cuda)

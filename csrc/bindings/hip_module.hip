@@ -725,6 +725,8 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.new_rows = (int)I("new_rows", 0);
              c.new_frac = D("new_frac", 0.0);
              c.new_cap = (int)I("new_cap", 0);
+             c.log_worker = (int)I("log_worker", 0);
+             c.delay_us = d.contains("delay_us") ? d["delay_us"].cast<std::vector<int>>() : std::vector<int>{};
              return std::make_unique<LanesLoop>(c, comm);
            }),
            py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())
@@ -736,6 +738,15 @@ PYBIND11_MODULE(_psx_hip, m) {
           },
           py::arg("rounds"), py::arg("r0"), py::arg("stream"), py::arg("max_wait_s") = 600.0,
           py::arg("deadline_ms") = 0.0)
+      .def(
+          "run_async",
+          [](LanesLoop& l, int64_t updates, uintptr_t stream, double max_wait_s, double deadline_ms) {
+            py::gil_scoped_release nogil;
+            return l.run_async(updates, S(stream), max_wait_s, deadline_ms);
+          },
+          py::arg("updates"), py::arg("stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0)
+      .def_property_readonly("tickets", &LanesLoop::tickets)
+      .def_property_readonly("host_us_per_update", &LanesLoop::host_us_per_update)
       .def("seen_at_solve", &LanesLoop::seen_at_solve)
       .def("set_seen_at_solve", &LanesLoop::set_seen_at_solve)
       .def("new_tuples_needed", &LanesLoop::new_tuples_needed)

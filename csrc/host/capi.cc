@@ -154,10 +154,14 @@ int c_submit_many(void* s, int n, const SinkRecord* recs) {
       -1);
 }
 
+int c_is_sent(void* t, int k) {
+  return guarded([&] { return static_cast<VectorClockTracker*>(t)->is_sent(k) ? 1 : 0; }, -1);
+}
+
 const HostApi kApi{kHostApiVersion, c_on_delta,   c_retire,         c_is_live,       c_revive,
                    c_clock,         c_sent,       c_pop,            c_push,          c_acquire,
                    c_submit,        c_last_error, c_window_insert_many, c_window_state, c_due_rows,
-                   c_bsp_round,     c_acquire_many, c_submit_many};
+                   c_bsp_round,     c_acquire_many, c_submit_many, c_is_sent};
 
 }  // namespace
 

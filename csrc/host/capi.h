@@ -14,7 +14,7 @@
 
 namespace psx {
 
-constexpr int kHostApiVersion = 3;
+constexpr int kHostApiVersion = 4;
 
 struct HostApi {
   int version;
@@ -52,6 +52,10 @@ struct HostApi {
   // under one lock and one wake-up).  addrs[i]: host address of slots[i]; 0 / -1 ----
   int (*sink_acquire_many)(void* sink, int n, int* slots, uint64_t* seqs, uintptr_t* addrs);
   int (*sink_submit_many)(void* sink, int n, const SinkRecord* recs);
+  // ---- version 4: the asynchronous lanes loop (SSP / ASP, csrc/runtime/lanes_loop.h)
+  // carries releases over launches: 1 = the weights of worker k's clock were
+  // dispatched (k is busy or about to start), 0 = idle, -1 = error ----
+  int (*tracker_is_sent)(void* tracker, int k);
 };
 
 const HostApi* host_api();

@@ -1,6 +1,7 @@
 #include "metrics_sink.h"
 
 #include <chrono>
+#include <cstring>
 #include <stdexcept>
 
 namespace psx {
@@ -33,6 +34,25 @@ void weighted_f1_accuracy(const int32_t* conf16, int K, double* f1, double* acc)
   }
   *f1 = wf1;
   *acc = tp_sum / total;
+}
+
+bool MetricsSink::read_tagged(const EvalSlot& s, uint64_t seq, int32_t* conf16, float* loss) const {
+  // chunk i = 4 words at byte 16 i: {tag, payload x 3}; each chunk is one 16-B
+  // device store, so a chunk whose tag matches carries its own payload
+  const uint32_t tag = (uint32_t)seq | 0x80000000u;  // eval_tag (lanes_kernels.h)
+  const volatile uint32_t* w = reinterpret_cast<const volatile uint32_t*>(&s);
+  const int K = K_, cells = K * K, nch = 1 + (cells + 2) / 3;
+  for (int i = 0; i < nch; ++i)
+    if (w[4 * i] != tag) return false;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  for (int i = 0; i < 256; ++i) conf16[i] = 0;
+  uint32_t lb = w[1];
+  std::memcpy(loss, &lb, 4);
+  for (int c = 0; c < cells; ++c) conf16[(c / K) * 16 + c % K] = (int32_t)w[4 * (1 + c / 3) + 1 + c % 3];
+  // re-check: a chunk rewritten meanwhile would be a protocol error, not a torn read
+  for (int i = 0; i < nch; ++i)
+    if (w[4 * i] != tag) return false;
+  return true;
 }
 
 MetricsSink::MetricsSink(uintptr_t slots, int nslots, int K, CsvLogger* wlog, CsvLogger* slog, bool keep_records)
@@ -110,10 +130,14 @@ void MetricsSink::run() {
       if (pending_.empty()) return;  // stop requested and nothing left
       p = pending_.front();
     }
-    // the producer (a kernel or the CPU path) publishes seq after the payload
+    // the producer (a kernel or the CPU path) publishes seq after the payload, or
+    // (kSinkTagged) tags every 16-B chunk of it with the sequence number
     EvalSlot& s = slots_[p.slot];
+    const bool tagged = (p.kind & kSinkTagged) != 0;
+    int32_t conf[256];
+    float tloss = 0.f;
     int spins = 0;
-    while (__atomic_load_n(&s.seq, __ATOMIC_ACQUIRE) != p.seq) {
+    while (tagged ? !read_tagged(s, p.seq, conf, &tloss) : __atomic_load_n(&s.seq, __ATOMIC_ACQUIRE) != p.seq) {
       if (++spins < 64) continue;
       std::this_thread::sleep_for(std::chrono::microseconds(spins < 4096 ? 5 : 200));
       std::lock_guard<std::mutex> lk(mu_);
@@ -126,9 +150,9 @@ void MetricsSink::run() {
                .count() /
            1000.0;
     double f1 = 0.0, acc = 0.0;
-    weighted_f1_accuracy(s.conf, K_, &f1, &acc);
-    const double loss = s.loss;
-    if (p.kind == 0) {
+    weighted_f1_accuracy(tagged ? conf : s.conf, K_, &f1, &acc);
+    const double loss = tagged ? tloss : s.loss;
+    if ((p.kind & 1) == 0) {
       if (wlog_) wlog_->log_worker((int64_t)ts, p.partition, p.vc, loss, f1, acc, p.nseen);
     } else {
       if (slog_) slog_->log_server((int64_t)ts, p.vc, f1, acc);
@@ -136,7 +160,7 @@ void MetricsSink::run() {
     {
       std::lock_guard<std::mutex> lk(mu_);
       if (keep_) {
-        if (p.kind == 0)
+        if ((p.kind & 1) == 0)
           wrows_.push_back(WorkerRow{ts, p.partition, p.vc, loss, f1, acc, p.nseen});
         else
           srows_.push_back(ServerRow{ts, p.vc, f1, acc});

@@ -68,7 +68,7 @@ class MetricsSink {
   uintptr_t slot_address(int slot) const;
   // n slots at once (one lock; blocks until n are free, n <= nslots).
   void acquire_many(int n, int* slots, uint64_t* seqs);
-  // kind 0 = worker row, 1 = server row.
+  // kind 0 = worker row, 1 = server row (| kSinkTagged: tagged-chunk payload).
   void submit(int slot, uint64_t seq, int kind, int64_t ts, int64_t partition, int64_t vc, int64_t nseen);
   // n records in order, one lock and one wake-up of the logger thread (a round of
   // the lanes loop hands over up to 9 rows)
@@ -88,6 +88,8 @@ class MetricsSink {
     int64_t ts, partition, vc, nseen;
   };
   void run();
+  // a kSinkTagged slot complete for `seq`: counts -> conf16 [16][16], loss
+  bool read_tagged(const EvalSlot& s, uint64_t seq, int32_t* conf16, float* loss) const;
   EvalSlot* slots_;
   int nslots_, K_;
   CsvLogger *wlog_, *slog_;

@@ -1,0 +1,496 @@
+// Asynchronous (SSP / ASP) multi-lane kernel: ONE persistent launch in which
+// every lane (logical worker, one XCD each) loops
+//
+//   release record (host) -> stage + solve -> push (ticket, serial slice
+//   updates, snapshot, token) -> evaluation of its local model (+ the global
+//   model on the logging lane) -> next release record
+//
+// See lanes_kernels.h for the protocol.  Reference: ServerProcessor.java:143-183
+// (apply on arrival, one partition = serial updates, server row on worker-0
+// deltas, reply to whom the tracker releases), WorkerTrainingProcessor.java:
+// 63-98 (pull -> train on the buffer -> log -> push), MessageTracker.java:69-87.
+#include <cstdlib>
+
+#include "lanes_body.h"
+#include "lanes_kernels.h"
+#include "solve_body.h"
+
+namespace psx {
+namespace {
+using namespace lanes_detail;
+
+// system-coherent 16-B accesses of pinned host memory (sc0 | sc1)
+constexpr int kAuxSys = 17;
+__device__ __forceinline__ TagChunk ld_sys_chunk(const void* base, unsigned bytes, unsigned off) {
+  return __builtin_bit_cast(TagChunk,
+                            __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base, bytes), (int)off, 0, kAuxSys));
+}
+__device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigned off, TagChunk v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
+}
+__device__ __forceinline__ TagChunk ld_nt_chunk(const void* p) {
+  return __builtin_bit_cast(TagChunk, __builtin_nontemporal_load((const u32x4*)p));
+}
+
+// The lane's leader waits for its next release record (pinned, written by the
+// host loop); wave 0's lanes 0..7 load one 16-B chunk each per poll, so one
+// PCIe round trip sees the whole record.  The record goes to the lane's
+// broadcast area (its XCD's L2); a timeout becomes a stop record (code 2).
+// A record is complete when its 8 chunks carry one tag; it is new when that tag
+// is at least the one the lane expects (a stop record written over an unread
+// release on the host's error path is newer still).
+__device__ __forceinline__ void leader_wait_release(const AsyncLaneDev& A, unsigned want, int spin_max,
+                                                    unsigned long long* err_host) {
+  const int tid = threadIdx.x;
+  if (tid >= 64) return;
+  TagChunk c = TagChunk{0, 0, 0, 0};
+  bool ok = false;
+  for (int spins = 0;; ++spins) {
+    if (tid < kRelChunks) c = ld_sys_chunk(A.rel, (unsigned)sizeof(AsyncRelease), (unsigned)tid * 16u);
+    const unsigned t0 = __shfl(c.tag, 0, 64);
+    ok = __all(tid >= kRelChunks || c.tag == t0) && (int)(t0 - want) >= 0;
+    if (ok || spins >= spin_max) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (!ok) {  // the host never answered: leave the launch, and say so
+    c = TagChunk{want, tid == 0 ? 2u : 0u, 0u, 0u};
+    if (tid == 0 && err_host)
+      __hip_atomic_store(err_host, (unsigned long long)7, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid < kRelChunks) ((TagChunk*)A.rec)[tid] = c;
+}
+
+// The update of slice `wg` by the delta of ticket t, after slice wg of ticket
+// t - 1 (serial per slice, in ticket order: the single GRADIENTS_TOPIC
+// partition), w += lr * delta (ServerProcessor.java:148-151, 225-228).  The new
+// slice also goes to snapshot slot t % R (the weights a release after ticket t
+// pulls) and, on the logging lane, to the server-row evaluation fragments.
+template <int FP>
+__device__ __forceinline__ void async_apply_slice(const SolverCfg& cfg, const SolveDev& dv, const AsyncLaneDev& A,
+                                                  const AsyncArgs& a, int wg, unsigned long long t, bool logl,
+                                                  unsigned long long* err, int spin, int* flag) {
+  const int tid = threadIdx.x, K = cfg.K, P = cfg.P;
+  const int c = tid >> 5, f = wg * 32 + (tid & 31);
+  const bool coef = c < K;
+  const bool icpt = wg == 0 && tid < K;
+  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
+  // a solve whose cross-workgroup wait timed out contributes nothing (its loss is NaN)
+  const bool bad = xload(err) != 0ull;
+  float dl = 0.f, di = 0.f;
+  if (coef && !bad) dl = ld_sc1(dv.delta + e);
+  if (icpt && !bad) di = ld_sc1(dv.delta + ei);
+  unsigned long long* turn = a.turn + (size_t)wg * 32;
+  if (tid == 0) {
+    int spins = 0;
+    while (xload(turn) + 1ull != t) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > spin) {  // never expected: record and go on
+        xstore(err, 6ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const size_t so = (size_t)(t % (unsigned long long)a.R) * P;
+  if (coef) {
+    const float nw = ld_sc1(a.w + e) + a.lr * dl;
+    st_sc1(a.w + e, nw);
+    st_sc1(a.snap + so + e, nw);
+    if (logl) write_frag(A.shi, A.slo, c, f, f < cfg.F ? nw : 0.f);
+  }
+  if (icpt) {
+    const float nw = ld_sc1(a.w + ei) + a.lr * di;
+    st_sc1(a.w + ei, nw);
+    st_sc1(a.snap + so + ei, nw);
+    if (logl) A.sb[tid] = nw;
+  }
+  if (tid == 0)
+    __hip_atomic_store(a.snap_tag + (size_t)(t % (unsigned long long)a.R) * (FP / 32) + wg, (unsigned)t,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) xstore(turn, t);
+  (void)flag;
+}
+
+// The lane's evaluation after its push: its local model (worker row,
+// LogisticRegressionTaskSpark.java:186) paired with, on the logging lane, the
+// global model right after this update (server row, ServerProcessor.java:
+// 154-165) -- one pass over the test tiles wg, wg + 32, ... by each of the
+// lane's workgroups; counts folded into the lane's accumulators; the last
+// workgroup publishes tagged chunks (no store-completion wait).
+template <int FP>
+__device__ __forceinline__ void async_lane_eval(char* lds, const SolverCfg& cfg, const SolveDev& dv,
+                                                const AsyncLaneDev& A, const AsyncArgs& a, const RelRec& q, int wg,
+                                                bool srow) {
+  const int tid = threadIdx.x, K = cfg.K, T = a.T;
+  const bool wrow = q.slot_w != 0ull;
+  srow = srow && q.slot_s != 0ull;
+  if (!wrow && !srow) return;  // (uniform)
+  char* red_base = lds + 32 * FP * 2;
+  int* cl = (int*)(red_base + 8192);  // [2][256]
+  int* lastp = cl + 512;
+  float* bl = (float*)(lastp + 4);    // [16]: local model 0..7, global model 8..15
+  cl[tid] = 0;
+  cl[256 + tid] = 0;
+  WFrag<FP> wf;
+  {  // fragments of both models (written this iteration on this XCD: nt loads)
+    const int lane = tid & 63, w = tid >> 6, col = lane & 15, cc = col & 7;
+    const bool live = cc < K && (col < 8 ? wrow : srow);
+    const uint16_t* fh = col < 8 ? dv.out_hi : A.shi;
+    const uint16_t* fo = col < 8 ? dv.out_lo : A.slo;
+    const auto rh = rsrc_of(fh, 16u * FP * 2u), rl = rsrc_of(fo, 16u * FP * 2u);
+#pragma unroll
+    for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+      const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
+      const unsigned off = (unsigned)((cg * 16 + (live ? cc : 0)) * 8) * 2u;
+      wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (live) {
+        wf.h[kk] = ld_h_b128<2>(rh, off);
+        wf.l[kk] = ld_h_b128<2>(rl, off);
+      }
+    }
+  }
+  if (tid < 16) {
+    const int cc = tid & 7;
+    const bool live = cc < K && (tid < 8 ? wrow : srow);
+    bl[tid] = live ? ld_h<2>((tid < 8 ? dv.b_fin : A.sb) + cc) : 0.f;
+  }
+  const int nT = (T + 31) / 32;
+  TileRegs<FP> tr;
+  if (wg < nT) tr.load(a.Xt, a.yt, wg, T);
+  __syncthreads();
+  for (int tile = wg; tile < nT; tile += kLaneWg) {
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+    tr.store(lds);
+    const int ylab = tr.y;
+    if (tile + kLaneWg < nT) tr.load(a.Xt, a.yt, tile + kLaneWg, T);
+    __syncthreads();
+    f32x4 a0, a1;
+    forward_tile_pre<FP>(lds, wf, a0, a1);
+    store_partial_logits(red_base, a0, a1);
+    __syncthreads();
+    {  // thread (row, model)
+      const int row = tid & 31, h = (tid >> 5) & 1;
+      const int yrow = __shfl(ylab, row, 64);
+      if (tid < 64 && row < nrows && (h == 0 ? wrow : srow)) {
+        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+        int best = 0;
+        float bz = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
+          if (z > bz) {
+            bz = z;
+            best = c;
+          }
+        }
+        atomicAdd(&cl[h * 256 + yl * 16 + best], 1);
+      }
+    }
+    __syncthreads();
+  }
+  for (int m = 0; m < 2; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(A.acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(A.eticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kLaneWg - 1;
+  __syncthreads();
+  if (!*lastp) return;
+  // the last workgroup: the lane's counts -> LDS, then tagged chunks to the pinned slots
+  const int t16 = tid >> 4, p16 = tid & 15;
+  const bool cell = t16 < K && p16 < K;
+  for (int m = 0; m < 2; ++m) {
+    const int v = cell ? __hip_atomic_exchange(A.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                       : 0;
+    if (cell) cl[m * 256 + t16 * K + p16] = v;  // compact [K][K]
+  }
+  const float lv = tid == 0 ? ld_h<2>(dv.loss) : 0.f;
+  if (tid == 0) __hip_atomic_store(A.eticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int nch = 1 + (K * K + 2) / 3;
+  const int m = tid >> 6, i = tid & 63;  // wave 0: the worker row, wave 1: the server row
+  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
+    const unsigned tag = eval_tag(m == 0 ? q.seq_w : q.seq_s);
+    TagChunk ch;
+    if (i == 0) {
+      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (i - 1);
+      auto cv = [&](int c) { return c < K * K ? (unsigned)cl[m * 256 + c] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    st_sys_chunk((void*)(m == 0 ? q.slot_w : q.slot_s), 1088u, (unsigned)i * 16u, ch);
+  }
+}
+
+// A pointer the compiler must treat as new on every loop iteration: the loads
+// through it stay inside the iteration instead of being hoisted in front of the
+// persistent loop (where their values would be live across it -- hundreds of
+// registers of structure fields, spilled).
+template <typename T>
+__device__ __forceinline__ const T* fresh(const T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// One iteration of lane l's loop (workgroup wg): release -> solve -> push ->
+// evaluation.  false: the lane got its stop record.
+template <int FP, int KP, int S>
+__device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg, const AsyncArgs& a,
+                                                const AsyncLaneDev& A, int l, int wg, unsigned& run,
+                                                unsigned long long& relc, unsigned long long& lw) {
+  constexpr int NS = FP / 32;
+  const int tid = threadIdx.x, K = cfg.K;
+  const SolveDev& dv = A.dv;
+  unsigned long long* const xch = dv.xch;
+  unsigned long long* const err = xch + kXchErr;
+  // ---- 1. the release record ----
+  if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.spin_rel, dv.err_host);
+  x_barrier(A.flags, wg, kLaneWg, ++lw, err, a.spin_rel);
+  // the lane's rows, state and the pulled snapshot were written by other CUs
+  // (other XCDs for the snapshot) since this CU last read them
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  RelRec q;
+  {
+    TagChunk ch[kRelChunks];
+#pragma unroll
+    for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(A.rec + 2 * i);
+    unpack_release(ch, q);
+    relc = ch[0].tag;  // the record consumed
+  }
+  if (q.stop) {
+    if (wg == 0 && tid == 0) *A.relc = relc;
+    return false;
+  }
+  // ---- 2. the solve (as lanes_round_kernel) ----
+  {
+    char* lf = lds;
+    char* lb = lds + persist_fwd_bytes(FP);
+    float* lsy = (float*)(lb + (kBwdLdsBytes + 15) / 16 * 16);
+    unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);
+    Ctrl* cl = (Ctrl*)(frl + 1024);
+    const int spin = spin_limit(dv);
+    const SolveParams win{q.r.B, q.r.start, 0, 0};
+    const WinTiles wt(win.start, win.B, cfg.cap);
+    const int ntr = wt.nt < wt.T ? wt.nt : wt.T;
+    const int G = ntr > NS ? ntr : NS;
+    const bool row = wg < ntr, owner = wg < NS;
+    const unsigned rn = run;
+    unsigned long long nb = 0;
+    auto barrier = [&]() {
+      ++nb;
+      if constexpr (S == 2)
+        x_barrier(xch + kXchFlags, wg, G, ((unsigned long long)rn << 16) | nb, err, spin);
+      else
+        p_barrier(xch + kXchGen + (rn & 1u), (unsigned long long)G * nb, err, spin);
+    };
+    if (wg < G) {
+      float wo_pre = 0.f, b_pre = 0.f;
+      if (owner) {  // the pulled weights of this slice: snapshot -> this solve's private copy
+        const int c = tid >> 5, f = wg * 32 + (tid & 31);
+        const size_t so = (size_t)(q.snap % (long long)a.R) * cfg.P;
+        if (c < K && f < cfg.F) wo_pre = a.snap[so + (size_t)c * FP + f];
+        if (wg == 0 && tid < K) b_pre = a.snap[so + (size_t)K * FP + tid];
+        if (c < K) A.wpull[(size_t)c * FP + f] = wo_pre;
+        if (wg == 0 && tid < K) A.wpull[(size_t)K * FP + tid] = b_pre;
+        if (tid == 0 &&
+            a.snap_tag[(size_t)(q.snap % (long long)a.R) * NS + wg] != (unsigned)(unsigned long long)q.snap)
+          xstore(err, 8ull);  // the snapshot slot was reused before this lane pulled it
+      }
+      if (wg == 0 && tid == 0) {
+        xstore(err, 0ull);
+        if constexpr (S == 1) xstore(xch + kXchGen + ((rn + 1u) & 1u), 0ull);
+      }
+      if (row) {
+        const int rt = wt.ring_tile(wg);
+        lane_stage_stats<FP, S>(lf, lsy, cfg, dv, q.r, a.dsX, a.dsy, rt, A.spart + (size_t)wg * FP * 2);
+      }
+      barrier();
+      if (owner) {
+        lane_prep<FP, KP, S>(lb, cfg, dv, A.spart, ntr, win.B, wg, wo_pre, b_pre);
+        if (tid == 0) ctrl_init(*cl);
+      }
+      barrier();
+      const bool inplace = G == NS;
+      int phase = kPhInit;
+      for (int slot = 0; slot < cfg.nslots; ++slot) {
+        if (phase == kPhDone) break;
+        if (row) {
+          constexpr int NT = FP / 64;
+          f32x4 acc[NT];
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
+          fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
+          store_gpf<FP, S == 1>(dv, wg, G, acc);
+        }
+        barrier();
+        if (owner)
+          bwd_body<FP, KP, S>(cfg, win, A.ctrl, slot, dv, G, lb, wg, NS, false, inplace ? 0 : kNoFinSlot,
+                              /*fin_sc1=*/true);
+        if (inplace && cl->phase == kPhDone) {
+          phase = kPhDone;
+          break;
+        }
+        if (wg == 0 && tid == 0) st_h64<S>(xch + kXchPhase, (unsigned long long)(unsigned)cl->phase);
+        barrier();
+        phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
+      }
+      if (owner) {
+        if (!inplace) {
+          FinIn<KP> in;
+          const int f = wg * 32 + tid;
+          if (tid < 32) {
+            in.load_f(cfg, dv, f);
+            finalize_feature<KP>(cfg, dv, f, in, /*sc1_delta=*/true);
+          }
+        }
+        if (wg == 0) {
+          __syncthreads();
+          if (tid == 0) {
+            FinScal sc;
+            sc.load(cfg, cl, dv);
+            sc.store(cfg, dv, /*sc1_delta=*/true, /*clear_err=*/false);
+          }
+          constexpr int CW = sizeof(Ctrl) / 8;
+          for (int k = tid; k < CW; k += 256) ((unsigned long long*)A.ctrl)[k] = ((const unsigned long long*)cl)[k];
+        }
+      }
+    }
+  }
+  ++run;
+  // ---- 3. push: ticket, serial slice updates, snapshot, token ----
+  if (wg == 0 && tid == 0) {
+    if (q.delay_us > 0) {  // injected straggler (tests): the solve "took" delay_us longer
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();  // 100 MHz
+      while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < (long long)q.delay_us * 100)
+        __builtin_amdgcn_s_sleep(64);
+    }
+    const unsigned long long t =
+        __hip_atomic_fetch_add(a.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;
+    *(volatile unsigned long long*)(A.rec + 16) = t;
+  }
+  const int spin = spin_limit(dv);
+  x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
+  const unsigned long long t = ld_h64<2>(A.rec + 16);
+  const bool logl = l == a.log_lane;
+  if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
+  x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
+  if (wg == 0 && tid == 0)
+    st_sys_chunk(a.tok, (unsigned)(a.ring * 16), (unsigned)((t % (unsigned long long)a.ring) * 16ull),
+                 TagChunk{(unsigned)t, (unsigned)l, (unsigned)(unsigned long long)q.vc,
+                          (unsigned)((unsigned long long)q.vc >> 32)});
+  // ---- 4. evaluation of this iteration's models ----
+  async_lane_eval<FP>(lds, cfg, dv, A, a, q, wg, logl);
+  return true;
+}
+
+template <int FP, int KP, int S>
+__global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __restrict__ pk,
+                                                          const AsyncLaneDev* __restrict__ als) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = (int)blockIdx.x, tid = threadIdx.x;
+  int l, wg;
+  {  // roles as lanes_round_kernel: a lane's workgroups claim its XCD's slots; no riders
+    const AsyncArgs& a = pk->a;
+    const int L = a.L;
+    __shared__ int role;
+    if (tid == 0) {
+      unsigned* c = a.claim + 16 * a.cpar;
+      int r = -1;
+      if constexpr (S == 2) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
+        if ((int)xcc < L) {
+          const unsigned k = __hip_atomic_fetch_add(c + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (k < (unsigned)kLaneWg) r = (int)(xcc * kLaneWg + k);
+        }
+      } else if (b < 8 * kLaneWg && (b & 7) < L) {
+        r = (b & 7) * kLaneWg + (b >> 3);
+      }
+      if (b == 0)
+        for (int j = 0; j < 16; ++j)
+          __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      role = r;
+    }
+    __syncthreads();
+    const int r = role;
+    __syncthreads();
+    if (r < 0) return;
+    l = r / kLaneWg;
+    wg = r - l * kLaneWg;
+  }
+  unsigned run = *als[l].dv.prm_count;           // solves so far (kernel entry: coherent)
+  unsigned long long relc = *als[l].relc;        // release records consumed so far
+  unsigned long long lw = (unsigned long long)pk->a.launch << 40;  // lane-wide barrier words
+  for (;;) {
+    const AsyncPack* p = fresh(pk);
+    const AsyncLaneDev* A = fresh(als + l);
+    if (!async_iteration<FP, KP, S>(lds, p->cfg, p->a, *A, l, wg, run, relc, lw)) return;
+  }
+}
+
+__global__ void async_init_kernel(const float* __restrict__ w, float* snap, unsigned* snap_tag,
+                                  unsigned long long* turn, unsigned long long* ticket, int P, int NS, int R,
+                                  unsigned long long t) {
+  const size_t so = (size_t)(t % (unsigned long long)R) * P;
+  for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < P; i += (int)(gridDim.x * blockDim.x))
+    snap[so + i] = w[i];
+  if (blockIdx.x == 0) {
+    for (int s = threadIdx.x; s < NS; s += blockDim.x) {
+      snap_tag[(size_t)(t % (unsigned long long)R) * NS + s] = (unsigned)t;
+      turn[(size_t)s * 32] = t;
+    }
+    if (threadIdx.x == 0) *ticket = t;
+  }
+}
+
+template <int FP, int KP, int S>
+void launch_afks(const AsyncPack* pk, const AsyncLaneDev* al, hipStream_t s) {
+  static const bool prepared = ((void)hipFuncSetAttribute((const void*)lanes_async_kernel<FP, KP, S>,
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                          (int)lanes_lds_bytes(FP)),
+                                true);
+  (void)prepared;
+  lanes_async_kernel<FP, KP, S><<<8 * kLaneWg, 256, lanes_lds_bytes(FP), s>>>(pk, al);
+}
+
+template <int FP, int KP>
+void launch_afk(const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+  if (S == 2)
+    launch_afks<FP, KP, 2>(pk, al, s);
+  else
+    launch_afks<FP, KP, 1>(pk, al, s);
+}
+
+template <int FP>
+void launch_af(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+  const int KP = padded_classes(cfg.K);
+  if (KP <= 2)
+    launch_afk<FP, 2>(pk, al, S, s);
+  else if (KP <= 4)
+    launch_afk<FP, 4>(pk, al, S, s);
+  else
+    launch_afk<FP, 8>(pk, al, S, s);
+}
+
+}  // namespace
+
+void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long long t, hipStream_t s) {
+  async_init_kernel<<<8, 256, 0, s>>>(a.w, a.snap, a.snap_tag, a.turn, a.ticket, cfg.P, cfg.Fp / 32, a.R, t);
+}
+
+void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+  switch (cfg.Fp) {
+    case 128: launch_af<128>(cfg, pk, al, S, s); break;
+    case 256: launch_af<256>(cfg, pk, al, S, s); break;
+    case 512: launch_af<512>(cfg, pk, al, S, s); break;
+    case 1024: launch_af<1024>(cfg, pk, al, S, s); break;
+    default: break;
+  }
+}
+
+}  // namespace psx

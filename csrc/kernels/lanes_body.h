@@ -1,0 +1,381 @@
+// Device bodies shared by the multi-lane round kernels (gfx950):
+// lanes_kernels.hip (BSP: one launch per round) and lanes_async.hip (SSP / ASP:
+// one persistent launch that serves many releases).  Phase I of a lane's solve
+// (staging + ingest + window statistics, x0 / first trial point) and the
+// test-set evaluation helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "lanes_kernels.h"
+#include "solve_body.h"
+
+namespace psx {
+namespace lanes_detail {
+
+// Element i of a kernel-argument array with a workgroup-uniform runtime index:
+// a switch over constant indices keeps every access a scalar load from the
+// kernarg segment (a dynamic index would copy the whole argument struct into
+// scratch memory, per lane, at kernel entry).
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&arr)[N], int i) {
+  T v = arr[0];
+#pragma unroll
+  for (int j = 1; j < N; ++j)
+    if (i == j) v = arr[j];
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Riders: evaluation of up to kMaxEvalModels models (the previous round's
+// local models and global model) over the test tiles.  Work items = (model
+// pair, test tile), pair-major, dealt to the riders in contiguous chunks so that
+// a rider keeps one pair's fragments in registers across its tiles.  Every
+// rider arrives on the ticket once; the last one publishes every model's
+// counts (and its loss) into its pinned slot, then the sequence number.
+template <int FP>
+__device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel* ma, const EvalModel* mb, int K) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, c = col & 7;
+  const EvalModel* m = col < 8 ? ma : mb;
+  const bool live = m != nullptr && c < K;
+#pragma unroll
+  for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+    const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
+    const size_t fo = ((size_t)cg * 16 + (live ? m->coff + c : 0)) * 8;
+    wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      wf.h[kk] = *(const u16x8*)(m->hi + fo);
+      wf.l[kk] = *(const u16x8*)(m->lo + fo);
+    }
+  }
+}
+
+// The last arriving workgroup publishes every model's counts into its pinned slot
+// (see eval_body.h): all M accumulator exchanges (and the losses) are issued
+// before the first system-scope store, so they cost one L2 round trip instead of M
+// dependent ones; then the drain, the ticket reset and the sequence numbers.
+__device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid) {
+  int tot[kMaxEvalModels];
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)
+    tot[m] = m < M ? __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                   : 0;
+  float lv = 0.f;
+  if (tid < M) {
+    const EvalModel E = pick(ev.m, tid);
+    lv = E.loss ? *E.loss : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)
+    if (m < M) __hip_atomic_store((int*)pick(ev.m, m).slot + tid, tot[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < M) __hip_atomic_store((float*)(pick(ev.m, tid).slot + 1024), lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < M)
+    __hip_atomic_store((unsigned long long*)(pick(ev.m, tid).slot + 1032), pick(ev.m, tid).seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A 32-row test tile held in registers (stage_tile's loads, split from its LDS
+// stores so that the next tile's loads fly while the current one is evaluated).
+template <int FP>
+struct TileRegs {
+  static constexpr int CPR = FP / 8, PER_T = 32 * CPR / 256;
+  u16x8 v[PER_T];
+  int y;
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ X, const int32_t* __restrict__ yt, int tile,
+                                       int T) {
+    const int64_t row0 = (int64_t)tile * 32;
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int q = threadIdx.x + 256 * j;
+      const int row = q / CPR, cg = q - row * CPR;
+      v[j] = row < nrows ? *(const u16x8*)(X + (row0 + row) * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    y = (int)threadIdx.x < nrows ? yt[row0 + threadIdx.x] : 0;
+  }
+  __device__ __forceinline__ void store(char* lds) const {  // stage_tile's LDS layout
+#pragma unroll
+    for (int j = 0; j < PER_T; ++j) {
+      const int q = threadIdx.x + 256 * j;
+      const int row = q / CPR, cg = q - row * CPR;
+      *(u16x8*)(lds + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+    }
+  }
+};
+
+template <int FP>
+__device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, int rid, int nride) {
+  if (ev.nmodels <= 0 || rid >= nride) return;
+  long long* dbg = ev.dbg;
+  auto rstamp = [&](int k) {
+    if (dbg && threadIdx.x == 0) dbg[k] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  if (dbg && threadIdx.x == 0) {
+    const long long t = (long long)__builtin_amdgcn_s_memrealtime();
+    atomicMin((unsigned long long*)(dbg + 12), (unsigned long long)t);
+    atomicMax((unsigned long long*)(dbg + 13), (unsigned long long)t);
+  }
+  if (rid == 0) rstamp(0);
+  char* red_base = lds + 32 * FP * 2;
+  int* cl = (int*)(red_base + 8192);  // [kMaxEvalModels][256]
+  int* lastp = cl + kMaxEvalModels * 256;
+  float* bl = (float*)(lastp + 4);  // [16]: the current pair's intercepts (model A: 0..7, B: 8..15)
+  const int tid = threadIdx.x, K = ev.K, T = ev.T, M = ev.nmodels;
+  const int nT = (T + 31) / 32, npairs = (M + 1) / 2;
+  for (int m = 0; m < M; ++m) cl[m * 256 + tid] = 0;
+  const int items = npairs * nT, chunk = (items + nride - 1) / nride;
+  const int i0 = rid * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
+  int curp = -1;
+  WFrag<FP> wf;
+  TileRegs<FP> tr;  // the next item's tile, in flight during the current item
+  if (i0 < i1) tr.load(ev.Xt, ev.yt, i0 % nT, T);
+  __syncthreads();
+  for (int it = i0; it < i1; ++it) {
+    const int p = it / nT, tile = it - p * nT;
+    const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
+    const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
+    if (p != curp) {  // (workgroup-uniform)
+      load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
+      if (tid < 16) {  // the intercepts into LDS once per pair, not a global load per class and row
+        const int h = tid >> 3, c = tid & 7;
+        const float* bp = h == 0 ? A.b + A.coff : Bm.b + Bm.coff;
+        bl[tid] = (c < K && (h == 0 || mb >= 0)) ? bp[c] : 0.f;
+      }
+      curp = p;
+    }
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+    tr.store(lds);
+    const int ylab = tr.y;
+    if (it + 1 < i1) tr.load(ev.Xt, ev.yt, (it + 1) % nT, T);
+    __syncthreads();
+    if (rid == 0 && it == i0) rstamp(1);
+    f32x4 a0, a1;
+    forward_tile_pre<FP>(lds, wf, a0, a1);
+    store_partial_logits(red_base, a0, a1);
+    __syncthreads();
+    {  // thread (row, model): rows 0..31 x models {A, B} -- both models' argmax at once
+      const int row = tid & 31, h = (tid >> 5) & 1;
+      const int yrow = __shfl(ylab, row, 64);  // the row's label (held by thread `row` of wave 0)
+      if (tid < 64 && row < nrows && (h == 0 || mb >= 0)) {
+        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+        int best = 0;
+        float bz = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
+          if (z > bz) {
+            bz = z;
+            best = c;
+          }
+        }
+        atomicAdd(&cl[(h == 0 ? ma : mb) * 256 + yl * 16 + best], 1);
+      }
+    }
+    __syncthreads();
+    if (rid == 0 && it - i0 < 4) rstamp(2 + (it - i0));
+  }
+  __syncthreads();
+  for (int m = 0; m < M; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(ev.acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (rid == 0) rstamp(8);
+  if (dbg && tid == 0)
+    atomicMax((unsigned long long*)(dbg + 14), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ev.nticket - 1;
+  __syncthreads();
+  if (!*lastp) return;
+  rstamp(10);
+  publish_counts(ev, M, tid);
+  rstamp(11);
+}
+
+// ---------------------------------------------------------------------------
+// Phase I of a lane's solve, row role: stage ring tile `rt` into the LDS image,
+// the round's new rows straight from the dataset (also written into the ring),
+// and publish the tile's column sums / sums of squares over its window rows.
+// Thread t holds chunk cg = t % CPR (8 features) of rows g + NG j (g = t / CPR),
+// so the sums come from the staging registers; the NG row groups are combined
+// in LDS (fixed order).
+template <int FP, int S>
+__device__ __forceinline__ void lane_stage_stats(char* lf, float* scratch, const SolverCfg& cfg, const SolveDev& dv,
+                                                 const LaneRound& r, const uint16_t* dsX, const int32_t* dsy, int rt,
+                                                 float* spart_wg) {
+  constexpr int CPR = FP / 8, NG = 256 / CPR, PER_T = 32 * CPR / 256;
+  const int tid = threadIdx.x, cap = cfg.cap;
+  const int cg = tid % CPR, g = tid / CPR;
+  uint16_t* X = const_cast<uint16_t*>(dv.X);
+  int32_t* Y = const_cast<int32_t*>(dv.y);
+  // labels travel with the first loads
+  int yv = 0;
+  bool ynew = false;
+  // the dataset row of ring slot s when it holds one of this round's new rows, else -1
+  auto new_src = [&](int s) -> long long {
+    int dn = s - r.dst;
+    if (dn < 0) dn += cap;
+    if (dn < r.n) return r.first + (long long)dn * r.step;
+    if (dn - r.n < r.n2) return r.first2 + (long long)(dn - r.n) * r.step;
+    return -1;
+  };
+  if (tid < 32) {
+    const int s = rt * 32 + tid;
+    const long long src = new_src(s);
+    ynew = src >= 0;
+    yv = ynew ? dsy[src] : dv.y[s];
+  }
+  u16x8 v[PER_T];
+  bool isnew[PER_T], valid[PER_T];
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int row = g + NG * j, s = rt * 32 + row;
+    const long long sr = new_src(s);
+    isnew[j] = sr >= 0;
+    int dw = s - r.start;
+    if (dw < 0) dw += cap;
+    valid[j] = dw < r.B;
+    const uint16_t* src = isnew[j] ? dsX + (size_t)sr * FP : dv.X + (size_t)s * FP;
+    v[j] = *(const u16x8*)(src + cg * 8);
+  }
+  float sm[8], sq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sm[e] = sq[e] = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int row = g + NG * j, s = rt * 32 + row;
+    *(u16x8*)(lf + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+    if (isnew[j]) *(u16x8*)(X + (size_t)s * FP + cg * 8) = v[j];  // the ring keeps the new row
+    if (valid[j]) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = bf2f(v[j][e]);
+        sm[e] += x;
+        sq[e] += x * x;
+      }
+    }
+  }
+  if (tid < 32) {
+    ((int*)(lf + 32 * FP * 2 + 8192 + 2048))[tid] = yv;  // fwd_body's label slots
+    if (ynew) Y[rt * 32 + tid] = yv;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    scratch[(g * CPR + cg) * 16 + e] = sm[e];
+    scratch[(g * CPR + cg) * 16 + 8 + e] = sq[e];
+  }
+  __syncthreads();
+  if (tid < CPR) {
+    float a[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) a[e] = 0.f;
+    for (int gg = 0; gg < NG; ++gg)  // fixed order
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a[e] += scratch[(gg * CPR + tid) * 16 + e];
+    // 8 features x (sum, sum of squares) = 64 contiguous bytes of spart[wg][f][2]
+    const auto rs = rsrc_of(spart_wg, (unsigned)(FP * 2 * 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 o = f32x4{a[2 * q], a[8 + 2 * q], a[2 * q + 1], a[8 + 2 * q + 1]};
+      st_h_b128<S>(rs, (unsigned)((tid * 8 + 2 * q) * 2 * 4), __builtin_bit_cast(u16x8, o));
+    }
+  }
+}
+
+// Phase I, slice role: the window statistics of features [fs, fs + 32) from the
+// row workgroups' partials, then x0 = w_old * std (Spark standardisation), the
+// solver vectors and the first trial point's fragments (as prep_epilogue).
+template <int FP, int KP, int S>
+__device__ __forceinline__ void lane_prep(char* lb, const SolverCfg& cfg, const SolveDev& dv, const float* spart,
+                                          int ntr, int B, int wg, float wo_pre, float b_pre) {
+  constexpr int FPI = FP > 256 ? FP : 256;
+  const int tid = threadIdx.x, fl = tid & 31, grp = tid >> 5, fs = wg * 32, K = cfg.K;
+  double* red = (double*)lb;                  // [8 groups][32][2]
+  float* sdl = (float*)(red + 8 * 32 * 2);    // [32]
+  float* ivl = sdl + 32;                      // [32]
+  unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);  // [2][512] (bwd_body's staging)
+  double s = 0.0, q = 0.0;
+  {  // the (<= 4) row tiles' partials of this thread all in flight, then summed in tile order
+    constexpr int NPT = (kLaneWg + 7) / 8;
+    double pv[NPT];
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int gg = grp + 8 * i;
+      pv[i] = gg < ntr ? ld_h<S>((const double*)(spart + ((size_t)gg * FP + fs + fl) * 2)) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i)
+      if (grp + 8 * i < ntr) {
+        const float2 u = __builtin_bit_cast(float2, pv[i]);
+        s += (double)u.x;
+        q += (double)u.y;
+      }
+  }
+  red[(grp * 32 + fl) * 2] = s;
+  red[(grp * 32 + fl) * 2 + 1] = q;
+  if (tid < 128) *(u16x8*)(frl + tid * 8) = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  __syncthreads();
+  if (tid < 32) {
+    double a = 0.0, b = 0.0;
+    for (int gg = 0; gg < 8; ++gg) {
+      a += red[(gg * 32 + tid) * 2];
+      b += red[(gg * 32 + tid) * 2 + 1];
+    }
+    const int f = fs + tid;
+    const double n = (double)B;
+    double sd = 0.0;
+    if (f < cfg.F && n > 1.0) {
+      const double mean = a / n;
+      const double var = (b - n * mean * mean) / (n - 1.0);
+      sd = var > 0.0 ? sqrt(var) : 0.0;
+    }
+    const float sdf = (float)sd, inv = sd > 0.0 ? (float)(1.0 / sd) : 0.f;
+    sdl[tid] = sdf;
+    ivl[tid] = inv;
+    dv.std_[f] = sdf;
+    dv.inv_std[f] = inv;
+  }
+  __syncthreads();
+  {  // element (c = tid / 32, feature fs + fl): x0, d, g_c, wfix, trial fragment
+    const int c = grp;
+    if (c < KP) {
+      const int f = fs + fl, pi = c * FPI + f;
+      const float xv = wo_pre * sdl[fl];
+      dv.x[pi] = xv;
+      dv.d[pi] = 0.f;
+      dv.g_c[pi] = 0.f;
+      const float fix = (sdl[fl] > 0.f || cfg.zero_const) ? 0.f : wo_pre;
+      dv.wfix[pi] = fix;
+      unsigned short h, l;
+      split_bf16(xv * ivl[fl] + fix, h, l);
+      const int o = (fl >> 3) * 128 + c * 8 + (fl & 7);
+      frl[o] = h;
+      frl[512 + o] = l;
+    }
+  }
+  if (wg == 0 && tid < 16) {  // intercepts: x0 = the pulled intercepts (not standardised)
+    const int pi = KP * FPI + tid;
+    dv.x[pi] = b_pre;
+    dv.d[pi] = 0.f;
+    dv.g_c[pi] = 0.f;
+    st_h<S>(dv.b_eff + tid, b_pre);
+  }
+  (void)K;
+  __syncthreads();
+  if (tid < 128) {  // this slice of the trial fragments: 16-B hand-off stores (wave 0 hi, wave 1 lo)
+    const size_t go = (size_t)(fs >> 3) * 128 + (tid & 63) * 8;
+    const u16x8 vv = *(const u16x8*)(frl + tid * 8);
+    if (tid < 64)
+      st_h_b128<S>(rsrc_of(dv.whi, 16u * FP * 2u), (unsigned)(go * 2), vv);
+    else
+      st_h_b128<S>(rsrc_of(dv.wlo, 16u * FP * 2u), (unsigned)(go * 2), vv);
+  }
+}
+
+}  // namespace lanes_detail
+}  // namespace psx

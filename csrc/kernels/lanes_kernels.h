@@ -130,4 +130,137 @@ void launch_xcc_probe(int* ids, int n, hipStream_t s);
 int lanes_eval_grid();
 void launch_lanes_eval(const SolverCfg& cfg, const EvalMulti& ev, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Asynchronous consistency (SSP / ASP) on one GPU: ONE persistent launch in
+// which every lane loops release -> solve -> push -> evaluate (lanes_async.hip).
+//
+// Reference: ServerProcessor.process (ServerProcessor.java:143-183) applies each
+// gradient on arrival -- GRADIENTS_TOPIC has ONE partition, so updates are
+// serial in arrival order -- and answers the workers MessageTracker releases
+// (MessageTracker.java:69-87) with the weights right after that update.
+// MI355X mapping:
+//   * arrival order = a device ticket taken when a lane's delta is final; slice
+//     s of the update of ticket t waits until slice s of ticket t - 1 is applied
+//     (per-slice turn words), so updates are serial per slice and pipelined
+//     across slices; each applied slice is also written to snapshot slot t % R
+//     (the weights "right after the update" a release refers to);
+//   * the tracker decision stays on the HOST (the C++ VectorClockTracker): a
+//     lane publishes a token (ticket, lane, vc) into a pinned ring once all its
+//     slices are applied; the host loop consumes tokens in ticket order, runs
+//     on_delta, and answers each released lane with a release record (pinned,
+//     polled by the lane's leader): its clock, the snapshot ticket, its window
+//     and new stream rows, the metrics slots of its rows;
+//   * a lane evaluates its local model (the worker row) -- paired with the
+//     global model after its own update on the logging lane (the server row) --
+//     with its own 32 workgroups right after its push, and publishes the counts
+//     as tagged 16-B chunks (no store-completion wait on the lane's path).
+// Host <-> device records are 16-B chunks {tag, 3 x u32 payload}: a chunk is
+// written by ONE 16-B store, so a reader that sees every chunk carry the
+// expected tag has the whole record, without ordering between the stores.
+struct alignas(16) TagChunk {
+  unsigned tag, a, b, c;
+};
+constexpr int kRelChunks = 8;
+struct alignas(16) AsyncRelease {  // host -> lane (pinned), tag = the lane's record count
+  TagChunk ch[kRelChunks];
+};
+// release record payload (unpacked on both sides by the same layout)
+struct RelRec {
+  int stop;              // 1: leave the launch (no solve)
+  long long vc;          // the pulled weights' version (tracker clock)
+  long long snap;        // ticket whose snapshot holds the pulled weights
+  LaneRound r;           // window + this solve's new stream rows
+  unsigned long long slot_w, slot_s;  // pinned EvalSlot addresses (0: no row)
+  unsigned seq_w, seq_s;              // their sequence numbers (low 32 bits)
+  int delay_us;          // injected straggler delay before the push (tests)
+};
+PSX_HD inline void pack_release(const RelRec& q, unsigned tag, TagChunk* ch) {
+  auto lo = [](long long v) { return (unsigned)(unsigned long long)v; };
+  auto hi = [](long long v) { return (unsigned)((unsigned long long)v >> 32); };
+  ch[0] = TagChunk{tag, (unsigned)q.stop, lo(q.vc), hi(q.vc)};
+  ch[1] = TagChunk{tag, lo(q.snap), hi(q.snap), (unsigned)q.r.B};
+  ch[2] = TagChunk{tag, (unsigned)q.r.start, (unsigned)q.r.n, (unsigned)q.r.dst};
+  ch[3] = TagChunk{tag, lo(q.r.first), hi(q.r.first), (unsigned)q.r.n2};
+  ch[4] = TagChunk{tag, lo(q.r.step), hi(q.r.step), lo(q.r.first2)};
+  ch[5] = TagChunk{tag, hi(q.r.first2), lo((long long)q.slot_w), hi((long long)q.slot_w)};
+  ch[6] = TagChunk{tag, q.seq_w, lo((long long)q.slot_s), hi((long long)q.slot_s)};
+  ch[7] = TagChunk{tag, q.seq_s, (unsigned)q.delay_us, 0u};
+}
+PSX_HD inline void unpack_release(const TagChunk* ch, RelRec& q) {
+  auto j = [](unsigned l, unsigned h) { return (long long)(((unsigned long long)h << 32) | l); };
+  q.stop = (int)ch[0].a;
+  q.vc = j(ch[0].b, ch[0].c);
+  q.snap = j(ch[1].a, ch[1].b);
+  q.r.B = (int)ch[1].c;
+  q.r.start = (int)ch[2].a;
+  q.r.n = (int)ch[2].b;
+  q.r.dst = (int)ch[2].c;
+  q.r.first = j(ch[3].a, ch[3].b);
+  q.r.n2 = (int)ch[3].c;
+  q.r.step = j(ch[4].a, ch[4].b);
+  q.r.first2 = j(ch[4].c, ch[5].a);
+  q.slot_w = (unsigned long long)j(ch[5].b, ch[5].c);
+  q.seq_w = ch[6].a;
+  q.slot_s = (unsigned long long)j(ch[6].b, ch[6].c);
+  q.seq_s = ch[7].a;
+  q.delay_us = (int)ch[7].b;
+  q.r.pad = 0;
+}
+// token: lane -> host (pinned ring, slot t % ring): {tag = ticket (low 32 bits,
+// tickets start at 1), lane, vc low, vc high}
+typedef TagChunk AsyncToken;
+// the tag of a tagged evaluation slot's chunks (never 0)
+PSX_HD inline unsigned eval_tag(unsigned long long seq) { return (unsigned)seq | 0x80000000u; }
+
+// Per-lane device state of the asynchronous launch (a device table prepared by
+// the host: the kernel reads it through a pointer it re-loads every iteration).
+struct AsyncLaneDev {
+  SolveDev dv;           // the lane's solver (LaneDev::dv with the buffers of this launch's mode)
+  float* spart;          // LaneDev::spart
+  Ctrl* ctrl;            // LaneDev::ctrl
+  float* wpull;          // [P] the pulled weights of the current solve (copied from the snapshot)
+  uint16_t *shi, *slo;   // server fragments of the logging lane's update (columns 0..K-1)
+  float* sb;             // [16]
+  int* acc;              // [2 models][256][kAccStride] evaluation accumulators (zero between solves)
+  unsigned* eticket;     // evaluation arrivals
+  unsigned long long* flags;  // [kLaneWg][32] lane-wide barrier words (own 256-B line each)
+  unsigned long long* rec;    // [kRelChunks * 2] the release record broadcast (+ the ticket at [16])
+  unsigned long long* relc;   // release records consumed by this lane (persists across launches)
+  AsyncRelease* rel;     // pinned release record (host -> device)
+};
+
+struct AsyncArgs {
+  int L;
+  const uint16_t* dsX;  // resident dataset [rows][FP] bf16
+  const int32_t* dsy;
+  float* w;             // server master weights [P]
+  float lr;
+  float* snap;          // [R][P] w after ticket t at slot t % R
+  unsigned* snap_tag;   // [R][FP/32] ticket of each slot's slices (sanity check)
+  int R;
+  unsigned long long* ticket;  // last ticket handed out (device counter)
+  unsigned long long* turn;    // [FP/32][32] last ticket applied to slice s (own 256-B line each)
+  AsyncToken* tok;             // pinned token ring
+  int ring;
+  const uint16_t* Xt;  // test set
+  const int32_t* yt;
+  int T;
+  int log_lane;        // lane whose deltas produce server rows (-1: none)
+  long long launch;    // launch number (> every earlier one): lane-wide barrier words
+  int spin_rel;        // release wait budget (polls)
+  unsigned* claim;     // [2][16] role claim counters
+  int cpar;
+};
+
+// The launch's uniform arguments, in device memory (see AsyncLaneDev).
+struct AsyncPack {
+  SolverCfg cfg;
+  AsyncArgs a;
+};
+
+// Initialise the snapshot slot of ticket t (= w) and the slices' turn words (t).
+void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long long t, hipStream_t s);
+// pk: device copy of {cfg, a} (a.launch / a.cpar of THIS launch); al: device table [L]
+void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s);
+
 }  // namespace psx

@@ -80,6 +80,11 @@ struct LanesLoopCfg {
   int new_rows = 0;
   double new_frac = 0.0;
   int new_cap = 0;
+  // asynchronous consistency (run_async): the worker whose deltas produce the
+  // server rows (ServerProcessor.java:154: worker 0, or the lowest live one;
+  // -1: none) and injected straggler delays per lane (us, tests / fault injection)
+  int log_worker = 0;
+  std::vector<int> delay_us;
 };
 
 class LanesLoop {
@@ -96,6 +101,18 @@ class LanesLoop {
   // still waiting for rows or for the cadence at that time is not run (the call
   // returns the rounds run so far) -- the wall-clock stop of a producer-clock run.
   int64_t run(int64_t rounds, int64_t r0, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
+  // Asynchronous consistency (SSP / ASP, the tracker's model): ONE persistent
+  // launch (lanes_async.hip) serves `updates` solves.  The lanes the tracker has
+  // dispatched start at once; every token (ticket, lane, vc) a lane pushes is
+  // consumed here in ticket order -- its rows to the metrics sink,
+  // tracker.on_delta, a release record (window, new rows, snapshot, slots) for
+  // every released lane -- until `updates` solves ran (or the streams ended /
+  // the deadline passed); then every lane gets a stop record and the launch
+  // drains.  Releases not yet started carry over to the next call.  Returns the
+  // updates applied.
+  int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
+  int64_t tickets() const { return (int64_t)aticket_; }  // deltas applied by the asynchronous loop so far
+  double host_us_per_update() const { return async_updates_ ? async_ns_ / 1000.0 / (double)async_updates_ : 0.0; }
   // Evaluate the last round's rows (one launch of riders only).
   void flush(hipStream_t stream);
   void set_sink(uintptr_t sink) { cfg_.sink = sink; }
@@ -158,6 +175,12 @@ class LanesLoop {
                    const std::vector<int>& kinds);
   void check_errors(int64_t round);
   int rider_count(int nmodels, int L) const;
+  // ---- asynchronous loop ----
+  void ensure_async();
+  int64_t poll_async(int lane, double now_ms);  // due rows -> window + the lane's pending runs
+  bool try_release(int lane, int64_t vc, double now_ms);
+  void write_release(int lane, const RelRec& q);
+  void stop_all(hipStream_t stream);
 
   LanesLoopCfg cfg_;
   RcclComm* comm_;
@@ -198,6 +221,33 @@ class LanesLoop {
   int inject_spin_ = 0;
   int64_t rounds_run_ = 0;
   double host_ns_ = 0.0;
+  // asynchronous loop state (allocated by the first run_async)
+  void* aws_ = nullptr;                 // device workspace
+  AsyncLaneDev* al_dev_ = nullptr;      // device table
+  std::vector<AsyncLaneDev> al_;
+  AsyncRelease* rel_host_ = nullptr;    // pinned [L]
+  AsyncToken* tok_host_ = nullptr;      // pinned [ring]
+  AsyncArgs aargs_{};
+  AsyncPack* pack_dev_ = nullptr;       // device copy of {cfg, args} of the current launch
+  AsyncPack* pack_host_ = nullptr;      // pinned staging
+  int R_ = 64, ring_ = 64;
+  uint64_t aticket_ = 0;                // last ticket applied (device counter mirror)
+  std::vector<uint64_t> relc_;          // release records written per lane
+  std::vector<LaneRound> pend_r_;       // new stream rows not yet in the lane's ring
+  enum { kIdle = 0, kWant = 1, kRunning = 2 };
+  std::vector<int> state_;
+  std::vector<int64_t> want_vc_;
+  struct RunRec {
+    int64_t vc = 0, nseen = 0;
+    int slot_w = -1, slot_s = -1;
+    uint64_t seq_w = 0, seq_s = 0;
+  };
+  std::vector<RunRec> runrec_;
+  std::vector<int> lane_of_;            // worker id -> lane (-1: not on this loop)
+  int log_lane_ = -1;
+  int64_t launch_no_ = 0;
+  int64_t async_updates_ = 0;
+  double async_ns_ = 0.0;
 };
 
 }  // namespace psx

@@ -1,6 +1,10 @@
 // Native multi-lane BSP round loop (see lanes_loop.h).
 #include "lanes_loop.h"
 
+#include <immintrin.h>
+
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -238,6 +242,10 @@ LanesLoop::~LanesLoop() {
     if (ev_eval_[p]) (void)hipEventDestroy(ev_eval_[p]);
   }
   if (ws_) (void)hipFree(ws_);
+  if (aws_) (void)hipFree(aws_);
+  if (rel_host_) (void)hipHostFree(rel_host_);
+  if (tok_host_) (void)hipHostFree(tok_host_);
+  if (pack_host_) (void)hipHostFree(pack_host_);
   if (err_host_) (void)hipHostFree(err_host_);
 }
 
@@ -647,6 +655,394 @@ void LanesLoop::copy_out(int lane, uintptr_t loss_dst, uintptr_t delta_dst, hipS
     hip_check(hipMemcpyAsync(reinterpret_cast<void*>(delta_dst), ld.dv.delta, (size_t)P_ * sizeof(float),
                              hipMemcpyDeviceToDevice, stream),
               "lane delta copy");
+}
+
+// ---------------------------------------------------------------------------
+// Asynchronous consistency (SSP / ASP): see lanes_loop.h and lanes_kernels.h.
+
+void LanesLoop::ensure_async() {
+  if (aws_) return;
+  const SolverCfg& s = cfg_.scfg;
+  const int L = cfg_.L, FP = s.Fp, NS = FP / 32;
+  if (L < 1) throw std::invalid_argument("LanesLoop::run_async: no lanes");
+  if (!cfg_.tracker) throw std::invalid_argument("LanesLoop::run_async: needs the tracker");
+  for (int l = 0; l < L; ++l)
+    if (local_total_[l] < s.cap)  // pending rows of one release span at most one epoch wrap
+      throw std::invalid_argument("LanesLoop::run_async: a worker's shard is smaller than its ring");
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  struct Offs {
+    size_t wpull, shi, slo, sb, acc, etk, flags, rec, relc;
+  };
+  std::vector<Offs> o(L);
+  for (int l = 0; l < L; ++l) {
+    o[l].wpull = take((size_t)P_ * 4);
+    o[l].shi = take((size_t)16 * FP * 2);
+    o[l].slo = take((size_t)16 * FP * 2);
+    o[l].sb = take(16 * 4);
+    o[l].acc = take((size_t)2 * 256 * kAccStride * 4);
+    o[l].etk = take(4);
+    o[l].flags = take((size_t)kLaneWg * 32 * 8);
+    o[l].rec = take(32 * 8);
+    o[l].relc = take(8);
+  }
+  const size_t o_tab = take(sizeof(AsyncLaneDev) * L);
+  const size_t o_pack = take(sizeof(AsyncPack));
+  const size_t o_snap = take((size_t)R_ * P_ * 4);
+  const size_t o_stag = take((size_t)R_ * NS * 4);
+  const size_t o_tick = take(8);
+  const size_t o_turn = take((size_t)NS * 32 * 8);
+  hip_check(hipMalloc(&aws_, off), "hipMalloc(async workspace)");
+  hip_check(hipMemset(aws_, 0, off), "hipMemset(async workspace)");
+  hip_check(hipHostMalloc((void**)&rel_host_, sizeof(AsyncRelease) * L, hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(release records)");
+  hip_check(hipHostMalloc((void**)&tok_host_, sizeof(AsyncToken) * ring_, hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(token ring)");
+  hip_check(hipHostMalloc((void**)&pack_host_, sizeof(AsyncPack), hipHostMallocDefault), "hipHostMalloc(pack)");
+  std::memset((void*)rel_host_, 0, sizeof(AsyncRelease) * L);
+  std::memset((void*)tok_host_, 0, sizeof(AsyncToken) * ring_);
+  char* b = static_cast<char*>(aws_);
+  al_.resize(L);
+  for (int l = 0; l < L; ++l) {
+    AsyncLaneDev& A = al_[l];
+    std::memset(&A, 0, sizeof(A));
+    A.wpull = reinterpret_cast<float*>(b + o[l].wpull);
+    // the lane's solver as the asynchronous launch uses it: buffer 0 of the local
+    // model / loss, the pulled weights from its private copy, no fused update
+    A.dv = lanes_[l].dv;
+    A.dv.out_hi = lanes_[l].ohi[0];
+    A.dv.out_lo = lanes_[l].olo[0];
+    A.dv.b_fin = lanes_[l].ob[0];
+    A.dv.loss = lanes_[l].loss2;
+    A.dv.w_old = A.wpull;
+    A.dv.w_new = nullptr;
+    A.dv.ap_w = nullptr;
+    A.dv.spin_max = 0;
+    A.spart = lanes_[l].spart;
+    A.ctrl = lanes_[l].ctrl;
+    A.shi = reinterpret_cast<uint16_t*>(b + o[l].shi);
+    A.slo = reinterpret_cast<uint16_t*>(b + o[l].slo);
+    A.sb = reinterpret_cast<float*>(b + o[l].sb);
+    A.acc = reinterpret_cast<int*>(b + o[l].acc);
+    A.eticket = reinterpret_cast<unsigned*>(b + o[l].etk);
+    A.flags = reinterpret_cast<unsigned long long*>(b + o[l].flags);
+    A.rec = reinterpret_cast<unsigned long long*>(b + o[l].rec);
+    A.relc = reinterpret_cast<unsigned long long*>(b + o[l].relc);
+    A.rel = rel_host_ + l;
+  }
+  al_dev_ = reinterpret_cast<AsyncLaneDev*>(b + o_tab);
+  pack_dev_ = reinterpret_cast<AsyncPack*>(b + o_pack);
+  hip_check(hipMemcpy(al_dev_, al_.data(), sizeof(AsyncLaneDev) * L, hipMemcpyHostToDevice), "async table upload");
+  AsyncArgs& a = aargs_;
+  std::memset(&a, 0, sizeof(a));
+  a.L = L;
+  a.dsX = cfg_.dsX;
+  a.dsy = cfg_.dsy;
+  a.w = cfg_.w;
+  a.snap = reinterpret_cast<float*>(b + o_snap);
+  a.snap_tag = reinterpret_cast<unsigned*>(b + o_stag);
+  a.R = R_;
+  a.ticket = reinterpret_cast<unsigned long long*>(b + o_tick);
+  a.turn = reinterpret_cast<unsigned long long*>(b + o_turn);
+  a.tok = tok_host_;
+  a.ring = ring_;
+  a.Xt = cfg_.Xt;
+  a.yt = cfg_.yt;
+  a.T = cfg_.T;
+  a.spin_rel = 1 << 24;  // ~30 s of polls: the host answers every release
+  a.claim = claim_;
+  relc_.assign(L, 0);
+  pend_r_.assign(L, LaneRound{});
+  state_.assign(L, kIdle);
+  want_vc_.assign(L, 0);
+  runrec_.assign(L, RunRec{});
+  lane_of_.assign(cfg_.N, -1);
+  for (int l = 0; l < L; ++l) lane_of_.at(cfg_.k[l]) = l;
+}
+
+namespace {
+// the pending new rows of a lane as <= 2 contiguous runs (LaneRound n / n2)
+void drop_front(LaneRound& r, int64_t d, int64_t cap) {
+  while (d > 0 && r.n > 0) {
+    const int64_t k = d < r.n ? d : r.n;
+    r.first += k * r.step;
+    r.dst = (int)((r.dst + k) % cap);
+    r.n -= (int)k;
+    d -= k;
+    if (r.n == 0 && r.n2 > 0) {
+      r.first = r.first2;
+      r.n = r.n2;
+      r.n2 = 0;
+    }
+  }
+}
+void append_run(LaneRound& r, long long src_first, long long step, int64_t slot, int64_t run, int64_t cap) {
+  if (r.n == 0) {
+    r.first = src_first;
+    r.step = step;
+    r.n = (int)run;
+    r.dst = (int)slot;
+    r.n2 = 0;
+    return;
+  }
+  if ((r.dst + r.n + r.n2) % cap != slot) throw std::logic_error("LanesLoop: ring slots of a delivery not contiguous");
+  if (r.n2 == 0 && src_first == r.first + (long long)r.n * r.step)
+    r.n += (int)run;
+  else if (r.n2 > 0 && src_first == r.first2 + (long long)r.n2 * r.step)
+    r.n2 += (int)run;
+  else if (r.n2 == 0) {
+    r.first2 = src_first;
+    r.n2 = (int)run;
+  } else {
+    throw std::logic_error("LanesLoop: pending rows of a release span three runs");
+  }
+}
+}  // namespace
+
+int64_t LanesLoop::poll_async(int lane, double now_ms) {
+  if (exhausted(lane)) return 0;
+  const int k = cfg_.k[lane];
+  const int64_t lt = local_total_[lane];
+  int64_t& nl = next_local_[lane];
+  const int64_t limit = lt * cfg_.epochs - nl;
+  int64_t n;
+  if (cfg_.per_iter_rows > 0) {
+    n = cfg_.per_iter_rows < limit ? cfg_.per_iter_rows : limit;
+    times_.assign((size_t)n, now_ms);
+  } else {
+    const int64_t epoch = nl / lt, cur = nl - epoch * lt;
+    int64_t mx = limit < lt - cur ? limit : lt - cur;
+    if (mx > (int64_t(1) << 22)) mx = int64_t(1) << 22;
+    times_.resize(mx > 0 ? (size_t)mx : 1);
+    n = api().due_rows(k, cfg_.N, cfg_.p_ms, cfg_.ds_rows, cur, now_ms, mx, times_.data());
+    check(n, "due_rows");
+  }
+  if (n <= 0) return 0;
+  const int64_t first = api().window_insert_many(reinterpret_cast<void*>(cfg_.window[lane]), times_.data(), n);
+  check(first, "window insert");
+  const int64_t cap = cfg_.scfg.cap;
+  const int64_t keep = n < cap ? n : cap, skip = n - keep;
+  LaneRound& r = pend_r_[lane];
+  const int64_t tot = (int64_t)r.n + r.n2 + keep;
+  if (tot > cap) drop_front(r, tot - cap, cap);  // rows the ring overwrites before the next solve
+  int64_t slot = (first + skip) % cap, pos = nl + skip, remaining = keep;
+  while (remaining > 0) {  // split at the shard's epoch boundaries
+    const int64_t cur = pos % lt;
+    const int64_t run = remaining < lt - cur ? remaining : lt - cur;
+    append_run(r, k + cur * (int64_t)cfg_.N, cfg_.N, slot, run, cap);
+    slot = (slot + run) % cap;
+    pos += run;
+    remaining -= run;
+  }
+  nl += n;
+  return n;
+}
+
+void LanesLoop::write_release(int lane, const RelRec& q) {
+  TagChunk ch[kRelChunks];
+  pack_release(q, (unsigned)(++relc_[lane]), ch);
+  volatile TagChunk* dst = rel_host_[lane].ch;
+  for (int i = 0; i < kRelChunks; ++i) {
+    __m128i v;
+    std::memcpy(&v, &ch[i], 16);
+    _mm_store_si128((__m128i*)(void*)&dst[i], v);  // one 16-B store per chunk
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+}
+
+bool LanesLoop::try_release(int lane, int64_t vc, double now_ms) {
+  poll_async(lane, now_ms);
+  int64_t size = 0, start = 0, sn = 0;
+  check(api().window_state(reinterpret_cast<void*>(cfg_.window[lane]), &size, &start, &sn), "window state");
+  const int64_t need = new_tuples_needed(size);
+  if (!(size > 0 && (need <= 0 || sn - seen_at_solve_[lane] >= need || exhausted(lane)))) return false;
+  seen_at_solve_[lane] = sn;
+  RelRec q;
+  std::memset(&q, 0, sizeof(q));
+  q.vc = vc;
+  q.snap = (long long)aticket_;  // the weights right after the latest applied update
+  q.r = pend_r_[lane];
+  q.r.B = (int)size;
+  q.r.start = (int)start;
+  if (q.r.n == 0) q.r.step = cfg_.N;
+  pend_r_[lane] = LaneRound{};
+  RunRec& rr = runrec_[lane];
+  rr = RunRec{};
+  rr.vc = vc;
+  rr.nseen = sn;
+  if (cfg_.sink) {
+    const bool w = cfg_.log_workers, sv = cfg_.log_server && lane == log_lane_;
+    const int n = (w ? 1 : 0) + (sv ? 1 : 0);
+    if (n) {
+      int sl[2];
+      uint64_t sq[2];
+      uintptr_t ad[2];
+      check(api().sink_acquire_many(reinterpret_cast<void*>(cfg_.sink), n, sl, sq, ad), "metrics sink acquire");
+      int i = 0;
+      if (w) {
+        rr.slot_w = sl[i];
+        rr.seq_w = sq[i];
+        q.slot_w = ad[i];
+        q.seq_w = (unsigned)sq[i];
+        ++i;
+      }
+      if (sv) {
+        rr.slot_s = sl[i];
+        rr.seq_s = sq[i];
+        q.slot_s = ad[i];
+        q.seq_s = (unsigned)sq[i];
+      }
+    }
+  }
+  q.delay_us = lane < (int)cfg_.delay_us.size() ? cfg_.delay_us[lane] : 0;
+  write_release(lane, q);
+  return true;
+}
+
+void LanesLoop::stop_all(hipStream_t stream) {
+  RelRec q;
+  std::memset(&q, 0, sizeof(q));
+  q.stop = 1;
+  for (int l = 0; l < cfg_.L; ++l) write_release(l, q);
+  hip_check(hipStreamSynchronize(stream), "asynchronous launch drain");
+}
+
+int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms) {
+  const int64_t t_begin = steady_ns();
+  ensure_async();
+  const int L = cfg_.L;
+  void* trk = reinterpret_cast<void*>(cfg_.tracker);
+  log_lane_ = (cfg_.log_worker >= 0 && cfg_.log_worker < cfg_.N) ? lane_of_[cfg_.log_worker] : -1;
+  // where this run starts: the lanes the tracker has dispatched (bootstrap: all, vc
+  // 0, MessageTracker.java:47-53), the others wait for a release
+  for (int l = 0; l < L; ++l) {
+    const int sent = api().tracker_is_sent(trk, cfg_.k[l]);
+    check(sent, "tracker state");
+    state_[l] = sent ? kWant : kIdle;
+    want_vc_[l] = api().tracker_clock(trk, cfg_.k[l]);
+    check(want_vc_[l], "tracker clock");
+  }
+  // the snapshot of the current weights (ticket_) + the slices' turn words
+  AsyncArgs a = aargs_;
+  a.log_lane = log_lane_;
+  a.launch = ++launch_no_;
+  a.cpar = (int)(launches_ & 1);
+  launch_async_init(cfg_.scfg, a, aticket_, stream);
+  hip_check(hipGetLastError(), "async init launch");
+  pack_host_->cfg = cfg_.scfg;
+  pack_host_->a = a;
+  hip_check(hipMemcpyAsync(pack_dev_, pack_host_, sizeof(AsyncPack), hipMemcpyHostToDevice, stream), "async args");
+  launch_lanes_async(cfg_.scfg, pack_dev_, al_dev_, S_, stream);
+  hip_check(hipGetLastError(), "async lanes launch");
+  ++launches_;
+  int64_t started = 0, done = 0;
+  int running = 0;
+  bool stopping = updates <= 0;
+  std::vector<int> ks((size_t)cfg_.N);
+  std::vector<int64_t> vs((size_t)cfg_.N);
+  try {
+    auto start_ready = [&](double now) {
+      for (int l = 0; l < L; ++l) {
+        if (state_[l] != kWant || stopping || started >= updates) continue;
+        if (try_release(l, want_vc_[l], now)) {
+          state_[l] = kRunning;
+          ++started;
+          ++running;
+        }
+      }
+    };
+    double wait0 = epoch_ms();
+    start_ready(epoch_ms() - cfg_.t0_ms);
+    uint64_t next = aticket_ + 1;
+    int64_t idle_spins = 0;
+    for (;;) {
+      const volatile AsyncToken* slot = tok_host_ + (next % (uint64_t)ring_);
+      __m128i v = _mm_load_si128((const __m128i*)(const void*)slot);
+      AsyncToken tk;
+      std::memcpy(&tk, &v, 16);
+      if (tk.tag == (unsigned)next) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const int l = (int)tk.a;
+        const int64_t vc = (int64_t)(((uint64_t)tk.c << 32) | tk.b);
+        if (l < 0 || l >= L || state_[l] != kRunning || runrec_[l].vc != vc)
+          throw std::logic_error("LanesLoop: unexpected token (lane " + std::to_string(l) + ", vc " +
+                                 std::to_string((long long)vc) + ")");
+        aticket_ = next++;
+        --running;
+        ++done;
+        // the rows of the iteration: server row first (ServerProcessor.java:154-165), then the worker row
+        const RunRec& rr = runrec_[l];
+        SinkRecord rec[2];
+        int nr = 0;
+        if (rr.slot_s >= 0) rec[nr++] = SinkRecord{rr.slot_s, 1 | kSinkTagged, rr.seq_s, -1, -1, vc, 0};
+        if (rr.slot_w >= 0) rec[nr++] = SinkRecord{rr.slot_w, kSinkTagged, rr.seq_w, -1, cfg_.k[l], vc, rr.nseen};
+        if (nr) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), nr, rec), "metrics sink submit");
+        state_[l] = kIdle;
+        const int n = api().tracker_on_delta(trk, cfg_.k[l], vc, ks.data(), vs.data(), cfg_.N);
+        check(n, "tracker");
+        for (int i = 0; i < n; ++i) {
+          const int j = ks[i] >= 0 && ks[i] < cfg_.N ? lane_of_[ks[i]] : -1;
+          if (j < 0) throw std::logic_error("LanesLoop: the tracker released a worker this loop does not host");
+          state_[j] = kWant;
+          want_vc_[j] = vs[i];
+        }
+        if (deadline_ms > 0.0 && epoch_ms() >= deadline_ms) stopping = true;
+        start_ready(epoch_ms() - cfg_.t0_ms);
+        idle_spins = 0;
+        wait0 = epoch_ms();
+        continue;
+      }
+      if (running > 0) {  // solves in flight: spin for their tokens
+        if ((++idle_spins & 1023) == 0) {
+          check_errors(-1);
+          const double now = epoch_ms();
+          if (deadline_ms > 0.0 && now >= deadline_ms) stopping = true;
+          if (now - wait0 > max_wait_s * 1000.0)
+            throw std::runtime_error("LanesLoop: no delta from the device for " + std::to_string(max_wait_s) + " s");
+        } else {
+          _mm_pause();
+        }
+        continue;
+      }
+      // nothing in flight: is the run over?
+      if (stopping || started >= updates) break;
+      bool any_want = false, end = false;
+      for (int l = 0; l < L; ++l)
+        if (state_[l] == kWant) {
+          int64_t size = 0, start = 0, sn = 0;
+          check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
+          if (size <= 0 && exhausted(l)) end = true;  // a worker with no rows left: the run ends
+          any_want = true;
+        }
+      if (end || !any_want) break;
+      const double now = epoch_ms();
+      if (deadline_ms > 0.0 && now >= deadline_ms) break;
+      start_ready(now - cfg_.t0_ms);  // every dispatched lane waits for rows (producer clock / cadence)
+      if (running == 0) {
+        if (now - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      } else {
+        wait0 = epoch_ms();
+      }
+    }
+    stop_all(stream);
+  } catch (...) {
+    // never leave the persistent launch running behind an exception
+    try {
+      stop_all(stream);
+    } catch (...) {
+    }
+    throw;
+  }
+  check_errors(-1);
+  last_par_ = 0;  // the lanes wrote loss / fragments of buffer 0
+  async_updates_ += done;
+  async_ns_ += (double)(steady_ns() - t_begin);
+  return done;
 }
 
 }  // namespace psx

@@ -171,6 +171,8 @@ class LocalEngine:
             # after its delta is applied (tracker: BSP, SSP(D) and ASP coincide), so the
             # lock-step loop runs it without the thread / queue / event hand-offs
             out = self._run_bsp()
+        elif self._async_lanes_ok():
+            out = self._run_async_lanes()
         elif self._event_scheduler():
             out = self._run_async_events()
         else:
@@ -234,12 +236,30 @@ class LocalEngine:
         the producer clock run natively: a round waits until every lane saw its
         new tuples."""
         c = self.cfg
+        if c.inject_worker_delay_ms:
+            return False
+        return self._lanes_shape_ok()
+
+    def _async_lanes_ok(self) -> bool:
+        """SSP / ASP in the native asynchronous lanes loop (LanesLoop.run_async: ONE
+        persistent launch, every worker released by the C++ tracker, updates serial
+        in arrival order on the device): the lanes loop's shapes, plus every
+        worker's shard at least its ring (a release's pending rows span at most one
+        epoch wrap).  Injected straggler delays run on the device; crash / stop
+        injection and tracing keep the Python schedulers."""
+        if os.environ.get("PSX_ASYNC_LANES", "1") == "0" or not self._lanes_shape_ok():
+            return False
+        W = [w for w in self.workers if w.k not in self.failed]
+        return all(w.source.ds.rows // max(1, self.cfg.num_workers) >= w.ring.cap for w in W)
+
+    def _lanes_shape_ok(self) -> bool:
+        c = self.cfg
         if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
         W = [w for w in self.workers if w.k not in self.failed]
         if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
             return False
-        if c.inject_worker_delay_ms or c.inject_worker_crash or c.inject_worker_stop:
+        if c.inject_worker_crash or c.inject_worker_stop:
             return False
         sp = self.spec
         for w in W:
@@ -281,7 +301,11 @@ class LocalEngine:
                  shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
                  sb=[f.b.data_ptr() for f in self._lane_frags], scoff=0, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(),
                  T=ev.T, sink=self.log.native.handle, tracker=srv.tracker.handle, api=_native.host.capi(),
-                 new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap))
+                 new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap),
+                 # the asynchronous loop: server rows on the lowest live worker's deltas
+                 # (ServerProcessor.java:154), straggler delays on the device
+                 log_worker=min(w.k for w in W),
+                 delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W])
         lp = h.LanesLoop(d, None)
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
@@ -310,12 +334,15 @@ class LocalEngine:
         r0 = r = self.rounds
         u0 = srv.updates
         chunk = 256
-        if cfg.checkpoint_dir and cfg.checkpoint_every:
+        ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
+        if ck:
             chunk = max(1, int(cfg.checkpoint_every))
         exhausted_since = None
         try:
             while True:
-                todo = chunk
+                # checkpoints fire at multiples of checkpoint_every: a run that starts
+                # between two of them first runs up to the next one
+                todo = chunk - (r % chunk) if ck else chunk
                 if cfg.max_iters:
                     todo = min(todo, cfg.max_iters - (r - r0))
                     if todo <= 0:
@@ -326,9 +353,14 @@ class LocalEngine:
                     break
                 n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
                 r += n
+                # the roles' counters advance with every chunk, so a checkpoint taken
+                # here carries the updates / clocks of the rounds it covers
+                srv.updates += n * len(W)
                 for i, w in enumerate(W):
                     w.source.next_local = int(lp.next_local(i))
                     w._seen_at_solve = int(lp.seen_at_solve(i))
+                    w.vc = r
+                    w.iters += n
                 if n:
                     maybe_checkpoint(cfg, srv, r, W)
                 if n < todo:  # a worker's stream is exhausted and its window empty, or the deadline
@@ -347,11 +379,7 @@ class LocalEngine:
             if "cross-workgroup wait timed out" in str(e):
                 raise WorkerFailure(W[0].k, str(e)) from e
             raise
-        n = r - r0
-        srv.updates += n * len(W)
         for i, w in enumerate(W):
-            w.vc = r
-            w.iters += n
             w._seen_at_solve = int(lp.seen_at_solve(i))
             if w.ring.XT is not None:
                 w.ring.xt_stale = True  # the round kernel writes the row-major ring only
@@ -361,6 +389,79 @@ class LocalEngine:
         return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True,
                 "lanes": len(W), "hand_off_scope": int(lp.hand_off_scope)}
+
+    def _run_async_lanes(self) -> dict:
+        """SSP / ASP of every live worker in ONE persistent launch
+        (LanesLoop.run_async, csrc/kernels/lanes_async.hip): each worker solves on its
+        own XCD as soon as the tracker releases it, pushes with a device ticket
+        (updates serial in arrival order, ServerProcessor.java:143-183), and evaluates
+        its local model (plus the global model on the logging worker, :154-165); the
+        C++ tracker answers every delta from the host loop (MessageTracker.java:
+        69-87).  max_iters: iterations per worker (max_iters x workers updates);
+        unbounded runs and checkpoints run in chunks."""
+        cfg, srv = self.cfg, self.server
+        W = [w for w in self.workers if w.k not in self.failed]
+        for w in W:
+            w.ring.flush()
+        if srv.pair is not None:
+            srv.pair.flush(self.log)
+        lp = self._lanes_loop(W)
+        for i, w in enumerate(W):
+            lp.set_next_local(i, int(w.source.next_local))
+            lp.set_seen_at_solve(i, int(w._seen_at_solve))
+        stream = stream_handle(self.device)
+        t_start = time.time()
+        deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
+        u0 = srv.updates
+        clock0 = {w.k: int(srv.tracker.clock(w.k)) for w in W}
+        total = int(cfg.max_iters) * len(W) if cfg.max_iters else 0
+        ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
+        chunk = max(1, int(cfg.checkpoint_every)) if ck else 1 << 16
+        done = 0
+        exhausted_since = None
+        try:
+            while True:
+                todo = chunk - (srv.updates % chunk) if ck else chunk
+                if total:
+                    todo = min(todo, total - done)
+                    if todo <= 0:
+                        break
+                if lp.all_exhausted:
+                    exhausted_since = exhausted_since or time.time()
+                if self._stop(done // max(1, len(W)), t_start, exhausted_since):
+                    break
+                n = int(lp.run_async(int(todo), stream, 600.0, deadline_ms))
+                done += n
+                srv.updates += n
+                for i, w in enumerate(W):
+                    w.source.next_local = int(lp.next_local(i))
+                    w._seen_at_solve = int(lp.seen_at_solve(i))
+                    w.vc = int(srv.tracker.clock(w.k))
+                    w.iters += w.vc - clock0[w.k]
+                    clock0[w.k] = w.vc
+                if n and ck:
+                    maybe_checkpoint(cfg, srv, srv.updates, W)
+                if n < todo:  # the streams ended, the deadline passed
+                    break
+            for i, w in enumerate(W):
+                lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+            if srv.frag is not None:
+                srv.frag.refresh(srv.w)
+            torch.cuda.synchronize(self.device)
+            lp.poll_errors()
+        except RuntimeError as e:
+            if "cross-workgroup wait timed out" in str(e):
+                raise WorkerFailure(W[0].k, str(e)) from e
+            raise
+        for w in W:
+            if w.ring.XT is not None:
+                w.ring.xt_stale = True
+        self.native_host_us_per_round = float(lp.host_us_per_update)
+        elapsed = time.time() - t_start
+        self.rounds = int(srv.tracker.min_clock())
+        return {"rounds": self.rounds, "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True,
+                "lanes": len(W), "async_lanes": True, "hand_off_scope": int(lp.hand_off_scope)}
 
     def _run_bsp_native(self) -> dict:
         """BSP rounds in the native loop: every round enqueued from C++ (producer,

@@ -1,36 +1,41 @@
 #!/bin/bash
-# One gpurun session: GPU tests, smoke, short bench, rocprofv3 kernel stats.
-# Every GPU step has its own time limit; a crash/timeout/fault ends the script.
+# One parameterised gpurun session (replaces the per-session one-off scripts).
+#   OUT=gpurun_out/<name>  STEPS="async bench ssp asp tests smoke prof" bash tools/gpu_session.sh
+# Every GPU step has its own time limit; a crash / timeout / fault ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out
-mkdir -p $OUT
+OUT=${OUT:-gpurun_out/session}
+mkdir -p "$OUT"
 STEPS="${STEPS:-tests smoke bench prof}"
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 ok_rc() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = test failures (not a crash)
 for s in $STEPS; do
   case $s in
+    async)   # the asynchronous lanes loop's GPU tests
+      timeout -k 10 ${ASYNC_TIMEOUT:-400} $PYT tests/test_gpu_async_lanes.py ${PYTEST_ARGS:-} > $OUT/pytest_async.log 2>&1
+      rc=$?; echo "async tests rc=$rc"; tail -15 $OUT/pytest_async.log
+      ok_rc $rc || exit $rc ;;
     tests)
-      timeout -k 10 ${TEST_TIMEOUT:-420} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
+      timeout -k 10 ${TEST_TIMEOUT:-600} $PYT tests -m gpu ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
       rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
       ok_rc $rc || exit $rc ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
       rc=$?; echo "smoke rc=$rc"; tail -3 $OUT/smoke.log
       [ $rc -eq 0 ] || exit $rc ;;
-    bench)
-      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 && timeout -k 10 300 python bench.py ${BENCH_ARGS:-} >> $OUT/bench.log 2>&1
-      rc=$?; echo "bench rc=$rc"; tail -2 $OUT/bench.log
+    bench)   # the driver's form, then the default
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} > $OUT/bench_short.json 2> $OUT/bench_short.err &&
+        timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
+      rc=$?; echo "bench rc=$rc"; cat $OUT/bench_short.json | head -c 600; echo
       [ $rc -eq 0 ] || exit $rc ;;
-    solver)
-      timeout -k 10 240 python tools/bench_solver.py > $OUT/bench_solver.log 2>&1
-      rc=$?; echo "bench_solver rc=$rc"; tail -12 $OUT/bench_solver.log
-      [ $rc -eq 0 ] || exit $rc
-      timeout -k 10 120 python tools/bench_solver.py --stamps > $OUT/stamps.log 2>&1
-      rc=$?; echo "stamps rc=$rc"; cat $OUT/stamps.log
+    ssp|asp)
+      c=10; [ $s = asp ] && c=-1
+      timeout -k 10 300 python bench.py --consistency $c --steps ${ASYNC_STEPS:-300} --warmup 30 ${BENCH_ARGS:-} > $OUT/bench_$s.json 2> $OUT/bench_$s.err
+      rc=$?; echo "bench $s rc=$rc"; head -c 700 $OUT/bench_$s.json; echo
       [ $rc -eq 0 ] || exit $rc ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps ${PROF_STEPS:-300} --warmup 50 > $OUT/prof.log 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps ${PROF_STEPS:-300} --warmup 50 ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -2 $OUT/prof.log
       [ $rc -eq 0 ] || exit $rc ;;
   esac

@@ -10,6 +10,7 @@
 #include <memory>
 #include <stdexcept>
 
+#include "../comm/ipc_comm.h"
 #include "../comm/rccl_comm.h"
 #include "../runtime/async_server.h"
 #include "../runtime/bsp_loop.h"
@@ -358,7 +359,36 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_readwrite("own_S", &WideCfg::own_S)
       .def_readwrite("persist", &WideCfg::persist);
 
-  py::class_<RcclComm>(m, "RcclComm")
+  // the collective transports (csrc/comm/comm.h): RCCL (one rank per GPU) and
+  // IPC (ranks sharing one GPU); the lanes loop takes either
+  py::class_<Comm>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("size", &Comm::size)
+      .def("all_reduce", [](Comm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, uintptr_t s) {
+        c.all_reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, S(s));
+      })
+      .def("reduce", [](Comm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, int root, uintptr_t s) {
+        c.reduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, root, S(s));
+      })
+      .def("broadcast", [](Comm& c, uintptr_t send, uintptr_t recv, size_t n, int dt, int root, uintptr_t s) {
+        c.broadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), n, dt, root, S(s));
+      });
+  py::class_<IpcComm, Comm>(m, "IpcComm")
+      .def(py::init<int, int, int, size_t>(), py::arg("nranks"), py::arg("rank"), py::arg("device"),
+           py::arg("max_bytes"))
+      .def("handle", [](const IpcComm& c) { return py::bytes(c.handle()); })
+      .def("connect",
+           [](IpcComm& c, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (const auto& h : hs) v.push_back(std::string(h));
+             c.connect(v);
+           })
+      .def_property_readonly("collectives", &IpcComm::collectives)
+      .def("close", [](IpcComm& c) {
+        py::gil_scoped_release nogil;
+        c.close();
+      });
+  py::class_<RcclComm, Comm>(m, "RcclComm")
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def_static("available", &RcclComm::available)
       .def(py::init([](py::bytes id, int nranks, int rank, int device) {
@@ -680,7 +710,7 @@ PYBIND11_MODULE(_psx_hip, m) {
   // Multi-lane BSP round loop (csrc/runtime/lanes_loop.h): `cfg` dict of ints /
   // floats / lists; pointers are device addresses or host-runtime handles.
   py::class_<LanesLoop>(m, "LanesLoop")
-      .def(py::init([](py::dict d, RcclComm* comm) {
+      .def(py::init([](py::dict d, Comm* comm) {
              auto I = [&](const char* k, int64_t def) { return d.contains(k) ? d[k].cast<int64_t>() : def; };
              auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
              auto D = [&](const char* k, double def) { return d.contains(k) ? d[k].cast<double>() : def; };
@@ -727,6 +757,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.new_cap = (int)I("new_cap", 0);
              c.log_worker = (int)I("log_worker", 0);
              c.delay_us = d.contains("delay_us") ? d["delay_us"].cast<std::vector<int>>() : std::vector<int>{};
+             c.xcd0 = (int)I("xcd0", 0);
              return std::make_unique<LanesLoop>(c, comm);
            }),
            py::arg("cfg"), py::arg("comm") = nullptr, py::keep_alive<1, 3>())

@@ -17,11 +17,12 @@
 #include <cstdint>
 #include <string>
 
+#include "comm.h"
+
 namespace psx {
 
-class RcclComm {
+class RcclComm : public Comm {
  public:
-  enum Dtype { kF32 = 0, kI32 = 1, kU8 = 2 };
   // 128-byte unique id (rank 0 creates it; every rank passes the same bytes)
   static std::string unique_id();
   static bool available();
@@ -30,12 +31,12 @@ class RcclComm {
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
-  int rank() const { return rank_; }
-  int size() const { return nranks_; }
+  int rank() const override { return rank_; }
+  int size() const override { return nranks_; }
   // all collectives sum (float / int32) and are in-place capable
-  void all_reduce(const void* send, void* recv, size_t count, int dtype, hipStream_t s);
-  void reduce(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s);
-  void broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s);
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, hipStream_t s) override;
+  void reduce(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s) override;
+  void broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s) override;
   void reduce_scatter(const void* send, void* recv, size_t recvcount, int dtype, hipStream_t s);
   void all_gather(const void* send, void* recv, size_t sendcount, int dtype, hipStream_t s);
   void send(const void* buf, size_t count, int dtype, int peer, hipStream_t s);

@@ -110,6 +110,7 @@ struct LanesArgs {
   // lane slots 0..7, riders at 8); this launch uses parity cpar and clears the other.
   unsigned* claim;
   int cpar;
+  int xcd0;             // lane l runs on XCD xcd0 + l (processes sharing a GPU take disjoint XCDs)
   int spin_max;         // cross-workgroup wait budget (0: default)
   int nride;            // rider workgroups
   EvalMulti ev;

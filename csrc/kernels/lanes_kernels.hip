@@ -102,13 +102,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       unsigned* c = a.claim + 16 * a.cpar;
       int r = -1;
       if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
-        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
-        if ((int)xcc < L) {
-          const unsigned k = __hip_atomic_fetch_add(c + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (k < (unsigned)kLaneWg) r = (int)(xcc * kLaneWg + k);
+        const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
+        if (lx >= 0 && lx < L) {
+          const unsigned k = __hip_atomic_fetch_add(c + lx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (k < (unsigned)kLaneWg) r = lx * kLaneWg + (int)k;
         }
-      } else if (b < 8 * kLaneWg && (b & 7) < L) {  // spread hand-offs: any placement works
-        r = (b & 7) * kLaneWg + (b >> 3);
+      } else if (b < 8 * kLaneWg && (b & 7) - a.xcd0 >= 0 && (b & 7) - a.xcd0 < L) {  // spread: any placement works
+        r = ((b & 7) - a.xcd0) * kLaneWg + (b >> 3);
       }
       if (r < 0) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
       if (b == 0)  // the other parity's counters (the previous launch is complete) for the next launch

@@ -30,7 +30,7 @@
 #include <string>
 #include <vector>
 
-#include "../comm/rccl_comm.h"
+#include "../comm/comm.h"
 #include "../host/capi.h"
 #include "../kernels/lanes_kernels.h"
 
@@ -85,13 +85,17 @@ struct LanesLoopCfg {
   // -1: none) and injected straggler delays per lane (us, tests / fault injection)
   int log_worker = 0;
   std::vector<int> delay_us;
+  // first XCD of this process's lanes (lane l on XCD xcd0 + l): processes that
+  // share one GPU (IpcComm) take disjoint XCDs
+  int xcd0 = 0;
 };
 
 class LanesLoop {
  public:
-  // comm: RCCL communicator of a multi-rank job (nullptr: one rank).  A rank with
-  // L == 0 is a dedicated server rank.
-  LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm);
+  // comm: the multi-rank job's transport (RcclComm: one rank per GPU; IpcComm:
+  // ranks sharing one GPU) -- nullptr: one rank.  A rank with L == 0 is a
+  // dedicated server rank.
+  LanesLoop(const LanesLoopCfg& cfg, Comm* comm);
   ~LanesLoop();
   LanesLoop(const LanesLoop&) = delete;
   LanesLoop& operator=(const LanesLoop&) = delete;
@@ -183,7 +187,7 @@ class LanesLoop {
   void stop_all(hipStream_t stream);
 
   LanesLoopCfg cfg_;
-  RcclComm* comm_;
+  Comm* comm_;
   const HostApi* api_;
   int S_ = 2;
   int P_ = 0;

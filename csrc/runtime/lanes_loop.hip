@@ -51,11 +51,12 @@ bool LanesLoop::probe_placement(hipStream_t stream) {
   return ok;
 }
 
-LanesLoop::LanesLoop(const LanesLoopCfg& cfg, RcclComm* comm)
+LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
     : cfg_(cfg), comm_(comm), api_(reinterpret_cast<const HostApi*>(cfg.api)) {
   const SolverCfg& s = cfg_.scfg;
   if (!api_ || api_->version != kHostApiVersion) throw std::invalid_argument("LanesLoop: host runtime API mismatch");
   if (cfg_.L < 0 || cfg_.L > kMaxLanes) throw std::invalid_argument("LanesLoop: 0..8 lanes per process");
+  if (cfg_.xcd0 < 0 || cfg_.xcd0 + cfg_.L > kMaxLanes) throw std::invalid_argument("LanesLoop: lanes beyond XCD 7");
   if (cfg_.L == 0 && !comm_) throw std::invalid_argument("LanesLoop: a rank without lanes needs a communicator");
   if (!lanes_supported(s.Fp, s.K, s.cap)) throw std::invalid_argument("LanesLoop: unsupported model / ring shape");
   if (s.P != s.K * s.Fp + s.K) throw std::invalid_argument("LanesLoop: P mismatch");
@@ -501,6 +502,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.arrive = arrive_;
     a.claim = claim_;
     a.cpar = (int)(launches_ & 1);
+    a.xcd0 = cfg_.xcd0;
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
@@ -517,16 +519,16 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     if (comm_) {
       if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
       if (cfg_.allreduce) {  // every replica applies the same summed update
-        comm_->all_reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, stream);
+        comm_->all_reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, stream);
         launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr,
                             cfg_.shi[par] ? cfg_.shi[par] : upd_hi_, cfg_.shi[par] ? cfg_.slo[par] : upd_lo_,
                             cfg_.shi[par] ? cfg_.sb[par] : upd_b_, stream, cfg_.scoff);
       } else {  // push: reduce to the server rank; update there; pull: broadcast
-        comm_->reduce(dsum_, dsum_, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+        comm_->reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, cfg_.server_rank, stream);
         if (is_server)
           launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr, cfg_.shi[par],
                               cfg_.slo[par], cfg_.sb[par], stream, cfg_.scoff);
-        comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, RcclComm::kF32, cfg_.server_rank, stream);
+        comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, Comm::kF32, cfg_.server_rank, stream);
       }
       hip_check(hipGetLastError(), "server update launch");
     }
@@ -599,6 +601,7 @@ void LanesLoop::flush(hipStream_t stream) {
   a.arrive = arrive_;
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
+  a.xcd0 = cfg_.xcd0;
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
     hip_check(hipGetLastError(), "lanes evaluation launch");

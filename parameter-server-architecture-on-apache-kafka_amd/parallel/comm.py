@@ -110,9 +110,66 @@ class NativeComm:
         self.c.close()
 
 
-def make_comm(rank: int, world: int, device) -> NativeComm | None:
+class IpcNativeComm(NativeComm):
+    """Ranks sharing ONE GPU (PSX_GPU_OVERSUBSCRIBE=1, gloo control plane): the
+    same-device IPC transport of csrc/comm/ipc_comm.h -- HIP IPC-mapped staging
+    buffers, stream-ordered flags -- with NativeComm's interface for the dense
+    collectives (all-reduce, reduce, broadcast).  RCCL refuses two ranks on one
+    device; this is what lets the multi-rank lanes loop (1 server rank + worker
+    ranks) run on a one-GPU box."""
+
+    kind = "ipc"
+
+    def __init__(self, rank: int, world: int, device, max_bytes: int = 1 << 22):
+        h = _native.hip()
+        self.rank, self.world, self.device = int(rank), int(world), torch.device(device)
+        self.c = h.IpcComm(self.world, self.rank, self.device.index or 0, int(max_bytes))
+        store = dist.distributed_c10d._get_default_store()
+        tag = f"psx_ipc_{next(_seq)}"
+        store.set(f"{tag}_{self.rank}", bytes(self.c.handle()))
+        self.c.connect([bytes(store.get(f"{tag}_{r}")) for r in range(self.world)])
+        dist.barrier()  # every rank mapped every area before the first collective
+        self.side = None
+        self._cs = None
+
+    def fork(self):  # no side stream: collectives run on the compute stream
+        pass
+
+    def join(self):
+        pass
+
+    def _s(self, side: bool) -> int:
+        return self.compute_stream()
+
+    def reduce_scatter(self, out, inp, side=False):
+        raise NotImplementedError("IpcNativeComm carries the dense BSP collectives only")
+
+    all_gather = send = recv = reduce_scatter
+
+    def close(self):
+        torch.cuda.current_stream(self.device).synchronize()
+        dist.barrier()  # nobody unmaps an area a peer may still read
+        self.c.close()
+
+
+NativeComm.kind = "rccl"
+
+
+def oversubscribed() -> bool:
+    """Every rank on GPU 0 over gloo (psx.parallel.dist.init_from_env)."""
+    return os.environ.get("PSX_GPU_OVERSUBSCRIBE") == "1"
+
+
+def make_comm(rank: int, world: int, device, ipc: bool = False) -> NativeComm | None:
+    """The native transport of this rank: RCCL (nccl backend, one rank per GPU), or
+    with ``ipc`` and ranks sharing one GPU the IPC transport; None: the caller uses
+    torch.distributed."""
     device = torch.device(device)
-    if device.type != "cuda" or not dist.is_initialized() or dist.get_backend() != "nccl":
+    if device.type != "cuda" or not dist.is_initialized():
+        return None
+    if dist.get_backend() != "nccl":
+        if ipc and oversubscribed() and os.environ.get("PSX_IPC_COMM", "1") != "0":
+            return IpcNativeComm(rank, world, device)
         return None
     if os.environ.get("PSX_NATIVE_RCCL", "1") == "0":
         return None

@@ -366,7 +366,9 @@ class DistEngine:
         if wk is not None:
             wk.w.copy_(boot)
         if not hasattr(self, "comm"):  # created once per engine (init is ~0.1-0.5 s), closed by close()
-            self.comm = make_comm(self.rank, self.world, self.device)  # None: torch.distributed collectives
+            # None: torch.distributed collectives; ranks sharing one GPU get the IPC
+            # transport when the lanes loop will carry the rounds
+            self.comm = make_comm(self.rank, self.world, self.device, ipc=self._lanes_cfg_ok(sched))
         comm = self.comm
         lanes = self._lanes_ok(sched, comm)
         # wait until every worker has data (the multi-lane loop waits for its lanes itself)
@@ -552,8 +554,11 @@ class DistEngine:
         """The multi-lane round loop runs this rank's BSP rounds.  Decided from the
         configuration alone, so every rank (the dedicated server has no workers)
         reaches the same answer."""
+        return comm is not None and self._lanes_cfg_ok(sched)
+
+    def _lanes_cfg_ok(self, sched: str) -> bool:
         c = self.cfg
-        if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or comm is None or not is_gpu(self.device):
+        if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
         if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
             return False
@@ -595,7 +600,10 @@ class DistEngine:
                      k=[w.k for w in W], X=[w.ring.X.data_ptr() for w in W], y=[w.ring.y.data_ptr() for w in W],
                      window=[w.window.handle for w in W], w=w_main.data_ptr(), lr=float(cfg.lr),
                      api=_native.host.capi(), server_rank=0, allreduce=int(cfg.bsp_schedule == "allreduce"),
-                     log_server=int(self.rank == 0), log_workers=int(bool(W)),
+                     log_server=int(self.rank == 0), log_workers=int(bool(W) and cfg.log_workers),
+                     # ranks sharing one GPU (IPC transport): worker rank i's lanes on XCDs
+                     # i*wpr .. i*wpr + wpr - 1, so no two ranks' lanes share an XCD
+                     xcd0=(self.worker_id * len(W)) if (W and getattr(comm, "kind", "rccl") == "ipc") else 0,
                      sink=self.log.native.handle if self.log is not None else 0,
                      tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0,
                      new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap))
@@ -675,6 +683,8 @@ class DistEngine:
         ride in the solves, a bounded run and nothing that needs Python per round."""
         c, wk, srv = self.cfg, self.worker, self.server
         if os.environ.get("PSX_NATIVE_BSP", "1") == "0" or sched != "allreduce" or comm is None:
+            return False
+        if getattr(comm, "kind", "rccl") != "rccl":  # the one-worker native loop is bound to RCCL
             return False
         if wk is None or srv is None or srv.pair is None or not srv.pair.ride_ok or not srv.pair.shared:
             return False

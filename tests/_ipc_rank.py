@@ -1,0 +1,51 @@
+"""One rank of the shared-GPU multi-rank rehearsal (tests/test_gpu_ipc_lanes.py):
+DistEngine's BSP lanes loop with a dedicated server rank and worker ranks of 4
+lanes each, every rank on GPU 0 (PSX_GPU_OVERSUBSCRIBE=1: gloo control plane,
+the IPC transport of csrc/comm/ipc_comm.h for the round's reduce + broadcast).
+
+usage: python tests/_ipc_rank.py <out_dir> <bounded|vote>   (torchrun-style env)"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def cfg_for(world: int, mode: str):
+    from psx.runtime.config import PSConfig
+
+    return PSConfig(num_workers=(world - 1) * 4, consistency_model=0, producer_time_per_event=0,
+                    stream_mode="per_iter", rows_per_iter=1024, epochs=1000,
+                    max_iters=6 if mode == "bounded" else 0, max_wallclock_s=0.0 if mode == "bounded" else 1.5,
+                    min_buffer_size=128, max_buffer_size=1024, init="random", seed=0, server_colocated=False,
+                    bsp_schedule="reduce_bcast", workers_per_rank=4)
+
+
+def main():
+    out_dir, mode = sys.argv[1], sys.argv[2]
+    import torch
+    import torch.distributed as dist
+
+    from psx.parallel.dist import DistEngine, init_from_env
+    from psx.utils.data import synth_finefood
+
+    rank, world, device = init_from_env()
+    train, test = synth_finefood(20000, seed=0), synth_finefood(4877, seed=1)
+    eng = DistEngine(cfg_for(world, mode), rank, world, device, train=train, test=test)
+    kind = None
+    out = eng.run()
+    res = {"rank": rank, "rounds": int(eng.rounds), "lanes": getattr(eng, "_lanes", None) is not None,
+           "updates": out.get("updates")}
+    if rank == 0:
+        torch.save(eng.server.w.detach().cpu(), os.path.join(out_dir, f"w_{mode}.pt"))
+        res["server_rows"] = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
+    with open(os.path.join(out_dir, f"{mode}_rank{rank}.json"), "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+    del kind
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,83 @@
+"""The multi-rank lanes loop rehearsed on ONE GPU: 1 dedicated server rank + 2
+worker ranks x 4 lanes as three processes on GPU 0, the round's push (reduce of
+the lane sums to the server rank) and pull (broadcast of the weights) through the
+same-device IPC transport (csrc/comm/ipc_comm.h) -- the code path
+`bench.py --gpus 3 --workers 4` runs over RCCL on three GPUs.
+
+Reference: BaseKafkaApp.java:25-33 (the topic bus), ServerApp.java:31-42,
+ServerProcessor.java:111-120,148-151 (BSP: w += (1/N) delta of every worker)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch(tmp, mode, world=3, timeout=150):
+    port = str(_port())
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, PSX_GPU_OVERSUBSCRIBE="1", PSX_PG_TIMEOUT_S="120")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_ipc_rank.py"), str(tmp), mode],
+                                      env=env))
+    rcs = []
+    try:
+        for p in procs:
+            rcs.append(p.wait(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * world, rcs
+    return [json.load(open(os.path.join(tmp, f"{mode}_rank{r}.json"))) for r in range(world)]
+
+
+def test_ipc_lanes_ranks_equal_in_process_engine(cuda, tmp_path):
+    """Weights and server rows of 1 server + 2 worker ranks (IPC) == one process
+    hosting the same 8 workers (tolerance 1e-5: the lane sums are added per rank
+    first, then across ranks)."""
+    res = _launch(tmp_path, "bounded")
+    assert all(r["lanes"] for r in res), res
+    assert [r["rounds"] for r in res] == [6, 6, 6]
+    w_ipc = torch.load(os.path.join(tmp_path, "w_bounded.pt"), weights_only=True)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _ipc_rank import cfg_for
+
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    cfg = cfg_for(3, "bounded")
+    cfg.server_colocated, cfg.bsp_schedule, cfg.workers_per_rank = True, "allreduce", 1
+    eng = LocalEngine(cfg, cuda, train=synth_finefood(20000, seed=0), test=synth_finefood(4877, seed=1))
+    out = eng.run(close_log=False)
+    eng.log.drain(block=True)
+    assert out.get("lanes") == 8, out
+    w_loc = eng.server.w.detach().cpu()
+    assert torch.allclose(w_ipc, w_loc, rtol=1e-5, atol=1e-5), (w_ipc - w_loc).abs().max().item()
+    rows_ipc = res[0]["server_rows"]
+    rows_loc = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
+    assert len(rows_ipc) == len(rows_loc) == 6
+    for a, b in zip(rows_ipc, rows_loc):
+        assert a[0] == b[0] and abs(a[1] - b[1]) < 2e-3 and abs(a[2] - b[2]) < 2e-3, (a, b)
+
+
+def test_ipc_lanes_stop_vote_chunks_end_together(cuda, tmp_path):
+    """An unbounded run (max_iters 0, wall clock 1.5 s): the ranks stop by the
+    collective vote between chunks and every rank ran the same rounds."""
+    res = _launch(tmp_path, "vote")
+    rounds = [r["rounds"] for r in res]
+    assert rounds[0] > 0 and len(set(rounds)) == 1, rounds

@@ -790,6 +790,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("all_exhausted", &LanesLoop::all_exhausted)
       .def_property_readonly("hand_off_scope", &LanesLoop::hand_off_scope)
       .def_property_readonly("side_eval", &LanesLoop::side_eval)
+      .def_property_readonly("lane_eval", &LanesLoop::lane_eval)
       .def_property_readonly("host_us_per_round", &LanesLoop::host_us_per_round)
       .def_property_readonly("rounds_run", &LanesLoop::rounds_run)
       .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })

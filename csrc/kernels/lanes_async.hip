@@ -19,14 +19,10 @@ namespace psx {
 namespace {
 using namespace lanes_detail;
 
-// system-coherent 16-B accesses of pinned host memory (sc0 | sc1)
-constexpr int kAuxSys = 17;
+// system-coherent 16-B loads of pinned host memory (sc0 | sc1)
 __device__ __forceinline__ TagChunk ld_sys_chunk(const void* base, unsigned bytes, unsigned off) {
   return __builtin_bit_cast(TagChunk,
                             __builtin_amdgcn_raw_buffer_load_b128(rsrc_of(base, bytes), (int)off, 0, kAuxSys));
-}
-__device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigned off, TagChunk v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
 }
 __device__ __forceinline__ TagChunk ld_nt_chunk(const void* p) {
   return __builtin_bit_cast(TagChunk, __builtin_nontemporal_load((const u32x4*)p));
@@ -111,121 +107,6 @@ __device__ __forceinline__ void async_apply_slice(const SolverCfg& cfg, const So
   __syncthreads();
   if (tid == 0) xstore(turn, t);
   (void)flag;
-}
-
-// The lane's evaluation after its push: its local model (worker row,
-// LogisticRegressionTaskSpark.java:186) paired with, on the logging lane, the
-// global model right after this update (server row, ServerProcessor.java:
-// 154-165) -- one pass over the test tiles wg, wg + 32, ... by each of the
-// lane's workgroups; counts folded into the lane's accumulators; the last
-// workgroup publishes tagged chunks (no store-completion wait).
-template <int FP>
-__device__ __forceinline__ void async_lane_eval(char* lds, const SolverCfg& cfg, const SolveDev& dv,
-                                                const AsyncLaneDev& A, const AsyncArgs& a, const RelRec& q, int wg,
-                                                bool srow) {
-  const int tid = threadIdx.x, K = cfg.K, T = a.T;
-  const bool wrow = q.slot_w != 0ull;
-  srow = srow && q.slot_s != 0ull;
-  if (!wrow && !srow) return;  // (uniform)
-  char* red_base = lds + 32 * FP * 2;
-  int* cl = (int*)(red_base + 8192);  // [2][256]
-  int* lastp = cl + 512;
-  float* bl = (float*)(lastp + 4);    // [16]: local model 0..7, global model 8..15
-  cl[tid] = 0;
-  cl[256 + tid] = 0;
-  WFrag<FP> wf;
-  {  // fragments of both models (written this iteration on this XCD: nt loads)
-    const int lane = tid & 63, w = tid >> 6, col = lane & 15, cc = col & 7;
-    const bool live = cc < K && (col < 8 ? wrow : srow);
-    const uint16_t* fh = col < 8 ? dv.out_hi : A.shi;
-    const uint16_t* fo = col < 8 ? dv.out_lo : A.slo;
-    const auto rh = rsrc_of(fh, 16u * FP * 2u), rl = rsrc_of(fo, 16u * FP * 2u);
-#pragma unroll
-    for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
-      const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
-      const unsigned off = (unsigned)((cg * 16 + (live ? cc : 0)) * 8) * 2u;
-      wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (live) {
-        wf.h[kk] = ld_h_b128<2>(rh, off);
-        wf.l[kk] = ld_h_b128<2>(rl, off);
-      }
-    }
-  }
-  if (tid < 16) {
-    const int cc = tid & 7;
-    const bool live = cc < K && (tid < 8 ? wrow : srow);
-    bl[tid] = live ? ld_h<2>((tid < 8 ? dv.b_fin : A.sb) + cc) : 0.f;
-  }
-  const int nT = (T + 31) / 32;
-  TileRegs<FP> tr;
-  if (wg < nT) tr.load(a.Xt, a.yt, wg, T);
-  __syncthreads();
-  for (int tile = wg; tile < nT; tile += kLaneWg) {
-    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
-    tr.store(lds);
-    const int ylab = tr.y;
-    if (tile + kLaneWg < nT) tr.load(a.Xt, a.yt, tile + kLaneWg, T);
-    __syncthreads();
-    f32x4 a0, a1;
-    forward_tile_pre<FP>(lds, wf, a0, a1);
-    store_partial_logits(red_base, a0, a1);
-    __syncthreads();
-    {  // thread (row, model)
-      const int row = tid & 31, h = (tid >> 5) & 1;
-      const int yrow = __shfl(ylab, row, 64);
-      if (tid < 64 && row < nrows && (h == 0 ? wrow : srow)) {
-        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
-        int best = 0;
-        float bz = -INFINITY;
-        for (int c = 0; c < K; ++c) {
-          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
-          if (z > bz) {
-            bz = z;
-            best = c;
-          }
-        }
-        atomicAdd(&cl[h * 256 + yl * 16 + best], 1);
-      }
-    }
-    __syncthreads();
-  }
-  for (int m = 0; m < 2; ++m) {
-    const int v = cl[m * 256 + tid];
-    if (v) atomicAdd(A.acc + (m * 256 + tid) * kAccStride, v);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    *lastp = __hip_atomic_fetch_add(A.eticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kLaneWg - 1;
-  __syncthreads();
-  if (!*lastp) return;
-  // the last workgroup: the lane's counts -> LDS, then tagged chunks to the pinned slots
-  const int t16 = tid >> 4, p16 = tid & 15;
-  const bool cell = t16 < K && p16 < K;
-  for (int m = 0; m < 2; ++m) {
-    const int v = cell ? __hip_atomic_exchange(A.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                       : 0;
-    if (cell) cl[m * 256 + t16 * K + p16] = v;  // compact [K][K]
-  }
-  const float lv = tid == 0 ? ld_h<2>(dv.loss) : 0.f;
-  if (tid == 0) __hip_atomic_store(A.eticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int nch = 1 + (K * K + 2) / 3;
-  const int m = tid >> 6, i = tid & 63;  // wave 0: the worker row, wave 1: the server row
-  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
-    const unsigned tag = eval_tag(m == 0 ? q.seq_w : q.seq_s);
-    TagChunk ch;
-    if (i == 0) {
-      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
-    } else {
-      const int c0 = 3 * (i - 1);
-      auto cv = [&](int c) { return c < K * K ? (unsigned)cl[m * 256 + c] : 0u; };
-      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
-    }
-    st_sys_chunk((void*)(m == 0 ? q.slot_w : q.slot_s), 1088u, (unsigned)i * 16u, ch);
-  }
 }
 
 // A pointer the compiler must treat as new on every loop iteration: the loads
@@ -384,8 +265,24 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     st_sys_chunk(a.tok, (unsigned)(a.ring * 16), (unsigned)((t % (unsigned long long)a.ring) * 16ull),
                  TagChunk{(unsigned)t, (unsigned)l, (unsigned)(unsigned long long)q.vc,
                           (unsigned)((unsigned long long)q.vc >> 32)});
-  // ---- 4. evaluation of this iteration's models ----
-  async_lane_eval<FP>(lds, cfg, dv, A, a, q, wg, logl);
+  // ---- 4. evaluation: the local model (worker row, LogisticRegressionTaskSpark.java:186)
+  // paired on the logging lane with the global model right after this update (server
+  // row, ServerProcessor.java:154-165) ----
+  {
+    PairModels pm;
+    pm.ah = dv.out_hi;
+    pm.al = dv.out_lo;
+    pm.ab = dv.b_fin;
+    pm.aloss = dv.loss;
+    pm.aslot = (char*)q.slot_w;
+    pm.aseq = q.seq_w;
+    pm.bh = A.shi;
+    pm.bl = A.slo;
+    pm.bb = A.sb;
+    pm.bslot = logl ? (char*)q.slot_s : nullptr;
+    pm.bseq = q.seq_s;
+    lane_pair_eval<FP>(lds, K, a.Xt, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
+  }
   return true;
 }
 

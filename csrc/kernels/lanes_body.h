@@ -377,5 +377,143 @@ __device__ __forceinline__ void lane_prep(char* lb, const SolverCfg& cfg, const 
   }
 }
 
+// ---------------------------------------------------------------------------
+// A lane's own evaluation pass (both the BSP round kernel and the asynchronous
+// launch): model A (the lane's local model -- the worker row,
+// LogisticRegressionTaskSpark.java:186) and optionally model B (a global model --
+// the server row, ServerProcessor.java:154-165) in one MFMA pass (A in columns
+// 0..7, B in 8..15) over the test tiles wg, wg + G, ... of the lane's G
+// workgroups, while the other lanes still solve on their XCDs.  Counts go to the
+// lane's accumulators; the last of the G arrivals publishes each row into its
+// pinned slot as tagged 16-B chunks (sink kind | kSinkTagged): no wait for the
+// system-scope stores to complete on the lane's path.
+// Fragments written in this launch by the lane's own workgroups (one XCD): nt loads.
+struct PairModels {
+  const uint16_t *ah, *al;  // model A fragments (columns acoff .. acoff + K - 1)
+  const float* ab;          // A's intercepts
+  const float* aloss;       // A's training loss (the worker row's), nullptr: 0
+  char* aslot;              // nullptr: no A row
+  unsigned aseq;
+  const uint16_t *bh, *bl;  // model B (columns 0..K-1 of its buffers)
+  const float* bb;
+  char* bslot;              // nullptr: no B row
+  unsigned bseq;
+  int acoff = 0, bcoff = 0;  // first class column of each model in its buffers
+};
+
+// system-coherent 16-B stores into pinned host memory (sc0 | sc1)
+constexpr int kAuxSys = 17;
+__device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigned off, TagChunk v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
+}
+
+template <int FP>
+__device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t* Xt, const int32_t* yt, int T, int wg,
+                                               int G, const PairModels& pm, int* acc, unsigned* ticket) {
+  const int tid = threadIdx.x;
+  const bool wrow = pm.aslot != nullptr, srow = pm.bslot != nullptr;
+  if (!wrow && !srow) return;  // (uniform)
+  char* red_base = lds + 32 * FP * 2;
+  int* cl = (int*)(red_base + 8192);  // [2][256]
+  int* lastp = cl + 512;
+  float* bl = (float*)(lastp + 4);    // [16]: model A 0..7, model B 8..15
+  cl[tid] = 0;
+  cl[256 + tid] = 0;
+  WFrag<FP> wf;
+  {
+    const int lane = tid & 63, w = tid >> 6, col = lane & 15, cc = col & 7;
+    const bool live = cc < K && (col < 8 ? wrow : srow);
+    const uint16_t* fh = col < 8 ? pm.ah : pm.bh;
+    const uint16_t* fo = col < 8 ? pm.al : pm.bl;
+    const auto rh = rsrc_of(live ? fh : pm.ah, 16u * FP * 2u), rl = rsrc_of(live ? fo : pm.al, 16u * FP * 2u);
+#pragma unroll
+    for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
+      const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
+      const int co = col < 8 ? pm.acoff : pm.bcoff;
+      const unsigned off = (unsigned)((cg * 16 + (live ? cc + co : 0)) * 8) * 2u;
+      wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (live) {
+        wf.h[kk] = ld_h_b128<2>(rh, off);
+        wf.l[kk] = ld_h_b128<2>(rl, off);
+      }
+    }
+  }
+  if (tid < 16) {
+    const int cc = tid & 7;
+    const bool live = cc < K && (tid < 8 ? wrow : srow);
+    bl[tid] = live ? ld_h<2>((tid < 8 ? pm.ab + pm.acoff : pm.bb + pm.bcoff) + cc) : 0.f;
+  }
+  const int nT = (T + 31) / 32;
+  TileRegs<FP> tr;
+  if (wg < nT) tr.load(Xt, yt, wg, T);
+  __syncthreads();
+  for (int tile = wg; tile < nT; tile += G) {
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+    tr.store(lds);
+    const int ylab = tr.y;
+    if (tile + G < nT) tr.load(Xt, yt, tile + G, T);
+    __syncthreads();
+    f32x4 a0, a1;
+    forward_tile_pre<FP>(lds, wf, a0, a1);
+    store_partial_logits(red_base, a0, a1);
+    __syncthreads();
+    {  // thread (row, model)
+      const int row = tid & 31, h = (tid >> 5) & 1;
+      const int yrow = __shfl(ylab, row, 64);
+      if (tid < 64 && row < nrows && (h == 0 ? wrow : srow)) {
+        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+        int best = 0;
+        float bz = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
+          if (z > bz) {
+            bz = z;
+            best = c;
+          }
+        }
+        atomicAdd(&cl[h * 256 + yl * 16 + best], 1);
+      }
+    }
+    __syncthreads();
+  }
+  for (int m = 0; m < 2; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1u;
+  __syncthreads();
+  if (!*lastp) return;
+  // the last workgroup: the lane's counts -> LDS [K][K], then tagged chunks to the slots
+  const int t16 = tid >> 4, p16 = tid & 15;
+  const bool cell = t16 < K && p16 < K;
+  for (int m = 0; m < 2; ++m) {
+    const int v = cell ? __hip_atomic_exchange(acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                       : 0;
+    if (cell) cl[m * 256 + t16 * K + p16] = v;
+  }
+  const float lv = (tid == 0 && wrow && pm.aloss) ? ld_h<2>(pm.aloss) : 0.f;
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int nch = 1 + (K * K + 2) / 3;
+  const int m = tid >> 6, i = tid & 63;  // wave 0: row A, wave 1: row B
+  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
+    const unsigned tag = eval_tag(m == 0 ? pm.aseq : pm.bseq);
+    TagChunk ch;
+    if (i == 0) {
+      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (i - 1);
+      auto cv = [&](int c) { return c < K * K ? (unsigned)cl[m * 256 + c] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    st_sys_chunk(m == 0 ? pm.aslot : pm.bslot, 1088u, (unsigned)i * 16u, ch);
+  }
+}
+
 }  // namespace lanes_detail
 }  // namespace psx

@@ -114,6 +114,13 @@ struct LanesArgs {
   int spin_max;         // cross-workgroup wait budget (0: default)
   int nride;            // rider workgroups
   EvalMulti ev;
+  // lane_eval = 1: each lane evaluates its own local model of THIS round right after
+  // its solve (ev.m[l], worker row) with its own workgroups, lane 0 paired with the
+  // global model of the previous update (ev.m[kMaxEvalModels - 1], server row); the
+  // riders evaluate nothing.  0: the riders evaluate ev's models (the previous round's).
+  int lane_eval;
+  int* lacc;            // [kMaxLanes][2][256] accumulators (stride kAccStride), zero between launches
+  unsigned* lticket;    // [kMaxLanes][32] per-lane evaluation arrivals
 };
 
 bool lanes_supported(int FP, int K, int cap);

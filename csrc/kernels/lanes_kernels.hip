@@ -219,31 +219,60 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     barrier();
     phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
   }
-  if (!owner) return;
-  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
-  // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
-  if (!inplace) {
-    FinIn<KP> in;
-    const int f = wg * 32 + tid;
-    if (tid < 32) {
-      in.load_f(cfg, dv, f);
-      finalize_feature<KP>(cfg, dv, f, in, /*sc1_delta=*/true);
+  if (!owner && !a.lane_eval) return;
+  if (owner) {
+    if (wg == 0 && tid == 0) stamp(dv, 30, 4);
+    // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
+    if (!inplace) {
+      FinIn<KP> in;
+      const int f = wg * 32 + tid;
+      if (tid < 32) {
+        in.load_f(cfg, dv, f);
+        finalize_feature<KP>(cfg, dv, f, in, /*sc1_delta=*/true);
+      }
     }
-  }
-  if (wg == 0) {
-    __syncthreads();  // (the intercept entries of x were written by this workgroup's threads)
-    if (tid == 0) {
-      FinScal sc;
-      sc.load(cfg, cl, dv);
-      sc.store(cfg, dv, /*sc1_delta=*/true, /*clear_err=*/false);
+    if (wg == 0) {
+      __syncthreads();  // (the intercept entries of x were written by this workgroup's threads)
+      if (tid == 0) {
+        FinScal sc;
+        sc.load(cfg, cl, dv);
+        sc.store(cfg, dv, /*sc1_delta=*/true, /*clear_err=*/false);
+      }
+      constexpr int CW = sizeof(Ctrl) / 8;
+      for (int k = tid; k < CW; k += 256) ((unsigned long long*)lanes[l].ctrl)[k] = ((const unsigned long long*)cl)[k];
     }
-    constexpr int CW = sizeof(Ctrl) / 8;
-    for (int k = tid; k < CW; k += 256) ((unsigned long long*)lanes[l].ctrl)[k] = ((const unsigned long long*)cl)[k];
+    // ---- the BSP update: the last lane to finish a slice applies the sum ----
+    if (wg == 0 && tid == 0) stamp(dv, 30, 5);
+    if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
+    if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   }
-  // ---- the BSP update: the last lane to finish a slice applies the sum ----
-  if (wg == 0 && tid == 0) stamp(dv, 30, 5);
-  if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
-  if (wg == 0 && tid == 0) stamp(dv, 30, 6);
+  if (!a.lane_eval) return;
+  // ---- the lane's own evaluation of this round's local model (+ the previous update's
+  // global model on lane 0), while the other lanes still solve ----
+  if constexpr (S == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // fragments across XCDs
+  barrier();
+  if constexpr (S == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  {
+    const EvalModel Am = pick(a.ev.m, l), Bm = a.ev.m[kMaxEvalModels - 1];
+    PairModels pm;
+    pm.ah = Am.hi;
+    pm.al = Am.lo;
+    pm.ab = Am.b;
+    pm.aloss = Am.loss;
+    pm.aslot = Am.slot;
+    pm.aseq = (unsigned)Am.seq;
+    pm.acoff = Am.coff;
+    pm.bh = Bm.hi;
+    pm.bl = Bm.lo;
+    pm.bb = Bm.b;
+    pm.bslot = l == 0 ? Bm.slot : nullptr;
+    pm.bseq = (unsigned)Bm.seq;
+    pm.bcoff = Bm.coff;
+    if (wg == 0 && tid == 0) stamp(dv, 30, 7);
+    lane_pair_eval<FP>(lds, cfg.K, a.ev.Xt, a.ev.yt, a.ev.T, wg, G, pm,
+                       a.lacc + (size_t)l * 2 * 256 * kAccStride, a.lticket + 32 * l);
+    if (wg == 0 && tid == 0) stamp(dv, 30, 8);
+  }
 }
 
 __global__ void xcc_probe_kernel(int* ids, int n) {

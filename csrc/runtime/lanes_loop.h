@@ -134,6 +134,9 @@ class LanesLoop {
   // true: a round's rows are evaluated by a launch of their own on a side stream
   // that co-runs with the next round (8 lanes: no XCD left for riders)
   bool side_eval() const { return side_eval_; }
+  // true (default): each lane evaluates its own local model inside the round kernel
+  // (PSX_LANES_RIDERS=1: the rider workgroups evaluate the previous round instead)
+  bool lane_eval() const { return lane_eval_; }
   double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
   int64_t rounds_run() const { return rounds_run_; }
   // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
@@ -164,6 +167,7 @@ class LanesLoop {
  private:
   struct Pending {  // deferred evaluation rows of the previous round
     bool valid = false;
+    bool workers = true;  // worker rows pending too (rider evaluation); false: the server row only
     int64_t vc = 0;
     int par = 0;
     std::vector<int64_t> nseen;
@@ -177,6 +181,9 @@ class LanesLoop {
                  std::vector<int>* kinds);
   void submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
                    const std::vector<int>& kinds);
+  // lane evaluation (LanesArgs::lane_eval): this round's worker rows + the previous
+  // round's server row in the round kernel; returns the rows to submit after the launch
+  int fill_lane_eval(LanesArgs* a, int64_t r, int par, const std::vector<int64_t>& seen, SinkRecord* recs);
   void check_errors(int64_t round);
   int rider_count(int nmodels, int L) const;
   // ---- asynchronous loop ----
@@ -208,6 +215,9 @@ class LanesLoop {
   // side-stream evaluation: events by round parity (round done -> evaluation;
   // evaluation done -> the round that rewrites that parity's fragments)
   bool side_eval_ = false;
+  bool lane_eval_ = true;
+  int* lacc_ = nullptr;
+  unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;
   hipEvent_t ev_round_[2] = {nullptr, nullptr}, ev_eval_[2] = {nullptr, nullptr};
   bool eval_pending_[2] = {false, false};

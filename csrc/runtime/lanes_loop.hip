@@ -149,6 +149,8 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const size_t o_acc2 = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
   const size_t o_tic2 = take(8 * sizeof(unsigned));
   const size_t o_sfl = take(8 * sizeof(unsigned));
+  const size_t o_lacc = take((size_t)kMaxLanes * 2 * 256 * kAccStride * sizeof(int));
+  const size_t o_ltic = take((size_t)kMaxLanes * 32 * sizeof(unsigned));
   const size_t o_rdbg = stamps ? take(64 * sizeof(long long)) : 0;
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
@@ -212,6 +214,8 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   acc2_ = reinterpret_cast<int*>(b + o_acc2);
   ticket2_ = reinterpret_cast<unsigned*>(b + o_tic2);
   sflags_ = reinterpret_cast<unsigned*>(b + o_sfl);
+  lacc_ = reinterpret_cast<int*>(b + o_lacc);
+  lticket_ = reinterpret_cast<unsigned*>(b + o_ltic);
   rider_dbg_ = stamps ? reinterpret_cast<long long*>(b + o_rdbg) : nullptr;
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
@@ -221,6 +225,8 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // the riders keep a round at one launch
   const char* se = std::getenv("PSX_LANES_SIDE_EVAL");
   side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : false;
+  const char* rd = std::getenv("PSX_LANES_RIDERS");
+  lane_eval_ = cfg_.L > 0 && !side_eval_ && !(rd && rd[0] == '1');
   if (side_eval_) {
     hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side eval)");
     for (int p = 0; p < 2; ++p) {
@@ -359,7 +365,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
   ev->K = cfg_.scfg.K;
   ev->acc = acc_;
   ev->ticket = ticket_;
-  const int nw = cfg_.log_workers ? cfg_.L : 0, n = nw + (cfg_.log_server ? 1 : 0);
+  const int nw = (cfg_.log_workers && p.workers) ? cfg_.L : 0, n = nw + (cfg_.log_server ? 1 : 0);
   if (n == 0) return;
   // the round's slots in one reservation (one lock of the sink)
   int sl[kMaxEvalModels];
@@ -385,6 +391,52 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
   ev->dbg = rider_dbg_;
+}
+
+int LanesLoop::fill_lane_eval(LanesArgs* a, int64_t r, int par, const std::vector<int64_t>& seen, SinkRecord* recs) {
+  EvalMulti& ev = a->ev;
+  std::memset(&ev, 0, sizeof(ev));
+  a->lane_eval = 1;
+  a->lacc = lacc_;
+  a->lticket = lticket_;
+  if (!cfg_.sink) return 0;
+  ev.Xt = cfg_.Xt;
+  ev.yt = cfg_.yt;
+  ev.T = cfg_.T;
+  ev.K = cfg_.scfg.K;
+  const int L = cfg_.L;
+  const bool wrows = cfg_.log_workers, srow = cfg_.log_server && pend_.valid;
+  const int n = (wrows ? L : 0) + (srow ? 1 : 0);
+  if (n == 0) return 0;
+  int sl[kMaxEvalModels];
+  uint64_t sq[kMaxEvalModels];
+  uintptr_t ad[kMaxEvalModels];
+  check(api().sink_acquire_many(reinterpret_cast<void*>(cfg_.sink), n, sl, sq, ad), "metrics sink acquire");
+  int i = 0, nr = 0;
+  if (srow) {  // the reference's order: the server row, then the worker rows
+    EvalModel& m = ev.m[kMaxEvalModels - 1];
+    m.hi = cfg_.shi[pend_.par];
+    m.lo = cfg_.slo[pend_.par];
+    m.b = cfg_.sb[pend_.par];
+    m.coff = cfg_.scoff;
+    m.slot = reinterpret_cast<char*>(ad[i]);
+    m.seq = sq[i];
+    recs[nr++] = SinkRecord{sl[i], 1 | kSinkTagged, sq[i], -1, -1, pend_.vc, 0};
+    ++i;
+  }
+  if (wrows)
+    for (int l = 0; l < L; ++l, ++i) {
+      EvalModel& m = ev.m[l];
+      m.hi = lanes_[l].ohi[par];
+      m.lo = lanes_[l].olo[par];
+      m.b = lanes_[l].ob[par];
+      m.coff = 0;
+      m.loss = lanes_[l].loss2 + par;
+      m.slot = reinterpret_cast<char*>(ad[i]);
+      m.seq = sq[i];
+      recs[nr++] = SinkRecord{sl[i], kSinkTagged, sq[i], -1, cfg_.k[l], r, seen[l]};
+    }
+  return nr;
 }
 
 void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, const std::vector<uint64_t>& seqs,
@@ -430,6 +482,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
   const int KF = cfg_.scfg.K * cfg_.scfg.Fp;
   std::vector<int> slots, kinds;
   std::vector<uint64_t> seqs;
+  SinkRecord lrec[kMaxEvalModels];
+  int nlrec = 0;
   const bool is_server = !comm_ || comm_->rank() == cfg_.server_rank;
   int64_t done = 0;
   for (; done < rounds; ++done) {
@@ -486,6 +540,9 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       }
       eval_pending_[par] = false;
       slots.clear();
+    } else if (lane_eval_) {
+      slots.clear();
+      nlrec = fill_lane_eval(&a, r, par, seen, lrec);
     } else {
       fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
     }
@@ -515,6 +572,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       ++launches_;
     }
     if (!slots.empty()) submit_rows(pend_, slots, seqs, kinds);
+    if (nlrec) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), nlrec, lrec), "metrics sink submit");
+    nlrec = 0;
     // ---- multi-rank: lane sums -> server (reduce), update, weights -> every rank ----
     if (comm_) {
       if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
@@ -535,7 +594,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     (void)KF;
     // ---- this round's rows: evaluated by the next launch, or side launch now ----
     last_par_ = par;
-    pend_.valid = cfg_.sink != 0;
+    pend_.valid = cfg_.sink != 0 && (!lane_eval_ || cfg_.log_server);
+    pend_.workers = !lane_eval_;  // lane evaluation: this round's worker rows are already out
     pend_.vc = r;
     pend_.par = par;
     pend_.nseen = seen;

@@ -288,3 +288,28 @@ def test_lanes_engine_producer_clock_cadence_and_deadline(cuda):
         seen = [r[-1] for r in rs]
         for a, b in zip(seen, seen[1:]):
             assert b - a >= min(new_tuples_needed(cfg, 128), 64), (k, seen)
+
+
+@pytest.mark.parametrize("L", [1, 3, 8])
+def test_lane_evaluation_rows_equal_riders(cuda, monkeypatch, L):
+    """Each lane evaluating its own local model right after its solve (the default,
+    LanesArgs::lane_eval; lane 0 paired with the previous update's global model)
+    logs the same rows as the rider workgroups evaluating the previous round
+    (PSX_LANES_RIDERS=1): identical confusion counts, losses and clocks."""
+    spec, train, ev = _data(cuda)
+    books = []
+    for riders in ("1", "0"):
+        monkeypatch.setenv("PSX_LANES_RIDERS", riders)
+        w = spec.init("random", seed=6, device=cuda)
+        log = LogSink(spec.K, cuda)
+        lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log)
+        assert lp.lane_eval == (riders == "0")
+        lp.run(3, 0, stream_handle(cuda))
+        lp.run(2, 3, stream_handle(cuda))  # a second call continues the pending server row
+        lp.flush(stream_handle(cuda))
+        torch.cuda.synchronize()
+        books.append(log.book)
+        log.close()
+    a, b = books
+    assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 5
+    assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 5 * L

@@ -156,9 +156,7 @@ def build_cfg(a, n_workers):
         bsp_schedule=a.schedule,
         server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,
-        # below 4 workers the step stays 1/4: one worker's fresh-window solve is a
-        # noisy estimate (evaluation/README.md; tools/stream_sim.py --lr)
-        server_lr=a.server_lr,  # None: 1/N, the reference's update rule
+        server_lr=a.server_lr,  # None: 1/N, the reference's update rule (ServerProcessor.java:36)
         workers_per_rank=1 if (wide or a.consistency != 0) else a.workers,
     )
 
@@ -502,6 +500,12 @@ def _accuracy_fields(server_rows, threshold=0.40, timed_from=0, start_ms=None):
         out["server_rows"] = len(server_rows)
         out["timed_server_rows"] = len(server_rows) - timed_from
         out["best_test_f1_all_rows"] = round(max(r[2] for r in server_rows), 4)
+        # robust accuracy: the median weighted F1 / accuracy over the last 10 % of the server
+        # rows (the global model's F1 swings from round to round: see README "Accuracy")
+        tail = server_rows[-max(1, len(server_rows) // 10):]
+        f1s, accs = sorted(r[2] for r in tail), sorted(r[3] for r in tail)
+        out["f1_last10pct_median"] = round(f1s[len(f1s) // 2], 4)
+        out["acc_last10pct_median"] = round(accs[len(accs) // 2], 4)
     return out
 
 

@@ -410,7 +410,9 @@ def bench_distributed(a):
     async_mode = a.consistency != 0
     keyrange = a.schedule == "keyrange"
     dedicated = (async_mode or a.dedicated_server) and not keyrange  # key-range: every rank holds a shard
-    wpr = 1 if (async_mode or a.model != "dense" or a.cpu) else a.workers
+    # workers per worker rank: BSP --workers lanes; SSP / ASP at most 7 lanes (the persistent
+    # asynchronous launch leaves one XCD to the RCCL p2p kernels beside it)
+    wpr = 1 if (a.model != "dense" or a.cpu) else (min(a.workers, 7) if async_mode else a.workers)
     worker_ranks = world - 1 if dedicated else world
     cfg = build_cfg(a, worker_ranks * wpr)
     cfg.workers_per_rank = wpr

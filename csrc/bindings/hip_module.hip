@@ -624,6 +624,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.dense_every = (int)I("dense_every", 64);
              c.cpu = (int)I("cpu", 0);
              if (d.contains("replies")) c.replies = d["replies"].cast<std::vector<uintptr_t>>();
+             if (d.contains("peer")) c.peer = d["peer"].cast<std::vector<int>>();
              if (!c.cpu && (c.model == kAsyncDense || c.sink)) prepare_kernels();
              return std::make_unique<AsyncServer>(&comm, c, S(stream));
            }),
@@ -776,6 +777,15 @@ PYBIND11_MODULE(_psx_hip, m) {
             return l.run_async(updates, S(stream), max_wait_s, deadline_ms);
           },
           py::arg("updates"), py::arg("stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0)
+      .def(
+          "run_async_remote",
+          [](LanesLoop& l, P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, uintptr_t stream,
+             uintptr_t comm_stream, double max_wait_s, double deadline_ms) {
+            py::gil_scoped_release nogil;
+            return l.run_async_remote(p2p, ctrl, reply, iters, S(stream), S(comm_stream), max_wait_s, deadline_ms);
+          },
+          py::arg("p2p"), py::arg("ctrl"), py::arg("reply"), py::arg("iters"), py::arg("stream"),
+          py::arg("comm_stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0)
       .def_property_readonly("tickets", &LanesLoop::tickets)
       .def_property_readonly("host_us_per_update", &LanesLoop::host_us_per_update)
       .def("seen_at_solve", &LanesLoop::seen_at_solve)

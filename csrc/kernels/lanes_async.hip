@@ -179,7 +179,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
         if (wg == 0 && tid < K) b_pre = a.snap[so + (size_t)K * FP + tid];
         if (c < K) A.wpull[(size_t)c * FP + f] = wo_pre;
         if (wg == 0 && tid < K) A.wpull[(size_t)K * FP + tid] = b_pre;
-        if (tid == 0 &&
+        if (!a.remote && tid == 0 &&
             a.snap_tag[(size_t)(q.snap % (long long)a.R) * NS + wg] != (unsigned)(unsigned long long)q.snap)
           xstore(err, 8ull);  // the snapshot slot was reused before this lane pulled it
       }
@@ -259,8 +259,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   const unsigned long long t = ld_h64<2>(A.rec + 16);
   const bool logl = l == a.log_lane;
-  if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
-  x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
+  if (!a.remote) {  // the server is this launch: serial slice updates in ticket order
+    if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
+    x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
+  }
   if (wg == 0 && tid == 0)
     st_sys_chunk(a.tok, (unsigned)(a.ring * 16), (unsigned)((t % (unsigned long long)a.ring) * 16ull),
                  TagChunk{(unsigned)t, (unsigned)l, (unsigned)(unsigned long long)q.vc,
@@ -300,13 +302,13 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
       unsigned* c = a.claim + 16 * a.cpar;
       int r = -1;
       if constexpr (S == 2) {
-        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID
-        if ((int)xcc < L) {
-          const unsigned k = __hip_atomic_fetch_add(c + xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (k < (unsigned)kLaneWg) r = (int)(xcc * kLaneWg + k);
+        const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
+        if (lx >= 0 && lx < L) {
+          const unsigned k = __hip_atomic_fetch_add(c + lx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (k < (unsigned)kLaneWg) r = lx * kLaneWg + (int)k;
         }
-      } else if (b < 8 * kLaneWg && (b & 7) < L) {
-        r = (b & 7) * kLaneWg + (b >> 3);
+      } else if (b < 8 * kLaneWg && (b & 7) - a.xcd0 >= 0 && (b & 7) - a.xcd0 < L) {
+        r = ((b & 7) - a.xcd0) * kLaneWg + (b >> 3);
       }
       if (b == 0)
         for (int j = 0; j < 16; ++j)
@@ -334,15 +336,16 @@ __global__ void async_init_kernel(const float* __restrict__ w, float* snap, unsi
                                   unsigned long long* turn, unsigned long long* ticket, int P, int NS, int R,
                                   unsigned long long t) {
   const size_t so = (size_t)(t % (unsigned long long)R) * P;
-  for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < P; i += (int)(gridDim.x * blockDim.x))
-    snap[so + i] = w[i];
-  if (blockIdx.x == 0) {
-    for (int s = threadIdx.x; s < NS; s += blockDim.x) {
-      snap_tag[(size_t)(t % (unsigned long long)R) * NS + s] = (unsigned)t;
-      turn[(size_t)s * 32] = t;
-    }
-    if (threadIdx.x == 0) *ticket = t;
+  if (w) {  // (remote mode: the ticket only)
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < P; i += (int)(gridDim.x * blockDim.x))
+      snap[so + i] = w[i];
+    if (blockIdx.x == 0)
+      for (int s = threadIdx.x; s < NS; s += blockDim.x) {
+        snap_tag[(size_t)(t % (unsigned long long)R) * NS + s] = (unsigned)t;
+        turn[(size_t)s * 32] = t;
+      }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = t;
 }
 
 template <int FP, int KP, int S>

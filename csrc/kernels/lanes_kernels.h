@@ -258,6 +258,11 @@ struct AsyncArgs {
   int spin_rel;        // release wait budget (polls)
   unsigned* claim;     // [2][16] role claim counters
   int cpar;
+  // remote = 1: the server is another rank (worker GPUs of a multi-rank job): a
+  // push only publishes the token (the host sends the delta, ticket = this rank's
+  // push order); a release's snapshot is the lane's receive slot (snap = slot)
+  int remote;
+  int xcd0;            // lane l runs on XCD xcd0 + l
 };
 
 // The launch's uniform arguments, in device memory (see AsyncLaneDev).

@@ -164,6 +164,11 @@ struct AsyncServerCfg {
   int64_t logcap = 0;
   std::vector<uintptr_t> replies;  // per-worker reply CtrlQueue handles
   int dense_every = 64;
+  // worker k's p2p peer (empty: k + 1, one worker per rank).  Several workers per
+  // rank (the asynchronous lanes loop on worker GPUs) share their rank's peer and
+  // reply queue: a dense pull then also carries a reply token, so the rank knows
+  // which of its workers the next weights are for (per-peer send order)
+  std::vector<int> peer;
   // host memory server (CPU ranks): the update / log / evaluation run on the host
   // (same arithmetic as the kernels; no evaluation fragments)
   int cpu = 0;
@@ -209,6 +214,7 @@ class AsyncServer {
   void apply_cpu(const CtrlToken& t);
   void eval_cpu(char* slot, uint64_t seq);
   int log_worker() const;
+  int peer_of(int k) const { return cfg_.peer.empty() ? k + 1 : cfg_.peer[k]; }
 
   P2P* comm_;
   AsyncServerCfg cfg_;

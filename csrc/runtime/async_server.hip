@@ -328,6 +328,10 @@ AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t strea
   if (cfg.model == kAsyncDense && cfg.sink && !cfg.cpu && (!cfg.fhi || !cfg.flo || !cfg.fb || !cfg.Xt || !cfg.yt))
     throw std::invalid_argument("AsyncServer: dense evaluation needs fragments and a test set");
   if (cfg.sink && (!cfg.acc || !cfg.ticket)) throw std::invalid_argument("AsyncServer: evaluation scratch");
+  if (!cfg.peer.empty() && (int)cfg.peer.size() != cfg.nworkers)
+    throw std::invalid_argument("AsyncServer: one peer per worker");
+  if (!cfg.replies.empty() && (int)cfg.replies.size() != cfg.nworkers)
+    throw std::invalid_argument("AsyncServer: one reply queue per worker");
   finished_.assign(cfg.nworkers, 0);
   failed_.assign(cfg.nworkers, 0);
   dead_.assign(cfg.nworkers, 0);
@@ -374,7 +378,14 @@ void AsyncServer::send_weights(const int* ks, const int64_t* vs, int n) {
     if (finished_[j]) continue;
     busy_since_[j] = t;
     if (!cfg_.sparse_pull) {
-      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
+      if (!cfg_.replies.empty()) {  // several workers per rank: which one the weights are for
+        CtrlToken r{};
+        r.worker = j;
+        r.vc = vs[i];
+        if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
+          throw std::runtime_error("AsyncServer: reply queue of worker " + std::to_string(j) + " full");
+      }
+      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, peer_of(j), stream_);
       pull_floats_ += cfg_.P;
       ++dense_pulls_;
       continue;
@@ -394,12 +405,12 @@ void AsyncServer::send_weights(const int* ks, const int64_t* vs, int n) {
       if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
         throw std::runtime_error("AsyncServer: reply queue of worker " + std::to_string(j) + " full");
       if (len1) {
-        comm_->send(cfg_.lids + start, (size_t)len1, RcclComm::kI32, j + 1, stream_);
-        comm_->send(cfg_.lvals + start * KP, (size_t)(len1 * KP), RcclComm::kF32, j + 1, stream_);
+        comm_->send(cfg_.lids + start, (size_t)len1, RcclComm::kI32, peer_of(j), stream_);
+        comm_->send(cfg_.lvals + start * KP, (size_t)(len1 * KP), RcclComm::kF32, peer_of(j), stream_);
       }
       if (len2) {
-        comm_->send(cfg_.lids, (size_t)len2, RcclComm::kI32, j + 1, stream_);
-        comm_->send(cfg_.lvals, (size_t)(len2 * KP), RcclComm::kF32, j + 1, stream_);
+        comm_->send(cfg_.lids, (size_t)len2, RcclComm::kI32, peer_of(j), stream_);
+        comm_->send(cfg_.lvals, (size_t)(len2 * KP), RcclComm::kF32, peer_of(j), stream_);
       }
       ++since_dense_[j];
       ++sparse_pulls_;
@@ -408,7 +419,7 @@ void AsyncServer::send_weights(const int* ks, const int64_t* vs, int n) {
       r.kind = 0;
       if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
         throw std::runtime_error("AsyncServer: reply queue of worker " + std::to_string(j) + " full");
-      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, j + 1, stream_);
+      comm_->send(cfg_.w, (size_t)cfg_.P, RcclComm::kF32, peer_of(j), stream_);
       since_dense_[j] = 0;
       ++dense_pulls_;
       pull_floats_ += cfg_.P;
@@ -448,7 +459,7 @@ void AsyncServer::begin() {
 // (server_apply / axpy: w += lr * delta; wide_apply_sparse: the pushed ids'
 // values and the intercepts; the pull log), without evaluation fragments.
 void AsyncServer::apply_cpu(const CtrlToken& t) {
-  const int peer = t.worker + 1;
+  const int peer = peer_of(t.worker);
   float* w = cfg_.w;
   const float lr = cfg_.lr;
   if (cfg_.model == kAsyncWideSparse) {
@@ -543,7 +554,7 @@ void AsyncServer::eval_cpu(char* slot, uint64_t seq) {
 
 void AsyncServer::apply_and_log(const CtrlToken& t) {
   const int k = t.worker;
-  const int peer = k + 1;
+  const int peer = peer_of(k);
   const int64_t v = t.vc;
   if (cfg_.cpu) {
     apply_cpu(t);

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../comm/comm.h"
+#include "async_server.h"
 #include "../host/capi.h"
 #include "../kernels/lanes_kernels.h"
 
@@ -115,6 +116,16 @@ class LanesLoop {
   // drains.  Releases not yet started carry over to the next call.  Returns the
   // updates applied.
   int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
+  // Multi-rank SSP / ASP on a worker GPU: the server is rank 0 (AsyncServer,
+  // async_server.h).  Same persistent launch in remote mode: a lane's push only
+  // publishes its token; this loop sends the delta to peer 0 (`p2p`, on
+  // `comm_stream`) with a control token (queue `ctrl`: worker, vc, FINAL on the
+  // lane's last of `iters` solves), and answers the server's reply tokens (this
+  // rank's queue `reply`: which worker the next weights are for) by receiving the
+  // weights into that lane's slot and releasing the lane once they landed.
+  // Returns the solves run (every lane's FINAL token sent).
+  int64_t run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, hipStream_t stream,
+                           hipStream_t comm_stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
   int64_t tickets() const { return (int64_t)aticket_; }  // deltas applied by the asynchronous loop so far
   double host_us_per_update() const { return async_updates_ ? async_ns_ / 1000.0 / (double)async_updates_ : 0.0; }
   // Evaluate the last round's rows (one launch of riders only).
@@ -189,7 +200,8 @@ class LanesLoop {
   // ---- asynchronous loop ----
   void ensure_async();
   int64_t poll_async(int lane, double now_ms);  // due rows -> window + the lane's pending runs
-  bool try_release(int lane, int64_t vc, double now_ms);
+  bool try_release(int lane, int64_t vc, double now_ms, int64_t snap = -1);
+  void launch_async(hipStream_t stream, bool remote);
   void write_release(int lane, const RelRec& q);
   void stop_all(hipStream_t stream);
 
@@ -260,6 +272,12 @@ class LanesLoop {
   std::vector<int> lane_of_;            // worker id -> lane (-1: not on this loop)
   int log_lane_ = -1;
   int64_t launch_no_ = 0;
+  std::vector<hipEvent_t> pull_ev_;     // remote mode: a lane's weights received
+  // the persistent launch runs on a stream of its own (non-blocking: no implicit
+  // synchronisation of the null stream, e.g. a host-staged transfer, waits for it),
+  // ordered after / before the caller's stream by events
+  hipStream_t astream_ = nullptr;
+  hipEvent_t aev_in_ = nullptr, aev_out_ = nullptr;
   int64_t async_updates_ = 0;
   double async_ns_ = 0.0;
 };

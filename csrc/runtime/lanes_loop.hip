@@ -251,6 +251,14 @@ LanesLoop::~LanesLoop() {
   if (ws_) (void)hipFree(ws_);
   if (aws_) (void)hipFree(aws_);
   if (rel_host_) (void)hipHostFree(rel_host_);
+  for (hipEvent_t e : pull_ev_)
+    if (e) (void)hipEventDestroy(e);
+  if (astream_) {
+    (void)hipStreamSynchronize(astream_);
+    (void)hipStreamDestroy(astream_);
+  }
+  if (aev_in_) (void)hipEventDestroy(aev_in_);
+  if (aev_out_) (void)hipEventDestroy(aev_out_);
   if (tok_host_) (void)hipHostFree(tok_host_);
   if (pack_host_) (void)hipHostFree(pack_host_);
   if (err_host_) (void)hipHostFree(err_host_);
@@ -728,7 +736,6 @@ void LanesLoop::ensure_async() {
   const SolverCfg& s = cfg_.scfg;
   const int L = cfg_.L, FP = s.Fp, NS = FP / 32;
   if (L < 1) throw std::invalid_argument("LanesLoop::run_async: no lanes");
-  if (!cfg_.tracker) throw std::invalid_argument("LanesLoop::run_async: needs the tracker");
   for (int l = 0; l < L; ++l)
     if (local_total_[l] < s.cap)  // pending rows of one release span at most one epoch wrap
       throw std::invalid_argument("LanesLoop::run_async: a worker's shard is smaller than its ring");
@@ -768,6 +775,9 @@ void LanesLoop::ensure_async() {
   hip_check(hipHostMalloc((void**)&pack_host_, sizeof(AsyncPack), hipHostMallocDefault), "hipHostMalloc(pack)");
   std::memset((void*)rel_host_, 0, sizeof(AsyncRelease) * L);
   std::memset((void*)tok_host_, 0, sizeof(AsyncToken) * ring_);
+  hip_check(hipStreamCreateWithFlags(&astream_, hipStreamNonBlocking), "hipStreamCreate(async)");
+  hip_check(hipEventCreateWithFlags(&aev_in_, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&aev_out_, hipEventDisableTiming), "hipEventCreate");
   char* b = static_cast<char*>(aws_);
   al_.resize(L);
   for (int l = 0; l < L; ++l) {
@@ -917,7 +927,7 @@ void LanesLoop::write_release(int lane, const RelRec& q) {
   std::atomic_thread_fence(std::memory_order_release);
 }
 
-bool LanesLoop::try_release(int lane, int64_t vc, double now_ms) {
+bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   poll_async(lane, now_ms);
   int64_t size = 0, start = 0, sn = 0;
   check(api().window_state(reinterpret_cast<void*>(cfg_.window[lane]), &size, &start, &sn), "window state");
@@ -927,7 +937,8 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms) {
   RelRec q;
   std::memset(&q, 0, sizeof(q));
   q.vc = vc;
-  q.snap = (long long)aticket_;  // the weights right after the latest applied update
+  // the weights right after the latest applied update (remote: the lane's receive slot)
+  q.snap = snap >= 0 ? (long long)snap : (long long)aticket_;
   q.r = pend_r_[lane];
   q.r.B = (int)size;
   q.r.start = (int)start;
@@ -971,11 +982,36 @@ void LanesLoop::stop_all(hipStream_t stream) {
   std::memset(&q, 0, sizeof(q));
   q.stop = 1;
   for (int l = 0; l < cfg_.L; ++l) write_release(l, q);
-  hip_check(hipStreamSynchronize(stream), "asynchronous launch drain");
+  hip_check(hipStreamSynchronize(astream_), "asynchronous launch drain");
+  hip_check(hipEventRecord(aev_out_, astream_), "async order out");  // the caller's later work after it
+  hip_check(hipStreamWaitEvent(stream, aev_out_, 0), "async order out");
+}
+
+void LanesLoop::launch_async(hipStream_t stream, bool remote) {
+  // local: the snapshot of the current weights (aticket_) + the slices' turn words;
+  // remote: the ticket (= this rank's push order) only
+  AsyncArgs a = aargs_;
+  a.log_lane = remote ? -1 : log_lane_;
+  a.remote = remote ? 1 : 0;
+  a.xcd0 = cfg_.xcd0;
+  if (remote) a.w = nullptr;
+  a.launch = ++launch_no_;
+  a.cpar = (int)(launches_ & 1);
+  hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
+  hip_check(hipStreamWaitEvent(astream_, aev_in_, 0), "async order in");
+  launch_async_init(cfg_.scfg, a, aticket_, astream_);
+  hip_check(hipGetLastError(), "async init launch");
+  pack_host_->cfg = cfg_.scfg;
+  pack_host_->a = a;
+  hip_check(hipMemcpyAsync(pack_dev_, pack_host_, sizeof(AsyncPack), hipMemcpyHostToDevice, astream_), "async args");
+  launch_lanes_async(cfg_.scfg, pack_dev_, al_dev_, S_, astream_);
+  hip_check(hipGetLastError(), "async lanes launch");
+  ++launches_;
 }
 
 int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms) {
   const int64_t t_begin = steady_ns();
+  if (!cfg_.tracker) throw std::invalid_argument("LanesLoop::run_async: needs the tracker");
   ensure_async();
   const int L = cfg_.L;
   void* trk = reinterpret_cast<void*>(cfg_.tracker);
@@ -989,19 +1025,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
     want_vc_[l] = api().tracker_clock(trk, cfg_.k[l]);
     check(want_vc_[l], "tracker clock");
   }
-  // the snapshot of the current weights (ticket_) + the slices' turn words
-  AsyncArgs a = aargs_;
-  a.log_lane = log_lane_;
-  a.launch = ++launch_no_;
-  a.cpar = (int)(launches_ & 1);
-  launch_async_init(cfg_.scfg, a, aticket_, stream);
-  hip_check(hipGetLastError(), "async init launch");
-  pack_host_->cfg = cfg_.scfg;
-  pack_host_->a = a;
-  hip_check(hipMemcpyAsync(pack_dev_, pack_host_, sizeof(AsyncPack), hipMemcpyHostToDevice, stream), "async args");
-  launch_lanes_async(cfg_.scfg, pack_dev_, al_dev_, S_, stream);
-  hip_check(hipGetLastError(), "async lanes launch");
-  ++launches_;
+  launch_async(stream, false);
   int64_t started = 0, done = 0;
   int running = 0;
   bool stopping = updates <= 0;
@@ -1103,6 +1127,126 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
   }
   check_errors(-1);
   last_par_ = 0;  // the lanes wrote loss / fragments of buffer 0
+  async_updates_ += done;
+  async_ns_ += (double)(steady_ns() - t_begin);
+  return done;
+}
+
+int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, hipStream_t stream,
+                                    hipStream_t cs, double max_wait_s, double deadline_ms) {
+  const int64_t t_begin = steady_ns();
+  if (!p2p || !ctrl || !reply) throw std::invalid_argument("LanesLoop::run_async_remote: transport / queues");
+  if (iters < 1) throw std::invalid_argument("LanesLoop::run_async_remote: iters >= 1");
+  ensure_async();
+  const int L = cfg_.L;
+  if (R_ < L) throw std::invalid_argument("LanesLoop::run_async_remote: more lanes than receive slots");
+  if (pull_ev_.empty()) {
+    pull_ev_.assign(L, nullptr);
+    for (auto& e : pull_ev_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  }
+  enum { kWaitPull = 3, kPulling = 4, kDone = 5 };
+  for (int l = 0; l < L; ++l) state_[l] = kWaitPull;  // the server's begin() sends everybody its clock
+  std::vector<int64_t> it(L, 0);
+  launch_async(stream, true);
+  int64_t done = 0;
+  int running = 0, finished = 0;
+  void* rq = reinterpret_cast<void*>(reply);
+  void* cq = reinterpret_cast<void*>(ctrl);
+  auto window_empty = [&](int l) {
+    int64_t size = 0, start = 0, sn = 0;
+    check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
+    return size <= 0;
+  };
+  try {
+    double wait0 = epoch_ms();
+    uint64_t next = aticket_ + 1;
+    int64_t spins = 0;
+    while (finished < L || running > 0) {
+      bool progress = false;
+      // the server's releases, in its send order to this rank
+      CtrlToken rt{};
+      while (api().ctrl_pop(rq, &rt, 0.0) == 1) {
+        const int j = rt.worker >= 0 && rt.worker < cfg_.N ? lane_of_[rt.worker] : -1;
+        if (j < 0 || state_[j] != kWaitPull)
+          throw std::logic_error("LanesLoop: reply for worker " + std::to_string(rt.worker) + " not waiting");
+        p2p->recv(aargs_.snap + (size_t)j * P_, (size_t)P_, Comm::kF32, 0, cs);
+        hip_check(hipEventRecord(pull_ev_[j], cs), "pull event");
+        state_[j] = kPulling;
+        want_vc_[j] = rt.vc;
+        progress = true;
+      }
+      const double now = epoch_ms();
+      for (int l = 0; l < L; ++l) {
+        if (state_[l] == kPulling) {
+          const hipError_t q = hipEventQuery(pull_ev_[l]);
+          if (q == hipSuccess)
+            state_[l] = kWant;
+          else if (q != hipErrorNotReady)
+            hip_check(q, "pull event query");
+        }
+        if (state_[l] == kWant && try_release(l, want_vc_[l], now - cfg_.t0_ms, l)) {
+          state_[l] = kRunning;
+          ++running;
+          progress = true;
+        }
+      }
+      // the lanes' pushes, in their push (ticket) order
+      const volatile AsyncToken* slot = tok_host_ + (next % (uint64_t)ring_);
+      __m128i v = _mm_load_si128((const __m128i*)(const void*)slot);
+      AsyncToken tk;
+      std::memcpy(&tk, &v, 16);
+      if (tk.tag == (unsigned)next) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const int l = (int)tk.a;
+        const int64_t vc = (int64_t)(((uint64_t)tk.c << 32) | tk.b);
+        if (l < 0 || l >= L || state_[l] != kRunning || runrec_[l].vc != vc)
+          throw std::logic_error("LanesLoop: unexpected token (lane " + std::to_string(l) + ")");
+        aticket_ = next++;
+        --running;
+        ++done;
+        const bool fin = ++it[l] >= iters || (deadline_ms > 0.0 && now >= deadline_ms) ||
+                         (exhausted(l) && window_empty(l));
+        // push: the delta to the server, then its token (WorkerTrainingProcessor.java:95-97)
+        p2p->send(lanes_[l].dv.delta, (size_t)P_, Comm::kF32, 0, cs);
+        CtrlToken ct{};
+        ct.worker = cfg_.k[l];
+        ct.kind = fin ? 1 : 0;
+        ct.vc = vc;
+        ct.aux = runrec_[l].nseen;
+        if (api().ctrl_push(cq, &ct, max_wait_s) != 1) throw std::runtime_error("LanesLoop: control queue full");
+        const RunRec& rr = runrec_[l];
+        if (rr.slot_w >= 0) {
+          SinkRecord rec{rr.slot_w, kSinkTagged, rr.seq_w, -1, cfg_.k[l], vc, rr.nseen};
+          check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), 1, &rec), "metrics sink submit");
+        }
+        state_[l] = fin ? (int)kDone : (int)kWaitPull;
+        finished += fin ? 1 : 0;
+        progress = true;
+      }
+      if (progress) {
+        wait0 = epoch_ms();
+        spins = 0;
+        continue;
+      }
+      if ((++spins & 1023) == 0) {
+        check_errors(-1);
+        if (epoch_ms() - wait0 > max_wait_s * 1000.0)
+          throw std::runtime_error("LanesLoop: no progress with the server for " + std::to_string(max_wait_s) + " s");
+        if (running == 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
+      } else {
+        _mm_pause();
+      }
+    }
+    stop_all(stream);
+  } catch (...) {
+    try {
+      stop_all(stream);
+    } catch (...) {
+    }
+    throw;
+  }
+  check_errors(-1);
+  last_par_ = 0;
   async_updates_ += done;
   async_ns_ += (double)(steady_ns() - t_begin);
   return done;

@@ -54,7 +54,7 @@ from ..runtime.config import PSConfig, cadence_free
 from ..runtime.engine import load_datasets
 from ..runtime.faults import WorkerFailure, drop_on_failure
 from ..ops.sparse import SparseDelta, nz_capacity
-from .comm import make_comm
+from .comm import make_comm, oversubscribed
 from ..runtime.roles import EvalPair, ServerRole, WorkerRole, is_wide, make_evalset
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
@@ -199,9 +199,10 @@ class DistEngine:
         n_workers = n_worker_ranks * wpr
         if n_worker_ranks < 1:
             raise ValueError("need at least one worker rank (world size >= 2 with a dedicated server)")
-        if wpr > 1 and (self.async_mode or cfg.bsp_schedule == "sharded" or torch.device(device).type != "cuda"):
-            raise ValueError("several workers per rank: BSP (allreduce / reduce_bcast) on GPUs only "
-                             "(the multi-lane round loop, csrc/runtime/lanes_loop.h)")
+        if wpr > 1 and ((not self.async_mode and cfg.bsp_schedule == "sharded") or torch.device(device).type != "cuda"):
+            raise ValueError("several workers per rank: BSP (allreduce / reduce_bcast) or SSP / ASP on GPUs only "
+                             "(the multi-lane loops, csrc/runtime/lanes_loop.h)")
+        self.wpr = wpr
         if cfg.num_workers != n_workers:
             cfg.num_workers = n_workers
         if cfg.solver.persist and not (dist.is_initialized() and dist.get_backend() == "nccl"):
@@ -775,20 +776,26 @@ class DistEngine:
         h = _native.hip()
         gpu = is_gpu(self.device)
         self._hp2p = None
+        lanes = self.wpr > 1  # several workers per rank: the asynchronous lanes loop
+        peers = self.world - 1 if lanes else N  # p2p peers: worker ranks (one worker each, or lanes)
         if self.rank == 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, True)
-            # sparse pull: one reply queue per worker tells it what its next pull carries
-            self._replies = ([_native.host.CtrlQueue(f"{name}_r{j}"[:250], 64, True) for j in range(N)]
-                             if self.sparse_pull else [])
+            # sparse pull: one reply queue per worker tells it what its next pull carries;
+            # lanes: one per worker rank, shared by its workers (which lane the weights are for)
+            if lanes:
+                self._replies = [_native.host.CtrlQueue(f"{name}_r{r}"[:250], 256, True) for r in range(peers)]
+            else:
+                self._replies = ([_native.host.CtrlQueue(f"{name}_r{j}"[:250], 64, True) for j in range(N)]
+                                 if self.sparse_pull else [])
             if host_p2p:
-                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], N, 0, True, gpu, self._p2p_cap())
+                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], peers, 0, True, gpu, self._p2p_cap())
         dist.barrier()
         if self.rank != 0:
             self._ctrl = _native.host.CtrlQueue(name, 1024, False)
-            self._reply = (_native.host.CtrlQueue(f"{name}_r{self.worker_id}"[:250], 64, False)
-                           if self.sparse_pull else None)
+            self._reply = (_native.host.CtrlQueue(f"{name}_r{self.worker_id}"[:250], 256 if lanes else 64, False)
+                           if (self.sparse_pull or lanes) else None)
             if host_p2p:
-                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], N, self.rank, False, gpu, self._p2p_cap())
+                self._hp2p = h.HostP2P(f"{name}_p2p"[:250], peers, self.rank, False, gpu, self._p2p_cap())
         dist.barrier()
 
     def _p2p_cap(self) -> int:
@@ -802,6 +809,8 @@ class DistEngine:
         try:
             if self.is_server:  # ONE server loop: the native one (RCCL p2p, or HostP2P without RCCL)
                 return self._server_loop_native()
+            if self.wpr > 1:
+                return self._worker_loop_lanes()
             return self._worker_loop()
         finally:
             dist.barrier()
@@ -862,6 +871,9 @@ class DistEngine:
                          t_y=ds.y.data_ptr())
             else:
                 d.update(Xt=ev.X.data_ptr(), yt=ev.y.data_ptr())
+        if self.wpr > 1:  # worker k on rank 1 + k // wpr; that rank's reply queue says whose weights come
+            d.update(peer=[1 + k // self.wpr for k in range(cfg.num_workers)],
+                     replies=[self._replies[k // self.wpr].handle for k in range(cfg.num_workers)])
         p2p = self._hp2p if self._hp2p is not None else h.RcclP2P(self.comm.c)
         a = h.AsyncServer(p2p, d, torch.cuda.current_stream(self.device).cuda_stream if gpu else 0)
         self._aserver, self._aserver_keep, self._aserver_p2p = a, keep + [p2p], (self._hp2p or self.comm)
@@ -908,6 +920,70 @@ class DistEngine:
                 "updates_per_s": n / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
                 "failed_workers": list(a.failed), "host_us_per_update": a.host_us_per_update, "native_server": True,
                 "sparse_pulls": int(a.sparse_pulls), "dense_pulls": int(a.dense_pulls)}
+
+    def _worker_loop_lanes(self) -> dict:
+        """This rank's workers as lanes of ONE persistent launch (LanesLoop.run_async_remote,
+        csrc/kernels/lanes_async.hip in remote mode): each worker solves on its own XCD
+        when its weights arrive, and the host loop pushes its delta to the server (p2p
+        peer 0) with its token, receives the weights of every release the server
+        announces on this rank's reply queue, and logs the worker rows the lanes
+        evaluate (WorkerTrainingProcessor.java:63-98, ServerProcessor.java:143-183)."""
+        cfg, W, sp = self.cfg, self.workers, self.spec
+        h = _native.hip()
+        lp = getattr(self, "_alanes", None)
+        if lp is None:
+            from ..ops.lr import Fragments
+
+            o = cfg.solver
+            sc = h.SolverCfg()
+            sc.K, sc.F, sc.Fp, sc.P, sc.cap = sp.K, sp.F, sp.Fp, sp.P, W[0].ring.cap
+            sc.iters, sc.hist, sc.ls_max = o.iters, o.hist, o.ls_max
+            sc.mode = 1 if o.mode == "gd" else 0
+            sc.center, sc.zero_const = int(o.center), int(o.zero_const)
+            sc.nslots, sc.gd_lr, sc.tol = o.nslots, o.gd_lr, o.tol
+            ds, ev = W[0].source.ds, self.evalset
+            self._alanes_frags = [Fragments(sp, self.device), Fragments(sp, self.device)]
+            d = dict(scfg=sc, dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows), N=int(cfg.num_workers),
+                     per_iter_rows=cfg.rows_per_iter if cfg.stream_mode == "per_iter" else 0,
+                     p_ms=float(cfg.producer_time_per_event), epochs=int(cfg.epochs), t0_ms=self.t0 * 1000.0,
+                     k=[w.k for w in W], X=[w.ring.X.data_ptr() for w in W], y=[w.ring.y.data_ptr() for w in W],
+                     window=[w.window.handle for w in W], w=W[0].w.data_ptr(), lr=float(cfg.lr),
+                     shi=[f.hi.data_ptr() for f in self._alanes_frags], slo=[f.lo.data_ptr() for f in self._alanes_frags],
+                     sb=[f.b.data_ptr() for f in self._alanes_frags], Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T,
+                     sink=self.log.native.handle, api=_native.host.capi(), log_server=0,
+                     log_workers=int(cfg.log_workers), new_rows=int(cfg.iter_new_rows),
+                     new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), log_worker=-1,
+                     delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W],
+                     # ranks sharing one GPU: worker rank i's lanes on XCDs i*wpr ..; on its own GPU a
+                     # rank keeps its last XCD free for the RCCL kernels beside the persistent launch
+                     xcd0=(self.worker_id * len(W)) if oversubscribed() else 0)
+            lp = h.LanesLoop(d, None)
+            self._alanes = lp
+        else:
+            lp.set_sink(self.log.native.handle)
+        for i, w in enumerate(W):
+            lp.set_next_local(i, int(w.source.next_local))
+            lp.set_seen_at_solve(i, int(w._seen_at_solve))
+        p2p = self._hp2p if self._hp2p is not None else h.RcclP2P(self.comm.c)
+        if not hasattr(self, "_comm_stream"):
+            self._comm_stream = torch.cuda.Stream(self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        t_start = time.time()
+        deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
+        iters = int(cfg.max_iters) if cfg.max_iters else 1 << 40
+        n = int(lp.run_async_remote(p2p, self._ctrl.handle, self._reply.handle, iters, stream,
+                                    self._comm_stream.cuda_stream, float(cfg.worker_timeout_s), deadline_ms))
+        torch.cuda.synchronize(self.device)
+        lp.poll_errors()
+        for i, w in enumerate(W):
+            w.source.next_local = int(lp.next_local(i))
+            w._seen_at_solve = int(lp.seen_at_solve(i))
+            if w.ring.XT is not None:
+                w.ring.xt_stale = True
+        if self.log is not None:
+            self.log.drain()
+        elapsed = time.time() - t_start
+        return {"rounds": n // max(1, len(W)), "updates": n, "elapsed_s": elapsed, "async_lanes": True}
 
     def _worker_loop(self) -> dict:
         cfg, wk = self.cfg, self.worker

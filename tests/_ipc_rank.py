@@ -15,6 +15,11 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
+    if mode.startswith("async"):  # SSP(2) / ASP: 1 server rank + worker ranks x 3 lanes (HostP2P data plane)
+        c = -1 if mode == "async_asp" else 2
+        return PSConfig(num_workers=(world - 1) * 3, consistency_model=c, producer_time_per_event=0,
+                        stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=8, min_buffer_size=128,
+                        max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3)
     return PSConfig(num_workers=(world - 1) * 4, consistency_model=0, producer_time_per_event=0,
                     stream_mode="per_iter", rows_per_iter=1024, epochs=1000,
                     max_iters=6 if mode == "bounded" else 0, max_wallclock_s=0.0 if mode == "bounded" else 1.5,
@@ -40,6 +45,9 @@ def main():
     if rank == 0:
         torch.save(eng.server.w.detach().cpu(), os.path.join(out_dir, f"w_{mode}.pt"))
         res["server_rows"] = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
+        res["max_vc_gap"] = out.get("max_vc_gap")
+    else:
+        res["async_lanes"] = bool(out.get("async_lanes"))
     with open(os.path.join(out_dir, f"{mode}_rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
     dist.barrier()

@@ -81,3 +81,20 @@ def test_ipc_lanes_stop_vote_chunks_end_together(cuda, tmp_path):
     res = _launch(tmp_path, "vote")
     rounds = [r["rounds"] for r in res]
     assert rounds[0] > 0 and len(set(rounds)) == 1, rounds
+
+
+@pytest.mark.parametrize("mode,bound", [("async_ssp", 3), ("async_asp", None)])
+def test_async_lanes_worker_ranks(cuda, tmp_path, mode, bound):
+    """SSP(2) / ASP across processes: 1 server rank (the native AsyncServer) + 2
+    worker ranks whose 3 workers each are lanes of one persistent launch
+    (LanesLoop.run_async_remote), every delta pushed with its token and every
+    release answered through the rank's reply queue (ServerProcessor.java:95-183)."""
+    res = _launch(tmp_path, mode)
+    assert all(r.get("async_lanes") for r in res[1:]), res
+    assert res[0]["updates"] == 6 * 8, res[0]
+    rows = res[0]["server_rows"]
+    assert len(rows) == 8 and all(r[1] > 0.2 for r in rows[2:]), rows  # one server row per worker-0 delta
+    if bound is not None:
+        assert res[0]["max_vc_gap"] <= bound, res[0]
+    w = torch.load(os.path.join(tmp_path, f"w_{mode}.pt"), weights_only=True)
+    assert torch.isfinite(w).all()

@@ -157,7 +157,7 @@ def build_cfg(a, n_workers):
         server_colocated=not a.dedicated_server,
         async_scheduler=a.async_scheduler,
         server_lr=a.server_lr,  # None: 1/N, the reference's update rule (ServerProcessor.java:36)
-        workers_per_rank=1 if (wide or a.consistency != 0) else a.workers,
+        workers_per_rank=1 if wide else a.workers,
     )
 
 

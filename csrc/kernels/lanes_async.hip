@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
     const int L = a.L;
     __shared__ int role;
     if (tid == 0) {
-      unsigned* c = a.claim + 16 * a.cpar;
+      unsigned* c = a.claim + 32 * a.cpar;
       int r = -1;
       if constexpr (S == 2) {
         const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
@@ -311,12 +311,12 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
         r = ((b & 7) - a.xcd0) * kLaneWg + (b >> 3);
       }
       if (b == 0)
-        for (int j = 0; j < 16; ++j)
-          __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < 32; ++j)
+          __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = r;
     }
     __syncthreads();
-    const int r = role;
+    const int r = __builtin_amdgcn_readfirstlane(role);  // (uniform: lane / workgroup indices in SGPRs)
     __syncthreads();
     if (r < 0) return;
     l = r / kLaneWg;

@@ -12,17 +12,37 @@
 namespace psx {
 namespace lanes_detail {
 
-// Element i of a kernel-argument array with a workgroup-uniform runtime index:
-// a switch over constant indices keeps every access a scalar load from the
-// kernarg segment (a dynamic index would copy the whole argument struct into
-// scratch memory, per lane, at kernel entry).
+// Element i of a kernel-argument array with a wave-uniform runtime index.  Each
+// candidate is read with a constant index and passed through readfirstlane word by
+// word: a plain select chain is folded by the compiler into ONE load from a selected
+// address, which needs the argument struct in memory -- every lane of every
+// workgroup then copies the kernel arguments into scratch at entry (measured: 1208
+// B per lane, 79 MB of scratch writes per round launch).  The index must be
+// uniform across the wave (it is read from the first lane).
 template <typename T, int N>
 __device__ __forceinline__ T pick(const T (&arr)[N], int i) {
-  T v = arr[0];
+  static_assert(sizeof(T) % 4 == 0, "pick: word-sized structs");
+  constexpr int W = sizeof(T) / 4;
+  i = __builtin_amdgcn_readfirstlane(i);
+  struct Words {
+    unsigned w[W];
+  } v;
 #pragma unroll
-  for (int j = 1; j < N; ++j)
-    if (i == j) v = arr[j];
-  return v;
+  for (int k = 0; k < W; ++k) v.w[k] = 0u;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (i == j) {
+      const unsigned* src = reinterpret_cast<const unsigned*>(&arr[j]);
+#pragma unroll
+      for (int k = 0; k < W; ++k) v.w[k] = __builtin_amdgcn_readfirstlane(src[k]);
+    }
+  return __builtin_bit_cast(T, v);
+}
+
+// system-coherent 16-B stores into pinned host memory (sc0 | sc1)
+constexpr int kAuxSys = 17;
+__device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigned off, TagChunk v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
 }
 
 // ---------------------------------------------------------------------------
@@ -33,50 +53,73 @@ __device__ __forceinline__ T pick(const T (&arr)[N], int i) {
 // rider arrives on the ticket once; the last one publishes every model's
 // counts (and its loss) into its pinned slot, then the sequence number.
 template <int FP>
-__device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel* ma, const EvalModel* mb, int K) {
+// (the per-lane choice between the two models selects field values, not struct
+// addresses: a pointer select would keep both structs in scratch memory)
+__device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel& ma, const EvalModel& mb, bool has_b,
+                                                int K) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = lane & 15, c = col & 7;
-  const EvalModel* m = col < 8 ? ma : mb;
-  const bool live = m != nullptr && c < K;
+  const bool a = col < 8;
+  const uint16_t* hi = a ? ma.hi : mb.hi;
+  const uint16_t* lo = a ? ma.lo : mb.lo;
+  const int coff = a ? ma.coff : mb.coff;
+  const bool live = (a || has_b) && c < K;
 #pragma unroll
   for (int kk = 0; kk < WFrag<FP>::KS; ++kk) {
     const int cg = (w * WFrag<FP>::KS + kk) * 4 + (lane >> 4);
-    const size_t fo = ((size_t)cg * 16 + (live ? m->coff + c : 0)) * 8;
+    const size_t fo = ((size_t)cg * 16 + (live ? coff + c : 0)) * 8;
     wf.h[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     wf.l[kk] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     if (live) {
-      wf.h[kk] = *(const u16x8*)(m->hi + fo);
-      wf.l[kk] = *(const u16x8*)(m->lo + fo);
+      wf.h[kk] = *(const u16x8*)(hi + fo);
+      wf.l[kk] = *(const u16x8*)(lo + fo);
     }
   }
 }
 
 // The last arriving workgroup publishes every model's counts into its pinned slot
-// (see eval_body.h): all M accumulator exchanges (and the losses) are issued
-// before the first system-scope store, so they cost one L2 round trip instead of M
-// dependent ones; then the drain, the ticket reset and the sequence numbers.
-__device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid) {
+// as tagged 16-B chunks (sink kind | kSinkTagged, eval_tag(seq)): all M
+// accumulator exchanges are issued before the first store (one L2 round trip), the
+// counts go through LDS (cells: [M][K*K] ints) into chunk form, and each chunk is
+// ONE system-scope store carrying its own tag -- no store-completion wait before a
+// sequence number, so the publication costs the workgroup no PCIe round trip.
+__device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid, int* cells) {
+  const int K = ev.K, KK = K * K;
+  const int t16 = tid >> 4, p16 = tid & 15;
+  const bool cell = t16 < K && p16 < K;
   int tot[kMaxEvalModels];
 #pragma unroll
   for (int m = 0; m < kMaxEvalModels; ++m)
-    tot[m] = m < M ? __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                   : 0;
-  float lv = 0.f;
-  if (tid < M) {
-    const EvalModel E = pick(ev.m, tid);
-    lv = E.loss ? *E.loss : 0.f;
-  }
+    tot[m] = (m < M && cell) ? __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)
+                             : 0;
+  float lv = 0.f;  // (constant model indices: a per-thread index would copy ev.m into scratch)
 #pragma unroll
   for (int m = 0; m < kMaxEvalModels; ++m)
-    if (m < M) __hip_atomic_store((int*)pick(ev.m, m).slot + tid, tot[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (tid < M) __hip_atomic_store((float*)(pick(ev.m, tid).slot + 1024), lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (m < M && tid == m && ev.m[m].loss) lv = *ev.m[m].loss;
+  __syncthreads();  // (the caller's counts in `cells` were consumed)
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)
+    if (m < M && cell) cells[m * KK + t16 * K + p16] = tot[m];
+  if (tid < M) cells[kMaxEvalModels * 64 + tid] = __float_as_int(lv);
   __syncthreads();
   if (tid == 0) __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid < M)
-    __hip_atomic_store((unsigned long long*)(pick(ev.m, tid).slot + 1032), pick(ev.m, tid).seq, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // wave w publishes models w, w + 4, ... (nch <= 23 chunks: one per lane); the model
+  // index is wave-uniform, so pick() stays a scalar select of kernel arguments
+  const int nch = 1 + (KK + 2) / 3, i = tid & 63;
+  for (int m = __builtin_amdgcn_readfirstlane(tid >> 6); m < M; m += 4) {
+    const EvalModel E = pick(ev.m, m);
+    const unsigned tag = eval_tag(E.seq);
+    TagChunk ch;
+    if (i == 0) {
+      ch = TagChunk{tag, (unsigned)cells[kMaxEvalModels * 64 + m], (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (i - 1);
+      auto cv = [&](int c) { return c < KK ? (unsigned)cells[m * KK + c] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    if (i < nch) st_sys_chunk(E.slot, 1088u, (unsigned)i * 16u, ch);
+  }
 }
 
 // A 32-row test tile held in registers (stage_tile's loads, split from its LDS
@@ -111,6 +154,7 @@ struct TileRegs {
 template <int FP>
 __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, int rid, int nride) {
   if (ev.nmodels <= 0 || rid >= nride) return;
+  rid = __builtin_amdgcn_readfirstlane(rid);  // (workgroup-uniform: keeps the item indices scalar)
   long long* dbg = ev.dbg;
   auto rstamp = [&](int k) {
     if (dbg && threadIdx.x == 0) dbg[k] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -129,54 +173,85 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   const int nT = (T + 31) / 32, npairs = (M + 1) / 2;
   for (int m = 0; m < M; ++m) cl[m * 256 + tid] = 0;
   const int items = npairs * nT, chunk = (items + nride - 1) / nride;
-  const int i0 = rid * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
   int curp = -1;
   WFrag<FP> wf;
   TileRegs<FP> tr;  // the next item's tile, in flight during the current item
-  if (i0 < i1) tr.load(ev.Xt, ev.yt, i0 % nT, T);
-  __syncthreads();
-  for (int it = i0; it < i1; ++it) {
-    const int p = it / nT, tile = it - p * nT;
-    const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
-    const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
-    if (p != curp) {  // (workgroup-uniform)
-      load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
-      if (tid < 16) {  // the intercepts into LDS once per pair, not a global load per class and row
-        const int h = tid >> 3, c = tid & 7;
-        const float* bp = h == 0 ? A.b + A.coff : Bm.b + Bm.coff;
-        bl[tid] = (c < K && (h == 0 || mb >= 0)) ? bp[c] : 0.f;
-      }
-      curp = p;
-    }
-    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
-    tr.store(lds);
-    const int ylab = tr.y;
-    if (it + 1 < i1) tr.load(ev.Xt, ev.yt, (it + 1) % nT, T);
+  // items [j0, j1) of the tile range [t0, t0 + ntx): item j = (pair j / ntx, tile t0 + j % ntx)
+  auto run_items = [&](int t0, int ntx, int j0, int j1, bool first) {
+    if (j0 < j1) tr.load(ev.Xt, ev.yt, t0 + j0 % ntx, T);
     __syncthreads();
-    if (rid == 0 && it == i0) rstamp(1);
-    f32x4 a0, a1;
-    forward_tile_pre<FP>(lds, wf, a0, a1);
-    store_partial_logits(red_base, a0, a1);
-    __syncthreads();
-    {  // thread (row, model): rows 0..31 x models {A, B} -- both models' argmax at once
-      const int row = tid & 31, h = (tid >> 5) & 1;
-      const int yrow = __shfl(ylab, row, 64);  // the row's label (held by thread `row` of wave 0)
-      if (tid < 64 && row < nrows && (h == 0 || mb >= 0)) {
-        const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
-        int best = 0;
-        float bz = -INFINITY;
-        for (int c = 0; c < K; ++c) {
-          const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
-          if (z > bz) {
-            bz = z;
-            best = c;
-          }
+    for (int it = j0; it < j1; ++it) {
+      const int p = it / ntx, tile = t0 + (it - p * ntx);
+      const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
+      if (p != curp) {  // (workgroup-uniform)
+        const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
+        load_pair_frags<FP>(wf, A, Bm, mb >= 0, K);
+        if (tid < 16) {  // the intercepts into LDS once per pair, not a global load per class and row
+          const int h = tid >> 3, c = tid & 7;
+          const float* bp = h == 0 ? A.b + A.coff : Bm.b + Bm.coff;
+          bl[tid] = (c < K && (h == 0 || mb >= 0)) ? bp[c] : 0.f;
         }
-        atomicAdd(&cl[(h == 0 ? ma : mb) * 256 + yl * 16 + best], 1);
+        curp = p;
       }
+      const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+      tr.store(lds);
+      const int ylab = tr.y;
+      if (it + 1 < j1) tr.load(ev.Xt, ev.yt, t0 + (it + 1) % ntx, T);
+      __syncthreads();
+      if (first && rid == 0 && it == j0) rstamp(1);
+      f32x4 a0, a1;
+      forward_tile_pre<FP>(lds, wf, a0, a1);
+      store_partial_logits(red_base, a0, a1);
+      __syncthreads();
+      {  // thread (row, model): rows 0..31 x models {A, B} -- both models' argmax at once
+        const int row = tid & 31, h = (tid >> 5) & 1;
+        const int yrow = __shfl(ylab, row, 64);  // the row's label (held by thread `row` of wave 0)
+        if (tid < 64 && row < nrows && (h == 0 || mb >= 0)) {
+          const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+          int best = 0;
+          float bz = -INFINITY;
+          for (int c = 0; c < K; ++c) {
+            const float z = load_logit(red_base, row, 8 * h + c) + bl[8 * h + c];
+            if (z > bz) {
+              bz = z;
+              best = c;
+            }
+          }
+          atomicAdd(&cl[(h == 0 ? ma : mb) * 256 + yl * 16 + best], 1);
+        }
+      }
+      __syncthreads();
+      if (first && rid == 0 && it - j0 < 4) rstamp(2 + (it - j0));
     }
-    __syncthreads();
-    if (rid == 0 && it - i0 < 4) rstamp(2 + (it - i0));
+  };
+  if (!ev.xq) {  // rider rid: items [rid * chunk, (rid + 1) * chunk), pair-major over the whole test set
+    const int i0 = rid * chunk, i1 = i0 + chunk < items ? i0 + chunk : items;
+    run_items(0, nT, i0, i1, true);
+  } else {
+    // XCD-local slices: the test set split into 8 tile ranges, range x evaluated by riders
+    // running on XCD x (its tiles stay in that XCD's L2 from round to round), in chunks
+    // popped from a per-XCD counter; a rider whose range is done pops the next XCD's --
+    // every chunk exactly once whatever the placement
+    const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);  // HW_REG_XCC_ID
+    int* cp = lastp + 1;
+    bool first = true;
+    for (int probe = 0; probe < 8;) {
+      const int x = (xcc + probe) & 7;
+      const int t0 = x * nT / 8, ntx = (x + 1) * nT / 8 - t0, itx = npairs * ntx;
+      const int chx = (itx + chunk - 1) / chunk;
+      if (tid == 0) *cp = (int)__hip_atomic_fetch_add(ev.xq + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int c = __builtin_amdgcn_readfirstlane(*cp);  // (uniform: scalar item indices)
+      __syncthreads();
+      if (c >= chx) {
+        ++probe;
+        continue;
+      }
+      const int j0 = c * chunk, j1 = j0 + chunk < itx ? j0 + chunk : itx;
+      curp = -1;
+      run_items(t0, ntx, j0, j1, first);
+      first = false;
+    }
   }
   __syncthreads();
   for (int m = 0; m < M; ++m) {
@@ -193,7 +268,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   __syncthreads();
   if (!*lastp) return;
   rstamp(10);
-  publish_counts(ev, M, tid);
+  publish_counts(ev, M, tid, cl);
   rstamp(11);
 }
 
@@ -401,11 +476,6 @@ struct PairModels {
   int acoff = 0, bcoff = 0;  // first class column of each model in its buffers
 };
 
-// system-coherent 16-B stores into pinned host memory (sc0 | sc1)
-constexpr int kAuxSys = 17;
-__device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigned off, TagChunk v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
-}
 
 template <int FP>
 __device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t* Xt, const int32_t* yt, int T, int wg,

@@ -83,6 +83,9 @@ struct EvalMulti {
   int* acc;          // [kMaxEvalModels][256] private accumulators (stride kAccStride), zero between passes
   unsigned* ticket;  // arrivals of the riders (reset by the last)
   unsigned nticket;
+  // != nullptr: XCD-local evaluation -- [8] chunk counters (zero at launch): riders on
+  // XCD x take chunks of the x-th eighth of the test tiles first (eval_multi_body)
+  unsigned* xq;
   // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
   // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the
   // ticket, [10] the last rider is known, [11] its publication done, [12] / [13] the
@@ -107,7 +110,8 @@ struct LanesArgs {
   // the next slot of that XCD's lane (< kLaneWg of them), else the next rider id,
   // so a lane's workgroups share one L2 whatever order the dispatcher deals the
   // workgroups to the XCDs in.  claim: [2 launch parities][16] counters (XCD
-  // lane slots 0..7, riders at 8); this launch uses parity cpar and clears the other.
+  // lane slots 0..7, riders at 8, XCD-local evaluation chunks at 16..23, EvalMulti::xq);
+  // this launch uses parity cpar ([2][32] counters) and clears the other.
   unsigned* claim;
   int cpar;
   int xcd0;             // lane l runs on XCD xcd0 + l (processes sharing a GPU take disjoint XCDs)

@@ -90,7 +90,10 @@ __device__ __forceinline__ bool lane_arrive(unsigned* arrive, int idx, int L, in
   return *flag != 0;
 }
 
-template <int FP, int KP, int S>
+// LE: the lanes evaluate their own models after the solve (LanesArgs::lane_eval).  A
+// template flag, not a run-time test: the evaluation tail compiled into the kernel
+// costs the solve its registers (1208 B of scratch against 120 B without it).
+template <int FP, int KP, int S, bool LE>
 __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const LaneDev* __restrict__ lanes,
                                                           LanesArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   {
     __shared__ int role;
     if (tid == 0) {
-      unsigned* c = a.claim + 16 * a.cpar;
+      unsigned* c = a.claim + 32 * a.cpar;
       int r = -1;
       if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
         const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
@@ -112,12 +115,12 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       }
       if (r < 0) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
       if (b == 0)  // the other parity's counters (the previous launch is complete) for the next launch
-        for (int j = 0; j < 16; ++j)
-          __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int j = 0; j < 32; ++j)
+          __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = r;
     }
     __syncthreads();
-    const int r = role;
+    const int r = __builtin_amdgcn_readfirstlane(role);  // (uniform: lane / workgroup indices in SGPRs)
     __syncthreads();
     if (r < 0) {  // a rider: the previous round's evaluation
       eval_multi_body<FP>(lds, a.ev, -r - 1, a.nride);
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     barrier();
     phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
   }
-  if (!owner && !a.lane_eval) return;
+  if (!owner && !LE) return;
   if (owner) {
     if (wg == 0 && tid == 0) stamp(dv, 30, 4);
     // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   }
-  if (!a.lane_eval) return;
+  if constexpr (!LE) return;
   // ---- the lane's own evaluation of this round's local model (+ the previous update's
   // global model on lane 0), while the other lanes still solve ----
   if constexpr (S == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // fragments across XCDs
@@ -280,26 +283,30 @@ __global__ void xcc_probe_kernel(int* ids, int n) {
     ids[blockIdx.x] = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
 }
 
-template <int FP, int KP, int S>
+template <int FP, int KP, int S, bool LE>
 void set_lanes_attr() {
-  (void)hipFuncSetAttribute((const void*)lanes_round_kernel<FP, KP, S>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lanes_lds_bytes(FP));
+  (void)hipFuncSetAttribute((const void*)lanes_round_kernel<FP, KP, S, LE>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lanes_lds_bytes(FP));
 }
 
-template <int FP, int KP, int S>
+template <int FP, int KP, int S, bool LE>
 void launch_fks(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a, hipStream_t s) {
-  static const bool prepared = (set_lanes_attr<FP, KP, S>(), true);
+  static const bool prepared = (set_lanes_attr<FP, KP, S, LE>(), true);
   (void)prepared;
   const int grid = lanes_grid(a.L, a.nride);
-  lanes_round_kernel<FP, KP, S><<<grid, 256, lanes_lds_bytes(FP), s>>>(cfg, lanes, a);
+  lanes_round_kernel<FP, KP, S, LE><<<grid, 256, lanes_lds_bytes(FP), s>>>(cfg, lanes, a);
 }
 
+// Lane evaluation is only built for the XCD-resident form (S == 2, the MI355X
+// default); LanesLoop never asks for it with S == 1.
 template <int FP, int KP>
 void launch_fk(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a, int S, hipStream_t s) {
-  if (S == 2)
-    launch_fks<FP, KP, 2>(cfg, lanes, a, s);
+  if (S == 2 && a.lane_eval)
+    launch_fks<FP, KP, 2, true>(cfg, lanes, a, s);
+  else if (S == 2)
+    launch_fks<FP, KP, 2, false>(cfg, lanes, a, s);
   else
-    launch_fks<FP, KP, 1>(cfg, lanes, a, s);
+    launch_fks<FP, KP, 1, false>(cfg, lanes, a, s);
 }
 
 template <int FP>
@@ -342,7 +349,7 @@ namespace {
 template <int FP>
 __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
   __shared__ f32x4 red[4][64];
-  __shared__ int cl[kMaxEvalModels][16][8];
+  __shared__ int cl[kMaxEvalModels][16][8];  // (>= kMaxEvalModels * 64 + kMaxEvalModels ints: publish_counts' cells)
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int K = ev.K, T = ev.T, M = ev.nmodels;
@@ -360,7 +367,7 @@ __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
     const int ma = 2 * p, mb = 2 * p + 1 < M ? 2 * p + 1 : -1;
     const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb >= 0 ? mb : 0);
     if (p != curp) {  // (workgroup-uniform)
-      load_pair_frags<FP>(wf, &A, mb >= 0 ? &Bm : nullptr, K);
+      load_pair_frags<FP>(wf, A, Bm, mb >= 0, K);
       curp = p;
     }
     const int64_t row = (int64_t)tile * 16 + r;
@@ -411,7 +418,7 @@ __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
     last = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  publish_counts(ev, M, tid);
+  publish_counts(ev, M, tid, &cl[0][0][0]);
 }
 
 }  // namespace

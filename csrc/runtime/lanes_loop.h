@@ -145,8 +145,8 @@ class LanesLoop {
   // true: a round's rows are evaluated by a launch of their own on a side stream
   // that co-runs with the next round (8 lanes: no XCD left for riders)
   bool side_eval() const { return side_eval_; }
-  // true (default): each lane evaluates its own local model inside the round kernel
-  // (PSX_LANES_RIDERS=1: the rider workgroups evaluate the previous round instead)
+  // true (PSX_LANES_LANE_EVAL=1): each lane evaluates its own local model inside the
+  // round kernel; false (default): the rider workgroups evaluate the previous round
   bool lane_eval() const { return lane_eval_; }
   double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
   int64_t rounds_run() const { return rounds_run_; }
@@ -228,6 +228,7 @@ class LanesLoop {
   // evaluation done -> the round that rewrites that parity's fragments)
   bool side_eval_ = false;
   bool lane_eval_ = true;
+  bool xcd_riders_ = true;
   int* lacc_ = nullptr;
   unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;

@@ -143,7 +143,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const size_t o_arr = take((FP / 32 + 1) * sizeof(unsigned));
   const size_t o_acc = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
   const size_t o_tic = take(8 * sizeof(unsigned));
-  const size_t o_claim = take(32 * sizeof(unsigned));
+  const size_t o_claim = take(64 * sizeof(unsigned));
   const size_t o_dsum = take((size_t)P_ * 4);
   const size_t o_uhi = take((size_t)16 * FP * 2), o_ulo = take((size_t)16 * FP * 2), o_ub = take(16 * 4);
   const size_t o_acc2 = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
@@ -225,8 +225,15 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // the riders keep a round at one launch
   const char* se = std::getenv("PSX_LANES_SIDE_EVAL");
   side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : false;
-  const char* rd = std::getenv("PSX_LANES_RIDERS");
-  lane_eval_ = cfg_.L > 0 && !side_eval_ && !(rd && rd[0] == '1');
+  // PSX_LANES_LANE_EVAL=1: each lane evaluates its own local model after its solve.  Off
+  // by default: with 8 lanes every XCD then streams the whole test set per round (8 x
+  // 10 MB): 113.5 against 100.8 us per round for the riders (profiles/r04_s1)
+  // PSX_RIDERS_XCD=0: riders take contiguous chunks of the whole test set instead of
+  // XCD-local slices (EvalMulti::xq)
+  const char* rx = std::getenv("PSX_RIDERS_XCD");
+  xcd_riders_ = !(rx && rx[0] == '0');
+  const char* le = std::getenv("PSX_LANES_LANE_EVAL");
+  lane_eval_ = cfg_.L > 0 && S_ == 2 && !side_eval_ && le && le[0] == '1';  // (built for S == 2 only)
   if (side_eval_) {
     hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side eval)");
     for (int p = 0; p < 2; ++p) {
@@ -454,11 +461,11 @@ void LanesLoop::submit_rows(const Pending& p, const std::vector<int>& slots, con
   SinkRecord rec[kMaxEvalModels];
   int n = 0;
   for (size_t i = 0; i < slots.size(); ++i)
-    if (kinds[i] == 1) rec[n++] = SinkRecord{slots[i], 1, seqs[i], -1, -1, p.vc, 0};
+    if (kinds[i] == 1) rec[n++] = SinkRecord{slots[i], 1 | kSinkTagged, seqs[i], -1, -1, p.vc, 0};
   int l = 0;
   for (size_t i = 0; i < slots.size(); ++i)
     if (kinds[i] == 0) {
-      rec[n++] = SinkRecord{slots[i], 0, seqs[i], -1, cfg_.k[l], p.vc, p.nseen[l]};
+      rec[n++] = SinkRecord{slots[i], kSinkTagged, seqs[i], -1, cfg_.k[l], p.vc, p.nseen[l]};
       ++l;
     }
   if (n) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), n, rec), "metrics sink submit");
@@ -568,6 +575,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.claim = claim_;
     a.cpar = (int)(launches_ & 1);
     a.xcd0 = cfg_.xcd0;
+    a.ev.xq = (xcd_riders_ && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
@@ -670,6 +678,7 @@ void LanesLoop::flush(hipStream_t stream) {
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
   a.xcd0 = cfg_.xcd0;
+  a.ev.xq = xcd_riders_ ? claim_ + 32 * a.cpar + 16 : nullptr;
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
     hip_check(hipGetLastError(), "lanes evaluation launch");
@@ -991,6 +1000,7 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   // local: the snapshot of the current weights (aticket_) + the slices' turn words;
   // remote: the ticket (= this rank's push order) only
   AsyncArgs a = aargs_;
+  a.lr = cfg_.lr;  // the server step (ServerProcessor.java:36): w += lr * delta
   a.log_lane = remote ? -1 : log_lane_;
   a.remote = remote ? 1 : 0;
   a.xcd0 = cfg_.xcd0;

@@ -292,14 +292,14 @@ def test_lanes_engine_producer_clock_cadence_and_deadline(cuda):
 
 @pytest.mark.parametrize("L", [1, 3, 8])
 def test_lane_evaluation_rows_equal_riders(cuda, monkeypatch, L):
-    """Each lane evaluating its own local model right after its solve (the default,
-    LanesArgs::lane_eval; lane 0 paired with the previous update's global model)
-    logs the same rows as the rider workgroups evaluating the previous round
-    (PSX_LANES_RIDERS=1): identical confusion counts, losses and clocks."""
+    """Each lane evaluating its own local model right after its solve
+    (PSX_LANES_LANE_EVAL=1, LanesArgs::lane_eval; lane 0 paired with the previous
+    update's global model) logs the same rows as the rider workgroups evaluating
+    the previous round (the default): identical confusion counts, losses, clocks."""
     spec, train, ev = _data(cuda)
     books = []
     for riders in ("1", "0"):
-        monkeypatch.setenv("PSX_LANES_RIDERS", riders)
+        monkeypatch.setenv("PSX_LANES_LANE_EVAL", "0" if riders == "1" else "1")
         w = spec.init("random", seed=6, device=cuda)
         log = LogSink(spec.K, cuda)
         lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log)

@@ -14,7 +14,11 @@ for s in $STEPS; do
   case $s in
     async)   # the asynchronous lanes loop's GPU tests
       timeout -k 10 ${ASYNC_TIMEOUT:-400} $PYT tests/test_gpu_async_lanes.py ${PYTEST_ARGS:-} > $OUT/pytest_async.log 2>&1
-      rc=$?; echo "async tests rc=$rc"; tail -15 $OUT/pytest_async.log
+      rc=$?; echo "async tests rc=$rc"; grep -E "PASS|FAIL|ERROR|assert" $OUT/pytest_async.log | tail -20
+      ok_rc $rc || exit $rc ;;
+    lanes)   # the lanes loops (BSP riders / lane evaluation, IPC ranks on one GPU)
+      timeout -k 10 ${LANES_TIMEOUT:-500} $PYT tests/test_gpu_lanes.py tests/test_gpu_ipc_lanes.py ${PYTEST_ARGS:-} > $OUT/pytest_lanes.log 2>&1
+      rc=$?; echo "lanes tests rc=$rc"; grep -E "PASS|FAIL|ERROR" $OUT/pytest_lanes.log | tail -30
       ok_rc $rc || exit $rc ;;
     tests)
       timeout -k 10 ${TEST_TIMEOUT:-600} $PYT tests -m gpu ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
@@ -29,6 +33,12 @@ for s in $STEPS; do
         timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
       rc=$?; echo "bench rc=$rc"; cat $OUT/bench_short.json | head -c 600; echo
       [ $rc -eq 0 ] || exit $rc ;;
+    ab)      # same-box A/B of the BSP round variants (driver form, 3 repeats each)
+      for v in "" "PSX_RIDERS_XCD=0" "PSX_LANES_LANE_EVAL=1" "" "PSX_RIDERS_XCD=0" "PSX_LANES_LANE_EVAL=1"; do
+        timeout -k 10 200 env $v python bench.py --steps ${AB_STEPS:-200} --warmup 20 ${BENCH_ARGS:-} > $OUT/ab.tmp 2>> $OUT/ab.err
+        rc=$?; [ $rc -eq 0 ] || { echo "ab [$v] rc=$rc"; exit $rc; }
+        echo "[$v] $(python -c "import json;d=json.load(open('$OUT/ab.tmp'));print(d['value'],d['ms_per_step'])")" | tee -a $OUT/ab.txt
+      done ;;
     ssp|asp)
       c=10; [ $s = asp ] && c=-1
       timeout -k 10 300 python bench.py --consistency $c --steps ${ASYNC_STEPS:-300} --warmup 30 ${BENCH_ARGS:-} > $OUT/bench_$s.json 2> $OUT/bench_$s.err

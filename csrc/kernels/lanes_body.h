@@ -272,6 +272,124 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
   rstamp(11);
 }
 
+// LDS of eval_tile_body: [pairs][4 waves][2 m-tiles][64 lanes] f32x4 partial logits,
+// then [kMaxEvalModels][256] counts, the publisher flag, [kMaxEvalModels][8]
+// intercepts and [32] labels.
+constexpr int kEvalPairs = (kMaxEvalModels + 1) / 2;
+constexpr size_t kEvalTileLds = (size_t)kEvalPairs * 8192 + kMaxEvalModels * 256 * 4 + 16 +
+                                kMaxEvalModels * 8 * 4 + 32 * 4;
+
+// Riders, tile-resident form: rider rid evaluates EVERY model on test tiles rid,
+// rid + nride, ...  The 32-row tile's MFMA A operands are loaded straight from
+// global memory into registers (no LDS staging) and stay there while the waves run
+// the model pairs' fragments past them, the next pair's fragments in flight during
+// the current pair's MFMAs; the test set is read once per round.  Each wave owns
+// the same K-slice and issues the same MFMA sequence as forward_tile_pre, and the
+// cross-wave sums run in the same order (load_logit), so the rows equal the
+// pair-major riders' bit for bit.  Counts: LDS atomics per tile, one flush per
+// rider, the last arrival publishes (publish_counts).
+template <int FP>
+__device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, int rid, int nride) {
+  if (ev.nmodels <= 0 || rid >= nride) return;
+  rid = __builtin_amdgcn_readfirstlane(rid);
+  long long* dbg = ev.dbg;
+  auto rstamp = [&](int k) {
+    if (dbg && threadIdx.x == 0) dbg[k] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  if (dbg && threadIdx.x == 0) {
+    const long long t = (long long)__builtin_amdgcn_s_memrealtime();
+    atomicMin((unsigned long long*)(dbg + 12), (unsigned long long)t);
+    atomicMax((unsigned long long*)(dbg + 13), (unsigned long long)t);
+  }
+  if (rid == 0) rstamp(0);
+  constexpr int KS = WFrag<FP>::KS;
+  char* red = lds;                                             // [kEvalPairs][8 KB]
+  int* cl = (int*)(lds + (size_t)kEvalPairs * 8192);           // [kMaxEvalModels][256]
+  int* lastp = cl + kMaxEvalModels * 256;
+  float* bl = (float*)(lastp + 4);                             // [kMaxEvalModels][8]
+  int* ylab = (int*)(bl + kMaxEvalModels * 8);                 // [32]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, kq = lane >> 4;
+  const int K = ev.K, T = ev.T, M = ev.nmodels, npairs = (M + 1) / 2;
+  const int nT = (T + 31) / 32;
+  for (int m = 0; m < M; ++m) cl[m * 256 + tid] = 0;
+#pragma unroll
+  for (int m = 0; m < kMaxEvalModels; ++m)  // (constant model indices: scalar kernel-argument loads)
+    if (m < M && tid < 8) bl[m * 8 + tid] = tid < K ? ev.m[m].b[ev.m[m].coff + tid] : 0.f;
+  auto load_pair = [&](WFrag<FP>& wf, int p) {
+    const int ma = 2 * p, mb = 2 * p + 1;
+    const EvalModel A = pick(ev.m, ma), Bm = pick(ev.m, mb < M ? mb : ma);
+    load_pair_frags<FP>(wf, A, Bm, mb < M, K);
+  };
+  bool first = true;
+  for (int tile = rid; tile < nT; tile += nride) {
+    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+    const int64_t row0 = (int64_t)tile * 32;
+    // the tile's A operands: rows r and 16 + r, wave w's k-steps (forward_tile_pre's)
+    u16x8 a0[KS], a1[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int cg = (w * KS + kk) * 4 + kq;
+      a0[kk] = r < nrows ? *(const u16x8*)(ev.Xt + (row0 + r) * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      a1[kk] = 16 + r < nrows ? *(const u16x8*)(ev.Xt + (row0 + 16 + r) * FP + cg * 8)
+                              : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    if (tid < 32) ylab[tid] = tid < nrows ? ev.yt[row0 + tid] : 0;
+    WFrag<FP> wc, wn;
+    load_pair(wc, 0);
+    for (int p = 0; p < npairs; ++p) {  // (uniform)
+      if (p + 1 < npairs) load_pair(wn, p + 1);
+      f32x4 acc0 = f32x4{0, 0, 0, 0}, acc1 = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wc.h[kk]), acc0);
+        acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wc.l[kk]), acc0);
+        acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wc.h[kk]), acc1);
+        acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wc.l[kk]), acc1);
+      }
+      store_partial_logits(red + (size_t)p * 8192, acc0, acc1);
+      if (p + 1 < npairs) wc = wn;
+    }
+    __syncthreads();
+    if (first && rid == 0) rstamp(1);
+    for (int it = tid; it < 32 * M; it += 256) {  // thread (row, model)
+      const int row = it & 31, m = it >> 5;
+      if (row < nrows) {
+        const char* rb = red + (size_t)(m >> 1) * 8192;
+        const int c0 = 8 * (m & 1);
+        int best = 0;
+        float bz = -INFINITY;
+        for (int c = 0; c < K; ++c) {
+          const float z = load_logit(rb, row, c0 + c) + bl[m * 8 + c];
+          if (z > bz) {
+            bz = z;
+            best = c;
+          }
+        }
+        const int yrow = ylab[row], yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
+        atomicAdd(&cl[m * 256 + yl * 16 + best], 1);
+      }
+    }
+    __syncthreads();  // (red / ylab are rewritten by the next tile)
+    first = false;
+  }
+  for (int m = 0; m < M; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(ev.acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (rid == 0) rstamp(8);
+  if (dbg && tid == 0)
+    atomicMax((unsigned long long*)(dbg + 14), (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ev.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ev.nticket - 1;
+  __syncthreads();
+  if (!*lastp) return;
+  rstamp(10);
+  publish_counts(ev, M, tid, cl);
+  rstamp(11);
+}
+
 // ---------------------------------------------------------------------------
 // Phase I of a lane's solve, row role: stage ring tile `rt` into the LDS image,
 // the round's new rows straight from the dataset (also written into the ring),

@@ -86,6 +86,9 @@ struct EvalMulti {
   // != nullptr: XCD-local evaluation -- [8] chunk counters (zero at launch): riders on
   // XCD x take chunks of the x-th eighth of the test tiles first (eval_multi_body)
   unsigned* xq;
+  // 0: pair-major riders (eval_multi_body: items = (model pair, tile)); 1: tile-resident
+  // riders (eval_tile_body: every model on a rider's tiles, the test set read once)
+  int form;
   // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
   // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the
   // ticket, [10] the last rider is known, [11] its publication done, [12] / [13] the

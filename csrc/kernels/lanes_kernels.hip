@@ -123,7 +123,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     const int r = __builtin_amdgcn_readfirstlane(role);  // (uniform: lane / workgroup indices in SGPRs)
     __syncthreads();
     if (r < 0) {  // a rider: the previous round's evaluation
-      eval_multi_body<FP>(lds, a.ev, -r - 1, a.nride);
+      if (a.ev.form == 1)
+        eval_tile_body<FP>(lds, a.ev, -r - 1, a.nride);
+      else
+        eval_multi_body<FP>(lds, a.ev, -r - 1, a.nride);
       return;
     }
     l = r / kLaneWg;

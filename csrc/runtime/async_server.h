@@ -119,7 +119,11 @@ class HostP2P : public P2P {
   size_t cap_, map_bytes_ = 0;
   double timeout_s_;
   char* base_ = nullptr;
-  std::vector<char> bounce_;
+  // pinned staging (device ranks): the copies run on the DMA engines, so a rank whose
+  // CUs are held by a persistent launch still moves its messages
+  char* bounce_ = nullptr;
+  size_t bounce_bytes_ = 0;
+  char* staging(size_t bytes);
 };
 
 struct AsyncServerCfg {

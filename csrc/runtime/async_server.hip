@@ -98,6 +98,7 @@ HostP2P::HostP2P(const std::string& name, int nworkers, int rank, bool create, b
 }
 
 HostP2P::~HostP2P() {
+  if (bounce_) (void)hipHostFree(bounce_);
   if (base_) munmap(base_, map_bytes_);
   if (owner_) shm_unlink(name_.c_str());
 }
@@ -187,10 +188,20 @@ void HostP2P::send(const void* buf, size_t count, int dtype, int peer, hipStream
     write(c, static_cast<const char*>(buf), bytes);
     return;
   }
-  bounce_.resize(bytes);  // stream order: the producer of buf first
+  char* st = staging(bytes);  // stream order: behind the producer of buf on s
+  hip_check(hipMemcpyAsync(st, buf, bytes, hipMemcpyDeviceToHost, s), "HostP2P send staging");
   hip_check(hipStreamSynchronize(s), "HostP2P send sync");
-  hip_check(hipMemcpy(bounce_.data(), buf, bytes, hipMemcpyDeviceToHost), "HostP2P send staging");
-  write(c, bounce_.data(), bytes);
+  write(c, st, bytes);
+}
+
+char* HostP2P::staging(size_t bytes) {
+  if (bytes > bounce_bytes_) {
+    if (bounce_) hip_check(hipHostFree(bounce_), "hipHostFree");
+    bounce_ = nullptr;
+    hip_check(hipHostMalloc((void**)&bounce_, bytes, hipHostMallocDefault), "HostP2P staging");
+    bounce_bytes_ = bytes;
+  }
+  return bounce_;
 }
 
 void HostP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) {
@@ -200,9 +211,10 @@ void HostP2P::recv(void* buf, size_t count, int dtype, int peer, hipStream_t s) 
     read(c, static_cast<char*>(buf), bytes);
     return;
   }
-  bounce_.resize(bytes);
-  read(c, bounce_.data(), bytes);
-  hip_check(hipMemcpyAsync(buf, bounce_.data(), bytes, hipMemcpyHostToDevice, s), "HostP2P recv staging");
+  char* st = staging(bytes);
+  hip_check(hipStreamSynchronize(s), "HostP2P recv sync");  // (the staging buffer's previous copy)
+  read(c, st, bytes);
+  hip_check(hipMemcpyAsync(buf, st, bytes, hipMemcpyHostToDevice, s), "HostP2P recv staging");
   hip_check(hipStreamSynchronize(s), "HostP2P recv sync");
 }
 
@@ -314,8 +326,12 @@ void LocalFeeder::run(int k) {
 AsyncServer::AsyncServer(P2P* comm, const AsyncServerCfg& cfg, hipStream_t stream)
     : comm_(comm), cfg_(cfg), stream_(stream) {
   if (!comm_) throw std::invalid_argument("AsyncServer: null transport");
-  if (cfg.nworkers < 1 || comm_->size() != cfg.nworkers + 1)
+  // one rank per worker, or (peer map) several workers per worker rank: every
+  // worker's rank in [1, size)
+  if (cfg.nworkers < 1 || (cfg.peer.empty() ? comm_->size() != cfg.nworkers + 1 : comm_->size() < 2))
     throw std::invalid_argument("AsyncServer: the communicator must hold the server + every worker");
+  for (int p : cfg.peer)
+    if (p < 1 || p >= comm_->size()) throw std::invalid_argument("AsyncServer: a worker's peer rank is outside the communicator");
   if (!cfg.api || !cfg.tracker || !cfg.ctrl) throw std::invalid_argument("AsyncServer: missing host runtime handles");
   api_ = reinterpret_cast<const HostApi*>(cfg.api);
   if (api_->version != kHostApiVersion) throw std::runtime_error("AsyncServer: host runtime C ABI version mismatch");

@@ -228,7 +228,8 @@ class LanesLoop {
   // evaluation done -> the round that rewrites that parity's fragments)
   bool side_eval_ = false;
   bool lane_eval_ = true;
-  bool xcd_riders_ = true;
+  bool xcd_riders_ = false;
+  bool tile_riders_ = false;
   int* lacc_ = nullptr;
   unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;

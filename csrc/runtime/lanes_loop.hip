@@ -227,11 +227,17 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   side_eval_ = se ? (se[0] == '1' && cfg_.L > 0) : false;
   // PSX_LANES_LANE_EVAL=1: each lane evaluates its own local model after its solve.  Off
   // by default: with 8 lanes every XCD then streams the whole test set per round (8 x
-  // 10 MB): 113.5 against 100.8 us per round for the riders (profiles/r04_s1)
-  // PSX_RIDERS_XCD=0: riders take contiguous chunks of the whole test set instead of
-  // XCD-local slices (EvalMulti::xq)
+  // 10 MB): 101.2 against 95.8 us per round for the riders (profiles/r04_s3, same box)
+  // PSX_RIDERS_XCD=1: riders take XCD-local slices of the test set from per-XCD chunk
+  // queues (EvalMulti::xq) instead of contiguous chunks of the whole set.  Off by
+  // default: 113.1 against 95.8 us per round (profiles/r04_s3) -- the queue pops and
+  // the per-slice pair reloads cost more than the L2 locality returns
+  // PSX_RIDERS_TILE=1: tile-resident riders (eval_tile_body: a rider holds its test tile
+  // in registers and runs every model pair past it; the test set is read once per round)
+  const char* rt = std::getenv("PSX_RIDERS_TILE");
+  tile_riders_ = rt && rt[0] == '1';
   const char* rx = std::getenv("PSX_RIDERS_XCD");
-  xcd_riders_ = !(rx && rx[0] == '0');
+  xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
   lane_eval_ = cfg_.L > 0 && S_ == 2 && !side_eval_ && le && le[0] == '1';  // (built for S == 2 only)
   if (side_eval_) {
@@ -358,7 +364,7 @@ int LanesLoop::rider_count(int nmodels, int L) const {
   // solves) enough riders to run after the lanes; a launch has grid - L * 32
   int extra = 0;
   if (nmodels > 0 && L == 8) {
-    const int nT = (cfg_.T + 31) / 32, items = (nmodels + 1) / 2 * nT;
+    const int nT = (cfg_.T + 31) / 32, items = tile_riders_ ? nT : (nmodels + 1) / 2 * nT;
     extra = items < 256 ? items : 256;
   }
   return lanes_grid(L, extra) - L * kLaneWg;
@@ -404,6 +410,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
   for (int l = 0; l < nw; ++l)
     add(l, lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
+  ev->form = tile_riders_ ? 1 : 0;
   ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
   ev->dbg = rider_dbg_;
 }
@@ -575,7 +582,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.claim = claim_;
     a.cpar = (int)(launches_ & 1);
     a.xcd0 = cfg_.xcd0;
-    a.ev.xq = (xcd_riders_ && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
+    a.ev.xq = (xcd_riders_ && !tile_riders_ && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
@@ -678,7 +685,7 @@ void LanesLoop::flush(hipStream_t stream) {
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
   a.xcd0 = cfg_.xcd0;
-  a.ev.xq = xcd_riders_ ? claim_ + 32 * a.cpar + 16 : nullptr;
+  a.ev.xq = (xcd_riders_ && !tile_riders_) ? claim_ + 32 * a.cpar + 16 : nullptr;
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
     hip_check(hipGetLastError(), "lanes evaluation launch");

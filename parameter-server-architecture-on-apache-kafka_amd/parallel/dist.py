@@ -33,8 +33,9 @@ AsyncServer (csrc/runtime/async_server.h) -- pops tokens in arrival order (= the
 single GRADIENTS_TOPIC partition), receives from that worker, applies, and sends
 the new weights to every worker the tracker releases.  The data plane is RCCL
 point-to-point over xGMI (one rank per GPU) or, for ranks without an RCCL
-communicator (CPU / gloo runs), the host shared-memory transport HostP2P with
-the same per-peer message order.  A worker always posts its recv right after
+communicator (CPU / gloo runs) and for worker ranks that host several workers as
+lanes of one persistent launch (whose CUs an RCCL kernel could not share), the
+host shared-memory transport HostP2P with the same per-peer message order.  A worker always posts its recv right after
 its send and the server only receives from workers whose token it has seen, so
 the send/recv graph is acyclic (deadlock free).
 """
@@ -805,7 +806,12 @@ class DistEngine:
     def _run_async(self) -> dict:
         if not hasattr(self, "comm"):  # collective: every rank creates it (None on gloo / CPU)
             self.comm = make_comm(self.rank, self.world, self.device)
-        self._open_ctrl(host_p2p=self.comm is None)
+        # several workers per worker rank (the asynchronous lanes loop): its persistent
+        # launch holds every CU of the lanes' XCDs, and an RCCL p2p kernel would have to
+        # co-reside there -- the pushes / pulls (P floats each) go through the host
+        # shared-memory data plane instead, staged by the DMA engines (all ranks share
+        # the node)
+        self._open_ctrl(host_p2p=self.comm is None or self.wpr > 1)
         try:
             if self.is_server:  # ONE server loop: the native one (RCCL p2p, or HostP2P without RCCL)
                 return self._server_loop_native()

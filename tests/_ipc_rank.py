@@ -36,6 +36,8 @@ def main():
     from psx.utils.data import synth_finefood
 
     rank, world, device = init_from_env()
+    if mode.startswith("async") and rank == 0:  # (see test_async_lanes_worker_ranks)
+        device = torch.device("cpu")
     train, test = synth_finefood(20000, seed=0), synth_finefood(4877, seed=1)
     eng = DistEngine(cfg_for(world, mode), rank, world, device, train=train, test=test)
     kind = None

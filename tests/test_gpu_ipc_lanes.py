@@ -26,23 +26,28 @@ def _port():
         return s.getsockname()[1]
 
 
-def _launch(tmp, mode, world=3, timeout=150):
+def _launch(tmp, mode, world=3, timeout=100):
     port = str(_port())
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=port, PSX_GPU_OVERSUBSCRIBE="1", PSX_PG_TIMEOUT_S="120")
+        log = open(os.path.join(tmp, f"{mode}_rank{r}.log"), "w")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_ipc_rank.py"), str(tmp), mode],
-                                      env=env))
+                                      env=env, stdout=log, stderr=subprocess.STDOUT))
     rcs = []
     try:
         for p in procs:
             rcs.append(p.wait(timeout=timeout))
+    except subprocess.TimeoutExpired:
+        rcs.append("timeout")
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    assert rcs == [0] * world, rcs
+    if rcs != [0] * world:
+        tails = [open(os.path.join(tmp, f"{mode}_rank{r}.log")).read()[-1500:] for r in range(world)]
+        raise AssertionError(f"{rcs}\n" + "\n".join(f"--- rank {r}:\n{t}" for r, t in enumerate(tails)))
     return [json.load(open(os.path.join(tmp, f"{mode}_rank{r}.json"))) for r in range(world)]
 
 
@@ -90,7 +95,10 @@ def test_async_lanes_worker_ranks(cuda, tmp_path, mode, bound):
     """SSP(2) / ASP across processes: 1 server rank (the native AsyncServer) + 2
     worker ranks whose 3 workers each are lanes of one persistent launch
     (LanesLoop.run_async_remote), every delta pushed with its token and every
-    release answered through the rank's reply queue (ServerProcessor.java:95-183)."""
+    release answered through the rank's reply queue (ServerProcessor.java:95-183).
+    The server rank runs on the CPU here: on a shared GPU its kernels would wait
+    for the CUs the worker ranks' persistent launches hold (on the node every rank
+    has its own GPU)."""
     res = _launch(tmp_path, mode)
     assert all(r.get("async_lanes") for r in res[1:]), res
     assert res[0]["updates"] == 6 * 8, res[0]

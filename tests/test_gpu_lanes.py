@@ -313,3 +313,47 @@ def test_lane_evaluation_rows_equal_riders(cuda, monkeypatch, L):
     a, b = books
     assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 5
     assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 5 * L
+
+
+@pytest.mark.parametrize("L", [3, 8])
+def test_xcd_local_riders_rows_equal_riders(cuda, monkeypatch, L):
+    """Riders popping XCD-local slices of the test set from per-XCD chunk queues
+    (PSX_RIDERS_XCD=1, EvalMulti::xq; every chunk exactly once, stealing across
+    XCDs) log the same rows as the default contiguous chunks."""
+    spec, train, ev = _data(cuda)
+    books = []
+    for xq in ("0", "1"):
+        monkeypatch.setenv("PSX_RIDERS_XCD", xq)
+        w = spec.init("random", seed=6, device=cuda)
+        log = LogSink(spec.K, cuda)
+        lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log)
+        lp.run(4, 0, stream_handle(cuda))
+        lp.flush(stream_handle(cuda))
+        torch.cuda.synchronize()
+        books.append(log.book)
+        log.close()
+    a, b = books
+    assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 4
+    assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L
+
+
+@pytest.mark.parametrize("L", [3, 8])
+def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L):
+    """Riders holding their test tile in registers and running every model pair past
+    it (PSX_RIDERS_TILE=1, eval_tile_body: the test set read once per round) log
+    the same rows, bit for bit, as the pair-major riders (eval_multi_body)."""
+    spec, train, ev = _data(cuda)
+    books = []
+    for form in ("0", "1"):
+        monkeypatch.setenv("PSX_RIDERS_TILE", form)
+        w = spec.init("random", seed=6, device=cuda)
+        log = LogSink(spec.K, cuda)
+        lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log)
+        lp.run(4, 0, stream_handle(cuda))
+        lp.flush(stream_handle(cuda))
+        torch.cuda.synchronize()
+        books.append(log.book)
+        log.close()
+    a, b = books
+    assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 4
+    assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L

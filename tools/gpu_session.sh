@@ -34,7 +34,9 @@ for s in $STEPS; do
       rc=$?; echo "bench rc=$rc"; cat $OUT/bench_short.json | head -c 600; echo
       [ $rc -eq 0 ] || exit $rc ;;
     ab)      # same-box A/B of the BSP round variants (driver form, 3 repeats each)
-      for v in "" "PSX_RIDERS_XCD=0" "PSX_LANES_LANE_EVAL=1" "" "PSX_RIDERS_XCD=0" "PSX_LANES_LANE_EVAL=1"; do
+      # AB_VARIANTS: space-separated env assignments, "-" = the defaults
+      for v in ${AB_VARIANTS:-- PSX_LANES_LANE_EVAL=1 - PSX_LANES_LANE_EVAL=1}; do
+        [ "$v" = "-" ] && v=""
         timeout -k 10 200 env $v python bench.py --steps ${AB_STEPS:-200} --warmup 20 ${BENCH_ARGS:-} > $OUT/ab.tmp 2>> $OUT/ab.err
         rc=$?; [ $rc -eq 0 ] || { echo "ab [$v] rc=$rc"; exit $rc; }
         echo "[$v] $(python -c "import json;d=json.load(open('$OUT/ab.tmp'));print(d['value'],d['ms_per_step'])")" | tee -a $OUT/ab.txt

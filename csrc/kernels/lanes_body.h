@@ -45,6 +45,14 @@ __device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigne
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
 }
 
+static_assert(kEvalAccInts == (size_t)kAccCopies * kMaxEvalModels * 256 * kAccStride, "EvalMulti::acc size");
+
+// Accumulator cell of model m in copy `copy` (EvalMulti::acc)
+__device__ __forceinline__ int* acc_cell(int* acc, int copy, int m, int cell) {
+  return acc + ((size_t)(copy * kMaxEvalModels + m) * 256 + cell) * kAccStride;
+}
+__device__ __forceinline__ int xcd_copy() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u); }
+
 // ---------------------------------------------------------------------------
 // Riders: evaluation of up to kMaxEvalModels models (the previous round's
 // local models and global model) over the test tiles.  Work items = (model
@@ -85,23 +93,42 @@ __device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel& 
 // sequence number, so the publication costs the workgroup no PCIe round trip.
 __device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid, int* cells) {
   const int K = ev.K, KK = K * K;
-  const int t16 = tid >> 4, p16 = tid & 15;
-  const bool cell = t16 < K && p16 < K;
-  int tot[kMaxEvalModels];
-#pragma unroll
-  for (int m = 0; m < kMaxEvalModels; ++m)
-    tot[m] = (m < M && cell) ? __hip_atomic_exchange(ev.acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)
-                             : 0;
+  // the counts of the kAccCopies accumulator copies: items (copy, model, cell) dealt
+  // to the threads, every sc1 load (past this XCD's L2: the adds were performed in
+  // memory) in flight together, summed with LDS atomics; then the copies zeroed
   float lv = 0.f;  // (constant model indices: a per-thread index would copy ev.m into scratch)
 #pragma unroll
   for (int m = 0; m < kMaxEvalModels; ++m)
     if (m < M && tid == m && ev.m[m].loss) lv = *ev.m[m].loss;
-  __syncthreads();  // (the caller's counts in `cells` were consumed)
-#pragma unroll
-  for (int m = 0; m < kMaxEvalModels; ++m)
-    if (m < M && cell) cells[m * KK + t16 * K + p16] = tot[m];
+  for (int i = tid; i < M * KK; i += 256) cells[i] = 0;  // (the caller's counts were flushed)
   if (tid < M) cells[kMaxEvalModels * 64 + tid] = __float_as_int(lv);
+  __syncthreads();
+  const int n = kAccCopies * M * KK;
+  const auto ra = rsrc_of(ev.acc, (unsigned)(kEvalAccInts * 4));
+  auto off_of = [&](int q) {  // byte offset of item q's accumulator cell
+    const int c = q / (M * KK), r = q - c * (M * KK), m = r / KK, ci = r - m * KK;
+    const int t16 = ci / K, p16 = ci - t16 * K;
+    return (unsigned)(((c * kMaxEvalModels + m) * 256 + t16 * 16 + p16) * kAccStride * 4);
+  };
+  constexpr int kPer = (kAccCopies * kMaxEvalModels * 64 + 255) / 256;  // items per thread (max)
+  for (int q0 = 0; q0 < n; q0 += 256 * kPer) {  // (one pass for K <= 8)
+    int v[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = q0 + tid + 256 * j;
+      v[j] = q < n ? (int)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)off_of(q), 0, kAuxSc1) : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = q0 + tid + 256 * j;
+      if (q < n && v[j]) atomicAdd(&cells[q % (M * KK)], v[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int q = q0 + tid + 256 * j;
+      if (q < n && v[j]) __builtin_amdgcn_raw_buffer_store_b32(0u, ra, (int)off_of(q), 0, kAuxSc1);
+    }
+  }
   __syncthreads();
   if (tid == 0) __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // wave w publishes models w, w + 4, ... (nch <= 23 chunks: one per lane); the model
@@ -254,9 +281,12 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
     }
   }
   __syncthreads();
-  for (int m = 0; m < M; ++m) {
-    const int v = cl[m * 256 + tid];
-    if (v) atomicAdd(ev.acc + (m * 256 + tid) * kAccStride, v);
+  {
+    const int cp = xcd_copy();
+    for (int m = 0; m < M; ++m) {
+      const int v = cl[m * 256 + tid];
+      if (v) atomicAdd(acc_cell(ev.acc, cp, m, tid), v);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -277,7 +307,7 @@ __device__ __forceinline__ void eval_multi_body(char* lds, const EvalMulti& ev, 
 // intercepts and [32] labels.
 constexpr int kEvalPairs = (kMaxEvalModels + 1) / 2;
 constexpr size_t kEvalTileLds = (size_t)kEvalPairs * 8192 + kMaxEvalModels * 256 * 4 + 16 +
-                                kMaxEvalModels * 8 * 4 + 32 * 4;
+                                kMaxEvalModels * 8 * 4 + 32 * 4 + 16;
 
 // Riders, tile-resident form: rider rid evaluates EVERY model on test tiles rid,
 // rid + nride, ...  The 32-row tile's MFMA A operands are loaded straight from
@@ -288,7 +318,8 @@ constexpr size_t kEvalTileLds = (size_t)kEvalPairs * 8192 + kMaxEvalModels * 256
 // cross-wave sums run in the same order (load_logit), so the rows equal the
 // pair-major riders' bit for bit.  Counts: LDS atomics per tile, one flush per
 // rider, the last arrival publishes (publish_counts).
-template <int FP>
+// (kStop < 3: tools/eval_probe.hip's cost split -- 1: the tiles only, 2: + the flush)
+template <int FP, int kStop = 3>
 __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, int rid, int nride) {
   if (ev.nmodels <= 0 || rid >= nride) return;
   rid = __builtin_amdgcn_readfirstlane(rid);
@@ -321,7 +352,18 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     load_pair_frags<FP>(wf, A, Bm, mb < M, K);
   };
   bool first = true;
-  for (int tile = rid; tile < nT; tile += nride) {
+  // tiles popped from ev.xq[0] (riders entering early take more of them); without a
+  // queue, tiles rid, rid + nride, ...
+  int* tq = ylab + 32;
+  auto pop = [&](int fallback) {
+    if (!ev.xq) return fallback;
+    if (tid == 0) *tq = (int)__hip_atomic_fetch_add(ev.xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(*tq);
+    __syncthreads();
+    return t;
+  };
+  for (int tile = pop(rid); tile < nT; tile = pop(tile + nride)) {
     const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
     const int64_t row0 = (int64_t)tile * 32;
     // the tile's A operands: rows r and 16 + r, wave w's k-steps (forward_tile_pre's)
@@ -372,12 +414,17 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     __syncthreads();  // (red / ylab are rewritten by the next tile)
     first = false;
   }
-  for (int m = 0; m < M; ++m) {
-    const int v = cl[m * 256 + tid];
-    if (v) atomicAdd(ev.acc + (m * 256 + tid) * kAccStride, v);
+  if constexpr (kStop == 1) return;
+  {
+    const int cp = xcd_copy();
+    for (int m = 0; m < M; ++m) {
+      const int v = cl[m * 256 + tid];
+      if (v) atomicAdd(acc_cell(ev.acc, cp, m, tid), v);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (kStop == 2) return;
   if (rid == 0) rstamp(8);
   if (dbg && tid == 0)
     atomicMax((unsigned long long*)(dbg + 14), (unsigned long long)__builtin_amdgcn_s_memrealtime());

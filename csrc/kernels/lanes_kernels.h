@@ -41,6 +41,11 @@ namespace psx {
 constexpr int kMaxLanes = 8;
 constexpr int kLaneWg = 32;  // cooperating workgroups per lane: the CUs of one XCD
 constexpr int kMaxEvalModels = kMaxLanes + 1;
+// EvalMulti accumulators: one copy per XCD, [kAccCopies][kMaxEvalModels][256 cells] at
+// stride kAccStride -- a rider adds into its own XCD's copy, so a cell takes ~1/8 of
+// the device-scope atomics (one copy: 8.4 us for 256 riders' flush, tools/eval_probe)
+constexpr int kAccCopies = 8;
+constexpr size_t kEvalAccInts = (size_t)kAccCopies * kMaxEvalModels * 256 * 32;
 
 // Per-lane device state (a device-resident table read by the lane's workgroups).
 struct LaneDev {
@@ -80,14 +85,15 @@ struct EvalMulti {
   int T, K;
   int nmodels;  // 0: nothing to evaluate
   EvalModel m[kMaxEvalModels];
-  int* acc;          // [kMaxEvalModels][256] private accumulators (stride kAccStride), zero between passes
+  int* acc;          // [kAccCopies][kMaxEvalModels][256] accumulators (stride kAccStride), zero between passes
   unsigned* ticket;  // arrivals of the riders (reset by the last)
   unsigned nticket;
   // != nullptr: XCD-local evaluation -- [8] chunk counters (zero at launch): riders on
   // XCD x take chunks of the x-th eighth of the test tiles first (eval_multi_body)
   unsigned* xq;
   // 0: pair-major riders (eval_multi_body: items = (model pair, tile)); 1: tile-resident
-  // riders (eval_tile_body: every model on a rider's tiles, the test set read once)
+  // riders (eval_tile_body: every model on a rider's tiles, the test set read once; the
+  // tiles popped from xq[0], zero at launch)
   int form;
   // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
   // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the

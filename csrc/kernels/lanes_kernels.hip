@@ -410,10 +410,11 @@ __global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
     }
     __syncthreads();
   }
+  const int cp = xcd_copy();
   for (int m = 0; m < M; ++m)
     if (tid < 128) {
       const int v = cl[m][tid >> 3][tid & 7];
-      if (v) atomicAdd(ev.acc + (m * 256 + (tid >> 3) * 16 + (tid & 7)) * kAccStride, v);
+      if (v) atomicAdd(acc_cell(ev.acc, cp, m, (tid >> 3) * 16 + (tid & 7)), v);
     }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

@@ -141,12 +141,12 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   }
   const size_t o_tab = take(sizeof(LaneDev) * (cfg_.L > 0 ? cfg_.L : 1));
   const size_t o_arr = take((FP / 32 + 1) * sizeof(unsigned));
-  const size_t o_acc = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
+  const size_t o_acc = take(kEvalAccInts * sizeof(int));
   const size_t o_tic = take(8 * sizeof(unsigned));
   const size_t o_claim = take(64 * sizeof(unsigned));
   const size_t o_dsum = take((size_t)P_ * 4);
   const size_t o_uhi = take((size_t)16 * FP * 2), o_ulo = take((size_t)16 * FP * 2), o_ub = take(16 * 4);
-  const size_t o_acc2 = take((size_t)kMaxEvalModels * 256 * kAccStride * sizeof(int));
+  const size_t o_acc2 = take(kEvalAccInts * sizeof(int));
   const size_t o_tic2 = take(8 * sizeof(unsigned));
   const size_t o_sfl = take(8 * sizeof(unsigned));
   const size_t o_lacc = take((size_t)kMaxLanes * 2 * 256 * kAccStride * sizeof(int));
@@ -582,7 +582,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.claim = claim_;
     a.cpar = (int)(launches_ & 1);
     a.xcd0 = cfg_.xcd0;
-    a.ev.xq = (xcd_riders_ && !tile_riders_ && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
+    // (the tile-resident riders pop their tiles from the first of these counters)
+    a.ev.xq = ((xcd_riders_ || tile_riders_) && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
     a.spin_max = r == inject_round_ ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
@@ -685,7 +686,7 @@ void LanesLoop::flush(hipStream_t stream) {
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
   a.xcd0 = cfg_.xcd0;
-  a.ev.xq = (xcd_riders_ && !tile_riders_) ? claim_ + 32 * a.cpar + 16 : nullptr;
+  a.ev.xq = (xcd_riders_ || tile_riders_) ? claim_ + 32 * a.cpar + 16 : nullptr;
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
     hip_check(hipGetLastError(), "lanes evaluation launch");
@@ -998,7 +999,23 @@ void LanesLoop::stop_all(hipStream_t stream) {
   std::memset(&q, 0, sizeof(q));
   q.stop = 1;
   for (int l = 0; l < cfg_.L; ++l) write_release(l, q);
-  hip_check(hipStreamSynchronize(astream_), "asynchronous launch drain");
+  // the launch drains once every workgroup has been dispatched and returned; a bounded
+  // wait turns a launch that cannot drain into an error that says how far dispatch got
+  const double t0 = epoch_ms();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(astream_);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) hip_check(e, "asynchronous launch drain");
+    if (epoch_ms() - t0 > 30000.0) {
+      unsigned c[32] = {0};
+      (void)hipMemcpy(c, claim_ + 32 * ((launches_ - 1) & 1), sizeof(c), hipMemcpyDeviceToHost);
+      std::string m = "LanesLoop: the asynchronous launch did not drain in 30 s; workgroups dispatched per XCD"
+                      " (lane claims 0..7, others):";
+      for (int j = 0; j < 9; ++j) m += " " + std::to_string(c[j]);
+      throw std::runtime_error(m);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
   hip_check(hipEventRecord(aev_out_, astream_), "async order out");  // the caller's later work after it
   hip_check(hipStreamWaitEvent(stream, aev_out_, 0), "async order out");
 }

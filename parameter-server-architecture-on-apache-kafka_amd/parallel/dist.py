@@ -200,7 +200,9 @@ class DistEngine:
         n_workers = n_worker_ranks * wpr
         if n_worker_ranks < 1:
             raise ValueError("need at least one worker rank (world size >= 2 with a dedicated server)")
-        if wpr > 1 and ((not self.async_mode and cfg.bsp_schedule == "sharded") or torch.device(device).type != "cuda"):
+        hosts_workers = not (self.dedicated and rank == 0)  # (a dedicated server rank hosts none)
+        if wpr > 1 and ((not self.async_mode and cfg.bsp_schedule == "sharded")
+                        or (hosts_workers and torch.device(device).type != "cuda")):
             raise ValueError("several workers per rank: BSP (allreduce / reduce_bcast) or SSP / ASP on GPUs only "
                              "(the multi-lane loops, csrc/runtime/lanes_loop.h)")
         self.wpr = wpr
@@ -224,6 +226,12 @@ class DistEngine:
 
             cfg.solver = dataclasses.replace(cfg.solver, persist=True)
         self.spec, train, test = load_datasets(cfg, train, test)
+        if int(train.rows) < cfg.num_workers:
+            # worker k's round-robin shard (rows k, k + N, ...) would be empty: its rank's
+            # native loop would stop on its own while the peers enter the round's
+            # collectives.  Every rank holds the same data, so every rank raises here.
+            raise ValueError(f"{int(train.rows)} training rows for {cfg.num_workers} workers: "
+                             "every worker needs a non-empty round-robin shard")
         self.wide = is_wide(self.spec)
         # wide model: collectives and dense p2p pushes need the dense delta;
         # SSP/ASP with sparse_push send (feature ids, values) instead

@@ -19,7 +19,8 @@ def cfg_for(world: int, mode: str):
         c = -1 if mode == "async_asp" else 2
         return PSConfig(num_workers=(world - 1) * 3, consistency_model=c, producer_time_per_event=0,
                         stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=8, min_buffer_size=128,
-                        max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3)
+                        max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3,
+                        worker_timeout_s=25.0)  # (a stuck transport raises with its reason, inside the test's limit)
     return PSConfig(num_workers=(world - 1) * 4, consistency_model=0, producer_time_per_event=0,
                     stream_mode="per_iter", rows_per_iter=1024, epochs=1000,
                     max_iters=6 if mode == "bounded" else 0, max_wallclock_s=0.0 if mode == "bounded" else 1.5,
@@ -29,6 +30,9 @@ def cfg_for(world: int, mode: str):
 
 def main():
     out_dir, mode = sys.argv[1], sys.argv[2]
+    import faulthandler
+
+    faulthandler.dump_traceback_later(80, exit=True)  # a hang names its frames (before the test's limit)
     import torch
     import torch.distributed as dist
 

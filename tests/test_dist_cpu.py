@@ -264,3 +264,21 @@ def test_native_comm_unique_id_exchange():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ids == [bytes(range(128))] * 2 for ids in got.values())
+
+
+def test_empty_worker_shard_rejected_on_every_rank():
+    """Fewer training rows than workers: a worker's round-robin shard would be empty
+    and its rank's native loop would stop alone while the peers wait in the round's
+    collectives.  Every rank holds the same data, so every rank raises
+    at construction, before any collective."""
+    import pytest
+
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+    from psx.utils.data import synth_finefood
+
+    cfg = PSConfig(num_workers=4, consistency_model=0, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=8, max_iters=2, server_colocated=False)
+    for rank in range(5):
+        with pytest.raises(ValueError, match="non-empty round-robin shard"):
+            DistEngine(cfg, rank, 5, "cpu", train=synth_finefood(3, seed=0), test=synth_finefood(16, seed=1))

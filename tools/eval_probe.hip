@@ -35,9 +35,35 @@ __global__ __launch_bounds__(256) void pair_major_kernel(EvalMulti ev, int nride
   eval_multi_body<FP>(lds, ev, (int)blockIdx.x, nride);
 }
 
-__global__ __launch_bounds__(256) void tile_resident_kernel(EvalMulti ev, int nride) {
+// q != nullptr: the tiles popped from q[32 * par] (cleared for the other parity, as the
+// round kernel's claim counters)
+template <int kStop = 3>
+__global__ __launch_bounds__(256) void tile_resident_kernel(EvalMulti ev, int nride, unsigned* q, int par) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  eval_tile_body<FP>(lds, ev, (int)blockIdx.x, nride);
+  if (q && blockIdx.x == 0 && threadIdx.x == 0) q[32 * (par ^ 1)] = 0u;
+  ev.xq = q ? q + 32 * par : nullptr;
+  eval_tile_body<FP, kStop>(lds, ev, (int)blockIdx.x, nride);
+}
+
+__global__ __launch_bounds__(256) void empty_kernel(EvalMulti ev, int nride) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (threadIdx.x == 0 && ev.nmodels < 0) lds[0] = (char)nride;  // (never: keeps the arguments live)
+}
+
+// the flush alone: every workgroup adds its (here: constant) counts into the shared
+// accumulators and arrives on the ticket, as a rider's tail does
+__global__ __launch_bounds__(256) void flush_only_kernel(EvalMulti ev, int nride) {
+  const int tid = threadIdx.x;
+  for (int m = 0; m < ev.nmodels; ++m)
+    if ((tid & 15) < ev.K && (tid >> 4) < ev.K) atomicAdd(acc_cell(ev.acc, xcd_copy(), m, tid), 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) (void)__hip_atomic_fetch_add(ev.ticket + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the ticket alone: one device-scope atomic per workgroup on one address
+__global__ __launch_bounds__(256) void ticket_only_kernel(EvalMulti ev, int nride) {
+  if (threadIdx.x == 0) (void)__hip_atomic_fetch_add(ev.ticket + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 static uint16_t bf16_bits(float v) {
@@ -89,10 +115,13 @@ int main(int argc, char** argv) {
   }
   int* acc;
   unsigned* ticket;
-  CK(hipMalloc(&acc, (size_t)kMaxEvalModels * 256 * kAccStride * 4));
+  CK(hipMalloc(&acc, kEvalAccInts * 4));
   CK(hipMalloc(&ticket, 64));
-  CK(hipMemset(acc, 0, (size_t)kMaxEvalModels * 256 * kAccStride * 4));
+  CK(hipMemset(acc, 0, kEvalAccInts * 4));
   CK(hipMemset(ticket, 0, 64));
+  unsigned* q;
+  CK(hipMalloc(&q, 64 * 4));
+  CK(hipMemset(q, 0, 64 * 4));
   char* slots;
   CK(hipHostMalloc(&slots, 2 * M * 1088, hipHostMallocDefault));
   std::memset(slots, 0, 2 * M * 1088);
@@ -123,13 +152,16 @@ int main(int argc, char** argv) {
   const size_t lds_pm = (size_t)32 * FP * 2 + 8192 + kMaxEvalModels * 256 * 4 + 16 + 64;
   const size_t lds_tr = kEvalTileLds;
   CK(hipFuncSetAttribute((const void*)pair_major_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pm));
-  CK(hipFuncSetAttribute((const void*)tile_resident_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_tr));
+  CK(hipFuncSetAttribute((const void*)tile_resident_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_tr));
+  CK(hipFuncSetAttribute((const void*)tile_resident_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_tr));
+  CK(hipFuncSetAttribute((const void*)tile_resident_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_tr));
+  CK(hipFuncSetAttribute((const void*)empty_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pm));
 
   // correctness: one launch of each into its own slot set
   pair_major_kernel<<<256, 256, lds_pm>>>(make(0, 256), 256);
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
-  tile_resident_kernel<<<nT, 256, lds_tr>>>(make(1, nT), nT);
+  tile_resident_kernel<3><<<nT, 256, lds_tr>>>(make(1, nT), nT, nullptr, 0);
   CK(hipGetLastError());
   CK(hipDeviceSynchronize());
   const bool same = std::memcmp(slots, slots + (size_t)M * 1088, (size_t)M * 1088) == 0;
@@ -157,8 +189,20 @@ int main(int argc, char** argv) {
   };
   const EvalMulti pm = make(0, 256), tr = make(1, nT), tr256 = make(1, 256);
   time_it("pair_major_256", [&] { pair_major_kernel<<<256, 256, lds_pm>>>(pm, 256); });
-  time_it("tile_resident_153", [&] { tile_resident_kernel<<<nT, 256, lds_tr>>>(tr, nT); });
-  time_it("tile_resident_256", [&] { tile_resident_kernel<<<256, 256, lds_tr>>>(tr256, 256); });
+  int par = 0;
+  time_it("tile_resident_153", [&] { tile_resident_kernel<3><<<nT, 256, lds_tr>>>(tr, nT, nullptr, 0); });
+  time_it("tile_resident_256", [&] { tile_resident_kernel<3><<<256, 256, lds_tr>>>(tr256, 256, nullptr, 0); });
+  time_it("tile_queue_256", [&] { tile_resident_kernel<3><<<256, 256, lds_tr>>>(tr256, 256, q, par); par ^= 1; });
+  CK(hipDeviceSynchronize());
+  std::printf(", \"queue_slots_equal\": %s",
+              std::memcmp(slots, slots + (size_t)M * 1088, (size_t)M * 1088) == 0 ? "true" : "false");
+  time_it("tile_tiles_only_153", [&] { tile_resident_kernel<1><<<nT, 256, lds_tr>>>(tr, nT, nullptr, 0); });
+  time_it("tile_plus_flush_153", [&] { tile_resident_kernel<2><<<nT, 256, lds_tr>>>(tr, nT, nullptr, 0); });
+  time_it("empty_256_lds83k", [&] { empty_kernel<<<256, 256, lds_pm>>>(pm, 256); });
+  time_it("flush_only_256", [&] { flush_only_kernel<<<256, 256>>>(pm, 256); });
+  time_it("ticket_only_256", [&] { ticket_only_kernel<<<256, 256>>>(pm, 256); });
+  // (the flush-only kernels leave counts in the accumulators: zero them for the next run)
+  CK(hipMemset(acc, 0, kEvalAccInts * 4));
   CK(hipDeviceSynchronize());
   std::printf("}\n");
   return same ? 0 : 3;

@@ -93,41 +93,29 @@ __device__ __forceinline__ void load_pair_frags(WFrag<FP>& wf, const EvalModel& 
 // sequence number, so the publication costs the workgroup no PCIe round trip.
 __device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int tid, int* cells) {
   const int K = ev.K, KK = K * K;
-  // the counts of the kAccCopies accumulator copies: items (copy, model, cell) dealt
-  // to the threads, every sc1 load (past this XCD's L2: the adds were performed in
-  // memory) in flight together, summed with LDS atomics; then the copies zeroed
+  // the counts of the kAccCopies accumulator copies: thread = (model, cell), its
+  // copies' sc1 loads (past this XCD's L2: the adds were performed in memory) all in
+  // flight, summed in registers; then the copies zeroed
   float lv = 0.f;  // (constant model indices: a per-thread index would copy ev.m into scratch)
 #pragma unroll
   for (int m = 0; m < kMaxEvalModels; ++m)
     if (m < M && tid == m && ev.m[m].loss) lv = *ev.m[m].loss;
-  for (int i = tid; i < M * KK; i += 256) cells[i] = 0;  // (the caller's counts were flushed)
   if (tid < M) cells[kMaxEvalModels * 64 + tid] = __float_as_int(lv);
-  __syncthreads();
-  const int n = kAccCopies * M * KK;
   const auto ra = rsrc_of(ev.acc, (unsigned)(kEvalAccInts * 4));
-  auto off_of = [&](int q) {  // byte offset of item q's accumulator cell
-    const int c = q / (M * KK), r = q - c * (M * KK), m = r / KK, ci = r - m * KK;
-    const int t16 = ci / K, p16 = ci - t16 * K;
-    return (unsigned)(((c * kMaxEvalModels + m) * 256 + t16 * 16 + p16) * kAccStride * 4);
-  };
-  constexpr int kPer = (kAccCopies * kMaxEvalModels * 64 + 255) / 256;  // items per thread (max)
-  for (int q0 = 0; q0 < n; q0 += 256 * kPer) {  // (one pass for K <= 8)
-    int v[kPer];
+  constexpr unsigned kCopyBytes = (unsigned)kMaxEvalModels * 256 * kAccStride * 4;
+  for (int q = tid; q < M * KK; q += 256) {
+    const int m = q / KK, ci = q - m * KK, t16 = ci / K, p16 = ci - t16 * K;
+    const unsigned o = (unsigned)((m * 256 + t16 * 16 + p16) * kAccStride * 4);
+    int v[kAccCopies];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int q = q0 + tid + 256 * j;
-      v[j] = q < n ? (int)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)off_of(q), 0, kAuxSc1) : 0;
-    }
+    for (int c = 0; c < kAccCopies; ++c) v[c] = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)(o + c * kCopyBytes), 0, kAuxSc1);
+    int t = 0;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int q = q0 + tid + 256 * j;
-      if (q < n && v[j]) atomicAdd(&cells[q % (M * KK)], v[j]);
-    }
+    for (int c = 0; c < kAccCopies; ++c) t += v[c];
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-      const int q = q0 + tid + 256 * j;
-      if (q < n && v[j]) __builtin_amdgcn_raw_buffer_store_b32(0u, ra, (int)off_of(q), 0, kAuxSc1);
-    }
+    for (int c = 0; c < kAccCopies; ++c)
+      if (v[c]) __builtin_amdgcn_raw_buffer_store_b32(0u, ra, (int)(o + c * kCopyBytes), 0, kAuxSc1);
+    cells[q] = t;  // (the caller's counts were flushed before the ticket)
   }
   __syncthreads();
   if (tid == 0) __hip_atomic_store(ev.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

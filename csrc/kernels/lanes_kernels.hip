@@ -348,9 +348,11 @@ namespace {
 // staging -- each wave streams its 256-feature slice of a 16-row test tile from
 // global memory straight into the MFMA A operand, against the pair's weight
 // fragments held in registers.  Items = (model pair, 16-row tile), pair-major
-// contiguous chunks per workgroup.
+// contiguous chunks per workgroup.  Co-residence with a lane workgroup needs the
+// registers it leaves: 512 - (256 VGPR + 128 AGPR) = 128 per SIMD lane, hence
+// waves_per_eu(4) (FP 1024: 128 VGPRs, 5 spilled; without it 134 + 4 did not fit).
 template <int FP>
-__global__ __launch_bounds__(256) void lanes_eval_kernel(EvalMulti ev) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lanes_eval_kernel(EvalMulti ev) {
   __shared__ f32x4 red[4][64];
   __shared__ int cl[kMaxEvalModels][16][8];  // (>= kMaxEvalModels * 64 + kMaxEvalModels ints: publish_counts' cells)
   __shared__ int last;

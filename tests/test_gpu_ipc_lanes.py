@@ -92,16 +92,17 @@ def test_ipc_lanes_stop_vote_chunks_end_together(cuda, tmp_path):
 
 @pytest.mark.parametrize("mode,bound", [("async_ssp", 3), ("async_asp", None)])
 def test_async_lanes_worker_ranks(cuda, tmp_path, mode, bound):
-    """SSP(2) / ASP across processes: 1 server rank (the native AsyncServer) + 2
-    worker ranks whose 3 workers each are lanes of one persistent launch
+    """SSP(2) / ASP across processes: 1 server rank (the native AsyncServer) + a
+    worker rank whose 3 workers are lanes of one persistent launch
     (LanesLoop.run_async_remote), every delta pushed with its token and every
     release answered through the rank's reply queue (ServerProcessor.java:95-183).
-    The server rank runs on the CPU here: on a shared GPU its kernels would wait
-    for the CUs the worker ranks' persistent launches hold (on the node every rank
-    has its own GPU)."""
-    res = _launch(tmp_path, mode)
+    One worker rank and a CPU server rank: on the node every rank has its own GPU;
+    on one shared GPU the server's kernels would wait for the CUs a persistent
+    launch holds, and two ranks' persistent launches (each a grid-wide cooperative
+    solve) would depend on the device scheduling both processes' queues at once."""
+    res = _launch(tmp_path, mode, world=2)
     assert all(r.get("async_lanes") for r in res[1:]), res
-    assert res[0]["updates"] == 6 * 8, res[0]
+    assert res[0]["updates"] == 3 * 8, res[0]
     rows = res[0]["server_rows"]
     assert len(rows) == 8 and all(r[1] > 0.2 for r in rows[2:]), rows  # one server row per worker-0 delta
     if bound is not None:

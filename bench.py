@@ -307,6 +307,7 @@ def main(argv=None):
     # logged inside it)
     t0 = time.perf_counter()
     out = eng.run(close_log=False)
+    t_run = time.perf_counter()
     eng.log.drain(block=True)
     if device != "cpu":
         torch.cuda.synchronize()
@@ -315,6 +316,8 @@ def main(argv=None):
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),
                      "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2)}
+    if "phases_ms" in out:  # where the timed region's wall clock went (host view)
+        res["native"]["phases_ms"] = dict(out["phases_ms"], drain=round((t0 + dt - t_run) * 1e3, 3))
     rows = list(eng.log.book.server)
     res.update(_accuracy_fields(rows, timed_from=n_warm, start_ms=eng.train_start_ms))
     if a.steps < ACC_ROUNDS and a.accuracy_run and a.model == "dense" and not a.cpu:

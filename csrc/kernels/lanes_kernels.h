@@ -132,6 +132,10 @@ struct LanesArgs {
   // global model of the previous update (ev.m[kMaxEvalModels - 1], server row); the
   // riders evaluate nothing.  0: the riders evaluate ev's models (the previous round's).
   int lane_eval;
+  // lane_riders = 1 (tile-resident form, ev.form == 1): every lane workgroup joins the
+  // evaluation as a rider once its part of the round is done (ev.nticket counts the
+  // nride riders + L * kLaneWg lane workgroups); the tiles come from ev.xq[0]
+  int lane_riders;
   int* lacc;            // [kMaxLanes][2][256] accumulators (stride kAccStride), zero between launches
   unsigned* lticket;    // [kMaxLanes][32] per-lane evaluation arrivals
 };

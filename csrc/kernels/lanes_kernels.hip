@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     __syncthreads();
     if (r < 0) {  // a rider: the previous round's evaluation
       if (a.ev.form == 1)
-        eval_tile_body<FP>(lds, a.ev, -r - 1, a.nride);
+        eval_tile_body<FP>(lds, a.ev, -r - 1, a.lane_riders ? (int)a.ev.nticket : a.nride);
       else
         eval_multi_body<FP>(lds, a.ev, -r - 1, a.nride);
       return;
@@ -132,13 +132,20 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     l = r / kLaneWg;
     wg = r - l * kLaneWg;
   }
+  // a lane workgroup whose part of the round is done joins the evaluation (lane_riders)
+  auto join_eval = [&]() {
+    if (a.lane_riders) eval_tile_body<FP>(lds, a.ev, a.nride + l * kLaneWg + wg, (int)a.ev.nticket);
+  };
   constexpr int NS = FP / 32;
   const LaneRound rr = pick(a.r, l);
   const SolveParams win{rr.B, rr.start, 0, 0};
   const WinTiles wt(win.start, win.B, cfg.cap);
   const int ntr = wt.nt < wt.T ? wt.nt : wt.T;  // row workgroups (ring tiles of the window)
   const int G = ntr > NS ? ntr : NS;
-  if (wg >= G) return;
+  if (wg >= G) {
+    join_eval();
+    return;
+  }
   SolveDev dv = lanes[l].dv;
   dv.out_hi = lanes[l].ohi[a.par];
   dv.out_lo = lanes[l].olo[a.par];
@@ -225,7 +232,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     barrier();
     phase = owner ? cl->phase : (int)(unsigned)ld_h64<S>(xch + kXchPhase);
   }
-  if (!owner && !LE) return;
+  if (!owner && !LE) {
+    join_eval();
+    return;
+  }
   if (owner) {
     if (wg == 0 && tid == 0) stamp(dv, 30, 4);
     // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
@@ -252,7 +262,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   }
-  if constexpr (!LE) return;
+  if constexpr (!LE) {
+    join_eval();
+    return;
+  }
   // ---- the lane's own evaluation of this round's local model (+ the previous update's
   // global model on lane 0), while the other lanes still solve ----
   if constexpr (S == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // fragments across XCDs

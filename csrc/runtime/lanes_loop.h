@@ -230,6 +230,7 @@ class LanesLoop {
   bool lane_eval_ = true;
   bool xcd_riders_ = false;
   bool tile_riders_ = false;
+  bool lane_riders_ = false;
   int* lacc_ = nullptr;
   unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;

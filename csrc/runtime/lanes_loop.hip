@@ -235,7 +235,10 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // PSX_RIDERS_TILE=1: tile-resident riders (eval_tile_body: a rider holds its test tile
   // in registers and runs every model pair past it; the test set is read once per round)
   const char* rt = std::getenv("PSX_RIDERS_TILE");
-  tile_riders_ = rt && rt[0] == '1';
+  tile_riders_ = rt && (rt[0] == '1' || rt[0] == '2');
+  // PSX_RIDERS_TILE=2: tile-resident riders + every lane workgroup joins them once its
+  // part of the round is done (LanesArgs::lane_riders)
+  lane_riders_ = rt && rt[0] == '2';
   const char* rx = std::getenv("PSX_RIDERS_XCD");
   xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
@@ -363,7 +366,7 @@ int LanesLoop::rider_count(int nmodels, int L) const {
   // the riders of the launch: the CUs of the XCDs no lane uses, or (every XCD
   // solves) enough riders to run after the lanes; a launch has grid - L * 32
   int extra = 0;
-  if (nmodels > 0 && L == 8) {
+  if (nmodels > 0 && L == 8 && !lane_riders_) {  // (lane riders: the lanes' own workgroups evaluate)
     const int nT = (cfg_.T + 31) / 32, items = tile_riders_ ? nT : (nmodels + 1) / 2 * nT;
     extra = items < 256 ? items : 256;
   }
@@ -411,7 +414,8 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
     add(l, lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->form = tile_riders_ ? 1 : 0;
-  ev->nticket = (unsigned)rider_count(ev->nmodels, cfg_.L);  // every rider of the launch arrives
+  // every rider of the launch arrives; lane riders: every lane workgroup as well
+  ev->nticket = (unsigned)(rider_count(ev->nmodels, cfg_.L) + (lane_riders_ ? cfg_.L * kLaneWg : 0));
   ev->dbg = rider_dbg_;
 }
 
@@ -568,7 +572,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     } else {
       fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
     }
-    a.nride = (int)a.ev.nticket;
+    a.nride = rider_count(a.ev.nmodels, L);
+    a.lane_riders = (lane_riders_ && a.ev.nmodels > 0 && !side_eval_ && !lane_eval_) ? 1 : 0;
     a.dsX = cfg_.dsX;
     a.dsy = cfg_.dsy;
     a.w = cfg_.w;

@@ -185,8 +185,11 @@ class LocalEngine:
         if close_log:
             self.log.close()
             self.tracer.close()
+        t_sum = time.time()
         if self.log.book is not None:
             out.update(summarize(self.log.book))
+        if "phases_ms" in out:
+            out["phases_ms"]["summary"] = round((time.time() - t_sum) * 1e3, 3)
         out["max_vc_gap"] = int(self.server.tracker.max_gap)
         out["failed_workers"] = sorted(self.failed)
         return out
@@ -365,6 +368,7 @@ class LocalEngine:
                     maybe_checkpoint(cfg, srv, r, W)
                 if n < todo:  # a worker's stream is exhausted and its window empty, or the deadline
                     break
+            t_loop = time.time()
             lp.flush(stream)
             # stream-ordered behind the rounds: the last local solve's loss / delta for code
             # that reads the roles, and the Python-side evaluation fragments of the global
@@ -373,7 +377,9 @@ class LocalEngine:
                 lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
+            t_enq = time.time()
             torch.cuda.synchronize(self.device)
+            t_sync = time.time()
             lp.poll_errors()  # a device error of the last rounds (the loop polls without syncs)
         except RuntimeError as e:
             if "cross-workgroup wait timed out" in str(e):
@@ -388,7 +394,10 @@ class LocalEngine:
         self.rounds = r
         return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True,
-                "lanes": len(W), "hand_off_scope": int(lp.hand_off_scope)}
+                "lanes": len(W), "hand_off_scope": int(lp.hand_off_scope),
+                # host wall clock of the run's parts (ms): rounds enqueued, tail enqueued, device done
+                "phases_ms": {"rounds": round((t_loop - t_start) * 1e3, 3), "tail": round((t_enq - t_loop) * 1e3, 3),
+                              "sync": round((t_sync - t_enq) * 1e3, 3)}}
 
     def _run_async_lanes(self) -> dict:
         """SSP / ASP of every live worker in ONE persistent launch

@@ -337,14 +337,15 @@ def test_xcd_local_riders_rows_equal_riders(cuda, monkeypatch, L):
     assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L
 
 
-@pytest.mark.parametrize("L", [3, 8])
-def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L):
+@pytest.mark.parametrize("L,tile", [(3, "1"), (8, "1"), (3, "2"), (8, "2")])
+def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile):
     """Riders holding their test tile in registers and running every model pair past
-    it (PSX_RIDERS_TILE=1, eval_tile_body: the test set read once per round) log
-    the same rows, bit for bit, as the pair-major riders (eval_multi_body)."""
+    it (PSX_RIDERS_TILE=1, eval_tile_body: the test set read once per round; =2: the
+    lanes' own workgroups join them once their part of the round is done) log the
+    same rows, bit for bit, as the pair-major riders (eval_multi_body)."""
     spec, train, ev = _data(cuda)
     books = []
-    for form in ("0", "1"):
+    for form in ("0", tile):
         monkeypatch.setenv("PSX_RIDERS_TILE", form)
         w = spec.init("random", seed=6, device=cuda)
         log = LogSink(spec.K, cuda)

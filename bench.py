@@ -306,12 +306,15 @@ def main(argv=None):
     # timed region: exactly `steps` rounds, synchronised on both sides (their rows
     # logged inside it)
     t0 = time.perf_counter()
-    out = eng.run(close_log=False)
+    out = eng.run(close_log=False, summary=False)  # (the log book's summary below, untimed)
     t_run = time.perf_counter()
-    eng.log.drain(block=True)
+    eng.log.drain(block=True)  # every row of the timed rounds finalised inside the region
     if device != "cpu":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    from psx.utils.logsink import summarize
+
+    out.update(summarize(eng.log.book))
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),

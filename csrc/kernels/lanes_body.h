@@ -51,7 +51,9 @@ static_assert(kEvalAccInts == (size_t)kAccCopies * kMaxEvalModels * 256 * kAccSt
 __device__ __forceinline__ int* acc_cell(int* acc, int copy, int m, int cell) {
   return acc + ((size_t)(copy * kMaxEvalModels + m) * 256 + cell) * kAccStride;
 }
-__device__ __forceinline__ int xcd_copy() { return (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u); }
+__device__ __forceinline__ int xcd_copy() {
+  return kAccCopies == 1 ? 0 : (int)((__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u) % kAccCopies);
+}
 
 // ---------------------------------------------------------------------------
 // Riders: evaluation of up to kMaxEvalModels models (the previous round's
@@ -103,18 +105,28 @@ __device__ __forceinline__ void publish_counts(const EvalMulti& ev, int M, int t
   if (tid < M) cells[kMaxEvalModels * 64 + tid] = __float_as_int(lv);
   const auto ra = rsrc_of(ev.acc, (unsigned)(kEvalAccInts * 4));
   constexpr unsigned kCopyBytes = (unsigned)kMaxEvalModels * 256 * kAccStride * 4;
-  for (int q = tid; q < M * KK; q += 256) {
+  constexpr int kPer = (kMaxEvalModels * 64 + 255) / 256;  // (model, cell) items per thread (K <= 8)
+  unsigned o[kPer];
+  int v[kPer][kAccCopies];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {  // every load of the thread in flight before any use
+    const int q = tid + 256 * j;
     const int m = q / KK, ci = q - m * KK, t16 = ci / K, p16 = ci - t16 * K;
-    const unsigned o = (unsigned)((m * 256 + t16 * 16 + p16) * kAccStride * 4);
-    int v[kAccCopies];
-#pragma unroll
-    for (int c = 0; c < kAccCopies; ++c) v[c] = (int)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)(o + c * kCopyBytes), 0, kAuxSc1);
-    int t = 0;
-#pragma unroll
-    for (int c = 0; c < kAccCopies; ++c) t += v[c];
+    o[j] = (unsigned)((m * 256 + t16 * 16 + p16) * kAccStride * 4);
 #pragma unroll
     for (int c = 0; c < kAccCopies; ++c)
-      if (v[c]) __builtin_amdgcn_raw_buffer_store_b32(0u, ra, (int)(o + c * kCopyBytes), 0, kAuxSc1);
+      v[j][c] = q < M * KK ? (int)__builtin_amdgcn_raw_buffer_load_b32(ra, (int)(o[j] + c * kCopyBytes), 0, kAuxSc1) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int q = tid + 256 * j;
+    if (q >= M * KK) continue;
+    int t = 0;
+#pragma unroll
+    for (int c = 0; c < kAccCopies; ++c) {
+      t += v[j][c];
+      if (v[j][c]) __builtin_amdgcn_raw_buffer_store_b32(0u, ra, (int)(o[j] + c * kCopyBytes), 0, kAuxSc1);
+    }
     cells[q] = t;  // (the caller's counts were flushed before the ticket)
   }
   __syncthreads();
@@ -351,7 +363,12 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     __syncthreads();
     return t;
   };
-  for (int tile = pop(rid); tile < nT; tile = pop(tile + nride)) {
+  // items = (tile, group of ev.ppi model pairs; 0: every pair), tile-major
+  const int ppi = ev.ppi > 0 && ev.ppi < npairs ? ev.ppi : npairs, ngr = (npairs + ppi - 1) / ppi;
+  for (int item = pop(rid); item < nT * ngr; item = pop(item + nride)) {
+    const int tile = item / ngr, gr = item - tile * ngr;
+    const int p0 = gr * ppi, p1 = p0 + ppi < npairs ? p0 + ppi : npairs;
+    const int m0 = 2 * p0, m1 = 2 * p1 < M ? 2 * p1 : M;  // the item's models
     const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
     const int64_t row0 = (int64_t)tile * 32;
     // the tile's A operands: rows r and 16 + r, wave w's k-steps (forward_tile_pre's)
@@ -365,9 +382,9 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     }
     if (tid < 32) ylab[tid] = tid < nrows ? ev.yt[row0 + tid] : 0;
     WFrag<FP> wc, wn;
-    load_pair(wc, 0);
-    for (int p = 0; p < npairs; ++p) {  // (uniform)
-      if (p + 1 < npairs) load_pair(wn, p + 1);
+    load_pair(wc, p0);
+    for (int p = p0; p < p1; ++p) {  // (uniform)
+      if (p + 1 < p1) load_pair(wn, p + 1);
       f32x4 acc0 = f32x4{0, 0, 0, 0}, acc1 = f32x4{0, 0, 0, 0};
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
@@ -377,12 +394,12 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
         acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wc.l[kk]), acc1);
       }
       store_partial_logits(red + (size_t)p * 8192, acc0, acc1);
-      if (p + 1 < npairs) wc = wn;
+      if (p + 1 < p1) wc = wn;
     }
     __syncthreads();
     if (first && rid == 0) rstamp(1);
-    for (int it = tid; it < 32 * M; it += 256) {  // thread (row, model)
-      const int row = it & 31, m = it >> 5;
+    for (int it = tid; it < 32 * (m1 - m0); it += 256) {  // thread (row, model)
+      const int row = it & 31, m = m0 + (it >> 5);
       if (row < nrows) {
         const char* rb = red + (size_t)(m >> 1) * 8192;
         const int c0 = 8 * (m & 1);

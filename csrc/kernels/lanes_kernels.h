@@ -41,10 +41,11 @@ namespace psx {
 constexpr int kMaxLanes = 8;
 constexpr int kLaneWg = 32;  // cooperating workgroups per lane: the CUs of one XCD
 constexpr int kMaxEvalModels = kMaxLanes + 1;
-// EvalMulti accumulators: one copy per XCD, [kAccCopies][kMaxEvalModels][256 cells] at
-// stride kAccStride -- a rider adds into its own XCD's copy, so a cell takes ~1/8 of
-// the device-scope atomics (one copy: 8.4 us for 256 riders' flush, tools/eval_probe)
-constexpr int kAccCopies = 8;
+// EvalMulti accumulators: [kAccCopies][kMaxEvalModels][256 cells] at stride kAccStride;
+// a rider adds into copy XCC_ID % kAccCopies.  One copy: measured best end to end
+// (tools/eval_probe, profiles/r04_s8-s9): 8 per-XCD copies cut the riders' flush from
+// 3.3 to 1.25 us but the publication's reads of every copy cost ~7 us more
+constexpr int kAccCopies = 1;
 constexpr size_t kEvalAccInts = (size_t)kAccCopies * kMaxEvalModels * 256 * 32;
 
 // Per-lane device state (a device-resident table read by the lane's workgroups).
@@ -95,6 +96,7 @@ struct EvalMulti {
   // riders (eval_tile_body: every model on a rider's tiles, the test set read once; the
   // tiles popped from xq[0], zero at launch)
   int form;
+  int ppi;  // tile-resident form: model pairs per work item (0: all; items = (tile, pair group))
   // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
   // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the
   // ticket, [10] the last rider is known, [11] its publication done, [12] / [13] the

@@ -231,6 +231,7 @@ class LanesLoop {
   bool xcd_riders_ = false;
   bool tile_riders_ = false;
   bool lane_riders_ = false;
+  int riders_ppi_ = 0;
   int* lacc_ = nullptr;
   unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;

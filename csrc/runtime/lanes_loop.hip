@@ -232,13 +232,19 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // queues (EvalMulti::xq) instead of contiguous chunks of the whole set.  Off by
   // default: 113.1 against 95.8 us per round (profiles/r04_s3) -- the queue pops and
   // the per-slice pair reloads cost more than the L2 locality returns
-  // PSX_RIDERS_TILE=1: tile-resident riders (eval_tile_body: a rider holds its test tile
-  // in registers and runs every model pair past it; the test set is read once per round)
+  // The riders' form, PSX_RIDERS_TILE: 2 (default) = tile-resident riders (eval_tile_body:
+  // a work item's 32-row test tile held in registers, its model pairs run past it, items
+  // popped from a queue) that every lane workgroup joins once its part of the round is
+  // done (LanesArgs::lane_riders); 1 = the tile-resident riders alone; 0 = the pair-major
+  // riders (eval_multi_body).  Same box, driver-form bench, 8 lanes (profiles/r04/s10,
+  // s11): 84.0 / 80.5k updates/s for 2 / 0, 85.3k with 2 model pairs per item
+  // (PSX_RIDERS_PPI, default 2; 1: 82.3k; 0 = all 5 pairs: 85.0k)
   const char* rt = std::getenv("PSX_RIDERS_TILE");
-  tile_riders_ = rt && (rt[0] == '1' || rt[0] == '2');
-  // PSX_RIDERS_TILE=2: tile-resident riders + every lane workgroup joins them once its
-  // part of the round is done (LanesArgs::lane_riders)
-  lane_riders_ = rt && rt[0] == '2';
+  const char tf = rt && rt[0] ? rt[0] : '2';
+  tile_riders_ = tf == '1' || tf == '2';
+  lane_riders_ = tf == '2';
+  const char* rp = std::getenv("PSX_RIDERS_PPI");
+  riders_ppi_ = rp ? std::atoi(rp) : 2;
   const char* rx = std::getenv("PSX_RIDERS_XCD");
   xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
@@ -367,7 +373,8 @@ int LanesLoop::rider_count(int nmodels, int L) const {
   // solves) enough riders to run after the lanes; a launch has grid - L * 32
   int extra = 0;
   if (nmodels > 0 && L == 8 && !lane_riders_) {  // (lane riders: the lanes' own workgroups evaluate)
-    const int nT = (cfg_.T + 31) / 32, items = tile_riders_ ? nT : (nmodels + 1) / 2 * nT;
+    const int np = (nmodels + 1) / 2, ppi = riders_ppi_ > 0 && riders_ppi_ < np ? riders_ppi_ : np;
+    const int nT = (cfg_.T + 31) / 32, items = tile_riders_ ? nT * ((np + ppi - 1) / ppi) : np * nT;
     extra = items < 256 ? items : 256;
   }
   return lanes_grid(L, extra) - L * kLaneWg;
@@ -414,6 +421,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
     add(l, lanes_[l].ohi[p.par], lanes_[l].olo[p.par], lanes_[l].ob[p.par], 0, lanes_[l].loss2 + p.par, 0);
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->form = tile_riders_ ? 1 : 0;
+  ev->ppi = riders_ppi_;
   // every rider of the launch arrives; lane riders: every lane workgroup as well
   ev->nticket = (unsigned)(rider_count(ev->nmodels, cfg_.L) + (lane_riders_ ? cfg_.L * kLaneWg : 0));
   ev->dbg = rider_dbg_;

@@ -160,9 +160,11 @@ class LocalEngine:
             return True
         return False
 
-    def run(self, close_log: bool = True) -> dict:
+    def run(self, close_log: bool = True, summary: bool = True) -> dict:
         """Run until the configured stop (max_iters / wall clock / data).  close_log
-        False: the log sink stays open for a later run (its rows are flushed)."""
+        False: the log sink stays open for a later run (its rows are flushed).
+        summary False: no headline numbers from the log book (a scan of every row
+        logged so far: bench.py computes them outside its timed region)."""
         if getattr(self, "train_start_ms", None) is None:  # epoch ms when training first began
             self.train_start_ms = time.time() * 1000.0
         live = [w for w in self.workers if w.k not in self.failed]
@@ -186,7 +188,7 @@ class LocalEngine:
             self.log.close()
             self.tracer.close()
         t_sum = time.time()
-        if self.log.book is not None:
+        if summary and self.log.book is not None:
             out.update(summarize(self.log.book))
         if "phases_ms" in out:
             out["phases_ms"]["summary"] = round((time.time() - t_sum) * 1e3, 3)

@@ -322,6 +322,7 @@ def test_xcd_local_riders_rows_equal_riders(cuda, monkeypatch, L):
     XCDs) log the same rows as the default contiguous chunks."""
     spec, train, ev = _data(cuda)
     books = []
+    monkeypatch.setenv("PSX_RIDERS_TILE", "0")  # (the pair-major riders' placement option)
     for xq in ("0", "1"):
         monkeypatch.setenv("PSX_RIDERS_XCD", xq)
         w = spec.init("random", seed=6, device=cuda)
@@ -337,14 +338,16 @@ def test_xcd_local_riders_rows_equal_riders(cuda, monkeypatch, L):
     assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L
 
 
-@pytest.mark.parametrize("L,tile", [(3, "1"), (8, "1"), (3, "2"), (8, "2")])
-def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile):
+@pytest.mark.parametrize("L,tile,ppi", [(3, "1", "0"), (8, "1", "0"), (3, "2", "0"), (8, "2", "0"), (8, "2", "1"),
+                                        (3, "2", "2")])
+def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile, ppi):
     """Riders holding their test tile in registers and running every model pair past
     it (PSX_RIDERS_TILE=1, eval_tile_body: the test set read once per round; =2: the
     lanes' own workgroups join them once their part of the round is done) log the
     same rows, bit for bit, as the pair-major riders (eval_multi_body)."""
     spec, train, ev = _data(cuda)
     books = []
+    monkeypatch.setenv("PSX_RIDERS_PPI", ppi)  # (work items of ppi model pairs; 0: all)
     for form in ("0", tile):
         monkeypatch.setenv("PSX_RIDERS_TILE", form)
         w = spec.init("random", seed=6, device=cuda)

@@ -196,6 +196,16 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   std::printf(", \"queue_slots_equal\": %s",
               std::memcmp(slots, slots + (size_t)M * 1088, (size_t)M * 1088) == 0 ? "true" : "false");
+  for (int ppi : {1, 2}) {
+    EvalMulti e = tr256;
+    e.ppi = ppi;
+    char name[64];
+    std::snprintf(name, sizeof(name), "tile_queue_ppi%d_256", ppi);
+    time_it(name, [&] { tile_resident_kernel<3><<<256, 256, lds_tr>>>(e, 256, q, par); par ^= 1; });
+    CK(hipDeviceSynchronize());
+    std::printf(", \"ppi%d_slots_equal\": %s", ppi,
+                std::memcmp(slots, slots + (size_t)M * 1088, (size_t)M * 1088) == 0 ? "true" : "false");
+  }
   time_it("tile_tiles_only_153", [&] { tile_resident_kernel<1><<<nT, 256, lds_tr>>>(tr, nT, nullptr, 0); });
   time_it("tile_plus_flush_153", [&] { tile_resident_kernel<2><<<nT, 256, lds_tr>>>(tr, nT, nullptr, 0); });
   time_it("empty_256_lds83k", [&] { empty_kernel<<<256, 256, lds_pm>>>(pm, 256); });

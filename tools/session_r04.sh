@@ -23,12 +23,20 @@ for s in ${STEPS:-probe ipc}; do
     ab)   # AB_VARIANTS: env assignments, "-" = the defaults
       for v in ${AB_VARIANTS:-- PSX_RIDERS_TILE=1 - PSX_RIDERS_TILE=1}; do
         [ "$v" = "-" ] && v=""
+        v=${v//,/ }  # (a,b: two assignments)
         timeout -k 10 200 env $v python bench.py --steps 200 --warmup 20 > $OUT/ab.tmp 2>> $OUT/ab.err || exit 1
         echo "[$v] $(python -c "import json;d=json.load(open('$OUT/ab.tmp'));print(d['value'],d['ms_per_step'])")" | tee -a $OUT/ab.txt
       done ;;
+    fault)   # the round-3 matrix fault's configuration on the Python concurrent-stream path
+      # (4 workers, producer clock -p 500, BSP, PSX_NATIVE_LANES=0 keeps it off the lanes
+      # loop); FAULT_ENV adds e.g. AMD_SERIALIZE_KERNEL=3.  Runs LAST: nothing follows it.
+      python -c "import sys; sys.path[:0] = ['tools', '.']; import experiment_matrix as m; m.ensure_data('data')" > $OUT/fault_data.log 2>&1 || exit 1
+      timeout -k 10 ${FAULT_TIMEOUT:-90} env PSX_NATIVE_LANES=0 ${FAULT_ENV:-} python -X faulthandler -m psx.apps.server_app_runner --inprocess --device cuda -training data/train.bin -test data/test.bin -p ${FAULT_P:-500} -c 0 --num_workers 4 -l --log_dir $OUT/fault_run --max_wallclock_s ${FAULT_S:-45} --async_scheduler threads > $OUT/fault_run.out 2>&1
+      rc=$?; echo "fault run rc=$rc"; tail -5 $OUT/fault_run.out; wc -l $OUT/fault_run/*.csv
+      exit $rc ;;
     timeline)
       for v in 0 1; do
-        PSX_RIDERS_TILE=$v PSX_LANES_STAMPS=1 timeout -k 10 120 python tools/lanes_profile.py --lanes 8 --rounds 400 >> $OUT/lanes_profile.jsonl 2>> $OUT/lanes_profile.err || exit 1
+        PSX_RIDERS_TILE=$((v * 2)) PSX_LANES_STAMPS=1 timeout -k 10 120 python tools/lanes_profile.py --lanes 8 --rounds 400 >> $OUT/lanes_profile.jsonl 2>> $OUT/lanes_profile.err || exit 1
       done ;;
   esac
 done

@@ -772,11 +772,13 @@ PYBIND11_MODULE(_psx_hip, m) {
           py::arg("deadline_ms") = 0.0)
       .def(
           "run_async",
-          [](LanesLoop& l, int64_t updates, uintptr_t stream, double max_wait_s, double deadline_ms) {
+          [](LanesLoop& l, int64_t updates, uintptr_t stream, double max_wait_s, double deadline_ms,
+             int64_t per_lane) {
             py::gil_scoped_release nogil;
-            return l.run_async(updates, S(stream), max_wait_s, deadline_ms);
+            return l.run_async(updates, S(stream), max_wait_s, deadline_ms, per_lane);
           },
-          py::arg("updates"), py::arg("stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0)
+          py::arg("updates"), py::arg("stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0,
+          py::arg("per_lane") = 0)
       .def(
           "run_async_remote",
           [](LanesLoop& l, P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, uintptr_t stream,

@@ -114,8 +114,11 @@ class LanesLoop {
   // every released lane -- until `updates` solves ran (or the streams ended /
   // the deadline passed); then every lane gets a stop record and the launch
   // drains.  Releases not yet started carry over to the next call.  Returns the
-  // updates applied.
-  int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
+  // updates applied.  per_lane > 0: no lane starts more than per_lane solves in this
+  // call (max_iters = iterations per worker, also under ASP where fast workers would
+  // otherwise take the slow ones' share of `updates`).
+  int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0,
+                    int64_t per_lane = 0);
   // Multi-rank SSP / ASP on a worker GPU: the server is rank 0 (AsyncServer,
   // async_server.h).  Same persistent launch in remote mode: a lane's push only
   // publishes its token; this loop sends the delta to peer 0 (`p2p`, on

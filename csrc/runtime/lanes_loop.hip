@@ -1056,7 +1056,8 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   ++launches_;
 }
 
-int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms) {
+int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms,
+                             int64_t per_lane) {
   const int64_t t_begin = steady_ns();
   if (!cfg_.tracker) throw std::invalid_argument("LanesLoop::run_async: needs the tracker");
   ensure_async();
@@ -1074,6 +1075,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
   }
   launch_async(stream, false);
   int64_t started = 0, done = 0;
+  std::vector<int64_t> lane_started((size_t)L, 0);
   int running = 0;
   bool stopping = updates <= 0;
   std::vector<int> ks((size_t)cfg_.N);
@@ -1082,9 +1084,11 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
     auto start_ready = [&](double now) {
       for (int l = 0; l < L; ++l) {
         if (state_[l] != kWant || stopping || started >= updates) continue;
+        if (per_lane > 0 && lane_started[l] >= per_lane) continue;
         if (try_release(l, want_vc_[l], now)) {
           state_[l] = kRunning;
           ++started;
+          ++lane_started[l];
           ++running;
         }
       }
@@ -1146,7 +1150,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
       if (stopping || started >= updates) break;
       bool any_want = false, end = false;
       for (int l = 0; l < L; ++l)
-        if (state_[l] == kWant) {
+        if (state_[l] == kWant && !(per_lane > 0 && lane_started[l] >= per_lane)) {
           int64_t size = 0, start = 0, sn = 0;
           check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
           if (size <= 0 && exhausted(l)) end = true;  // a worker with no rows left: the run ends

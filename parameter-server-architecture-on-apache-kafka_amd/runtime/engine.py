@@ -441,7 +441,10 @@ class LocalEngine:
                     exhausted_since = exhausted_since or time.time()
                 if self._stop(done // max(1, len(W)), t_start, exhausted_since):
                     break
-                n = int(lp.run_async(int(todo), stream, 600.0, deadline_ms))
+                # one call for the whole run: max_iters iterations per worker exactly (under
+                # ASP the fast workers would otherwise take the slow ones' share)
+                per_lane = int(cfg.max_iters) if (cfg.max_iters and not ck) else 0
+                n = int(lp.run_async(int(todo), stream, 600.0, deadline_ms, per_lane))
                 done += n
                 srv.updates += n
                 for i, w in enumerate(W):

@@ -808,6 +808,10 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })
       .def("loss", [](const LanesLoop& l, int lane, uintptr_t s) { return l.loss(lane, S(s)); })
       .def("delta_ptr", &LanesLoop::delta_ptr)
+      .def("copy_out_all",
+           [](const LanesLoop& l, const std::vector<uintptr_t>& loss, const std::vector<uintptr_t>& delta,
+              uintptr_t s) { l.copy_out_all(loss, delta, S(s)); },
+           py::arg("loss"), py::arg("delta"), py::arg("stream"))
       .def("copy_out", [](const LanesLoop& l, int lane, uintptr_t loss, uintptr_t delta,
                           uintptr_t s) { l.copy_out(lane, loss, delta, S(s)); },
            py::arg("lane"), py::arg("loss") = 0, py::arg("delta") = 0, py::arg("stream") = 0)

@@ -151,6 +151,16 @@ int lanes_grid(int L, int min_riders);
 void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const LanesArgs& a, int S, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).
 void launch_xcc_probe(int* ids, int n, hipStream_t s);
+// Every lane's last delta [P] and training loss to caller buffers in ONE launch (the
+// end of a run: 2 L memcpy launches of ~5 us each otherwise)
+struct LanesCopyOut {
+  int L, P;
+  const float* src_d[kMaxLanes];
+  float* dst_d[kMaxLanes];
+  const float* src_l[kMaxLanes];
+  float* dst_l[kMaxLanes];
+};
+void launch_lanes_copy_out(const LanesCopyOut& c, hipStream_t s);
 // Evaluation of ev's models as a launch of its own that co-runs with a lanes
 // round (side stream; 8.6 KB LDS per workgroup, lanes_eval_grid() workgroups,
 // ev.nticket must equal that grid).  Same EvalSlot publication.

@@ -351,6 +351,29 @@ void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const La
 void launch_xcc_probe(int* ids, int n, hipStream_t s) { xcc_probe_kernel<<<n, 64, 0, s>>>(ids, n); }
 
 namespace {
+// grid (blocks per lane, L): the lane's delta in float4 pieces, its loss by block 0
+__global__ __launch_bounds__(256) void lanes_copy_out_kernel(LanesCopyOut c) {
+  const int l = (int)blockIdx.y;
+  const LanesCopyOut& cc = c;
+  const float* sd = pick(cc.src_d, l);
+  float* dd = pick(cc.dst_d, l);
+  if (dd) {
+    const int n4 = c.P / 4;
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < n4; i += (int)(gridDim.x * blockDim.x))
+      ((f32x4*)dd)[i] = ((const f32x4*)sd)[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < c.P - 4 * n4) dd[4 * n4 + threadIdx.x] = sd[4 * n4 + threadIdx.x];
+  }
+  float* dl = pick(cc.dst_l, l);
+  if (dl && blockIdx.x == 0 && threadIdx.x == 0) *dl = *pick(cc.src_l, l);
+}
+}  // namespace
+
+void launch_lanes_copy_out(const LanesCopyOut& c, hipStream_t s) {
+  if (c.L < 1 || c.L > kMaxLanes) return;
+  lanes_copy_out_kernel<<<dim3(8, c.L), 256, 0, s>>>(c);
+}
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // Side-stream evaluation (8 lanes: every XCD solves, so in-launch riders could

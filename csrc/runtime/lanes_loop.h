@@ -161,6 +161,9 @@ class LanesLoop {
   // stream-ordered copies of lane `lane`'s last loss (1 float) and delta (P floats);
   // a null destination is skipped
   void copy_out(int lane, uintptr_t loss_dst, uintptr_t delta_dst, hipStream_t stream) const;
+  // every lane's at once (one launch): loss_dst / delta_dst per lane, 0 = skip
+  void copy_out_all(const std::vector<uintptr_t>& loss_dst, const std::vector<uintptr_t>& delta_dst,
+                    hipStream_t stream) const;
   // fault injection (tests): round r runs with a wait budget of `spin` polls
   void inject_spin_timeout(int64_t round, int spin) {
     inject_round_ = round;

@@ -758,6 +758,32 @@ void LanesLoop::copy_out(int lane, uintptr_t loss_dst, uintptr_t delta_dst, hipS
               "lane delta copy");
 }
 
+void LanesLoop::copy_out_all(const std::vector<uintptr_t>& loss_dst, const std::vector<uintptr_t>& delta_dst,
+                             hipStream_t stream) const {
+  const int L = cfg_.L;
+  if ((int)loss_dst.size() != L || (int)delta_dst.size() != L)
+    throw std::invalid_argument("LanesLoop::copy_out_all: one destination per lane");
+  LanesCopyOut c;
+  std::memset(&c, 0, sizeof(c));
+  c.L = L;
+  c.P = (int)P_;
+  for (int l = 0; l < L; ++l) {
+    const LaneDev& ld = lanes_.at(l);
+    // (16-B pieces: the destinations are torch allocations, the sources workspace
+    // slices; anything else takes the per-lane copies)
+    if (delta_dst[l] % 16 != 0 || reinterpret_cast<uintptr_t>(ld.dv.delta) % 16 != 0) {
+      for (int j = 0; j < L; ++j) copy_out(j, loss_dst[j], delta_dst[j], stream);
+      return;
+    }
+    c.src_d[l] = ld.dv.delta;
+    c.dst_d[l] = reinterpret_cast<float*>(delta_dst[l]);
+    c.src_l[l] = ld.loss2 + last_par_;
+    c.dst_l[l] = reinterpret_cast<float*>(loss_dst[l]);
+  }
+  launch_lanes_copy_out(c, stream);
+  hip_check(hipGetLastError(), "lanes copy-out launch");
+}
+
 // ---------------------------------------------------------------------------
 // Asynchronous consistency (SSP / ASP): see lanes_loop.h and lanes_kernels.h.
 

@@ -647,9 +647,10 @@ class DistEngine:
             w.source.next_local = int(lp.next_local(i))
             w.iters += n
             w._seen_at_solve = int(lp.seen_at_solve(i))
-            lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
             if w.ring.XT is not None:
                 w.ring.xt_stale = True
+        if W:
+            lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
         if srv is not None and srv.frag is not None:
             srv.frag.refresh(srv.w)
         self.native_host_us_per_round = float(lp.host_us_per_round)

@@ -375,8 +375,7 @@ class LocalEngine:
             # stream-ordered behind the rounds: the last local solve's loss / delta for code
             # that reads the roles, and the Python-side evaluation fragments of the global
             # model (the native update rewrote w); ONE synchronisation covers them all
-            for i, w in enumerate(W):
-                lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+            lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
             t_enq = time.time()
@@ -457,8 +456,7 @@ class LocalEngine:
                     maybe_checkpoint(cfg, srv, srv.updates, W)
                 if n < todo:  # the streams ended, the deadline passed
                     break
-            for i, w in enumerate(W):
-                lp.copy_out(i, w.solver.loss.data_ptr(), w.solver.delta.data_ptr(), stream)
+            lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
             torch.cuda.synchronize(self.device)

@@ -361,3 +361,24 @@ def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile, 
     a, b = books
     assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 4
     assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L
+
+
+def test_copy_out_all_equals_per_lane_copies(cuda):
+    """The end-of-run batched copy (one launch for every lane's delta and loss)
+    delivers what the per-lane copies deliver."""
+    spec, train, ev = _data(cuda)
+    L = 5
+    w = spec.init("random", seed=2, device=cuda)
+    lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda)
+    lp.run(2, 0, stream_handle(cuda))
+    one = _deltas(lp, L, spec, cuda)
+    d_all = [torch.full((spec.P,), float("nan"), device=cuda) for _ in range(L)]
+    l_all = [torch.full((1,), float("nan"), device=cuda) for _ in range(L)]
+    l_one = [torch.full((1,), float("nan"), device=cuda) for _ in range(L)]
+    lp.copy_out_all([x.data_ptr() for x in l_all], [x.data_ptr() for x in d_all], stream_handle(cuda))
+    for i in range(L):
+        lp.copy_out(i, l_one[i].data_ptr(), 0, stream_handle(cuda))
+    torch.cuda.synchronize()
+    for i in range(L):
+        assert torch.equal(d_all[i], one[i]), i
+        assert torch.equal(l_all[i], l_one[i]) and torch.isfinite(l_all[i]).all(), i

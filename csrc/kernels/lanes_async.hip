@@ -131,6 +131,8 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   unsigned long long* const xch = dv.xch;
   unsigned long long* const err = xch + kXchErr;
   // ---- 1. the release record ----
+  // (PSX_LANES_STAMPS, slot 30 of the lane's table: 0 released, 4 solved, 5 ticket,
+  // 6 applied, 7 token out / evaluation starts, 8 evaluation done)
   if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.spin_rel, dv.err_host);
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, a.spin_rel);
   // the lane's rows, state and the pulled snapshot were written by other CUs
@@ -148,6 +150,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     if (wg == 0 && tid == 0) *A.relc = relc;
     return false;
   }
+  if (wg == 0 && tid == 0) stamp(dv, 30, 0);
   // ---- 2. the solve (as lanes_round_kernel) ----
   {
     char* lf = lds;
@@ -244,6 +247,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     }
   }
   ++run;
+  if (wg == 0 && tid == 0) stamp(dv, 30, 4);
   // ---- 3. push: ticket, serial slice updates, snapshot, token ----
   if (wg == 0 && tid == 0) {
     if (q.delay_us > 0) {  // injected straggler (tests): the solve "took" delay_us longer
@@ -258,11 +262,13 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   const int spin = spin_limit(dv);
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   const unsigned long long t = ld_h64<2>(A.rec + 16);
+  if (wg == 0 && tid == 0) stamp(dv, 30, 5);
   const bool logl = l == a.log_lane;
   if (!a.remote) {  // the server is this launch: serial slice updates in ticket order
     if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
     x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   }
+  if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   if (wg == 0 && tid == 0)
     st_sys_chunk(a.tok, (unsigned)(a.ring * 16), (unsigned)((t % (unsigned long long)a.ring) * 16ull),
                  TagChunk{(unsigned)t, (unsigned)l, (unsigned)(unsigned long long)q.vc,
@@ -283,7 +289,9 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     pm.bb = A.sb;
     pm.bslot = logl ? (char*)q.slot_s : nullptr;
     pm.bseq = q.seq_s;
+    if (wg == 0 && tid == 0) stamp(dv, 30, 7);
     lane_pair_eval<FP>(lds, K, a.Xt, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
+    if (wg == 0 && tid == 0) stamp(dv, 30, 8);
   }
   return true;
 }

@@ -102,6 +102,8 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   {
     __shared__ int role;
     if (tid == 0) {
+      if (a.ev.dbg)  // PSX_LANES_STAMPS: the earliest workgroup entry of the launch ([15])
+        atomicMin((unsigned long long*)(a.ev.dbg + 15), (unsigned long long)__builtin_amdgcn_s_memrealtime());
       unsigned* c = a.claim + 32 * a.cpar;
       int r = -1;
       if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane

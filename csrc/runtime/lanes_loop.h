@@ -164,7 +164,7 @@ class LanesLoop {
   // every lane's at once (one launch): loss_dst / delta_dst per lane, 0 = skip
   void copy_out_all(const std::vector<uintptr_t>& loss_dst, const std::vector<uintptr_t>& delta_dst,
                     hipStream_t stream) const;
-  // fault injection (tests): round r runs with a wait budget of `spin` polls
+  // fault injection (tests): the rounds from r on run with a wait budget of `spin` polls
   void inject_spin_timeout(int64_t round, int spin) {
     inject_round_ = round;
     inject_spin_ = spin;

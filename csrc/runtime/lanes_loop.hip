@@ -597,12 +597,15 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.xcd0 = cfg_.xcd0;
     // (the tile-resident riders pop their tiles from the first of these counters)
     a.ev.xq = ((xcd_riders_ || tile_riders_) && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
-    a.spin_max = r == inject_round_ ? inject_spin_ : 0;
+    // (from the injected round on: a round whose workgroups happen to arrive together
+    // polls nothing, so one round alone would not always time out)
+    a.spin_max = (inject_round_ >= 0 && r >= inject_round_) ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
       if (rider_dbg_ && a.ev.nmodels > 0) {  // PSX_LANES_STAMPS: this launch's rider timeline
         hip_check(hipMemsetAsync(rider_dbg_, 0, 64 * sizeof(long long), stream), "rider stamps");
         hip_check(hipMemsetAsync(rider_dbg_ + 12, 0xff, sizeof(long long), stream), "rider stamps");
+        hip_check(hipMemsetAsync(rider_dbg_ + 15, 0xff, sizeof(long long), stream), "rider stamps");
       }
       launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
       hip_check(hipGetLastError(), "lanes round launch");

@@ -118,7 +118,7 @@ def main():
         rs, base = lp.read_rider_stamps(s), lp.read_stamps(0, s)[30 * 16]
         if rs and base:
             rel = lambda t: round((t - base) / 100.0, 2) if 0 < t < (1 << 62) else None
-            res["riders"] = {"first_entry": rel(rs[12]), "last_entry": rel(rs[13]), "rider0_entry": rel(rs[0]),
+            res["riders"] = {"kernel_first_entry": rel(rs[15]), "first_entry": rel(rs[12]), "last_entry": rel(rs[13]), "rider0_entry": rel(rs[0]),
                              "rider0_first_tile": rel(rs[1]), "rider0_items": [rel(rs[2 + i]) for i in range(4)],
                              "rider0_ticket": rel(rs[8]), "last_ticket": rel(rs[14]),
                              "publisher_known": rel(rs[10]), "published": rel(rs[11])}

@@ -442,6 +442,85 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
   rstamp(11);
 }
 
+// The BSP update of one slice by the last lane to finish it: w += lr * (sum of
+// the lanes' deltas, lane order) and the server's evaluation fragments, or the
+// plain sum into dsum (multi-rank).  A lane whose solve reported a timed-out
+// wait (sticky error word) contributes nothing.  Slice 0 also carries the
+// intercepts (each lane's workgroup 0 stored them before arriving).  Every
+// lane's error word and delta element are loaded before the first is used: one
+// round trip to the other XCDs' data, not one per lane.
+struct ApplyArgs {
+  int L;
+  float* w;
+  float lr;
+  float* dsum;  // != nullptr: the lane sum goes here (multi-rank), w untouched
+  uint16_t *shi, *slo;  // the server's evaluation fragments of this update
+  float* sb;
+  int scoff;
+};
+
+template <int FP>
+__device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const LaneDev* lanes, const ApplyArgs& a,
+                                                 int wg) {
+  const int tid = threadIdx.x, K = cfg.K, L = a.L;
+  const int c = tid >> 5, f = wg * 32 + (tid & 31);
+  const bool coef = c < K;
+  const bool icpt = wg == 0 && tid < K;  // (threads 0..K-1 carry one intercept each as well)
+  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
+  unsigned long long er[kMaxLanes];
+  float dl[kMaxLanes], di[kMaxLanes];
+#pragma unroll
+  for (int l = 0; l < kMaxLanes; ++l) {
+    er[l] = 0ull;
+    dl[l] = di[l] = 0.f;
+    if (l < L) {
+      er[l] = xload(lanes[l].dv.xch + kXchErr);
+      if (coef) dl[l] = ld_sc1(lanes[l].dv.delta + e);
+      if (icpt) di[l] = ld_sc1(lanes[l].dv.delta + ei);
+    }
+  }
+  float sum = 0.f, sumi = 0.f;
+#pragma unroll
+  for (int l = 0; l < kMaxLanes; ++l)
+    if (l < L && er[l] == 0ull) {
+      sum += dl[l];
+      sumi += di[l];
+    }
+  if (coef) {
+    if (a.dsum) {
+      a.dsum[e] = sum;
+    } else {
+      const float nw = a.w[e] + a.lr * sum;
+      a.w[e] = nw;
+      write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
+    }
+  }
+  if (icpt) {
+    if (a.dsum) {
+      a.dsum[ei] = sumi;
+    } else {
+      const float nw = a.w[ei] + a.lr * sumi;
+      a.w[ei] = nw;
+      a.sb[a.scoff + tid] = nw;
+    }
+  }
+}
+
+// Arrive on slice `idx`'s lane counter (every store of this workgroup drained
+// first); true for the last lane, which resets the counter for the next launch.
+__device__ __forceinline__ bool lane_arrive(unsigned* arrive, int idx, int L, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(arrive + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == (unsigned)L - 1u;
+    if (last) __hip_atomic_store(arrive + idx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 // ---------------------------------------------------------------------------
 // Phase I of a lane's solve, row role: stage ring tile `rt` into the LDS image,
 // the round's new rows straight from the dataset (also written into the ring),
@@ -684,23 +763,44 @@ __device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t*
     const bool live = cc < K && (tid < 8 ? wrow : srow);
     bl[tid] = live ? ld_h<2>((tid < 8 ? pm.ab + pm.acoff : pm.bb + pm.bcoff) + cc) : 0.f;
   }
+  // the tile's MFMA A operands straight from global memory into registers (rows r
+  // and 16 + r, wave w's k-steps, as forward_tile_pre reads them from LDS), the next
+  // tile's in flight during the current tile's MFMAs -- no LDS staging
   const int nT = (T + 31) / 32;
-  TileRegs<FP> tr;
-  if (wg < nT) tr.load(Xt, yt, wg, T);
+  constexpr int KS = WFrag<FP>::KS;
+  const int lane = tid & 63, w = tid >> 6, r = lane & 15, kq = lane >> 4;
+  u16x8 a0[KS], a1[KS];
+  int ylab = 0;
+  auto load_tile = [&](int tile) {
+    const int64_t row0 = (int64_t)tile * 32;
+    const int nr = T - tile * 32 < 32 ? T - tile * 32 : 32;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int cg = (w * KS + kk) * 4 + kq;
+      a0[kk] = r < nr ? *(const u16x8*)(Xt + (row0 + r) * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      a1[kk] = 16 + r < nr ? *(const u16x8*)(Xt + (row0 + 16 + r) * FP + cg * 8) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    ylab = tid < nr ? yt[row0 + tid] : 0;
+  };
+  if (wg < nT) load_tile(wg);
   __syncthreads();
   for (int tile = wg; tile < nT; tile += G) {
     const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
-    tr.store(lds);
-    const int ylab = tr.y;
-    if (tile + G < nT) tr.load(Xt, yt, tile + G, T);
-    __syncthreads();
-    f32x4 a0, a1;
-    forward_tile_pre<FP>(lds, wf, a0, a1);
-    store_partial_logits(red_base, a0, a1);
+    f32x4 acc0 = f32x4{0, 0, 0, 0}, acc1 = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wf.h[kk]), acc0);
+      acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wf.l[kk]), acc0);
+      acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wf.h[kk]), acc1);
+      acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wf.l[kk]), acc1);
+    }
+    const int ycur = ylab;
+    if (tile + G < nT) load_tile(tile + G);  // (the MFMAs above consumed a0 / a1)
+    store_partial_logits(red_base, acc0, acc1);
     __syncthreads();
     {  // thread (row, model)
       const int row = tid & 31, h = (tid >> 5) & 1;
-      const int yrow = __shfl(ylab, row, 64);
+      const int yrow = __shfl(ycur, row, 64);
       if (tid < 64 && row < nrows && (h == 0 ? wrow : srow)) {
         const int yl = yrow < 0 ? 0 : (yrow > 15 ? 15 : yrow);
         int best = 0;

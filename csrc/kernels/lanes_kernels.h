@@ -305,4 +305,66 @@ void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long l
 // pk: device copy of {cfg, a} (a.launch / a.cpar of THIS launch); al: device table [L]
 void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Persistent BSP (LanesLoop::run with PSX_LANES_PERSIST): ONE launch serves every
+// round of a run.  Round i of the launch is a record of kBspChunks tagged 16-B
+// chunks in pinned host memory (tag = tag0 + i + 1): lane l's LaneRound in chunks
+// 4l..4l+3 (10 payload words), the round's common words in chunk 32 {par, nmodels,
+// flags (1: the lanes solve, 2: stop), workers}, the evaluation slots of the
+// previous round's rows in chunks 33..41 {slot lo, slot hi, seq} per model.  A lane
+// workgroup
+//   * polls its lane's chunks and the common chunk (the host posts rounds ahead),
+//   * runs the round's solve (as lanes_round_kernel), reading its slice of w only
+//     once every lane's update of the previous round reached that slice
+//     (applied[slice] >= i), and arrives on the slice (the last lane applies the sum,
+//     then applied[slice] = i + 1),
+//   * joins evaluation pass i (the previous round's rows: its local models by round
+//     parity, the global model's fragments) as a tile-resident rider -- and goes on to
+//     round i + 1 while the slower lanes' items finish, so the evaluation tail overlaps
+//     the next round's staging.
+// The last arrival of pass i publishes the rows, then token i (round i applied, its
+// predecessor's rows out) and evdone = i + 1.  Hazards between rounds are waits on
+// these counters: pass i pops its items only after pass i - 2 reset its queue
+// parity, and round i rewrites the parity-(i & 1) fragments only after pass i - 1
+// (which reads them) is done.
+constexpr int kBspChunks = 48;
+constexpr int kBspCommon = 32;     // chunk of {par, nmodels, flags, workers}
+constexpr int kBspSlots = 33;      // first chunk of the evaluation slots
+constexpr unsigned kBspSolve = 1u, kBspStop = 2u;
+struct BspArgs {
+  int L, nride, xcd0, cpar;
+  const uint16_t* dsX;
+  const int32_t* dsy;
+  float* w;
+  float lr;
+  uint16_t* shi[2];
+  uint16_t* slo[2];
+  float* sb[2];
+  int scoff;
+  int log_workers, log_server;
+  unsigned* arrive;          // [FP/32 + 1] per-slice lane arrival counters (zero between rounds)
+  unsigned* claim;           // role claims (as LanesArgs::claim)
+  const TagChunk* rec;       // pinned [RR][kBspChunks]
+  int RR;
+  unsigned tag0;
+  TagChunk* tok;             // pinned [RR]: {tag0 + i + 1, i, 0, 0} once round i is applied and pass i published
+  unsigned* applied;         // [FP/32] rounds applied per slice in this launch (zero at launch)
+  unsigned* evdone;          // evaluation passes published in this launch (zero at launch)
+  unsigned* evq;             // [2][32] pass queue counters by parity (zero at launch)
+  unsigned* evticket;        // [2] pass arrivals by parity (zero at launch)
+  int* acc;                  // EvalMulti accumulators (zero)
+  const uint16_t* Xt;
+  const int32_t* yt;
+  int T, K, ppi;
+  int spin_max;
+  long long* dbg;            // PSX_LANES_STAMPS: riders' stamps (EvalMulti::dbg)
+};
+struct BspPack {
+  SolverCfg cfg;
+  BspArgs a;
+};
+// pk: device copy of {cfg, a}; the grid is lanes_grid(a.L, a.nride) (S == 2 only)
+void launch_lanes_bsp_persist(const SolverCfg& cfg, const BspPack* pk, const LaneDev* lanes, int L, int nride,
+                              hipStream_t s);
+
 }  // namespace psx

@@ -21,75 +21,6 @@ int lanes_grid(int L, int min_riders) {
 namespace {
 using namespace lanes_detail;
 
-// The BSP update of one slice by the last lane to finish it: w += lr * (sum of
-// the lanes' deltas, lane order) and the server's evaluation fragments, or the
-// plain sum into dsum (multi-rank).  A lane whose solve reported a timed-out
-// wait (sticky error word) contributes nothing.  Slice 0 also carries the
-// intercepts (each lane's workgroup 0 stored them before arriving).  Every
-// lane's error word and delta element are loaded before the first is used: one
-// round trip to the other XCDs' data, not one per lane.
-template <int FP>
-__device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const LaneDev* lanes, const LanesArgs& a,
-                                                 int wg) {
-  const int tid = threadIdx.x, K = cfg.K, L = a.L;
-  const int c = tid >> 5, f = wg * 32 + (tid & 31);
-  const bool coef = c < K;
-  const bool icpt = wg == 0 && tid < K;  // (threads 0..K-1 carry one intercept each as well)
-  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
-  unsigned long long er[kMaxLanes];
-  float dl[kMaxLanes], di[kMaxLanes];
-#pragma unroll
-  for (int l = 0; l < kMaxLanes; ++l) {
-    er[l] = 0ull;
-    dl[l] = di[l] = 0.f;
-    if (l < L) {
-      er[l] = xload(lanes[l].dv.xch + kXchErr);
-      if (coef) dl[l] = ld_sc1(lanes[l].dv.delta + e);
-      if (icpt) di[l] = ld_sc1(lanes[l].dv.delta + ei);
-    }
-  }
-  float sum = 0.f, sumi = 0.f;
-#pragma unroll
-  for (int l = 0; l < kMaxLanes; ++l)
-    if (l < L && er[l] == 0ull) {
-      sum += dl[l];
-      sumi += di[l];
-    }
-  if (coef) {
-    if (a.dsum) {
-      a.dsum[e] = sum;
-    } else {
-      const float nw = a.w[e] + a.lr * sum;
-      a.w[e] = nw;
-      write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
-    }
-  }
-  if (icpt) {
-    if (a.dsum) {
-      a.dsum[ei] = sumi;
-    } else {
-      const float nw = a.w[ei] + a.lr * sumi;
-      a.w[ei] = nw;
-      a.sb[a.scoff + tid] = nw;
-    }
-  }
-}
-
-// Arrive on slice `idx`'s lane counter (every store of this workgroup drained
-// first); true for the last lane, which resets the counter for the next launch.
-__device__ __forceinline__ bool lane_arrive(unsigned* arrive, int idx, int L, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(arrive + idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == (unsigned)L - 1u;
-    if (last) __hip_atomic_store(arrive + idx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  return *flag != 0;
-}
-
 // LE: the lanes evaluate their own models after the solve (LanesArgs::lane_eval).  A
 // template flag, not a run-time test: the evaluation tail compiled into the kernel
 // costs the solve its registers (1208 B of scratch against 120 B without it).
@@ -261,7 +192,8 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     }
     // ---- the BSP update: the last lane to finish a slice applies the sum ----
     if (wg == 0 && tid == 0) stamp(dv, 30, 5);
-    if (lane_arrive(a.arrive, wg, L, flag)) lane_apply_slice<FP>(cfg, lanes, a, wg);
+    if (lane_arrive(a.arrive, wg, L, flag))
+      lane_apply_slice<FP>(cfg, lanes, ApplyArgs{L, a.w, a.lr, a.dsum, a.shi, a.slo, a.sb, a.scoff}, wg);
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   }
   if constexpr (!LE) {

@@ -737,7 +737,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.w = P<float>(U("w"));
              c.lr = (float)D("lr", 1.0);
              const auto shi = V("shi"), slo = V("slo"), sb = V("sb");
-             for (int i = 0; i < 2; ++i) {
+             for (int i = 0; i < kLaneBufs; ++i) {
                c.shi[i] = i < (int)shi.size() ? P<uint16_t>(shi[i]) : nullptr;
                c.slo[i] = i < (int)slo.size() ? P<uint16_t>(slo[i]) : nullptr;
                c.sb[i] = i < (int)sb.size() ? P<float>(sb[i]) : nullptr;
@@ -803,6 +803,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("hand_off_scope", &LanesLoop::hand_off_scope)
       .def_property_readonly("side_eval", &LanesLoop::side_eval)
       .def_property_readonly("lane_eval", &LanesLoop::lane_eval)
+      .def_property_readonly("overlap", &LanesLoop::overlap)
       .def_property_readonly("host_us_per_round", &LanesLoop::host_us_per_round)
       .def_property_readonly("rounds_run", &LanesLoop::rounds_run)
       .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })

@@ -438,6 +438,8 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
   __syncthreads();
   if (!*lastp) return;
   rstamp(10);
+  // (every rider has popped its last item: the queue is free for the next pass)
+  if (ev.xq && tid == 0) __hip_atomic_store(ev.xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   publish_counts(ev, M, tid, cl);
   rstamp(11);
 }
@@ -457,7 +459,26 @@ struct ApplyArgs {
   uint16_t *shi, *slo;  // the server's evaluation fragments of this update
   float* sb;
   int scoff;
+  // overlapped launches (LanesArgs::ovl): w read and written through (its readers
+  // run on other XCDs in a launch that overlaps this one), then applied[slice] = round + 1
+  unsigned* applied = nullptr;
+  unsigned round = 0;
 };
+
+// Spin until *p >= want (device-scope loads); a timeout sets the sticky error word
+__device__ __forceinline__ void wait_ge(unsigned* p, unsigned want, unsigned long long* err, int spin_max) {
+  if (threadIdx.x == 0) {
+    int spins = 0;
+    while ((int)(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > spin_max) {  // never expected: record and fall through rather than hang
+        if (err) xstore(err, 9ull);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
 
 template <int FP>
 __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const LaneDev* lanes, const ApplyArgs& a,
@@ -479,6 +500,7 @@ __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const Lan
       if (icpt) di[l] = ld_sc1(lanes[l].dv.delta + ei);
     }
   }
+  const bool wt = a.applied != nullptr;  // (write-through: overlapped launches)
   float sum = 0.f, sumi = 0.f;
 #pragma unroll
   for (int l = 0; l < kMaxLanes; ++l)
@@ -490,8 +512,11 @@ __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const Lan
     if (a.dsum) {
       a.dsum[e] = sum;
     } else {
-      const float nw = a.w[e] + a.lr * sum;
-      a.w[e] = nw;
+      const float nw = (wt ? ld_sc1(a.w + e) : a.w[e]) + a.lr * sum;
+      if (wt)
+        st_sc1(a.w + e, nw);
+      else
+        a.w[e] = nw;
       write_frag(a.shi, a.slo, a.scoff + c, f, f < cfg.F ? nw : 0.f);
     }
   }
@@ -499,10 +524,18 @@ __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const Lan
     if (a.dsum) {
       a.dsum[ei] = sumi;
     } else {
-      const float nw = a.w[ei] + a.lr * sumi;
-      a.w[ei] = nw;
+      const float nw = (wt ? ld_sc1(a.w + ei) : a.w[ei]) + a.lr * sumi;
+      if (wt)
+        st_sc1(a.w + ei, nw);
+      else
+        a.w[ei] = nw;
       a.sb[a.scoff + tid] = nw;
     }
+  }
+  if (wt) {  // the slice's new weights are out: the next round's owners may read them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.applied + wg, a.round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

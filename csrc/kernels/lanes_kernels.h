@@ -41,6 +41,10 @@ namespace psx {
 constexpr int kMaxLanes = 8;
 constexpr int kLaneWg = 32;  // cooperating workgroups per lane: the CUs of one XCD
 constexpr int kMaxEvalModels = kMaxLanes + 1;
+// model buffers per lane (local fragments, intercepts, loss) and of the server
+// fragments, by round: r % 2, or r % 3 with overlapped launches (round r's
+// evaluation of round r - 1 can still run while round r + 1 writes its models)
+constexpr int kLaneBufs = 3;
 // EvalMulti accumulators: [kAccCopies][kMaxEvalModels][256 cells] at stride kAccStride;
 // a rider adds into copy XCC_ID % kAccCopies.  One copy: measured best end to end
 // (tools/eval_probe, profiles/r04_s8-s9): 8 per-XCD copies cut the riders' flush from
@@ -52,11 +56,12 @@ constexpr size_t kEvalAccInts = (size_t)kAccCopies * kMaxEvalModels * 256 * 32;
 struct LaneDev {
   SolveDev dv;        // solver workspace + the lane's ring (dv.X, dv.y); dv.delta = delta
   float* spart;       // [32 tiles][FP][2] window column sums / sums of squares (phase I hand-off)
-  uint16_t* ohi[2];   // local model fragments by round parity (class columns 0..K-1)
-  uint16_t* olo[2];
-  float* ob[2];
-  float* loss2;       // [2] training loss by round parity
+  uint16_t* ohi[kLaneBufs];  // local model fragments by round buffer (class columns 0..K-1)
+  uint16_t* olo[kLaneBufs];
+  float* ob[kLaneBufs];
+  float* loss2;       // [kLaneBufs] training loss by round buffer
   Ctrl* ctrl;         // the lane's controller after the round (host diagnostics)
+  float* wpull;       // [P] overlapped launches: the lane's copy of the pulled weights (LanesArgs::ovl)
 };
 
 // Per-round arguments of one lane: the window and the new rows of this round:
@@ -106,7 +111,7 @@ struct EvalMulti {
 
 struct LanesArgs {
   int L;    // lanes (0: evaluation only)
-  int par;  // round parity: lanes write fragments / loss of buffer `par`
+  int par;  // round buffer (r % 2, or r % 3 with ovl): lanes write fragments / loss of buffer `par`
   LaneRound r[kMaxLanes];
   const uint16_t* dsX;  // resident dataset [rows][FP] bf16
   const int32_t* dsy;
@@ -120,9 +125,11 @@ struct LanesArgs {
   // workgroup roles are CLAIMED at run time: a workgroup reads its XCC_ID and takes
   // the next slot of that XCD's lane (< kLaneWg of them), else the next rider id,
   // so a lane's workgroups share one L2 whatever order the dispatcher deals the
-  // workgroups to the XCDs in.  claim: [2 launch parities][16] counters (XCD
-  // lane slots 0..7, riders at 8, XCD-local evaluation chunks at 16..23, EvalMulti::xq);
-  // this launch uses parity cpar ([2][32] counters) and clears the other.
+  // workgroups to the XCDs in.  claim: [2 launch parities][32] counters (XCD
+  // lane slots 0..7, riders at 8, every workgroup at 9 -- the launch is fully
+  // dispatched once it reaches the grid, XCD-local evaluation chunks / the
+  // tile-resident riders' queue at 16..23, EvalMulti::xq); this launch uses parity
+  // cpar and clears the other.
   unsigned* claim;
   int cpar;
   int xcd0;             // lane l runs on XCD xcd0 + l (processes sharing a GPU take disjoint XCDs)
@@ -134,6 +141,23 @@ struct LanesArgs {
   // global model of the previous update (ev.m[kMaxEvalModels - 1], server row); the
   // riders evaluate nothing.  0: the riders evaluate ev's models (the previous round's).
   int lane_eval;
+  // ovl = 1 (LanesLoop with PSX_LANES_OVERLAP=1): consecutive round launches alternate
+  // between two streams, launch n + 1 enqueued once every workgroup of launch n has
+  // claimed its role (claim counter 9 at the grid: a stream wait on it), so launch n +
+  // 1's workgroups take the CUs launch n's leave while its evaluation still runs, with
+  // no kernel boundary in between.  The cross-round hand-offs go through counters
+  // instead: the last lane's update of slice s writes w through and then sets
+  // applied[s] = round + 1; the lane workgroups of launch `round` start once every
+  // slice reads >= round (every lane is then past round - 1: its rings, workspaces and
+  // run counter are free), pull their slice of w with write-through loads into
+  // LaneDev::wpull and acquire.  The fragments rotate over three buffers (par = round
+  // % 3): launch n evaluates buffer (n - 1) % 3 while launch n + 1 writes (n + 1) % 3.
+  // evdone = n + 1 is a stream write behind launch n: launch n + 1's evaluation (same
+  // accumulators, ticket and tile queue) starts only once evdone >= its round.
+  int ovl;
+  unsigned round;
+  unsigned* applied;  // [FP/32]
+  unsigned* evdone;
   // lane_riders = 1 (tile-resident form, ev.form == 1): every lane workgroup joins the
   // evaluation as a rider once its part of the round is done (ev.nticket counts the
   // nride riders + L * kLaneWg lane workgroups); the tiles come from ev.xq[0]
@@ -304,67 +328,5 @@ struct AsyncPack {
 void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long long t, hipStream_t s);
 // pk: device copy of {cfg, a} (a.launch / a.cpar of THIS launch); al: device table [L]
 void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s);
-
-// ---------------------------------------------------------------------------
-// Persistent BSP (LanesLoop::run with PSX_LANES_PERSIST): ONE launch serves every
-// round of a run.  Round i of the launch is a record of kBspChunks tagged 16-B
-// chunks in pinned host memory (tag = tag0 + i + 1): lane l's LaneRound in chunks
-// 4l..4l+3 (10 payload words), the round's common words in chunk 32 {par, nmodels,
-// flags (1: the lanes solve, 2: stop), workers}, the evaluation slots of the
-// previous round's rows in chunks 33..41 {slot lo, slot hi, seq} per model.  A lane
-// workgroup
-//   * polls its lane's chunks and the common chunk (the host posts rounds ahead),
-//   * runs the round's solve (as lanes_round_kernel), reading its slice of w only
-//     once every lane's update of the previous round reached that slice
-//     (applied[slice] >= i), and arrives on the slice (the last lane applies the sum,
-//     then applied[slice] = i + 1),
-//   * joins evaluation pass i (the previous round's rows: its local models by round
-//     parity, the global model's fragments) as a tile-resident rider -- and goes on to
-//     round i + 1 while the slower lanes' items finish, so the evaluation tail overlaps
-//     the next round's staging.
-// The last arrival of pass i publishes the rows, then token i (round i applied, its
-// predecessor's rows out) and evdone = i + 1.  Hazards between rounds are waits on
-// these counters: pass i pops its items only after pass i - 2 reset its queue
-// parity, and round i rewrites the parity-(i & 1) fragments only after pass i - 1
-// (which reads them) is done.
-constexpr int kBspChunks = 48;
-constexpr int kBspCommon = 32;     // chunk of {par, nmodels, flags, workers}
-constexpr int kBspSlots = 33;      // first chunk of the evaluation slots
-constexpr unsigned kBspSolve = 1u, kBspStop = 2u;
-struct BspArgs {
-  int L, nride, xcd0, cpar;
-  const uint16_t* dsX;
-  const int32_t* dsy;
-  float* w;
-  float lr;
-  uint16_t* shi[2];
-  uint16_t* slo[2];
-  float* sb[2];
-  int scoff;
-  int log_workers, log_server;
-  unsigned* arrive;          // [FP/32 + 1] per-slice lane arrival counters (zero between rounds)
-  unsigned* claim;           // role claims (as LanesArgs::claim)
-  const TagChunk* rec;       // pinned [RR][kBspChunks]
-  int RR;
-  unsigned tag0;
-  TagChunk* tok;             // pinned [RR]: {tag0 + i + 1, i, 0, 0} once round i is applied and pass i published
-  unsigned* applied;         // [FP/32] rounds applied per slice in this launch (zero at launch)
-  unsigned* evdone;          // evaluation passes published in this launch (zero at launch)
-  unsigned* evq;             // [2][32] pass queue counters by parity (zero at launch)
-  unsigned* evticket;        // [2] pass arrivals by parity (zero at launch)
-  int* acc;                  // EvalMulti accumulators (zero)
-  const uint16_t* Xt;
-  const int32_t* yt;
-  int T, K, ppi;
-  int spin_max;
-  long long* dbg;            // PSX_LANES_STAMPS: riders' stamps (EvalMulti::dbg)
-};
-struct BspPack {
-  SolverCfg cfg;
-  BspArgs a;
-};
-// pk: device copy of {cfg, a}; the grid is lanes_grid(a.L, a.nride) (S == 2 only)
-void launch_lanes_bsp_persist(const SolverCfg& cfg, const BspPack* pk, const LaneDev* lanes, int L, int nride,
-                              hipStream_t s);
 
 }  // namespace psx

@@ -36,6 +36,14 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       if (a.ev.dbg)  // PSX_LANES_STAMPS: the earliest workgroup entry of the launch ([15])
         atomicMin((unsigned long long*)(a.ev.dbg + 15), (unsigned long long)__builtin_amdgcn_s_memrealtime());
       unsigned* c = a.claim + 32 * a.cpar;
+      if (b == 0) {  // the other parity's counters (the previous launch has claimed) for the next launch
+        for (int j = 0; j < 32; ++j)
+          __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (reset before this launch counts as dispatched)
+      }
+      // every workgroup: the launch is fully dispatched once this reaches the grid (the
+      // next overlapped launch waits for that before its own dispatch)
+      (void)__hip_atomic_fetch_add(c + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int r = -1;
       if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
         const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
@@ -47,15 +55,14 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
         r = ((b & 7) - a.xcd0) * kLaneWg + (b >> 3);
       }
       if (r < 0) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
-      if (b == 0)  // the other parity's counters (the previous launch is complete) for the next launch
-        for (int j = 0; j < 32; ++j)
-          __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = r;
     }
     __syncthreads();
     const int r = __builtin_amdgcn_readfirstlane(role);  // (uniform: lane / workgroup indices in SGPRs)
     __syncthreads();
     if (r < 0) {  // a rider: the previous round's evaluation
+      if (a.ovl && a.ev.nmodels > 0)  // round - 1's launch complete: its fragments written back
+        wait_ge(a.evdone, a.round, (unsigned long long*)nullptr, a.spin_max > 0 ? a.spin_max : 1 << 22);
       if (a.ev.form == 1)
         eval_tile_body<FP>(lds, a.ev, -r - 1, a.lane_riders ? (int)a.ev.nticket : a.nride);
       else
@@ -67,7 +74,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   }
   // a lane workgroup whose part of the round is done joins the evaluation (lane_riders)
   auto join_eval = [&]() {
-    if (a.lane_riders) eval_tile_body<FP>(lds, a.ev, a.nride + l * kLaneWg + wg, (int)a.ev.nticket);
+    if (!a.lane_riders) return;
+    if (a.ovl && a.ev.nmodels > 0)  // round - 1's launch complete: its fragments written back
+      wait_ge(a.evdone, a.round, (unsigned long long*)nullptr, a.spin_max > 0 ? a.spin_max : 1 << 22);
+    eval_tile_body<FP>(lds, a.ev, a.nride + l * kLaneWg + wg, (int)a.ev.nticket);
   };
   constexpr int NS = FP / 32;
   const LaneRound rr = pick(a.r, l);
@@ -84,7 +94,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   dv.out_lo = lanes[l].olo[a.par];
   dv.b_fin = lanes[l].ob[a.par];
   dv.loss = lanes[l].loss2 + a.par;
-  dv.w_old = a.w;
+  dv.w_old = a.ovl ? lanes[l].wpull : a.w;  // (overlapped: the slice's copy pulled below)
   dv.w_new = nullptr;
   dv.ap_w = nullptr;
   dv.spin_max = a.spin_max;
@@ -94,7 +104,34 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   unsigned short* frl = (unsigned short*)(lb + 4 * 16 * 32 * 4);
   Ctrl* cl = (Ctrl*)(frl + 1024);  // bwd_body's controller copy (persists across slots)
   int* flag = (int*)(lsy + 8192);
-  const unsigned run = *dv.prm_count;
+  const bool owner = wg < NS;
+  __shared__ int ovl_late;
+  if (a.ovl) {
+    // Overlapped launches: the previous round's launch may still run (its evaluation).
+    // Every slice of its update applied means every lane is past that round (the last
+    // lane to arrive on a slice applies it; each lane's workgroup 0 arrives on slice 0
+    // after advancing its run counter), so its rings, workspaces and counters are free
+    // and w holds the update (written through).  Then an acquire: this CU's L1 may hold
+    // lines of them cached by the previous round's workgroups after this launch began.
+    if (tid == 0) ovl_late = 0;
+    __syncthreads();
+    if (tid < NS) {
+      const int sp = spin_limit(dv);
+      int spins = 0;
+      while ((int)(__hip_atomic_load(a.applied + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.round) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > sp) {  // never expected: reported below (after this round's error word is cleared)
+          ovl_late = 1;
+          break;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const unsigned run = a.ovl ? __hip_atomic_load(dv.prm_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : *dv.prm_count;
   unsigned long long* xch = dv.xch;
   unsigned long long* bar = xch + kXchGen + (run & 1u);
   unsigned long long* err = xch + kXchErr;
@@ -107,18 +144,25 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     else
       p_barrier(bar, (unsigned long long)G * nb, err, spin);
   };
-  const bool row = wg < ntr, owner = wg < NS;
+  const bool row = wg < ntr;
   const int K = cfg.K, FPr = FP;
+  if (wg == 0 && tid == 0) {
+    xstore(err, 0ull);  // this round's sticky error word (set by any timed-out wait below)
+    if constexpr (S == 1) xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counter
+  }
   // the pulled weights of this slice, fetched first (their latency overlaps the staging)
   float wo_pre = 0.f, b_pre = 0.f;
   if (owner) {
     const int c = tid >> 5, f = wg * 32 + (tid & 31);
-    if (c < K && f < cfg.F) wo_pre = a.w[(size_t)c * FPr + f];
-    if (wg == 0 && tid < K) b_pre = a.w[(size_t)K * FPr + tid];
-  }
-  if (wg == 0 && tid == 0) {
-    xstore(err, 0ull);  // this round's sticky error word (set by any timed-out wait below)
-    if constexpr (S == 1) xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counter
+    if (a.ovl) {  // the previous round's update of this slice is in w (written through, waited for above)
+      if (c < K && f < cfg.F) wo_pre = ld_sc1(a.w + (size_t)c * FPr + f);
+      if (wg == 0 && tid < K) b_pre = ld_sc1(a.w + (size_t)K * FPr + tid);
+      if (c < K) lanes[l].wpull[(size_t)c * FPr + f] = wo_pre;  // the solve's w_old (this slice)
+      if (wg == 0 && tid < K) lanes[l].wpull[(size_t)K * FPr + tid] = b_pre;
+    } else {
+      if (c < K && f < cfg.F) wo_pre = a.w[(size_t)c * FPr + f];
+      if (wg == 0 && tid < K) b_pre = a.w[(size_t)K * FPr + tid];
+    }
   }
   // ---- phase I: stage + ingest + window statistics, then x0 / first trial point ----
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
@@ -129,6 +173,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   if (wg == 0 && tid == 0) stamp(dv, 30, 1);
   barrier();
   if (wg == 0 && tid == 0) stamp(dv, 30, 2);
+  if (a.ovl && tid == 0 && ovl_late) xstore(err, 9ull);  // (after workgroup 0 cleared the error word)
   if (owner) {
     lane_prep<FP, KP, S>(lb, cfg, dv, lanes[l].spart, ntr, win.B, wg, wo_pre, b_pre);
     if (tid == 0) ctrl_init(*cl);
@@ -193,7 +238,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     // ---- the BSP update: the last lane to finish a slice applies the sum ----
     if (wg == 0 && tid == 0) stamp(dv, 30, 5);
     if (lane_arrive(a.arrive, wg, L, flag))
-      lane_apply_slice<FP>(cfg, lanes, ApplyArgs{L, a.w, a.lr, a.dsum, a.shi, a.slo, a.sb, a.scoff}, wg);
+      lane_apply_slice<FP>(cfg, lanes,
+                           ApplyArgs{L, a.w, a.lr, a.dsum, a.shi, a.slo, a.sb, a.scoff, a.ovl ? a.applied : nullptr,
+                                     a.round},
+                           wg);
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   }
   if constexpr (!LE) {

@@ -56,9 +56,10 @@ struct LanesLoopCfg {
   // server state (replica): w [P], its evaluation fragments (two buffers, columns scoff..)
   float* w = nullptr;
   float lr = 1.f;
-  uint16_t* shi[2] = {nullptr, nullptr};
-  uint16_t* slo[2] = {nullptr, nullptr};
-  float* sb[2] = {nullptr, nullptr};
+  // (a third buffer enables overlapped launches, LanesArgs::ovl)
+  uint16_t* shi[kLaneBufs] = {nullptr, nullptr, nullptr};
+  uint16_t* slo[kLaneBufs] = {nullptr, nullptr, nullptr};
+  float* sb[kLaneBufs] = {nullptr, nullptr, nullptr};
   int scoff = 0;
   // evaluation
   const uint16_t* Xt = nullptr;
@@ -151,6 +152,9 @@ class LanesLoop {
   // true (PSX_LANES_LANE_EVAL=1): each lane evaluates its own local model inside the
   // round kernel; false (default): the rider workgroups evaluate the previous round
   bool lane_eval() const { return lane_eval_; }
+  // true (PSX_LANES_OVERLAP=1, one rank, rider evaluation, three fragment buffers):
+  // consecutive rounds overlap (LanesArgs::ovl)
+  bool overlap() const { return ovl_; }
   double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
   int64_t rounds_run() const { return rounds_run_; }
   // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
@@ -250,6 +254,18 @@ class LanesLoop {
   int side_sync_ = 0;
   unsigned* sflags_ = nullptr;  // [0] last round done (main), [1] last evaluation done (side)
   long long* rider_dbg_ = nullptr;  // PSX_LANES_STAMPS: the riders' stamps
+  // overlapped launches (PSX_LANES_OVERLAP=1, LanesArgs::ovl): rounds alternate between
+  // the caller's stream and ostream_
+  bool ovl_ = false;
+  hipStream_t ostream_ = nullptr;
+  hipEvent_t ovl_in_ = nullptr, ovl_out_ = nullptr, ovl_last_ = nullptr;
+  unsigned* applied_ = nullptr;  // [32] LanesArgs::applied
+  unsigned* evdone_ = nullptr;   // LanesArgs::evdone
+  unsigned* ovlq_ = nullptr;     // the riders' tile queue (EvalMulti::xq) of overlapped launches
+  uint64_t ovl_n_ = 0;           // overlapped launches so far (LanesArgs::round)
+  bool ovl_chain_ = false;       // a launch of this run() call precedes (wait for its dispatch)
+  int ovl_prev_grid_ = 0, ovl_prev_cpar_ = 0;
+  void ovl_wait_last(hipStream_t stream);  // a separate ring-ingest launch: after the last round
   int64_t eval_round_[2] = {-1, -1};
   Pending pend_;
   int last_par_ = 0;  // parity of the last round run

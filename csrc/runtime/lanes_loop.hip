@@ -107,8 +107,8 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
     return o;
   };
   struct Offs {
-    size_t x, d, gc, wfix, std_, istd, beff, whi, wlo, part, xch, gpf, spart, delta, ohi[2], olo[2], ob[2], loss2,
-        stats, cnt, ctrl, dbg;
+    size_t x, d, gc, wfix, std_, istd, beff, whi, wlo, part, xch, gpf, spart, delta, ohi[kLaneBufs], olo[kLaneBufs],
+        ob[kLaneBufs], loss2, stats, cnt, ctrl, dbg, wpull;
   };
   const bool stamps = std::getenv("PSX_LANES_STAMPS") != nullptr;
   std::vector<Offs> o(cfg_.L);
@@ -128,12 +128,13 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
     q.gpf = take((size_t)kLaneWg * KP * FP * 4);
     q.spart = take((size_t)kLaneWg * FP * 2 * 4);
     q.delta = take((size_t)P_ * 4);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kLaneBufs; ++p) {
       q.ohi[p] = take(16 * FP * 2);
       q.olo[p] = take(16 * FP * 2);
       q.ob[p] = take(16 * 4);
     }
-    q.loss2 = take(2 * 4);
+    q.loss2 = take(kLaneBufs * 4);
+    q.wpull = take((size_t)P_ * 4);
     q.stats = take(8 * 4);
     q.cnt = take(16);
     q.ctrl = take(sizeof(Ctrl));
@@ -152,6 +153,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const size_t o_lacc = take((size_t)kMaxLanes * 2 * 256 * kAccStride * sizeof(int));
   const size_t o_ltic = take((size_t)kMaxLanes * 32 * sizeof(unsigned));
   const size_t o_rdbg = stamps ? take(64 * sizeof(long long)) : 0;
+  const size_t o_ovl = take(64 * sizeof(unsigned));  // applied [0, 32), evdone [32], tile queue [48]
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
   char* b = static_cast<char*>(ws_);
@@ -194,12 +196,13 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
     dv.err_host = err_host_ + l;
     dv.dbg = stamps ? reinterpret_cast<long long*>(b + q.dbg) : nullptr;
     ld.spart = reinterpret_cast<float*>(b + q.spart);
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < kLaneBufs; ++p) {
       ld.ohi[p] = reinterpret_cast<uint16_t*>(b + q.ohi[p]);
       ld.olo[p] = reinterpret_cast<uint16_t*>(b + q.olo[p]);
       ld.ob[p] = reinterpret_cast<float*>(b + q.ob[p]);
     }
     ld.loss2 = reinterpret_cast<float*>(b + q.loss2);
+    ld.wpull = reinterpret_cast<float*>(b + q.wpull);
     ld.ctrl = reinterpret_cast<Ctrl*>(b + q.ctrl);
   }
   lanes_dev_ = reinterpret_cast<LaneDev*>(b + o_tab);
@@ -217,6 +220,9 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   lacc_ = reinterpret_cast<int*>(b + o_lacc);
   lticket_ = reinterpret_cast<unsigned*>(b + o_ltic);
   rider_dbg_ = stamps ? reinterpret_cast<long long*>(b + o_rdbg) : nullptr;
+  applied_ = reinterpret_cast<unsigned*>(b + o_ovl);
+  evdone_ = applied_ + 32;
+  ovlq_ = applied_ + 48;
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
   // PSX_LANES_SIDE_EVAL=1: the rows go to a co-running side launch instead of riders
@@ -249,6 +255,20 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
   lane_eval_ = cfg_.L > 0 && S_ == 2 && !side_eval_ && le && le[0] == '1';  // (built for S == 2 only)
+  // PSX_LANES_OVERLAP=1: overlapped round launches (LanesArgs::ovl).  One rank (the
+  // multi-rank rounds end in collectives on the caller's stream), rider evaluation in
+  // the tile-resident or pair-major form without the XCD chunk counters (the claim
+  // block is reset while the previous launch runs), the XCD-resident form, and a third
+  // server fragment buffer
+  const char* ov = std::getenv("PSX_LANES_OVERLAP");
+  const bool sfr = !cfg_.shi[0] || (cfg_.shi[2] && cfg_.slo[2] && cfg_.sb[2]);  // (a sink may come later)
+  ovl_ = ov && ov[0] == '1' && !comm_ && cfg_.L > 0 && S_ == 2 && !side_eval_ && !lane_eval_ && !xcd_riders_ && sfr;
+  if (ovl_) {
+    hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
+    hip_check(hipEventCreateWithFlags(&ovl_in_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&ovl_out_, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&ovl_last_, hipEventDisableTiming), "hipEventCreate");
+  }
   if (side_eval_) {
     hip_check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "hipStreamCreate(side eval)");
     for (int p = 0; p < 2; ++p) {
@@ -279,6 +299,12 @@ LanesLoop::~LanesLoop() {
     (void)hipStreamSynchronize(astream_);
     (void)hipStreamDestroy(astream_);
   }
+  if (ostream_) {
+    (void)hipStreamSynchronize(ostream_);
+    (void)hipStreamDestroy(ostream_);
+  }
+  for (hipEvent_t e : {ovl_in_, ovl_out_, ovl_last_})
+    if (e) (void)hipEventDestroy(e);
   if (aev_in_) (void)hipEventDestroy(aev_in_);
   if (aev_out_) (void)hipEventDestroy(aev_out_);
   if (tok_host_) (void)hipHostFree(tok_host_);
@@ -332,6 +358,7 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
     const int64_t run = remaining < lt - cur ? remaining : lt - cur;
     const int64_t src_first = k + cur * (int64_t)cfg_.N;
     if (r->n2 > 0) {  // a third run: the oldest goes to a launch of its own
+      ovl_wait_last(stream);
       launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]),
                          nullptr, reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
       r->dst = (int)((r->dst + r->n) % cap);
@@ -356,8 +383,14 @@ int64_t LanesLoop::poll(int lane, double now_ms, LaneRound* r, hipStream_t strea
   return n;
 }
 
+void LanesLoop::ovl_wait_last(hipStream_t stream) {
+  // (the previous round's launch runs on the other stream and reads the ring)
+  if (ovl_ && ovl_n_ > 0) hip_check(hipStreamWaitEvent(stream, ovl_last_, 0), "ingest waits the last round");
+}
+
 void LanesLoop::flush_ingest(int lane, LaneRound* r, hipStream_t stream) {
   const int64_t cap = cfg_.scfg.cap;
+  if (r->n > 0 || r->n2 > 0) ovl_wait_last(stream);
   if (r->n > 0)
     launch_ring_ingest(cfg_.dsX, cfg_.dsy, r->first, r->step, r->n, reinterpret_cast<uint16_t*>(cfg_.X[lane]), nullptr,
                        reinterpret_cast<int32_t*>(cfg_.y[lane]), r->dst, cap, cfg_.scfg.Fp, stream);
@@ -519,10 +552,21 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
   SinkRecord lrec[kMaxEvalModels];
   int nlrec = 0;
   const bool is_server = !comm_ || comm_->rank() == cfg_.server_rank;
+  if (ovl_) {  // the second stream after the caller's earlier work
+    ovl_chain_ = false;
+    hip_check(hipEventRecord(ovl_in_, stream), "overlap order in");
+    hip_check(hipStreamWaitEvent(ostream_, ovl_in_, 0), "overlap order in");
+  }
+  auto ovl_join = [&]() {  // the caller's later work after every round of this call
+    if (!ovl_) return;
+    hip_check(hipEventRecord(ovl_out_, ostream_), "overlap order out");
+    hip_check(hipStreamWaitEvent(stream, ovl_out_, 0), "overlap order out");
+  };
   int64_t done = 0;
   for (; done < rounds; ++done) {
     const int64_t r = r0 + done;
-    const int par = (int)(r & 1);
+    const int par = ovl_ ? (int)(((r % 3) + 3) % 3) : (int)(r & 1);
+    hipStream_t rs = (ovl_ && (ovl_n_ & 1)) ? ostream_ : stream;  // this round's stream
     LanesArgs a;
     std::memset(&a, 0, sizeof(a));
     a.L = L;
@@ -534,7 +578,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     const double wait0 = epoch_ms();
     for (;;) {
       const double now = epoch_ms() - cfg_.t0_ms;
-      for (int l = 0; l < L; ++l) poll(l, now, &a.r[l], stream);
+      for (int l = 0; l < L; ++l) poll(l, now, &a.r[l], rs);
       bool ready = true, rows = true;
       for (int l = 0; l < L; ++l) {
         int64_t size = 0, start = 0, sn = 0;
@@ -553,7 +597,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       if (deadline_ms > 0.0 && epoch_ms() >= deadline_ms) end = true;
       if (end) {
         for (int l = 0; l < L; ++l)  // rows delivered meanwhile: into the ring now
-          if (a.r[l].n > 0 || a.r[l].n2 > 0) flush_ingest(l, &a.r[l], stream);
+          if (a.r[l].n > 0 || a.r[l].n2 > 0) flush_ingest(l, &a.r[l], rs);
+        ovl_join();
         rounds_run_ += done;
         host_ns_ += (double)(steady_ns() - t_begin);
         return done;
@@ -596,20 +641,41 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.cpar = (int)(launches_ & 1);
     a.xcd0 = cfg_.xcd0;
     // (the tile-resident riders pop their tiles from the first of these counters)
-    a.ev.xq = ((xcd_riders_ || tile_riders_) && a.ev.nmodels > 0) ? claim_ + 32 * a.cpar + 16 : nullptr;
+    a.ev.xq = ((xcd_riders_ || tile_riders_) && a.ev.nmodels > 0) ? (ovl_ ? ovlq_ : claim_ + 32 * a.cpar + 16)
+                                                                     : nullptr;
     // (from the injected round on: a round whose workgroups happen to arrive together
     // polls nothing, so one round alone would not always time out)
     a.spin_max = (inject_round_ >= 0 && r >= inject_round_) ? inject_spin_ : 0;
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
       if (rider_dbg_ && a.ev.nmodels > 0) {  // PSX_LANES_STAMPS: this launch's rider timeline
-        hip_check(hipMemsetAsync(rider_dbg_, 0, 64 * sizeof(long long), stream), "rider stamps");
-        hip_check(hipMemsetAsync(rider_dbg_ + 12, 0xff, sizeof(long long), stream), "rider stamps");
-        hip_check(hipMemsetAsync(rider_dbg_ + 15, 0xff, sizeof(long long), stream), "rider stamps");
+        hip_check(hipMemsetAsync(rider_dbg_, 0, 64 * sizeof(long long), rs), "rider stamps");
+        hip_check(hipMemsetAsync(rider_dbg_ + 12, 0xff, sizeof(long long), rs), "rider stamps");
+        hip_check(hipMemsetAsync(rider_dbg_ + 15, 0xff, sizeof(long long), rs), "rider stamps");
       }
-      launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);
+      if (ovl_) {
+        a.ovl = 1;
+        a.round = (unsigned)ovl_n_;
+        a.applied = applied_;
+        a.evdone = evdone_;
+        // dispatched once every workgroup of the previous round's launch holds its CU
+        // (its lanes wait for nothing of this launch, so this one may take the CUs it frees)
+        if (ovl_chain_)
+          hip_check(hipStreamWaitValue32(rs, claim_ + 32 * ovl_prev_cpar_ + 9, (uint32_t)ovl_prev_grid_,
+                                         hipStreamWaitValueGte),
+                    "overlap: previous launch dispatched");
+      }
+      launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, rs);
       hip_check(hipGetLastError(), "lanes round launch");
       ++launches_;
+      if (ovl_) {
+        hip_check(hipStreamWriteValue32(rs, evdone_, (uint32_t)(ovl_n_ + 1), 0), "overlap: launch done");
+        hip_check(hipEventRecord(ovl_last_, rs), "overlap: last launch");
+        ovl_prev_grid_ = lanes_grid(L, a.nride);
+        ovl_prev_cpar_ = a.cpar;
+        ovl_chain_ = true;
+        ++ovl_n_;
+      }
     }
     if (!slots.empty()) submit_rows(pend_, slots, seqs, kinds);
     if (nlrec) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), nlrec, lrec), "metrics sink submit");
@@ -677,6 +743,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     if (cfg_.tracker && is_server) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
     check_errors(r);
   }
+  ovl_join();
   rounds_run_ += done;
   host_ns_ += (double)(steady_ns() - t_begin);
   return done;
@@ -721,8 +788,9 @@ std::vector<int> LanesLoop::stats(int lane, hipStream_t stream) const {
 }
 
 float LanesLoop::loss(int lane, hipStream_t stream) const {
-  float v[2] = {0.f, 0.f};
-  hip_check(hipMemcpyAsync(v, lanes_.at(lane).loss2, 2 * sizeof(float), hipMemcpyDeviceToHost, stream), "lane loss");
+  float v[kLaneBufs] = {0.f, 0.f, 0.f};
+  hip_check(hipMemcpyAsync(v, lanes_.at(lane).loss2, kLaneBufs * sizeof(float), hipMemcpyDeviceToHost, stream),
+            "lane loss");
   hip_check(hipStreamSynchronize(stream), "sync");
   return v[last_par_];
 }

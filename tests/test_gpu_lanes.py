@@ -385,3 +385,36 @@ def test_copy_out_all_equals_per_lane_copies(cuda):
     for i in range(L):
         assert torch.equal(d_all[i], one[i]), i
         assert torch.equal(l_all[i], l_one[i]) and torch.isfinite(l_all[i]).all(), i
+
+
+@pytest.mark.parametrize("L,tile,rows", [(8, "2", True), (3, "2", True), (8, "0", True), (8, "2", False)])
+def test_overlapped_launches_equal_serial(cuda, monkeypatch, L, tile, rows):
+    """Overlapped round launches (PSX_LANES_OVERLAP=1, LanesArgs::ovl: round r + 1's
+    launch dispatched while round r's evaluation still runs, the hand-offs through
+    the applied / evdone counters, fragments over three buffers) give the serial
+    launches' weights and deltas bit for bit and the same rows, across two calls."""
+    spec, train, ev = _data(cuda)
+    monkeypatch.setenv("PSX_RIDERS_TILE", tile)
+    out = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("PSX_LANES_OVERLAP", ov)
+        w = spec.init("random", seed=6, device=cuda)
+        log = LogSink(spec.K, cuda) if rows else None
+        frags = [Fragments(spec, cuda) for _ in range(3)]
+        lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, sink=log, frags=frags)
+        assert lp.overlap == (ov == "1")
+        assert lp.run(6, 0, stream_handle(cuda)) == 6
+        assert lp.run(3, 6, stream_handle(cuda)) == 3  # (a second call continues the chain)
+        lp.flush(stream_handle(cuda))
+        torch.cuda.synchronize()
+        lp.poll_errors()
+        out.append((w.clone(), _deltas(lp, L, spec, cuda), log.book if rows else None))
+        if rows:
+            log.close()
+    (wa, da, a), (wb, db, b) = out
+    assert torch.equal(wa, wb), (wa - wb).abs().max().item()
+    for l in range(L):
+        assert torch.equal(da[l], db[l]), l
+    if rows:
+        assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 9
+        assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 9 * L

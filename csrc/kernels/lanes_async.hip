@@ -121,7 +121,10 @@ __device__ __forceinline__ const T* fresh(const T* p) {
 
 // One iteration of lane l's loop (workgroup wg): release -> solve -> push ->
 // evaluation.  false: the lane got its stop record.
-template <int FP, int KP, int S>
+// MT: rings over 32 tiles possible (a build of its own: the restaging forward's
+// registers would spill in the resident form -- 192 B of scratch, 62.6k -> 58.0k
+// updates/s, profiles/r04/s19)
+template <int FP, int KP, int S, bool MT>
 __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg, const AsyncArgs& a,
                                                 const AsyncLaneDev& A, int l, int wg, unsigned& run,
                                                 unsigned long long& relc, unsigned long long& lw) {
@@ -161,7 +164,8 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     const int spin = spin_limit(dv);
     const SolveParams win{q.r.B, q.r.start, 0, 0};
     const WinTiles wt(win.start, win.B, cfg.cap);
-    const int ntr = wt.nt < wt.T ? wt.nt : wt.T;
+    const int ntt = wt.nt < wt.T ? wt.nt : wt.T;   // ring tiles of the window
+    const int ntr = ntt < kLaneWg ? ntt : kLaneWg;  // row workgroups (tiles wg, wg + ntr, ...)
     const int G = ntr > NS ? ntr : NS;
     const bool row = wg < ntr, owner = wg < NS;
     const unsigned rn = run;
@@ -191,8 +195,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
         if constexpr (S == 1) xstore(xch + kXchGen + ((rn + 1u) & 1u), 0ull);
       }
       if (row) {
-        const int rt = wt.ring_tile(wg);
-        lane_stage_stats<FP, S>(lf, lsy, cfg, dv, q.r, a.dsX, a.dsy, rt, A.spart + (size_t)wg * FP * 2);
+        lane_stage_stats<FP, S>(lf, lsy, cfg, dv, q.r, a.dsX, a.dsy, wt, wg, ntr, ntt, A.spart + (size_t)wg * FP * 2);
       }
       barrier();
       if (owner) {
@@ -209,7 +212,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
           f32x4 acc[NT];
 #pragma unroll
           for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
-          fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
+          if (MT && ntt > kLaneWg)  // (several ring tiles per row workgroup: staged every slot)
+            fwd_body<FP, true, false, S, true, true>(cfg, win, slot, dv, lf, wg, G, acc);
+          else
+            fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
           store_gpf<FP, S == 1>(dv, wg, G, acc);
         }
         barrier();
@@ -296,7 +302,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   return true;
 }
 
-template <int FP, int KP, int S>
+template <int FP, int KP, int S, bool MT>
 __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __restrict__ pk,
                                                           const AsyncLaneDev* __restrict__ als) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
   for (;;) {
     const AsyncPack* p = fresh(pk);
     const AsyncLaneDev* A = fresh(als + l);
-    if (!async_iteration<FP, KP, S>(lds, p->cfg, p->a, *A, l, wg, run, relc, lw)) return;
+    if (!async_iteration<FP, KP, S, MT>(lds, p->cfg, p->a, *A, l, wg, run, relc, lw)) return;
   }
 }
 
@@ -356,33 +362,38 @@ __global__ void async_init_kernel(const float* __restrict__ w, float* snap, unsi
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = t;
 }
 
-template <int FP, int KP, int S>
+template <int FP, int KP, int S, bool MT>
 void launch_afks(const AsyncPack* pk, const AsyncLaneDev* al, hipStream_t s) {
-  static const bool prepared = ((void)hipFuncSetAttribute((const void*)lanes_async_kernel<FP, KP, S>,
+  static const bool prepared = ((void)hipFuncSetAttribute((const void*)lanes_async_kernel<FP, KP, S, MT>,
                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                                           (int)lanes_lds_bytes(FP)),
                                 true);
   (void)prepared;
-  lanes_async_kernel<FP, KP, S><<<8 * kLaneWg, 256, lanes_lds_bytes(FP), s>>>(pk, al);
+  lanes_async_kernel<FP, KP, S, MT><<<8 * kLaneWg, 256, lanes_lds_bytes(FP), s>>>(pk, al);
 }
 
 template <int FP, int KP>
-void launch_afk(const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
-  if (S == 2)
-    launch_afks<FP, KP, 2>(pk, al, s);
+void launch_afk(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+  const bool mt = cfg.cap > 32 * kLaneWg;
+  if (S == 2 && mt)
+    launch_afks<FP, KP, 2, true>(pk, al, s);
+  else if (S == 2)
+    launch_afks<FP, KP, 2, false>(pk, al, s);
+  else if (mt)
+    launch_afks<FP, KP, 1, true>(pk, al, s);
   else
-    launch_afks<FP, KP, 1>(pk, al, s);
+    launch_afks<FP, KP, 1, false>(pk, al, s);
 }
 
 template <int FP>
 void launch_af(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
   const int KP = padded_classes(cfg.K);
   if (KP <= 2)
-    launch_afk<FP, 2>(pk, al, S, s);
+    launch_afk<FP, 2>(cfg, pk, al, S, s);
   else if (KP <= 4)
-    launch_afk<FP, 4>(pk, al, S, s);
+    launch_afk<FP, 4>(cfg, pk, al, S, s);
   else
-    launch_afk<FP, 8>(pk, al, S, s);
+    launch_afk<FP, 8>(cfg, pk, al, S, s);
 }
 
 }  // namespace

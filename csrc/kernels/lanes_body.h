@@ -555,24 +555,23 @@ __device__ __forceinline__ bool lane_arrive(unsigned* arrive, int idx, int L, in
 }
 
 // ---------------------------------------------------------------------------
-// Phase I of a lane's solve, row role: stage ring tile `rt` into the LDS image,
-// the round's new rows straight from the dataset (also written into the ring),
-// and publish the tile's column sums / sums of squares over its window rows.
-// Thread t holds chunk cg = t % CPR (8 features) of rows g + NG j (g = t / CPR),
-// so the sums come from the staging registers; the NG row groups are combined
-// in LDS (fixed order).
+// Phase I of a lane's solve, row role: row workgroup `wg` of `ntr` takes window ring
+// tiles wg, wg + ntr, ... (of `ntt`: one each up to 32 tiles, a 1,024-row ring; more
+// for longer windows), stages them into the LDS image (the last one stays: resident
+// when it is the only one), the round's new rows straight from the dataset (also
+// written into the ring), and publishes its tiles' column sums / sums of squares
+// over their window rows.  Thread t holds chunk cg = t % CPR (8 features) of rows
+// g + NG j (g = t / CPR), so the sums come from the staging registers (tile order);
+// the NG row groups are combined in LDS (fixed order).
 template <int FP, int S>
 __device__ __forceinline__ void lane_stage_stats(char* lf, float* scratch, const SolverCfg& cfg, const SolveDev& dv,
-                                                 const LaneRound& r, const uint16_t* dsX, const int32_t* dsy, int rt,
-                                                 float* spart_wg) {
+                                                 const LaneRound& r, const uint16_t* dsX, const int32_t* dsy,
+                                                 const WinTiles& wt, int wg, int ntr, int ntt, float* spart_wg) {
   constexpr int CPR = FP / 8, NG = 256 / CPR, PER_T = 32 * CPR / 256;
   const int tid = threadIdx.x, cap = cfg.cap;
   const int cg = tid % CPR, g = tid / CPR;
   uint16_t* X = const_cast<uint16_t*>(dv.X);
   int32_t* Y = const_cast<int32_t*>(dv.y);
-  // labels travel with the first loads
-  int yv = 0;
-  bool ynew = false;
   // the dataset row of ring slot s when it holds one of this round's new rows, else -1
   auto new_src = [&](int s) -> long long {
     int dn = s - r.dst;
@@ -581,45 +580,52 @@ __device__ __forceinline__ void lane_stage_stats(char* lf, float* scratch, const
     if (dn - r.n < r.n2) return r.first2 + (long long)(dn - r.n) * r.step;
     return -1;
   };
-  if (tid < 32) {
-    const int s = rt * 32 + tid;
-    const long long src = new_src(s);
-    ynew = src >= 0;
-    yv = ynew ? dsy[src] : dv.y[s];
-  }
-  u16x8 v[PER_T];
-  bool isnew[PER_T], valid[PER_T];
-#pragma unroll
-  for (int j = 0; j < PER_T; ++j) {
-    const int row = g + NG * j, s = rt * 32 + row;
-    const long long sr = new_src(s);
-    isnew[j] = sr >= 0;
-    int dw = s - r.start;
-    if (dw < 0) dw += cap;
-    valid[j] = dw < r.B;
-    const uint16_t* src = isnew[j] ? dsX + (size_t)sr * FP : dv.X + (size_t)s * FP;
-    v[j] = *(const u16x8*)(src + cg * 8);
-  }
   float sm[8], sq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) sm[e] = sq[e] = 0.f;
+  for (int ti = wg; ti < ntt; ti += ntr) {
+    const int rt = wt.ring_tile(ti);
+    // labels travel with the first loads
+    int yv = 0;
+    bool ynew = false;
+    if (tid < 32) {
+      const int s = rt * 32 + tid;
+      const long long src = new_src(s);
+      ynew = src >= 0;
+      yv = ynew ? dsy[src] : dv.y[s];
+    }
+    u16x8 v[PER_T];
+    bool isnew[PER_T], valid[PER_T];
 #pragma unroll
-  for (int j = 0; j < PER_T; ++j) {
-    const int row = g + NG * j, s = rt * 32 + row;
-    *(u16x8*)(lf + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
-    if (isnew[j]) *(u16x8*)(X + (size_t)s * FP + cg * 8) = v[j];  // the ring keeps the new row
-    if (valid[j]) {
+    for (int j = 0; j < PER_T; ++j) {
+      const int row = g + NG * j, s = rt * 32 + row;
+      const long long sr = new_src(s);
+      isnew[j] = sr >= 0;
+      int dw = s - r.start;
+      if (dw < 0) dw += cap;
+      valid[j] = dw < r.B;
+      const uint16_t* src = isnew[j] ? dsX + (size_t)sr * FP : dv.X + (size_t)s * FP;
+      v[j] = *(const u16x8*)(src + cg * 8);
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float x = bf2f(v[j][e]);
-        sm[e] += x;
-        sq[e] += x * x;
+    for (int j = 0; j < PER_T; ++j) {
+      const int row = g + NG * j, s = rt * 32 + row;
+      *(u16x8*)(lf + (cg >> 4) * 8192 + lds_off(row, cg & 15)) = v[j];
+      if (isnew[j]) *(u16x8*)(X + (size_t)s * FP + cg * 8) = v[j];  // the ring keeps the new row
+      if (valid[j]) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = bf2f(v[j][e]);
+          sm[e] += x;
+          sq[e] += x * x;
+        }
       }
     }
-  }
-  if (tid < 32) {
-    ((int*)(lf + 32 * FP * 2 + 8192 + 2048))[tid] = yv;  // fwd_body's label slots
-    if (ynew) Y[rt * 32 + tid] = yv;
+    if (tid < 32) {
+      ((int*)(lf + 32 * FP * 2 + 8192 + 2048))[tid] = yv;  // fwd_body's label slots
+      if (ynew) Y[rt * 32 + tid] = yv;
+    }
+    if (ti + ntr < ntt) __syncthreads();  // (the next tile's image over this one)
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {

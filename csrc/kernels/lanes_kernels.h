@@ -40,6 +40,9 @@ namespace psx {
 
 constexpr int kMaxLanes = 8;
 constexpr int kLaneWg = 32;  // cooperating workgroups per lane: the CUs of one XCD
+// longest ring (window) of a lane: up to 32 tiles (1,024 rows) stay resident in the
+// row workgroups' LDS; longer rings are staged tile by tile every slot
+constexpr int kLanesMaxCap = 8192;
 constexpr int kMaxEvalModels = kMaxLanes + 1;
 // model buffers per lane (local fragments, intercepts, loss) and of the server
 // fragments, by round: r % 2, or r % 3 with overlapped launches (round r's

@@ -9,8 +9,9 @@
 namespace psx {
 
 bool lanes_supported(int FP, int K, int cap) {
+  // (rings over 32 tiles: each row workgroup stages several tiles every slot)
   return FP >= 128 && FP <= 1024 && (FP & (FP - 1)) == 0 && K >= 2 && K <= 8 && cap >= 32 && cap % 32 == 0 &&
-         cap <= 32 * kLaneWg;
+         cap <= kLanesMaxCap;
 }
 size_t lanes_lds_bytes(int FP) { return persist_fwd_bytes(FP) + (kBwdLdsBytes + 15) / 16 * 16 + kSyBytes; }
 int lanes_grid(int L, int min_riders) {
@@ -83,7 +84,8 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   const LaneRound rr = pick(a.r, l);
   const SolveParams win{rr.B, rr.start, 0, 0};
   const WinTiles wt(win.start, win.B, cfg.cap);
-  const int ntr = wt.nt < wt.T ? wt.nt : wt.T;  // row workgroups (ring tiles of the window)
+  const int ntt = wt.nt < wt.T ? wt.nt : wt.T;   // ring tiles of the window
+  const int ntr = ntt < kLaneWg ? ntt : kLaneWg;  // row workgroups (tiles wg, wg + ntr, ...)
   const int G = ntr > NS ? ntr : NS;
   if (wg >= G) {
     join_eval();
@@ -167,8 +169,8 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   // ---- phase I: stage + ingest + window statistics, then x0 / first trial point ----
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
   if (row) {
-    const int rt = wt.ring_tile(wg);
-    lane_stage_stats<FP, S>(lf, lsy, cfg, dv, rr, a.dsX, a.dsy, rt, lanes[l].spart + (size_t)wg * FP * 2);
+    lane_stage_stats<FP, S>(lf, lsy, cfg, dv, rr, a.dsX, a.dsy, wt, wg, ntr, ntt,
+                            lanes[l].spart + (size_t)wg * FP * 2);
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 1);
   barrier();
@@ -195,7 +197,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       f32x4 acc[NT];
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[n] = f32x4{0, 0, 0, 0};
-      fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
+      if (ntt > kLaneWg)  // (several ring tiles per row workgroup: staged every slot)
+        fwd_body<FP, true, false, S, true, true>(cfg, win, slot, dv, lf, wg, G, acc);
+      else
+        fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
       store_gpf<FP, S == 1>(dv, wg, G, acc);
     }
     barrier();

@@ -119,7 +119,7 @@ __device__ __forceinline__ void bwd_tile_acc(const char* lds, const unsigned sho
 // kModRows (multi-lane round kernel): workgroup tiles are the window's RING tiles
 // (at most cap/32 of them: a window that wraps onto its own first ring tile is one
 // tile, not two) and a row is in the window iff (slot - start) mod cap < B.
-template <int FP, bool kRows = false, bool kF32 = false, int kP = 0, bool kModRows = false>
+template <int FP, bool kRows = false, bool kF32 = false, int kP = 0, bool kModRows = false, bool kRestage = false>
 __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams pr, int slot, const SolveDev& dv,
                                          char* lds, const int wg, const int G, f32x4* gacc = nullptr,
                                          const int entry_phase = -1) {
@@ -153,15 +153,20 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
   // the two memory latencies overlap (register budget allows it up to FP 1024)
   constexpr bool kPre = FP <= 1024;
   WFrag<kPre ? FP : 128> wf;
-  if constexpr (kPre) {
-    if constexpr (kP != 0)
+  auto fetch_w = [&]() {
+    if constexpr (kPre && kP != 0)
       load_wfrag_sc1<FP, kP>(wf, dv.whi, dv.wlo, K);
-    else
+    else if constexpr (kPre)
       load_wfrag<FP>(wf, dv.whi, dv.wlo, K);
-  }
+  };
+  // (kRestage: fetched per tile, after its staging loads -- both sets of registers
+  // live at once would spill)
+  if constexpr (kPre && !kRestage) fetch_w();
+  // persistent: the tile staged once, at the start of the solve -- unless the window
+  // has more ring tiles than row workgroups (kRestage: every slot stages each of them)
   for (int tile = wg; tile < ntiles; tile += G) {
     const int64_t row0 = (int64_t)wt.ring_tile(tile) * 32;
-    if constexpr (kP == 0) {  // (persistent: staged once, at the start of the solve)
+    if constexpr (kP == 0 || kRestage) {
       const int yv = tid < 32 ? dv.y[row0 + tid] : 0;  // issued with the tile's loads (one round trip)
       if constexpr (kF32)
         stage_tile_f32<FP>(lds, lds_lo, dv.Xf, row0);
@@ -169,6 +174,7 @@ __device__ __forceinline__ void fwd_body(const SolverCfg& cfg, const SolveParams
         stage_tile<FP>(lds, dv.X, row0, 32, cfg.cap, false);
       if (tid < 32) ylds[tid] = yv;
     }
+    if constexpr (kPre && kRestage) fetch_w();
     __syncthreads();
     // converged in an earlier slot: exit (the phase word was loaded at kernel
     // entry, so its latency overlapped the tile staging; nothing written yet)

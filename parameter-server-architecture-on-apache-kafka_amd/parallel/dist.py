@@ -621,7 +621,7 @@ class DistEngine:
                 ds = W[0].source.ds
                 d.update(dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows))
             if srv is not None:
-                self._lane_frags = [Fragments(sp, self.device), Fragments(sp, self.device)]
+                self._lane_frags = [Fragments(sp, self.device) for _ in range(3)]  # (3: overlapped rounds)
                 d.update(shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
                          sb=[f.b.data_ptr() for f in self._lane_frags])
             ev = self.evalset

@@ -234,7 +234,7 @@ class LocalEngine:
 
     def _lanes_ok(self) -> bool:
         """The multi-lane round loop (csrc/runtime/lanes_loop.h) runs this BSP run:
-        1..8 dense GPU workers with bf16 rings of <= 1024 rows, ONE launch per round
+        1..8 dense GPU workers with bf16 rings of <= 8192 rows, ONE launch per round
         (every worker's solve on its own XCD, the update, the previous round's
         evaluation rows).  Runs that need Python between rounds (tracing, injected
         faults) use the loops below.  The tuple-driven cadence (--iter_new_*) and
@@ -296,7 +296,7 @@ class LocalEngine:
         sc.mode = 1 if o.mode == "gd" else 0
         sc.center, sc.zero_const = int(o.center), int(o.zero_const)
         sc.nslots, sc.gd_lr, sc.tol = o.nslots, o.gd_lr, o.tol
-        self._lane_frags = [Fragments(sp, self.device), Fragments(sp, self.device)]
+        self._lane_frags = [Fragments(sp, self.device) for _ in range(3)]  # (3: overlapped rounds)
         src0, ev = W[0].source, self.evalset
         d = dict(scfg=sc, dsX=src0.ds.X.data_ptr(), dsy=src0.ds.y.data_ptr(), ds_rows=int(src0.ds.rows),
                  N=int(cfg.num_workers), per_iter_rows=src0.rows_per_iter if src0.mode == "per_iter" else 0,

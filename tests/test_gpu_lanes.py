@@ -418,3 +418,87 @@ def test_overlapped_launches_equal_serial(cuda, monkeypatch, L, tile, rows):
     if rows:
         assert [r[1:] for r in a.server] == [r[1:] for r in b.server] and len(a.server) == 9
         assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 9 * L
+
+
+@pytest.mark.parametrize("cap", [2048, 4096])
+def test_lanes_long_ring_matches_reference(cuda, cap):
+    """Rings over 1,024 rows (-max 2048 / 4096) stay on the one-launch path: each row
+    workgroup stages several ring tiles every slot.  One lane's delta against the
+    float64 oracle of the reference solve over its full window, and the update."""
+    spec, train, ev = _data(cuda, rows=4 * cap + 64)
+    assert _native.hip().lanes_supported(spec.Fp, spec.K, cap)
+    L = 4
+    w0 = spec.init("random", seed=5, device=cuda)
+    w = w0.clone()
+    lp, keep = _loop(spec, list(range(L)), L, train, ev, w, cuda, rows=cap, cap=cap, lr=0.25)
+    assert lp.run(1, 0, stream_handle(cuda)) == 1
+    ds = _deltas(lp, L, spec, cuda)
+    lp.poll_errors()
+    ref_w = w0 + 0.25 * (((ds[0] + ds[1]) + ds[2]) + ds[3])
+    assert torch.allclose(w, ref_w, atol=2e-6, rtol=1e-5)
+    Xw = train.X[1::L][:cap, : spec.F].float().cpu()
+    yw = train.y[1::L][:cap].long().cpu()
+    res = local_solve_reference(Xw, yw, spec.coef(w0.cpu()), spec.intercept(w0.cpu()))
+    ref = spec.pack(res.coef, res.intercept) - w0.cpu()
+    got = ds[1].cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 2e-2 * scale + 1e-4, (err, scale)
+
+
+def test_lanes_long_ring_wraps_and_equals_alone(cuda):
+    """A 2,048-row ring filled 1,500 rows per round: the second round's window wraps
+    the ring at an unaligned start (its newest rows share the first ring tile).  The
+    ring holds the expected rows, and lane l of the 3-lane round equals worker l's
+    round run alone, bit for bit, in both rounds."""
+    cap, rows, L = 2048, 1500, 3
+    spec, train, ev = _data(cuda, rows=3 * 3000 + 64)
+    w0 = spec.init("random", seed=3, device=cuda)
+    w = w0.clone()
+    lp, (rings, wins, frags) = _loop(spec, list(range(L)), L, train, ev, w, cuda, rows=rows, cap=cap, lr=0.0)
+    multi = []
+    for rnd in range(2):
+        lp.run(1, rnd, stream_handle(cuda))
+        multi.append(_deltas(lp, L, spec, cuda))
+    lp.poll_errors()
+    for k in range(L):
+        j = torch.arange(3000)
+        X, y = rings[k]
+        slots = j % cap
+        keep_ = j >= 3000 - cap
+        src = (k + j * L)[keep_]
+        assert torch.equal(X[slots[keep_].to(cuda)].cpu(), train.X[src.to(cuda)].cpu()), k
+        assert torch.equal(y[slots[keep_].to(cuda)].cpu(), train.y[src.to(cuda)].cpu()), k
+    for l in range(L):  # the wrapped window against the float64 oracle
+        src = (l + torch.arange(3000 - cap, 3000) * L).to(cuda)
+        res = local_solve_reference(train.X[src][:, : spec.F].float().cpu(), train.y[src].long().cpu(),
+                                    spec.coef(w0.cpu()), spec.intercept(w0.cpu()))
+        ref = spec.pack(res.coef, res.intercept) - w0.cpu()
+        err = (multi[1][l].cpu() - ref).abs().max().item()
+        assert err <= 2e-2 * ref.abs().max().item() + 1e-4, (l, err, ref.abs().max().item())
+    for l in range(L):
+        wl = w0.clone()  # (held: the loop keeps only its address)
+        lp1, keep1 = _loop(spec, [l], L, train, ev, wl, cuda, rows=rows, cap=cap, lr=0.0)
+        for rnd in range(2):
+            lp1.run(1, rnd, stream_handle(cuda))
+            alone = _deltas(lp1, 1, spec, cuda)[0]
+            assert torch.equal(alone, multi[rnd][l]), (rnd, l, (alone - multi[rnd][l]).abs().max().item())
+
+
+@pytest.mark.parametrize("c", [0, 10])
+def test_engine_long_window_runs_on_lanes(cuda, c):
+    """-max 4096 with several workers: BSP on the one-launch lanes loop, SSP on the
+    asynchronous lanes loop (no fallback to the per-worker stream schedulers)."""
+    train, test = synth_finefood(40000, seed=0), synth_finefood(2000, seed=1)
+    cfg = PSConfig(num_workers=4, consistency_model=c, producer_time_per_event=0, stream_mode="per_iter",
+                   rows_per_iter=1024, epochs=100, max_iters=8, min_buffer_size=128, max_buffer_size=4096,
+                   init="random")
+    eng = LocalEngine(cfg, cuda, train=train, test=test)
+    out = eng.run()
+    if c == 0:
+        assert out.get("lanes") == 4 and out["rounds"] == 8, out
+    else:
+        assert out.get("async_lanes"), out
+    assert len(eng.log.book.server) >= 8
+    loss = eng.workers[0].solver.loss.item()
+    assert loss == loss and loss > 0

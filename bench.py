@@ -318,7 +318,8 @@ def main(argv=None):
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
     res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),
-                     "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2)}
+                     "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2),
+                     "host_phases_us": getattr(eng, "native_host_phases_us", None)}
     if "phases_ms" in out:  # where the timed region's wall clock went (host view)
         res["native"]["phases_ms"] = dict(out["phases_ms"], drain=round((t0 + dt - t_run) * 1e3, 3))
     rows = list(eng.log.book.server)

@@ -805,6 +805,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("lane_eval", &LanesLoop::lane_eval)
       .def_property_readonly("overlap", &LanesLoop::overlap)
       .def_property_readonly("host_us_per_round", &LanesLoop::host_us_per_round)
+      .def("host_phases_us", &LanesLoop::host_phases_us)
       .def_property_readonly("rounds_run", &LanesLoop::rounds_run)
       .def("stats", [](const LanesLoop& l, int lane, uintptr_t s) { return l.stats(lane, S(s)); })
       .def("loss", [](const LanesLoop& l, int lane, uintptr_t s) { return l.loss(lane, S(s)); })

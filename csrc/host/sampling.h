@@ -44,24 +44,36 @@ class RateEstimator {
     last_ms_ = now_ms;
   }
   // k arrivals at the last stamp (k zero deltas): the same state as k arrival()
-  // calls -- adding 0.0 leaves the sum unchanged (it is never -0.0), evictions are
-  // subtracted in order.
+  // calls -- adding 0.0 leaves the sum unchanged (it is never -0.0), the evictions of
+  // the entries present before the call are subtracted in order (an entry is evicted
+  // before its slot is rewritten: the buffer holds window + 1), and the evictions of
+  // this call's own zeros change nothing.  O(window), not O(k): a round's 1,024-row
+  // delivery to 8 workers cost ~42 us of the host loop one zero at a time.
   void zeros(int64_t k) {
     if (!have_last_) {  // the first of them only sets the stamp
       if (k <= 0) return;
       have_last_ = true;
       --k;
     }
-    const int B = (int)buf_.size();
-    for (int64_t i = 0; i < k; ++i) {
-      buf_[tail_] = 0.0;
-      tail_ = tail_ + 1 == B ? 0 : tail_ + 1;
-      if (++n_ > window_) {
-        sum_ -= buf_[head_];
-        head_ = head_ + 1 == B ? 0 : head_ + 1;
-        --n_;
-      }
+    if (k <= 0) return;
+    const int64_t B = (int64_t)buf_.size();
+    const int64_t e = n_ + k > window_ ? n_ + k - window_ : 0;  // evictions
+    const int64_t eo = e < n_ ? e : n_;                          // ... of entries present before
+    int h = head_;
+    for (int64_t i = 0; i < eo; ++i) {
+      const double v = buf_[h];
+      if (v != 0.0) sum_ -= v;  // (x - 0.0 == x: only the nonzero deltas form the chain)
+      h = h + 1 == (int)B ? 0 : h + 1;
     }
+    const int64_t kw = k < B ? k : B;  // the slots this call's zeros end in
+    int64_t t = (tail_ + (k - kw)) % B;
+    for (int64_t i = 0; i < kw; ++i) {
+      buf_[t] = 0.0;
+      t = t + 1 == B ? 0 : t + 1;
+    }
+    tail_ = (int)((tail_ + k) % B);
+    head_ = (int)((head_ + e) % B);
+    n_ = (int)(n_ + k - e);
   }
   // Mean inter-arrival time in ms (1000 when fewer than two arrivals).
   double mean_interarrival_ms() const { return n_ == 0 ? 1000.0 : sum_ / static_cast<double>(n_); }

@@ -420,6 +420,15 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     first = false;
   }
   if constexpr (kStop == 1) return;
+  if (ev.slab) {  // slab form: this rider's counts, every cell (zeros included); no ticket
+    int* row = ev.slab + (size_t)rid * kMaxEvalModels * kSlabCells;
+    for (int q = tid; q < M * kSlabCells; q += 256) {
+      const int m = q >> 6, c = q & 63;
+      row[q] = cl[m * 256 + (c >> 3) * 16 + (c & 7)];
+    }
+    if (rid == 0) rstamp(8);
+    return;
+  }
   {
     const int cp = xcd_copy();
     for (int m = 0; m < M; ++m) {

@@ -105,6 +105,11 @@ struct EvalMulti {
   // tiles popped from xq[0], zero at launch)
   int form;
   int ppi;  // tile-resident form: model pairs per work item (0: all; items = (tile, pair group))
+  // != nullptr (tile-resident form, overlapped launches): no ticket -- every rider
+  // stores its counts, [rider][kMaxEvalModels][64] ints (cell = label * 8 + predicted),
+  // and a publish launch behind the round (launch_lanes_publish, co-running with the
+  // next round) sums them and fills the slots; its nticket riders write their rows
+  int* slab;
   // PSX_LANES_STAMPS: s_memrealtime stamps of the riders (nullptr: none): [0] rider 0
   // enters, [1] its first tile staged, [2..5] its items done, [8] it arrives on the
   // ticket, [10] the last rider is known, [11] its publication done, [12] / [13] the
@@ -176,6 +181,12 @@ size_t lanes_lds_bytes(int FP);
 int lanes_grid(int L, int min_riders);
 // S = 2: one-XCD hand-offs (blockIdx % 8 == XCC_ID verified); S = 1: sc1 hand-offs.
 void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const LanesArgs& a, int S, hipStream_t s);
+// The slab form's publication (EvalMulti::slab): one small workgroup per model sums the
+// ev.nticket riders' counts and writes the model's slot; it also clears the tile queue
+// ev.xq.  Sized to co-run with a round kernel (a few KB of LDS, <= 64 VGPRs).
+constexpr int kSlabCells = 64;
+constexpr int kSlabRiders = 1024;  // slab rows allocated (riders of one launch at most)
+void launch_lanes_publish(const EvalMulti& ev, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).
 void launch_xcc_probe(int* ids, int n, hipStream_t s);
 // Every lane's last delta [P] and training loss to caller buffers in ONE launch (the

@@ -338,6 +338,49 @@ void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const La
 void launch_xcc_probe(int* ids, int n, hipStream_t s) { xcc_probe_kernel<<<n, 64, 0, s>>>(ids, n); }
 
 namespace {
+// Workgroup m: model m's counts summed over the riders' slab rows (4 row groups of
+// 64 cells, integer sums: any order gives the same counts), then its slot as tagged
+// 16-B system-scope chunks (publish_counts' format).  Block 0 clears the tile queue.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void lanes_publish_kernel(EvalMulti ev) {
+  __shared__ int part[4][kSlabCells];
+  __shared__ int cells[kSlabCells];
+  const int m = (int)blockIdx.x, tid = threadIdx.x, K = ev.K, KK = K * K;
+  const int c = tid & 63, g = tid >> 6;
+  int t = 0;
+  const int* col = ev.slab + (size_t)m * kSlabCells + c;
+  for (int r = g; r < (int)ev.nticket; r += 4) t += col[(size_t)r * kMaxEvalModels * kSlabCells];
+  part[g][c] = t;
+  __syncthreads();
+  if (tid < KK) {
+    const int yl = tid / K, p = tid - yl * K, cc = yl * 8 + p;
+    cells[tid] = part[0][cc] + part[1][cc] + part[2][cc] + part[3][cc];
+  }
+  if (m == 0 && tid == 0 && ev.xq) __hip_atomic_store(ev.xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid < 64) {
+    const EvalModel E = pick(ev.m, m);
+    const unsigned tag = eval_tag(E.seq);
+    const int nch = 1 + (KK + 2) / 3;
+    TagChunk ch;
+    if (tid == 0) {
+      const float lv = E.loss ? *E.loss : 0.f;
+      ch = TagChunk{tag, (unsigned)__float_as_int(lv), (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (tid - 1);
+      auto cv = [&](int q) { return q < KK ? (unsigned)cells[q] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    if (tid < nch) st_sys_chunk(E.slot, 1088u, (unsigned)tid * 16u, ch);
+  }
+}
+}  // namespace
+
+void launch_lanes_publish(const EvalMulti& ev, hipStream_t s) {
+  if (ev.nmodels <= 0 || !ev.slab) return;
+  lanes_publish_kernel<<<ev.nmodels, 256, 0, s>>>(ev);
+}
+
+namespace {
 // grid (blocks per lane, L): the lane's delta in float4 pieces, its loss by block 0
 __global__ __launch_bounds__(256) void lanes_copy_out_kernel(LanesCopyOut c) {
   const int l = (int)blockIdx.y;

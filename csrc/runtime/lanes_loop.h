@@ -156,6 +156,14 @@ class LanesLoop {
   // consecutive rounds overlap (LanesArgs::ovl)
   bool overlap() const { return ovl_; }
   double host_us_per_round() const { return rounds_run_ ? host_ns_ / 1000.0 / (double)rounds_run_ : 0.0; }
+  // the host loop's time per round by phase (us): [0] deliveries + window wait, [1]
+  // evaluation slots (sink), [2] the launches (+ the stream operations of overlap),
+  // [3] rows handed over, tracker, error words
+  std::vector<double> host_phases_us() const {
+    std::vector<double> v(4, 0.0);
+    for (int i = 0; i < 4; ++i) v[i] = rounds_run_ ? host_ph_ns_[i] / 1000.0 / (double)rounds_run_ : 0.0;
+    return v;
+  }
   int64_t rounds_run() const { return rounds_run_; }
   // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
   std::vector<int> stats(int lane, hipStream_t stream) const;
@@ -262,6 +270,8 @@ class LanesLoop {
   unsigned* applied_ = nullptr;  // [32] LanesArgs::applied
   unsigned* evdone_ = nullptr;   // LanesArgs::evdone
   unsigned* ovlq_ = nullptr;     // the riders' tile queue (EvalMulti::xq) of overlapped launches
+  int* slab_ = nullptr;          // EvalMulti::slab (overlapped launches, tile-resident riders)
+  bool slab_on_ = false;         // PSX_RIDERS_SLAB (default 1): the slab form with overlap
   uint64_t ovl_n_ = 0;           // overlapped launches so far (LanesArgs::round)
   bool ovl_chain_ = false;       // a launch of this run() call precedes (wait for its dispatch)
   int ovl_prev_grid_ = 0, ovl_prev_cpar_ = 0;
@@ -273,6 +283,7 @@ class LanesLoop {
   int inject_spin_ = 0;
   int64_t rounds_run_ = 0;
   double host_ns_ = 0.0;
+  double host_ph_ns_[4] = {0.0, 0.0, 0.0, 0.0};
   // asynchronous loop state (allocated by the first run_async)
   void* aws_ = nullptr;                 // device workspace
   AsyncLaneDev* al_dev_ = nullptr;      // device table

@@ -154,6 +154,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const size_t o_ltic = take((size_t)kMaxLanes * 32 * sizeof(unsigned));
   const size_t o_rdbg = stamps ? take(64 * sizeof(long long)) : 0;
   const size_t o_ovl = take(64 * sizeof(unsigned));  // applied [0, 32), evdone [32], tile queue [48]
+  const size_t o_slab = take((size_t)kSlabRiders * kMaxEvalModels * kSlabCells * sizeof(int));
   hip_check(hipMalloc(&ws_, off), "hipMalloc(lanes workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(lanes workspace)");
   char* b = static_cast<char*>(ws_);
@@ -223,6 +224,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   applied_ = reinterpret_cast<unsigned*>(b + o_ovl);
   evdone_ = applied_ + 32;
   ovlq_ = applied_ + 48;
+  slab_ = reinterpret_cast<int*>(b + o_slab);
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
   // PSX_LANES_SIDE_EVAL=1: the rows go to a co-running side launch instead of riders
@@ -263,6 +265,12 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const char* ov = std::getenv("PSX_LANES_OVERLAP");
   const bool sfr = !cfg_.shi[0] || (cfg_.shi[2] && cfg_.slo[2] && cfg_.sb[2]);  // (a sink may come later)
   ovl_ = ov && ov[0] == '1' && !comm_ && cfg_.L > 0 && S_ == 2 && !side_eval_ && !lane_eval_ && !xcd_riders_ && sfr;
+  // PSX_RIDERS_SLAB (default 1, overlapped launches with tile-resident riders): the
+  // riders store their counts (EvalMulti::slab) instead of flushing them with atomics
+  // and waiting on a ticket; a publish launch behind each round sums them and fills
+  // the slots while the next round runs
+  const char* sl = std::getenv("PSX_RIDERS_SLAB");
+  slab_on_ = ovl_ && tile_riders_ && !(sl && sl[0] == '0');
   if (ovl_) {
     hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
     hip_check(hipEventCreateWithFlags(&ovl_in_, hipEventDisableTiming), "hipEventCreate");
@@ -567,6 +575,12 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     const int64_t r = r0 + done;
     const int par = ovl_ ? (int)(((r % 3) + 3) % 3) : (int)(r & 1);
     hipStream_t rs = (ovl_ && (ovl_n_ & 1)) ? ostream_ : stream;  // this round's stream
+    int64_t tph = steady_ns();
+    auto phase = [&](int i) {
+      const int64_t t = steady_ns();
+      host_ph_ns_[i] += (double)(t - tph);
+      tph = t;
+    };
     LanesArgs a;
     std::memset(&a, 0, sizeof(a));
     a.L = L;
@@ -607,6 +621,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
     for (int l = 0; l < L; ++l) seen_at_solve_[l] = seen[l];
+    phase(0);
     // ---- the round kernel: solves + update + riding evaluation of the last round ----
     if (side_eval_) {
       // this round rewrites the fragments the evaluation of round r - 2 reads
@@ -625,6 +640,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     } else {
       fill_eval(&a.ev, pend_, &slots, &seqs, &kinds);
     }
+    phase(1);
     a.nride = rider_count(a.ev.nmodels, L);
     a.lane_riders = (lane_riders_ && a.ev.nmodels > 0 && !side_eval_ && !lane_eval_) ? 1 : 0;
     a.dsX = cfg_.dsX;
@@ -656,6 +672,8 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       if (ovl_) {
         a.ovl = 1;
         a.round = (unsigned)ovl_n_;
+        if (slab_on_ && a.ev.nmodels > 0 && a.ev.form == 1 && a.ev.nticket <= (unsigned)kSlabRiders)
+          a.ev.slab = slab_;
         a.applied = applied_;
         a.evdone = evdone_;
         // dispatched once every workgroup of the previous round's launch holds its CU
@@ -669,6 +687,10 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       hip_check(hipGetLastError(), "lanes round launch");
       ++launches_;
       if (ovl_) {
+        if (a.ev.slab) {  // the rows of this launch's evaluation, co-running with the next round
+          launch_lanes_publish(a.ev, rs);
+          hip_check(hipGetLastError(), "publish launch");
+        }
         hip_check(hipStreamWriteValue32(rs, evdone_, (uint32_t)(ovl_n_ + 1), 0), "overlap: launch done");
         hip_check(hipEventRecord(ovl_last_, rs), "overlap: last launch");
         ovl_prev_grid_ = lanes_grid(L, a.nride);
@@ -677,6 +699,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
         ++ovl_n_;
       }
     }
+    phase(2);
     if (!slots.empty()) submit_rows(pend_, slots, seqs, kinds);
     if (nlrec) check(api().sink_submit_many(reinterpret_cast<void*>(cfg_.sink), nlrec, lrec), "metrics sink submit");
     nlrec = 0;
@@ -742,6 +765,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     }
     if (cfg_.tracker && is_server) check(api().tracker_bsp_round(reinterpret_cast<void*>(cfg_.tracker), r), "tracker");
     check_errors(r);
+    phase(3);
   }
   ovl_join();
   rounds_run_ += done;

@@ -391,6 +391,7 @@ class LocalEngine:
             if w.ring.XT is not None:
                 w.ring.xt_stale = True  # the round kernel writes the row-major ring only
         self.native_host_us_per_round = float(lp.host_us_per_round)
+        self.native_host_phases_us = [round(float(x), 2) for x in lp.host_phases_us()]
         elapsed = time.time() - t_start
         self.rounds = r
         return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,

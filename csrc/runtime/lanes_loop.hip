@@ -257,14 +257,17 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
   lane_eval_ = cfg_.L > 0 && S_ == 2 && !side_eval_ && le && le[0] == '1';  // (built for S == 2 only)
-  // PSX_LANES_OVERLAP=1: overlapped round launches (LanesArgs::ovl).  One rank (the
-  // multi-rank rounds end in collectives on the caller's stream), rider evaluation in
-  // the tile-resident or pair-major form without the XCD chunk counters (the claim
-  // block is reset while the previous launch runs), the XCD-resident form, and a third
-  // server fragment buffer
+  // PSX_LANES_OVERLAP (default 1; 0: one launch after the other on the caller's
+  // stream): overlapped round launches (LanesArgs::ovl).  One rank (the multi-rank
+  // rounds end in collectives on the caller's stream), rider evaluation in the
+  // tile-resident or pair-major form without the XCD chunk counters (the claim block is
+  // reset while the previous launch runs), the XCD-resident form, and a third server
+  // fragment buffer.  Same box, driver-form A/B: 83.5 / 83.4 / 84.1k against 82.2 /
+  // 82.1 / 83.2k updates/s (profiles/r04/s19, s21, s22); the rocprofv3 trace shows
+  // each launch dispatched ~46 us before the previous one ends (s23)
   const char* ov = std::getenv("PSX_LANES_OVERLAP");
   const bool sfr = !cfg_.shi[0] || (cfg_.shi[2] && cfg_.slo[2] && cfg_.sb[2]);  // (a sink may come later)
-  ovl_ = ov && ov[0] == '1' && !comm_ && cfg_.L > 0 && S_ == 2 && !side_eval_ && !lane_eval_ && !xcd_riders_ && sfr;
+  ovl_ = !(ov && ov[0] == '0') && !comm_ && cfg_.L > 0 && S_ == 2 && !side_eval_ && !lane_eval_ && !xcd_riders_ && sfr;
   // PSX_RIDERS_SLAB (default 1, overlapped launches with tile-resident riders): the
   // riders store their counts (EvalMulti::slab) instead of flushing them with atomics
   // and waiting on a ticket; a publish launch behind each round sums them and fills

@@ -30,7 +30,7 @@ def _loop(spec, ks, N, train, test, w, dev, rows=1024, cap=1024, sink=None, lr=N
     rings = [(torch.zeros(cap, spec.Fp, dtype=torch.bfloat16, device=dev),
               torch.zeros(cap, dtype=torch.int32, device=dev)) for _ in ks]
     wins = [host.SlidingWindow(cap, cap, 0.3, 500, cap) for _ in ks]
-    frags = frags or [Fragments(spec, dev), Fragments(spec, dev)]
+    frags = frags or [Fragments(spec, dev) for _ in range(3)]  # (3: overlapped launches)
     d = dict(scfg=sc, dsX=train.X.data_ptr(), dsy=train.y.data_ptr(), ds_rows=int(train.rows), N=N,
              per_iter_rows=rows, k=list(ks), X=[r[0].data_ptr() for r in rings], y=[r[1].data_ptr() for r in rings],
              window=[wn.handle for wn in wins], w=w.data_ptr(), lr=float(lr if lr is not None else 1.0 / N),

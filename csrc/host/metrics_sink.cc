@@ -1,5 +1,7 @@
 #include "metrics_sink.h"
 
+#include <sys/prctl.h>
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -122,6 +124,9 @@ void MetricsSink::submit_many(int n, const SinkRecord* recs) {
 }
 
 void MetricsSink::run() {
+  // the waits below are 5 us sleeps: with the default 50 us timer slack a row that
+  // lands while this thread sleeps was seen ~60 us late (every run's last rows)
+  (void)prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0);
   for (;;) {
     Pending p;
     {

@@ -1151,7 +1151,7 @@ void LanesLoop::stop_all(hipStream_t stream) {
       for (int j = 0; j < 9; ++j) m += " " + std::to_string(c[j]);
       throw std::runtime_error(m);
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
   hip_check(hipEventRecord(aev_out_, astream_), "async order out");  // the caller's later work after it
   hip_check(hipStreamWaitEvent(stream, aev_out_, 0), "async order out");

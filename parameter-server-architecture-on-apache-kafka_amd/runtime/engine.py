@@ -165,6 +165,7 @@ class LocalEngine:
         False: the log sink stays open for a later run (its rows are flushed).
         summary False: no headline numbers from the log book (a scan of every row
         logged so far: bench.py computes them outside its timed region)."""
+        t_entry = time.time()
         if getattr(self, "train_start_ms", None) is None:  # epoch ms when training first began
             self.train_start_ms = time.time() * 1000.0
         live = [w for w in self.workers if w.k not in self.failed]
@@ -191,7 +192,11 @@ class LocalEngine:
         if summary and self.log.book is not None:
             out.update(summarize(self.log.book))
         if "phases_ms" in out:
-            out["phases_ms"]["summary"] = round((time.time() - t_sum) * 1e3, 3)
+            ph = out["phases_ms"]
+            ph["summary"] = round((time.time() - t_sum) * 1e3, 3)
+            # the whole call less its loop phases: the Python around the native loop
+            ph["python"] = round((time.time() - t_entry) * 1e3 - ph.get("rounds", 0.0) - ph.get("tail", 0.0)
+                                 - ph.get("sync", 0.0) - ph["summary"], 3)
         out["max_vc_gap"] = int(self.server.tracker.max_gap)
         out["failed_workers"] = sorted(self.failed)
         return out

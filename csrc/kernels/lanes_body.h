@@ -365,14 +365,9 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
   };
   // items = (tile, group of ev.ppi model pairs; 0: every pair), tile-major
   const int ppi = ev.ppi > 0 && ev.ppi < npairs ? ev.ppi : npairs, ngr = (npairs + ppi - 1) / ppi;
-  for (int item = pop(rid); item < nT * ngr; item = pop(item + nride)) {
-    const int tile = item / ngr, gr = item - tile * ngr;
-    const int p0 = gr * ppi, p1 = p0 + ppi < npairs ? p0 + ppi : npairs;
-    const int m0 = 2 * p0, m1 = 2 * p1 < M ? 2 * p1 : M;  // the item's models
-    const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+  u16x8 a0[KS], a1[KS];  // the tile's A operands: rows r and 16 + r, wave w's k-steps (forward_tile_pre's)
+  auto load_tile = [&](int tile, int nrows) {
     const int64_t row0 = (int64_t)tile * 32;
-    // the tile's A operands: rows r and 16 + r, wave w's k-steps (forward_tile_pre's)
-    u16x8 a0[KS], a1[KS];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       const int cg = (w * KS + kk) * 4 + kq;
@@ -381,21 +376,19 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
                               : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
     if (tid < 32) ylab[tid] = tid < nrows ? ev.yt[row0 + tid] : 0;
-    WFrag<FP> wc, wn;
-    load_pair(wc, p0);
-    for (int p = p0; p < p1; ++p) {  // (uniform)
-      if (p + 1 < p1) load_pair(wn, p + 1);
-      f32x4 acc0 = f32x4{0, 0, 0, 0}, acc1 = f32x4{0, 0, 0, 0};
+  };
+  auto mfma_pair = [&](const WFrag<FP>& wf, int p) {
+    f32x4 acc0 = f32x4{0, 0, 0, 0}, acc1 = f32x4{0, 0, 0, 0};
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wc.h[kk]), acc0);
-        acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wc.l[kk]), acc0);
-        acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wc.h[kk]), acc1);
-        acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wc.l[kk]), acc1);
-      }
-      store_partial_logits(red + (size_t)p * 8192, acc0, acc1);
-      if (p + 1 < p1) wc = wn;
+    for (int kk = 0; kk < KS; ++kk) {
+      acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wf.h[kk]), acc0);
+      acc0 = mfma16x16x32(as_bf16x8(a0[kk]), as_bf16x8(wf.l[kk]), acc0);
+      acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wf.h[kk]), acc1);
+      acc1 = mfma16x16x32(as_bf16x8(a1[kk]), as_bf16x8(wf.l[kk]), acc1);
     }
+    store_partial_logits(red + (size_t)p * 8192, acc0, acc1);
+  };
+  auto count_tile = [&](int m0, int m1, int nrows) {
     __syncthreads();
     if (first && rid == 0) rstamp(1);
     for (int it = tid; it < 32 * (m1 - m0); it += 256) {  // thread (row, model)
@@ -418,6 +411,51 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
     }
     __syncthreads();  // (red / ylab are rewritten by the next tile)
     first = false;
+  };
+  if (ev.gq && ev.xq && ppi <= 2 && ngr <= kEvalGroups) {
+    // Group queues (EvalMulti::gq): rider rid starts on group rid % ngr and pops that
+    // group's tiles from ev.xq[group]; the group's (<= 2) model pairs stay in registers
+    // across its tiles, so a tile costs its own 64 KB and no fragment reloads.  An
+    // exhausted group sends the rider to the next one.
+    WFrag<FP> h0, h1;
+    int g = rid % ngr, cur = -1;
+    for (int left = ngr; left > 0;) {
+      if (tid == 0) *tq = (int)__hip_atomic_fetch_add(ev.xq + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const int tile = __builtin_amdgcn_readfirstlane(*tq);
+      __syncthreads();
+      if (tile >= nT) {
+        g = g + 1 == ngr ? 0 : g + 1;
+        --left;
+        continue;
+      }
+      const int p0 = g * ppi, p1 = p0 + ppi < npairs ? p0 + ppi : npairs;
+      const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+      load_tile(tile, nrows);
+      if (g != cur) {  // (uniform)
+        load_pair(h0, p0);
+        if (p0 + 1 < p1) load_pair(h1, p0 + 1);
+        cur = g;
+      }
+      mfma_pair(h0, p0);
+      if (p0 + 1 < p1) mfma_pair(h1, p0 + 1);
+      count_tile(2 * p0, 2 * p1 < M ? 2 * p1 : M, nrows);
+    }
+  } else {
+    for (int item = pop(rid); item < nT * ngr; item = pop(item + nride)) {
+      const int tile = item / ngr, gr = item - tile * ngr;
+      const int p0 = gr * ppi, p1 = p0 + ppi < npairs ? p0 + ppi : npairs;
+      const int nrows = T - tile * 32 < 32 ? T - tile * 32 : 32;
+      load_tile(tile, nrows);
+      WFrag<FP> wc, wn;
+      load_pair(wc, p0);
+      for (int p = p0; p < p1; ++p) {  // (uniform)
+        if (p + 1 < p1) load_pair(wn, p + 1);
+        mfma_pair(wc, p);
+        if (p + 1 < p1) wc = wn;
+      }
+      count_tile(2 * p0, 2 * p1 < M ? 2 * p1 : M, nrows);
+    }
   }
   if constexpr (kStop == 1) return;
   if (ev.slab) {  // slab form: this rider's counts, every cell (zeros included); no ticket
@@ -448,7 +486,7 @@ __device__ __forceinline__ void eval_tile_body(char* lds, const EvalMulti& ev, i
   if (!*lastp) return;
   rstamp(10);
   // (every rider has popped its last item: the queue is free for the next pass)
-  if (ev.xq && tid == 0) __hip_atomic_store(ev.xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ev.xq && tid < (ev.gq ? kEvalGroups : 1)) __hip_atomic_store(ev.xq + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   publish_counts(ev, M, tid, cl);
   rstamp(11);
 }

@@ -105,6 +105,9 @@ struct EvalMulti {
   // tiles popped from xq[0], zero at launch)
   int form;
   int ppi;  // tile-resident form: model pairs per work item (0: all; items = (tile, pair group))
+  // tile-resident form, gq = 1: one tile queue per pair group (xq[0 .. kEvalGroups)), a
+  // rider keeps its group's fragments in registers across the group's tiles
+  int gq;
   // != nullptr (tile-resident form, overlapped launches): no ticket -- every rider
   // stores its counts, [rider][kMaxEvalModels][64] ints (cell = label * 8 + predicted),
   // and a publish launch behind the round (launch_lanes_publish, co-running with the
@@ -185,6 +188,7 @@ void launch_lanes_round(const SolverCfg& cfg, const LaneDev* lanes_dev, const La
 // ev.nticket riders' counts and writes the model's slot; it also clears the tile queue
 // ev.xq.  Sized to co-run with a round kernel (a few KB of LDS, <= 64 VGPRs).
 constexpr int kSlabCells = 64;
+constexpr int kEvalGroups = 8;  // EvalMulti::gq: tile queues (pair groups) at most
 constexpr int kSlabRiders = 1024;  // slab rows allocated (riders of one launch at most)
 void launch_lanes_publish(const EvalMulti& ev, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).

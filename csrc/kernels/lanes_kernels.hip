@@ -355,7 +355,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void l
     const int yl = tid / K, p = tid - yl * K, cc = yl * 8 + p;
     cells[tid] = part[0][cc] + part[1][cc] + part[2][cc] + part[3][cc];
   }
-  if (m == 0 && tid == 0 && ev.xq) __hip_atomic_store(ev.xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (m == 0 && ev.xq && tid < (ev.gq ? kEvalGroups : 1))
+    __hip_atomic_store(ev.xq + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (tid < 64) {
     const EvalModel E = pick(ev.m, m);

@@ -250,6 +250,7 @@ class LanesLoop {
   bool tile_riders_ = false;
   bool lane_riders_ = false;
   int riders_ppi_ = 0;
+  bool riders_gq_ = false;
   int* lacc_ = nullptr;
   unsigned* lticket_ = nullptr;
   hipStream_t side_ = nullptr;

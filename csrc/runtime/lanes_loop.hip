@@ -253,6 +253,13 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   lane_riders_ = tf == '2';
   const char* rp = std::getenv("PSX_RIDERS_PPI");
   riders_ppi_ = rp ? std::atoi(rp) : 2;
+  // PSX_RIDERS_GQ=1: tile queues per pair group, the group's fragments held in
+  // registers across its tiles (EvalMulti::gq).  Off by default: 80.6-80.9k against
+  // 83.3-83.5k updates/s (profiles/r04/s27) -- the tile-major queue has a tile's groups
+  // popped back to back, so the 64 KB tile comes from L2 after the first; fragment
+  // reloads cost less than the lost tile locality
+  const char* rg = std::getenv("PSX_RIDERS_GQ");
+  riders_gq_ = rg && rg[0] == '1';
   const char* rx = std::getenv("PSX_RIDERS_XCD");
   xcd_riders_ = rx && rx[0] == '1';
   const char* le = std::getenv("PSX_LANES_LANE_EVAL");
@@ -466,6 +473,7 @@ void LanesLoop::fill_eval(EvalMulti* ev, const Pending& p, std::vector<int>* slo
   if (cfg_.log_server) add(nw, cfg_.shi[p.par], cfg_.slo[p.par], cfg_.sb[p.par], cfg_.scoff, nullptr, 1);
   ev->form = tile_riders_ ? 1 : 0;
   ev->ppi = riders_ppi_;
+  ev->gq = riders_gq_ ? 1 : 0;
   // every rider of the launch arrives; lane riders: every lane workgroup as well
   ev->nticket = (unsigned)(rider_count(ev->nmodels, cfg_.L) + (lane_riders_ ? cfg_.L * kLaneWg : 0));
   ev->dbg = rider_dbg_;

@@ -341,16 +341,19 @@ def test_xcd_local_riders_rows_equal_riders(cuda, monkeypatch, L):
     assert [r[1:] for r in a.worker] == [r[1:] for r in b.worker] and len(a.worker) == 4 * L
 
 
-@pytest.mark.parametrize("L,tile,ppi", [(3, "1", "0"), (8, "1", "0"), (3, "2", "0"), (8, "2", "0"), (8, "2", "1"),
-                                        (3, "2", "2")])
-def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile, ppi):
+@pytest.mark.parametrize("L,tile,ppi,gq", [(3, "1", "0", "0"), (8, "1", "0", "0"), (3, "2", "0", "0"),
+                                           (8, "2", "0", "0"), (8, "2", "1", "0"), (3, "2", "2", "0"),
+                                           (8, "2", "2", "1"), (3, "2", "1", "1"), (8, "1", "2", "1")])
+def test_tile_resident_riders_rows_equal_pair_major(cuda, monkeypatch, L, tile, ppi, gq):
     """Riders holding their test tile in registers and running every model pair past
     it (PSX_RIDERS_TILE=1, eval_tile_body: the test set read once per round; =2: the
     lanes' own workgroups join them once their part of the round is done) log the
-    same rows, bit for bit, as the pair-major riders (eval_multi_body)."""
+    same rows, bit for bit, as the pair-major riders (eval_multi_body); gq = 1: one tile
+    queue per pair group, the group's fragments held across its tiles (PSX_RIDERS_GQ)."""
     spec, train, ev = _data(cuda)
     books = []
     monkeypatch.setenv("PSX_RIDERS_PPI", ppi)  # (work items of ppi model pairs; 0: all)
+    monkeypatch.setenv("PSX_RIDERS_GQ", gq)
     for form in ("0", tile):
         monkeypatch.setenv("PSX_RIDERS_TILE", form)
         w = spec.init("random", seed=6, device=cuda)

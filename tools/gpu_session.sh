@@ -1,6 +1,6 @@
 #!/bin/bash
 # One parameterised gpurun session (replaces the per-session one-off scripts).
-#   OUT=gpurun_out/<name>  STEPS="async bench ssp asp tests smoke prof" bash tools/gpu_session.sh
+#   OUT=gpurun_out/<name>  STEPS="tests smoke bench ssp asp lanes async ipc ab prof timeline probe fault" bash tools/gpu_session.sh
 # Every GPU step has its own time limit; a crash / timeout / fault ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -41,6 +41,23 @@ for s in $STEPS; do
         rc=$?; [ $rc -eq 0 ] || { echo "ab [$v] rc=$rc"; exit $rc; }
         echo "[$v] $(python -c "import json;d=json.load(open('$OUT/ab.tmp'));print(d['value'],d['ms_per_step'])")" | tee -a $OUT/ab.txt
       done ;;
+    probe)   # the standalone evaluation probe (tools/eval_probe.hip, built beforehand)
+      timeout -k 10 60 ./tools/eval_probe 200 > $OUT/eval_probe.json 2> $OUT/eval_probe.err; rc=$?
+      echo "probe rc=$rc"; cat $OUT/eval_probe.json
+      [ $rc -eq 0 ] || [ $rc -eq 3 ] || exit $rc ;;
+    ipc)     # the multi-process ranks sharing the GPU (IPC transport)
+      timeout -k 10 300 $PYT tests/test_gpu_ipc_lanes.py > $OUT/pytest_ipc.log 2>&1; rc=$?
+      echo "ipc rc=$rc"; grep -E "PASS|FAIL|ERROR|passed|failed" $OUT/pytest_ipc.log | tail -8
+      ok_rc $rc || exit $rc ;;
+    timeline)  # the lanes kernel's phase stamps (tools/lanes_profile.py)
+      PSX_LANES_STAMPS=1 timeout -k 10 120 python tools/lanes_profile.py --lanes 8 --rounds 400 >> $OUT/lanes_profile.jsonl 2>> $OUT/lanes_profile.err || exit 1 ;;
+    fault)   # the round-3 matrix fault's configuration on the Python concurrent-stream path
+      # (4 workers, producer clock -p 500, BSP, PSX_NATIVE_LANES=0 keeps it off the lanes
+      # loop); FAULT_ENV adds e.g. AMD_SERIALIZE_KERNEL=3.  Runs LAST: nothing follows it.
+      python -c "import sys; sys.path[:0] = ['tools', '.']; import experiment_matrix as m; m.ensure_data('data')" > $OUT/fault_data.log 2>&1 || exit 1
+      timeout -k 10 ${FAULT_TIMEOUT:-90} env PSX_NATIVE_LANES=0 ${FAULT_ENV:-} python -X faulthandler -m psx.apps.server_app_runner --inprocess --device cuda -training data/train.bin -test data/test.bin -p ${FAULT_P:-500} -c 0 --num_workers 4 -l --log_dir $OUT/fault_run --max_wallclock_s ${FAULT_S:-45} --async_scheduler threads > $OUT/fault_run.out 2>&1
+      rc=$?; echo "fault run rc=$rc"; tail -5 $OUT/fault_run.out
+      exit $rc ;;
     ssp|asp)
       c=10; [ $s = asp ] && c=-1
       timeout -k 10 300 python bench.py --consistency $c --steps ${ASYNC_STEPS:-300} --warmup 30 ${BENCH_ARGS:-} > $OUT/bench_$s.json 2> $OUT/bench_$s.err

@@ -861,12 +861,12 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   const bool xs2 = kXs == 2 && (kP == 2 || cfg.xcd >= 0);
   // only the m stored pairs' dots travel (ring slots (head - m + 1 + j) mod H)
   const int nv = 4 + 2 * m;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (m), Y_i.gt (m)
-  const int hbase = ((head - m + 1) % H + H) % H;
+  const int hbase = head - m + 1 < 0 ? head - m + 1 + H : head - m + 1;  // (head - m + 1) mod H: > -H
   const unsigned tag = run_tag + (unsigned)slot + 1u;
   unsigned* gat32 = (unsigned*)gat;  // [ns][2*nv]
   if (tid < 2 * nv) {
     const int k = tid >> 1;
-    const int ring = k < 4 ? 0 : (hbase + (k < 4 + m ? k - 4 : k - 4 - m)) % H;
+    const int rr = hbase + (k < 4 + m ? k - 4 : k - 4 - m), ring = k < 4 ? 0 : (rr >= H ? rr - H : rr);
     const int si = k < 3 ? k : (k == 3 ? kND : (k < 4 + m ? 3 + ring : 3 + kMaxHist + ring));
     const double v = sdot[si] + sdot[kNDX + si] + sdot[2 * kNDX + si] + sdot[3 * kNDX + si];
     const unsigned long long u = d2u(v);
@@ -929,7 +929,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       v += u2d(u);
     }
     // order expected by ctrl_step: 3 scalars, S_i.g (H ring slots), Y_i.g (H); loss in dots[kND]
-    const int ring = tid < 4 ? 0 : (hbase + (tid < 4 + m ? tid - 4 : tid - 4 - m)) % H;
+    const int rr = hbase + (tid < 4 + m ? tid - 4 : tid - 4 - m), ring = tid < 4 ? 0 : (rr >= H ? rr - H : rr);
     const int pos = tid < 3 ? tid : (tid == 3 ? kND : (tid < 4 + m ? 3 + ring : 3 + H + ring));
     dots[pos] = v;
   }

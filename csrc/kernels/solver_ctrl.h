@@ -191,7 +191,10 @@ PSX_HD inline double ctrl_direction(Ctrl& __restrict__ c, int H, CtrlScratch& __
     return -c.gg_c;
   }
   int* idx = ws.idx;  // logical (oldest..newest) -> physical
-  for (int i = 0; i < m; ++i) idx[i] = ((c.head - (m - 1 - i)) % H + H) % H;
+  for (int i = 0; i < m; ++i) {  // (head - (m - 1 - i)) mod H; the operand is > -H (no integer division)
+    const int x = c.head - (m - 1 - i);
+    idx[i] = x < 0 ? x + H : x;
+  }
   const double gamma = c.gamma;
   double *u = ws.u, *v = ws.v, *a = ws.a, *rhs = ws.rhs, *p = ws.p;
   for (int i = 0; i < m; ++i) {
@@ -268,7 +271,10 @@ PSX_HD inline void ctrl_accept(Ctrl& __restrict__ c, const SolverCfg& cfg, doubl
   // --- new curvature pair s = t d, y = g_t - g_c ---
   const int m = c.m;
   int* idx = ws.idx;
-  for (int i = 0; i < m; ++i) idx[i] = ((c.head - (m - 1 - i)) % H + H) % H;
+  for (int i = 0; i < m; ++i) {  // (head - (m - 1 - i)) mod H; the operand is > -H (no integer division)
+    const int x = c.head - (m - 1 - i);
+    idx[i] = x < 0 ? x + H : x;
+  }
   // d . y_j for the stored pairs (d is known through its coefficients)
   double* dy = ws.dy;
   for (int jj = 0; jj < m; ++jj) {
@@ -284,7 +290,7 @@ PSX_HD inline void ctrl_accept(Ctrl& __restrict__ c, const SolverCfg& cfg, doubl
   const double yy_new = tt - 2.0 * tc + c.gg_c;
   const bool keep = sy_new > 1e-10 * (yy_new > 0 ? yy_new : 1.0) && yy_new > 0.0;
   if (keep) {
-    int slotp = (c.head + 1) % H;
+    int slotp = c.head + 1 == H ? 0 : c.head + 1;  // (head + 1) mod H, head in [-1, H)
     // if the ring is full the oldest pair (physical slotp) is evicted
     int mm = m < H ? m : m - 1;  // surviving old pairs
     int first = m - mm;          // logical index of the first survivor

@@ -335,9 +335,14 @@ class LocalEngine:
         if srv.pair is not None:
             srv.pair.flush(self.log)  # nothing may be pending from an earlier run
         lp = self._lanes_loop(W)
-        for i, w in enumerate(W):
-            lp.set_next_local(i, int(w.source.next_local))
-            lp.set_seen_at_solve(i, int(w._seen_at_solve))
+        # (the loop's own counters are current unless something moved the roles' since
+        # its last run -- a resume or a test: a pybind call per worker saved per run)
+        synced = getattr(self, "_lanes_synced", None)
+        now = [(int(w.source.next_local), int(w._seen_at_solve)) for w in W]
+        if synced is None or synced[0] is not lp or synced[1] != now:
+            for i, (nl, ss) in enumerate(now):
+                lp.set_next_local(i, nl)
+                lp.set_seen_at_solve(i, ss)
         stream = stream_handle(self.device)
         t_start = time.time()
         deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
@@ -380,7 +385,11 @@ class LocalEngine:
             # stream-ordered behind the rounds: the last local solve's loss / delta for code
             # that reads the roles, and the Python-side evaluation fragments of the global
             # model (the native update rewrote w); ONE synchronisation covers them all
-            lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
+            ca = getattr(self, "_lanes_copy_args", None)  # (the roles' tensors outlive the loop)
+            if ca is None or ca[0] is not lp:
+                ca = (lp, [w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W])
+                self._lanes_copy_args = ca
+            lp.copy_out_all(ca[1], ca[2], stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
             t_enq = time.time()
@@ -395,6 +404,7 @@ class LocalEngine:
             w._seen_at_solve = int(lp.seen_at_solve(i))
             if w.ring.XT is not None:
                 w.ring.xt_stale = True  # the round kernel writes the row-major ring only
+        self._lanes_synced = (lp, [(int(w.source.next_local), int(w._seen_at_solve)) for w in W])
         self.native_host_us_per_round = float(lp.host_us_per_round)
         self.native_host_phases_us = [round(float(x), 2) for x in lp.host_phases_us()]
         elapsed = time.time() - t_start
@@ -422,9 +432,14 @@ class LocalEngine:
         if srv.pair is not None:
             srv.pair.flush(self.log)
         lp = self._lanes_loop(W)
-        for i, w in enumerate(W):
-            lp.set_next_local(i, int(w.source.next_local))
-            lp.set_seen_at_solve(i, int(w._seen_at_solve))
+        # (the loop's own counters are current unless something moved the roles' since
+        # its last run -- a resume or a test: a pybind call per worker saved per run)
+        synced = getattr(self, "_lanes_synced", None)
+        now = [(int(w.source.next_local), int(w._seen_at_solve)) for w in W]
+        if synced is None or synced[0] is not lp or synced[1] != now:
+            for i, (nl, ss) in enumerate(now):
+                lp.set_next_local(i, nl)
+                lp.set_seen_at_solve(i, ss)
         stream = stream_handle(self.device)
         t_start = time.time()
         deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
@@ -462,7 +477,11 @@ class LocalEngine:
                     maybe_checkpoint(cfg, srv, srv.updates, W)
                 if n < todo:  # the streams ended, the deadline passed
                     break
-            lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
+            ca = getattr(self, "_lanes_copy_args", None)  # (the roles' tensors outlive the loop)
+            if ca is None or ca[0] is not lp:
+                ca = (lp, [w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W])
+                self._lanes_copy_args = ca
+            lp.copy_out_all(ca[1], ca[2], stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
             torch.cuda.synchronize(self.device)

@@ -119,15 +119,18 @@ def test_zero_mean_interarrival_policy():
     assert java_int_cast == -1 and max(128, min(1024, java_int_cast)) == 128
 
 
-def test_bulk_insert_equals_row_by_row():
-    """The round loops' bulk insert (equal-stamp runs at the max target in one step)
-    leaves the window and the rate estimator exactly as row-by-row inserts do."""
+@pytest.mark.parametrize("rate_window", [500, 1, 3, 64, 2000])
+def test_bulk_insert_equals_row_by_row(rate_window):
+    """The round loops' bulk insert (equal-stamp runs at the max target in one step;
+    the estimator's zero deltas in closed form) leaves the window and the rate
+    estimator exactly as row-by-row inserts do -- also for estimator windows shorter
+    and longer than a delivery."""
     import numpy as np
 
     rng = np.random.default_rng(7)
     for trial in range(20):
-        a = host.SlidingWindow(128, 1024, 0.3, 500, 1024)
-        b = host.SlidingWindow(128, 1024, 0.3, 500, 1024)
+        a = host.SlidingWindow(128, 1024, 0.3, rate_window, 1024)
+        b = host.SlidingWindow(128, 1024, 0.3, rate_window, 1024)
         now = 0.0
         for _ in range(60):
             k = int(rng.integers(1, 1500))

@@ -246,13 +246,15 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // done (LanesArgs::lane_riders); 1 = the tile-resident riders alone; 0 = the pair-major
   // riders (eval_multi_body).  Same box, driver-form bench, 8 lanes (profiles/r04/s10,
   // s11): 84.0 / 80.5k updates/s for 2 / 0, 85.3k with 2 model pairs per item
-  // (PSX_RIDERS_PPI, default 2; 1: 82.3k; 0 = all 5 pairs: 85.0k)
+  // (PSX_RIDERS_PPI; 1: 82.3k; 0 = all 5 pairs: 85.0k).  With overlapped launches and
+  // the slab form every pair per item (0, the default) is best: 86.7 / 86.4k against
+  // 84.3 / 84.5k for 2 pairs, 86.3 / 86.0k for 3, 80.0 / 80.1k for 1 (profiles/r04/s35)
   const char* rt = std::getenv("PSX_RIDERS_TILE");
   const char tf = rt && rt[0] ? rt[0] : '2';
   tile_riders_ = tf == '1' || tf == '2';
   lane_riders_ = tf == '2';
   const char* rp = std::getenv("PSX_RIDERS_PPI");
-  riders_ppi_ = rp ? std::atoi(rp) : 2;
+  riders_ppi_ = rp ? std::atoi(rp) : 0;
   // PSX_RIDERS_GQ=1: tile queues per pair group, the group's fragments held in
   // registers across its tiles (EvalMulti::gq).  Off by default: 80.6-80.9k against
   // 83.3-83.5k updates/s (profiles/r04/s27) -- the tile-major queue has a tile's groups

@@ -578,11 +578,22 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     hip_check(hipEventRecord(ovl_in_, stream), "overlap order in");
     hip_check(hipStreamWaitEvent(ostream_, ovl_in_, 0), "overlap order in");
   }
+  bool joined = false;
   auto ovl_join = [&]() {  // the caller's later work after every round of this call
-    if (!ovl_) return;
+    if (!ovl_ || joined) return;
+    joined = true;
     hip_check(hipEventRecord(ovl_out_, ostream_), "overlap order out");
     hip_check(hipStreamWaitEvent(stream, ovl_out_, 0), "overlap order out");
   };
+  struct JoinOnThrow {  // an exception out of a round still orders the caller's stream
+    bool* joined;
+    bool ovl;
+    hipEvent_t ev;
+    hipStream_t from, to;
+    ~JoinOnThrow() {
+      if (ovl && !*joined && hipEventRecord(ev, from) == hipSuccess) (void)hipStreamWaitEvent(to, ev, 0);
+    }
+  } join_guard{&joined, ovl_, ovl_out_, ostream_, stream};
   int64_t done = 0;
   for (; done < rounds; ++done) {
     const int64_t r = r0 + done;

@@ -598,7 +598,11 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
   for (; done < rounds; ++done) {
     const int64_t r = r0 + done;
     const int par = ovl_ ? (int)(((r % 3) + 3) % 3) : (int)(r & 1);
-    hipStream_t rs = (ovl_ && (ovl_n_ & 1)) ? ostream_ : stream;  // this round's stream
+    // this round's stream: the two alternate, the call's last round on the caller's --
+    // what follows the call there (the last round's evaluation launch, the copies) then
+    // needs no wait on the other queue (profiles/r04/s46: 31 us from the last round to
+    // that launch when the last round ran on the other stream)
+    hipStream_t rs = (ovl_ && ((rounds - 1 - done) & 1)) ? ostream_ : stream;
     int64_t tph = steady_ns();
     auto phase = [&](int i) {
       const int64_t t = steady_ns();
@@ -696,7 +700,10 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       if (ovl_) {
         a.ovl = 1;
         a.round = (unsigned)ovl_n_;
-        if (slab_on_ && a.ev.nmodels > 0 && a.ev.form == 1 && a.ev.nticket <= (unsigned)kSlabRiders)
+        // (the call's last round publishes in its own launch: nothing follows it to co-run
+        // with a publish launch, which would only lengthen the call's tail)
+        if (slab_on_ && done + 1 < rounds && a.ev.nmodels > 0 && a.ev.form == 1 &&
+            a.ev.nticket <= (unsigned)kSlabRiders)
           a.ev.slab = slab_;
         a.applied = applied_;
         a.evdone = evdone_;

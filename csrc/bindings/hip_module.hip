@@ -11,10 +11,12 @@
 #include <stdexcept>
 
 #include "../comm/ipc_comm.h"
+#include "../comm/peer_bus.h"
 #include "../comm/rccl_comm.h"
 #include "../runtime/async_server.h"
 #include "../runtime/bsp_loop.h"
 #include "../runtime/lanes_loop.h"
+#include "../runtime/peer_server.h"
 #include "../runtime/keyrange_loop.h"
 #include "../kernels/lr_kernels.h"
 #include "../solver/solver.h"
@@ -578,6 +580,94 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("sparse_pulls", &LocalFeeder::sparse_pulls)
       .def("start", &LocalFeeder::start)
       .def("join", &LocalFeeder::join, py::call_guard<py::gil_scoped_release>());
+  // Peer data plane (csrc/comm/peer_bus.h): IPC-exported fine-grained regions
+  py::class_<PeerRegion>(m, "PeerRegion")
+      .def(py::init([](int64_t P, int NS, int slots, int device) {
+             PeerLayout lay;
+             lay.P = P;
+             lay.NS = NS;
+             lay.slots = slots;
+             return std::make_unique<PeerRegion>(lay, device);
+           }),
+           py::arg("P"), py::arg("NS"), py::arg("slots"), py::arg("device") = 0)
+      .def("handle", [](const PeerRegion& r) { return py::bytes(r.handle()); })
+      .def_property_readonly("base", &PeerRegion::base)
+      .def_property_readonly("stride", [](const PeerRegion& r) { return r.layout().stride(); })
+      .def_property_readonly("nbytes", [](const PeerRegion& r) { return r.layout().bytes(); })
+      .def("data", [](const PeerRegion& r, int slot) { return reinterpret_cast<uintptr_t>(r.data(slot)); })
+      .def("tags", [](const PeerRegion& r, int slot) { return reinterpret_cast<uintptr_t>(r.tags(slot)); });
+  py::class_<PeerMapping>(m, "PeerMapping")
+      .def(py::init([](py::bytes h, int64_t P, int NS, int slots) {
+             PeerLayout lay;
+             lay.P = P;
+             lay.NS = NS;
+             lay.slots = slots;
+             return std::make_unique<PeerMapping>(std::string(h), lay);
+           }),
+           py::arg("handle"), py::arg("P"), py::arg("NS"), py::arg("slots"))
+      .def_property_readonly("base", &PeerMapping::base)
+      .def("data", [](const PeerMapping& r, int slot) { return reinterpret_cast<uintptr_t>(r.data(slot)); })
+      .def("tags", [](const PeerMapping& r, int slot) { return reinterpret_cast<uintptr_t>(r.tags(slot)); })
+      .def("close", &PeerMapping::close);
+  py::class_<PeerServer>(m, "PeerServer")
+      .def(py::init([](py::dict d) {
+             auto I = [&](const char* k, int64_t def) { return d.contains(k) ? d[k].cast<int64_t>() : def; };
+             auto U = [&](const char* k) { return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0; };
+             auto V = [&](const char* k) {
+               return d.contains(k) ? d[k].cast<std::vector<uintptr_t>>() : std::vector<uintptr_t>{};
+             };
+             PeerServerCfg c;
+             c.nworkers = (int)I("nworkers", 0);
+             c.lr = d.contains("lr") ? d["lr"].cast<float>() : 1.f;
+             c.K = (int)I("K", 0);
+             c.F = (int)I("F", 0);
+             c.FP = (int)I("FP", 0);
+             c.P = I("P", 0);
+             c.w = P<float>(U("w"));
+             c.Xt = P<const uint16_t>(U("Xt"));
+             c.yt = P<const int32_t>(U("yt"));
+             c.T = (int)I("T", 0);
+             c.inbox = U("inbox");
+             c.lay.P = c.P;
+             c.lay.NS = c.FP / 32;
+             c.lay.slots = (int)I("inbox_slots", c.nworkers);
+             c.rx = V("rx");
+             c.rx_tag = V("rx_tag");
+             c.api = U("api");
+             c.tracker = U("tracker");
+             c.ctrl = U("ctrl");
+             c.sink = U("sink");
+             c.replies = V("replies");
+             c.worker_timeout_s = d.contains("worker_timeout_s") ? d["worker_timeout_s"].cast<double>() : 600.0;
+             c.sxcd = (int)I("sxcd", 0);
+             prepare_kernels();
+             return std::make_unique<PeerServer>(c, nullptr);
+           }),
+           py::arg("cfg"))
+      .def("begin", &PeerServer::begin, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "run",
+          [](PeerServer& s, int64_t checkpoint_every) {
+            AsyncStatus st;
+            {
+              py::gil_scoped_release nogil;
+              st = s.run(checkpoint_every);
+            }
+            return py::make_tuple(st.code, st.worker, st.updates);
+          },
+          py::arg("checkpoint_every") = 0)
+      .def("fail", &PeerServer::fail, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &PeerServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("set_stream", [](PeerServer&, uintptr_t) {})  // (own stream; AsyncServer's interface)
+      .def_property("updates", &PeerServer::updates, &PeerServer::set_updates)
+      .def_property_readonly("tokens", &PeerServer::tokens)
+      .def_property_readonly("commands", &PeerServer::commands)
+      .def_property_readonly("running", &PeerServer::running)
+      .def_property_readonly("arrivals", &PeerServer::arrivals)
+      .def_property_readonly("host_us_per_update", &PeerServer::host_us_per_update)
+      .def_property_readonly("failed", &PeerServer::failed)
+      .def_property_readonly("sparse_pulls", [](const PeerServer&) { return (int64_t)0; })
+      .def_property_readonly("dense_pulls", &PeerServer::tokens);
   py::class_<AsyncServer>(m, "AsyncServer")
       .def(py::init([](P2P& comm, py::dict d, uintptr_t stream) {
              auto I = [&](const char* k, int64_t def) {
@@ -772,13 +862,25 @@ PYBIND11_MODULE(_psx_hip, m) {
           py::arg("deadline_ms") = 0.0)
       .def(
           "run_async",
+          // per_lane: an int (the same bound for every lane, 0 = none) or one bound per lane
           [](LanesLoop& l, int64_t updates, uintptr_t stream, double max_wait_s, double deadline_ms,
-             int64_t per_lane) {
+             py::object per_lane) {
+            std::vector<int64_t> b;
+            if (py::isinstance<py::int_>(per_lane)) {
+              const int64_t v = per_lane.cast<int64_t>();
+              if (v > 0) b.assign((size_t)l.lanes(), v);
+            } else if (!per_lane.is_none()) {
+              b = per_lane.cast<std::vector<int64_t>>();
+            }
             py::gil_scoped_release nogil;
-            return l.run_async(updates, S(stream), max_wait_s, deadline_ms, per_lane);
+            return l.run_async(updates, S(stream), max_wait_s, deadline_ms, b);
           },
           py::arg("updates"), py::arg("stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0,
           py::arg("per_lane") = 0)
+      .def("set_peer", &LanesLoop::set_peer, py::arg("rx_data"), py::arg("rx_tags"), py::arg("rx_stride"),
+           py::arg("inbox"), py::arg("inbox_tag"))
+      .def("prepare_async", &LanesLoop::prepare_async)
+      .def_property_readonly("peer", &LanesLoop::peer)
       .def(
           "run_async_remote",
           [](LanesLoop& l, P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, uintptr_t stream,

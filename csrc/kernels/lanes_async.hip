@@ -56,6 +56,39 @@ __device__ __forceinline__ void leader_wait_release(const AsyncLaneDev& A, unsig
   if (tid < kRelChunks) ((TagChunk*)A.rec)[tid] = c;
 }
 
+// The lane's sticky error word -> its pinned host word ((solves + 1) << 8 | code,
+// the format of FinScal::store), then cleared.  One thread.
+__device__ __forceinline__ void report_and_clear(const SolveDev& dv, unsigned long long* err, unsigned run) {
+  const unsigned long long e = xload(err);
+  if (e) {
+    if (dv.err_host)
+      __hip_atomic_store(dv.err_host, (unsigned long long)run << 8 | (e & 0xffull), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    xstore(err, 0ull);
+  }
+}
+
+// Peer data plane push (remote mode with a mapped server inbox): slice `wg` of
+// the lane's delta straight into its slot of the server GPU's inbox over xGMI,
+// then the slice's tag = vc + 1 (WorkerTrainingProcessor.java:95-97: the
+// GradientMessage of clock vc).  A solve whose wait timed out pushes zeros.
+template <int FP>
+__device__ __forceinline__ void peer_push_slice(const SolverCfg& cfg, const SolveDev& dv, const AsyncLaneDev& A,
+                                                int wg, long long vc, unsigned long long* err) {
+  const int tid = threadIdx.x, K = cfg.K;
+  const int c = tid >> 5, f = wg * 32 + (tid & 31);
+  const bool bad = xload(err) != 0ull;
+  if (c < K) {
+    const size_t e = (size_t)c * FP + f;
+    st_sys_f32(A.inbox + e, bad ? 0.f : ld_sc1(dv.delta + e));
+  }
+  if (wg == 0 && tid < K) {
+    const size_t e = (size_t)K * FP + tid;
+    st_sys_f32(A.inbox + e, bad ? 0.f : ld_sc1(dv.delta + e));
+  }
+  publish_sys_tag(A.inbox_tag + wg, (unsigned)(vc + 1));
+}
+
 // The update of slice `wg` by the delta of ticket t, after slice wg of ticket
 // t - 1 (serial per slice, in ticket order: the single GRADIENTS_TOPIC
 // partition), w += lr * delta (ServerProcessor.java:148-151, 225-228).  The new
@@ -65,7 +98,7 @@ template <int FP>
 __device__ __forceinline__ void async_apply_slice(const SolverCfg& cfg, const SolveDev& dv, const AsyncLaneDev& A,
                                                   const AsyncArgs& a, int wg, unsigned long long t, bool logl,
                                                   unsigned long long* err, int spin, int* flag) {
-  const int tid = threadIdx.x, K = cfg.K, P = cfg.P;
+  const int tid = threadIdx.x, K = cfg.K;
   const int c = tid >> 5, f = wg * 32 + (tid & 31);
   const bool coef = c < K;
   const bool icpt = wg == 0 && tid < K;
@@ -87,7 +120,7 @@ __device__ __forceinline__ void async_apply_slice(const SolverCfg& cfg, const So
     }
   }
   __syncthreads();
-  const size_t so = (size_t)(t % (unsigned long long)a.R) * P;
+  const size_t so = (size_t)(t % (unsigned long long)a.R) * (size_t)a.sstride;
   if (coef) {
     const float nw = ld_sc1(a.w + e) + a.lr * dl;
     st_sc1(a.w + e, nw);
@@ -137,6 +170,11 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   // (PSX_LANES_STAMPS, slot 30 of the lane's table: 0 released, 4 solved, 5 ticket,
   // 6 applied, 7 token out / evaluation starts, 8 evaluation done)
   if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.spin_rel, dv.err_host);
+  // The lane's sticky error word: a wait that timed out after the previous solve's
+  // report (FinScal::store) -- its push (turn words, barriers) or its evaluation --
+  // is reported here, then the word is cleared BEFORE the barrier every workgroup
+  // of this iteration passes, so nothing stored in this iteration is wiped.
+  if (wg == 0 && tid == 0) report_and_clear(dv, err, run);
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, a.spin_rel);
   // the lane's rows, state and the pulled snapshot were written by other CUs
   // (other XCDs for the snapshot) since this CU last read them
@@ -150,7 +188,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     relc = ch[0].tag;  // the record consumed
   }
   if (q.stop) {
-    if (wg == 0 && tid == 0) *A.relc = relc;
+    if (wg == 0 && tid == 0) {
+      *A.relc = relc;
+      report_and_clear(dv, err, run);  // (a wait of this iteration's barrier)
+    }
     return false;
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
@@ -181,17 +222,34 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
       float wo_pre = 0.f, b_pre = 0.f;
       if (owner) {  // the pulled weights of this slice: snapshot -> this solve's private copy
         const int c = tid >> 5, f = wg * 32 + (tid & 31);
-        const size_t so = (size_t)(q.snap % (long long)a.R) * cfg.P;
-        if (c < K && f < cfg.F) wo_pre = a.snap[so + (size_t)c * FP + f];
-        if (wg == 0 && tid < K) b_pre = a.snap[so + (size_t)K * FP + tid];
+        const size_t so = (size_t)(q.snap % (long long)a.R) * (size_t)a.sstride;
+        if (a.peer_rx) {
+          // peer data plane: the server GPU writes this slice of the lane's receive
+          // slot over xGMI and then its tag (system scope); wait for the tag of this
+          // pull, acquire, read the slice with system-scope loads
+          if (tid == 0) {
+            const unsigned* tg = a.snap_tag + (size_t)(q.snap % (long long)a.R) * NS + wg;
+            int spins = 0;
+            while ((int)(ld_sys_u32(tg) - q.pull_tag) < 0 && ++spins <= a.spin_rel) __builtin_amdgcn_s_sleep(2);
+            if (spins > a.spin_rel) xstore(err, 10ull);  // the server's weights never arrived
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+          }
+          __syncthreads();
+          if (c < K && f < cfg.F) wo_pre = ld_sys_f32(a.snap + so + (size_t)c * FP + f);
+          if (wg == 0 && tid < K) b_pre = ld_sys_f32(a.snap + so + (size_t)K * FP + tid);
+        } else {
+          if (c < K && f < cfg.F) wo_pre = a.snap[so + (size_t)c * FP + f];
+          if (wg == 0 && tid < K) b_pre = a.snap[so + (size_t)K * FP + tid];
+        }
         if (c < K) A.wpull[(size_t)c * FP + f] = wo_pre;
         if (wg == 0 && tid < K) A.wpull[(size_t)K * FP + tid] = b_pre;
+        // (the error word was cleared before this iteration's first barrier: this
+        // store is not wiped and FinScal::store reports it with the solve)
         if (!a.remote && tid == 0 &&
             a.snap_tag[(size_t)(q.snap % (long long)a.R) * NS + wg] != (unsigned)(unsigned long long)q.snap)
           xstore(err, 8ull);  // the snapshot slot was reused before this lane pulled it
       }
       if (wg == 0 && tid == 0) {
-        xstore(err, 0ull);
         if constexpr (S == 1) xstore(xch + kXchGen + ((rn + 1u) & 1u), 0ull);
       }
       if (row) {
@@ -273,6 +331,9 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   if (!a.remote) {  // the server is this launch: serial slice updates in ticket order
     if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
     x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
+  } else if (A.inbox) {  // the server GPU's inbox: the delta goes out with the token
+    if (wg < NS) peer_push_slice<FP>(cfg, dv, A, wg, q.vc, err);
+    x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 6);
   if (wg == 0 && tid == 0)
@@ -348,8 +409,8 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
 
 __global__ void async_init_kernel(const float* __restrict__ w, float* snap, unsigned* snap_tag,
                                   unsigned long long* turn, unsigned long long* ticket, int P, int NS, int R,
-                                  unsigned long long t) {
-  const size_t so = (size_t)(t % (unsigned long long)R) * P;
+                                  unsigned long long t, long long sstride) {
+  const size_t so = (size_t)(t % (unsigned long long)R) * (size_t)sstride;
   if (w) {  // (remote mode: the ticket only)
     for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < P; i += (int)(gridDim.x * blockDim.x))
       snap[so + i] = w[i];
@@ -399,7 +460,8 @@ void launch_af(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al
 }  // namespace
 
 void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long long t, hipStream_t s) {
-  async_init_kernel<<<8, 256, 0, s>>>(a.w, a.snap, a.snap_tag, a.turn, a.ticket, cfg.P, cfg.Fp / 32, a.R, t);
+  async_init_kernel<<<8, 256, 0, s>>>(a.w, a.snap, a.snap_tag, a.turn, a.ticket, cfg.P, cfg.Fp / 32, a.R, t,
+                                      a.sstride);
 }
 
 void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {

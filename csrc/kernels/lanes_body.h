@@ -45,6 +45,36 @@ __device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigne
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsrc_of(base, bytes), (int)off, 0, kAuxSys);
 }
 
+// Peer data plane (csrc/comm/peer_bus.h): words another GPU writes over xGMI into
+// fine-grained memory, or this GPU writes into another's.  System-scope relaxed
+// atomics = global loads / stores with sc0 sc1 (no L1 / L2 reuse); the hand-off
+// is payload stores -> s_waitcnt vmcnt(0) -> barrier -> one lane: release fence
+// (system) + tag store; the reader polls the tag, acquires (system), then loads.
+typedef __attribute__((address_space(1))) unsigned g_u32;
+__device__ __forceinline__ unsigned ld_sys_u32(const unsigned* p) {
+  asm volatile("" ::: "memory");  // a spin re-reads
+  return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys_u32(unsigned* p, unsigned v) {
+  __hip_atomic_store((g_u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys_f32(const float* p) {
+  return __hip_atomic_load((g_f32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys_f32(float* p, float v) {
+  __hip_atomic_store((g_f32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// One lane publishes `tag` for the stores of its whole workgroup (call from every
+// thread: the wait / barrier are the workgroup's).
+__device__ __forceinline__ void publish_sys_tag(unsigned* tagp, unsigned tag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    st_sys_u32(tagp, tag);
+  }
+}
+
 static_assert(kEvalAccInts == (size_t)kAccCopies * kMaxEvalModels * 256 * kAccStride, "EvalMulti::acc size");
 
 // Accumulator cell of model m in copy `copy` (EvalMulti::acc)
@@ -812,13 +842,14 @@ struct PairModels {
 };
 
 
+// red_base: kPairEvalLds bytes of LDS (the logits' exchange, the counts)
+constexpr int kPairEvalLds = 8192 + 2 * 256 * 4 + 16 + 16 * 4;
 template <int FP>
-__device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t* Xt, const int32_t* yt, int T, int wg,
-                                               int G, const PairModels& pm, int* acc, unsigned* ticket) {
+__device__ __forceinline__ void lane_pair_eval_at(char* red_base, int K, const uint16_t* Xt, const int32_t* yt, int T,
+                                                  int wg, int G, const PairModels& pm, int* acc, unsigned* ticket) {
   const int tid = threadIdx.x;
   const bool wrow = pm.aslot != nullptr, srow = pm.bslot != nullptr;
   if (!wrow && !srow) return;  // (uniform)
-  char* red_base = lds + 32 * FP * 2;
   int* cl = (int*)(red_base + 8192);  // [2][256]
   int* lastp = cl + 512;
   float* bl = (float*)(lastp + 4);    // [16]: model A 0..7, model B 8..15
@@ -939,6 +970,12 @@ __device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t*
     }
     st_sys_chunk(m == 0 ? pm.aslot : pm.bslot, 1088u, (unsigned)i * 16u, ch);
   }
+}
+// (the lane kernels: the exchange sits behind the row workgroups' 32-row tile image)
+template <int FP>
+__device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t* Xt, const int32_t* yt, int T, int wg,
+                                               int G, const PairModels& pm, int* acc, unsigned* ticket) {
+  lane_pair_eval_at<FP>(lds + 32 * FP * 2, K, Xt, yt, T, wg, G, pm, acc, ticket);
 }
 
 }  // namespace lanes_detail

@@ -252,6 +252,7 @@ struct RelRec {
   unsigned long long slot_w, slot_s;  // pinned EvalSlot addresses (0: no row)
   unsigned seq_w, seq_s;              // their sequence numbers (low 32 bits)
   int delay_us;          // injected straggler delay before the push (tests)
+  unsigned pull_tag;     // peer data plane: the receive slot's tag that carries these weights
 };
 PSX_HD inline void pack_release(const RelRec& q, unsigned tag, TagChunk* ch) {
   auto lo = [](long long v) { return (unsigned)(unsigned long long)v; };
@@ -263,7 +264,7 @@ PSX_HD inline void pack_release(const RelRec& q, unsigned tag, TagChunk* ch) {
   ch[4] = TagChunk{tag, lo(q.r.step), hi(q.r.step), lo(q.r.first2)};
   ch[5] = TagChunk{tag, hi(q.r.first2), lo((long long)q.slot_w), hi((long long)q.slot_w)};
   ch[6] = TagChunk{tag, q.seq_w, lo((long long)q.slot_s), hi((long long)q.slot_s)};
-  ch[7] = TagChunk{tag, q.seq_s, (unsigned)q.delay_us, 0u};
+  ch[7] = TagChunk{tag, q.seq_s, (unsigned)q.delay_us, q.pull_tag};
 }
 PSX_HD inline void unpack_release(const TagChunk* ch, RelRec& q) {
   auto j = [](unsigned l, unsigned h) { return (long long)(((unsigned long long)h << 32) | l); };
@@ -283,6 +284,7 @@ PSX_HD inline void unpack_release(const TagChunk* ch, RelRec& q) {
   q.slot_s = (unsigned long long)j(ch[6].b, ch[6].c);
   q.seq_s = ch[7].a;
   q.delay_us = (int)ch[7].b;
+  q.pull_tag = ch[7].c;
   q.r.pad = 0;
 }
 // token: lane -> host (pinned ring, slot t % ring): {tag = ticket (low 32 bits,
@@ -306,6 +308,10 @@ struct AsyncLaneDev {
   unsigned long long* rec;    // [kRelChunks * 2] the release record broadcast (+ the ticket at [16])
   unsigned long long* relc;   // release records consumed by this lane (persists across launches)
   AsyncRelease* rel;     // pinned release record (host -> device)
+  // peer data plane (remote mode, csrc/comm/peer_bus.h): this lane's worker's slot in
+  // the server GPU's inbox (an IPC mapping over xGMI) -- [P] delta + [FP/32] slice tags
+  float* inbox;
+  unsigned* inbox_tag;
 };
 
 struct AsyncArgs {
@@ -314,9 +320,10 @@ struct AsyncArgs {
   const int32_t* dsy;
   float* w;             // server master weights [P]
   float lr;
-  float* snap;          // [R][P] w after ticket t at slot t % R
+  float* snap;          // [R][sstride] w after ticket t at slot t % R
   unsigned* snap_tag;   // [R][FP/32] ticket of each slot's slices (sanity check)
   int R;
+  long long sstride;    // floats between snapshot slots (P; a peer region's padded stride)
   unsigned long long* ticket;  // last ticket handed out (device counter)
   unsigned long long* turn;    // [FP/32][32] last ticket applied to slice s (own 256-B line each)
   AsyncToken* tok;             // pinned token ring
@@ -334,6 +341,10 @@ struct AsyncArgs {
   // push order); a release's snapshot is the lane's receive slot (snap = slot)
   int remote;
   int xcd0;            // lane l runs on XCD xcd0 + l
+  // peer_rx = 1 (remote mode, peer data plane): snap / snap_tag are this rank's
+  // receive slots [L][P] / [L][FP/32] in fine-grained memory the server GPU writes
+  // over xGMI; a release's pull_tag says which slice tags carry its weights
+  int peer_rx;
 };
 
 // The launch's uniform arguments, in device memory (see AsyncLaneDev).

@@ -120,6 +120,10 @@ class LanesLoop {
   // otherwise take the slow ones' share of `updates`).
   int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s = 600.0, double deadline_ms = 0.0,
                     int64_t per_lane = 0);
+  // lane_budget[l]: the most solves lane l starts in this call (empty: no per-lane bound) --
+  // a chunked run (checkpoints) passes each worker's remaining share of max_iters
+  int64_t run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms,
+                    const std::vector<int64_t>& lane_budget);
   // Multi-rank SSP / ASP on a worker GPU: the server is rank 0 (AsyncServer,
   // async_server.h).  Same persistent launch in remote mode: a lane's push only
   // publishes its token; this loop sends the delta to peer 0 (`p2p`, on
@@ -128,8 +132,20 @@ class LanesLoop {
   // rank's queue `reply`: which worker the next weights are for) by receiving the
   // weights into that lane's slot and releasing the lane once they landed.
   // Returns the solves run (every lane's FINAL token sent).
+  // p2p == nullptr: the peer data plane (set_peer) -- no host transfer at all.
   int64_t run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, hipStream_t stream,
                            hipStream_t comm_stream, double max_wait_s = 600.0, double deadline_ms = 0.0);
+  // Peer data plane (csrc/comm/peer_bus.h) for run_async_remote: this rank's receive
+  // region (slot l = lane l's weights, written by the server GPU) and, per lane, its
+  // worker's slot in the server's inbox (an IPC mapping).  Then run_async_remote takes
+  // no transport: the lanes push their deltas into the inbox themselves and wait for
+  // their slots' tags; the host only forwards tokens and answers reply tokens.
+  void set_peer(uintptr_t rx_data, uintptr_t rx_tags, int64_t rx_stride, const std::vector<uintptr_t>& inbox,
+                const std::vector<uintptr_t>& inbox_tag);
+  bool peer() const { return peer_rx_ != nullptr; }
+  // Allocate (and zero) the asynchronous workspace now: ranks sharing one GPU do this
+  // before any rank's persistent launch holds CUs a fill kernel would wait for.
+  void prepare_async() { ensure_async(); }
   int64_t tickets() const { return (int64_t)aticket_; }  // deltas applied by the asynchronous loop so far
   double host_us_per_update() const { return async_updates_ ? async_ns_ / 1000.0 / (double)async_updates_ : 0.0; }
   // Evaluate the last round's rows (one launch of riders only).
@@ -165,6 +181,7 @@ class LanesLoop {
     return v;
   }
   int64_t rounds_run() const { return rounds_run_; }
+  int lanes() const { return cfg_.L; }
   // device stats of lane l's last solve: evals, accepted, ls failures, resets, error
   std::vector<int> stats(int lane, hipStream_t stream) const;
   float loss(int lane, hipStream_t stream) const;
@@ -311,6 +328,14 @@ class LanesLoop {
   int log_lane_ = -1;
   int64_t launch_no_ = 0;
   std::vector<hipEvent_t> pull_ev_;     // remote mode: a lane's weights received
+  // peer data plane (set_peer): receive region, per-lane inbox slots, the pull tag of
+  // each lane's pending release
+  float* peer_rx_ = nullptr;
+  unsigned* peer_rx_tag_ = nullptr;
+  int64_t peer_stride_ = 0;
+  std::vector<uintptr_t> peer_inbox_, peer_inbox_tag_;
+  std::vector<unsigned> pull_tag_;
+  unsigned long long* tick_host_ = nullptr;  // pinned: the ticket a remote launch starts from
   // the persistent launch runs on a stream of its own (non-blocking: no implicit
   // synchronisation of the null stream, e.g. a host-staged transfer, waits for it),
   // ordered after / before the caller's stream by events

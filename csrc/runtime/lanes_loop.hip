@@ -329,6 +329,7 @@ LanesLoop::~LanesLoop() {
   if (aev_out_) (void)hipEventDestroy(aev_out_);
   if (tok_host_) (void)hipHostFree(tok_host_);
   if (pack_host_) (void)hipHostFree(pack_host_);
+  if (tick_host_) (void)hipHostFree(tick_host_);
   if (err_host_) (void)hipHostFree(err_host_);
 }
 
@@ -988,6 +989,10 @@ void LanesLoop::ensure_async() {
     A.rec = reinterpret_cast<unsigned long long*>(b + o[l].rec);
     A.relc = reinterpret_cast<unsigned long long*>(b + o[l].relc);
     A.rel = rel_host_ + l;
+    if (peer_rx_) {
+      A.inbox = reinterpret_cast<float*>(peer_inbox_[l]);
+      A.inbox_tag = reinterpret_cast<unsigned*>(peer_inbox_tag_[l]);
+    }
   }
   al_dev_ = reinterpret_cast<AsyncLaneDev*>(b + o_tab);
   pack_dev_ = reinterpret_cast<AsyncPack*>(b + o_pack);
@@ -1001,6 +1006,16 @@ void LanesLoop::ensure_async() {
   a.snap = reinterpret_cast<float*>(b + o_snap);
   a.snap_tag = reinterpret_cast<unsigned*>(b + o_stag);
   a.R = R_;
+  a.sstride = P_;
+  if (peer_rx_) {  // the receive slots are the peer region's (lane l = slot l)
+    a.snap = peer_rx_;
+    a.snap_tag = peer_rx_tag_;
+    a.R = L;
+    a.sstride = peer_stride_;
+    a.peer_rx = 1;
+  }
+  hip_check(hipHostMalloc((void**)&tick_host_, sizeof(unsigned long long), hipHostMallocDefault),
+            "hipHostMalloc(ticket)");
   a.ticket = reinterpret_cast<unsigned long long*>(b + o_tick);
   a.turn = reinterpret_cast<unsigned long long*>(b + o_turn);
   a.tok = tok_host_;
@@ -1155,6 +1170,7 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
     }
   }
   q.delay_us = lane < (int)cfg_.delay_us.size() ? cfg_.delay_us[lane] : 0;
+  q.pull_tag = peer_rx_ ? pull_tag_[lane] : 0u;
   write_release(lane, q);
   return true;
 }
@@ -1198,8 +1214,17 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   a.cpar = (int)(launches_ & 1);
   hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
   hip_check(hipStreamWaitEvent(astream_, aev_in_, 0), "async order in");
-  launch_async_init(cfg_.scfg, a, aticket_, astream_);
-  hip_check(hipGetLastError(), "async init launch");
+  if (remote) {
+    // the ticket only: an SDMA copy from pinned memory, not a kernel -- on a GPU shared
+    // with other ranks' persistent launches a kernel's workgroups could wait for CUs
+    // those launches hold
+    *tick_host_ = aticket_;
+    hip_check(hipMemcpyAsync(a.ticket, tick_host_, sizeof(unsigned long long), hipMemcpyHostToDevice, astream_),
+              "async ticket");
+  } else {
+    launch_async_init(cfg_.scfg, a, aticket_, astream_);
+    hip_check(hipGetLastError(), "async init launch");
+  }
   pack_host_->cfg = cfg_.scfg;
   pack_host_->a = a;
   hip_check(hipMemcpyAsync(pack_dev_, pack_host_, sizeof(AsyncPack), hipMemcpyHostToDevice, astream_), "async args");
@@ -1210,7 +1235,17 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
 
 int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms,
                              int64_t per_lane) {
+  std::vector<int64_t> b;
+  if (per_lane > 0) b.assign((size_t)cfg_.L, per_lane);
+  return run_async(updates, stream, max_wait_s, deadline_ms, b);
+}
+
+int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wait_s, double deadline_ms,
+                             const std::vector<int64_t>& lane_budget) {
   const int64_t t_begin = steady_ns();
+  if (!lane_budget.empty() && (int)lane_budget.size() != cfg_.L)
+    throw std::invalid_argument("LanesLoop::run_async: one budget per lane");
+  auto at_budget = [&](int l, int64_t started) { return !lane_budget.empty() && started >= lane_budget[l]; };
   if (!cfg_.tracker) throw std::invalid_argument("LanesLoop::run_async: needs the tracker");
   ensure_async();
   const int L = cfg_.L;
@@ -1236,7 +1271,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
     auto start_ready = [&](double now) {
       for (int l = 0; l < L; ++l) {
         if (state_[l] != kWant || stopping || started >= updates) continue;
-        if (per_lane > 0 && lane_started[l] >= per_lane) continue;
+        if (at_budget(l, lane_started[l])) continue;
         if (try_release(l, want_vc_[l], now)) {
           state_[l] = kRunning;
           ++started;
@@ -1302,7 +1337,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
       if (stopping || started >= updates) break;
       bool any_want = false, end = false;
       for (int l = 0; l < L; ++l)
-        if (state_[l] == kWant && !(per_lane > 0 && lane_started[l] >= per_lane)) {
+        if (state_[l] == kWant && !at_budget(l, lane_started[l])) {
           int64_t size = 0, start = 0, sn = 0;
           check(api().window_state(reinterpret_cast<void*>(cfg_.window[l]), &size, &start, &sn), "window state");
           if (size <= 0 && exhausted(l)) end = true;  // a worker with no rows left: the run ends
@@ -1335,15 +1370,34 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
   return done;
 }
 
+void LanesLoop::set_peer(uintptr_t rx_data, uintptr_t rx_tags, int64_t rx_stride, const std::vector<uintptr_t>& inbox,
+                         const std::vector<uintptr_t>& inbox_tag) {
+  if (aws_) throw std::logic_error("LanesLoop::set_peer: before the first asynchronous run");
+  const int L = cfg_.L;
+  if (!rx_data || !rx_tags || rx_stride < P_ || (int)inbox.size() != L || (int)inbox_tag.size() != L)
+    throw std::invalid_argument("LanesLoop::set_peer: receive region / one inbox slot per lane");
+  for (int l = 0; l < L; ++l)
+    if (!inbox[l] || !inbox_tag[l]) throw std::invalid_argument("LanesLoop::set_peer: null inbox slot");
+  peer_rx_ = reinterpret_cast<float*>(rx_data);
+  peer_rx_tag_ = reinterpret_cast<unsigned*>(rx_tags);
+  peer_stride_ = rx_stride;
+  peer_inbox_ = inbox;
+  peer_inbox_tag_ = inbox_tag;
+  pull_tag_.assign(L, 0u);
+}
+
 int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, int64_t iters, hipStream_t stream,
                                     hipStream_t cs, double max_wait_s, double deadline_ms) {
   const int64_t t_begin = steady_ns();
-  if (!p2p || !ctrl || !reply) throw std::invalid_argument("LanesLoop::run_async_remote: transport / queues");
+  const bool peer = p2p == nullptr;
+  if ((!p2p && !peer_rx_) || !ctrl || !reply)
+    throw std::invalid_argument("LanesLoop::run_async_remote: transport (or set_peer) / queues");
+  if (p2p && peer_rx_) throw std::invalid_argument("LanesLoop::run_async_remote: a transport AND the peer data plane");
   if (iters < 1) throw std::invalid_argument("LanesLoop::run_async_remote: iters >= 1");
   ensure_async();
   const int L = cfg_.L;
   if (R_ < L) throw std::invalid_argument("LanesLoop::run_async_remote: more lanes than receive slots");
-  if (pull_ev_.empty()) {
+  if (!peer && pull_ev_.empty()) {
     pull_ev_.assign(L, nullptr);
     for (auto& e : pull_ev_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   }
@@ -1372,11 +1426,16 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
         const int j = rt.worker >= 0 && rt.worker < cfg_.N ? lane_of_[rt.worker] : -1;
         if (j < 0 || state_[j] != kWaitPull)
           throw std::logic_error("LanesLoop: reply for worker " + std::to_string(rt.worker) + " not waiting");
+        want_vc_[j] = rt.vc;
+        progress = true;
+        if (peer) {  // the server GPU writes the weights into slot j itself: the lane waits for tag aux
+          pull_tag_[j] = (unsigned)rt.aux;
+          state_[j] = kWant;
+          continue;
+        }
         p2p->recv(aargs_.snap + (size_t)j * P_, (size_t)P_, Comm::kF32, 0, cs);
         hip_check(hipEventRecord(pull_ev_[j], cs), "pull event");
         state_[j] = kPulling;
-        want_vc_[j] = rt.vc;
-        progress = true;
       }
       const double now = epoch_ms();
       for (int l = 0; l < L; ++l) {
@@ -1409,8 +1468,9 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
         ++done;
         const bool fin = ++it[l] >= iters || (deadline_ms > 0.0 && now >= deadline_ms) ||
                          (exhausted(l) && window_empty(l));
-        // push: the delta to the server, then its token (WorkerTrainingProcessor.java:95-97)
-        p2p->send(lanes_[l].dv.delta, (size_t)P_, Comm::kF32, 0, cs);
+        // push: the delta to the server, then its token (WorkerTrainingProcessor.java:95-97);
+        // peer data plane: the lane already wrote it into the server's inbox (tagged)
+        if (!peer) p2p->send(lanes_[l].dv.delta, (size_t)P_, Comm::kF32, 0, cs);
         CtrlToken ct{};
         ct.worker = cfg_.k[l];
         ct.kind = fin ? 1 : 0;

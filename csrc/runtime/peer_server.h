@@ -1,0 +1,115 @@
+// Host loop of the peer data plane's server rank (SSP / ASP across GPUs).
+//
+// Reference: ServerProcessor.process (ServerProcessor.java:143-183) -- apply
+// every gradient on arrival in the single partition's order, log a server row
+// on worker-0 gradients, answer the workers MessageTracker releases
+// (MessageTracker.java:69-87) with the weights after that update.
+//
+// Division of labour (csrc/comm/peer_bus.h, csrc/kernels/server_persist.h):
+//   * device: ONE persistent launch on this GPU applies the deltas (already in
+//     this GPU's inbox: the workers' lanes wrote them over xGMI), writes the new
+//     weights into the released workers' receive slots on their GPUs and
+//     evaluates the server rows;
+//   * host (this class): pops the worker ranks' tokens from the shared-memory
+//     queue in arrival order, runs the C++ vector-clock tracker, writes one
+//     64-B command per token into a pinned ring, and answers each release on
+//     the worker's rank reply queue with its pull tag.  It never waits for the
+//     device and never synchronises a stream per delta (host_us_per_update).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#include "../comm/peer_bus.h"
+#include "../host/capi.h"
+#include "../kernels/server_persist.h"
+#include "async_server.h"
+
+namespace psx {
+
+struct PeerServerCfg {
+  int nworkers = 0;
+  float lr = 1.f;
+  int K = 0, F = 0, FP = 0;
+  int64_t P = 0;
+  float* w = nullptr;            // fp32 master weights [P] on this GPU
+  const uint16_t* Xt = nullptr;  // test set (server rows)
+  const int32_t* yt = nullptr;
+  int T = 0;
+  uintptr_t inbox = 0;           // this rank's PeerRegion (one slot per worker)
+  PeerLayout lay;                // its layout (P, NS, slots = nworkers)
+  std::vector<uintptr_t> rx, rx_tag;  // per worker: its receive slot / slice tags on its GPU (IPC mappings)
+  uintptr_t api = 0, tracker = 0, ctrl = 0, sink = 0;
+  std::vector<uintptr_t> replies;     // per worker: its rank's reply queue
+  double worker_timeout_s = 600.0;
+  int sxcd = 0;                  // the XCD of the persistent launch
+};
+
+class PeerServer {
+ public:
+  PeerServer(const PeerServerCfg& cfg, hipStream_t stream);
+  ~PeerServer();
+  PeerServer(const PeerServer&) = delete;
+  PeerServer& operator=(const PeerServer&) = delete;
+  // New run (AsyncServer::begin semantics): launches the persistent kernel if it is
+  // not running and sends every live worker the weights of its clock.
+  void begin();
+  // Serve tokens until every worker finished (the launch then drains: w is final),
+  // a checkpoint is due (drained as well) or a worker needs the caller's decision.
+  AsyncStatus run(int64_t checkpoint_every);
+  void fail(int k);
+  // Stop the persistent launch and wait for it (idempotent).
+  void stop();
+  int64_t updates() const { return updates_; }
+  void set_updates(int64_t u) { updates_ = u; }
+  int64_t tokens() const { return tokens_; }
+  int64_t commands() const { return (int64_t)cmds_; }
+  double host_us_per_update() const { return updates_run_ ? host_ns_ / 1000.0 / (double)updates_run_ : 0.0; }
+  std::vector<int> failed() const;
+  bool running() const { return running_; }
+  // (worker, vc) of every delta in arrival order (the single partition's order; tests
+  // replay it through a fresh tracker), the first kMaxArrivals
+  static constexpr size_t kMaxArrivals = 1 << 20;
+  const std::vector<std::pair<int, int64_t>>& arrivals() const { return arrivals_; }
+
+ private:
+  const HostApi& api() const { return *api_; }
+  void check_api(int rc, const char* what) const;
+  void check_device() const;
+  void launch();
+  void write_cmd(const SrvCmd& c);
+  // command k (-1: none) + releases (ks, vs) + replies; returns after the host part
+  void issue(int k, int64_t vc, const int* ks, const int64_t* vs, int n);
+  int log_worker() const;
+
+  PeerServerCfg cfg_;
+  hipStream_t stream_;
+  const HostApi* api_;
+  int NS_ = 0;
+  // device workspace
+  void* ws_ = nullptr;
+  SrvArgs* args_dev_ = nullptr;
+  SrvArgs args_{};
+  // pinned
+  TagChunk* cmd_ring_ = nullptr;
+  SrvArgs* args_host_ = nullptr;
+  unsigned long long* err_host_ = nullptr;
+  unsigned long long* consumed_host_ = nullptr;
+  int ring_ = 256;
+  uint64_t cmds_ = 0;          // commands written (the kernel's numbering: 1..cmds_)
+  uint64_t cmds_launch_ = 0;   // commands written before the current launch
+  int64_t launches_ = 0;
+  bool running_ = false;
+  std::vector<uint32_t> ptag_;  // pulls sent per worker (the device counters' mirror)
+  std::vector<uint8_t> finished_, failed_, dead_;
+  std::vector<double> busy_since_;
+  std::vector<int> rel_k_;
+  std::vector<int64_t> rel_v_;
+  std::vector<std::pair<int, int64_t>> arrivals_;
+  int64_t updates_ = 0, tokens_ = 0, updates_run_ = 0;
+  double host_ns_ = 0.0;
+};
+
+}  // namespace psx

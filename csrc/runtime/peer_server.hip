@@ -1,0 +1,365 @@
+// Host loop of the peer data plane's server rank (see peer_server.h).
+#include "peer_server.h"
+
+#include <emmintrin.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "../host/sink_record.h"
+#include "../kernels/common.h"
+#include "../solver/solver.h"
+
+namespace psx {
+namespace {
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+constexpr int kKindDelta = 0, kKindFinal = 1, kKindError = 2;
+}  // namespace
+
+PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg), stream_(nullptr) {
+  (void)stream;  // the persistent launch gets a stream of its own (nothing else is ordered behind it)
+  const int N = cfg.nworkers;
+  if (N < 1 || N > kSrvMaxWorkers) throw std::invalid_argument("PeerServer: 1 .. 64 workers");
+  if (!cfg.api || !cfg.tracker || !cfg.ctrl) throw std::invalid_argument("PeerServer: missing host runtime handles");
+  api_ = reinterpret_cast<const HostApi*>(cfg.api);
+  if (api_->version != kHostApiVersion) throw std::runtime_error("PeerServer: host runtime C ABI version mismatch");
+  if (!cfg.w || cfg.P <= 0 || cfg.K < 1 || cfg.K > 8) throw std::invalid_argument("PeerServer: weights / classes");
+  if (cfg.FP != 128 && cfg.FP != 256 && cfg.FP != 512 && cfg.FP != 1024)
+    throw std::invalid_argument("PeerServer: FP in {128, 256, 512, 1024}");
+  if (cfg.P != (int64_t)cfg.K * cfg.FP + cfg.K) throw std::invalid_argument("PeerServer: P != K * FP + K");
+  NS_ = cfg.FP / 32;
+  if (!cfg.inbox || cfg.lay.P != cfg.P || cfg.lay.NS != NS_ || cfg.lay.slots < N)
+    throw std::invalid_argument("PeerServer: inbox region layout");
+  if ((int)cfg.rx.size() != N || (int)cfg.rx_tag.size() != N || (int)cfg.replies.size() != N)
+    throw std::invalid_argument("PeerServer: one receive slot, tag array and reply queue per worker");
+  for (int j = 0; j < N; ++j)
+    if (!cfg.rx[j] || !cfg.rx_tag[j] || !cfg.replies[j]) throw std::invalid_argument("PeerServer: null peer handle");
+  if (cfg.sink && (!cfg.Xt || !cfg.yt || cfg.T < 1)) throw std::invalid_argument("PeerServer: server rows need the test set");
+  if (cfg.sxcd < 0 || cfg.sxcd > 7) throw std::invalid_argument("PeerServer: sxcd in 0..7");
+  // device workspace (ALL device memory and its zero-fill here, before any
+  // persistent launch of another rank can hold the CUs a fill kernel would need)
+  const int FP = cfg.FP;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  const size_t o_args = take(sizeof(SrvArgs));
+  const size_t o_rx = take(sizeof(float*) * N);
+  const size_t o_rxt = take(sizeof(unsigned*) * N);
+  const size_t o_ptag = take((size_t)N * NS_ * 4);
+  const size_t o_shi = take((size_t)16 * FP * 2);
+  const size_t o_slo = take((size_t)16 * FP * 2);
+  const size_t o_sb = take(16 * 4);
+  const size_t o_acc = take((size_t)2 * 256 * kAccStride * 4);
+  const size_t o_etk = take(4);
+  const size_t o_flags = take((size_t)(kSrvWg + 1) * 32 * 8);
+  const size_t o_rec = take(32 * 8);
+  const size_t o_claim = take(64 * 4);
+  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(peer server)");
+  hip_check(hipMalloc(&ws_, off), "hipMalloc(peer server workspace)");
+  hip_check(hipMemset(ws_, 0, off), "hipMemset(peer server workspace)");
+  char* b = static_cast<char*>(ws_);
+  hip_check(hipMemcpy(b + o_rx, cfg.rx.data(), sizeof(float*) * N, hipMemcpyHostToDevice), "rx table");
+  hip_check(hipMemcpy(b + o_rxt, cfg.rx_tag.data(), sizeof(unsigned*) * N, hipMemcpyHostToDevice), "rx tag table");
+  hip_check(hipHostMalloc((void**)&cmd_ring_, sizeof(TagChunk) * kCmdChunks * ring_,
+                          hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(command ring)");
+  hip_check(hipHostMalloc((void**)&err_host_, 2 * sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(error word)");
+  hip_check(hipHostMalloc((void**)&args_host_, sizeof(SrvArgs), hipHostMallocDefault), "hipHostMalloc(args)");
+  std::memset((void*)cmd_ring_, 0, sizeof(TagChunk) * kCmdChunks * ring_);
+  err_host_[0] = err_host_[1] = 0;
+  consumed_host_ = err_host_ + 1;
+  hip_check(hipDeviceSynchronize(), "peer server setup");
+  SrvArgs& a = args_;
+  std::memset(&a, 0, sizeof(a));
+  a.K = cfg.K;
+  a.F = cfg.F;
+  a.FP = FP;
+  a.P = (int)cfg.P;
+  a.N = N;
+  a.lr = cfg.lr;
+  a.w = cfg.w;
+  a.shi = reinterpret_cast<uint16_t*>(b + o_shi);
+  a.slo = reinterpret_cast<uint16_t*>(b + o_slo);
+  a.sb = reinterpret_cast<float*>(b + o_sb);
+  a.inbox = reinterpret_cast<const float*>(cfg.inbox);
+  a.inbox_tag = reinterpret_cast<const unsigned*>(cfg.inbox + cfg.lay.tag_off());
+  a.in_stride = cfg.lay.stride();
+  a.rx = reinterpret_cast<float* const*>(b + o_rx);
+  a.rx_tag = reinterpret_cast<unsigned* const*>(b + o_rxt);
+  a.ptag = reinterpret_cast<unsigned*>(b + o_ptag);
+  a.cmd = cmd_ring_;
+  a.ring = ring_;
+  a.consumed_host = consumed_host_;
+  a.err_host = err_host_;
+  a.Xt = cfg.Xt;
+  a.yt = cfg.yt;
+  a.T = cfg.T;
+  a.acc = reinterpret_cast<int*>(b + o_acc);
+  a.eticket = reinterpret_cast<unsigned*>(b + o_etk);
+  a.flags = reinterpret_cast<unsigned long long*>(b + o_flags);
+  a.rec = reinterpret_cast<unsigned long long*>(b + o_rec);
+  a.claim = reinterpret_cast<unsigned*>(b + o_claim);
+  a.sxcd = cfg.sxcd;
+  // ~1 PCIe round trip per poll: the command wait covers the worker timeout; a delta's
+  // tag is written before its token leaves the worker's GPU (a short wait at most)
+  const double polls = cfg.worker_timeout_s * 5e5;
+  a.spin_cmd = polls > 2e9 ? 2000000000 : (polls < 1e6 ? 1000000 : (int)polls);
+  a.spin = 1 << 22;
+  args_dev_ = reinterpret_cast<SrvArgs*>(b + o_args);
+  ptag_.assign(N, 0u);
+  finished_.assign(N, 0);
+  failed_.assign(N, 0);
+  dead_.assign(N, 0);
+  busy_since_.assign(N, -1.0);
+  rel_k_.resize(N + 1);
+  rel_v_.resize(N + 1);
+}
+
+PeerServer::~PeerServer() {
+  try {
+    stop();
+  } catch (...) {
+  }
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+  }
+  if (ws_) (void)hipFree(ws_);
+  if (cmd_ring_) (void)hipHostFree(cmd_ring_);
+  if (err_host_) (void)hipHostFree(err_host_);
+  if (args_host_) (void)hipHostFree(args_host_);
+}
+
+void PeerServer::check_api(int rc, const char* what) const {
+  if (rc < 0) throw std::runtime_error(std::string("PeerServer: ") + what + ": " + api_->last_error());
+}
+
+void PeerServer::check_device() const {
+  const unsigned long long e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
+  if (e)
+    throw std::runtime_error("PeerServer: the server kernel's wait timed out (command " + std::to_string(e >> 8) +
+                             ", code " + std::to_string((int)(e & 0xff)) +
+                             (int(e & 0xff) == 11 ? ": a worker's delta never reached the inbox)" : ")"));
+}
+
+int PeerServer::log_worker() const {
+  // server rows follow worker 0's deltas (ServerProcessor.java:154-165), or the
+  // lowest surviving worker's once 0 has failed
+  for (int j = 0; j < cfg_.nworkers; ++j)
+    if (!failed_[j]) return j;
+  return -1;
+}
+
+std::vector<int> PeerServer::failed() const {
+  std::vector<int> out;
+  for (int j = 0; j < cfg_.nworkers; ++j)
+    if (failed_[j]) out.push_back(j);
+  return out;
+}
+
+void PeerServer::launch() {
+  if (running_) return;
+  SrvArgs a = args_;
+  a.cmd0 = cmds_;
+  a.cpar = (int)(launches_ & 1);
+  a.launch = ++launches_;
+  *args_host_ = a;
+  // (an SDMA copy from pinned memory and the launch: no fill / copy kernel that
+  // would need CUs another rank's persistent launch may hold on a shared GPU)
+  hip_check(hipMemcpyAsync(args_dev_, args_host_, sizeof(SrvArgs), hipMemcpyHostToDevice, stream_), "server args");
+  launch_server_persist(args_dev_, cfg_.FP, stream_);
+  hip_check(hipGetLastError(), "server kernel launch");
+  cmds_launch_ = cmds_;
+  running_ = true;
+}
+
+void PeerServer::write_cmd(const SrvCmd& c) {
+  // ring flow control: slot (n - 1) % ring is free once the kernel read command n - ring
+  const uint64_t n = cmds_ + 1;
+  if (n > (uint64_t)ring_) {
+    const double t0 = now_s();
+    while (__atomic_load_n(consumed_host_, __ATOMIC_ACQUIRE) + (uint64_t)ring_ < n) {
+      check_device();
+      if (now_s() - t0 > cfg_.worker_timeout_s) throw std::runtime_error("PeerServer: the server kernel stopped reading commands");
+      _mm_pause();
+    }
+  }
+  TagChunk ch[kCmdChunks];
+  pack_cmd(c, (unsigned)n, ch);
+  volatile TagChunk* dst = cmd_ring_ + (size_t)((n - 1) % (uint64_t)ring_) * kCmdChunks;
+  for (int i = 0; i < kCmdChunks; ++i) {
+    __m128i v;
+    std::memcpy(&v, &ch[i], 16);
+    _mm_store_si128((__m128i*)(void*)&dst[i], v);  // one 16-B store per chunk (a chunk is never torn)
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  cmds_ = n;
+}
+
+void PeerServer::issue(int k, int64_t vc, const int* ks, const int64_t* vs, int n) {
+  SrvCmd c{};
+  c.k = k;
+  c.dtag = k >= 0 ? (unsigned)(vc + 1) : 0u;
+  int slot = -1;
+  uint64_t seq = 0;
+  if (k >= 0 && cfg_.sink && k == log_worker()) {  // the global model's test metrics: one server row
+    uintptr_t addr = 0;
+    slot = api().sink_acquire((void*)cfg_.sink, &seq, &addr);
+    check_api(slot, "metrics sink acquire");
+    c.log = 1;
+    c.slot_s = addr;
+    c.seq_s = (unsigned)seq;
+  }
+  const double t = now_s();
+  for (int i = 0; i < n; ++i) {
+    const int j = ks[i];
+    if (j < 0 || j >= cfg_.nworkers) throw std::logic_error("PeerServer: release of an unknown worker");
+    if (finished_[j]) continue;
+    c.relmask |= 1ull << j;
+  }
+  write_cmd(c);
+  // the replies: which worker the weights in flight are for, and their pull tag
+  for (int i = 0; i < n; ++i) {
+    const int j = ks[i];
+    if (finished_[j]) continue;
+    busy_since_[j] = t;
+    CtrlToken r{};
+    r.worker = j;
+    r.vc = vs[i];
+    r.aux = (int64_t)++ptag_[j];
+    if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
+      throw std::runtime_error("PeerServer: reply queue of worker " + std::to_string(j) + " full");
+  }
+  if (slot >= 0) {
+    SinkRecord rec{slot, 1 | kSinkTagged, seq, -1, -1, vc, 0};
+    check_api(api().sink_submit_many((void*)cfg_.sink, 1, &rec), "metrics sink submit");
+  }
+}
+
+void PeerServer::begin() {
+  launch();
+  std::fill(finished_.begin(), finished_.end(), 0);
+  std::fill(failed_.begin(), failed_.end(), 0);
+  std::fill(busy_since_.begin(), busy_since_.end(), -1.0);
+  int n = 0;
+  for (int j = 0; j < cfg_.nworkers; ++j) {
+    int live = api().tracker_is_live((void*)cfg_.tracker, j);
+    check_api(live, "tracker is_live");
+    if (!live && !dead_[j]) {  // retired because it finished the previous run: rejoins
+      check_api(api().tracker_revive((void*)cfg_.tracker, j), "tracker revive");
+      live = 1;
+    }
+    if (!live) {
+      failed_[j] = finished_[j] = dead_[j] = 1;
+      continue;
+    }
+    const int64_t u = api().tracker_clock((void*)cfg_.tracker, j);
+    if (u > 0) api().tracker_sent((void*)cfg_.tracker, j, u);
+    rel_k_[n] = j;
+    rel_v_[n] = u;
+    ++n;
+  }
+  issue(-1, 0, rel_k_.data(), rel_v_.data(), n);  // the bootstrap (ServerProcessor.java:75-87)
+}
+
+void PeerServer::fail(int k) {
+  if (k < 0 || k >= cfg_.nworkers) throw std::out_of_range("PeerServer::fail: worker id");
+  launch();
+  failed_[k] = finished_[k] = dead_[k] = 1;
+  busy_since_[k] = -1.0;
+  const int n = api().tracker_retire((void*)cfg_.tracker, k, rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
+  check_api(n, "tracker retire");
+  if (n) issue(-1, 0, rel_k_.data(), rel_v_.data(), n);
+}
+
+void PeerServer::stop() {
+  if (!running_) return;
+  SrvCmd c{};
+  c.stop = 1;
+  write_cmd(c);
+  running_ = false;
+  const double t0 = now_s();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(stream_);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) hip_check(e, "server launch drain");
+    if (now_s() - t0 > 60.0) throw std::runtime_error("PeerServer: the server launch did not drain in 60 s");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  check_device();
+}
+
+AsyncStatus PeerServer::run(int64_t checkpoint_every) {
+  AsyncStatus st;
+  launch();
+  const double poll = cfg_.worker_timeout_s < 1.0 ? cfg_.worker_timeout_s : 1.0;
+  for (;;) {
+    int open = 0;
+    for (int j = 0; j < cfg_.nworkers; ++j) open += !finished_[j];
+    if (open == 0) break;
+    CtrlToken t;
+    const int got = api().ctrl_pop((void*)cfg_.ctrl, &t, poll);
+    check_api(got, "token pop");
+    check_device();
+    if (!got) {  // watchdog: a worker holding weights that stays silent has failed
+      const double now = now_s();
+      for (int j = 0; j < cfg_.nworkers; ++j)
+        if (!finished_[j] && busy_since_[j] >= 0.0 && now - busy_since_[j] > cfg_.worker_timeout_s) {
+          st.code = kAsyncWatchdog;
+          st.worker = j;
+          st.updates = updates_;
+          return st;
+        }
+      continue;
+    }
+    const auto h0 = std::chrono::steady_clock::now();
+    ++tokens_;
+    const int k = t.worker;
+    if (k < 0 || k >= cfg_.nworkers) throw std::runtime_error("PeerServer: token from an unknown worker");
+    if (t.kind == kKindError) {
+      st.code = kAsyncErrorToken;
+      st.worker = k;
+      st.updates = updates_;
+      return st;
+    }
+    if (finished_[k]) throw std::runtime_error("PeerServer: delta from a finished worker " + std::to_string(k));
+    busy_since_[k] = -1.0;
+    if (arrivals_.size() < kMaxArrivals) arrivals_.emplace_back(k, t.vc);
+    int n = api().tracker_on_delta((void*)cfg_.tracker, k, t.vc, rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
+    check_api(n, "tracker on_delta");
+    if (t.kind == kKindFinal) {  // a finished worker no longer holds the others back
+      finished_[k] = 1;
+      const int m = api().tracker_retire((void*)cfg_.tracker, k, rel_k_.data() + n, rel_v_.data() + n,
+                                         (int)rel_k_.size() - n);
+      check_api(m, "tracker retire");
+      n += m;
+    }
+    issue(k, t.vc, rel_k_.data(), rel_v_.data(), n);
+    ++updates_;
+    ++updates_run_;
+    host_ns_ += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - h0).count();
+    if (checkpoint_every > 0 && updates_ % checkpoint_every == 0) {
+      stop();  // (the caller reads w: the launch must have drained)
+      st.code = kAsyncCheckpoint;
+      st.updates = updates_;
+      return st;
+    }
+  }
+  stop();
+  st.code = kAsyncDone;
+  st.updates = updates_;
+  return st;
+}
+
+}  // namespace psx

@@ -113,6 +113,9 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--workers_per_rank", type=int, default=1,
                    help="multi-rank BSP on GPUs: logical workers per worker rank, one XCD each in one launch per "
                         "round (the native lanes loop)")
+    g.add_argument("--async_plane", default="auto", choices=["auto", "peer", "host"],
+                   help="SSP/ASP with --workers_per_rank > 1: peer = deltas / weights written GPU to GPU by the "
+                        "kernels over xGMI (IPC-mapped fine-grained memory), host = shared-memory staging")
     g.add_argument("--checkpoint_dir", default=None)
     g.add_argument("--checkpoint_every", type=int, default=0)
     g.add_argument("--resume", action="store_true")
@@ -176,7 +179,7 @@ def server_config(a) -> PSConfig:
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,
         resume=a.resume, inject_worker_delay_ms=parse_delays(a.inject_worker_delay), trace_path=a.trace,
-        perf_log=a.perf_log, async_scheduler=a.async_scheduler, workers_per_rank=a.workers_per_rank,
+        perf_log=a.perf_log, async_scheduler=a.async_scheduler, workers_per_rank=a.workers_per_rank, async_plane=a.async_plane,
         model=a.model, dtype=a.dtype, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push, sparse_pull=not a.dense_pull,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         inject_worker_stop={k: int(v) for k, v in parse_worker_map(a.inject_worker_stop).items()},

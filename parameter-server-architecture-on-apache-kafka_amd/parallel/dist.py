@@ -338,6 +338,7 @@ class DistEngine:
 
     def close(self):
         """Release the native communicator (collective: every rank calls it)."""
+        self._close_async()
         comm = getattr(self, "comm", None)
         self.comm = None
         if comm is not None:
@@ -812,30 +813,113 @@ class DistEngine:
         """Bytes per HostP2P direction: a few of the largest messages (dense weights)."""
         return max(1 << 20, 4 * 4 * int(self.spec.P))
 
+    def _peer_plane(self) -> bool:
+        """SSP / ASP with several workers per worker rank (the asynchronous lanes loop):
+        the peer data plane (csrc/comm/peer_bus.h) when every rank is on a GPU -- the
+        lanes write their deltas into the server GPU's inbox and the server kernel
+        writes the weights into their receive slots over xGMI.  Agreed collectively."""
+        if not (self.async_mode and self.wpr > 1) or self.wide or self.cfg.async_plane == "host":
+            return False
+        flags = [None] * self.world
+        dist.all_gather_object(flags, bool(is_gpu(self.device)))
+        ok = all(flags)
+        if self.cfg.async_plane == "peer" and not ok:
+            raise ValueError("--async_plane peer: every rank (the server too) must be on a GPU")
+        return ok
+
     def _run_async(self) -> dict:
         if not hasattr(self, "comm"):  # collective: every rank creates it (None on gloo / CPU)
             self.comm = make_comm(self.rank, self.world, self.device)
         # several workers per worker rank (the asynchronous lanes loop): its persistent
-        # launch holds every CU of the lanes' XCDs, and an RCCL p2p kernel would have to
-        # co-reside there -- the pushes / pulls (P floats each) go through the host
-        # shared-memory data plane instead, staged by the DMA engines (all ranks share
-        # the node)
-        self._open_ctrl(host_p2p=self.comm is None or self.wpr > 1)
+        # launch holds every CU of the lanes' XCDs, so no RCCL p2p kernel could run
+        # beside it.  The pushes / pulls go either through the peer data plane (the
+        # kernels themselves store into IPC-mapped fine-grained memory of the other
+        # GPU: no transfer kernel, no host staging) or, with a CPU rank, through the
+        # host shared-memory transport HostP2P
+        # the control plane (and the data plane's regions) are set up once per engine and
+        # kept across runs (the warm-up and timed runs of bench.py): the native server
+        # loops hold their queues' handles
+        if not hasattr(self, "_peer"):
+            self._peer = self._peer_plane()
+        if self._ctrl is None:
+            self._open_ctrl(host_p2p=(self.comm is None or self.wpr > 1) and not self._peer)
+            if self._peer:
+                self._peer_setup()
         try:
-            if self.is_server:  # ONE server loop: the native one (RCCL p2p, or HostP2P without RCCL)
+            if self.is_server:  # ONE server loop: the native one (peer plane, RCCL p2p or HostP2P)
                 return self._server_loop_native()
             if self.wpr > 1:
                 return self._worker_loop_lanes()
             return self._worker_loop()
         finally:
             dist.barrier()
-            if self.rank == 0 and self._ctrl is not None:
+
+    def _close_async(self):
+        """Tear down the asynchronous control / data planes (after the last run)."""
+        ps = getattr(self, "_pserver", None)
+        if ps is not None:
+            ps.stop()
+            self._pserver = None
+        for m in getattr(self, "_peer_maps", []):
+            m.close()
+        self._peer_maps = []
+        if getattr(self, "_ctrl", None) is not None:
+            if self.rank == 0:
                 self._ctrl.unlink()
                 for q in getattr(self, "_replies", []):
                     q.unlink()
-            if self._hp2p is not None:
-                self._hp2p.unlink()
-                self._hp2p = None
+            self._ctrl = None
+        if getattr(self, "_hp2p", None) is not None:
+            self._hp2p.unlink()
+            self._hp2p = None
+
+    def _peer_setup(self):
+        """Peer data plane bring-up (collective): every rank exports one region of
+        fine-grained device memory -- the server its inbox (one delta slot per worker),
+        a worker rank its receive slots (one per lane) -- the handles are exchanged, each
+        side maps the other's, and the loops are built with EVERY allocation and fill
+        done now: on a GPU shared by several ranks (the one-GPU rehearsal) a fill kernel
+        enqueued after another rank's persistent launch could wait for its CUs."""
+        cfg, sp = self.cfg, self.spec
+        h = _native.hip()
+        N, NS = cfg.num_workers, sp.Fp // 32
+        dev = self.device.index or 0
+        reg = h.PeerRegion(sp.P, NS, N if self.is_server else self.wpr, dev)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, reg.handle())
+        self._peer_region = reg
+        if self.is_server:
+            maps, rx, rxt = {}, [], []
+            for k in range(N):
+                r, l = 1 + k // self.wpr, k % self.wpr
+                if r not in maps:
+                    maps[r] = h.PeerMapping(handles[r], sp.P, NS, self.wpr)
+                rx.append(maps[r].data(l))
+                rxt.append(maps[r].tags(l))
+            self._peer_maps = list(maps.values())
+            n_lanes = (self.world - 1) * self.wpr
+            if oversubscribed() and n_lanes >= 8:
+                raise ValueError("one shared GPU: the worker ranks' lanes leave no XCD for the server kernel")
+            ev = self.evalset
+            d = dict(nworkers=N, lr=float(cfg.lr), K=sp.K, F=sp.F, FP=sp.Fp, P=int(sp.P),
+                     w=self.server.w.data_ptr(), inbox=reg.base, rx=rx, rx_tag=rxt, api=_native.host.capi(),
+                     tracker=self.server.tracker.handle, ctrl=self._ctrl.handle,
+                     replies=[self._replies[k // self.wpr].handle for k in range(N)],
+                     worker_timeout_s=float(cfg.worker_timeout_s),
+                     # one GPU shared by every rank: the XCD after the worker ranks' lanes
+                     sxcd=n_lanes if oversubscribed() else 0)
+            if self.log is not None and ev is not None:
+                d.update(sink=self.log.native.handle, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=int(ev.T))
+            self._pserver = h.PeerServer(d)
+        else:
+            m = h.PeerMapping(handles[0], sp.P, NS, N)
+            self._peer_maps = [m]
+            lp = self._alanes_build()
+            ks = [w.k for w in self.workers]
+            lp.set_peer(reg.data(0), reg.tags(0), reg.stride, [m.data(k) for k in ks], [m.tags(k) for k in ks])
+            lp.prepare_async()
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
 
     def _native_server(self):
         """The C++ server loop (csrc/runtime/async_server.h) bound to this engine's
@@ -901,8 +985,9 @@ class DistEngine:
         handles checkpoints and failed workers (ServerProcessor.java:143-183)."""
         cfg, srv = self.cfg, self.server
         h = _native.hip()
-        a = self._native_server()
-        if self.log is not None:
+        peer = getattr(self, "_peer", False)
+        a = self._pserver if peer else self._native_server()
+        if self.log is not None and not peer:
             # rows logged natively go to the sink bound at creation: rebind if swapped
             if getattr(self, "_aserver_sink", None) not in (None, self.log.native.handle):
                 self._aserver = None
@@ -934,7 +1019,8 @@ class DistEngine:
         return {"rounds": int(srv.tracker.min_clock()), "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": n / elapsed if elapsed > 0 else 0.0, "max_vc_gap": int(srv.tracker.max_gap),
                 "failed_workers": list(a.failed), "host_us_per_update": a.host_us_per_update, "native_server": True,
-                "sparse_pulls": int(a.sparse_pulls), "dense_pulls": int(a.dense_pulls)}
+                "sparse_pulls": int(a.sparse_pulls), "dense_pulls": int(a.dense_pulls),
+                "data_plane": "peer" if peer else ("rccl" if self._hp2p is None else "host")}
 
     def _worker_loop_lanes(self) -> dict:
         """This rank's workers as lanes of ONE persistent launch (LanesLoop.run_async_remote,
@@ -943,10 +1029,46 @@ class DistEngine:
         peer 0) with its token, receives the weights of every release the server
         announces on this rank's reply queue, and logs the worker rows the lanes
         evaluate (WorkerTrainingProcessor.java:63-98, ServerProcessor.java:143-183)."""
-        cfg, W, sp = self.cfg, self.workers, self.spec
+        cfg, W = self.cfg, self.workers
         h = _native.hip()
         lp = getattr(self, "_alanes", None)
         if lp is None:
+            lp = self._alanes_build()
+        else:
+            lp.set_sink(self.log.native.handle)
+        for i, w in enumerate(W):
+            lp.set_next_local(i, int(w.source.next_local))
+            lp.set_seen_at_solve(i, int(w._seen_at_solve))
+        peer = getattr(self, "_peer", False)
+        p2p = None if peer else (self._hp2p if self._hp2p is not None else h.RcclP2P(self.comm.c))
+        if not hasattr(self, "_comm_stream"):
+            self._comm_stream = torch.cuda.Stream(self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        t_start = time.time()
+        deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
+        iters = int(cfg.max_iters) if cfg.max_iters else 1 << 40
+        n = int(lp.run_async_remote(p2p, self._ctrl.handle, self._reply.handle, iters, stream,
+                                    self._comm_stream.cuda_stream, float(cfg.worker_timeout_s), deadline_ms))
+        torch.cuda.synchronize(self.device)
+        lp.poll_errors()
+        for i, w in enumerate(W):
+            w.source.next_local = int(lp.next_local(i))
+            w._seen_at_solve = int(lp.seen_at_solve(i))
+            if w.ring.XT is not None:
+                w.ring.xt_stale = True
+        if self.log is not None:
+            self.log.drain()
+        elapsed = time.time() - t_start
+        return {"rounds": n // max(1, len(W)), "updates": n, "elapsed_s": elapsed, "async_lanes": True,
+                "data_plane": "peer" if peer else "host", "host_us_per_update": float(lp.host_us_per_update)}
+
+    def _alanes_build(self):
+        """This rank's asynchronous lanes loop (created once): every worker of the rank
+        a lane of one persistent launch, on consecutive XCDs."""
+        lp = getattr(self, "_alanes", None)
+        if lp is None:
+            cfg, W, sp = self.cfg, self.workers, self.spec
+            h = _native.hip()
             from ..ops.lr import Fragments
 
             o = cfg.solver
@@ -969,36 +1091,14 @@ class DistEngine:
                      log_workers=int(cfg.log_workers), new_rows=int(cfg.iter_new_rows),
                      new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), log_worker=-1,
                      delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W],
-                     # ranks sharing one GPU: worker rank i's lanes on XCDs i*wpr ..; on its own GPU a
-                     # rank keeps its last XCD free for the RCCL kernels beside the persistent launch
+                     # ranks sharing one GPU (the one-GPU rehearsals): worker rank i's lanes on XCDs
+                     # i*wpr ..; on its own GPU a rank's lanes start at XCD 0 and may take all 8 (no
+                     # transfer kernel runs beside the persistent launch: the pushes / pulls are the
+                     # lanes' own stores (peer plane) or host staging by the DMA engines)
                      xcd0=(self.worker_id * len(W)) if oversubscribed() else 0)
             lp = h.LanesLoop(d, None)
             self._alanes = lp
-        else:
-            lp.set_sink(self.log.native.handle)
-        for i, w in enumerate(W):
-            lp.set_next_local(i, int(w.source.next_local))
-            lp.set_seen_at_solve(i, int(w._seen_at_solve))
-        p2p = self._hp2p if self._hp2p is not None else h.RcclP2P(self.comm.c)
-        if not hasattr(self, "_comm_stream"):
-            self._comm_stream = torch.cuda.Stream(self.device)
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        t_start = time.time()
-        deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
-        iters = int(cfg.max_iters) if cfg.max_iters else 1 << 40
-        n = int(lp.run_async_remote(p2p, self._ctrl.handle, self._reply.handle, iters, stream,
-                                    self._comm_stream.cuda_stream, float(cfg.worker_timeout_s), deadline_ms))
-        torch.cuda.synchronize(self.device)
-        lp.poll_errors()
-        for i, w in enumerate(W):
-            w.source.next_local = int(lp.next_local(i))
-            w._seen_at_solve = int(lp.seen_at_solve(i))
-            if w.ring.XT is not None:
-                w.ring.xt_stale = True
-        if self.log is not None:
-            self.log.drain()
-        elapsed = time.time() - t_start
-        return {"rounds": n // max(1, len(W)), "updates": n, "elapsed_s": elapsed, "async_lanes": True}
+        return lp
 
     def _worker_loop(self) -> dict:
         cfg, wk = self.cfg, self.worker

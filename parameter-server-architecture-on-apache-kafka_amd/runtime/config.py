@@ -70,6 +70,11 @@ class PSConfig:
     # logical workers per worker rank (one XCD each: the multi-lane round loop);
     # the reference hosts all of its workers in one process (BaseKafkaApp.java:25,70)
     workers_per_rank: int = 1
+    # SSP / ASP data plane of worker ranks with several lanes: "peer" = the lanes push
+    # their deltas into the server GPU's inbox and the server kernel writes the weights
+    # into the workers' receive slots over xGMI (csrc/comm/peer_bus.h; every rank on a
+    # GPU); "host" = the host shared-memory transport HostP2P; "auto" = peer when possible
+    async_plane: str = "auto"
     # checkpoint
     checkpoint_dir: str | None = None
     checkpoint_every: int = 0

@@ -445,6 +445,7 @@ class LocalEngine:
         deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
         u0 = srv.updates
         clock0 = {w.k: int(srv.tracker.clock(w.k)) for w in W}
+        clock_start = dict(clock0)
         total = int(cfg.max_iters) * len(W) if cfg.max_iters else 0
         ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
         chunk = max(1, int(cfg.checkpoint_every)) if ck else 1 << 16
@@ -461,10 +462,12 @@ class LocalEngine:
                     exhausted_since = exhausted_since or time.time()
                 if self._stop(done // max(1, len(W)), t_start, exhausted_since):
                     break
-                # one call for the whole run: max_iters iterations per worker exactly (under
-                # ASP the fast workers would otherwise take the slow ones' share)
-                per_lane = int(cfg.max_iters) if (cfg.max_iters and not ck) else 0
-                n = int(lp.run_async(int(todo), stream, 600.0, deadline_ms, per_lane))
+                # max_iters iterations per worker exactly (under ASP the fast workers would
+                # otherwise take the slow ones' share): each lane's remaining share, also
+                # across the chunks of a checkpointed run
+                budget = ([max(0, int(cfg.max_iters) - (int(srv.tracker.clock(w.k)) - clock_start[w.k])) for w in W]
+                          if cfg.max_iters else 0)
+                n = int(lp.run_async(int(todo), stream, float(cfg.worker_timeout_s), deadline_ms, budget))
                 done += n
                 srv.updates += n
                 for i, w in enumerate(W):

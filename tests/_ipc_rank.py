@@ -15,11 +15,16 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
-    if mode.startswith("async"):  # SSP(2) / ASP: 1 server rank + worker ranks x 3 lanes (HostP2P data plane)
-        c = -1 if mode == "async_asp" else 2
+    if mode.startswith("async") or mode.startswith("peer"):
+        # SSP(2) / ASP: 1 server rank + worker ranks x 3 lanes -- async_*: a CPU server and
+        # the host shared-memory data plane; peer_*: a GPU server rank and the peer data
+        # plane (csrc/comm/peer_bus.h), worker 1 a straggler (+2 ms per iteration)
+        c = -1 if mode.endswith("_asp") else 2
+        peer = mode.startswith("peer")
         return PSConfig(num_workers=(world - 1) * 3, consistency_model=c, producer_time_per_event=0,
                         stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=8, min_buffer_size=128,
                         max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3,
+                        async_plane="peer" if peer else "host", inject_worker_delay_ms={1: 2.0} if peer else {},
                         worker_timeout_s=25.0)  # (a stuck transport raises with its reason, inside the test's limit)
     return PSConfig(num_workers=(world - 1) * 4, consistency_model=0, producer_time_per_event=0,
                     stream_mode="per_iter", rows_per_iter=1024, epochs=1000,
@@ -40,7 +45,7 @@ def main():
     from psx.utils.data import synth_finefood
 
     rank, world, device = init_from_env()
-    if mode.startswith("async") and rank == 0:  # (see test_async_lanes_worker_ranks)
+    if mode.startswith("async") and rank == 0:  # (see test_async_lanes_worker_ranks; peer_*: a GPU server)
         device = torch.device("cpu")
     train, test = synth_finefood(20000, seed=0), synth_finefood(4877, seed=1)
     eng = DistEngine(cfg_for(world, mode), rank, world, device, train=train, test=test)
@@ -48,10 +53,16 @@ def main():
     out = eng.run()
     res = {"rank": rank, "rounds": int(eng.rounds), "lanes": getattr(eng, "_lanes", None) is not None,
            "updates": out.get("updates")}
+    for key in ("data_plane", "host_us_per_update"):
+        if key in out:
+            res[key] = out[key]
     if rank == 0:
         torch.save(eng.server.w.detach().cpu(), os.path.join(out_dir, f"w_{mode}.pt"))
         res["server_rows"] = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
         res["max_vc_gap"] = out.get("max_vc_gap")
+        ps = getattr(eng, "_pserver", None)
+        if ps is not None:
+            res["arrivals"] = [list(a) for a in ps.arrivals]
     else:
         res["async_lanes"] = bool(out.get("async_lanes"))
     with open(os.path.join(out_dir, f"{mode}_rank{rank}.json"), "w") as fh:

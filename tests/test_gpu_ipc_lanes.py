@@ -109,3 +109,55 @@ def test_async_lanes_worker_ranks(cuda, tmp_path, mode, bound):
         assert res[0]["max_vc_gap"] <= bound, res[0]
     w = torch.load(os.path.join(tmp_path, f"w_{mode}.pt"), weights_only=True)
     assert torch.isfinite(w).all()
+
+
+def _replay_arrivals(arrivals, workers, c):
+    """The server's arrival order through a fresh C++ VectorClockTracker (every
+    delta the one the tracker expects) and the gap of the workers' latest clocks
+    along it (tools/plot_logs.py:max_vc_gap, in arrival order)."""
+    from psx import _native
+
+    t = _native.host.VectorClockTracker(workers, c)
+    released = {k: 0 for k in range(workers)}
+    latest, gap = {}, 0
+    for k, v in arrivals:
+        assert released.get(k) == v, (k, v, released)
+        del released[k]
+        for j, u in t.on_delta(k, v):
+            assert j not in released
+            released[j] = u
+        latest[k] = v
+        if len(latest) == workers:
+            gap = max(gap, max(latest.values()) - min(latest.values()))
+    return gap
+
+
+@pytest.mark.parametrize("mode,bound", [("peer_ssp", 3), ("peer_asp", None)])
+def test_peer_plane_gpu_server_two_worker_ranks(cuda, tmp_path, mode, bound):
+    """SSP(2) / ASP over the peer data plane (csrc/comm/peer_bus.h): a GPU server
+    rank running the persistent server kernel (csrc/kernels/server_persist.hip) on
+    XCD 6 and TWO worker ranks of 3 lanes each on XCDs 0-2 / 3-5, three processes
+    on one GPU.  Every delta is stored by its lane into the server GPU's inbox,
+    every pull by the server kernel into the worker's receive slot -- no HostP2P, no
+    stream synchronisation per delta.  Worker 1 is a straggler (+2 ms per
+    iteration): the arrival order replays through a fresh tracker, its gap stays
+    <= D + 1 under SSP(2) and runs ahead under ASP (ServerProcessor.java:95-183,
+    MessageTracker.java:69-87, README.md:299-321)."""
+    res = _launch(tmp_path, mode, world=3, timeout=150)
+    srv, wks = res[0], res[1:]
+    assert srv.get("data_plane") == "peer", srv
+    assert all(w.get("async_lanes") and w.get("data_plane") == "peer" for w in wks), wks
+    assert srv["updates"] == 6 * 8, srv["updates"]
+    rows = srv["server_rows"]
+    assert len(rows) == 8 and all(r[1] > 0.2 for r in rows[2:]), rows  # one server row per worker-0 delta
+    arr = srv["arrivals"]
+    assert len(arr) == 6 * 8
+    gap = _replay_arrivals(arr, 6, 2 if bound is not None else -1)
+    if bound is not None:
+        assert gap <= bound and srv["max_vc_gap"] <= bound, (gap, srv["max_vc_gap"])
+    else:
+        assert gap >= 4, gap  # eventual: the fast workers are not held back by worker 1
+    # the server's host time per applied delta: pop, tracker, one command, the replies
+    assert srv["host_us_per_update"] <= 10.0, srv["host_us_per_update"]
+    w = torch.load(os.path.join(tmp_path, f"w_{mode}.pt"), weights_only=True)
+    assert torch.isfinite(w).all()

@@ -880,6 +880,8 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("set_peer", &LanesLoop::set_peer, py::arg("rx_data"), py::arg("rx_tags"), py::arg("rx_stride"),
            py::arg("inbox"), py::arg("inbox_tag"))
       .def("prepare_async", &LanesLoop::prepare_async)
+      .def("set_async_debug", &LanesLoop::set_async_debug, py::arg("buf"), py::arg("cap"))
+      .def_property_readonly("async_log", &LanesLoop::async_log)
       .def_property_readonly("peer", &LanesLoop::peer)
       .def(
           "run_async_remote",

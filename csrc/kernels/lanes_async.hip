@@ -108,6 +108,11 @@ __device__ __forceinline__ void async_apply_slice(const SolverCfg& cfg, const So
   float dl = 0.f, di = 0.f;
   if (coef && !bad) dl = ld_sc1(dv.delta + e);
   if (icpt && !bad) di = ld_sc1(dv.delta + ei);
+  if (a.dbg_delta) {  // (tests) the delta of ticket t as applied
+    float* dd = a.dbg_delta + (size_t)((t - 1ull) % (unsigned long long)a.dbg_cap) * (size_t)cfg.P;
+    if (coef) dd[e] = dl;
+    if (icpt) dd[ei] = di;
+  }
   unsigned long long* turn = a.turn + (size_t)wg * 32;
   if (tid == 0) {
     int spins = 0;

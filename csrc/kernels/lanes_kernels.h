@@ -345,6 +345,10 @@ struct AsyncArgs {
   // receive slots [L][P] / [L][FP/32] in fine-grained memory the server GPU writes
   // over xGMI; a release's pull_tag says which slice tags carry its weights
   int peer_rx;
+  // debug (tests: the float64 replay of an asynchronous run): the delta every ticket t
+  // applied, at dbg_delta[(t - 1) % dbg_cap][P]; nullptr: off
+  float* dbg_delta;
+  int dbg_cap;
 };
 
 // The launch's uniform arguments, in device memory (see AsyncLaneDev).

@@ -202,6 +202,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       else
         fwd_body<FP, true, false, S, true>(cfg, win, slot, dv, lf, wg, G, acc);
       store_gpf<FP, S == 1>(dv, wg, G, acc);
+      if (wg == 0 && tid == 0) stamp(dv, slot, 15);
     }
     barrier();
     if (owner)

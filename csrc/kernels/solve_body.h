@@ -851,6 +851,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     }
   }
   __syncthreads();
+  if (wg0 && tid == 0) stamp(dv, slot, 12);
   // ---- all-gather of the partial dots as tagged granules (the data is its
   // own flag: R2 of the CDNA4 playbook).  Each workgroup stores its nv partial
   // sums as 2*nv 8-byte words {tag, 32-bit half of the fp64 value} with sc1
@@ -919,6 +920,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   }
   __syncthreads();
   wg_stamp(dv, slot, 3, wg);
+  if (wg0 && tid == 0) stamp(dv, slot, 13);
   if (tid < kNDX) dots[tid] = 0.0;  // pairs not stored stay 0
   __syncthreads();
   if (tid < nv) {
@@ -934,6 +936,7 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     dots[pos] = v;
   }
   __syncthreads();
+  if (wg0 && tid == 0) stamp(dv, slot, 14);
   if (tid == 0) {
     if (wg0) stamp(dv, slot, 5);
     ctrl_step(*cl, cfg, dots[kND] / (double)B, dots, slot, *csw);

@@ -143,6 +143,14 @@ class LanesLoop {
   void set_peer(uintptr_t rx_data, uintptr_t rx_tags, int64_t rx_stride, const std::vector<uintptr_t>& inbox,
                 const std::vector<uintptr_t>& inbox_tag);
   bool peer() const { return peer_rx_ != nullptr; }
+  // Debug (tests): every applied ticket's delta into buf [cap][P] (device, slot (t - 1) %
+  // cap) and a host log per ticket of what the release that solved it carried:
+  // {ticket, lane, worker, vc, snapshot ticket, B, start, first, step, n, first2, n2}
+  void set_async_debug(uintptr_t buf, int cap) {
+    dbg_delta_ = reinterpret_cast<float*>(buf);
+    dbg_cap_ = cap;
+  }
+  const std::vector<std::vector<int64_t>>& async_log() const { return alog_; }
   // Allocate (and zero) the asynchronous workspace now: ranks sharing one GPU do this
   // before any rank's persistent launch holds CUs a fill kernel would wait for.
   void prepare_async() { ensure_async(); }
@@ -322,7 +330,12 @@ class LanesLoop {
     int64_t vc = 0, nseen = 0;
     int slot_w = -1, slot_s = -1;
     uint64_t seq_w = 0, seq_s = 0;
+    int64_t snap = 0;  // the pulled snapshot's ticket
+    LaneRound r{};     // the window + new rows of the release
   };
+  float* dbg_delta_ = nullptr;
+  int dbg_cap_ = 0;
+  std::vector<std::vector<int64_t>> alog_;
   std::vector<RunRec> runrec_;
   std::vector<int> lane_of_;            // worker id -> lane (-1: not on this loop)
   int log_lane_ = -1;

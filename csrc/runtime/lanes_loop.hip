@@ -1145,6 +1145,8 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   rr = RunRec{};
   rr.vc = vc;
   rr.nseen = sn;
+  rr.snap = q.snap;
+  rr.r = q.r;
   if (cfg_.sink) {
     const bool w = cfg_.log_workers, sv = cfg_.log_server && lane == log_lane_;
     const int n = (w ? 1 : 0) + (sv ? 1 : 0);
@@ -1210,6 +1212,8 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   a.remote = remote ? 1 : 0;
   a.xcd0 = cfg_.xcd0;
   if (remote) a.w = nullptr;
+  a.dbg_delta = remote ? nullptr : dbg_delta_;
+  a.dbg_cap = dbg_cap_ > 0 ? dbg_cap_ : 1;
   a.launch = ++launch_no_;
   a.cpar = (int)(launches_ & 1);
   hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
@@ -1301,6 +1305,9 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
         ++done;
         // the rows of the iteration: server row first (ServerProcessor.java:154-165), then the worker row
         const RunRec& rr = runrec_[l];
+        if (dbg_delta_)
+          alog_.push_back({(int64_t)aticket_, l, cfg_.k[l], vc, rr.snap, rr.r.B, rr.r.start, rr.r.first, rr.r.step,
+                           rr.r.n, rr.r.first2, rr.r.n2});
         SinkRecord rec[2];
         int nr = 0;
         if (rr.slot_s >= 0) rec[nr++] = SinkRecord{rr.slot_s, 1 | kSinkTagged, rr.seq_s, -1, -1, vc, 0};

@@ -857,9 +857,8 @@ class DistEngine:
     def _close_async(self):
         """Tear down the asynchronous control / data planes (after the last run)."""
         ps = getattr(self, "_pserver", None)
-        if ps is not None:
+        if ps is not None:  # (the object stays for its counters: host_us_per_update, arrivals)
             ps.stop()
-            self._pserver = None
         for m in getattr(self, "_peer_maps", []):
             m.close()
         self._peer_maps = []

@@ -126,3 +126,80 @@ def test_async_lanes_continue_across_runs(cuda):
     assert len(rows) == 8 * 12
     _replay(rows, 8, 2)
     assert eng._lanes.tickets == 8 * 12
+
+
+@pytest.mark.parametrize("c", [2, -1])
+def test_async_lanes_replay_float64_oracle(cuda, c):
+    """8 workers, SSP(2) / ASP, worker 2 a straggler: the run replayed on the CPU
+    from the loop's own record of every ticket (LanesLoop.set_async_debug) --
+      (1) the server's update chain w = w0 + lr * delta_t in ticket order
+          reproduces the device weights (ServerProcessor.java:148-151, one
+          partition = serial updates);
+      (2) every delta equals the float64 oracle of the reference solve
+          (psx/models/reference.py) from the SNAPSHOT its release pulled (the
+          replayed weights after ticket q.snap) on the window it logged;
+      (3) the float64 chain -- oracle deltas applied to oracle snapshots -- ends
+          within tolerance of the device weights;
+      (4) every server row's F1 / accuracy equals the replayed global model's
+          test-set metrics right after the logging worker's update (:154-165)."""
+    from psx.models.reference import local_solve_reference, predict
+    from psx.utils.metrics import confusion, metrics_from_confusion
+
+    iters, N = 3, 8
+    eng = _engine(cuda, c, workers=N, iters=iters, delays={2: 2.0})
+    spec, lr = eng.spec, float(eng.cfg.lr)
+    W = list(eng.workers)
+    w0 = eng.server.w.detach().double().cpu().clone()
+    lp = eng._lanes_loop(W)
+    n_upd = N * iters
+    dbg = torch.zeros(n_upd, spec.P, dtype=torch.float32, device=cuda)
+    lp.set_async_debug(dbg.data_ptr(), n_upd)
+    out = eng.run()
+    assert out.get("async_lanes"), out
+    eng.log.drain(block=True)
+    torch.cuda.synchronize()
+    log = [list(r) for r in lp.async_log]
+    assert [r[0] for r in log] == list(range(1, n_upd + 1)), [r[0] for r in log]
+    D = dbg.double().cpu()
+    ds = W[0].source.ds
+    # (1) the update chain, and the snapshots it passes through
+    snaps = {0: w0.clone()}
+    w = w0.clone()
+    for i in range(n_upd):
+        w = w + lr * D[i]
+        snaps[i + 1] = w.clone()
+    wdev = eng.server.w.detach().double().cpu()
+    assert torch.allclose(w, wdev, atol=2e-6, rtol=0), (w - wdev).abs().max().item()
+    # (2) + (3) the deltas against the oracle from their pulled snapshots
+    ref_snaps = {0: w0.clone()}
+    wref = w0.clone()
+    worst = 0.0
+    for i, (t, l, k, vc, snap, B, start, first, step, n, first2, n2) in enumerate(log):
+        assert n + n2 == B, (t, B, n, n2)  # (per-iteration rows: the window IS the new rows)
+        rows = [first + j * step for j in range(n)] + [first2 + j * step for j in range(n2)]
+        Xw = ds.X[rows, : spec.F].double().cpu()
+        yw = ds.y[rows].long().cpu()
+        ws = snaps[snap]
+        res = local_solve_reference(Xw, yw, spec.coef(ws), spec.intercept(ws))
+        ref = spec.pack(res.coef, res.intercept).double() - ws
+        err, scale = (D[i] - ref).abs().max().item(), ref.abs().max().item()
+        worst = max(worst, err / max(scale, 1e-12))
+        assert err <= 2e-2 * scale + 1e-4, (t, k, err, scale)
+        wr = ref_snaps[snap]
+        r2 = local_solve_reference(Xw, yw, spec.coef(wr), spec.intercept(wr))
+        wref = wref + lr * (spec.pack(r2.coef, r2.intercept).double() - wr)
+        ref_snaps[i + 1] = wref.clone()
+    assert worst <= 1e-3, worst  # (measured 6e-6 .. 8e-6: profiles/r05/README.md)
+    chain = (wref - wdev).abs().max().item()
+    assert chain <= 2e-4, chain  # (measured 1.4e-5 .. 1.7e-5)
+    # (4) the server rows: worker 0's updates in ticket order
+    Xt, yt = eng.evalset.X[:, : spec.F].double().cpu(), eng.evalset.y.long().cpu()
+    srows = list(eng.log.book.server)
+    t_log = [r[0] for r in log if r[2] == 0]
+    assert len(srows) == len(t_log) == iters
+    for (ts, vc, f1, acc), t in zip(srows, t_log):
+        ws = snaps[t]
+        pred = predict(Xt, spec.coef(ws), spec.intercept(ws))
+        f1r, accr = metrics_from_confusion(confusion(yt.numpy(), pred.numpy(), spec.K))
+        assert abs(f1 - f1r) <= 2e-3 and abs(acc - accr) <= 2e-3, (t, f1, f1r, acc, accr)
+    print(f"replay c={c}: worst delta rel err {worst:.2e}, float64 chain max |dw| {chain:.2e}")

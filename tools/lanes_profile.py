@@ -80,7 +80,12 @@ def phases(st):
                       # controller copy, apply + next trial point
                       "b.reduce": us(T(s, 2), T(s, 3)), "b.grad": us(T(s, 3), T(s, 4)),
                       "b.dots+gather": us(T(s, 4), T(s, 5)), "b.ctrl": us(T(s, 5), T(s, 6)),
-                      "b.copy": us(T(s, 6), T(s, 7)), "b.apply+next": us(T(s, 7), T(s, 8))})
+                      "b.copy": us(T(s, 6), T(s, 7)), "b.apply+next": us(T(s, 7), T(s, 8)),
+                      # finer: partials store issue / barrier wait; the dots' local part, the
+                      # all-gather wait, the fixed-order sum
+                      "f.gpf": us(T(s, 1), T(s, 15)), "f.barrier": us(T(s, 15), T(s, 2)),
+                      "b.dots.local": us(T(s, 4), T(s, 12)), "b.gather": us(T(s, 12), T(s, 13)),
+                      "b.dots.sum": us(T(s, 13), T(s, 14))})
     out["slots"] = slots
     out["slots_total"] = us(T(30, 3), T(30, 4))
     out["finalize"] = us(T(30, 4), T(30, 5))

@@ -16,24 +16,41 @@ import os
 import sys
 
 
+def short_name(name: str) -> str:
+    """Kernel name without namespaces and parameter list.  (Round 4's version cut at the
+    first '(' BEFORE removing '(anonymous namespace)', so every kernel of psx's anonymous
+    namespaces collapsed into one row with an empty name: lanes_round_kernel averaged
+    with the 1-KB publish launch and the rest -- the inconsistent SQ_WAVES / MFMA rows.)"""
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "").replace("psx::", "")
+    return n.split("(")[0].strip() or name
+
+
 def load(root):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    """{kernel: {counter: [value per dispatch]}}, the rows of one dispatch (several
+    dimension instances, if the profiler splits them) summed first."""
+    per = collections.defaultdict(float)
+    grids = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
-            name = r.get("Kernel_Name", "?")
-            short = name.split("(")[0].replace("void ", "").replace("psx::", "")
-            acc[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return acc
+        for i, r in enumerate(csv.DictReader(open(f))):
+            k = short_name(r.get("Kernel_Name", "?"))
+            disp = (f, r.get("Dispatch_Id") or r.get("Correlation_Id") or str(i))
+            per[(k, disp, r["Counter_Name"])] += float(r["Counter_Value"])
+            if r.get("Grid_Size"):
+                grids[k] = r["Grid_Size"]
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, disp, c), v in per.items():
+        acc[k][c].append(v)
+    return acc, grids
 
 
 def main(argv):
     root = argv[0] if argv else "gpurun_out/pmc"
-    acc = load(root)
+    acc, grids = load(root)
     rows = []
     for k, cs in acc.items():
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         calls = max(len(v) for v in cs.values())
-        d = {"kernel": k, "dispatches": calls}
+        d = {"kernel": k, "dispatches": calls, "grid": grids.get(k, "")}
         if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and avg.get("SQ_BUSY_CYCLES"):
             d["mfma_busy_frac"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * avg["SQ_BUSY_CYCLES"])
         if avg.get("SQ_LDS_IDX_ACTIVE"):
@@ -52,7 +69,7 @@ def main(argv):
                 d[c] = avg[c]
         rows.append(d)
     rows.sort(key=lambda d: -d["dispatches"])
-    cols = ["kernel", "dispatches", "mfma_busy_frac", "lds_conflict", "wait_frac", "hbm_read_KB", "hbm_write_KB",
+    cols = ["kernel", "dispatches", "grid", "mfma_busy_frac", "lds_conflict", "wait_frac", "hbm_read_KB", "hbm_write_KB",
             "l2_hit", "SQ_INSTS_MFMA", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_WAVES", "SQ_INSTS_VMEM_RD",
             "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_LDS_UNALIGNED_STALL"]
     print("| " + " | ".join(cols) + " |")

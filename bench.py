@@ -86,7 +86,10 @@ def parse(argv=None):
                     help="logical workers per worker GPU, one XCD each in one launch per round (default 8: one "
                          "per XCD of the MI355X -- BASELINE's 8-worker configuration on one GPU; --workers 4 is the "
                          "reference's numWorkers = 4, all hosted in one process, BaseKafkaApp.java:25,70)")
-    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded", "keyrange"])
+    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer"],
+                    help="multi-GPU BSP: ... peer = sequential consistency over the peer data plane (the lanes "
+                         "store their deltas into the server GPU's inbox, the server kernel applies each on "
+                         "arrival and writes the weights into the workers' receive slots over xGMI)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--persist", action="store_true",
@@ -183,7 +186,7 @@ def _backend_label() -> str:
 
 
 def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, topo=None):
-    async_mode = a.consistency != 0
+    async_mode = a.consistency != 0 or cfg.bsp_schedule == "peer"
     n_workers = cfg.num_workers
     wpr = max(1, int(cfg.workers_per_rank))
     if a.model == "dense":
@@ -201,7 +204,7 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
         data = (f"synthetic sparse hashed bag-of-words ({a.train_rows} train / {a.test_rows} test rows, "
                 f"~48 nnz/row, random-init weights)")
         vs = None  # the reference never ran this configuration
-    mode = "asp" if a.consistency == -1 else ("ssp" if async_mode else "bsp")
+    mode = "asp" if a.consistency == -1 else ("ssp" if a.consistency > 0 else "bsp")
     backend = _backend_label()
     lanes = f"{wpr} workers/GPU, one XCD each" if wpr > 1 else "1 worker/GPU"
     if cfg.bsp_schedule == "keyrange":
@@ -209,6 +212,9 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
                f"range; pull/push of the window's ids over {backend if world > 1 else 'local copies'})")
     elif world == 1:
         par = f"ps-{mode} w{n_workers} (server colocated, {lanes if n_workers > 1 else '1 worker'})"
+    elif async_mode and wpr > 1:
+        par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers (peer data plane over xGMI: "
+               f"lanes -> server inbox, server kernel -> receive slots)")
     elif async_mode:
         par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
     elif not cfg.server_colocated:
@@ -320,6 +326,8 @@ def main(argv=None):
     res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),
                      "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2),
                      "host_phases_us": getattr(eng, "native_host_phases_us", None)}
+    if getattr(eng, "native_host_busy_us_per_token", None) is not None:  # SSP / ASP: the host loop's share
+        res["native"]["host_busy_us_per_token"] = round(eng.native_host_busy_us_per_token, 2)
     if "phases_ms" in out:  # where the timed region's wall clock went (host view)
         res["native"]["phases_ms"] = dict(out["phases_ms"], drain=round((t0 + dt - t_run) * 1e3, 3))
     rows = list(eng.log.book.server)
@@ -414,17 +422,20 @@ def bench_distributed(a):
     rank, world, device = init_from_env(cpu=a.cpu)
     if dist.get_world_size() != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
-    async_mode = a.consistency != 0
+    peer_bsp = a.consistency == 0 and a.schedule == "peer"
+    async_mode = a.consistency != 0 or peer_bsp  # (peer BSP: the asynchronous loops, sequential tracker)
     keyrange = a.schedule == "keyrange"
     dedicated = (async_mode or a.dedicated_server) and not keyrange  # key-range: every rank holds a shard
-    # workers per worker rank: BSP --workers lanes; SSP / ASP at most 7 lanes (the persistent
-    # asynchronous launch leaves one XCD to the RCCL p2p kernels beside it)
-    wpr = 1 if (a.model != "dense" or a.cpu) else (min(a.workers, 7) if async_mode else a.workers)
+    # workers per worker rank: --workers lanes, one XCD each (SSP / ASP / peer BSP: the lanes of one
+    # persistent launch; the peer data plane runs no transfer kernel beside it, so all 8 XCDs)
+    wpr = 1 if (a.model != "dense" or a.cpu) else a.workers
     worker_ranks = world - 1 if dedicated else world
     cfg = build_cfg(a, worker_ranks * wpr)
     cfg.workers_per_rank = wpr
     cfg.server_colocated = not dedicated
-    if not async_mode:
+    if peer_bsp:
+        cfg.bsp_schedule = "peer"
+    elif not async_mode:
         cfg.bsp_schedule = a.schedule if a.schedule != "reduce_bcast" or dedicated else "allreduce"
         if dedicated and cfg.bsp_schedule == "allreduce":
             cfg.bsp_schedule = "reduce_bcast"
@@ -459,7 +470,8 @@ def bench_distributed(a):
     rccl = comm.c.size if comm is not None else (dist.get_world_size() if dist.get_backend() == "nccl" else None)
     res = None
     topo = {"server_rank": 0 if dedicated else None, "worker_ranks": worker_ranks, "workers_per_rank": wpr,
-            "workers": cfg.num_workers, "schedule": cfg.bsp_schedule if not async_mode else "p2p",
+            "workers": cfg.num_workers,
+            "schedule": cfg.bsp_schedule if not async_mode else ("peer" if wpr > 1 else "p2p"),
             "native_lanes_loop": getattr(eng, "_lanes", None) is not None}
     if rank == 0:
         book = eng.log.book

@@ -836,6 +836,9 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.Xt = P<const uint16_t>(U("Xt"));
              c.yt = P<const int32_t>(U("yt"));
              c.T = (int)I("T", 0);
+             c.Ti = P<const uint16_t>(U("Ti"));
+             c.Tv = P<const uint16_t>(U("Tv"));
+             c.tnz = (int)I("tnz", 0);
              c.sink = U("sink");
              c.log_server = I("log_server", 1) != 0;
              c.log_workers = I("log_workers", 1) != 0;
@@ -894,6 +897,7 @@ PYBIND11_MODULE(_psx_hip, m) {
           py::arg("comm_stream"), py::arg("max_wait_s") = 600.0, py::arg("deadline_ms") = 0.0)
       .def_property_readonly("tickets", &LanesLoop::tickets)
       .def_property_readonly("host_us_per_update", &LanesLoop::host_us_per_update)
+      .def_property_readonly("host_busy_us_per_token", &LanesLoop::host_busy_us_per_token)
       .def("seen_at_solve", &LanesLoop::seen_at_solve)
       .def("set_seen_at_solve", &LanesLoop::set_seen_at_solve)
       .def("new_tuples_needed", &LanesLoop::new_tuples_needed)

@@ -163,18 +163,28 @@ __device__ __forceinline__ const T* fresh(const T* p) {
 // registers would spill in the resident form -- 192 B of scratch, 62.6k -> 58.0k
 // updates/s, profiles/r04/s19)
 template <int FP, int KP, int S, bool MT>
-__device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg, const AsyncArgs& a,
+__device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_mem, const AsyncArgs& a,
                                                 const AsyncLaneDev& A, int l, int wg, unsigned& run,
                                                 unsigned long long& relc, unsigned long long& lw) {
   constexpr int NS = FP / 32;
+  const SolverCfg& cfg = cfg_mem;  // (by value: 300 B of scratch, no faster -- profiles/r05/README.md)
   const int tid = threadIdx.x, K = cfg.K;
-  const SolveDev& dv = A.dv;
+  // The solver's pointers BY VALUE (registers), not a reference into the launch's device
+  // table: every spin loop's memory clobber and every acquire fence of the hand-offs
+  // would otherwise re-issue their loads -- a memory round trip ahead of each phase's
+  // data loads (measured: 78-96 us per solve by reference, 63-76 by value, against 56-66
+  // in the BSP round kernel, which holds its SolveDev by value; profiles/r05/README.md)
+  const SolveDev dv = A.dv;
   unsigned long long* const xch = dv.xch;
   unsigned long long* const err = xch + kXchErr;
   // ---- 1. the release record ----
   // (PSX_LANES_STAMPS, slot 30 of the lane's table: 0 released, 4 solved, 5 ticket,
   // 6 applied, 7 token out / evaluation starts, 8 evaluation done)
+  // (PSX_LANES_STAMPS: the iteration's start and the release record seen, kept as stamps 9
+  // / 10 of a real release -- the final stop record does not overwrite them)
+  const long long t_it = dv.dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.spin_rel, dv.err_host);
+  const long long t_rel = dv.dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   // The lane's sticky error word: a wait that timed out after the previous solve's
   // report (FinScal::store) -- its push (turn words, barriers) or its evaluation --
   // is reported here, then the word is cleared BEFORE the barrier every workgroup
@@ -198,6 +208,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
       report_and_clear(dv, err, run);  // (a wait of this iteration's barrier)
     }
     return false;
+  }
+  if (wg == 0 && tid == 0 && dv.dbg) {
+    dv.dbg[30 * 16 + 9] = t_it;
+    dv.dbg[30 * 16 + 10] = t_rel;
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
   // ---- 2. the solve (as lanes_round_kernel) ----
@@ -317,6 +331,14 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
   }
   ++run;
   if (wg == 0 && tid == 0) stamp(dv, 30, 4);
+  // the record's late fields again from the broadcast area (nothing but the window and
+  // the snapshot is kept live across the solve: registers for the solve's pointers)
+  {
+    TagChunk ch[kRelChunks];
+#pragma unroll
+    for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(A.rec + 2 * i);
+    unpack_release(ch, q);
+  }
   // ---- 3. push: ticket, serial slice updates, snapshot, token ----
   if (wg == 0 && tid == 0) {
     if (q.delay_us > 0) {  // injected straggler (tests): the solve "took" delay_us longer
@@ -362,8 +384,15 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg,
     pm.bslot = logl ? (char*)q.slot_s : nullptr;
     pm.bseq = q.seq_s;
     if (wg == 0 && tid == 0) stamp(dv, 30, 7);
-    lane_pair_eval<FP>(lds, K, a.Xt, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
+    if (dv.dbg && tid == 0 && wg < 32)  // (every workgroup's evaluation start: rows 26-27)
+      dv.dbg[(26 + (wg >> 4)) * 16 + (wg & 15)] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (a.tnz > 0)  // (the hashed bag-of-words test rows in ELL form: 1.3 instead of 10 MB per pass)
+      lane_pair_eval_ell<FP>(lds, K, a.Ti, a.Tv, a.tnz, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
+    else
+      lane_pair_eval<FP>(lds, K, a.Xt, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
     if (wg == 0 && tid == 0) stamp(dv, 30, 8);
+    if (dv.dbg && tid == 0 && wg < 32)  // (every workgroup's evaluation end: rows 24-25 of the table)
+      dv.dbg[(24 + (wg >> 4)) * 16 + (wg & 15)] = (long long)__builtin_amdgcn_s_memrealtime();
   }
   return true;
 }

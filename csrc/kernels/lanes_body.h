@@ -842,6 +842,51 @@ struct PairModels {
 };
 
 
+// The counts of a pair pass: this workgroup's LDS counts cl[2][256] into the lane's
+// accumulators, then the last of the G arrivals writes each row into its pinned slot as
+// tagged 16-B chunks (sink kind | kSinkTagged): no wait for the system-scope stores to
+// complete on the lane's path.
+__device__ __forceinline__ void pair_eval_publish(int* cl, int* lastp, int K, const PairModels& pm, int* acc,
+                                                  unsigned* ticket, int G, bool wrow, bool srow) {
+  const int tid = threadIdx.x;
+  for (int m = 0; m < 2; ++m) {
+    const int v = cl[m * 256 + tid];
+    if (v) atomicAdd(acc + (m * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1u;
+  __syncthreads();
+  if (!*lastp) return;
+  // the last workgroup: the lane's counts -> LDS [K][K], then tagged chunks to the slots
+  const int t16 = tid >> 4, p16 = tid & 15;
+  const bool cell = t16 < K && p16 < K;
+  for (int m = 0; m < 2; ++m) {
+    const int v = cell ? __hip_atomic_exchange(acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                       : 0;
+    if (cell) cl[m * 256 + t16 * K + p16] = v;
+  }
+  const float lv = (tid == 0 && wrow && pm.aloss) ? ld_h<2>(pm.aloss) : 0.f;
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int nch = 1 + (K * K + 2) / 3;
+  const int m = tid >> 6, i = tid & 63;  // wave 0: row A, wave 1: row B
+  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
+    const unsigned tag = eval_tag(m == 0 ? pm.aseq : pm.bseq);
+    TagChunk ch;
+    if (i == 0) {
+      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (i - 1);
+      auto cv = [&](int c) { return c < K * K ? (unsigned)cl[m * 256 + c] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    st_sys_chunk(m == 0 ? pm.aslot : pm.bslot, 1088u, (unsigned)i * 16u, ch);
+  }
+}
+
 // red_base: kPairEvalLds bytes of LDS (the logits' exchange, the counts)
 constexpr int kPairEvalLds = 8192 + 2 * 256 * 4 + 16 + 16 * 4;
 template <int FP>
@@ -934,48 +979,117 @@ __device__ __forceinline__ void lane_pair_eval_at(char* red_base, int K, const u
     }
     __syncthreads();
   }
-  for (int m = 0; m < 2; ++m) {
-    const int v = cl[m * 256 + tid];
-    if (v) atomicAdd(acc + (m * 256 + tid) * kAccStride, v);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    *lastp = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1u;
-  __syncthreads();
-  if (!*lastp) return;
-  // the last workgroup: the lane's counts -> LDS [K][K], then tagged chunks to the slots
-  const int t16 = tid >> 4, p16 = tid & 15;
-  const bool cell = t16 < K && p16 < K;
-  for (int m = 0; m < 2; ++m) {
-    const int v = cell ? __hip_atomic_exchange(acc + (m * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                       : 0;
-    if (cell) cl[m * 256 + t16 * K + p16] = v;
-  }
-  const float lv = (tid == 0 && wrow && pm.aloss) ? ld_h<2>(pm.aloss) : 0.f;
-  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int nch = 1 + (K * K + 2) / 3;
-  const int m = tid >> 6, i = tid & 63;  // wave 0: row A, wave 1: row B
-  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
-    const unsigned tag = eval_tag(m == 0 ? pm.aseq : pm.bseq);
-    TagChunk ch;
-    if (i == 0) {
-      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
-    } else {
-      const int c0 = 3 * (i - 1);
-      auto cv = [&](int c) { return c < K * K ? (unsigned)cl[m * 256 + c] : 0u; };
-      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
-    }
-    st_sys_chunk(m == 0 ? pm.aslot : pm.bslot, 1088u, (unsigned)i * 16u, ch);
-  }
+  pair_eval_publish(cl, lastp, K, pm, acc, ticket, G, wrow, srow);
 }
 // (the lane kernels: the exchange sits behind the row workgroups' 32-row tile image)
 template <int FP>
 __device__ __forceinline__ void lane_pair_eval(char* lds, int K, const uint16_t* Xt, const int32_t* yt, int T, int wg,
                                                int G, const PairModels& pm, int* acc, unsigned* ticket) {
   lane_pair_eval_at<FP>(lds + 32 * FP * 2, K, Xt, yt, T, wg, G, pm, acc, ticket);
+}
+
+
+// The same pair pass over the test set in ELL form (EvalSet.ell: [T][nz] feature ids +
+// bf16 values, nz a multiple of 8; the hashed bag-of-words rows are ~3 % dense, so 1.3 MB
+// instead of the 10 MB dense tiles): both models' weights w = hi + lo (exact in fp32)
+// staged into LDS feature-major, [model][FP][8 classes] (one feature's classes = two
+// 16-B LDS reads), then one thread per row -- z_c = b_c + sum_j x_j w_c[id_j] in feature
+// order -- and the argmax counts.  Every product x * w is exact as in the MFMA form (8 x
+// 16 significant bits); only the summation order differs.
+// LDS: ell_eval_lds_bytes(FP).
+constexpr size_t ell_eval_lds_bytes(int FP) { return (size_t)2 * 8 * FP * 4 + 2 * 256 * 4 + 16 + 16 * 4; }
+template <int FP>
+__device__ __forceinline__ void lane_pair_eval_ell(char* lds, int K, const uint16_t* Ti, const uint16_t* Tv, int nz,
+                                                   const int32_t* yt, int T, int wg, int G, const PairModels& pm,
+                                                   int* acc, unsigned* ticket) {
+  const int tid = threadIdx.x;
+  const bool wrow = pm.aslot != nullptr, srow = pm.bslot != nullptr;
+  if (!wrow && !srow) return;  // (uniform)
+  float* wl = (float*)lds;                         // [2][FP][8]
+  int* cl = (int*)(lds + (size_t)2 * 8 * FP * 4);  // [2][256]
+  int* lastp = cl + 512;
+  float* bl = (float*)(lastp + 4);  // [16]: model A 0..7, model B 8..15
+  cl[tid] = 0;
+  cl[256 + tid] = 0;
+  constexpr int NCH = FP / 8;  // 8-feature chunks of a fragment column
+  // thread -> (model, chunk of 8 features): every class column of that chunk (hi + lo)
+  for (int i = tid; i < 2 * NCH; i += 256) {
+    const int m = i / NCH, ch = i - m * NCH;
+    const bool mine = m == 0 ? wrow : srow;
+    const int co = m == 0 ? pm.acoff : pm.bcoff;
+    float v[8][8];  // [class][feature in chunk]
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bool live = mine && c < K;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+      if (live) {
+        const size_t o = ((size_t)ch * 16 + co + c) * 8;
+        const u16x8 h = __builtin_nontemporal_load((const u16x8*)((m == 0 ? pm.ah : pm.bh) + o));
+        const u16x8 l = __builtin_nontemporal_load((const u16x8*)((m == 0 ? pm.al : pm.bl) + o));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(h[j]) + bf2f(l[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float* dst = wl + ((size_t)m * FP + ch * 8 + j) * 8;
+      *(f32x4*)dst = f32x4{v[0][j], v[1][j], v[2][j], v[3][j]};
+      *(f32x4*)(dst + 4) = f32x4{v[4][j], v[5][j], v[6][j], v[7][j]};
+    }
+  }
+  if (tid < 16) {
+    const int cc = tid & 7;
+    const bool live = cc < K && (tid < 8 ? wrow : srow);
+    bl[tid] = live ? ld_h<2>((tid < 8 ? pm.ab + pm.acoff : pm.bb + pm.bcoff) + cc) : 0.f;
+  }
+  __syncthreads();
+  const f32x4* wv = (const f32x4*)wl;
+  // a contiguous block of rows per workgroup (every workgroup busy: 4,877 rows over 32
+  // workgroups, not 256-row blocks over the first 19), a thread per row
+  const int per = (T + G - 1) / G, r1 = (wg + 1) * per < T ? (wg + 1) * per : T;
+  for (int r = wg * per + tid; r < r1; r += 256) {
+    f32x4 a0 = f32x4{bl[0], bl[1], bl[2], bl[3]}, a1 = f32x4{bl[4], bl[5], bl[6], bl[7]};
+    f32x4 b0 = f32x4{bl[8], bl[9], bl[10], bl[11]}, b1 = f32x4{bl[12], bl[13], bl[14], bl[15]};
+    const uint16_t* ip = Ti + (size_t)r * nz;
+    const uint16_t* vp = Tv + (size_t)r * nz;
+    for (int q = 0; q < nz; q += 8) {
+      const u16x8 iv = *(const u16x8*)(ip + q);
+      const u16x8 vv = *(const u16x8*)(vp + q);
+      if (vv[0] == 0) break;  // (the row's nonzeros come first: the rest is padding)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = bf2f(vv[j]);
+        const int f = iv[j];
+        a0 += x * wv[f * 2];
+        a1 += x * wv[f * 2 + 1];
+        b0 += x * wv[(FP + f) * 2];
+        b1 += x * wv[(FP + f) * 2 + 1];
+      }
+    }
+    const int y = yt[r];
+    const int yl = y < 0 ? 0 : (y > 15 ? 15 : y);
+    const float za[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    const float zb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    int ba = 0, bb = 0;
+    float za_best = -INFINITY, zb_best = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < K) {
+        if (za[c] > za_best) {
+          za_best = za[c];
+          ba = c;
+        }
+        if (zb[c] > zb_best) {
+          zb_best = zb[c];
+          bb = c;
+        }
+      }
+    if (wrow) atomicAdd(&cl[yl * 16 + ba], 1);
+    if (srow) atomicAdd(&cl[256 + yl * 16 + bb], 1);
+  }
+  __syncthreads();
+  pair_eval_publish(cl, lastp, K, pm, acc, ticket, G, wrow, srow);
 }
 
 }  // namespace lanes_detail

@@ -331,6 +331,11 @@ struct AsyncArgs {
   const uint16_t* Xt;  // test set
   const int32_t* yt;
   int T;
+  // the test set in ELL form (EvalSet.ell: [T][tnz] feature ids + bf16 values); tnz == 0:
+  // the dense MFMA pass over Xt
+  const uint16_t* Ti;
+  const uint16_t* Tv;
+  int tnz;
   int log_lane;        // lane whose deltas produce server rows (-1: none)
   long long launch;    // launch number (> every earlier one): lane-wide barrier words
   int spin_rel;        // release wait budget (polls)

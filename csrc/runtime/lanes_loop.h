@@ -65,6 +65,11 @@ struct LanesLoopCfg {
   const uint16_t* Xt = nullptr;
   const int32_t* yt = nullptr;
   int T = 0;
+  // the test set in ELL form (psx/ops/lr.py EvalSet.ell), used by the asynchronous lanes'
+  // evaluation; tnz == 0: the dense pass
+  const uint16_t* Ti = nullptr;
+  const uint16_t* Tv = nullptr;
+  int tnz = 0;
   uintptr_t sink = 0;       // MetricsSink* (0: no rows)
   bool log_server = true;   // server rows on this rank
   bool log_workers = true;  // worker rows on this rank
@@ -156,6 +161,9 @@ class LanesLoop {
   void prepare_async() { ensure_async(); }
   int64_t tickets() const { return (int64_t)aticket_; }  // deltas applied by the asynchronous loop so far
   double host_us_per_update() const { return async_updates_ ? async_ns_ / 1000.0 / (double)async_updates_ : 0.0; }
+  // host time spent per consumed token (token seen -> its rows handed over, tracker, the
+  // releases it triggers written): the host loop's share of an asynchronous update
+  double host_busy_us_per_token() const { return tok_n_ ? tok_ns_ / 1000.0 / (double)tok_n_ : 0.0; }
   // Evaluate the last round's rows (one launch of riders only).
   void flush(hipStream_t stream);
   void set_sink(uintptr_t sink) { cfg_.sink = sink; }
@@ -356,6 +364,8 @@ class LanesLoop {
   hipEvent_t aev_in_ = nullptr, aev_out_ = nullptr;
   int64_t async_updates_ = 0;
   double async_ns_ = 0.0;
+  int64_t tok_n_ = 0;
+  double tok_ns_ = 0.0;
 };
 
 }  // namespace psx

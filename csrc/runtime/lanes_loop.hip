@@ -1023,6 +1023,9 @@ void LanesLoop::ensure_async() {
   a.Xt = cfg_.Xt;
   a.yt = cfg_.yt;
   a.T = cfg_.T;
+  a.Ti = cfg_.Ti;
+  a.Tv = cfg_.Tv;
+  a.tnz = (cfg_.Ti && cfg_.Tv && cfg_.tnz > 0 && cfg_.tnz % 8 == 0) ? cfg_.tnz : 0;
   a.spin_rel = 1 << 24;  // ~30 s of polls: the host answers every release
   a.claim = claim_;
   relc_.assign(L, 0);
@@ -1294,6 +1297,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
       AsyncToken tk;
       std::memcpy(&tk, &v, 16);
       if (tk.tag == (unsigned)next) {
+        const int64_t tk0 = steady_ns();
         std::atomic_thread_fence(std::memory_order_acquire);
         const int l = (int)tk.a;
         const int64_t vc = (int64_t)(((uint64_t)tk.c << 32) | tk.b);
@@ -1326,6 +1330,8 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
         start_ready(epoch_ms() - cfg_.t0_ms);
         idle_spins = 0;
         wait0 = epoch_ms();
+        ++tok_n_;
+        tok_ns_ += (double)(steady_ns() - tk0);
         continue;
       }
       if (running > 0) {  // solves in flight: spin for their tokens

@@ -109,7 +109,11 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--async_scheduler", default="auto", choices=["auto", "events", "threads"],
                    help="--inprocess SSP/ASP: one host thread polling the workers' HIP events, or a thread "
                         "per worker (auto: events on a GPU unless a delay is injected)")
-    g.add_argument("--bsp_schedule", default="reduce_bcast", choices=["allreduce", "reduce_bcast", "sharded", "keyrange"])
+    g.add_argument("--bsp_schedule", default="reduce_bcast",
+                   choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer"],
+                   help="multi-rank Sequential consistency: RCCL all-reduce / reduce + broadcast / reduce-scatter + "
+                        "all-gather, the key-range server, or peer = the lanes push into the server GPU's inbox "
+                        "and pull from their receive slots over xGMI (--workers_per_rank > 1)")
     g.add_argument("--workers_per_rank", type=int, default=1,
                    help="multi-rank BSP on GPUs: logical workers per worker rank, one XCD each in one launch per "
                         "round (the native lanes loop)")

@@ -7,6 +7,8 @@ same ops run the PyTorch reference in :mod:`psx.models.reference`.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -226,6 +228,37 @@ class EvalSet:
         self.y = y.to(self.device, torch.int32).contiguous()
         self.T = int(self.X.shape[0])
         self._Xf = None
+        self.ell_idx = self.ell_val = None
+        self.ell_nz = 0
+        self._build_ell()
+
+    def _build_ell(self, max_nz: int = 128):
+        """The test rows in ELL form for the evaluation passes that read the whole set per
+        update (the asynchronous lanes): [T][nz] feature ids (int16) + bf16 values, nonzeros
+        first in feature order, nz = the longest row rounded up to 8.  The hashed
+        bag-of-words rows of the reference's data are sparse (the reference itself builds
+        Vectors.sparse rows, LogisticRegressionTaskSpark.java:146-162): ~34 of 1,024 in the
+        synthetic set, 1.3 MB instead of 10 MB per pass.  Only when nz <= max_nz and the
+        rows are at most 1/4 dense (PSX_SPARSE_EVAL=0: never)."""
+        if not is_gpu(self.device) or self.T == 0 or os.environ.get("PSX_SPARSE_EVAL", "1") == "0":
+            return
+        mask = self.X != 0
+        mx = int(mask.sum(1).max().item())
+        nz = max(8, (mx + 7) // 8 * 8)
+        if nz > max_nz or 4 * nz > self.spec.Fp:
+            return
+        order = torch.argsort((~mask).to(torch.int8), dim=1, stable=True)[:, :nz]
+        keep = torch.gather(mask, 1, order)
+        self.ell_idx = torch.where(keep, order, torch.zeros_like(order)).to(torch.int16).contiguous()
+        self.ell_val = torch.where(keep, torch.gather(self.X, 1, order), torch.zeros((), dtype=self.X.dtype,
+                                                                                   device=self.device)).contiguous()
+        self.ell_nz = nz
+
+    def ell_args(self) -> dict:
+        """The native loops' ELL arguments (tnz 0: the dense pass)."""
+        if self.ell_idx is None:
+            return {}
+        return {"Ti": self.ell_idx.data_ptr(), "Tv": self.ell_val.data_ptr(), "tnz": int(self.ell_nz)}
 
     def confusion_async(self, frag: Fragments | None, w: torch.Tensor, out: torch.Tensor):
         """Write the [16,16] confusion counts of model ``w`` into ``out`` (int32)."""

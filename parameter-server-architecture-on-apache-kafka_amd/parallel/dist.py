@@ -193,7 +193,13 @@ class DistEngine:
 
     def __init__(self, cfg: PSConfig, rank: int, world: int, device, train=None, test=None):
         self.cfg, self.rank, self.world, self.device = cfg, rank, world, torch.device(device)
-        self.async_mode = cfg.consistency_model != 0
+        # bsp_schedule "peer": sequential consistency through the asynchronous loops of the
+        # peer data plane -- the server applies each delta on arrival (ServerProcessor.java:
+        # 148-151) and the sequential tracker (MessageTracker.java:111-120 semantics) answers
+        # every worker once the round is complete; no collective, so nothing serialises the
+        # worker ranks' persistent launches behind a reduce / broadcast
+        self.peer_bsp = cfg.consistency_model == 0 and cfg.bsp_schedule == "peer"
+        self.async_mode = cfg.consistency_model != 0 or self.peer_bsp
         self.dedicated = self.async_mode or not cfg.server_colocated
         wpr = max(1, int(cfg.workers_per_rank))
         n_worker_ranks = world - 1 if self.dedicated else world
@@ -819,11 +825,13 @@ class DistEngine:
         lanes write their deltas into the server GPU's inbox and the server kernel
         writes the weights into their receive slots over xGMI.  Agreed collectively."""
         if not (self.async_mode and self.wpr > 1) or self.wide or self.cfg.async_plane == "host":
+            if self.peer_bsp:
+                raise ValueError("--bsp_schedule peer: several dense workers per worker rank on GPUs")
             return False
         flags = [None] * self.world
         dist.all_gather_object(flags, bool(is_gpu(self.device)))
         ok = all(flags)
-        if self.cfg.async_plane == "peer" and not ok:
+        if (self.cfg.async_plane == "peer" or self.peer_bsp) and not ok:
             raise ValueError("--async_plane peer: every rank (the server too) must be on a GPU")
         return ok
 
@@ -1095,6 +1103,7 @@ class DistEngine:
                      # transfer kernel runs beside the persistent launch: the pushes / pulls are the
                      # lanes' own stores (peer plane) or host staging by the DMA engines)
                      xcd0=(self.worker_id * len(W)) if oversubscribed() else 0)
+            d.update(ev.ell_args())
             lp = h.LanesLoop(d, None)
             self._alanes = lp
         return lp

@@ -65,7 +65,9 @@ class PSConfig:
     log_dir: str = "."
     verbose: bool = False
     # distributed
-    bsp_schedule: str = "allreduce"  # allreduce | reduce_bcast | sharded | keyrange (wide: sharded == keyrange)
+    # allreduce | reduce_bcast | sharded | keyrange (wide: sharded == keyrange) | peer (dense, several
+    # workers per rank: the sequential tracker over the peer data plane, csrc/comm/peer_bus.h)
+    bsp_schedule: str = "allreduce"
     server_colocated: bool = True
     # logical workers per worker rank (one XCD each: the multi-lane round loop);
     # the reference hosts all of its workers in one process (BaseKafkaApp.java:25,70)

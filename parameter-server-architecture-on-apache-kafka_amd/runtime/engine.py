@@ -316,6 +316,7 @@ class LocalEngine:
                  # (ServerProcessor.java:154), straggler delays on the device
                  log_worker=min(w.k for w in W),
                  delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W])
+        d.update(ev.ell_args())  # (the asynchronous lanes' evaluation reads the sparse test rows)
         lp = h.LanesLoop(d, None)
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
@@ -497,6 +498,7 @@ class LocalEngine:
             if w.ring.XT is not None:
                 w.ring.xt_stale = True
         self.native_host_us_per_round = float(lp.host_us_per_update)
+        self.native_host_busy_us_per_token = float(lp.host_busy_us_per_token)
         elapsed = time.time() - t_start
         self.rounds = int(srv.tracker.min_clock())
         return {"rounds": self.rounds, "updates": srv.updates, "elapsed_s": elapsed,

@@ -15,6 +15,11 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
+    if mode == "peer_bsp":  # sequential consistency over the peer data plane: 1 GPU server + ranks x 3 lanes
+        return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,
+                        stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=6, min_buffer_size=128,
+                        max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3,
+                        bsp_schedule="peer", worker_timeout_s=25.0)
     if mode.startswith("async") or mode.startswith("peer"):
         # SSP(2) / ASP: 1 server rank + worker ranks x 3 lanes -- async_*: a CPU server and
         # the host shared-memory data plane; peer_*: a GPU server rank and the peer data

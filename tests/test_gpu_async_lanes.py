@@ -94,9 +94,11 @@ def test_async_lanes_gap_with_straggler(cuda, c, bound):
         assert gap >= 4, gap  # eventual: the fast workers are not held back by worker 2
 
 
-def test_async_one_lane_equals_bsp_lanes_bitwise(cuda):
+def test_async_one_lane_equals_bsp_lanes_bitwise(cuda, monkeypatch):
     """One lane: the asynchronous update w += lr * delta is the BSP lanes loop's
-    update of a one-worker round -- weights and rows bit for bit."""
+    update of a one-worker round -- weights and rows bit for bit (both evaluating with
+    the dense MFMA pass: PSX_SPARSE_EVAL=0)."""
+    monkeypatch.setenv("PSX_SPARSE_EVAL", "0")
     outs = []
     for mode in ("bsp", "async"):
         eng = _engine(cuda, -1, workers=1, iters=6)
@@ -203,3 +205,27 @@ def test_async_lanes_replay_float64_oracle(cuda, c):
         f1r, accr = metrics_from_confusion(confusion(yt.numpy(), pred.numpy(), spec.K))
         assert abs(f1 - f1r) <= 2e-3 and abs(acc - accr) <= 2e-3, (t, f1, f1r, acc, accr)
     print(f"replay c={c}: worst delta rel err {worst:.2e}, float64 chain max |dw| {chain:.2e}")
+
+
+def test_async_sparse_eval_rows_equal_dense(cuda, monkeypatch):
+    """The asynchronous lanes' evaluation over the ELL test rows (EvalSet.ell,
+    lanes_body.h lane_pair_eval_ell) against the dense MFMA pass: the same training
+    (weights bit for bit: the evaluation does not feed back) and the same rows -- every
+    product x * w is exact in both, only the summation order differs, so at most an
+    argmax tie flips (counts within 2 of 4,877)."""
+    outs = []
+    for sp in ("0", "1"):
+        monkeypatch.setenv("PSX_SPARSE_EVAL", sp)
+        eng = _engine(cuda, -1, workers=1, iters=6)  # (one worker: a deterministic schedule)
+        assert (eng.evalset.ell_nz > 0) == (sp == "1")
+        eng.run(close_log=False)
+        eng.log.drain(block=True)
+        torch.cuda.synchronize()
+        outs.append((eng.server.w.clone(), sorted((r[1], r[2], r[4], r[5]) for r in eng.log.book.worker),
+                     sorted((-1, r[1], r[2], r[3]) for r in eng.log.book.server)))
+        eng.log.close()
+    (wa, ra, sa), (wb, rb, sb) = outs
+    assert torch.equal(wa, wb)
+    assert len(ra) == len(rb) == 6 and len(sa) == len(sb)
+    for a, b in zip(ra + sa, rb + sb):
+        assert a[:2] == b[:2] and all(abs(x - y) <= 2 / 4877 + 1e-6 for x, y in zip(a[2:], b[2:])), (a, b)

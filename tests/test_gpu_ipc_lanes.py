@@ -161,3 +161,41 @@ def test_peer_plane_gpu_server_two_worker_ranks(cuda, tmp_path, mode, bound):
     assert srv["host_us_per_update"] <= 10.0, srv["host_us_per_update"]
     w = torch.load(os.path.join(tmp_path, f"w_{mode}.pt"), weights_only=True)
     assert torch.isfinite(w).all()
+
+
+def test_peer_plane_bsp_equals_in_process_engine(cuda, tmp_path):
+    """Sequential consistency over the peer data plane (--bsp_schedule peer): 1 GPU
+    server rank + 2 worker ranks x 3 lanes, no collective -- the server kernel applies
+    each delta on arrival (ServerProcessor.java:148-151) and the sequential tracker
+    releases every worker once the round is complete (MessageTracker.java:69-87).
+    The weights equal one process hosting the same 6 workers in the BSP lanes loop
+    (the same deltas, summed in another order), one server row per round."""
+    res = _launch(tmp_path, "peer_bsp", world=3, timeout=150)
+    srv = res[0]
+    assert srv.get("data_plane") == "peer", srv
+    assert srv["updates"] == 6 * 6, srv["updates"]
+    gap = _replay_arrivals(srv["arrivals"], 6, 0)
+    assert gap <= 1 and srv["max_vc_gap"] <= 1, (gap, srv["max_vc_gap"])
+    w_peer = torch.load(os.path.join(tmp_path, "w_peer_bsp.pt"), weights_only=True)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _ipc_rank import cfg_for
+
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    cfg = cfg_for(3, "peer_bsp")
+    cfg.server_colocated, cfg.bsp_schedule, cfg.workers_per_rank = True, "allreduce", 1
+    eng = LocalEngine(cfg, cuda, train=synth_finefood(20000, seed=0), test=synth_finefood(4877, seed=1))
+    out = eng.run(close_log=False)
+    eng.log.drain(block=True)
+    assert out.get("lanes") == 6, out
+    w_loc = eng.server.w.detach().cpu()
+    assert torch.allclose(w_peer, w_loc, rtol=2e-4, atol=2e-4), (w_peer - w_loc).abs().max().item()
+    # (a server row follows worker 0's delta as the reference's does -- right after THAT
+    # update, the round's other deltas may still be on their way: the same clocks, not
+    # the same model as the lanes loop's row after the whole round)
+    rows_peer = srv["server_rows"]
+    rows_loc = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
+    assert len(rows_peer) == len(rows_loc) == 6
+    assert [a[0] for a in rows_peer] == [b[0] for b in rows_loc]
+    assert all(a[1] > 0.2 for a in rows_peer[2:]), rows_peer

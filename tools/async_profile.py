@@ -15,6 +15,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def main():
@@ -50,8 +51,19 @@ def main():
             st = lp.read_stamps(l, stream_handle("cuda:0"))
             T = lambda k: st[30 * 16 + k]
             us = lambda x, y: round((T(y) - T(x)) / 100.0, 2) if T(x) and T(y) else None
-            lanes.append({"solve": us(0, 4), "ticket": us(4, 5), "apply": us(5, 6),
-                          "token": us(6, 7), "eval": us(7, 8)})
+            ln = {"solve": us(0, 4), "ticket": us(4, 5), "apply": us(5, 6), "token": us(6, 7), "eval": us(7, 8),
+                  # the last iteration's start: release record seen, the lane-wide barrier
+                  "wait_release": us(9, 10), "barrier": us(10, 0)}
+            # the solve's slots (the same stamps as the BSP round kernel: tools/lanes_profile.py)
+            from lanes_profile import phases
+            ends = [st[(24 + (w >> 4)) * 16 + (w & 15)] for w in range(32)]
+            starts = [st[(26 + (w >> 4)) * 16 + (w & 15)] for w in range(32)]
+            if all(ends) and all(starts) and T(7):
+                ln["eval_wg_start_us"] = [round((x - T(7)) / 100.0, 2) for x in (min(starts), max(starts))]
+                ln["eval_wg_end_us"] = [round((x - T(7)) / 100.0, 2) for x in (min(ends), max(ends))]
+            ph = phases(st)
+            ln["slots"] = ph.get("slots")
+            lanes.append(ln)
         res["last_update_us"] = lanes
     eng.log.close()
     print(json.dumps(res))

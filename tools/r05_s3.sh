@@ -11,3 +11,4 @@ export PSX_LANES_OVERLAP=0 PMC_STEPS=150
 bash tools/pmc_profile.sh > $O/pmc.log 2>&1; rc=$?; echo "pmc rc=$rc"; cat $O/pmc.log
 mv gpurun_out/pmc $O/pmc_serial 2>/dev/null
 python tools/pmc_summary.py $O/pmc_serial > $O/pmc_summary.md; head -5 $O/pmc_summary.md
+PSX_LANES_STAMPS=1 timeout -k 10 120 python tools/async_profile.py --consistency -1 --iters 300 > $O/async_profile.json 2> $O/async_profile.err; echo "async profile rc=$?"

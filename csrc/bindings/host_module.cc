@@ -190,6 +190,7 @@ PYBIND11_MODULE(_psx_host, m) {
       .def("unlink", &CtrlQueue::unlink)
       .def_property_readonly("capacity", &CtrlQueue::capacity)
       .def_property_readonly("name", &CtrlQueue::name)
+      .def("state", [](const CtrlQueue& q) { return py::make_tuple(q.enqueued(), q.dequeued(), q.inode()); })
       .def_property_readonly("handle", [](CtrlQueue& q) { return reinterpret_cast<uintptr_t>(&q); });
 
   // Host build of the device solver state machine (csrc/kernels/solver_ctrl.h),

@@ -64,6 +64,10 @@ CtrlQueue::CtrlQueue(const std::string& name, uint32_t capacity, bool create) : 
       std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
   }
+  {
+    struct stat st;
+    if (fstat(fd, &st) == 0) ino_ = (uint64_t)st.st_ino;
+  }
   base_ = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   ::close(fd);
   if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed for " + name);

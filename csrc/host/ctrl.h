@@ -46,6 +46,10 @@ class CtrlQueue {
   uint32_t capacity() const;
   const std::string& name() const { return name_; }
   void unlink();
+  // (diagnostics) tokens pushed / popped so far and the segment's inode
+  uint64_t enqueued() const { return hdr_->enq.load(std::memory_order_relaxed); }
+  uint64_t dequeued() const { return hdr_->deq.load(std::memory_order_relaxed); }
+  uint64_t inode() const { return ino_; }
 
  private:
   struct Slot {
@@ -62,6 +66,7 @@ class CtrlQueue {
   std::string name_;
   bool owner_;
   size_t bytes_ = 0;
+  uint64_t ino_ = 0;
   void* base_ = nullptr;
   Header* hdr_ = nullptr;
   Slot* slots_ = nullptr;

@@ -35,17 +35,18 @@ __device__ __forceinline__ TagChunk ld_nt_chunk(const void* p) {
 // A record is complete when its 8 chunks carry one tag; it is new when that tag
 // is at least the one the lane expects (a stop record written over an unread
 // release on the host's error path is newer still).
-__device__ __forceinline__ void leader_wait_release(const AsyncLaneDev& A, unsigned want, int spin_max,
+__device__ __forceinline__ void leader_wait_release(const AsyncLaneDev& A, unsigned want, long long ticks,
                                                     unsigned long long* err_host) {
   const int tid = threadIdx.x;
   if (tid >= 64) return;
   TagChunk c = TagChunk{0, 0, 0, 0};
   bool ok = false;
-  for (int spins = 0;; ++spins) {
+  const long long t_end = rt_now() + ticks;
+  for (;;) {
     if (tid < kRelChunks) c = ld_sys_chunk(A.rel, (unsigned)sizeof(AsyncRelease), (unsigned)tid * 16u);
     const unsigned t0 = __shfl(c.tag, 0, 64);
     ok = __all(tid >= kRelChunks || c.tag == t0) && (int)(t0 - want) >= 0;
-    if (ok || spins >= spin_max) break;
+    if (ok || rt_now() > t_end) break;
     __builtin_amdgcn_s_sleep(8);
   }
   if (!ok) {  // the host never answered: leave the launch, and say so
@@ -183,14 +184,18 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   // (PSX_LANES_STAMPS: the iteration's start and the release record seen, kept as stamps 9
   // / 10 of a real release -- the final stop record does not overwrite them)
   const long long t_it = dv.dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-  if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.spin_rel, dv.err_host);
+  if (wg == 0) leader_wait_release(A, (unsigned)(relc + 1), a.rel_ticks, dv.err_host);
   const long long t_rel = dv.dbg ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
   // The lane's sticky error word: a wait that timed out after the previous solve's
   // report (FinScal::store) -- its push (turn words, barriers) or its evaluation --
   // is reported here, then the word is cleared BEFORE the barrier every workgroup
   // of this iteration passes, so nothing stored in this iteration is wiped.
   if (wg == 0 && tid == 0) report_and_clear(dv, err, run);
-  x_barrier(A.flags, wg, kLaneWg, ++lw, err, a.spin_rel);
+  // (only the leader publishes through this barrier -- the release record; the others'
+  // outstanding stores, e.g. the last evaluation's pinned-slot chunks, need not land first)
+  // (no budget of their own for the others: the leader's release wait is bounded and
+  // ends in a stop record)
+  x_barrier(A.flags, wg, kLaneWg, ++lw, err, 0x7fffffff, /*drain=*/wg == 0);
   // the lane's rows, state and the pulled snapshot were written by other CUs
   // (other XCDs for the snapshot) since this CU last read them
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -248,9 +253,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
           // pull, acquire, read the slice with system-scope loads
           if (tid == 0) {
             const unsigned* tg = a.snap_tag + (size_t)(q.snap % (long long)a.R) * NS + wg;
-            int spins = 0;
-            while ((int)(ld_sys_u32(tg) - q.pull_tag) < 0 && ++spins <= a.spin_rel) __builtin_amdgcn_s_sleep(2);
-            if (spins > a.spin_rel) xstore(err, 10ull);  // the server's weights never arrived
+            const long long t_end = rt_now() + a.rel_ticks;
+            bool late = false;
+            while ((int)(ld_sys_u32(tg) - q.pull_tag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
+            if (late) xstore(err, 10ull);  // the server's weights never arrived
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
           }
           __syncthreads();
@@ -387,7 +393,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
     if (dv.dbg && tid == 0 && wg < 32)  // (every workgroup's evaluation start: rows 26-27)
       dv.dbg[(26 + (wg >> 4)) * 16 + (wg & 15)] = (long long)__builtin_amdgcn_s_memrealtime();
     if (a.tnz > 0)  // (the hashed bag-of-words test rows in ELL form: 1.3 instead of 10 MB per pass)
-      lane_pair_eval_ell<FP>(lds, K, a.Ti, a.Tv, a.tnz, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
+      lane_pair_eval_ell<FP>(lds, K, a.Ti, a.Tv, a.tnz, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket, A.eslab);
     else
       lane_pair_eval<FP>(lds, K, a.Xt, a.yt, a.T, wg, kLaneWg, pm, A.acc, A.eticket);
     if (wg == 0 && tid == 0) stamp(dv, 30, 8);

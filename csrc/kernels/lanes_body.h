@@ -51,6 +51,11 @@ __device__ __forceinline__ void st_sys_chunk(void* base, unsigned bytes, unsigne
 // is payload stores -> s_waitcnt vmcnt(0) -> barrier -> one lane: release fence
 // (system) + tag store; the reader polls the tag, acquires (system), then loads.
 typedef __attribute__((address_space(1))) unsigned g_u32;
+// Wall-clock budgets of the cross-device waits (another process answers them, so a
+// poll count would make the budget depend on the poll's latency): s_memrealtime
+// is the constant 100 MHz clock.
+constexpr long long kRtTicksPerS = 100000000ll;
+__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ unsigned ld_sys_u32(const unsigned* p) {
   asm volatile("" ::: "memory");  // a spin re-reads
   return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -887,6 +892,51 @@ __device__ __forceinline__ void pair_eval_publish(int* cl, int* lastp, int K, co
   }
 }
 
+// The slab form of pair_eval_publish (no device-scope atomics): each workgroup stores its
+// K x K counts of both models into its row of `slab` [G][2][64] ints, arrives on the
+// ticket, and the last one sums the G rows in workgroup order (nt loads: the lane's
+// workgroups share one XCD's L2) and publishes the rows as tagged chunks.
+__device__ __forceinline__ void pair_eval_publish_slab(int* cl, int* lastp, int K, const PairModels& pm, int* slab,
+                                                       unsigned* ticket, int wg, int G, bool wrow, bool srow) {
+  const int tid = threadIdx.x, KK = K * K;
+  if (tid < 128) {
+    const int m = tid >> 6, c = tid & 63;
+    slab[(size_t)wg * 128 + tid] = c < KK ? cl[m * 256 + (c / K) * 16 + (c - (c / K) * K)] : 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *lastp = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1u;
+  __syncthreads();
+  if (!*lastp) return;
+  if (tid < 128) {
+    int v[kLaneWg];
+#pragma unroll
+    for (int g = 0; g < kLaneWg; ++g) v[g] = g < G ? __builtin_nontemporal_load(slab + (size_t)g * 128 + tid) : 0;
+    int t = 0;
+#pragma unroll
+    for (int g = 0; g < kLaneWg; ++g) t += v[g];
+    cl[(tid >> 6) * 256 + (tid & 63)] = t;  // [model][cell k = true * K + pred]
+  }
+  const float lv = (tid == 0 && wrow && pm.aloss) ? ld_h<2>(pm.aloss) : 0.f;
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int nch = 1 + (KK + 2) / 3;
+  const int m = tid >> 6, i = tid & 63;  // wave 0: row A, wave 1: row B
+  if (m < 2 && i < nch && (m == 0 ? wrow : srow)) {
+    const unsigned tag = eval_tag(m == 0 ? pm.aseq : pm.bseq);
+    TagChunk ch;
+    if (i == 0) {
+      ch = TagChunk{tag, __float_as_uint(m == 0 ? __shfl(lv, 0, 64) : 0.f), (unsigned)K, 0u};
+    } else {
+      const int c0 = 3 * (i - 1);
+      auto cv = [&](int c) { return c < KK ? (unsigned)cl[m * 256 + c] : 0u; };
+      ch = TagChunk{tag, cv(c0), cv(c0 + 1), cv(c0 + 2)};
+    }
+    st_sys_chunk(m == 0 ? pm.aslot : pm.bslot, 1088u, (unsigned)i * 16u, ch);
+  }
+}
+
 // red_base: kPairEvalLds bytes of LDS (the logits' exchange, the counts)
 constexpr int kPairEvalLds = 8192 + 2 * 256 * 4 + 16 + 16 * 4;
 template <int FP>
@@ -1001,7 +1051,7 @@ constexpr size_t ell_eval_lds_bytes(int FP) { return (size_t)2 * 8 * FP * 4 + 2 
 template <int FP>
 __device__ __forceinline__ void lane_pair_eval_ell(char* lds, int K, const uint16_t* Ti, const uint16_t* Tv, int nz,
                                                    const int32_t* yt, int T, int wg, int G, const PairModels& pm,
-                                                   int* acc, unsigned* ticket) {
+                                                   int* acc, unsigned* ticket, int* slab = nullptr) {
   const int tid = threadIdx.x;
   const bool wrow = pm.aslot != nullptr, srow = pm.bslot != nullptr;
   if (!wrow && !srow) return;  // (uniform)
@@ -1089,7 +1139,10 @@ __device__ __forceinline__ void lane_pair_eval_ell(char* lds, int K, const uint1
     if (srow) atomicAdd(&cl[256 + yl * 16 + bb], 1);
   }
   __syncthreads();
-  pair_eval_publish(cl, lastp, K, pm, acc, ticket, G, wrow, srow);
+  if (slab)
+    pair_eval_publish_slab(cl, lastp, K, pm, slab, ticket, wg, G, wrow, srow);
+  else
+    pair_eval_publish(cl, lastp, K, pm, acc, ticket, G, wrow, srow);
 }
 
 }  // namespace lanes_detail

@@ -312,6 +312,7 @@ struct AsyncLaneDev {
   // the server GPU's inbox (an IPC mapping over xGMI) -- [P] delta + [FP/32] slice tags
   float* inbox;
   unsigned* inbox_tag;
+  int* eslab;            // [kLaneWg][2][64] the evaluation's per-workgroup counts (slab form)
 };
 
 struct AsyncArgs {
@@ -338,7 +339,7 @@ struct AsyncArgs {
   int tnz;
   int log_lane;        // lane whose deltas produce server rows (-1: none)
   long long launch;    // launch number (> every earlier one): lane-wide barrier words
-  int spin_rel;        // release wait budget (polls)
+  long long rel_ticks; // release / pull wait budget (s_memrealtime ticks, 100 MHz)
   unsigned* claim;     // [2][16] role claim counters
   int cpar;
   // remote = 1: the server is another rank (worker GPUs of a multi-rank job): a

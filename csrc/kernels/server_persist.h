@@ -93,8 +93,9 @@ struct SrvArgs {
   int cpar;
   int sxcd;                    // the XCD the server workgroups claim
   long long launch;
-  int spin_cmd;                // command wait budget (polls)
-  int spin;                    // inbox tag wait budget (polls)
+  long long cmd_ticks;         // command wait budget (s_memrealtime ticks, 100 MHz)
+  long long tag_ticks;         // inbox tag wait budget (ticks)
+  int spin;                    // the workgroups' barrier budget (polls)
 };
 
 size_t server_persist_lds_bytes();

@@ -22,11 +22,12 @@ __device__ __forceinline__ void srv_wait_cmd(const SrvArgs& a, unsigned long lon
   const TagChunk* slot = a.cmd + (size_t)((want - 1) % (unsigned long long)a.ring) * kCmdChunks;
   TagChunk c = TagChunk{0, 0, 0, 0};
   bool ok = false;
-  for (int spins = 0;; ++spins) {
+  const long long t_end = rt_now() + a.cmd_ticks;
+  for (;;) {
     if (tid < kCmdChunks) c = srv_ld_sys_chunk(slot, (unsigned)(kCmdChunks * 16), (unsigned)tid * 16u);
     const unsigned t0 = __shfl(c.tag, 0, 64);
     ok = __all(tid >= kCmdChunks || c.tag == t0) && t0 == (unsigned)want;
-    if (ok || spins >= a.spin_cmd) break;
+    if (ok || rt_now() > t_end) break;
     __builtin_amdgcn_s_sleep(8);
   }
   if (!ok) {
@@ -53,9 +54,10 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
       __shared__ int ok_s;
       if (tid == 0) {
         const unsigned* tg = a.inbox_tag + (size_t)cmd.k * NS + wg;
-        int spins = 0;
-        while ((int)(ld_sys_u32(tg) - cmd.dtag) < 0 && ++spins <= a.spin) __builtin_amdgcn_s_sleep(2);
-        ok_s = spins <= a.spin;
+        const long long t_end = rt_now() + a.tag_ticks;
+        bool late = false;
+        while ((int)(ld_sys_u32(tg) - cmd.dtag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
+        ok_s = !late;
         if (!ok_s) xstore(err, 11ull);  // the delta never arrived: apply nothing
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       }
@@ -158,7 +160,10 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs* __re
   for (unsigned long long n = a.cmd0 + 1;; ++n) {
     if (wg == 0) srv_wait_cmd(a, n);
     if (wg == 0 && tid == 0) report(n - 1);
-    x_barrier(a.flags, wg, kSrvWg, ++lw, err, a.spin_cmd);
+    // (the others wait for the leader without a budget of their own: the leader's command
+    // wait is bounded and ends in a stop command -- with the same poll budget the others'
+    // faster polls would give up first during a long idle period)
+    x_barrier(a.flags, wg, kSrvWg, ++lw, err, 0x7fffffff);
     if (wg == 0 && tid == 0)  // (its ring slot may be reused: the record is in the broadcast area)
       __hip_atomic_store(a.consumed_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     SrvCmd cmd;

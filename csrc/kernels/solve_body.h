@@ -1109,9 +1109,11 @@ __device__ __forceinline__ void p_barrier(unsigned long long* ctr, unsigned long
 // polls workgroup i's line with nt loads (the L2 of the shared XCD), so all
 // arrivals are observed in one round trip.  The words only grow over the runs
 // (the run counter advances per solve): nothing is reset.
+// drain = false: the workgroup publishes nothing through this barrier (its outstanding
+// stores -- e.g. system-scope stores into pinned host memory -- need not complete first).
 __device__ __forceinline__ void x_barrier(unsigned long long* flags, int wg, int G, unsigned long long word,
-                                          unsigned long long* err, int spin_max = 1 << 22) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores reached the L2
+                                          unsigned long long* err, int spin_max = 1 << 22, bool drain = true) {
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's stores reached the L2
   __syncthreads();
   if (threadIdx.x == 0) st_h64<2>(flags + (size_t)wg * 32, word);
   if ((int)threadIdx.x < G) {

@@ -348,6 +348,7 @@ class LanesLoop {
   std::vector<int> lane_of_;            // worker id -> lane (-1: not on this loop)
   int log_lane_ = -1;
   int64_t launch_no_ = 0;
+  double rel_wait_s_ = 60.0;  // the host loop's no-progress limit of the current run (the lanes' wait budget)
   std::vector<hipEvent_t> pull_ev_;     // remote mode: a lane's weights received
   // peer data plane (set_peer): receive region, per-lane inbox slots, the pull tag of
   // each lane's pending release

@@ -929,7 +929,7 @@ void LanesLoop::ensure_async() {
     return o;
   };
   struct Offs {
-    size_t wpull, shi, slo, sb, acc, etk, flags, rec, relc;
+    size_t wpull, shi, slo, sb, acc, etk, flags, rec, relc, eslab;
   };
   std::vector<Offs> o(L);
   for (int l = 0; l < L; ++l) {
@@ -942,6 +942,7 @@ void LanesLoop::ensure_async() {
     o[l].flags = take((size_t)kLaneWg * 32 * 8);
     o[l].rec = take(32 * 8);
     o[l].relc = take(8);
+    o[l].eslab = take((size_t)kLaneWg * 128 * 4);
   }
   const size_t o_tab = take(sizeof(AsyncLaneDev) * L);
   const size_t o_pack = take(sizeof(AsyncPack));
@@ -988,6 +989,7 @@ void LanesLoop::ensure_async() {
     A.flags = reinterpret_cast<unsigned long long*>(b + o[l].flags);
     A.rec = reinterpret_cast<unsigned long long*>(b + o[l].rec);
     A.relc = reinterpret_cast<unsigned long long*>(b + o[l].relc);
+    A.eslab = reinterpret_cast<int*>(b + o[l].eslab);
     A.rel = rel_host_ + l;
     if (peer_rx_) {
       A.inbox = reinterpret_cast<float*>(peer_inbox_[l]);
@@ -1026,7 +1028,6 @@ void LanesLoop::ensure_async() {
   a.Ti = cfg_.Ti;
   a.Tv = cfg_.Tv;
   a.tnz = (cfg_.Ti && cfg_.Tv && cfg_.tnz > 0 && cfg_.tnz % 8 == 0) ? cfg_.tnz : 0;
-  a.spin_rel = 1 << 24;  // ~30 s of polls: the host answers every release
   a.claim = claim_;
   relc_.assign(L, 0);
   pend_r_.assign(L, LaneRound{});
@@ -1219,6 +1220,8 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   a.dbg_cap = dbg_cap_ > 0 ? dbg_cap_ : 1;
   a.launch = ++launch_no_;
   a.cpar = (int)(launches_ & 1);
+  // the lanes' release / pull waits outlast the host loop's own no-progress limit
+  a.rel_ticks = (long long)((std::min(rel_wait_s_, 7200.0) + 10.0) * 1e8);
   hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
   hip_check(hipStreamWaitEvent(astream_, aev_in_, 0), "async order in");
   if (remote) {
@@ -1267,6 +1270,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
     want_vc_[l] = api().tracker_clock(trk, cfg_.k[l]);
     check(want_vc_[l], "tracker clock");
   }
+  rel_wait_s_ = max_wait_s;
   launch_async(stream, false);
   int64_t started = 0, done = 0;
   std::vector<int64_t> lane_started((size_t)L, 0);
@@ -1417,6 +1421,7 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
   enum { kWaitPull = 3, kPulling = 4, kDone = 5 };
   for (int l = 0; l < L; ++l) state_[l] = kWaitPull;  // the server's begin() sends everybody its clock
   std::vector<int64_t> it(L, 0);
+  rel_wait_s_ = max_wait_s;
   launch_async(stream, true);
   int64_t done = 0;
   int running = 0, finished = 0;
@@ -1506,8 +1511,15 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
       }
       if ((++spins & 1023) == 0) {
         check_errors(-1);
-        if (epoch_ms() - wait0 > max_wait_s * 1000.0)
-          throw std::runtime_error("LanesLoop: no progress with the server for " + std::to_string(max_wait_s) + " s");
+        if (epoch_ms() - wait0 > max_wait_s * 1000.0) {
+          std::string m = "LanesLoop: no progress with the server for " + std::to_string(max_wait_s) +
+                          " s; lanes (state 1 want / 2 running / 3 wait pull / 4 pulling / 5 done, vc, pull tag):";
+          for (int l = 0; l < L; ++l)
+            m += " [" + std::to_string(state_[l]) + " " + std::to_string((long long)want_vc_[l]) + " " +
+                 std::to_string(peer ? pull_tag_[l] : 0u) + " it " + std::to_string((long long)it[l]) + "]";
+          m += "; tokens pushed " + std::to_string((long long)done);
+          throw std::runtime_error(m);
+        }
         if (running == 0) std::this_thread::sleep_for(std::chrono::microseconds(100));
       } else {
         _mm_pause();

@@ -3,6 +3,7 @@
 
 #include <emmintrin.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstring>
@@ -111,10 +112,12 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   a.rec = reinterpret_cast<unsigned long long*>(b + o_rec);
   a.claim = reinterpret_cast<unsigned*>(b + o_claim);
   a.sxcd = cfg.sxcd;
-  // ~1 PCIe round trip per poll: the command wait covers the worker timeout; a delta's
-  // tag is written before its token leaves the worker's GPU (a short wait at most)
-  const double polls = cfg.worker_timeout_s * 5e5;
-  a.spin_cmd = polls > 2e9 ? 2000000000 : (polls < 1e6 ? 1000000 : (int)polls);
+  // wall-clock budgets: the command wait outlasts the host's own watchdog (the worker
+  // timeout: a silent worker is failed and the commands resume); a delta's tag is
+  // written before its token leaves the worker's GPU (a short wait at most)
+  const double cmd_s = std::min(cfg.worker_timeout_s + 30.0, 7200.0);
+  a.cmd_ticks = (long long)(cmd_s * 1e8);
+  a.tag_ticks = 10ll * 100000000ll;
   a.spin = 1 << 22;
   args_dev_ = reinterpret_cast<SrvArgs*>(b + o_args);
   ptag_.assign(N, 0u);
@@ -147,10 +150,22 @@ void PeerServer::check_api(int rc, const char* what) const {
 
 void PeerServer::check_device() const {
   const unsigned long long e = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
-  if (e)
-    throw std::runtime_error("PeerServer: the server kernel's wait timed out (command " + std::to_string(e >> 8) +
-                             ", code " + std::to_string((int)(e & 0xff)) +
-                             (int(e & 0xff) == 11 ? ": a worker's delta never reached the inbox)" : ")"));
+  if (e) {
+    // (the protocol state for the report: deltas applied per worker, commands written /
+    // read by the kernel, the last arrivals)
+    std::string m = "PeerServer: the server kernel's wait timed out (command " + std::to_string(e >> 8) + ", code " +
+                    std::to_string((int)(e & 0xff)) +
+                    (int(e & 0xff) == 11 ? ": a worker's delta never reached the inbox" : "") + "); commands " +
+                    std::to_string(cmds_) + " written, " +
+                    std::to_string(__atomic_load_n(consumed_host_, __ATOMIC_ACQUIRE)) + " read; deltas per worker:";
+    std::vector<int> per(cfg_.nworkers, 0);
+    for (const auto& a : arrivals_) ++per[a.first];
+    for (int j = 0; j < cfg_.nworkers; ++j) m += " " + std::to_string(per[j]);
+    m += "; last arrivals:";
+    for (size_t i = arrivals_.size() > 12 ? arrivals_.size() - 12 : 0; i < arrivals_.size(); ++i)
+      m += " (" + std::to_string(arrivals_[i].first) + "," + std::to_string((long long)arrivals_[i].second) + ")";
+    throw std::runtime_error(m);
+  }
 }
 
 int PeerServer::log_worker() const {

@@ -19,7 +19,7 @@ def cfg_for(world: int, mode: str):
         return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,
                         stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=6, min_buffer_size=128,
                         max_buffer_size=1024, init="random", seed=0, server_colocated=False, workers_per_rank=3,
-                        bsp_schedule="peer", worker_timeout_s=25.0)
+                        bsp_schedule="peer", worker_timeout_s=20.0)
     if mode.startswith("async") or mode.startswith("peer"):
         # SSP(2) / ASP: 1 server rank + worker ranks x 3 lanes -- async_*: a CPU server and
         # the host shared-memory data plane; peer_*: a GPU server rank and the peer data
@@ -42,7 +42,8 @@ def main():
     out_dir, mode = sys.argv[1], sys.argv[2]
     import faulthandler
 
-    faulthandler.dump_traceback_later(80, exit=True)  # a hang names its frames (before the test's limit)
+    # a hang names its frames (before the test's limit; the peer modes' native timeouts first)
+    faulthandler.dump_traceback_later(140 if mode.startswith("peer") else 80, exit=True)
     import torch
     import torch.distributed as dist
 

@@ -143,7 +143,7 @@ def test_peer_plane_gpu_server_two_worker_ranks(cuda, tmp_path, mode, bound):
     iteration): the arrival order replays through a fresh tracker, its gap stays
     <= D + 1 under SSP(2) and runs ahead under ASP (ServerProcessor.java:95-183,
     MessageTracker.java:69-87, README.md:299-321)."""
-    res = _launch(tmp_path, mode, world=3, timeout=150)
+    res = _launch(tmp_path, mode, world=3, timeout=175)
     srv, wks = res[0], res[1:]
     assert srv.get("data_plane") == "peer", srv
     assert all(w.get("async_lanes") and w.get("data_plane") == "peer" for w in wks), wks
@@ -170,7 +170,7 @@ def test_peer_plane_bsp_equals_in_process_engine(cuda, tmp_path):
     releases every worker once the round is complete (MessageTracker.java:69-87).
     The weights equal one process hosting the same 6 workers in the BSP lanes loop
     (the same deltas, summed in another order), one server row per round."""
-    res = _launch(tmp_path, "peer_bsp", world=3, timeout=150)
+    res = _launch(tmp_path, "peer_bsp", world=3, timeout=175)
     srv = res[0]
     assert srv.get("data_plane") == "peer", srv
     assert srv["updates"] == 6 * 6, srv["updates"]

@@ -862,6 +862,17 @@ class DistEngine:
         finally:
             dist.barrier()
 
+    def _ctrl_diag(self) -> str:
+        """(failure reports) the control plane as this rank sees it: tokens pushed /
+        popped and the shared-memory segment of each queue."""
+        out = []
+        for tag, q in [("ctrl", getattr(self, "_ctrl", None)), ("reply", getattr(self, "_reply", None))] + \
+                [(f"reply{i}", q) for i, q in enumerate(getattr(self, "_replies", None) or [])]:
+            if q is not None:
+                e, d, ino = q.state()
+                out.append(f"{tag} {q.name} pushed {e} popped {d} inode {ino}")
+        return "control plane: " + ", ".join(out)
+
     def _close_async(self):
         """Tear down the asynchronous control / data planes (after the last run)."""
         ps = getattr(self, "_pserver", None)
@@ -1007,7 +1018,10 @@ class DistEngine:
         u0 = srv.updates
         a.begin()
         while True:
-            code, k, upd = a.run(int(cfg.checkpoint_every or 0) if cfg.checkpoint_dir else 0)
+            try:
+                code, k, upd = a.run(int(cfg.checkpoint_every or 0) if cfg.checkpoint_dir else 0)
+            except RuntimeError as e:
+                raise RuntimeError(f"{e}; {self._ctrl_diag()}") from None
             srv.updates = int(upd)
             if code == h.ASYNC_DONE:
                 break
@@ -1016,7 +1030,7 @@ class DistEngine:
                 continue
             reason = "reported an error" if code == h.ASYNC_ERROR_TOKEN else "busy and silent (watchdog)"
             if not drop_on_failure(cfg):
-                raise WorkerFailure(int(k), reason)
+                raise WorkerFailure(int(k), reason + "; " + self._ctrl_diag())
             print(f"psx server: worker {k} failed ({reason}); continuing without it", flush=True)
             a.fail(int(k))
         if gpu:
@@ -1054,8 +1068,11 @@ class DistEngine:
         t_start = time.time()
         deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
         iters = int(cfg.max_iters) if cfg.max_iters else 1 << 40
-        n = int(lp.run_async_remote(p2p, self._ctrl.handle, self._reply.handle, iters, stream,
-                                    self._comm_stream.cuda_stream, float(cfg.worker_timeout_s), deadline_ms))
+        try:
+            n = int(lp.run_async_remote(p2p, self._ctrl.handle, self._reply.handle, iters, stream,
+                                        self._comm_stream.cuda_stream, float(cfg.worker_timeout_s), deadline_ms))
+        except RuntimeError as e:
+            raise RuntimeError(f"{e}; {self._ctrl_diag()}") from None
         torch.cuda.synchronize(self.device)
         lp.poll_errors()
         for i, w in enumerate(W):

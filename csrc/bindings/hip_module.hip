@@ -884,6 +884,9 @@ PYBIND11_MODULE(_psx_hip, m) {
            py::arg("inbox"), py::arg("inbox_tag"))
       .def("prepare_async", &LanesLoop::prepare_async)
       .def("set_async_debug", &LanesLoop::set_async_debug, py::arg("buf"), py::arg("cap"))
+      .def("set_injection", &LanesLoop::set_injection, py::arg("crash"), py::arg("stop"), py::arg("drop"))
+      .def_property_readonly("crashed", &LanesLoop::crashed)
+      .def_property_readonly("left", &LanesLoop::left)
       .def_property_readonly("async_log", &LanesLoop::async_log)
       .def_property_readonly("peer", &LanesLoop::peer)
       .def(

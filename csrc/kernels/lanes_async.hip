@@ -360,7 +360,9 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   const unsigned long long t = ld_h64<2>(A.rec + 16);
   if (wg == 0 && tid == 0) stamp(dv, 30, 5);
-  const bool logl = l == a.log_lane;
+  // the logging lane: the host asks this release for a server row (the lowest live
+  // worker's deltas, ServerProcessor.java:154-165 -- it moves when that worker fails)
+  const bool logl = !a.remote && q.slot_s != 0ull;
   if (!a.remote) {  // the server is this launch: serial slice updates in ticket order
     if (wg < NS) async_apply_slice<FP>(cfg, dv, A, a, wg, t, logl, err, spin, nullptr);
     x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);

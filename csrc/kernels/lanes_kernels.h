@@ -74,7 +74,8 @@ struct LaneDev {
 struct LaneRound {
   int B, start, n, dst;
   long long first, step, first2;
-  int n2, pad;
+  int n2;
+  int delay_us;  // BSP round kernel: injected straggler delay before the lane's solve (0: none)
 };
 
 struct EvalModel {
@@ -285,7 +286,7 @@ PSX_HD inline void unpack_release(const TagChunk* ch, RelRec& q) {
   q.seq_s = ch[7].a;
   q.delay_us = (int)ch[7].b;
   q.pull_tag = ch[7].c;
-  q.r.pad = 0;
+  q.r.delay_us = 0;
 }
 // token: lane -> host (pinned ring, slot t % ring): {tag = ticket (low 32 bits,
 // tickets start at 1), lane, vc low, vc high}

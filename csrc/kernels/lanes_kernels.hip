@@ -151,6 +151,10 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   if (wg == 0 && tid == 0) {
     xstore(err, 0ull);  // this round's sticky error word (set by any timed-out wait below)
     if constexpr (S == 1) xstore(xch + kXchGen + ((run + 1u) & 1u), 0ull);  // re-arm the next run's counter
+    if (rr.delay_us > 0) {  // injected straggler (--inject_worker_delay): the lane's solve starts late
+      const long long t0 = rt_now();
+      while (rt_now() - t0 < (long long)rr.delay_us * (kRtTicksPerS / 1000000)) __builtin_amdgcn_s_sleep(64);
+    }
   }
   // the pulled weights of this slice, fetched first (their latency overlaps the staging)
   float wo_pre = 0.f, b_pre = 0.f;

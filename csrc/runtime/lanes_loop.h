@@ -148,6 +148,15 @@ class LanesLoop {
   void set_peer(uintptr_t rx_data, uintptr_t rx_tags, int64_t rx_stride, const std::vector<uintptr_t>& inbox,
                 const std::vector<uintptr_t>& inbox_tag);
   bool peer() const { return peer_rx_ != nullptr; }
+  // Fault injection for the NEXT run_async (the Python schedulers'
+  // --inject_worker_crash / --inject_worker_stop): crash[l] >= 0 -- lane l fails when
+  // released after crash[l] more solves (no delta; `drop`: the tracker retires its
+  // worker and the run goes on, else the run stops at once); stop[l] >= 0 -- lane l
+  // leaves cleanly after stop[l] more solves (its last delta applied, then retired).
+  // Empty vectors: none.  The workers concerned: crashed() / left() after the run.
+  void set_injection(const std::vector<int64_t>& crash, const std::vector<int64_t>& stop, bool drop);
+  const std::vector<int>& crashed() const { return crashed_; }
+  const std::vector<int>& left() const { return left_; }
   // Debug (tests): every applied ticket's delta into buf [cap][P] (device, slot (t - 1) %
   // cap) and a host log per ticket of what the release that solved it carried:
   // {ticket, lane, worker, vc, snapshot ticket, B, start, first, step, n, first2, n2}
@@ -255,6 +264,7 @@ class LanesLoop {
   void launch_async(hipStream_t stream, bool remote);
   void write_release(int lane, const RelRec& q);
   void stop_all(hipStream_t stream);
+  void stop_lane(int l);  // lane l's stop record (once per launch)
 
   LanesLoopCfg cfg_;
   Comm* comm_;
@@ -331,8 +341,12 @@ class LanesLoop {
   uint64_t aticket_ = 0;                // last ticket applied (device counter mirror)
   std::vector<uint64_t> relc_;          // release records written per lane
   std::vector<LaneRound> pend_r_;       // new stream rows not yet in the lane's ring
-  enum { kIdle = 0, kWant = 1, kRunning = 2 };
+  enum { kIdle = 0, kWant = 1, kRunning = 2, kGone = 6 };
   std::vector<int> state_;
+  std::vector<int64_t> inj_crash_, inj_stop_;  // set_injection (consumed by the next run_async)
+  bool inj_drop_ = true;
+  std::vector<int> crashed_, left_;             // workers that crashed / left in the last run
+  std::vector<uint8_t> lane_stopped_;           // lanes already sent their stop record (this launch)
   std::vector<int64_t> want_vc_;
   struct RunRec {
     int64_t vc = 0, nseen = 0;

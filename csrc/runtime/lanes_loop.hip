@@ -649,7 +649,10 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
       if (!rows && epoch_ms() - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
       std::this_thread::sleep_for(std::chrono::microseconds(500));
     }
-    for (int l = 0; l < L; ++l) seen_at_solve_[l] = seen[l];
+    for (int l = 0; l < L; ++l) {
+      seen_at_solve_[l] = seen[l];
+      a.r[l].delay_us = l < (int)cfg_.delay_us.size() ? cfg_.delay_us[l] : 0;
+    }
     phase(0);
     // ---- the round kernel: solves + update + riding evaluation of the last round ----
     if (side_eval_) {
@@ -1181,11 +1184,26 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   return true;
 }
 
-void LanesLoop::stop_all(hipStream_t stream) {
+void LanesLoop::set_injection(const std::vector<int64_t>& crash, const std::vector<int64_t>& stop, bool drop) {
+  if ((!crash.empty() && (int)crash.size() != cfg_.L) || (!stop.empty() && (int)stop.size() != cfg_.L))
+    throw std::invalid_argument("LanesLoop::set_injection: one entry per lane");
+  inj_crash_ = crash;
+  inj_stop_ = stop;
+  inj_drop_ = drop;
+}
+
+void LanesLoop::stop_lane(int l) {
+  if (lane_stopped_.size() != (size_t)cfg_.L) lane_stopped_.assign(cfg_.L, 0);
+  if (lane_stopped_[l]) return;  // (an unread second stop record would end the lane's next launch at once)
   RelRec q;
   std::memset(&q, 0, sizeof(q));
   q.stop = 1;
-  for (int l = 0; l < cfg_.L; ++l) write_release(l, q);
+  write_release(l, q);
+  lane_stopped_[l] = 1;
+}
+
+void LanesLoop::stop_all(hipStream_t stream) {
+  for (int l = 0; l < cfg_.L; ++l) stop_lane(l);
   // the launch drains once every workgroup has been dispatched and returned; a bounded
   // wait turns a launch that cannot drain into an error that says how far dispatch got
   const double t0 = epoch_ms();
@@ -1220,6 +1238,7 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   a.dbg_cap = dbg_cap_ > 0 ? dbg_cap_ : 1;
   a.launch = ++launch_no_;
   a.cpar = (int)(launches_ & 1);
+  lane_stopped_.assign(cfg_.L, 0);
   // the lanes' release / pull waits outlast the host loop's own no-progress limit
   a.rel_ticks = (long long)((std::min(rel_wait_s_, 7200.0) + 10.0) * 1e8);
   hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
@@ -1271,6 +1290,12 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
     check(want_vc_[l], "tracker clock");
   }
   rel_wait_s_ = max_wait_s;
+  // fault injection of this run (set_injection), consumed here
+  const std::vector<int64_t> crash = std::move(inj_crash_), stop = std::move(inj_stop_);
+  inj_crash_.clear();
+  inj_stop_.clear();
+  crashed_.clear();
+  left_.clear();
   launch_async(stream, false);
   int64_t started = 0, done = 0;
   std::vector<int64_t> lane_started((size_t)L, 0);
@@ -1278,10 +1303,44 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
   bool stopping = updates <= 0;
   std::vector<int> ks((size_t)cfg_.N);
   std::vector<int64_t> vs((size_t)cfg_.N);
+  // a lane whose worker crashed / left: it gets its stop record now (its workgroups
+  // leave the launch), the tracker retires the worker (the others are no longer held
+  // back by its clock) and the lanes that releases are dispatched
+  auto lane_leave = [&](int l, bool crashed) {
+    const int k = cfg_.k[l];
+    state_[l] = kGone;
+    stop_lane(l);
+    (crashed ? crashed_ : left_).push_back(k);
+    if (crashed && !inj_drop_) {  // --on_worker_failure fail: the run ends here
+      stopping = true;
+      return;
+    }
+    if (l == log_lane_) {  // server rows follow the lowest surviving worker's deltas
+      int nl = -1;
+      for (int j = 0; j < L; ++j)
+        if (state_[j] != kGone && (nl < 0 || cfg_.k[j] < cfg_.k[nl])) nl = j;
+      log_lane_ = nl;
+      if (nl >= 0) cfg_.log_worker = cfg_.k[nl];
+    }
+    const int n = api().tracker_retire(trk, k, ks.data(), vs.data(), cfg_.N);
+    check(n, "tracker retire");
+    for (int i = 0; i < n; ++i) {
+      const int j = ks[i] >= 0 && ks[i] < cfg_.N ? lane_of_[ks[i]] : -1;
+      if (j < 0) throw std::logic_error("LanesLoop: the tracker released a worker this loop does not host");
+      if (state_[j] == kGone) continue;
+      state_[j] = kWant;
+      want_vc_[j] = vs[i];
+    }
+  };
   try {
     auto start_ready = [&](double now) {
       for (int l = 0; l < L; ++l) {
         if (state_[l] != kWant || stopping || started >= updates) continue;
+        if (!crash.empty() && crash[l] >= 0 && lane_started[l] >= crash[l]) {
+          lane_leave(l, true);  // released, and fails before its solve (roles.py WorkerRole.compute)
+          l = -1;               // (a retirement may have released a lane already passed)
+          continue;
+        }
         if (at_budget(l, lane_started[l])) continue;
         if (try_release(l, want_vc_[l], now)) {
           state_[l] = kRunning;
@@ -1327,9 +1386,11 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
         for (int i = 0; i < n; ++i) {
           const int j = ks[i] >= 0 && ks[i] < cfg_.N ? lane_of_[ks[i]] : -1;
           if (j < 0) throw std::logic_error("LanesLoop: the tracker released a worker this loop does not host");
+          if (state_[j] == kGone) continue;
           state_[j] = kWant;
           want_vc_[j] = vs[i];
         }
+        if (!stop.empty() && stop[l] >= 0 && lane_started[l] >= stop[l]) lane_leave(l, false);
         if (deadline_ms > 0.0 && epoch_ms() >= deadline_ms) stopping = true;
         start_ready(epoch_ms() - cfg_.t0_ms);
         idle_spins = 0;

@@ -145,6 +145,7 @@ class LocalEngine:
         if (cfg.consistency_model == 0 or cfg.num_workers == 1) and cfg.pair_eval:
             EvalPair(self.server, self.workers[0])
         self.failed: set[int] = set()
+        self.left: set[int] = set()  # workers that left cleanly (--inject_worker_stop)
         if maybe_resume(cfg, self.server, self.workers):
             self.rounds = int(self.server.tracker.min_clock())
             self.failed = {k for k in range(cfg.num_workers) if not self.server.tracker.is_live(k)}
@@ -199,6 +200,8 @@ class LocalEngine:
                                  - ph.get("sync", 0.0) - ph["summary"], 3)
         out["max_vc_gap"] = int(self.server.tracker.max_gap)
         out["failed_workers"] = sorted(self.failed)
+        if self.left:
+            out["left_workers"] = sorted(self.left)
         return out
 
     def _worker_failed(self, e: Exception, k: int):
@@ -244,10 +247,8 @@ class LocalEngine:
         evaluation rows).  Runs that need Python between rounds (tracing, injected
         faults) use the loops below.  The tuple-driven cadence (--iter_new_*) and
         the producer clock run natively: a round waits until every lane saw its
-        new tuples."""
-        c = self.cfg
-        if c.inject_worker_delay_ms:
-            return False
+        new tuples.  Injected stragglers sleep on the device (LaneRound.delay_us);
+        an injected crash ends a chunk of rounds at its iteration (_run_bsp_lanes)."""
         return self._lanes_shape_ok()
 
     def _async_lanes_ok(self) -> bool:
@@ -255,8 +256,9 @@ class LocalEngine:
         persistent launch, every worker released by the C++ tracker, updates serial
         in arrival order on the device): the lanes loop's shapes, plus every
         worker's shard at least its ring (a release's pending rows span at most one
-        epoch wrap).  Injected straggler delays run on the device; crash / stop
-        injection and tracing keep the Python schedulers."""
+        epoch wrap).  Injected straggler delays run on the device, injected crashes /
+        clean leaves in the host loop (LanesLoop.set_injection); tracing keeps the
+        Python schedulers."""
         if os.environ.get("PSX_ASYNC_LANES", "1") == "0" or not self._lanes_shape_ok():
             return False
         W = [w for w in self.workers if w.k not in self.failed]
@@ -268,8 +270,6 @@ class LocalEngine:
             return False
         W = [w for w in self.workers if w.k not in self.failed]
         if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
-            return False
-        if c.inject_worker_crash or c.inject_worker_stop:
             return False
         sp = self.spec
         for w in W:
@@ -324,10 +324,14 @@ class LocalEngine:
         self._lanes, self._lanes_key = lp, key
         return lp
 
-    def _run_bsp_lanes(self) -> dict:
+    def _run_bsp_lanes(self, max_rounds: int | None = None, t_start: float | None = None) -> dict:
         """BSP rounds of every live worker in the native multi-lane loop: one launch
         per round, no Python per round.  An unbounded run (max_iters 0: until the
-        data or the wall clock says stop) and checkpoints run in chunks of rounds."""
+        data or the wall clock says stop) and checkpoints run in chunks of rounds.
+        An injected crash (--inject_worker_crash K:ITER) ends a chunk at round ITER of
+        worker K: the failure policy then aborts the run or retires K, and the run
+        goes on with the other workers in a loop of their own (max_rounds: the rest
+        of max_iters; roles.py WorkerRole.compute fails at the same iteration)."""
         cfg, srv = self.cfg, self.server
         W = [w for w in self.workers if w.k not in self.failed]
         for w in W:
@@ -345,10 +349,13 @@ class LocalEngine:
                 lp.set_next_local(i, nl)
                 lp.set_seen_at_solve(i, ss)
         stream = stream_handle(self.device)
-        t_start = time.time()
+        t_start = time.time() if t_start is None else t_start
         deadline_ms = (t_start + cfg.max_wallclock_s) * 1000.0 if cfg.max_wallclock_s else 0.0
         r0 = r = self.rounds
         u0 = srv.updates
+        limit = cfg.max_iters if max_rounds is None else max_rounds
+        crashing = [w for w in W if w.crash_at is not None]
+        crashed = []
         chunk = 256
         ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
         if ck:
@@ -359,14 +366,19 @@ class LocalEngine:
                 # checkpoints fire at multiples of checkpoint_every: a run that starts
                 # between two of them first runs up to the next one
                 todo = chunk - (r % chunk) if ck else chunk
-                if cfg.max_iters:
-                    todo = min(todo, cfg.max_iters - (r - r0))
+                if limit:
+                    todo = min(todo, limit - (r - r0))
                     if todo <= 0:
                         break
                 if lp.all_exhausted:  # the streams ended: stale windows for idle_exit_s more
                     exhausted_since = exhausted_since or time.time()
                 if self._stop(r - r0, t_start, exhausted_since):
                     break
+                if crashing:  # the next injected crash ends this chunk
+                    crashed = [w for w in crashing if w.iters >= w.crash_at]
+                    if crashed:
+                        break
+                    todo = min(todo, min(w.crash_at - w.iters for w in crashing))
                 n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
                 r += n
                 # the roles' counters advance with every chunk, so a checkpoint taken
@@ -408,8 +420,16 @@ class LocalEngine:
         self._lanes_synced = (lp, [(int(w.source.next_local), int(w._seen_at_solve)) for w in W])
         self.native_host_us_per_round = float(lp.host_us_per_round)
         self.native_host_phases_us = [round(float(x), 2) for x in lp.host_phases_us()]
-        elapsed = time.time() - t_start
         self.rounds = r
+        if crashed:
+            for w in crashed:  # fail: raises; drop: retired, the others go on without it
+                self._worker_failed(WorkerFailure(w.k, f"injected crash at iteration {w.iters}"), w.k)
+            rest = (limit - (r - r0)) if limit else None
+            if (rest is None or rest > 0) and any(w.k not in self.failed for w in self.workers):
+                out = self._run_bsp_lanes(rest if limit else None, t_start)
+                out["updates_per_s"] = (srv.updates - u0) / max(1e-9, time.time() - t_start)
+                return out
+        elapsed = time.time() - t_start
         return {"rounds": r, "updates": srv.updates, "elapsed_s": elapsed,
                 "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True,
                 "lanes": len(W), "hand_off_scope": int(lp.hand_off_scope),
@@ -448,6 +468,8 @@ class LocalEngine:
         clock0 = {w.k: int(srv.tracker.clock(w.k)) for w in W}
         clock_start = dict(clock0)
         total = int(cfg.max_iters) * len(W) if cfg.max_iters else 0
+        inject = any(w.crash_at is not None for w in W) or bool(cfg.inject_worker_stop)
+        crashed: list[WorkerFailure] = []
         ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
         chunk = max(1, int(cfg.checkpoint_every)) if ck else 1 << 16
         done = 0
@@ -468,6 +490,12 @@ class LocalEngine:
                 # across the chunks of a checkpointed run
                 budget = ([max(0, int(cfg.max_iters) - (int(srv.tracker.clock(w.k)) - clock_start[w.k])) for w in W]
                           if cfg.max_iters else 0)
+                if inject:  # crashes / clean leaves: solves left before each (roles.py WorkerRole.compute)
+                    crash = [max(0, w.crash_at - w.iters) if w.crash_at is not None and w.k not in self.failed
+                             else -1 for w in W]
+                    stop = [max(0, int(cfg.inject_worker_stop[w.k]) - w.iters) if w.k in cfg.inject_worker_stop
+                            else -1 for w in W]
+                    lp.set_injection(crash, stop, drop_on_failure(cfg))
                 n = int(lp.run_async(int(todo), stream, float(cfg.worker_timeout_s), deadline_ms, budget))
                 done += n
                 srv.updates += n
@@ -477,8 +505,14 @@ class LocalEngine:
                     w.vc = int(srv.tracker.clock(w.k))
                     w.iters += w.vc - clock0[w.k]
                     clock0[w.k] = w.vc
+                if inject:
+                    for k in lp.crashed:  # (the loop retired it already under drop, or stopped the run)
+                        crashed.append(WorkerFailure(k, f"injected crash at iteration {self.workers[k].iters}"))
+                    self.left.update(int(k) for k in lp.left)
                 if n and ck:
                     maybe_checkpoint(cfg, srv, srv.updates, W)
+                if crashed and not drop_on_failure(cfg):
+                    break
                 if n < todo:  # the streams ended, the deadline passed
                     break
             ca = getattr(self, "_lanes_copy_args", None)  # (the roles' tensors outlive the loop)
@@ -497,6 +531,11 @@ class LocalEngine:
         for w in W:
             if w.ring.XT is not None:
                 w.ring.xt_stale = True
+        for e in crashed:
+            if not drop_on_failure(cfg):
+                raise e
+            self.failed.add(e.worker)
+            print(f"psx: worker {e.worker} failed ({e}); continuing with {srv.tracker.num_live} workers", flush=True)
         self.native_host_us_per_round = float(lp.host_us_per_update)
         self.native_host_busy_us_per_token = float(lp.host_busy_us_per_token)
         elapsed = time.time() - t_start

@@ -229,3 +229,56 @@ def test_async_sparse_eval_rows_equal_dense(cuda, monkeypatch):
     assert len(ra) == len(rb) == 6 and len(sa) == len(sb)
     for a, b in zip(ra + sa, rb + sb):
         assert a[:2] == b[:2] and all(abs(x - y) <= 2 / 4877 + 1e-6 for x, y in zip(a[2:], b[2:])), (a, b)
+
+
+# ---- fault injection on the lanes loops (the Python schedulers' semantics:
+# roles.py WorkerRole.compute fails at iteration ITER, engine.py _worker_failed) ----
+
+def test_async_lanes_crash_dropped_rows_move(cuda):
+    """ASP, worker 0 crashes at its 4th iteration: the host loop retires it (drop), the
+    others run their 12 iterations, and the server rows move to worker 1's deltas."""
+    eng = _engine(cuda, -1, workers=4, iters=12, inject_worker_crash={0: 3})
+    assert eng._async_lanes_ok()
+    out = eng.run()
+    assert out["async_lanes"] and out["failed_workers"] == [0]
+    assert eng.workers[0].iters == 3 and [w.iters for w in eng.workers[1:]] == [12, 12, 12]
+    assert out["updates"] == 3 + 36
+    srv = eng.log.book.server  # worker 0's 3, then worker 1's released after the crash
+    assert 3 + 6 <= len(srv) <= 3 + 12, len(srv)
+    assert [r[1] for r in srv[3:]] == sorted(r[1] for r in srv[3:])
+    wrows = eng.log.book.worker
+    assert sum(1 for r in wrows if r[1] == 0) == 3
+    assert torch.isfinite(eng.server.w).all()
+
+
+def test_async_lanes_crash_fail_policy_raises(cuda):
+    """SSP(2) (auto policy = fail): the crash ends the run with WorkerFailure."""
+    from psx.runtime.faults import WorkerFailure
+
+    eng = _engine(cuda, 2, workers=3, iters=10, inject_worker_crash={1: 2})
+    with pytest.raises(WorkerFailure, match="worker 1"):
+        eng.run()
+    assert eng.workers[1].iters == 2
+
+
+def test_async_lanes_stop_leaves_cleanly(cuda):
+    """SSP(1): worker 2 leaves after 3 iterations (its last delta applied, then retired):
+    the others are no longer held back by its clock and finish their 10."""
+    eng = _engine(cuda, 1, workers=3, iters=10, inject_worker_stop={2: 3})
+    out = eng.run()
+    assert out.get("left_workers") == [2] and out["failed_workers"] == []
+    assert [w.iters for w in eng.workers] == [10, 10, 3]
+    assert out["updates"] == 23
+
+
+def test_bsp_lanes_crash_dropped_and_delay(cuda):
+    """BSP on the lanes loop: a straggler sleeps on the device (no Python scheduler), an
+    injected crash (drop) ends a chunk at its round and the rest runs without it."""
+    eng = _engine(cuda, 0, workers=3, iters=8, delays={1: 2.0}, inject_worker_crash={2: 4},
+                  on_worker_failure="drop")
+    assert eng._lanes_ok()
+    out = eng.run()
+    assert out["lanes"] and out["rounds"] == 8 and out["failed_workers"] == [2]
+    assert [w.iters for w in eng.workers] == [8, 8, 4]
+    assert out["updates"] == 4 * 3 + 4 * 2
+    assert 0.002 * 8 <= out["elapsed_s"]  # the 2 ms straggler holds every round

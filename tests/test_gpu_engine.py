@@ -231,9 +231,11 @@ def test_async_event_scheduler_four_workers(cuda, c):
     assert len(accs) >= 40 and accs[-1] > 0.25
 
 
-def test_async_event_scheduler_drops_crashed_worker(cuda):
+def test_async_event_scheduler_drops_crashed_worker(cuda, monkeypatch):
     """Event scheduler on a GPU: an injected crash retires the worker (ASP) and the
-    survivors keep stepping; server rows move to the lowest surviving worker."""
+    survivors keep stepping; server rows move to the lowest surviving worker.  (The
+    lanes loop takes such runs by default: tests/test_gpu_async_lanes.py.)"""
+    monkeypatch.setenv("PSX_ASYNC_LANES", "0")
     train, test = synth_finefood(12000, seed=0), synth_finefood(1000, seed=1)
     cfg = _cfg(num_workers=3, consistency_model=-1, max_iters=20, inject_worker_crash={0: 3})
     eng = LocalEngine(cfg, cuda, train=train, test=test)

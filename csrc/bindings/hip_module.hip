@@ -658,6 +658,7 @@ PYBIND11_MODULE(_psx_hip, m) {
           py::arg("checkpoint_every") = 0)
       .def("fail", &PeerServer::fail, py::call_guard<py::gil_scoped_release>())
       .def("stop", &PeerServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("warm_up", &PeerServer::warm_up, py::call_guard<py::gil_scoped_release>())
       .def("set_stream", [](PeerServer&, uintptr_t) {})  // (own stream; AsyncServer's interface)
       .def_property("updates", &PeerServer::updates, &PeerServer::set_updates)
       .def_property_readonly("tokens", &PeerServer::tokens)

@@ -405,10 +405,20 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   return true;
 }
 
+// The launch's {cfg, args} is its first kernel argument, read in place in the kernarg
+// segment (constant address space: scalar loads) through fresh_k per iteration.
+typedef const __attribute__((address_space(4))) AsyncPack KPack;
+__device__ __forceinline__ KPack* fresh_k(KPack* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 template <int FP, int KP, int S, bool MT>
-__global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __restrict__ pk,
+__global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack pkv,
                                                           const AsyncLaneDev* __restrict__ als) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  KPack* const pk4 = (KPack*)__builtin_amdgcn_kernarg_segment_ptr();  // = &pkv (argument 0)
+  const AsyncPack* const pk = (const AsyncPack*)pk4;
   const int b = (int)blockIdx.x, tid = threadIdx.x;
   int l, wg;
   {  // roles as lanes_round_kernel: a lane's workgroups claim its XCD's slots; no riders
@@ -430,6 +440,7 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
       if (b == 0)
         for (int j = 0; j < 32; ++j)
           __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      (void)__hip_atomic_fetch_add(c + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (diagnostics)
       role = r;
     }
     __syncthreads();
@@ -443,7 +454,7 @@ __global__ __launch_bounds__(256) void lanes_async_kernel(const AsyncPack* __res
   unsigned long long relc = *als[l].relc;        // release records consumed so far
   unsigned long long lw = (unsigned long long)pk->a.launch << 40;  // lane-wide barrier words
   for (;;) {
-    const AsyncPack* p = fresh(pk);
+    const AsyncPack* p = (const AsyncPack*)fresh_k(pk4);
     const AsyncLaneDev* A = fresh(als + l);
     if (!async_iteration<FP, KP, S, MT>(lds, p->cfg, p->a, *A, l, wg, run, relc, lw)) return;
   }
@@ -466,7 +477,7 @@ __global__ void async_init_kernel(const float* __restrict__ w, float* snap, unsi
 }
 
 template <int FP, int KP, int S, bool MT>
-void launch_afks(const AsyncPack* pk, const AsyncLaneDev* al, hipStream_t s) {
+void launch_afks(const AsyncPack& pk, const AsyncLaneDev* al, hipStream_t s) {
   static const bool prepared = ((void)hipFuncSetAttribute((const void*)lanes_async_kernel<FP, KP, S, MT>,
                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                                           (int)lanes_lds_bytes(FP)),
@@ -476,7 +487,7 @@ void launch_afks(const AsyncPack* pk, const AsyncLaneDev* al, hipStream_t s) {
 }
 
 template <int FP, int KP>
-void launch_afk(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+void launch_afk(const SolverCfg& cfg, const AsyncPack& pk, const AsyncLaneDev* al, int S, hipStream_t s) {
   const bool mt = cfg.cap > 32 * kLaneWg;
   if (S == 2 && mt)
     launch_afks<FP, KP, 2, true>(pk, al, s);
@@ -489,7 +500,7 @@ void launch_afk(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* a
 }
 
 template <int FP>
-void launch_af(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+void launch_af(const SolverCfg& cfg, const AsyncPack& pk, const AsyncLaneDev* al, int S, hipStream_t s) {
   const int KP = padded_classes(cfg.K);
   if (KP <= 2)
     launch_afk<FP, 2>(cfg, pk, al, S, s);
@@ -506,7 +517,7 @@ void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long l
                                       a.sstride);
 }
 
-void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s) {
+void launch_lanes_async(const SolverCfg& cfg, const AsyncPack& pk, const AsyncLaneDev* al, int S, hipStream_t s) {
   switch (cfg.Fp) {
     case 128: launch_af<128>(cfg, pk, al, S, s); break;
     case 256: launch_af<256>(cfg, pk, al, S, s); break;

@@ -366,7 +366,9 @@ struct AsyncPack {
 
 // Initialise the snapshot slot of ticket t (= w) and the slices' turn words (t).
 void launch_async_init(const SolverCfg& cfg, const AsyncArgs& a, unsigned long long t, hipStream_t s);
-// pk: device copy of {cfg, a} (a.launch / a.cpar of THIS launch); al: device table [L]
-void launch_lanes_async(const SolverCfg& cfg, const AsyncPack* pk, const AsyncLaneDev* al, int S, hipStream_t s);
+// pk: {cfg, a} of THIS launch (a.launch / a.cpar), passed as the kernel argument -- no
+// copy before the launch (on a GPU shared with other processes' persistent launches
+// a copy can wait behind them for minutes); al: device table [L]
+void launch_lanes_async(const SolverCfg& cfg, const AsyncPack& pk, const AsyncLaneDev* al, int S, hipStream_t s);
 
 }  // namespace psx

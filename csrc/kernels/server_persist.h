@@ -100,7 +100,8 @@ struct SrvArgs {
 
 size_t server_persist_lds_bytes();
 // One persistent launch on `s` (8 x kSrvWg workgroups; those not on XCD
-// a.sxcd leave at once).  a: a DEVICE copy of the arguments.
-void launch_server_persist(const SrvArgs* a, int FP, hipStream_t s);
+// a.sxcd leave at once).  The arguments travel as the kernel argument: no copy
+// before the launch (it could wait behind other processes' persistent launches).
+void launch_server_persist(const SrvArgs& a, int FP, hipStream_t s);
 
 }  // namespace psx

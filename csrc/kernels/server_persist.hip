@@ -121,23 +121,23 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
 }
 
 template <int FP>
-__global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs* __restrict__ pa) {
+__global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs pa) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = (int)blockIdx.x, tid = threadIdx.x;
   int wg;
   {
     __shared__ int role;
     if (tid == 0) {
-      unsigned* cl = pa->claim + 32 * pa->cpar;
+      unsigned* cl = pa.claim + 32 * pa.cpar;
       int r = -1;
       const int x = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
-      if (x == pa->sxcd) {
+      if (x == pa.sxcd) {
         const unsigned k = __hip_atomic_fetch_add(cl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k < (unsigned)kSrvWg) r = (int)k;
       }
       if (b == 0)
         for (int j = 0; j < 32; ++j)
-          __hip_atomic_store(pa->claim + 32 * (pa->cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(pa.claim + 32 * (pa.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = r;
     }
     __syncthreads();
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs* __re
     __syncthreads();
     if (wg < 0) return;
   }
-  const SrvArgs& a = *pa;
+  const SrvArgs& a = pa;
   unsigned long long* err = a.flags + (size_t)kSrvWg * 32;  // (the line behind the barrier lines)
   unsigned long long lw = (unsigned long long)a.launch << 40;
   // a timed-out wait (the sticky word `err`) -> the pinned host word as (command << 8) |
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs* __re
 
 size_t server_persist_lds_bytes() { return (size_t)kPairEvalLds; }
 
-void launch_server_persist(const SrvArgs* a, int FP, hipStream_t s) {
+void launch_server_persist(const SrvArgs& a, int FP, hipStream_t s) {
   const size_t lds = server_persist_lds_bytes();
   switch (FP) {
     case 128: server_persist_kernel<128><<<8 * kSrvWg, 256, lds, s>>>(a); break;

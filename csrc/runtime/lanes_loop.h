@@ -166,8 +166,11 @@ class LanesLoop {
   }
   const std::vector<std::vector<int64_t>>& async_log() const { return alog_; }
   // Allocate (and zero) the asynchronous workspace now: ranks sharing one GPU do this
-  // before any rank's persistent launch holds CUs a fill kernel would wait for.
-  void prepare_async() { ensure_async(); }
+  // before any rank's persistent launch holds CUs a fill kernel would wait for.  With
+  // the peer data plane also one empty launch (every lane stopped at once) that drains
+  // here: the first launch's one-time device work (the code object's load, the
+  // runtime's copy paths) must not wait behind another rank's persistent launch.
+  void prepare_async();
   int64_t tickets() const { return (int64_t)aticket_; }  // deltas applied by the asynchronous loop so far
   double host_us_per_update() const { return async_updates_ ? async_ns_ / 1000.0 / (double)async_updates_ : 0.0; }
   // host time spent per consumed token (token seen -> its rows handed over, tracker, the
@@ -265,6 +268,7 @@ class LanesLoop {
   void write_release(int lane, const RelRec& q);
   void stop_all(hipStream_t stream);
   void stop_lane(int l);  // lane l's stop record (once per launch)
+  std::string launch_report();  // (failure reports) the persistent launch's progress
 
   LanesLoopCfg cfg_;
   Comm* comm_;
@@ -335,8 +339,6 @@ class LanesLoop {
   AsyncRelease* rel_host_ = nullptr;    // pinned [L]
   AsyncToken* tok_host_ = nullptr;      // pinned [ring]
   AsyncArgs aargs_{};
-  AsyncPack* pack_dev_ = nullptr;       // device copy of {cfg, args} of the current launch
-  AsyncPack* pack_host_ = nullptr;      // pinned staging
   int R_ = 64, ring_ = 64;
   uint64_t aticket_ = 0;                // last ticket applied (device counter mirror)
   std::vector<uint64_t> relc_;          // release records written per lane
@@ -371,7 +373,6 @@ class LanesLoop {
   int64_t peer_stride_ = 0;
   std::vector<uintptr_t> peer_inbox_, peer_inbox_tag_;
   std::vector<unsigned> pull_tag_;
-  unsigned long long* tick_host_ = nullptr;  // pinned: the ticket a remote launch starts from
   // the persistent launch runs on a stream of its own (non-blocking: no implicit
   // synchronisation of the null stream, e.g. a host-staged transfer, waits for it),
   // ordered after / before the caller's stream by events

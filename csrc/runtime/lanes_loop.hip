@@ -328,8 +328,6 @@ LanesLoop::~LanesLoop() {
   if (aev_in_) (void)hipEventDestroy(aev_in_);
   if (aev_out_) (void)hipEventDestroy(aev_out_);
   if (tok_host_) (void)hipHostFree(tok_host_);
-  if (pack_host_) (void)hipHostFree(pack_host_);
-  if (tick_host_) (void)hipHostFree(tick_host_);
   if (err_host_) (void)hipHostFree(err_host_);
 }
 
@@ -948,7 +946,6 @@ void LanesLoop::ensure_async() {
     o[l].eslab = take((size_t)kLaneWg * 128 * 4);
   }
   const size_t o_tab = take(sizeof(AsyncLaneDev) * L);
-  const size_t o_pack = take(sizeof(AsyncPack));
   const size_t o_snap = take((size_t)R_ * P_ * 4);
   const size_t o_stag = take((size_t)R_ * NS * 4);
   const size_t o_tick = take(8);
@@ -959,7 +956,6 @@ void LanesLoop::ensure_async() {
             "hipHostMalloc(release records)");
   hip_check(hipHostMalloc((void**)&tok_host_, sizeof(AsyncToken) * ring_, hipHostMallocCoherent | hipHostMallocMapped),
             "hipHostMalloc(token ring)");
-  hip_check(hipHostMalloc((void**)&pack_host_, sizeof(AsyncPack), hipHostMallocDefault), "hipHostMalloc(pack)");
   std::memset((void*)rel_host_, 0, sizeof(AsyncRelease) * L);
   std::memset((void*)tok_host_, 0, sizeof(AsyncToken) * ring_);
   hip_check(hipStreamCreateWithFlags(&astream_, hipStreamNonBlocking), "hipStreamCreate(async)");
@@ -1000,7 +996,6 @@ void LanesLoop::ensure_async() {
     }
   }
   al_dev_ = reinterpret_cast<AsyncLaneDev*>(b + o_tab);
-  pack_dev_ = reinterpret_cast<AsyncPack*>(b + o_pack);
   hip_check(hipMemcpy(al_dev_, al_.data(), sizeof(AsyncLaneDev) * L, hipMemcpyHostToDevice), "async table upload");
   AsyncArgs& a = aargs_;
   std::memset(&a, 0, sizeof(a));
@@ -1019,8 +1014,6 @@ void LanesLoop::ensure_async() {
     a.sstride = peer_stride_;
     a.peer_rx = 1;
   }
-  hip_check(hipHostMalloc((void**)&tick_host_, sizeof(unsigned long long), hipHostMallocDefault),
-            "hipHostMalloc(ticket)");
   a.ticket = reinterpret_cast<unsigned long long*>(b + o_tick);
   a.turn = reinterpret_cast<unsigned long long*>(b + o_turn);
   a.tok = tok_host_;
@@ -1184,6 +1177,45 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   return true;
 }
 
+std::string LanesLoop::launch_report() {
+  // (failure reports) how far the current persistent launch got: its workgroups that
+  // claimed a lane slot per XCD and all that started, read on a stream of its own
+  // with a bounded wait
+  std::string m = "launch " + std::to_string((long long)launches_) + ": ";
+  const hipError_t q = hipStreamQuery(astream_);
+  m += q == hipSuccess ? "drained" : (q == hipErrorNotReady ? "running" : hipGetErrorString(q));
+  unsigned* h = nullptr;
+  hipStream_t s = nullptr;
+  if (hipHostMalloc((void**)&h, 32 * sizeof(unsigned), hipHostMallocDefault) != hipSuccess) return m;
+  std::memset(h, 0xff, 32 * sizeof(unsigned));
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+      hipMemcpyAsync(h, claim_ + 32 * ((launches_ - 1) & 1), 32 * sizeof(unsigned), hipMemcpyDeviceToHost, s) ==
+          hipSuccess) {
+    const double t0 = epoch_ms();
+    while (hipStreamQuery(s) == hipErrorNotReady && epoch_ms() - t0 < 2000.0)
+      std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (hipStreamQuery(s) == hipSuccess) {
+      m += "; lane slots claimed per XCD:";
+      for (int j = 0; j < 8; ++j) m += " " + std::to_string(h[j]);
+      m += "; workgroups started " + std::to_string(h[9]) + " of " + std::to_string(8 * kLaneWg);
+    } else {
+      m += "; (claim counters unreadable: the copy did not complete in 2 s)";
+    }
+  }
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipHostFree(h);
+  return m;
+}
+
+void LanesLoop::prepare_async() {
+  ensure_async();
+  if (!peer_rx_) return;
+  launch_async(astream_, true);
+  stop_all(astream_);
+  hip_check(hipStreamSynchronize(astream_), "warm-up launch");
+  check_errors(-1);
+}
+
 void LanesLoop::set_injection(const std::vector<int64_t>& crash, const std::vector<int64_t>& stop, bool drop) {
   if ((!crash.empty() && (int)crash.size() != cfg_.L) || (!stop.empty() && (int)stop.size() != cfg_.L))
     throw std::invalid_argument("LanesLoop::set_injection: one entry per lane");
@@ -1244,20 +1276,18 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   hip_check(hipEventRecord(aev_in_, stream), "async order in");  // after the caller's work so far
   hip_check(hipStreamWaitEvent(astream_, aev_in_, 0), "async order in");
   if (remote) {
-    // the ticket only: an SDMA copy from pinned memory, not a kernel -- on a GPU shared
-    // with other ranks' persistent launches a kernel's workgroups could wait for CUs
-    // those launches hold
-    *tick_host_ = aticket_;
-    hip_check(hipMemcpyAsync(a.ticket, tick_host_, sizeof(unsigned long long), hipMemcpyHostToDevice, astream_),
-              "async ticket");
+    // nothing to initialise: the device ticket counter only ever counts this loop's
+    // pushes, so it equals aticket_ (every push is consumed before a run ends).  No copy
+    // or fill before a remote launch: on a GPU shared with other ranks' persistent
+    // launches the runtime's copy / fill work waits behind them (profiles/r05/README.md)
   } else {
     launch_async_init(cfg_.scfg, a, aticket_, astream_);
     hip_check(hipGetLastError(), "async init launch");
   }
-  pack_host_->cfg = cfg_.scfg;
-  pack_host_->a = a;
-  hip_check(hipMemcpyAsync(pack_dev_, pack_host_, sizeof(AsyncPack), hipMemcpyHostToDevice, astream_), "async args");
-  launch_lanes_async(cfg_.scfg, pack_dev_, al_dev_, S_, astream_);
+  AsyncPack pk;
+  pk.cfg = cfg_.scfg;
+  pk.a = a;
+  launch_lanes_async(cfg_.scfg, pk, al_dev_, S_, astream_);
   hip_check(hipGetLastError(), "async lanes launch");
   ++launches_;
 }
@@ -1578,7 +1608,7 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
           for (int l = 0; l < L; ++l)
             m += " [" + std::to_string(state_[l]) + " " + std::to_string((long long)want_vc_[l]) + " " +
                  std::to_string(peer ? pull_tag_[l] : 0u) + " it " + std::to_string((long long)it[l]) + "]";
-          m += "; tokens pushed " + std::to_string((long long)done);
+          m += "; tokens pushed " + std::to_string((long long)done) + "; " + launch_report();
           throw std::runtime_error(m);
         }
         if (running == 0) std::this_thread::sleep_for(std::chrono::microseconds(100));

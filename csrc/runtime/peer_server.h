@@ -62,6 +62,13 @@ class PeerServer {
   void fail(int k);
   // Stop the persistent launch and wait for it (idempotent).
   void stop();
+  // One launch that stops at once, drained here: the first launch's one-time device work
+  // (code object load, copy paths) done before other ranks' persistent launches hold CUs
+  // of a shared GPU.
+  void warm_up() {
+    launch();
+    stop();
+  }
   int64_t updates() const { return updates_; }
   void set_updates(int64_t u) { updates_ = u; }
   int64_t tokens() const { return tokens_; }
@@ -90,11 +97,9 @@ class PeerServer {
   int NS_ = 0;
   // device workspace
   void* ws_ = nullptr;
-  SrvArgs* args_dev_ = nullptr;
   SrvArgs args_{};
   // pinned
   TagChunk* cmd_ring_ = nullptr;
-  SrvArgs* args_host_ = nullptr;
   unsigned long long* err_host_ = nullptr;
   unsigned long long* consumed_host_ = nullptr;
   int ring_ = 256;

@@ -53,7 +53,6 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
     off = align_up(off + bytes, 256);
     return o;
   };
-  const size_t o_args = take(sizeof(SrvArgs));
   const size_t o_rx = take(sizeof(float*) * N);
   const size_t o_rxt = take(sizeof(unsigned*) * N);
   const size_t o_ptag = take((size_t)N * NS_ * 4);
@@ -76,7 +75,6 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
             "hipHostMalloc(command ring)");
   hip_check(hipHostMalloc((void**)&err_host_, 2 * sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped),
             "hipHostMalloc(error word)");
-  hip_check(hipHostMalloc((void**)&args_host_, sizeof(SrvArgs), hipHostMallocDefault), "hipHostMalloc(args)");
   std::memset((void*)cmd_ring_, 0, sizeof(TagChunk) * kCmdChunks * ring_);
   err_host_[0] = err_host_[1] = 0;
   consumed_host_ = err_host_ + 1;
@@ -119,7 +117,6 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   a.cmd_ticks = (long long)(cmd_s * 1e8);
   a.tag_ticks = 10ll * 100000000ll;
   a.spin = 1 << 22;
-  args_dev_ = reinterpret_cast<SrvArgs*>(b + o_args);
   ptag_.assign(N, 0u);
   finished_.assign(N, 0);
   failed_.assign(N, 0);
@@ -141,7 +138,6 @@ PeerServer::~PeerServer() {
   if (ws_) (void)hipFree(ws_);
   if (cmd_ring_) (void)hipHostFree(cmd_ring_);
   if (err_host_) (void)hipHostFree(err_host_);
-  if (args_host_) (void)hipHostFree(args_host_);
 }
 
 void PeerServer::check_api(int rc, const char* what) const {
@@ -189,11 +185,9 @@ void PeerServer::launch() {
   a.cmd0 = cmds_;
   a.cpar = (int)(launches_ & 1);
   a.launch = ++launches_;
-  *args_host_ = a;
-  // (an SDMA copy from pinned memory and the launch: no fill / copy kernel that
-  // would need CUs another rank's persistent launch may hold on a shared GPU)
-  hip_check(hipMemcpyAsync(args_dev_, args_host_, sizeof(SrvArgs), hipMemcpyHostToDevice, stream_), "server args");
-  launch_server_persist(args_dev_, cfg_.FP, stream_);
+  // (the arguments are the kernel argument: no copy in front of the launch -- on a GPU
+  // shared with other ranks' persistent launches it could wait behind them)
+  launch_server_persist(a, cfg_.FP, stream_);
   hip_check(hipGetLastError(), "server kernel launch");
   cmds_launch_ = cmds_;
   running_ = true;

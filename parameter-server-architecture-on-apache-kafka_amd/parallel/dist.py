@@ -896,8 +896,11 @@ class DistEngine:
         fine-grained device memory -- the server its inbox (one delta slot per worker),
         a worker rank its receive slots (one per lane) -- the handles are exchanged, each
         side maps the other's, and the loops are built with EVERY allocation and fill
-        done now: on a GPU shared by several ranks (the one-GPU rehearsal) a fill kernel
-        enqueued after another rank's persistent launch could wait for its CUs."""
+        done now, and each loop's first launch too (an empty one, drained here): on a GPU
+        shared by several ranks (the one-GPU rehearsal) a fill kernel or a first launch's
+        one-time device work enqueued after another rank's persistent launch could wait
+        for its CUs -- seen as a worker rank whose host loop stalled 20 s in its first
+        launch while the server's watchdog fired."""
         cfg, sp = self.cfg, self.spec
         h = _native.hip()
         N, NS = cfg.num_workers, sp.Fp // 32
@@ -929,13 +932,14 @@ class DistEngine:
             if self.log is not None and ev is not None:
                 d.update(sink=self.log.native.handle, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=int(ev.T))
             self._pserver = h.PeerServer(d)
+            self._pserver.warm_up()
         else:
             m = h.PeerMapping(handles[0], sp.P, NS, N)
             self._peer_maps = [m]
             lp = self._alanes_build()
             ks = [w.k for w in self.workers]
             lp.set_peer(reg.data(0), reg.tags(0), reg.stride, [m.data(k) for k in ks], [m.tags(k) for k in ks])
-            lp.prepare_async()
+            lp.prepare_async()  # (with one empty launch: see LanesLoop::prepare_async)
         torch.cuda.synchronize(self.device)
         dist.barrier()
 

@@ -44,6 +44,50 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// 32 values per lane summed over the wave's 64 lanes at once: a reduce-scatter
+// butterfly (xor 32, 16, 8, 4, 2 halve the values a lane carries, xor 1 completes
+// the sum) -- 31 shuffles for all 32 sums instead of 6 per value.  Lane l returns
+// the sum of v[l >> 1].  Fixed order: bitwise reproducible.
+__device__ __forceinline__ double wave_sum_scatter32(const double (&v)[32]) {
+  const int lane = threadIdx.x & 63;
+  double a[16], b[8], c[4], d[2];
+  {
+    const bool hi = (lane & 32) != 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double keep = hi ? v[16 + j] : v[j], send = hi ? v[j] : v[16 + j];
+      a[j] = keep + __shfl_xor(send, 32, 64);
+    }
+  }
+  {
+    const bool hi = (lane & 16) != 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double keep = hi ? a[8 + j] : a[j], send = hi ? a[j] : a[8 + j];
+      b[j] = keep + __shfl_xor(send, 16, 64);
+    }
+  }
+  {
+    const bool hi = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double keep = hi ? b[4 + j] : b[j], send = hi ? b[j] : b[4 + j];
+      c[j] = keep + __shfl_xor(send, 8, 64);
+    }
+  }
+  {
+    const bool hi = (lane & 4) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const double keep = hi ? c[2 + j] : c[j], send = hi ? c[j] : c[2 + j];
+      d[j] = keep + __shfl_xor(send, 4, 64);
+    }
+  }
+  const bool hi = (lane & 2) != 0;
+  double r = (hi ? d[1] : d[0]) + __shfl_xor(hi ? d[0] : d[1], 2, 64);
+  return r + __shfl_xor(r, 1, 64);
+}
+
 // Copy N 8-byte words global -> LDS with all of a thread's loads in flight
 // before its first store (a load -> wait -> store loop pays one memory round
 // trip per word).  NTHR threads take words tid, tid + NTHR, ...

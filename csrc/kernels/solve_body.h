@@ -810,7 +810,14 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   if (wg0 && tid == 0) stamp(dv, slot, 4);
 
   // ---- partial dot products -> exchange area ----
+  // The wave's values in the all-gather's order (k < nv = 4 + 2m): gt.gt, gt.d, gt.gc,
+  // loss, then per stored pair j (oldest first, ring slot (hbase + j) mod H) S_j.gt,
+  // Y_j.gt.  Up to 32 values go through ONE multi-value butterfly per wave (a
+  // reduce-scatter over the lanes: 31 shuffles of doubles for all of them instead of
+  // 6 per value -- the dots phase was 1.5-2.3 us of every 12-us slot, profiles/r05).
   const int m = cl->m, head = cl->head;
+  const int nv = 4 + 2 * m;  // gt.gt, gt.d, gt.gc, loss, (S_j.gt, Y_j.gt) x m
+  const int hbase = head - m + 1 < 0 ? head - m + 1 + H : head - m + 1;  // (head - m + 1) mod H: > -H
   double tt = (double)gb * gb, td = (double)gb * db0, tc = (double)gb * gcb0;
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
@@ -819,35 +826,57 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
     tc += (double)g[e] * GC[e];
   }
   const double lsum = (wg0 && tid == 16) ? (double)rpart : 0.0;
-  tt = wave_sum(tt);
-  td = wave_sum(td);
-  tc = wave_sum(tc);
-  const double ls = wave_sum(lsum);
-  if (lane == 0) {
-    sdot[w * kNDX + 0] = tt;
-    sdot[w * kNDX + 1] = td;
-    sdot[w * kNDX + 2] = tc;
-    sdot[w * kNDX + kND] = ls;
-  }
-  for (int i = 0; i < H; ++i) {  // wave-uniform loop over stored pairs
-    const bool valid = pair_valid(i, m, head, H);
-    double si = 0.0, yi = 0.0;
-    if (valid) {
+  auto pair_dots = [&](int j, double& si, double& yi) {
+    int i = hbase + j;
+    if (i >= H) i -= H;
+    si = 0.0;
+    yi = 0.0;
 #pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        si += (double)s_at(i, e) * g[e];
-        yi += (double)y_at(i, e) * g[e];
-      }
-      if (ib0) {
-        si += (double)sb_at(i) * gb;
-        yi += (double)yb_at(i) * gb;
-      }
+    for (int e = 0; e < NE; ++e) {
+      si += (double)s_at(i, e) * g[e];
+      yi += (double)y_at(i, e) * g[e];
+    }
+    if (ib0) {
+      si += (double)sb_at(i) * gb;
+      yi += (double)yb_at(i) * gb;
+    }
+  };
+  if (nv <= 32) {
+    double v[32];
+    v[0] = tt;
+    v[1] = td;
+    v[2] = tc;
+    v[3] = lsum;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      double si = 0.0, yi = 0.0;
+      if (j < m) pair_dots(j, si, yi);  // (wave-uniform)
+      v[4 + 2 * j] = si;
+      v[5 + 2 * j] = yi;
+    }
+    const double r = wave_sum_scatter32(v);  // lane l: the wave's sum of value l >> 1
+    const int k = lane >> 1;
+    if ((lane & 1) == 0 && k < nv) sdot[w * kNDX + k] = r;
+  } else {  // (more than 14 stored pairs: one reduction per value)
+    tt = wave_sum(tt);
+    td = wave_sum(td);
+    tc = wave_sum(tc);
+    const double ls = wave_sum(lsum);
+    if (lane == 0) {
+      sdot[w * kNDX + 0] = tt;
+      sdot[w * kNDX + 1] = td;
+      sdot[w * kNDX + 2] = tc;
+      sdot[w * kNDX + 3] = ls;
+    }
+    for (int j = 0; j < m; ++j) {  // wave-uniform loop over the stored pairs
+      double si, yi;
+      pair_dots(j, si, yi);
       si = wave_sum(si);
       yi = wave_sum(yi);
-    }
-    if (lane == 0) {
-      sdot[w * kNDX + 3 + i] = si;
-      sdot[w * kNDX + 3 + kMaxHist + i] = yi;
+      if (lane == 0) {
+        sdot[w * kNDX + 4 + 2 * j] = si;
+        sdot[w * kNDX + 5 + 2 * j] = yi;
+      }
     }
   }
   __syncthreads();
@@ -860,16 +889,12 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
   const int ns = NS;
   // the slices share one XCD (one L2) unless the solver spreads them (cfg.xcd < 0)
   const bool xs2 = kXs == 2 && (kP == 2 || cfg.xcd >= 0);
-  // only the m stored pairs' dots travel (ring slots (head - m + 1 + j) mod H)
-  const int nv = 4 + 2 * m;  // gt.gt, gt.d, gt.gc, loss, S_i.gt (m), Y_i.gt (m)
-  const int hbase = head - m + 1 < 0 ? head - m + 1 + H : head - m + 1;  // (head - m + 1) mod H: > -H
+  // only the m stored pairs' dots travel, in the order above
   const unsigned tag = run_tag + (unsigned)slot + 1u;
   unsigned* gat32 = (unsigned*)gat;  // [ns][2*nv]
   if (tid < 2 * nv) {
     const int k = tid >> 1;
-    const int rr = hbase + (k < 4 + m ? k - 4 : k - 4 - m), ring = k < 4 ? 0 : (rr >= H ? rr - H : rr);
-    const int si = k < 3 ? k : (k == 3 ? kND : (k < 4 + m ? 3 + ring : 3 + kMaxHist + ring));
-    const double v = sdot[si] + sdot[kNDX + si] + sdot[2 * kNDX + si] + sdot[3 * kNDX + si];
+    const double v = sdot[k] + sdot[kNDX + k] + sdot[2 * kNDX + k] + sdot[3 * kNDX + k];
     const unsigned long long u = d2u(v);
     const unsigned half = (tid & 1) ? (unsigned)(u >> 32) : (unsigned)u;
     if (ns > 1) {
@@ -931,8 +956,8 @@ __device__ __forceinline__ void bwd_body(const SolverCfg& cfg, const SolveParams
       v += u2d(u);
     }
     // order expected by ctrl_step: 3 scalars, S_i.g (H ring slots), Y_i.g (H); loss in dots[kND]
-    const int rr = hbase + (tid < 4 + m ? tid - 4 : tid - 4 - m), ring = tid < 4 ? 0 : (rr >= H ? rr - H : rr);
-    const int pos = tid < 3 ? tid : (tid == 3 ? kND : (tid < 4 + m ? 3 + ring : 3 + H + ring));
+    const int rr = hbase + ((tid - 4) >> 1), ring = tid < 4 ? 0 : (rr >= H ? rr - H : rr);
+    const int pos = tid < 3 ? tid : (tid == 3 ? kND : (((tid - 4) & 1) == 0 ? 3 + ring : 3 + H + ring));
     dots[pos] = v;
   }
   __syncthreads();

@@ -886,6 +886,11 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("prepare_async", &LanesLoop::prepare_async)
       .def("set_async_debug", &LanesLoop::set_async_debug, py::arg("buf"), py::arg("cap"))
       .def("set_injection", &LanesLoop::set_injection, py::arg("crash"), py::arg("stop"), py::arg("drop"))
+      .def("set_trace", &LanesLoop::set_trace, py::arg("cap"))
+      .def("trace_take", [](LanesLoop& lp, uintptr_t s) { return lp.trace_take(reinterpret_cast<hipStream_t>(s)); },
+           py::arg("stream"))
+      .def("clock_ref", [](LanesLoop& lp, uintptr_t s) { return lp.clock_ref(reinterpret_cast<hipStream_t>(s)); },
+           py::arg("stream"))
       .def_property_readonly("crashed", &LanesLoop::crashed)
       .def_property_readonly("left", &LanesLoop::left)
       .def_property_readonly("async_log", &LanesLoop::async_log)

@@ -219,6 +219,10 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
     dv.dbg[30 * 16 + 10] = t_rel;
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
+  // --trace: released / solved parked in the lane's two words behind the ring (no
+  // registers held across the solve), copied to the ticket's entry after the push
+  long long* tr_park = a.tr ? a.tr + (size_t)a.tr_cap * 4 + 2 * l : nullptr;
+  if (tr_park && wg == 0 && tid == 0) tr_park[0] = rt_now();
   // ---- 2. the solve (as lanes_round_kernel) ----
   {
     char* lf = lds;
@@ -337,6 +341,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   }
   ++run;
   if (wg == 0 && tid == 0) stamp(dv, 30, 4);
+  if (a.tr && wg == 0 && tid == 0) a.tr[(size_t)a.tr_cap * 4 + 2 * l + 1] = rt_now();
   // the record's late fields again from the broadcast area (nothing but the window and
   // the snapshot is kept live across the solve: registers for the solve's pointers)
   {
@@ -371,6 +376,14 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
     x_barrier(A.flags, wg, kLaneWg, ++lw, err, spin);
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 6);
+  if (a.tr && wg == 0 && tid == 0) {
+    long long* e = a.tr + (size_t)(t % (unsigned long long)a.tr_cap) * 4;
+    const long long* pk = a.tr + (size_t)a.tr_cap * 4 + 2 * l;
+    e[0] = l;
+    e[1] = pk[0];
+    e[2] = pk[1];
+    e[3] = rt_now();
+  }
   if (wg == 0 && tid == 0)
     st_sys_chunk(a.tok, (unsigned)(a.ring * 16), (unsigned)((t % (unsigned long long)a.ring) * 16ull),
                  TagChunk{(unsigned)t, (unsigned)l, (unsigned)(unsigned long long)q.vc,

@@ -146,6 +146,10 @@ struct LanesArgs {
   int cpar;
   int xcd0;             // lane l runs on XCD xcd0 + l (processes sharing a GPU take disjoint XCDs)
   int spin_max;         // cross-workgroup wait budget (0: default)
+  // --trace / --perf_log: each lane's phase times of this round (s_memrealtime ticks) ->
+  // tr[(tr_slot * kMaxLanes + lane) * 4 + {0 stage, 1 solve, 2 solved, 3 updated}]; null: off
+  long long* tr;
+  int tr_slot;
   int nride;            // rider workgroups
   EvalMulti ev;
   // lane_eval = 1: each lane evaluates its own local model of THIS round right after
@@ -192,6 +196,8 @@ constexpr int kSlabCells = 64;
 constexpr int kEvalGroups = 8;  // EvalMulti::gq: tile queues (pair groups) at most
 constexpr int kSlabRiders = 1024;  // slab rows allocated (riders of one launch at most)
 void launch_lanes_publish(const EvalMulti& ev, hipStream_t s);
+// --trace: the device clock (s_memrealtime, 100 MHz) into *out (pinned host memory).
+void launch_clock_probe(long long* out, hipStream_t s);
 // XCC_ID of every workgroup of a 2048-workgroup launch -> ids[2048] (device).
 void launch_xcc_probe(int* ids, int n, hipStream_t s);
 // Every lane's last delta [P] and training loss to caller buffers in ONE launch (the
@@ -356,6 +362,10 @@ struct AsyncArgs {
   // applied, at dbg_delta[(t - 1) % dbg_cap][P]; nullptr: off
   float* dbg_delta;
   int dbg_cap;
+  // --trace / --perf_log: per ticket t -> tr[(t % tr_cap) * 4 + {0 lane, 1 released,
+  // 2 solved, 3 pushed}] (s_memrealtime ticks); null: off
+  long long* tr;
+  int tr_cap;
 };
 
 // The launch's uniform arguments, in device memory (see AsyncLaneDev).

@@ -170,8 +170,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       if (wg == 0 && tid < K) b_pre = a.w[(size_t)K * FPr + tid];
     }
   }
+  // --trace: the lane's phase times of this round (one lane thread)
+  auto trace = [&](int k) {
+    if (a.tr && wg == 0 && tid == 0) a.tr[((size_t)a.tr_slot * kMaxLanes + l) * 4 + k] = rt_now();
+  };
   // ---- phase I: stage + ingest + window statistics, then x0 / first trial point ----
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
+  trace(0);
   if (row) {
     lane_stage_stats<FP, S>(lf, lsy, cfg, dv, rr, a.dsX, a.dsy, wt, wg, ntr, ntt,
                             lanes[l].spart + (size_t)wg * FP * 2);
@@ -186,6 +191,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   }
   barrier();
   if (wg == 0 && tid == 0) stamp(dv, 30, 3);
+  trace(1);
   // ---- slots (as solve_persist_kernel) ----
   // Every workgroup a slice owner (G == NS: the window has no more tiles than the
   // model has 32-feature slices): the controller's phase is in every workgroup's
@@ -226,6 +232,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   }
   if (owner) {
     if (wg == 0 && tid == 0) stamp(dv, 30, 4);
+    trace(2);
     // ---- finalisation of this slice (delta written through for the cross-lane sum) ----
     if (!inplace) {
       FinIn<KP> in;
@@ -253,6 +260,7 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
                                      a.round},
                            wg);
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
+    trace(3);
   }
   if constexpr (!LE) {
     join_eval();
@@ -380,6 +388,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void l
   }
 }
 }  // namespace
+
+namespace {
+__global__ void clock_probe_kernel(long long* out) {
+  if (threadIdx.x == 0) __hip_atomic_store(out, rt_now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+void launch_clock_probe(long long* out, hipStream_t s) { clock_probe_kernel<<<1, 64, 0, s>>>(out); }
 
 void launch_lanes_publish(const EvalMulti& ev, hipStream_t s) {
   if (ev.nmodels <= 0 || !ev.slab) return;

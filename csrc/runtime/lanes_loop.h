@@ -155,6 +155,14 @@ class LanesLoop {
   // leaves cleanly after stop[l] more solves (its last delta applied, then retired).
   // Empty vectors: none.  The workers concerned: crashed() / left() after the run.
   void set_injection(const std::vector<int64_t>& crash, const std::vector<int64_t>& stop, bool drop);
+  // --trace / --perf_log: record every lane's phase times on the device (ring of cap
+  // rounds / tickets; 0: off).  trace_take synchronises `s` and returns the entries
+  // since the last take: BSP {0, round, lane, worker, stage, solve, solved, updated},
+  // asynchronous {1, ticket, lane, worker, released, solved, pushed, 0} in s_memrealtime
+  // ticks (100 MHz); clock_ref = {host CLOCK_MONOTONIC ns before, device ticks, ns after}.
+  void set_trace(int cap);
+  std::vector<std::vector<int64_t>> trace_take(hipStream_t s);
+  std::vector<int64_t> clock_ref(hipStream_t s);
   const std::vector<int>& crashed() const { return crashed_; }
   const std::vector<int>& left() const { return left_; }
   // Debug (tests): every applied ticket's delta into buf [cap][P] (device, slot (t - 1) %
@@ -348,6 +356,11 @@ class LanesLoop {
   std::vector<int64_t> inj_crash_, inj_stop_;  // set_injection (consumed by the next run_async)
   bool inj_drop_ = true;
   std::vector<int> crashed_, left_;             // workers that crashed / left in the last run
+  long long* tr_ = nullptr;                     // set_trace ring (device)
+  int tr_cap_ = 0;
+  int64_t tr_n_ = 0, tr_taken_ = 0;             // BSP rounds recorded / taken
+  std::vector<int64_t> tr_round_;               // round of each BSP ring slot
+  uint64_t tr_tick_ = 0;                        // asynchronous: last ticket taken
   std::vector<uint8_t> lane_stopped_;           // lanes already sent their stop record (this launch)
   std::vector<int64_t> want_vc_;
   struct RunRec {

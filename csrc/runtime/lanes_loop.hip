@@ -4,6 +4,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <ctime>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -329,6 +330,7 @@ LanesLoop::~LanesLoop() {
   if (aev_out_) (void)hipEventDestroy(aev_out_);
   if (tok_host_) (void)hipHostFree(tok_host_);
   if (err_host_) (void)hipHostFree(err_host_);
+  if (tr_) (void)hipFree(tr_);
 }
 
 void LanesLoop::check(int64_t rc, const char* what) const {
@@ -692,6 +694,12 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     // (from the injected round on: a round whose workgroups happen to arrive together
     // polls nothing, so one round alone would not always time out)
     a.spin_max = (inject_round_ >= 0 && r >= inject_round_) ? inject_spin_ : 0;
+    if (tr_) {
+      a.tr = tr_;
+      a.tr_slot = (int)(tr_n_ % tr_cap_);
+      tr_round_[a.tr_slot] = r;
+      ++tr_n_;
+    }
     if (L > 0 || a.ev.nmodels > 0) {
       if (a.nride == 0) a.nride = rider_count(0, L);
       if (rider_dbg_ && a.ev.nmodels > 0) {  // PSX_LANES_STAMPS: this launch's rider timeline
@@ -1177,6 +1185,65 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   return true;
 }
 
+void LanesLoop::set_trace(int cap) {
+  if (tr_) {
+    hip_check(hipDeviceSynchronize(), "trace ring free");
+    (void)hipFree(tr_);
+    tr_ = nullptr;
+  }
+  tr_cap_ = cap > 0 ? cap : 0;
+  tr_n_ = tr_taken_ = 0;
+  tr_tick_ = aticket_;
+  if (!tr_cap_) return;
+  const size_t bytes = ((size_t)tr_cap_ * kMaxLanes * 4 + 2 * kMaxLanes) * sizeof(long long);
+  hip_check(hipMalloc((void**)&tr_, bytes), "trace ring");
+  hip_check(hipMemset(tr_, 0, bytes), "trace ring");
+  tr_round_.assign((size_t)tr_cap_, -1);
+}
+
+std::vector<std::vector<int64_t>> LanesLoop::trace_take(hipStream_t s) {
+  std::vector<std::vector<int64_t>> out;
+  if (!tr_) return out;
+  hip_check(hipStreamSynchronize(s), "trace take");
+  hip_check(hipDeviceSynchronize(), "trace take");  // (the round / asynchronous streams too)
+  std::vector<long long> h((size_t)tr_cap_ * kMaxLanes * 4);
+  hip_check(hipMemcpy(h.data(), tr_, h.size() * sizeof(long long), hipMemcpyDeviceToHost), "trace copy");
+  const int L = cfg_.L;
+  // BSP rounds
+  const int64_t first = std::max(tr_taken_, tr_n_ - (int64_t)tr_cap_);
+  for (int64_t n = first; n < tr_n_; ++n) {
+    const int sl = (int)(n % tr_cap_);
+    for (int l = 0; l < L; ++l) {
+      const long long* e = h.data() + ((size_t)sl * kMaxLanes + l) * 4;
+      out.push_back({0, tr_round_[sl], l, cfg_.k[l], e[0], e[1], e[2], e[3]});
+    }
+  }
+  tr_taken_ = tr_n_;
+  // asynchronous tickets (their entries are [t % cap][4] in the same ring)
+  const uint64_t t0 = std::max<uint64_t>(tr_tick_, aticket_ > (uint64_t)tr_cap_ ? aticket_ - tr_cap_ : 0);
+  for (uint64_t t = t0 + 1; t <= aticket_; ++t) {
+    const long long* e = h.data() + (size_t)(t % (uint64_t)tr_cap_) * 4;
+    const int l = (int)e[0];
+    out.push_back({1, (int64_t)t, l, (l >= 0 && l < L) ? cfg_.k[l] : -1, e[1], e[2], e[3], 0});
+  }
+  tr_tick_ = aticket_;
+  return out;
+}
+
+std::vector<int64_t> LanesLoop::clock_ref(hipStream_t s) {
+  long long* h = nullptr;
+  hip_check(hipHostMalloc((void**)&h, sizeof(long long), hipHostMallocDefault), "clock probe");
+  *h = 0;
+  timespec a{}, b{};
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  launch_clock_probe(h, s);
+  hip_check(hipStreamSynchronize(s), "clock probe");
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  const int64_t ticks = *h;
+  (void)hipHostFree(h);
+  return {(int64_t)a.tv_sec * 1000000000ll + a.tv_nsec, ticks, (int64_t)b.tv_sec * 1000000000ll + b.tv_nsec};
+}
+
 std::string LanesLoop::launch_report() {
   // (failure reports) how far the current persistent launch got: its workgroups that
   // claimed a lane slot per XCD and all that started, read on a stream of its own
@@ -1267,6 +1334,8 @@ void LanesLoop::launch_async(hipStream_t stream, bool remote) {
   a.xcd0 = cfg_.xcd0;
   if (remote) a.w = nullptr;
   a.dbg_delta = remote ? nullptr : dbg_delta_;
+  a.tr = tr_;
+  a.tr_cap = tr_cap_;
   a.dbg_cap = dbg_cap_ > 0 ? dbg_cap_ : 1;
   a.launch = ++launch_no_;
   a.cpar = (int)(launches_ & 1);

@@ -269,7 +269,7 @@ class LocalEngine:
         if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
         W = [w for w in self.workers if w.k not in self.failed]
-        if not W or len(W) > 8 or self.tracer.enabled or self.evalset is None:
+        if not W or len(W) > 8 or self.evalset is None:
             return False
         sp = self.spec
         for w in W:
@@ -318,11 +318,20 @@ class LocalEngine:
                  delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W])
         d.update(ev.ell_args())  # (the asynchronous lanes' evaluation reads the sparse test rows)
         lp = h.LanesLoop(d, None)
+        if self.tracer.enabled:  # --trace / --perf_log: phase times recorded by the kernels
+            lp.set_trace(1024)
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
             lp.inject_spin_timeout(int(rr), int(sp_))
         self._lanes, self._lanes_key = lp, key
         return lp
+
+    def _lane_trace(self, lp, stream, ups: float):
+        """--trace / --perf_log of a lanes loop: the phase times its kernels recorded on the
+        device since the last call, placed on the host timeline by one clock probe."""
+        rows = lp.trace_take(stream)
+        if rows:
+            self.tracer.lane_rows(rows, lp.clock_ref(stream), ups)
 
     def _run_bsp_lanes(self, max_rounds: int | None = None, t_start: float | None = None) -> dict:
         """BSP rounds of every live worker in the native multi-lane loop: one launch
@@ -381,6 +390,8 @@ class LocalEngine:
                     todo = min(todo, min(w.crash_at - w.iters for w in crashing))
                 n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
                 r += n
+                if self.tracer.enabled:  # (a synchronisation per chunk of rounds: tracing only)
+                    self._lane_trace(lp, stream, (srv.updates + n * len(W) - u0) / max(1e-9, time.time() - t_start))
                 # the roles' counters advance with every chunk, so a checkpoint taken
                 # here carries the updates / clocks of the rounds it covers
                 srv.updates += n * len(W)
@@ -499,6 +510,8 @@ class LocalEngine:
                 n = int(lp.run_async(int(todo), stream, float(cfg.worker_timeout_s), deadline_ms, budget))
                 done += n
                 srv.updates += n
+                if self.tracer.enabled:
+                    self._lane_trace(lp, stream, done / max(1e-9, time.time() - t_start))
                 for i, w in enumerate(W):
                     w.source.next_local = int(lp.next_local(i))
                     w._seen_at_solve = int(lp.seen_at_solve(i))

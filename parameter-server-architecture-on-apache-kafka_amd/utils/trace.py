@@ -126,10 +126,62 @@ class Tracer:
         for rnd, ts, host_us, phases, ups in self._rows:
             dev = {}
             for name, evs in phases.items():
-                dev[name] = sum(a.elapsed_time(b) * 1000.0 for a, b in evs) if self._gpu else float("nan")
+                if isinstance(evs, float):  # (lane_rows: device time already in us)
+                    dev[name] = evs
+                else:
+                    dev[name] = sum(a.elapsed_time(b) * 1000.0 for a, b in evs) if self._gpu else float("nan")
             cols = [dev.get(p, 0.0) for p in ("ingest", "solve", "comm", "server")]
             self._perf_fh.write(f"{rnd};{ts};{host_us:.1f};" + ";".join(f"{c:.1f}" for c in cols) + f";{ups:.2f}\n")
         self._rows.clear()
+
+    # ---- the native lanes loops: device phase times recorded by the kernels ----------
+    def lane_rows(self, rows, ref, ups: float = 0.0):
+        """Phase times the lanes kernels recorded on the device (LanesLoop.trace_take,
+        s_memrealtime ticks of 10 ns) -> "device" trace events and logs-perf.csv rows.
+        ``ref`` = LanesLoop.clock_ref: (host CLOCK_MONOTONIC ns before, device ticks, ns
+        after) -- time.perf_counter_ns's clock on Linux -- places them on the host
+        timeline.  BSP rows {0, round, lane, worker, stage, solve, solved, updated}: one
+        perf row per round (ingest = staging + window statistics, solve, server = the
+        update, the slowest lane of each); asynchronous rows {1, ticket, lane, worker,
+        released, solved, pushed}: one perf row per update."""
+        if not self.enabled or not rows:
+            return
+        off_us = (ref[0] + ref[2]) / 2000.0 - ref[1] / 100.0
+
+        def us(t):
+            return off_us + t / 100.0
+
+        rounds = {}
+        for r in rows:
+            kind, n, lane, k = int(r[0]), int(r[1]), int(r[2]), int(r[3])
+            t = [int(x) for x in r[4:8]]
+            if kind == 0:
+                if min(t) <= 0:
+                    continue
+                spans = (("ingest", t[0], t[1]), ("solve", t[1], t[2]), ("server", t[2], t[3]))
+            else:
+                if min(t[:3]) <= 0:
+                    continue
+                spans = (("solve", t[0], t[1]), ("push", t[1], t[2]))
+            if self.path is not None:
+                with self._lock:
+                    for name, a, b in spans:
+                        self.events.append({"name": name, "ph": "X", "ts": us(a), "dur": (b - a) / 100.0,
+                                            "pid": self.pid, "tid": "device", "cat": "gpu",
+                                            "args": {"round" if kind == 0 else "ticket": n, "lane": lane,
+                                                     "worker": k}})
+            if self.perf_path is not None:
+                ph = rounds.setdefault((kind, n), {"_t0": spans[0][1], "_t1": spans[-1][2]})
+                ph["_t0"] = min(ph["_t0"], spans[0][1])
+                ph["_t1"] = max(ph["_t1"], spans[-1][2])
+                for name, a, b in spans:
+                    key = "server" if name == "push" else name
+                    ph[key] = max(ph.get(key, 0.0), (b - a) / 100.0)
+        for (kind, n), ph in sorted(rounds.items()):
+            span_us = (ph.pop("_t1") - ph.pop("_t0")) / 100.0
+            self._rows.append((n, int(time.time() * 1000), span_us, ph, ups))
+        if len(self._rows) >= 4096:
+            self._flush_perf()
 
     # ------------------------------------------------------------------
     def close(self):

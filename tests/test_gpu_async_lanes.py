@@ -282,3 +282,26 @@ def test_bsp_lanes_crash_dropped_and_delay(cuda):
     assert [w.iters for w in eng.workers] == [8, 8, 4]
     assert out["updates"] == 4 * 3 + 4 * 2
     assert 0.002 * 8 <= out["elapsed_s"]  # the 2 ms straggler holds every round
+
+
+def test_async_lanes_trace_and_perf_log(cuda, tmp_path):
+    """--trace / --perf_log on the async lanes loop: the kernels record each update's
+    released / solved / pushed times on the device; one perf row per update and device
+    "solve" spans on the host timeline (no Python scheduler)."""
+    import json
+
+    eng = _engine(cuda, -1, workers=3, iters=6, log_dir=str(tmp_path), perf_log=True,
+                  trace_path=str(tmp_path / "t.json"))
+    assert eng._async_lanes_ok()
+    out = eng.run()
+    assert out["async_lanes"] and out["updates"] == 18
+    rows = [r.split(";") for r in (tmp_path / "logs-perf.csv").read_text().strip().split("\n")[1:]]
+    assert len(rows) == 18 and [int(r[0]) for r in rows] == sorted(int(r[0]) for r in rows)
+    assert all(5.0 < float(r[4]) < 50000.0 for r in rows)  # the solve's device time (us)
+    ev = json.loads((tmp_path / "t.json").read_text())["traceEvents"]
+    dev = [e for e in ev if e.get("tid") == "device" and e["name"] == "solve"]
+    assert len(dev) == 18 and {e["args"]["worker"] for e in dev} == {0, 1, 2}
+    host = [e for e in ev if e.get("tid") != "device"]
+    if host:  # device spans sit inside the run's host time frame
+        t0 = min(e["ts"] for e in ev if e.get("tid") != "device") - 1e6
+        assert all(e["ts"] > t0 for e in dev)

@@ -161,3 +161,36 @@ def test_perf_log_and_trace(tmp_path):
     assert [int(r.split(";")[0]) for r in rows[1:]] == [0, 1, 2, 3, 4]
     ev = json.loads((tmp_path / "t.json").read_text())["traceEvents"]
     assert {"ingest", "solve", "server"} <= {e["name"] for e in ev}
+
+
+def test_tracer_lane_rows(tmp_path):
+    """Tracer.lane_rows (the lanes loops' device phase stamps, 100 MHz ticks) -> device
+    trace spans on the host timeline and one perf row per round / per update."""
+    import json
+
+    from psx.utils.trace import Tracer
+
+    tr = Tracer(str(tmp_path / "t.json"), perf_path=str(tmp_path / "logs-perf.csv"))
+    ref = (2_000_000_000, 1_000_000, 2_000_010_000)  # host ns around the probe, device ticks
+    base = 1_000_000
+    bsp = []
+    for rnd in (4, 5):
+        for lane in range(2):
+            t0 = base + rnd * 10_000 + lane * 10
+            bsp.append([0, rnd, lane, lane, t0, t0 + 1500, t0 + 6500 + lane * 100, t0 + 7000 + lane * 100])
+    bsp.append([0, 6, 0, 0, 0, 0, 0, 0])  # a round the kernel never stamped: skipped
+    tr.lane_rows(bsp, ref, ups=123.0)
+    tr.lane_rows([[1, 9, 1, 3, base, base + 4000, base + 4500, 0]], ref, ups=7.0)
+    tr.close()
+    rows = [r.split(";") for r in (tmp_path / "logs-perf.csv").read_text().strip().split("\n")[1:]]
+    assert [int(r[0]) for r in rows] == [4, 5, 9]
+    # round 4: ingest 15 us, solve = the slower lane's 51 us, server 5 us, span 71.1 us
+    assert float(rows[0][3]) == pytest.approx(15.0) and float(rows[0][4]) == pytest.approx(51.0)
+    assert float(rows[0][6]) == pytest.approx(5.0) and float(rows[0][2]) == pytest.approx(71.1)
+    assert float(rows[2][4]) == pytest.approx(40.0) and float(rows[2][6]) == pytest.approx(5.0)
+    ev = json.loads((tmp_path / "t.json").read_text())["traceEvents"]
+    dev = [e for e in ev if e.get("tid") == "device"]
+    assert len(dev) == 2 * 2 * 3 + 2
+    off_us = (ref[0] + ref[2]) / 2000.0 - ref[1] / 100.0
+    s4 = [e for e in dev if e["name"] == "solve" and e["args"].get("round") == 4 and e["args"]["lane"] == 0][0]
+    assert s4["ts"] == pytest.approx(off_us + (base + 40_000 + 1500) / 100.0) and s4["dur"] == pytest.approx(50.0)

@@ -388,6 +388,7 @@ class LocalEngine:
                     if crashed:
                         break
                     todo = min(todo, min(w.crash_at - w.iters for w in crashing))
+                self._t_lp_run_ns = time.perf_counter_ns()  # (tools/round_timeline.py)
                 n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
                 r += n
                 if self.tracer.enabled:  # (a synchronisation per chunk of rounds: tracing only)
@@ -405,6 +406,7 @@ class LocalEngine:
                 if n < todo:  # a worker's stream is exhausted and its window empty, or the deadline
                     break
             t_loop = time.time()
+            self._t_lp_done_ns = time.perf_counter_ns()
             lp.flush(stream)
             # stream-ordered behind the rounds: the last local solve's loss / delta for code
             # that reads the roles, and the Python-side evaluation fragments of the global

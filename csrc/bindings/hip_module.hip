@@ -850,6 +850,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.new_rows = (int)I("new_rows", 0);
              c.new_frac = D("new_frac", 0.0);
              c.new_cap = (int)I("new_cap", 0);
+             c.new_ramp = (int)I("new_ramp", 0);
              c.log_worker = (int)I("log_worker", 0);
              c.delay_us = d.contains("delay_us") ? d["delay_us"].cast<std::vector<int>>() : std::vector<int>{};
              c.xcd0 = (int)I("xcd0", 0);
@@ -909,7 +910,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("host_busy_us_per_token", &LanesLoop::host_busy_us_per_token)
       .def("seen_at_solve", &LanesLoop::seen_at_solve)
       .def("set_seen_at_solve", &LanesLoop::set_seen_at_solve)
-      .def("new_tuples_needed", &LanesLoop::new_tuples_needed)
+      .def("new_tuples_needed", &LanesLoop::new_tuples_needed, py::arg("size"), py::arg("updates") = -1)
       .def("flush", [](LanesLoop& l, uintptr_t stream) { l.flush(S(stream)); })
       .def("set_sink", &LanesLoop::set_sink)
       .def("set_lr", &LanesLoop::set_lr)

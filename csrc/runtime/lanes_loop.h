@@ -87,6 +87,8 @@ struct LanesLoopCfg {
   int new_rows = 0;
   double new_frac = 0.0;
   int new_cap = 0;
+  // ... capped at new_ramp << (the lane's completed solves) for its first solves (0: off)
+  int new_ramp = 0;
   // asynchronous consistency (run_async): the worker whose deltas produce the
   // server rows (ServerProcessor.java:154: worker 0, or the lowest live one;
   // -1: none) and injected straggler delays per lane (us, tests / fault injection)
@@ -194,7 +196,7 @@ class LanesLoop {
   int64_t seen_at_solve(int lane) const { return seen_at_solve_.at(lane); }
   void set_seen_at_solve(int lane, int64_t v) { seen_at_solve_.at(lane) = v; }
   // new tuples lane windows of `size` rows wait for (0: no cadence)
-  int64_t new_tuples_needed(int64_t size) const;
+  int64_t new_tuples_needed(int64_t size, int64_t updates = -1) const;  // updates < 0: no ramp
   bool exhausted(int lane) const { return next_local_[lane] >= local_total_[lane] * cfg_.epochs; }
   bool all_exhausted() const;
   int hand_off_scope() const { return S_; }  // 2: one-XCD hand-offs, 1: sc1 (placement check failed)

@@ -72,7 +72,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   if (cfg_.per_iter_rows <= 0 && !(cfg_.p_ms > 0.0) && cfg_.L > 0)
     throw std::invalid_argument("LanesLoop: need rows per round or a producer period");
   if (!cfg_.w) throw std::invalid_argument("LanesLoop: no server weights");
-  if (cfg_.new_rows < 0 || cfg_.new_frac < 0.0 || cfg_.new_cap < 0)
+  if (cfg_.new_rows < 0 || cfg_.new_frac < 0.0 || cfg_.new_cap < 0 || cfg_.new_ramp < 0)
     throw std::invalid_argument("LanesLoop: negative cadence");
   const bool evaluates = cfg_.sink && (cfg_.log_server || cfg_.log_workers);
   if (evaluates && (!cfg_.Xt || !cfg_.yt || cfg_.T <= 0)) throw std::invalid_argument("LanesLoop: no test set");
@@ -558,10 +558,14 @@ void LanesLoop::check_errors(int64_t round) {
   }
 }
 
-int64_t LanesLoop::new_tuples_needed(int64_t size) const {
+int64_t LanesLoop::new_tuples_needed(int64_t size, int64_t updates) const {
   int64_t k = (int64_t)std::ceil(cfg_.new_frac * (double)size);  // as math.ceil in config.py
   if (k < 0) k = 0;
   if (cfg_.new_cap > 0 && k > cfg_.new_cap) k = cfg_.new_cap;
+  if (cfg_.new_ramp > 0 && updates >= 0 && updates < 30) {  // the first solves come early
+    const int64_t r = (int64_t)cfg_.new_ramp << updates;
+    if (k > r) k = r;
+  }
   return k > cfg_.new_rows ? k : cfg_.new_rows;
 }
 
@@ -630,7 +634,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
         a.r[l].start = (int)start;
         seen[l] = sn;
         rows &= size > 0;
-        const int64_t need = new_tuples_needed(size);
+        const int64_t need = new_tuples_needed(size, r);  // (BSP: every lane solved r times)
         ready &= size > 0 && (need <= 0 || sn - seen_at_solve_[l] >= need || exhausted(l));
       }
       if (ready) break;
@@ -1136,7 +1140,7 @@ bool LanesLoop::try_release(int lane, int64_t vc, double now_ms, int64_t snap) {
   poll_async(lane, now_ms);
   int64_t size = 0, start = 0, sn = 0;
   check(api().window_state(reinterpret_cast<void*>(cfg_.window[lane]), &size, &start, &sn), "window state");
-  const int64_t need = new_tuples_needed(size);
+  const int64_t need = new_tuples_needed(size, vc);  // (vc: the worker's completed pushes)
   if (!(size > 0 && (need <= 0 || sn - seen_at_solve_[lane] >= need || exhausted(lane)))) return false;
   seen_at_solve_[lane] = sn;
   RelRec q;

@@ -104,6 +104,10 @@ def server_parser() -> argparse.ArgumentParser:
     g.add_argument("--iter_new_cap", type=int, default=128,
                    help="cap of the new tuples --iter_new_frac waits for (0: none): a 1024-row window at 10 tps "
                         "would otherwise update every ~50 s")
+    g.add_argument("--iter_new_ramp", type=int, default=0,
+                   help="a worker's first local solves wait for at most R, 2R, 4R, ... new tuples (0: off): "
+                        "at a low producer rate the frac / cap rule alone holds the first update back for tens "
+                        "of seconds (evaluation/README.md section 5)")
     g.add_argument("--inprocess", action="store_true",
                    help="run server + all workers in this process on one device (single-GPU / CPU mode)")
     g.add_argument("--async_scheduler", default="auto", choices=["auto", "events", "threads"],
@@ -178,7 +182,7 @@ def server_config(a) -> PSConfig:
         label_col=a.label_col, num_features=a.num_features, num_classes=a.num_classes,
         num_workers=a.num_workers, consistency_model=a.consistency_model,
         producer_time_per_event=a.producer_time_per_event, stream_mode=a.stream_mode,
-        rows_per_iter=a.rows_per_iter, iter_new_rows=a.iter_new_rows, iter_new_frac=a.iter_new_frac, iter_new_cap=a.iter_new_cap, epochs=a.epochs, init=a.init, seed=a.seed, server_lr=a.server_lr,
+        rows_per_iter=a.rows_per_iter, iter_new_rows=a.iter_new_rows, iter_new_frac=a.iter_new_frac, iter_new_cap=a.iter_new_cap, iter_new_ramp=a.iter_new_ramp, epochs=a.epochs, init=a.init, seed=a.seed, server_lr=a.server_lr,
         solver=solver, max_iters=a.max_iters, max_wallclock_s=a.max_wallclock_s, idle_exit_s=a.idle_exit_s,
         logging=a.logging, log_dir=a.log_dir, verbose=a.verbose, bsp_schedule=a.bsp_schedule,
         server_colocated=False, checkpoint_dir=a.checkpoint_dir, checkpoint_every=a.checkpoint_every,

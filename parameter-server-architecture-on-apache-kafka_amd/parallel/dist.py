@@ -623,7 +623,7 @@ class DistEngine:
                      xcd0=(self.worker_id * len(W)) if (W and getattr(comm, "kind", "rccl") == "ipc") else 0,
                      sink=self.log.native.handle if self.log is not None else 0,
                      tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0,
-                     new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap))
+                     new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), new_ramp=int(cfg.iter_new_ramp))
             if W:
                 ds = W[0].source.ds
                 d.update(dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows))
@@ -1117,7 +1117,7 @@ class DistEngine:
                      sb=[f.b.data_ptr() for f in self._alanes_frags], Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T,
                      sink=self.log.native.handle, api=_native.host.capi(), log_server=0,
                      log_workers=int(cfg.log_workers), new_rows=int(cfg.iter_new_rows),
-                     new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), log_worker=-1,
+                     new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), new_ramp=int(cfg.iter_new_ramp), log_worker=-1,
                      delay_us=[int(round(float(cfg.inject_worker_delay_ms.get(w.k, 0.0)) * 1000.0)) for w in W],
                      # ranks sharing one GPU (the one-GPU rehearsals): worker rank i's lanes on XCDs
                      # i*wpr ..; on its own GPU a rank's lanes start at XCD 0 and may take all 8 (no

@@ -47,6 +47,10 @@ class PSConfig:
     # many times over, which over-fits it (evaluation/README.md)
     iter_new_frac: float = 0.0
     iter_new_cap: int = 128  # ... but never more than this many new tuples per iteration (0: no cap)
+    # ... and a worker's first local solves wait for at most ramp, 2 ramp, 4 ramp, ... new
+    # tuples (0: off): at a low producer rate the frac / cap rule alone would hold the
+    # first update back for tens of seconds (evaluation/README.md section 5)
+    iter_new_ramp: int = 0
     # buffer
     min_buffer_size: int = 128
     max_buffer_size: int = 1024
@@ -118,15 +122,20 @@ def cadence_free(c: "PSConfig") -> bool:
     return c.rows_per_iter >= new_tuples_needed(c, c.max_buffer_size)
 
 
-def new_tuples_needed(c: "PSConfig", window: int) -> int:
+def new_tuples_needed(c: "PSConfig", window: int, updates: int | None = None) -> int:
     """New tuples a worker with a `window`-row buffer waits for before its next
     local solve: iter_new_rows, or the iter_new_frac share of the window capped at
     iter_new_cap (a large window at a high rate would otherwise wait for hundreds
-    of tuples between updates)."""
+    of tuples between updates).  With iter_new_ramp R and the worker's completed
+    local solves `updates`, the share is also capped at R * 2^updates (the first
+    updates of a slow stream come early; None: no ramp)."""
     import math
 
     k = math.ceil(c.iter_new_frac * int(window))
     if c.iter_new_cap > 0:
         k = min(k, c.iter_new_cap)
+    ramp = int(getattr(c, "iter_new_ramp", 0) or 0)
+    if ramp > 0 and updates is not None and updates < 30:
+        k = min(k, ramp << max(0, int(updates)))
     return max(c.iter_new_rows, k)
 

@@ -311,7 +311,7 @@ class LocalEngine:
                  shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
                  sb=[f.b.data_ptr() for f in self._lane_frags], scoff=0, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(),
                  T=ev.T, sink=self.log.native.handle, tracker=srv.tracker.handle, api=_native.host.capi(),
-                 new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap),
+                 new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), new_ramp=int(cfg.iter_new_ramp),
                  # the asynchronous loop: server rows on the lowest live worker's deltas
                  # (ServerProcessor.java:154), straggler delays on the device
                  log_worker=min(w.k for w in W),

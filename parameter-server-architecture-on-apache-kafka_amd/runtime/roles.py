@@ -124,7 +124,7 @@ class WorkerRole:
         window only re-fits the same rows)."""
         if self.window.size <= 0:
             return False
-        K = new_tuples_needed(self.cfg, int(self.window.size))
+        K = new_tuples_needed(self.cfg, int(self.window.size), self.iters)
         return K <= 0 or self.tuples_seen - self._seen_at_solve >= K or self.source.exhausted
 
     def compute(self, log=None) -> torch.Tensor:

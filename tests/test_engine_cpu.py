@@ -222,3 +222,18 @@ def test_synth_finefood_round1_generator():
     assert not torch.equal(a.X, b.X)
     n = a.float_features().norm(dim=1)
     assert torch.allclose(n, torch.ones_like(n), atol=1e-2)
+
+
+def test_cadence_ramp():
+    """--iter_new_ramp R: a worker's first solves wait for at most R, 2R, 4R, ... new
+    tuples; afterwards (and without a solve count) the frac / cap rule alone."""
+    from psx.runtime.config import PSConfig, new_tuples_needed
+
+    c = PSConfig(iter_new_frac=0.5, iter_new_cap=128, iter_new_ramp=8)
+    assert [new_tuples_needed(c, 1024, u) for u in range(6)] == [8, 16, 32, 64, 128, 128]
+    assert [new_tuples_needed(c, 128, u) for u in range(5)] == [8, 16, 32, 64, 64]
+    assert new_tuples_needed(c, 1024) == 128 and new_tuples_needed(c, 1024, 40) == 128
+    off = PSConfig(iter_new_frac=0.5, iter_new_cap=128)
+    assert new_tuples_needed(off, 1024, 0) == 128
+    rows = PSConfig(iter_new_rows=20, iter_new_frac=0.5, iter_new_cap=128, iter_new_ramp=8)
+    assert new_tuples_needed(rows, 1024, 0) == 20  # iter_new_rows stays a floor

@@ -260,8 +260,10 @@ def test_lanes_cadence_fraction_and_cap(cuda):
 
     spec, train, ev = _data(cuda)
     w = spec.init("zeros", device=cuda)
-    lp, keep = _loop(spec, [0], 1, train, ev, w, cuda, rows=16, new_frac=0.3, new_cap=100)
-    c = PSConfig(iter_new_frac=0.3, iter_new_cap=100)
+    lp, keep = _loop(spec, [0], 1, train, ev, w, cuda, rows=16, new_frac=0.3, new_cap=100, new_ramp=4)
+    c = PSConfig(iter_new_frac=0.3, iter_new_cap=100, iter_new_ramp=4)
+    for u in range(8):  # the ramp of the first solves (C++ and Python agree)
+        assert lp.new_tuples_needed(1000, u) == new_tuples_needed(c, 1000, u), u
     for size in (1, 10, 16, 300, 333, 1024):
         assert lp.new_tuples_needed(size) == new_tuples_needed(c, size), size
 

@@ -66,7 +66,7 @@ def launch(a, tr, te):
                "-training", tr, "-test", te, "-p", str(p), "-c", str(c), "--num_workers", str(n), "-l",
                "--log_dir", d, "--max_wallclock_s", str(a.seconds), "--async_scheduler", "threads",
                "--iter_new_rows", str(a.iter_new_rows), "--iter_new_frac", str(a.iter_new_frac),
-               "--iter_new_cap", str(a.iter_new_cap)]
+               "--iter_new_cap", str(a.iter_new_cap), "--iter_new_ramp", str(a.iter_new_ramp)]
         procs.append((name, subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=open(os.path.join(d, "run.out"), "w"),
                                              stderr=subprocess.STDOUT)))
 
@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--runs", default="", help="comma-separated run names (default: all 8)")
     ap.add_argument("--max-concurrent", dest="max_concurrent", type=int, default=8,
                     help="engines running at once (on one GPU every one is a process of its own)")
+    ap.add_argument("--iter_new_ramp", type=int, default=0, help="first solves wait for R, 2R, 4R, ... new tuples")
     ap.add_argument("--iter_new_rows", type=int, default=0,
                     help="worker cadence: iterate after this many new tuples (0: continuously, the reference's way)")
     a = ap.parse_args()

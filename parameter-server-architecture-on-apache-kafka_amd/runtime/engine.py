@@ -265,6 +265,19 @@ class LocalEngine:
         return all(w.source.ds.rows // max(1, self.cfg.num_workers) >= w.ring.cap for w in W)
 
     def _lanes_shape_ok(self) -> bool:
+        # (cached per engine: its workers' rings, sources and solver options are fixed at
+        # construction -- 16 us of Python per call otherwise, in every bench.py step
+        # window; profiles/r05/README.md section 10)
+        key = (tuple(sorted(self.failed)), os.environ.get("PSX_NATIVE_LANES", "1"), self.evalset is None,
+               self.cfg.stream_mode, self.cfg.rows_per_iter, self.cfg.producer_time_per_event)
+        hit = getattr(self, "_shape_ok", None)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        ok = self._lanes_shape_check()
+        self._shape_ok = (key, ok)
+        return ok
+
+    def _lanes_shape_check(self) -> bool:
         c = self.cfg
         if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
@@ -288,8 +301,11 @@ class LocalEngine:
         key = tuple(w.k for w in W)
         lp = getattr(self, "_lanes", None)
         if lp is not None and self._lanes_key == key:
-            lp.set_sink(self.log.native.handle)
-            lp.set_lr(float(self.cfg.lr))
+            bound = (self.log.native.handle, float(self.cfg.lr))
+            if bound != getattr(self, "_lanes_bound", None):  # (rebound only when they change)
+                lp.set_sink(bound[0])
+                lp.set_lr(bound[1])
+                self._lanes_bound = bound
             return lp
         from ..ops.lr import Fragments
 
@@ -324,6 +340,7 @@ class LocalEngine:
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
             lp.inject_spin_timeout(int(rr), int(sp_))
         self._lanes, self._lanes_key = lp, key
+        self._lanes_bound = (self.log.native.handle, float(cfg.lr))
         return lp
 
     def _lane_trace(self, lp, stream, ups: float):

@@ -174,6 +174,9 @@ struct LanesArgs {
   unsigned round;
   unsigned* applied;  // [FP/32]
   unsigned* evdone;
+  // multi-rank (dsum): += 1 per slice once its lane sum is written back (agent scope);
+  // the host starts the round's collectives on its own stream at NS * rounds (null: off)
+  unsigned* dsum_done;
   // lane_riders = 1 (tile-resident form, ev.form == 1): every lane workgroup joins the
   // evaluation as a rider once its part of the round is done (ev.nticket counts the
   // nride riders + L * kLaneWg lane workgroups); the tiles come from ev.xq[0]

@@ -254,11 +254,20 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     }
     // ---- the BSP update: the last lane to finish a slice applies the sum ----
     if (wg == 0 && tid == 0) stamp(dv, 30, 5);
-    if (lane_arrive(a.arrive, wg, L, flag))
+    if (lane_arrive(a.arrive, wg, L, flag)) {
       lane_apply_slice<FP>(cfg, lanes,
                            ApplyArgs{L, a.w, a.lr, a.dsum, a.shi, a.slo, a.sb, a.scoff, a.ovl ? a.applied : nullptr,
                                      a.round},
                            wg);
+      if (a.dsum_done) {  // this slice's lane sum is final: written back for the collective's kernels
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          (void)__hip_atomic_fetch_add(a.dsum_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
     trace(3);
   }

@@ -296,6 +296,13 @@ class LanesLoop {
   unsigned* claim_ = nullptr;
   int64_t launches_ = 0;
   float* dsum_ = nullptr;
+  // multi-rank: the round's collectives on their own stream, started by the kernel's
+  // dsum_done counter (PSX_EARLY_COLL, default on) instead of behind the whole launch
+  bool early_coll_ = false;
+  unsigned* dsum_done_ = nullptr;
+  uint64_t coll_n_ = 0;           // rounds whose dsum the counter has announced (NS per round)
+  hipStream_t cstream_ = nullptr;
+  hipEvent_t coll_ev_ = nullptr;
   uint16_t *upd_hi_ = nullptr, *upd_lo_ = nullptr;  // fragments of an update nobody evaluates
   float* upd_b_ = nullptr;
   unsigned long long* err_host_ = nullptr;  // pinned [kMaxLanes]

@@ -225,6 +225,7 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   applied_ = reinterpret_cast<unsigned*>(b + o_ovl);
   evdone_ = applied_ + 32;
   ovlq_ = applied_ + 48;
+  dsum_done_ = applied_ + 40;  // (multi-rank; the overlap words are unused then)
   slab_ = reinterpret_cast<int*>(b + o_slab);
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
@@ -284,6 +285,18 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // the slots while the next round runs
   const char* sl = std::getenv("PSX_RIDERS_SLAB");
   slab_on_ = ovl_ && tile_riders_ && !(sl && sl[0] == '0');
+  // PSX_EARLY_COLL=1 (default off): a rank with lanes and a communicator starts the
+  // round's reduce / all-reduce, update and broadcast on a stream of its own as soon as
+  // every slice's lane sum is written, while the launch's riders still evaluate the
+  // previous round's rows.  Off by default: the world-1 RCCL rehearsal measured 71.9k
+  // against 79.5k updates/s (profiles/r05/s37) -- the cross-stream hand-off costs more
+  // than a one-rank collective saves; unmeasured on several GPUs
+  const char* ec = std::getenv("PSX_EARLY_COLL");
+  early_coll_ = comm_ && cfg_.L > 0 && ec && ec[0] == '1';
+  if (early_coll_) {
+    hip_check(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking), "hipStreamCreate(collectives)");
+    hip_check(hipEventCreateWithFlags(&coll_ev_, hipEventDisableTiming), "hipEventCreate");
+  }
   if (ovl_) {
     hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
     hip_check(hipEventCreateWithFlags(&ovl_in_, hipEventDisableTiming), "hipEventCreate");
@@ -331,6 +344,11 @@ LanesLoop::~LanesLoop() {
   if (tok_host_) (void)hipHostFree(tok_host_);
   if (err_host_) (void)hipHostFree(err_host_);
   if (tr_) (void)hipFree(tr_);
+  if (cstream_) {
+    (void)hipStreamSynchronize(cstream_);
+    (void)hipStreamDestroy(cstream_);
+  }
+  if (coll_ev_) (void)hipEventDestroy(coll_ev_);
 }
 
 void LanesLoop::check(int64_t rc, const char* what) const {
@@ -684,6 +702,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.w = cfg_.w;
     a.lr = cfg_.lr;
     a.dsum = comm_ ? dsum_ : nullptr;
+    a.dsum_done = (early_coll_ && L > 0) ? dsum_done_ : nullptr;
     a.shi = cfg_.shi[par];
     a.slo = cfg_.slo[par];
     a.sb = cfg_.sb[par];
@@ -750,20 +769,34 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     nlrec = 0;
     // ---- multi-rank: lane sums -> server (reduce), update, weights -> every rank ----
     if (comm_) {
+      // (early collectives: on cstream_ once the kernel announced every slice's sum; the
+      // next round's launch on `stream` waits for them below)
+      hipStream_t cs = stream;
+      if (early_coll_ && L > 0) {
+        ++coll_n_;
+        const int NSl = cfg_.scfg.Fp / 32;
+        hip_check(hipStreamWaitValue32(cstream_, dsum_done_, (uint32_t)((uint64_t)NSl * coll_n_), hipStreamWaitValueGte),
+                  "collectives wait for the lane sums");
+        cs = cstream_;
+      }
       if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
       if (cfg_.allreduce) {  // every replica applies the same summed update
-        comm_->all_reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, stream);
+        comm_->all_reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, cs);
         launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr,
                             cfg_.shi[par] ? cfg_.shi[par] : upd_hi_, cfg_.shi[par] ? cfg_.slo[par] : upd_lo_,
-                            cfg_.shi[par] ? cfg_.sb[par] : upd_b_, stream, cfg_.scoff);
+                            cfg_.shi[par] ? cfg_.sb[par] : upd_b_, cs, cfg_.scoff);
       } else {  // push: reduce to the server rank; update there; pull: broadcast
-        comm_->reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, cfg_.server_rank, stream);
+        comm_->reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, cfg_.server_rank, cs);
         if (is_server)
           launch_server_apply(cfg_.scfg.K, cfg_.scfg.F, cfg_.scfg.Fp, cfg_.w, dsum_, cfg_.lr, cfg_.shi[par],
-                              cfg_.slo[par], cfg_.sb[par], stream, cfg_.scoff);
-        comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, Comm::kF32, cfg_.server_rank, stream);
+                              cfg_.slo[par], cfg_.sb[par], cs, cfg_.scoff);
+        comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, Comm::kF32, cfg_.server_rank, cs);
       }
       hip_check(hipGetLastError(), "server update launch");
+      if (cs != stream) {  // everything after the round on `stream` (the next launch) follows them
+        hip_check(hipEventRecord(coll_ev_, cs), "collectives done");
+        hip_check(hipStreamWaitEvent(stream, coll_ev_, 0), "collectives done");
+      }
     }
     (void)KF;
     // ---- this round's rows: evaluated by the next launch, or side launch now ----

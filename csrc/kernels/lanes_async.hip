@@ -195,18 +195,33 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   // outstanding stores, e.g. the last evaluation's pinned-slot chunks, need not land first)
   // (no budget of their own for the others: the leader's release wait is bounded and
   // ends in a stop record)
+  // (the broadcast area's address in a register across the barrier: read from the lane
+  // table behind the acquire it would be one more memory round trip, after the invalidate)
+  const unsigned long long* const rec = A.rec;
   x_barrier(A.flags, wg, kLaneWg, ++lw, err, 0x7fffffff, /*drain=*/wg == 0);
-  // the lane's rows, state and the pulled snapshot were written by other CUs
-  // (other XCDs for the snapshot) since this CU last read them
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const long long t_bar = dv.dbg ? rt_now() : 0;
   RelRec q;
   {
+    // The record BEFORE the acquire: nt loads are served by the XCD's L2, which the
+    // leader's stores reached before its barrier word (drain), so they need no
+    // invalidate -- and their round trip no longer waits behind it (the record read
+    // behind the fence took 7.5 us of the lane's ~100-us iteration, profiles/r05/s39)
     TagChunk ch[kRelChunks];
 #pragma unroll
-    for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(A.rec + 2 * i);
+    for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(rec + 2 * i);
+    // the lane's rows, state and the pulled snapshot were written by other CUs
+    // (other XCDs for the snapshot) since this CU last read them.  ONE wave invalidates
+    // the CU's L1 and waits for it, the others wait at the workgroup barrier: four
+    // waves fencing queue four invalidates (6-7.8 us measured, profiles/r05/s41)
+    if (tid < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     unpack_release(ch, q);
     relc = ch[0].tag;  // the record consumed
   }
+  const long long t_acq = dv.dbg ? rt_now() : 0;
   if (q.stop) {
     if (wg == 0 && tid == 0) {
       *A.relc = relc;
@@ -217,6 +232,8 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
   if (wg == 0 && tid == 0 && dv.dbg) {
     dv.dbg[30 * 16 + 9] = t_it;
     dv.dbg[30 * 16 + 10] = t_rel;
+    dv.dbg[30 * 16 + 11] = t_bar;
+    dv.dbg[30 * 16 + 12] = t_acq;
   }
   if (wg == 0 && tid == 0) stamp(dv, 30, 0);
   // --trace: released / solved parked in the lane's two words behind the ring (no
@@ -272,6 +289,7 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
         }
         if (c < K) A.wpull[(size_t)c * FP + f] = wo_pre;
         if (wg == 0 && tid < K) A.wpull[(size_t)K * FP + tid] = b_pre;
+        if (wg == 0 && tid == 0) stamp(dv, 30, 13);  // (the pulled weights read)
         // (the error word was cleared before this iteration's first barrier: this
         // store is not wiped and FinScal::store reports it with the solve)
         if (!a.remote && tid == 0 &&
@@ -284,7 +302,9 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
       if (row) {
         lane_stage_stats<FP, S>(lf, lsy, cfg, dv, q.r, a.dsX, a.dsy, wt, wg, ntr, ntt, A.spart + (size_t)wg * FP * 2);
       }
+      if (wg == 0 && tid == 0) stamp(dv, 30, 14);  // (staged)
       barrier();
+      if (wg == 0 && tid == 0) stamp(dv, 30, 15);  // (every row workgroup staged)
       if (owner) {
         lane_prep<FP, KP, S>(lb, cfg, dv, A.spart, ntr, win.B, wg, wo_pre, b_pre);
         if (tid == 0) ctrl_init(*cl);

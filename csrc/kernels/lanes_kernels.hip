@@ -128,8 +128,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (one wave: the L1 is the CU's, and four waves fencing queue four invalidates;
+    // behind every polling wave)
+    if constexpr (NS > 64) __syncthreads();
+    if (tid < 64) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   }
   const unsigned run = a.ovl ? __hip_atomic_load(dv.prm_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)

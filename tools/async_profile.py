@@ -53,7 +53,13 @@ def main():
             us = lambda x, y: round((T(y) - T(x)) / 100.0, 2) if T(x) and T(y) else None
             ln = {"solve": us(0, 4), "ticket": us(4, 5), "apply": us(5, 6), "token": us(6, 7), "eval": us(7, 8),
                   # the last iteration's start: release record seen, the lane-wide barrier
-                  "wait_release": us(9, 10), "barrier": us(10, 0)}
+                  "wait_release": us(9, 10), "barrier": us(10, 0),
+                  # (its parts: the lane-wide barrier; the record read + the acquire fence;
+                  # from there to the released stamp)
+                  "barrier_wait": us(10, 11), "record+acquire": us(11, 12), "to_stamp": us(12, 0),
+                  # (the solve's start: the pulled weights read, this workgroup's rows staged,
+                  # every row workgroup staged)
+                  "s.pull": us(0, 13), "s.stage": us(13, 14), "s.stage_barrier": us(14, 15)}
             # the solve's slots (the same stamps as the BSP round kernel: tools/lanes_profile.py)
             from lanes_profile import phases
             ends = [st[(24 + (w >> 4)) * 16 + (w & 15)] for w in range(32)]

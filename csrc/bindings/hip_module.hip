@@ -913,6 +913,7 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("new_tuples_needed", &LanesLoop::new_tuples_needed, py::arg("size"), py::arg("updates") = -1)
       .def("flush", [](LanesLoop& l, uintptr_t stream) { l.flush(S(stream)); })
       .def("set_sink", &LanesLoop::set_sink)
+      .def("set_idle_wait", &LanesLoop::set_idle_wait)
       .def("set_lr", &LanesLoop::set_lr)
       .def("next_local", &LanesLoop::next_local)
       .def("set_next_local", &LanesLoop::set_next_local)

@@ -207,8 +207,23 @@ __device__ __forceinline__ bool async_iteration(char* lds, const SolverCfg& cfg_
     // invalidate -- and their round trip no longer waits behind it (the record read
     // behind the fence took 7.5 us of the lane's ~100-us iteration, profiles/r05/s39)
     TagChunk ch[kRelChunks];
+    // every chunk must carry one tag at least the one the leader waited for: a line of
+    // an older record still in this CU's L1 would otherwise replay the previous window
+    // silently -- re-read until they do (bounded: a persistent mismatch is error 12)
+    const unsigned want = (unsigned)(relc + 1ull);
+    for (int tries = 0;; ++tries) {
 #pragma unroll
-    for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(rec + 2 * i);
+      for (int i = 0; i < kRelChunks; ++i) ch[i] = ld_nt_chunk(rec + 2 * i);
+      bool fresh = (int)(ch[0].tag - want) >= 0;
+#pragma unroll
+      for (int i = 1; i < kRelChunks; ++i) fresh &= ch[i].tag == ch[0].tag;
+      if (__syncthreads_and(fresh ? 1 : 0)) break;
+      if (tries >= 4096) {
+        if (tid == 0) xstore(err, 12ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
     // the lane's rows, state and the pulled snapshot were written by other CUs
     // (other XCDs for the snapshot) since this CU last read them.  ONE wave invalidates
     // the CU's L1 and waits for it, the others wait at the workgroup barrier: four

@@ -189,6 +189,10 @@ class LanesLoop {
   // Evaluate the last round's rows (one launch of riders only).
   void flush(hipStream_t stream);
   void set_sink(uintptr_t sink) { cfg_.sink = sink; }
+  // Idle waits of run_async / run_async_remote (a row-starved stream, a lane waiting for
+  // its release): this bound, never below the in-flight watchdog max_wait_s (the CLI's
+  // --idle_wait; default 600 s).  A short --worker_timeout then only bounds busy workers.
+  void set_idle_wait(double s) { idle_wait_s_ = s > 0.0 ? s : 600.0; }
   void set_lr(float lr) { cfg_.lr = lr; }
   int64_t next_local(int lane) const { return next_local_.at(lane); }
   void set_next_local(int lane, int64_t v) { next_local_.at(lane) = v; }
@@ -386,7 +390,8 @@ class LanesLoop {
   std::vector<int> lane_of_;            // worker id -> lane (-1: not on this loop)
   int log_lane_ = -1;
   int64_t launch_no_ = 0;
-  double rel_wait_s_ = 60.0;  // the host loop's no-progress limit of the current run (the lanes' wait budget)
+  double rel_wait_s_ = 60.0;  // the lanes' release / pull wait budget of the current run (device)
+  double idle_wait_s_ = 600.0;  // set_idle_wait
   std::vector<hipEvent_t> pull_ev_;     // remote mode: a lane's weights received
   // peer data plane (set_peer): receive region, per-lane inbox slots, the pull tag of
   // each lane's pending release

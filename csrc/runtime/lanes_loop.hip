@@ -1419,13 +1419,19 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
   // where this run starts: the lanes the tracker has dispatched (bootstrap: all, vc
   // 0, MessageTracker.java:47-53), the others wait for a release
   for (int l = 0; l < L; ++l) {
+    // a worker the tracker retired (it crashed or left in an earlier call: its `sent` bit
+    // stays set) never starts again -- its lane stays gone and gets a stop record below
+    const int live = api().tracker_is_live(trk, cfg_.k[l]);
+    check(live, "tracker state");
     const int sent = api().tracker_is_sent(trk, cfg_.k[l]);
     check(sent, "tracker state");
-    state_[l] = sent ? kWant : kIdle;
+    state_[l] = !live ? kGone : (sent ? kWant : kIdle);
     want_vc_[l] = api().tracker_clock(trk, cfg_.k[l]);
     check(want_vc_[l], "tracker clock");
   }
-  rel_wait_s_ = max_wait_s;
+  // the lanes' release waits (the device) and the row-starved waits below are idle waits:
+  // bounded by the idle limit, not by the in-flight watchdog max_wait_s
+  rel_wait_s_ = std::max(max_wait_s, idle_wait_s_);
   // fault injection of this run (set_injection), consumed here
   const std::vector<int64_t> crash = std::move(inj_crash_), stop = std::move(inj_stop_);
   inj_crash_.clear();
@@ -1562,7 +1568,7 @@ int64_t LanesLoop::run_async(int64_t updates, hipStream_t stream, double max_wai
       if (deadline_ms > 0.0 && now >= deadline_ms) break;
       start_ready(now - cfg_.t0_ms);  // every dispatched lane waits for rows (producer clock / cadence)
       if (running == 0) {
-        if (now - wait0 > max_wait_s * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
+        if (now - wait0 > idle_wait_s_ * 1000.0) throw std::runtime_error("LanesLoop: no rows for a worker");
         std::this_thread::sleep_for(std::chrono::microseconds(200));
       } else {
         wait0 = epoch_ms();
@@ -1618,7 +1624,7 @@ int64_t LanesLoop::run_async_remote(P2P* p2p, uintptr_t ctrl, uintptr_t reply, i
   enum { kWaitPull = 3, kPulling = 4, kDone = 5 };
   for (int l = 0; l < L; ++l) state_[l] = kWaitPull;  // the server's begin() sends everybody its clock
   std::vector<int64_t> it(L, 0);
-  rel_wait_s_ = max_wait_s;
+  rel_wait_s_ = std::max(max_wait_s, idle_wait_s_);
   launch_async(stream, true);
   int64_t done = 0;
   int running = 0, finished = 0;

@@ -135,6 +135,9 @@ def server_parser() -> argparse.ArgumentParser:
                    help="worker K leaves the run cleanly (final push) after ITER iterations")
     g.add_argument("--worker_timeout", type=float, default=600.0,
                    help="watchdog: a worker busy and silent this many seconds has failed")
+    g.add_argument("--idle_wait", type=float, default=600.0,
+                   help="how long a run may wait for a worker's rows or release while nothing is in flight "
+                        "(a row-starved stream; never below --worker_timeout)")
     g.add_argument("--on_worker_failure", default="auto", choices=["auto", "drop", "fail"],
                    help="drop the failed worker and continue, or abort (auto: drop under -c -1)")
     return ap
@@ -191,7 +194,7 @@ def server_config(a) -> PSConfig:
         model=a.model, dtype=a.dtype, sigmoid=a.sigmoid, ring_nz=a.ring_nz, sparse_push=not a.dense_push, sparse_pull=not a.dense_pull,
         inject_worker_crash={k: int(v) for k, v in parse_worker_map(a.inject_worker_crash).items()},
         inject_worker_stop={k: int(v) for k, v in parse_worker_map(a.inject_worker_stop).items()},
-        worker_timeout_s=a.worker_timeout, on_worker_failure=a.on_worker_failure)
+        worker_timeout_s=a.worker_timeout, idle_wait_s=a.idle_wait, on_worker_failure=a.on_worker_failure)
 
 
 def print_params(title: str, items: dict):

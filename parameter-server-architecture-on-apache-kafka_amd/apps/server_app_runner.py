@@ -64,9 +64,13 @@ def main(argv=None) -> int:
         rank, world, dev = init_from_env(cpu=device == "cpu")
         payload = [cfg.to_dict()]
         dist.broadcast_object_list(payload, src=0)
+        eng = None
         try:
-            out = DistEngine(cfg, rank, world, dev).run()
+            eng = DistEngine(cfg, rank, world, dev)
+            out = eng.run()
         finally:
+            if eng is not None:  # the control / data planes (IPC maps, shm queues, server launch) even on failure
+                eng.close()
             dist.destroy_process_group()
     if a.verbose or not a.logging:
         print(json.dumps({k: (float(v) if hasattr(v, "item") else v) for k, v in out.items()}), file=sys.stderr)

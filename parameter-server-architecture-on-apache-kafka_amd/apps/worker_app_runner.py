@@ -44,9 +44,13 @@ def _worker_main(i: int, a_dict: dict, env: dict):
     cfg.max_buffer_size = a_dict["max_buffer_size"]
     cfg.buffer_size_coefficient = a_dict["buffer_size_coefficient"]
     cfg.logging = cfg.logging or a_dict["logging"]
+    eng = None
     try:
-        DistEngine(cfg, rank, world, dev).run()
+        eng = DistEngine(cfg, rank, world, dev)
+        eng.run()
     finally:
+        if eng is not None:  # the control / data planes (IPC maps, shm queues) even on failure
+            eng.close()
         dist.destroy_process_group()
 
 

@@ -1126,6 +1126,7 @@ class DistEngine:
                      xcd0=(self.worker_id * len(W)) if oversubscribed() else 0)
             d.update(ev.ell_args())
             lp = h.LanesLoop(d, None)
+            lp.set_idle_wait(float(cfg.idle_wait_s))
             self._alanes = lp
         return lp
 

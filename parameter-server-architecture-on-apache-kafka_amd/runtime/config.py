@@ -90,6 +90,9 @@ class PSConfig:
     inject_worker_crash: dict = field(default_factory=dict)  # worker -> iteration at which it fails
     inject_worker_stop: dict = field(default_factory=dict)  # worker -> iterations after which it leaves cleanly
     worker_timeout_s: float = 600.0  # watchdog: a busy worker silent this long has failed
+    # idle waits (a row-starved stream, a lane waiting for its release) are bounded by this,
+    # never by the watchdog above: a short --worker_timeout must not end a healthy idle run
+    idle_wait_s: float = 600.0
     on_worker_failure: str = "auto"  # drop | fail | auto (drop under eventual consistency)
     trace_path: str | None = None
     pair_eval: bool = True

@@ -146,6 +146,7 @@ class LocalEngine:
             EvalPair(self.server, self.workers[0])
         self.failed: set[int] = set()
         self.left: set[int] = set()  # workers that left cleanly (--inject_worker_stop)
+        self._trace_cap = 1024  # device trace ring of the lanes loops (rounds / tickets between takes)
         if maybe_resume(cfg, self.server, self.workers):
             self.rounds = int(self.server.tracker.min_clock())
             self.failed = {k for k in range(cfg.num_workers) if not self.server.tracker.is_live(k)}
@@ -177,6 +178,10 @@ class LocalEngine:
             out = self._run_bsp()
         elif self._async_lanes_ok():
             out = self._run_async_lanes()
+        # the Python SSP / ASP schedulers: the runs the native lanes loop cannot take --
+        # CPU runs, the wide model, fp32 rings, windows over 8,192 rows, shards shorter than
+        # a ring.  Their dense-GPU branch stays exercised by tests/test_gpu_engine.py
+        # (PSX_ASYNC_LANES=0: the crash-retirement test on the event scheduler)
         elif self._event_scheduler():
             out = self._run_async_events()
         else:
@@ -335,7 +340,8 @@ class LocalEngine:
         d.update(ev.ell_args())  # (the asynchronous lanes' evaluation reads the sparse test rows)
         lp = h.LanesLoop(d, None)
         if self.tracer.enabled:  # --trace / --perf_log: phase times recorded by the kernels
-            lp.set_trace(1024)
+            lp.set_trace(self._trace_cap)
+        lp.set_idle_wait(float(cfg.idle_wait_s))
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
             lp.inject_spin_timeout(int(rr), int(sp_))
@@ -406,7 +412,7 @@ class LocalEngine:
                         break
                     todo = min(todo, min(w.crash_at - w.iters for w in crashing))
                 self._t_lp_run_ns = time.perf_counter_ns()  # (tools/round_timeline.py)
-                n = int(lp.run(int(todo), int(r), stream, 600.0, deadline_ms))
+                n = int(lp.run(int(todo), int(r), stream, float(cfg.idle_wait_s), deadline_ms))
                 r += n
                 if self.tracer.enabled:  # (a synchronisation per chunk of rounds: tracing only)
                     self._lane_trace(lp, stream, (srv.updates + n * len(W) - u0) / max(1e-9, time.time() - t_start))
@@ -502,7 +508,10 @@ class LocalEngine:
         crashed: list[WorkerFailure] = []
         ck = bool(cfg.checkpoint_dir and cfg.checkpoint_every)
         chunk = max(1, int(cfg.checkpoint_every)) if ck else 1 << 16
+        if self.tracer.enabled:  # one device trace row per update: a chunk never outruns the trace ring
+            chunk = min(chunk, self._trace_cap)
         done = 0
+        gone: set[int] = set(self.left)  # workers that left (earlier runs) or crashed / left in an earlier chunk
         exhausted_since = None
         try:
             while True:
@@ -518,13 +527,14 @@ class LocalEngine:
                 # max_iters iterations per worker exactly (under ASP the fast workers would
                 # otherwise take the slow ones' share): each lane's remaining share, also
                 # across the chunks of a checkpointed run
-                budget = ([max(0, int(cfg.max_iters) - (int(srv.tracker.clock(w.k)) - clock_start[w.k])) for w in W]
+                budget = ([0 if w.k in gone else
+                           max(0, int(cfg.max_iters) - (int(srv.tracker.clock(w.k)) - clock_start[w.k])) for w in W]
                           if cfg.max_iters else 0)
                 if inject:  # crashes / clean leaves: solves left before each (roles.py WorkerRole.compute)
-                    crash = [max(0, w.crash_at - w.iters) if w.crash_at is not None and w.k not in self.failed
-                             else -1 for w in W]
-                    stop = [max(0, int(cfg.inject_worker_stop[w.k]) - w.iters) if w.k in cfg.inject_worker_stop
-                            else -1 for w in W]
+                    crash = [max(0, w.crash_at - w.iters) if (w.crash_at is not None and w.k not in self.failed
+                                                              and w.k not in gone) else -1 for w in W]
+                    stop = [max(0, int(cfg.inject_worker_stop[w.k]) - w.iters)
+                            if (w.k in cfg.inject_worker_stop and w.k not in gone) else -1 for w in W]
                     lp.set_injection(crash, stop, drop_on_failure(cfg))
                 n = int(lp.run_async(int(todo), stream, float(cfg.worker_timeout_s), deadline_ms, budget))
                 done += n
@@ -541,6 +551,8 @@ class LocalEngine:
                     for k in lp.crashed:  # (the loop retired it already under drop, or stopped the run)
                         crashed.append(WorkerFailure(k, f"injected crash at iteration {self.workers[k].iters}"))
                     self.left.update(int(k) for k in lp.left)
+                    gone.update(int(k) for k in lp.crashed)
+                    gone.update(int(k) for k in lp.left)
                 if n and ck:
                     maybe_checkpoint(cfg, srv, srv.updates, W)
                 if crashed and not drop_on_failure(cfg):

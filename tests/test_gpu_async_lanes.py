@@ -271,6 +271,25 @@ def test_async_lanes_stop_leaves_cleanly(cuda):
     assert out["updates"] == 23
 
 
+def test_async_lanes_leave_and_crash_across_chunks(cuda, tmp_path):
+    """ASP with checkpoints every 4 updates (a chunk of the run per checkpoint): worker 1
+    leaves after 3 iterations and worker 2 crashes at its 3rd (drop) in early chunks.  The
+    later chunks -- and a second run of the engine -- must not start either again: a retired
+    worker keeps its tracker `sent` bit, and re-starting it would push a delta the tracker
+    refuses ('delta from retired worker') or report the crash twice."""
+    eng = _engine(cuda, -1, workers=4, iters=10, inject_worker_stop={1: 3}, inject_worker_crash={2: 2},
+                  on_worker_failure="drop", checkpoint_dir=str(tmp_path / "ck"), checkpoint_every=4)
+    assert eng._async_lanes_ok()
+    out = eng.run(close_log=False)
+    assert out.get("left_workers") == [1] and out["failed_workers"] == [2]
+    assert [w.iters for w in eng.workers] == [10, 3, 2, 10]
+    assert out["updates"] == 10 + 3 + 2 + 10
+    eng.cfg.max_iters = 4  # a second run: the live workers only
+    out2 = eng.run()
+    assert out2["failed_workers"] == [2] and [w.iters for w in eng.workers] == [14, 3, 2, 14]
+    assert torch.isfinite(eng.server.w).all()
+
+
 def test_bsp_lanes_crash_dropped_and_delay(cuda):
     """BSP on the lanes loop: a straggler sleeps on the device (no Python scheduler), an
     injected crash (drop) ends a chunk at its round and the rest runs without it."""

@@ -36,9 +36,10 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--model M]
        ranks come from its environment; a plain ``python bench.py --gpus N``
        spawns the N ranks itself (before anything touches the GPU) and every
        rank checks that the world it joined has exactly N ranks.
-       --dedicated-server: BASELINE config 2 (1 server rank + N-1 worker ranks,
-       RCCL reduce + broadcast); --consistency D>0 / -1: configs 3/4 (dedicated
-       server rank, RCCL point-to-point).
+       --dedicated-server (the default): BASELINE config 2/3 (1 server rank + N-1
+       worker ranks; dense: the peer_sum schedule, no collective per round --
+       --schedule reduce_bcast for RCCL reduce + broadcast); --consistency D>0 /
+       -1: configs 3/4 (dedicated server rank, peer data plane / RCCL p2p).
 """
 from __future__ import annotations
 
@@ -86,10 +87,13 @@ def parse(argv=None):
                     help="logical workers per worker GPU, one XCD each in one launch per round (default 8: one "
                          "per XCD of the MI355X -- BASELINE's 8-worker configuration on one GPU; --workers 4 is the "
                          "reference's numWorkers = 4, all hosted in one process, BaseKafkaApp.java:25,70)")
-    ap.add_argument("--schedule", default=None, choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer"],
-                    help="multi-GPU BSP: ... peer = sequential consistency over the peer data plane (the lanes "
-                         "store their deltas into the server GPU's inbox, the server kernel applies each on "
-                         "arrival and writes the weights into the workers' receive slots over xGMI)")
+    ap.add_argument("--schedule", default=None,
+                    choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer", "peer_sum"],
+                    help="multi-GPU BSP (dense default with a dedicated server: peer_sum = each worker rank's "
+                         "lane sum stored into the server GPU's inbox by the round kernel, summed and applied "
+                         "slice-parallel by the server kernel, written back into every rank's receive slot over "
+                         "xGMI -- no collective on the round's path); reduce_bcast = RCCL reduce + broadcast; "
+                         "peer = the asynchronous loops with the sequential tracker (per-worker deltas)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay each solve as one hipGraph (dense default: eager)")
     ap.add_argument("--persist", action="store_true",
@@ -128,7 +132,12 @@ def parse(argv=None):
     if a.warmup is None:
         a.warmup = 30 if wide else 200
     if a.schedule is None:
-        a.schedule = "reduce_bcast" if a.dedicated_server else "allreduce"
+        # dense with a dedicated server: the peer_sum schedule (measured against RCCL reduce +
+        # broadcast in the one-GPU rehearsals, profiles/r06/README.md); CPU / wide: RCCL or gloo
+        if a.dedicated_server:
+            a.schedule = "peer_sum" if (not wide and not a.cpu and a.consistency == 0) else "reduce_bcast"
+        else:
+            a.schedule = "allreduce"
     if a.workers is None:  # the wide configs keep one worker per GPU; dense: one worker per XCD
         a.workers = 1 if wide else 8
     return a
@@ -217,6 +226,10 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
                f"lanes -> server inbox, server kernel -> receive slots)")
     elif async_mode:
         par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
+    elif cfg.bsp_schedule == "peer_sum":
+        par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers (peer_sum over xGMI: each "
+               f"rank's lane sum stored into the server GPU's inbox by its round kernel, summed + applied by the "
+               f"server kernel, weights written into every rank's receive slot; no collective per round)")
     elif not cfg.server_colocated:
         par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers "
                f"({backend} reduce + broadcast, {cfg.bsp_schedule})")
@@ -423,9 +436,11 @@ def bench_distributed(a):
     if dist.get_world_size() != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
     peer_bsp = a.consistency == 0 and a.schedule == "peer"
+    peer_sum = a.consistency == 0 and a.schedule == "peer_sum"
     async_mode = a.consistency != 0 or peer_bsp  # (peer BSP: the asynchronous loops, sequential tracker)
     keyrange = a.schedule == "keyrange"
-    dedicated = (async_mode or a.dedicated_server) and not keyrange  # key-range: every rank holds a shard
+    # (key-range: every rank holds a shard; peer_sum: rank 0 is the server GPU)
+    dedicated = (async_mode or a.dedicated_server or peer_sum) and not keyrange
     # workers per worker rank: --workers lanes, one XCD each (SSP / ASP / peer BSP: the lanes of one
     # persistent launch; the peer data plane runs no transfer kernel beside it, so all 8 XCDs)
     wpr = 1 if (a.model != "dense" or a.cpu) else a.workers
@@ -473,12 +488,17 @@ def bench_distributed(a):
             "workers": cfg.num_workers,
             "schedule": cfg.bsp_schedule if not async_mode else ("peer" if wpr > 1 else "p2p"),
             "native_lanes_loop": getattr(eng, "_lanes", None) is not None}
+    # where each rank's call went (untimed: after the measurement)
+    phases = [None] * world
+    dist.all_gather_object(phases, getattr(eng, "_phases", None))
     if rank == 0:
         book = eng.log.book
         summ = summarize(book)
         ups = a.steps * cfg.num_workers / dt
         res = describe(a, world, cfg, ups, dt, summ, rccl_ranks=rccl, topo=topo)
         res["max_vc_gap"] = out.get("max_vc_gap")
+        if any(p is not None for p in phases):
+            res["rank_phases"] = phases
         if "keyrange" in out:
             k = out["keyrange"]
             res["keyrange"] = dict(k, model_bytes_per_round=round(k["model_bytes"] / max(1, a.steps + a.warmup), 1),

@@ -640,6 +640,9 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.replies = V("replies");
              c.worker_timeout_s = d.contains("worker_timeout_s") ? d["worker_timeout_s"].cast<double>() : 600.0;
              c.sxcd = (int)I("sxcd", 0);
+             c.bsp = I("bsp", 0) != 0;
+             c.nwg = (int)I("nwg", kSrvWg);
+             c.tag_wait_s = d.contains("tag_wait_s") ? d["tag_wait_s"].cast<double>() : 600.0;
              prepare_kernels();
              return std::make_unique<PeerServer>(c, nullptr);
            }),
@@ -656,6 +659,10 @@ PYBIND11_MODULE(_psx_hip, m) {
             return py::make_tuple(st.code, st.worker, st.updates);
           },
           py::arg("checkpoint_every") = 0)
+      .def("run_bsp", &PeerServer::run_bsp, py::arg("rounds"), py::arg("r0"), py::call_guard<py::gil_scoped_release>())
+      .def("seed_rx", &PeerServer::seed_rx, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("bsp_rounds", &PeerServer::bsp_rounds)
+      .def_property_readonly("host_us_per_round", &PeerServer::host_us_per_round)
       .def("fail", &PeerServer::fail, py::call_guard<py::gil_scoped_release>())
       .def("stop", &PeerServer::stop, py::call_guard<py::gil_scoped_release>())
       .def("warm_up", &PeerServer::warm_up, py::call_guard<py::gil_scoped_release>())
@@ -885,6 +892,11 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("set_peer", &LanesLoop::set_peer, py::arg("rx_data"), py::arg("rx_tags"), py::arg("rx_stride"),
            py::arg("inbox"), py::arg("inbox_tag"))
       .def("prepare_async", &LanesLoop::prepare_async)
+      .def("set_peer_sum", &LanesLoop::set_peer_sum, py::arg("rx"), py::arg("rx_tag"), py::arg("push"),
+           py::arg("push_tag"), py::arg("wait_s"))
+      .def_property_readonly("peer_sum", &LanesLoop::peer_sum)
+      .def("peer_sum_tags", &LanesLoop::peer_sum_tags)
+      .def("set_xcd_skip", &LanesLoop::set_xcd_skip, py::arg("mask"))
       .def("set_async_debug", &LanesLoop::set_async_debug, py::arg("buf"), py::arg("cap"))
       .def("set_injection", &LanesLoop::set_injection, py::arg("crash"), py::arg("stop"), py::arg("drop"))
       .def("set_trace", &LanesLoop::set_trace, py::arg("cap"))

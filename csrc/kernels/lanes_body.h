@@ -545,6 +545,11 @@ struct ApplyArgs {
   // run on other XCDs in a launch that overlaps this one), then applied[slice] = round + 1
   unsigned* applied = nullptr;
   unsigned round = 0;
+  // peer_sum (LanesArgs::push): the lane sum goes to this rank's inbox slot on the server
+  // GPU (system-scope stores over xGMI), then the slice's tag push_val; w untouched
+  float* push = nullptr;
+  unsigned* push_tag = nullptr;
+  unsigned push_val = 0;
 };
 
 // Spin until *p >= want (device-scope loads); a timeout sets the sticky error word
@@ -590,6 +595,18 @@ __device__ __forceinline__ void lane_apply_slice(const SolverCfg& cfg, const Lan
       sum += dl[l];
       sumi += di[l];
     }
+  if (a.push) {  // the rank's push (WorkerTrainingProcessor.java:95-97): the server sums the ranks
+    // system-scope stores (sc0 sc1: written through to the server GPU's memory), every
+    // wave's vmcnt(0), a barrier, then the tag: no release fence -- nothing of the hand-off
+    // sits dirty in an L2 (the sc0 sc1 form of the CDNA4 playbook, at system scope), and a
+    // system-scope release would write back this XCD's whole L2 on the round's critical path
+    if (coef) st_sys_f32(a.push + e, sum);
+    if (icpt) st_sys_f32(a.push + ei, sumi);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) st_sys_u32(a.push_tag + wg, a.push_val);
+    return;
+  }
   if (coef) {
     if (a.dsum) {
       a.dsum[e] = sum;

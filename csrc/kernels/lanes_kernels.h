@@ -174,15 +174,28 @@ struct LanesArgs {
   unsigned round;
   unsigned* applied;  // [FP/32]
   unsigned* evdone;
-  // multi-rank (dsum): += 1 per slice once its lane sum is written back (agent scope);
-  // the host starts the round's collectives on its own stream at NS * rounds (null: off)
-  unsigned* dsum_done;
   // lane_riders = 1 (tile-resident form, ev.form == 1): every lane workgroup joins the
   // evaluation as a rider once its part of the round is done (ev.nticket counts the
   // nride riders + L * kLaneWg lane workgroups); the tiles come from ev.xq[0]
   int lane_riders;
   int* lacc;            // [kMaxLanes][2][256] accumulators (stride kAccStride), zero between launches
   unsigned* lticket;    // [kMaxLanes][32] per-lane evaluation arrivals
+  // peer_sum (multi-rank BSP over the peer data plane, LanesLoop::set_peer_sum; needs ovl):
+  // the last lane of slice s stores this rank's lane sum into its inbox slot on the server
+  // GPU (system-scope stores over xGMI, csrc/comm/peer_bus.h) and tags it round + 1 (the
+  // push); the launch's lane workgroups start once every slice of this rank's receive slot
+  // carries a tag >= round (the server kernel's update of round - 1, written over xGMI) and
+  // pull w from there -- no collective, no host and no kernel boundary between a round's
+  // push and the next round's pull.  push == nullptr: off
+  float* push;
+  unsigned* push_tag;
+  const float* rx;
+  const unsigned* rx_tag;
+  long long peer_ticks;  // the pull wait's wall-clock budget (s_memrealtime ticks, 100 MHz)
+  // workgroups on an XCD whose bit is set leave at once (no role, no count): ranks that
+  // share one GPU (the one-GPU rehearsals) keep off each other's and the server kernel's
+  // XCDs, so no rider spins on a CU another process's persistent launch needs
+  unsigned xcd_skip;
 };
 
 bool lanes_supported(int FP, int K, int cap);
@@ -213,6 +226,10 @@ struct LanesCopyOut {
   float* dst_l[kMaxLanes];
 };
 void launch_lanes_copy_out(const LanesCopyOut& c, hipStream_t s);
+// peer_sum, the end of a run: w[P] <- this rank's receive slot once every slice's tag is >=
+// want (the server's last update); a wait beyond `ticks` sets *err_host (code 10)
+void launch_peer_pull(const float* rx, const unsigned* rx_tag, unsigned want, float* w, int K, int FP,
+                      long long ticks, unsigned long long* err_host, hipStream_t s);
 // Evaluation of ev's models as a launch of its own that co-runs with a lanes
 // round (side stream; 8.6 KB LDS per workgroup, lanes_eval_grid() workgroups,
 // ev.nticket must equal that grid).  Same EvalSlot publication.

@@ -22,6 +22,8 @@ int lanes_grid(int L, int min_riders) {
 namespace {
 using namespace lanes_detail;
 
+constexpr int kSkipRole = -(1 << 30);  // a workgroup on an XCD of LanesArgs::xcd_skip
+
 // LE: the lanes evaluate their own models after the solve (LanesArgs::lane_eval).  A
 // template flag, not a run-time test: the evaluation tail compiled into the kernel
 // costs the solve its registers (1208 B of scratch against 120 B without it).
@@ -37,17 +39,23 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       if (a.ev.dbg)  // PSX_LANES_STAMPS: the earliest workgroup entry of the launch ([15])
         atomicMin((unsigned long long*)(a.ev.dbg + 15), (unsigned long long)__builtin_amdgcn_s_memrealtime());
       unsigned* c = a.claim + 32 * a.cpar;
-      if (b == 0) {  // the other parity's counters (the previous launch has claimed) for the next launch
+      const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
+      const bool skip = ((a.xcd_skip >> xcc) & 1u) != 0u;
+      // (a skipped workgroup -- another process's XCD -- may be placed late: it touches
+      // nothing, and the first workgroup of every other XCD resets the counters instead)
+      if (b < 8 && !skip) {  // the other parity's counters (the previous launch has claimed) for the next launch
         for (int j = 0; j < 32; ++j)
           __hip_atomic_store(a.claim + 32 * (a.cpar ^ 1) + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (reset before this launch counts as dispatched)
       }
-      // every workgroup: the launch is fully dispatched once this reaches the grid (the
-      // next overlapped launch waits for that before its own dispatch)
-      (void)__hip_atomic_fetch_add(c + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // every workgroup not skipped: the launch is fully dispatched once this reaches the
+      // grid less the skipped XCDs' share (the next overlapped launch waits for that)
+      if (!skip) (void)__hip_atomic_fetch_add(c + 9, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int r = -1;
-      if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
-        const int lx = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u) - a.xcd0;  // HW_REG_XCC_ID
+      if (skip) {
+        r = kSkipRole;  // another process's XCD (shared-GPU rehearsals): leave at once
+      } else if constexpr (S == 2) {  // the XCD this workgroup runs on decides its lane
+        const int lx = xcc - a.xcd0;
         if (lx >= 0 && lx < L) {
           const unsigned k = __hip_atomic_fetch_add(c + lx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (k < (unsigned)kLaneWg) r = lx * kLaneWg + (int)k;
@@ -55,12 +63,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
       } else if (b < 8 * kLaneWg && (b & 7) - a.xcd0 >= 0 && (b & 7) - a.xcd0 < L) {  // spread: any placement works
         r = ((b & 7) - a.xcd0) * kLaneWg + (b >> 3);
       }
-      if (r < 0) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
+      if (r == -1) r = -(int)__hip_atomic_fetch_add(c + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
       role = r;
     }
     __syncthreads();
     const int r = __builtin_amdgcn_readfirstlane(role);  // (uniform: lane / workgroup indices in SGPRs)
     __syncthreads();
+    if (r == kSkipRole) return;
     if (r < 0) {  // a rider: the previous round's evaluation
       if (a.ovl && a.ev.nmodels > 0)  // round - 1's launch complete: its fragments written back
         wait_ge(a.evdone, a.round, (unsigned long long*)nullptr, a.spin_max > 0 ? a.spin_max : 1 << 22);
@@ -118,19 +127,36 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     if (tid == 0) ovl_late = 0;
     __syncthreads();
     if (tid < NS) {
-      const int sp = spin_limit(dv);
-      int spins = 0;
-      while ((int)(__hip_atomic_load(a.applied + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.round) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > sp) {  // never expected: reported below (after this round's error word is cleared)
-          ovl_late = 1;
-          break;
+      if (a.rx_tag) {
+        // peer_sum: this slice of the server's update of round - 1, written into this
+        // rank's receive slot over xGMI (system scope), then its tag; a wall-clock budget
+        // (the slowest rank's round, which may wait for its rows, gates the update)
+        const long long t_end = rt_now() + a.peer_ticks;
+        while ((int)(ld_sys_u32(a.rx_tag + tid) - a.round) < 0) {
+          if (rt_now() > t_end) {
+            ovl_late = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      } else {
+        const int sp = spin_limit(dv);
+        int spins = 0;
+        while ((int)(__hip_atomic_load(a.applied + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.round) < 0) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > sp) {  // never expected: reported below (after this round's error word is cleared)
+            ovl_late = 1;
+            break;
+          }
         }
       }
     }
     // (one wave: the L1 is the CU's, and four waves fencing queue four invalidates;
     // behind every polling wave)
     if constexpr (NS > 64) __syncthreads();
+    // (peer_sum: the receive slot is read with system-scope loads below, which the
+    // server's sc0 sc1 stores + tag need no acquire for; this CU's L1 still needs the
+    // agent acquire for the previous round's rings and workspaces)
     if (tid < 64) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -166,8 +192,13 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
   if (owner) {
     const int c = tid >> 5, f = wg * 32 + (tid & 31);
     if (a.ovl) {  // the previous round's update of this slice is in w (written through, waited for above)
-      if (c < K && f < cfg.F) wo_pre = ld_sc1(a.w + (size_t)c * FPr + f);
-      if (wg == 0 && tid < K) b_pre = ld_sc1(a.w + (size_t)K * FPr + tid);
+      if (a.rx) {  // peer_sum: in this rank's receive slot (the server GPU's system-scope stores)
+        if (c < K && f < cfg.F) wo_pre = ld_sys_f32(a.rx + (size_t)c * FPr + f);
+        if (wg == 0 && tid < K) b_pre = ld_sys_f32(a.rx + (size_t)K * FPr + tid);
+      } else {
+        if (c < K && f < cfg.F) wo_pre = ld_sc1(a.w + (size_t)c * FPr + f);
+        if (wg == 0 && tid < K) b_pre = ld_sc1(a.w + (size_t)K * FPr + tid);
+      }
       if (c < K) lanes[l].wpull[(size_t)c * FPr + f] = wo_pre;  // the solve's w_old (this slice)
       if (wg == 0 && tid < K) lanes[l].wpull[(size_t)K * FPr + tid] = b_pre;
     } else {
@@ -262,16 +293,8 @@ __global__ __launch_bounds__(256) void lanes_round_kernel(SolverCfg cfg, const L
     if (lane_arrive(a.arrive, wg, L, flag)) {
       lane_apply_slice<FP>(cfg, lanes,
                            ApplyArgs{L, a.w, a.lr, a.dsum, a.shi, a.slo, a.sb, a.scoff, a.ovl ? a.applied : nullptr,
-                                     a.round},
+                                     a.round, a.push, a.push_tag, a.round + 1u},
                            wg);
-      if (a.dsum_done) {  // this slice's lane sum is final: written back for the collective's kernels
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          (void)__hip_atomic_fetch_add(a.dsum_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
     }
     if (wg == 0 && tid == 0) stamp(dv, 30, 6);
     trace(3);
@@ -433,6 +456,35 @@ __global__ __launch_bounds__(256) void lanes_copy_out_kernel(LanesCopyOut c) {
   if (dl && blockIdx.x == 0 && threadIdx.x == 0) *dl = *pick(cc.src_l, l);
 }
 }  // namespace
+
+namespace {
+// block s: slice s of w (32 features x K classes; block 0 also the intercepts) from the
+// receive slot once its tag reached `want`
+__global__ __launch_bounds__(256) void peer_pull_kernel(const float* rx, const unsigned* rx_tag, unsigned want,
+                                                        float* w, int K, int FP, long long ticks,
+                                                        unsigned long long* err_host) {
+  const int s = (int)blockIdx.x, tid = threadIdx.x;
+  __shared__ int late;
+  if (tid == 0) {
+    const long long t_end = rt_now() + ticks;
+    bool l = false;
+    while ((int)(ld_sys_u32(rx_tag + s) - want) < 0 && !(l = rt_now() > t_end)) __builtin_amdgcn_s_sleep(4);
+    late = l ? 1 : 0;
+    if (l && err_host) __hip_atomic_store(err_host, 10ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (late) return;
+  const int c = tid >> 5, f = s * 32 + (tid & 31);
+  if (c < K) w[(size_t)c * FP + f] = ld_sys_f32(rx + (size_t)c * FP + f);
+  if (s == 0 && tid < K) w[(size_t)K * FP + tid] = ld_sys_f32(rx + (size_t)K * FP + tid);
+}
+}  // namespace
+
+void launch_peer_pull(const float* rx, const unsigned* rx_tag, unsigned want, float* w, int K, int FP,
+                      long long ticks, unsigned long long* err_host, hipStream_t s) {
+  if (K < 1 || K > 8 || FP < 32 || FP % 32) return;
+  peer_pull_kernel<<<FP / 32, 256, 0, s>>>(rx, rx_tag, want, w, K, FP, ticks, err_host);
+}
 
 void launch_lanes_copy_out(const LanesCopyOut& c, hipStream_t s) {
   if (c.L < 1 || c.L > kMaxLanes) return;

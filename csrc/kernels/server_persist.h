@@ -36,12 +36,17 @@
 namespace psx {
 
 constexpr int kSrvWg = 32;        // workgroups of the server launch (one XCD)
+// SrvCmd::k of a peer_sum BSP round (LanesArgs::push): sum the N worker RANKS' inbox slots
+// (each already the sum of that rank's lanes) once all carry tag dtag, apply
+// w += lr * sum, and write the new weights into every rank of relmask's receive slot with
+// tag dtag (ServerProcessor.java:111-120: every worker answered once the round is complete)
+constexpr int kSrvBspSum = -2;
 constexpr int kSrvMaxWorkers = 64;  // the release mask's width
 constexpr int kCmdChunks = 4;     // 64-B command records
 
 struct SrvCmd {
   int stop;                      // 1: leave the launch
-  int k;                         // worker whose delta is applied (-1: releases only)
+  int k;                         // worker whose delta is applied (-1: releases only; kSrvBspSum: a BSP round)
   unsigned dtag;                 // the delta's inbox tag (its vc + 1)
   unsigned log;                  // 1: evaluate the global model after the update (server row)
   unsigned long long relmask;    // bit j: send the weights after this command to worker j
@@ -92,6 +97,7 @@ struct SrvArgs {
   unsigned* claim;             // [2][32] role claims
   int cpar;
   int sxcd;                    // the XCD the server workgroups claim
+  int nwg;                     // server workgroups (<= kSrvWg; each owns slices wg, wg + nwg, ...)
   long long launch;
   long long cmd_ticks;         // command wait budget (s_memrealtime ticks, 100 MHz)
   long long tag_ticks;         // inbox tag wait budget (ticks)
@@ -99,7 +105,7 @@ struct SrvArgs {
 };
 
 size_t server_persist_lds_bytes();
-// One persistent launch on `s` (8 x kSrvWg workgroups; those not on XCD
+// One persistent launch on `s` (8 x nwg workgroups; those not on XCD
 // a.sxcd leave at once).  The arguments travel as the kernel argument: no copy
 // before the launch (it could wait behind other processes' persistent launches).
 void launch_server_persist(const SrvArgs& a, int FP, hipStream_t s);

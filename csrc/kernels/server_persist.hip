@@ -37,72 +37,101 @@ __device__ __forceinline__ void srv_wait_cmd(const SrvArgs& a, unsigned long lon
   if (tid < kCmdChunks) ((TagChunk*)a.rec)[tid] = c;
 }
 
+// Slice s of command `cmd` (one workgroup; every thread calls it).
+template <int FP>
+__device__ __forceinline__ void srv_slice(const SrvArgs& a, const SrvCmd& cmd, int s, unsigned long long* err) {
+  constexpr int NS = FP / 32;
+  const int tid = threadIdx.x, K = a.K;
+  const int c = tid >> 5, f = s * 32 + (tid & 31);
+  const bool coef = c < K, icpt = s == 0 && tid < K;
+  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
+  // this slice of w (only this workgroup role touches it; sc1: the role may have run on
+  // another CU in an earlier launch)
+  float nw = coef ? ld_sc1(a.w + e) : 0.f;
+  float nb = icpt ? ld_sc1(a.w + ei) : 0.f;
+  __shared__ int ok_s;
+  if (cmd.k == kSrvBspSum || cmd.k >= 0) {
+    // the delta(s) in the inbox: worker k's (ServerProcessor.java:148-151), or under a BSP
+    // round every worker rank's lane sum (waited for in rank order)
+    if (tid == 0) {
+      const long long t_end = rt_now() + a.tag_ticks;
+      bool late = false;
+      const int j0 = cmd.k == kSrvBspSum ? 0 : cmd.k, j1 = cmd.k == kSrvBspSum ? a.N : cmd.k + 1;
+      for (int j = j0; j < j1 && !late; ++j) {
+        const unsigned* tg = a.inbox_tag + (size_t)j * NS + s;
+        while ((int)(ld_sys_u32(tg) - cmd.dtag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
+      }
+      ok_s = !late;
+      if (late) xstore(err, 11ull);  // a delta never arrived: apply nothing
+      // (the inbox is read with system-scope loads; a BSP round's sums were stored sc0 sc1
+      // and need no acquire -- the per-worker deltas of the asynchronous plane keep it)
+      if (cmd.k != kSrvBspSum) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    __syncthreads();
+    if (ok_s) {
+      const int j0 = cmd.k == kSrvBspSum ? 0 : cmd.k, j1 = cmd.k == kSrvBspSum ? a.N : cmd.k + 1;
+      float sum = 0.f, sumi = 0.f;  // (a BSP round: the ranks' sums added in rank order)
+      for (int j = j0; j < j1; ++j) {
+        const float* d = a.inbox + (size_t)j * (size_t)a.in_stride;
+        if (coef) sum += ld_sys_f32(d + e);
+        if (icpt) sumi += ld_sys_f32(d + ei);
+      }
+      if (coef) {
+        nw += a.lr * sum;
+        st_sc1(a.w + e, nw);
+      }
+      if (icpt) {
+        nb += a.lr * sumi;
+        st_sc1(a.w + ei, nb);
+      }
+    }
+  }
+  if (cmd.log) {  // the global model's fragments for the server row
+    if (coef) write_frag(a.shi, a.slo, c, f, f < a.F ? nw : 0.f);
+    if (icpt) a.sb[tid] = nb;
+  }
+  // the weights right after this update to every released worker's receive slot
+  // (ServerProcessor.java:172-182), then ONE release and the slots' slice tags
+  if (cmd.relmask) {
+    for (unsigned long long m = cmd.relmask; m; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      float* dst = a.rx[j];
+      if (coef) st_sys_f32(dst + e, nw);
+      if (icpt) st_sys_f32(dst + ei, nb);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      // (a BSP round: the slices are sc0 sc1 stores, drained above -- no release fence, which
+      // would write back this XCD's L2 on the round's critical path)
+      if (cmd.k != kSrvBspSum) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      for (unsigned long long m = cmd.relmask; m; m &= m - 1) {
+        const int j = __builtin_ctzll(m);
+        unsigned* pt = a.ptag + (size_t)j * NS + s;
+        // (a BSP round's tag is the round's own: the ranks wait for tag >= round)
+        const unsigned t = cmd.k == kSrvBspSum
+                               ? cmd.dtag
+                               : __hip_atomic_load((g_u32*)pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        __hip_atomic_store((g_u32*)pt, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sys_u32(a.rx_tag[j] + s, t);
+      }
+    }
+  }
+}
+
 template <int FP>
 __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const SrvCmd& cmd, int wg,
                                             unsigned long long n, unsigned long long& lw, unsigned long long* err) {
   constexpr int NS = FP / 32;
-  const int tid = threadIdx.x, K = a.K;
-  const int c = tid >> 5, f = wg * 32 + (tid & 31);
-  const bool coef = c < K, icpt = wg == 0 && tid < K;
-  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
-  if (wg < NS) {
-    // this slice of w (only this workgroup role touches it; sc1: the role may have
-    // run on another CU in an earlier launch)
-    float nw = coef ? ld_sc1(a.w + e) : 0.f;
-    float nb = icpt ? ld_sc1(a.w + ei) : 0.f;
-    if (cmd.k >= 0) {  // w += lr * delta_k (ServerProcessor.java:148-151)
-      __shared__ int ok_s;
-      if (tid == 0) {
-        const unsigned* tg = a.inbox_tag + (size_t)cmd.k * NS + wg;
-        const long long t_end = rt_now() + a.tag_ticks;
-        bool late = false;
-        while ((int)(ld_sys_u32(tg) - cmd.dtag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
-        ok_s = !late;
-        if (!ok_s) xstore(err, 11ull);  // the delta never arrived: apply nothing
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      }
-      __syncthreads();
-      if (ok_s) {
-        const float* d = a.inbox + (size_t)cmd.k * (size_t)a.in_stride;
-        if (coef) {
-          nw += a.lr * ld_sys_f32(d + e);
-          st_sc1(a.w + e, nw);
-        }
-        if (icpt) {
-          nb += a.lr * ld_sys_f32(d + ei);
-          st_sc1(a.w + ei, nb);
-        }
-      }
-    }
-    if (cmd.log) {  // the global model's fragments for the server row
-      if (coef) write_frag(a.shi, a.slo, c, f, f < a.F ? nw : 0.f);
-      if (icpt) a.sb[tid] = nb;
-    }
-    // the weights right after this update to every released worker's receive slot
-    // (ServerProcessor.java:172-182), then ONE release and the slots' slice tags
-    if (cmd.relmask) {
-      for (unsigned long long m = cmd.relmask; m; m &= m - 1) {
-        const int j = __builtin_ctzll(m);
-        float* dst = a.rx[j];
-        if (coef) st_sys_f32(dst + e, nw);
-        if (icpt) st_sys_f32(dst + ei, nb);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        for (unsigned long long m = cmd.relmask; m; m &= m - 1) {
-          const int j = __builtin_ctzll(m);
-          unsigned* pt = a.ptag + (size_t)j * NS + wg;
-          const unsigned t = __hip_atomic_load((g_u32*)pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-          __hip_atomic_store((g_u32*)pt, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          st_sys_u32(a.rx_tag[j] + wg, t);
-        }
-      }
-    }
+  const int K = a.K;
+  // workgroup wg owns slices wg, wg + nwg, ... (nwg < NS: a server launch that leaves CUs of
+  // its XCD to other processes on a shared GPU)
+  for (int s = wg; s < NS; s += a.nwg) {
+    srv_slice<FP>(a, cmd, s, err);
+    if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
   }
   if (cmd.log && cmd.slot_s) {  // the server row: every workgroup on the test tiles
-    x_barrier(a.flags, wg, kSrvWg, ++lw, err, a.spin);
+    x_barrier(a.flags, wg, a.nwg, ++lw, err, a.spin);
     PairModels pm;
     pm.ah = a.shi;
     pm.al = a.slo;
@@ -115,7 +144,7 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
     pm.bb = a.sb;
     pm.bslot = (char*)cmd.slot_s;
     pm.bseq = cmd.seq_s;
-    lane_pair_eval_at<FP>(lds, K, a.Xt, a.yt, a.T, wg, kSrvWg, pm, a.acc, a.eticket);
+    lane_pair_eval_at<FP>(lds, K, a.Xt, a.yt, a.T, wg, a.nwg, pm, a.acc, a.eticket);
   }
   (void)n;
 }
@@ -133,7 +162,7 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs pa) {
       const int x = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
       if (x == pa.sxcd) {
         const unsigned k = __hip_atomic_fetch_add(cl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k < (unsigned)kSrvWg) r = (int)k;
+        if (k < (unsigned)pa.nwg) r = (int)k;
       }
       if (b == 0)
         for (int j = 0; j < 32; ++j)
@@ -163,7 +192,7 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs pa) {
     // (the others wait for the leader without a budget of their own: the leader's command
     // wait is bounded and ends in a stop command -- with the same poll budget the others'
     // faster polls would give up first during a long idle period)
-    x_barrier(a.flags, wg, kSrvWg, ++lw, err, 0x7fffffff);
+    x_barrier(a.flags, wg, a.nwg, ++lw, err, 0x7fffffff);
     if (wg == 0 && tid == 0)  // (its ring slot may be reused: the record is in the broadcast area)
       __hip_atomic_store(a.consumed_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     SrvCmd cmd;
@@ -188,11 +217,12 @@ size_t server_persist_lds_bytes() { return (size_t)kPairEvalLds; }
 
 void launch_server_persist(const SrvArgs& a, int FP, hipStream_t s) {
   const size_t lds = server_persist_lds_bytes();
+  if (a.nwg < 1 || a.nwg > kSrvWg) return;
   switch (FP) {
-    case 128: server_persist_kernel<128><<<8 * kSrvWg, 256, lds, s>>>(a); break;
-    case 256: server_persist_kernel<256><<<8 * kSrvWg, 256, lds, s>>>(a); break;
-    case 512: server_persist_kernel<512><<<8 * kSrvWg, 256, lds, s>>>(a); break;
-    case 1024: server_persist_kernel<1024><<<8 * kSrvWg, 256, lds, s>>>(a); break;
+    case 128: server_persist_kernel<128><<<8 * a.nwg, 256, lds, s>>>(a); break;
+    case 256: server_persist_kernel<256><<<8 * a.nwg, 256, lds, s>>>(a); break;
+    case 512: server_persist_kernel<512><<<8 * a.nwg, 256, lds, s>>>(a); break;
+    case 1024: server_persist_kernel<1024><<<8 * a.nwg, 256, lds, s>>>(a); break;
     default: break;
   }
 }

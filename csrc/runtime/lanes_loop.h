@@ -20,6 +20,10 @@
 //     rank reduces it to the server rank over RCCL and receives the new weights
 //     by broadcast (BASELINE config 2/3 topology); on the server rank the update
 //     and its fragments follow the reduce;
+//   * multi-rank peer_sum (set_peer_sum, no communicator): the kernel stores the
+//     lane sum into the rank's inbox slot on the server GPU itself and the next
+//     round's launch -- already dispatched -- pulls the server kernel's update from
+//     this rank's receive slot: no collective, host or kernel boundary in between;
 //   * the vector-clock tracker advances one round; the device error word (pinned)
 //     is polled: a timed-out cross-workgroup wait surfaces as an exception naming
 //     the round.
@@ -150,6 +154,19 @@ class LanesLoop {
   void set_peer(uintptr_t rx_data, uintptr_t rx_tags, int64_t rx_stride, const std::vector<uintptr_t>& inbox,
                 const std::vector<uintptr_t>& inbox_tag);
   bool peer() const { return peer_rx_ != nullptr; }
+  // peer_sum BSP (multi-rank sequential consistency over the peer data plane; needs the
+  // overlapped launches and no communicator): this rank's lane sums go to its inbox slot on
+  // the server GPU (push / push_tag, an IPC mapping), the next round's weights come from
+  // its receive slot (rx / rx_tag, fine-grained memory the server kernel writes, tag =
+  // round + 1 after round `round`'s update) -- LanesArgs::push.  wait_s bounds a round's
+  // pull wait (the slowest rank's round).  After a run() the rank's w holds the last update.
+  void set_peer_sum(uintptr_t rx, uintptr_t rx_tag, uintptr_t push, uintptr_t push_tag, double wait_s);
+  bool peer_sum() const { return psum_rx_ != nullptr; }
+  // (diagnostics) this rank's receive-slot tags then its push tags, [2][FP/32] (synchronous)
+  std::vector<unsigned> peer_sum_tags() const;
+  // Ranks sharing one GPU: workgroups of this loop's launches on the XCDs of `mask` leave
+  // at once (LanesArgs::xcd_skip) -- none of this loop's lanes may sit there
+  void set_xcd_skip(unsigned mask);
   // Fault injection for the NEXT run_async (the Python schedulers'
   // --inject_worker_crash / --inject_worker_stop): crash[l] >= 0 -- lane l fails when
   // released after crash[l] more solves (no delta; `drop`: the tracker retires its
@@ -300,13 +317,6 @@ class LanesLoop {
   unsigned* claim_ = nullptr;
   int64_t launches_ = 0;
   float* dsum_ = nullptr;
-  // multi-rank: the round's collectives on their own stream, started by the kernel's
-  // dsum_done counter (PSX_EARLY_COLL, default on) instead of behind the whole launch
-  bool early_coll_ = false;
-  unsigned* dsum_done_ = nullptr;
-  uint64_t coll_n_ = 0;           // rounds whose dsum the counter has announced (NS per round)
-  hipStream_t cstream_ = nullptr;
-  hipEvent_t coll_ev_ = nullptr;
   uint16_t *upd_hi_ = nullptr, *upd_lo_ = nullptr;  // fragments of an update nobody evaluates
   float* upd_b_ = nullptr;
   unsigned long long* err_host_ = nullptr;  // pinned [kMaxLanes]
@@ -400,6 +410,13 @@ class LanesLoop {
   int64_t peer_stride_ = 0;
   std::vector<uintptr_t> peer_inbox_, peer_inbox_tag_;
   std::vector<unsigned> pull_tag_;
+  // peer_sum BSP (set_peer_sum)
+  const float* psum_rx_ = nullptr;
+  const unsigned* psum_rx_tag_ = nullptr;
+  float* psum_push_ = nullptr;
+  unsigned* psum_push_tag_ = nullptr;
+  long long psum_ticks_ = 0;
+  unsigned xcd_skip_ = 0;  // set_xcd_skip
   // the persistent launch runs on a stream of its own (non-blocking: no implicit
   // synchronisation of the null stream, e.g. a host-staged transfer, waits for it),
   // ordered after / before the caller's stream by events

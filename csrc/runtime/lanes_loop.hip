@@ -225,7 +225,6 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   applied_ = reinterpret_cast<unsigned*>(b + o_ovl);
   evdone_ = applied_ + 32;
   ovlq_ = applied_ + 48;
-  dsum_done_ = applied_ + 40;  // (multi-rank; the overlap words are unused then)
   slab_ = reinterpret_cast<int*>(b + o_slab);
   if (const char* ss = std::getenv("PSX_SIDE_SYNC"))
     side_sync_ = std::string(ss) == "value" ? 1 : (std::string(ss) == "nowait" ? 2 : (std::string(ss) == "inline" ? 3 : 0));
@@ -285,18 +284,6 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   // the slots while the next round runs
   const char* sl = std::getenv("PSX_RIDERS_SLAB");
   slab_on_ = ovl_ && tile_riders_ && !(sl && sl[0] == '0');
-  // PSX_EARLY_COLL=1 (default off): a rank with lanes and a communicator starts the
-  // round's reduce / all-reduce, update and broadcast on a stream of its own as soon as
-  // every slice's lane sum is written, while the launch's riders still evaluate the
-  // previous round's rows.  Off by default: the world-1 RCCL rehearsal measured 71.9k
-  // against 79.5k updates/s (profiles/r05/s37) -- the cross-stream hand-off costs more
-  // than a one-rank collective saves; unmeasured on several GPUs
-  const char* ec = std::getenv("PSX_EARLY_COLL");
-  early_coll_ = comm_ && cfg_.L > 0 && ec && ec[0] == '1';
-  if (early_coll_) {
-    hip_check(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking), "hipStreamCreate(collectives)");
-    hip_check(hipEventCreateWithFlags(&coll_ev_, hipEventDisableTiming), "hipEventCreate");
-  }
   if (ovl_) {
     hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
     hip_check(hipEventCreateWithFlags(&ovl_in_, hipEventDisableTiming), "hipEventCreate");
@@ -344,11 +331,6 @@ LanesLoop::~LanesLoop() {
   if (tok_host_) (void)hipHostFree(tok_host_);
   if (err_host_) (void)hipHostFree(err_host_);
   if (tr_) (void)hipFree(tr_);
-  if (cstream_) {
-    (void)hipStreamSynchronize(cstream_);
-    (void)hipStreamDestroy(cstream_);
-  }
-  if (coll_ev_) (void)hipEventDestroy(coll_ev_);
 }
 
 void LanesLoop::check(int64_t rc, const char* what) const {
@@ -449,7 +431,39 @@ int LanesLoop::rider_count(int nmodels, int L) const {
     const int nT = (cfg_.T + 31) / 32, items = tile_riders_ ? nT * ((np + ppi - 1) / ppi) : np * nT;
     extra = items < 256 ? items : 256;
   }
-  return lanes_grid(L, extra) - L * kLaneWg;
+  const int g = lanes_grid(L, extra);
+  // (skipped XCDs: the grid is 8 x 32, one XCD's share each -- set_xcd_skip keeps extra at 0)
+  return g - L * kLaneWg - (xcd_skip_ ? kLaneWg * __builtin_popcount(xcd_skip_) : 0);
+}
+
+void LanesLoop::set_xcd_skip(unsigned mask) {
+  mask &= 0xffu;
+  const unsigned lanes = ((1u << cfg_.L) - 1u) << cfg_.xcd0;
+  if (mask & lanes) throw std::invalid_argument("LanesLoop::set_xcd_skip: a lane's XCD in the mask");
+  if (mask && cfg_.L == 8) throw std::invalid_argument("LanesLoop::set_xcd_skip: 8 lanes use every XCD");
+  if (mask && !lane_riders_ && cfg_.L == 8) throw std::invalid_argument("LanesLoop::set_xcd_skip: extra riders");
+  xcd_skip_ = mask;
+}
+
+std::vector<unsigned> LanesLoop::peer_sum_tags() const {
+  const int NS = cfg_.scfg.Fp / 32;
+  std::vector<unsigned> h(2 * (size_t)NS, 0u);
+  if (!psum_rx_) return h;
+  hip_check(hipMemcpy(h.data(), psum_rx_tag_, (size_t)NS * 4, hipMemcpyDeviceToHost), "peer_sum rx tags");
+  hip_check(hipMemcpy(h.data() + NS, psum_push_tag_, (size_t)NS * 4, hipMemcpyDeviceToHost), "peer_sum push tags");
+  return h;
+}
+
+void LanesLoop::set_peer_sum(uintptr_t rx, uintptr_t rx_tag, uintptr_t push, uintptr_t push_tag, double wait_s) {
+  if (!rx || !rx_tag || !push || !push_tag) throw std::invalid_argument("LanesLoop::set_peer_sum: null region");
+  if (!ovl_ || comm_ || cfg_.L < 1)
+    throw std::invalid_argument("LanesLoop::set_peer_sum: needs the overlapped launches (PSX_LANES_OVERLAP), lanes "
+                                "and no communicator");
+  psum_rx_ = reinterpret_cast<const float*>(rx);
+  psum_rx_tag_ = reinterpret_cast<const unsigned*>(rx_tag);
+  psum_push_ = reinterpret_cast<float*>(push);
+  psum_push_tag_ = reinterpret_cast<unsigned*>(push_tag);
+  psum_ticks_ = (long long)(std::min(std::max(wait_s, 1.0), 7200.0) * 1e8);
 }
 
 // The previous round's rows as models of one evaluation pass: the lanes' local
@@ -607,6 +621,11 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     joined = true;
     hip_check(hipEventRecord(ovl_out_, ostream_), "overlap order out");
     hip_check(hipStreamWaitEvent(stream, ovl_out_, 0), "overlap order out");
+    if (psum_rx_ && ovl_n_ > 0) {  // peer_sum: the server's update of the last round into w
+      launch_peer_pull(psum_rx_, psum_rx_tag_, (unsigned)ovl_n_, cfg_.w, cfg_.scfg.K, cfg_.scfg.Fp, psum_ticks_,
+                       err_host_, stream);
+      hip_check(hipGetLastError(), "peer pull launch");
+    }
   };
   struct JoinOnThrow {  // an exception out of a round still orders the caller's stream
     bool* joined;
@@ -702,7 +721,6 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     a.w = cfg_.w;
     a.lr = cfg_.lr;
     a.dsum = comm_ ? dsum_ : nullptr;
-    a.dsum_done = (early_coll_ && L > 0) ? dsum_done_ : nullptr;
     a.shi = cfg_.shi[par];
     a.slo = cfg_.slo[par];
     a.sb = cfg_.sb[par];
@@ -717,6 +735,14 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     // (from the injected round on: a round whose workgroups happen to arrive together
     // polls nothing, so one round alone would not always time out)
     a.spin_max = (inject_round_ >= 0 && r >= inject_round_) ? inject_spin_ : 0;
+    a.xcd_skip = xcd_skip_;
+    if (psum_rx_) {  // the push into the server's inbox, the pull from this rank's receive slot
+      a.push = psum_push_;
+      a.push_tag = psum_push_tag_;
+      a.rx = psum_rx_;
+      a.rx_tag = psum_rx_tag_;
+      a.peer_ticks = psum_ticks_;
+    }
     if (tr_) {
       a.tr = tr_;
       a.tr_slot = (int)(tr_n_ % tr_cap_);
@@ -757,7 +783,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
         }
         hip_check(hipStreamWriteValue32(rs, evdone_, (uint32_t)(ovl_n_ + 1), 0), "overlap: launch done");
         hip_check(hipEventRecord(ovl_last_, rs), "overlap: last launch");
-        ovl_prev_grid_ = lanes_grid(L, a.nride);
+        ovl_prev_grid_ = lanes_grid(L, a.nride) - (xcd_skip_ ? kLaneWg * __builtin_popcount(xcd_skip_) : 0);
         ovl_prev_cpar_ = a.cpar;
         ovl_chain_ = true;
         ++ovl_n_;
@@ -769,16 +795,7 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
     nlrec = 0;
     // ---- multi-rank: lane sums -> server (reduce), update, weights -> every rank ----
     if (comm_) {
-      // (early collectives: on cstream_ once the kernel announced every slice's sum; the
-      // next round's launch on `stream` waits for them below)
       hipStream_t cs = stream;
-      if (early_coll_ && L > 0) {
-        ++coll_n_;
-        const int NSl = cfg_.scfg.Fp / 32;
-        hip_check(hipStreamWaitValue32(cstream_, dsum_done_, (uint32_t)((uint64_t)NSl * coll_n_), hipStreamWaitValueGte),
-                  "collectives wait for the lane sums");
-        cs = cstream_;
-      }
       if (L == 0) hip_check(hipMemsetAsync(dsum_, 0, (size_t)P_ * 4, stream), "zero contribution");
       if (cfg_.allreduce) {  // every replica applies the same summed update
         comm_->all_reduce(dsum_, dsum_, (size_t)P_, Comm::kF32, cs);
@@ -793,10 +810,6 @@ int64_t LanesLoop::run(int64_t rounds, int64_t r0, hipStream_t stream, double ma
         comm_->broadcast(cfg_.w, cfg_.w, (size_t)P_, Comm::kF32, cfg_.server_rank, cs);
       }
       hip_check(hipGetLastError(), "server update launch");
-      if (cs != stream) {  // everything after the round on `stream` (the next launch) follows them
-        hip_check(hipEventRecord(coll_ev_, cs), "collectives done");
-        hip_check(hipStreamWaitEvent(stream, coll_ev_, 0), "collectives done");
-      }
     }
     (void)KF;
     // ---- this round's rows: evaluated by the next launch, or side launch now ----
@@ -871,6 +884,7 @@ void LanesLoop::flush(hipStream_t stream) {
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
   a.xcd0 = cfg_.xcd0;
+  a.xcd_skip = xcd_skip_;
   a.ev.xq = (xcd_riders_ || tile_riders_) ? claim_ + 32 * a.cpar + 16 : nullptr;
   if (a.ev.nmodels > 0) {
     launch_lanes_round(cfg_.scfg, lanes_dev_, a, S_, stream);

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -45,6 +46,15 @@ struct PeerServerCfg {
   std::vector<uintptr_t> replies;     // per worker: its rank's reply queue
   double worker_timeout_s = 600.0;
   int sxcd = 0;                  // the XCD of the persistent launch
+  // peer_sum BSP (run_bsp): the "workers" are the worker RANKS -- inbox slot j / receive
+  // slot j = worker rank j's lane sum / weights; no token queues, no reply queues (the
+  // rounds are the protocol); tag_wait_s bounds a round's wait for the ranks' sums (a
+  // paced stream can hold a round for as long as its rows take)
+  bool bsp = false;
+  double tag_wait_s = 600.0;
+  // workgroups of the server launch on its XCD (<= 32, each owns every nwg-th slice): a
+  // GPU shared with other ranks' launches gets fewer, leaving CUs of the XCD to them
+  int nwg = kSrvWg;
 };
 
 class PeerServer {
@@ -60,6 +70,18 @@ class PeerServer {
   // a checkpoint is due (drained as well) or a worker needs the caller's decision.
   AsyncStatus run(int64_t checkpoint_every);
   void fail(int k);
+  // peer_sum BSP: `rounds` rounds from round r0 -- one command per round (the ranks' sums
+  // summed, applied, the weights written into every rank's receive slot; the server row of
+  // the global model into the metrics sink, vc = the round), the tracker advanced per
+  // round; returns once the launch has drained (w final).  The ranks' lanes loops run the
+  // same rounds (LanesLoop::set_peer_sum).
+  int64_t run_bsp(int64_t rounds, int64_t r0);
+  // peer_sum BSP bring-up: the current weights into every rank's receive slot (tag 0: the
+  // pull of round 0)
+  void seed_rx();
+  int64_t bsp_rounds() const { return (int64_t)bsp_n_; }
+  std::string bsp_tags() const;  // (failure reports) every rank's push / pull slice tags
+  double host_us_per_round() const { return bsp_run_ ? bsp_ns_ / 1000.0 / (double)bsp_run_ : 0.0; }
   // Stop the persistent launch and wait for it (idempotent).
   void stop();
   // One launch that stops at once, drained here: the first launch's one-time device work
@@ -115,6 +137,9 @@ class PeerServer {
   std::vector<std::pair<int, int64_t>> arrivals_;
   int64_t updates_ = 0, tokens_ = 0, updates_run_ = 0;
   double host_ns_ = 0.0;
+  uint64_t bsp_n_ = 0;  // BSP rounds commanded so far (the tag of the last one)
+  int64_t bsp_run_ = 0;
+  double bsp_ns_ = 0.0;
 };
 
 }  // namespace psx

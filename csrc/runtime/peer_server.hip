@@ -28,7 +28,8 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   (void)stream;  // the persistent launch gets a stream of its own (nothing else is ordered behind it)
   const int N = cfg.nworkers;
   if (N < 1 || N > kSrvMaxWorkers) throw std::invalid_argument("PeerServer: 1 .. 64 workers");
-  if (!cfg.api || !cfg.tracker || !cfg.ctrl) throw std::invalid_argument("PeerServer: missing host runtime handles");
+  if (!cfg.api || (!cfg.bsp && (!cfg.tracker || !cfg.ctrl)))
+    throw std::invalid_argument("PeerServer: missing host runtime handles");
   api_ = reinterpret_cast<const HostApi*>(cfg.api);
   if (api_->version != kHostApiVersion) throw std::runtime_error("PeerServer: host runtime C ABI version mismatch");
   if (!cfg.w || cfg.P <= 0 || cfg.K < 1 || cfg.K > 8) throw std::invalid_argument("PeerServer: weights / classes");
@@ -38,10 +39,11 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   NS_ = cfg.FP / 32;
   if (!cfg.inbox || cfg.lay.P != cfg.P || cfg.lay.NS != NS_ || cfg.lay.slots < N)
     throw std::invalid_argument("PeerServer: inbox region layout");
-  if ((int)cfg.rx.size() != N || (int)cfg.rx_tag.size() != N || (int)cfg.replies.size() != N)
+  if ((int)cfg.rx.size() != N || (int)cfg.rx_tag.size() != N || (!cfg.bsp && (int)cfg.replies.size() != N))
     throw std::invalid_argument("PeerServer: one receive slot, tag array and reply queue per worker");
   for (int j = 0; j < N; ++j)
-    if (!cfg.rx[j] || !cfg.rx_tag[j] || !cfg.replies[j]) throw std::invalid_argument("PeerServer: null peer handle");
+    if (!cfg.rx[j] || !cfg.rx_tag[j] || (!cfg.bsp && !cfg.replies[j]))
+      throw std::invalid_argument("PeerServer: null peer handle");
   if (cfg.sink && (!cfg.Xt || !cfg.yt || cfg.T < 1)) throw std::invalid_argument("PeerServer: server rows need the test set");
   if (cfg.sxcd < 0 || cfg.sxcd > 7) throw std::invalid_argument("PeerServer: sxcd in 0..7");
   // device workspace (ALL device memory and its zero-fill here, before any
@@ -110,12 +112,16 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   a.rec = reinterpret_cast<unsigned long long*>(b + o_rec);
   a.claim = reinterpret_cast<unsigned*>(b + o_claim);
   a.sxcd = cfg.sxcd;
+  if (cfg.nwg < 1 || cfg.nwg > kSrvWg) throw std::invalid_argument("PeerServer: 1 .. 32 server workgroups");
+  a.nwg = cfg.nwg;
   // wall-clock budgets: the command wait outlasts the host's own watchdog (the worker
   // timeout: a silent worker is failed and the commands resume); a delta's tag is
   // written before its token leaves the worker's GPU (a short wait at most)
   const double cmd_s = std::min(cfg.worker_timeout_s + 30.0, 7200.0);
   a.cmd_ticks = (long long)(cmd_s * 1e8);
-  a.tag_ticks = 10ll * 100000000ll;
+  // (BSP rounds: the slowest rank's round, which may wait for its stream's rows)
+  a.tag_ticks = cfg.bsp ? (long long)(std::min(std::max(cfg.tag_wait_s, 10.0), 7200.0) * 1e8) : 10ll * 100000000ll;
+  if (cfg.bsp) a.cmd_ticks = std::max(a.cmd_ticks, a.tag_ticks + (long long)(30.0 * 1e8));
   a.spin = 1 << 22;
   ptag_.assign(N, 0u);
   finished_.assign(N, 0);
@@ -160,6 +166,7 @@ void PeerServer::check_device() const {
     m += "; last arrivals:";
     for (size_t i = arrivals_.size() > 12 ? arrivals_.size() - 12 : 0; i < arrivals_.size(); ++i)
       m += " (" + std::to_string(arrivals_[i].first) + "," + std::to_string((long long)arrivals_[i].second) + ")";
+    if (cfg_.bsp) m += "; BSP rounds commanded " + std::to_string((long long)bsp_n_) + "; " + bsp_tags();
     throw std::runtime_error(m);
   }
 }
@@ -299,14 +306,98 @@ void PeerServer::stop() {
   write_cmd(c);
   running_ = false;
   const double t0 = now_s();
+  // (BSP: the commands ahead of the stop wait for the ranks' rounds)
+  const double limit = cfg_.bsp ? std::max(60.0, cfg_.tag_wait_s + 30.0) : 60.0;
   for (;;) {
     const hipError_t e = hipStreamQuery(stream_);
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) hip_check(e, "server launch drain");
-    if (now_s() - t0 > 60.0) throw std::runtime_error("PeerServer: the server launch did not drain in 60 s");
+    if (now_s() - t0 > limit) {
+      check_device();
+      throw std::runtime_error("PeerServer: the server launch did not drain in " + std::to_string((int)limit) + " s");
+    }
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   check_device();
+}
+
+std::string PeerServer::bsp_tags() const {
+  // (failure reports) the slice tags of every rank's inbox slot (its pushes) and receive
+  // slot (the server's pulls), read on a stream of their own with a bounded wait
+  const int N = cfg_.nworkers, NS = NS_;
+  const size_t nt = (size_t)N * NS;
+  std::vector<unsigned> h(2 * nt, 0xffffffffu);
+  hipStream_t s = nullptr;
+  std::string m = "tags (rank: inbox min..max / receive min..max):";
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return m + " (no stream)";
+  bool ok = hipMemcpyAsync(h.data(), reinterpret_cast<const void*>(cfg_.inbox + cfg_.lay.tag_off()), nt * 4,
+                           hipMemcpyDeviceToHost, s) == hipSuccess;
+  for (int j = 0; j < N && ok; ++j)
+    ok = hipMemcpyAsync(h.data() + nt + (size_t)j * NS, reinterpret_cast<const void*>(cfg_.rx_tag[j]), (size_t)NS * 4,
+                        hipMemcpyDeviceToHost, s) == hipSuccess;
+  const double t0 = now_s();
+  while (ok && hipStreamQuery(s) == hipErrorNotReady && now_s() - t0 < 2.0)
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  ok = ok && hipStreamQuery(s) == hipSuccess;
+  (void)hipStreamDestroy(s);
+  if (!ok) return m + " (unreadable)";
+  for (int j = 0; j < N; ++j) {
+    unsigned a0 = ~0u, a1 = 0, b0 = ~0u, b1 = 0;
+    for (int q = 0; q < NS; ++q) {
+      a0 = std::min(a0, h[(size_t)j * NS + q]);
+      a1 = std::max(a1, h[(size_t)j * NS + q]);
+      b0 = std::min(b0, h[nt + (size_t)j * NS + q]);
+      b1 = std::max(b1, h[nt + (size_t)j * NS + q]);
+    }
+    m += " " + std::to_string(j) + ": " + std::to_string(a0) + ".." + std::to_string(a1) + " / " + std::to_string(b0) +
+         ".." + std::to_string(b1);
+  }
+  return m;
+}
+
+void PeerServer::seed_rx() {
+  if (running_) throw std::logic_error("PeerServer::seed_rx: the server launch is running");
+  for (int j = 0; j < cfg_.nworkers; ++j)
+    hip_check(hipMemcpy(reinterpret_cast<void*>(cfg_.rx[j]), cfg_.w, (size_t)cfg_.P * sizeof(float),
+                        hipMemcpyDeviceToDevice),
+              "peer_sum: weights into a rank's receive slot");
+  hip_check(hipDeviceSynchronize(), "peer_sum seed");
+}
+
+int64_t PeerServer::run_bsp(int64_t rounds, int64_t r0) {
+  if (!cfg_.bsp) throw std::logic_error("PeerServer::run_bsp: built for the asynchronous protocol");
+  if (rounds <= 0) return 0;
+  const auto h0 = std::chrono::steady_clock::now();
+  launch();
+  const unsigned long long all = cfg_.nworkers >= 64 ? ~0ull : ((1ull << cfg_.nworkers) - 1ull);
+  for (int64_t i = 0; i < rounds; ++i) {
+    SrvCmd c{};
+    c.k = kSrvBspSum;
+    c.dtag = (unsigned)(bsp_n_ + 1);
+    c.relmask = all;
+    int slot = -1;
+    uint64_t seq = 0;
+    if (cfg_.sink) {  // the global model after the round's update: its server row (ServerProcessor.java:154-165)
+      uintptr_t addr = 0;
+      slot = api().sink_acquire((void*)cfg_.sink, &seq, &addr);
+      check_api(slot, "metrics sink acquire");
+      c.log = 1;
+      c.slot_s = addr;
+      c.seq_s = (unsigned)seq;
+    }
+    write_cmd(c);
+    ++bsp_n_;
+    if (slot >= 0) {
+      SinkRecord rec{slot, 1 | kSinkTagged, seq, -1, -1, r0 + i, 0};
+      check_api(api().sink_submit_many((void*)cfg_.sink, 1, &rec), "metrics sink submit");
+    }
+    if (cfg_.tracker) check_api(api().tracker_bsp_round((void*)cfg_.tracker, r0 + i), "tracker");
+    check_device();
+  }
+  bsp_ns_ += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - h0).count();
+  stop();  // (the ranks' last sums applied: w is final)
+  bsp_run_ += rounds;
+  return rounds;
 }
 
 AsyncStatus PeerServer::run(int64_t checkpoint_every) {

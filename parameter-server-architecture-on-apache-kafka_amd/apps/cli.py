@@ -114,10 +114,12 @@ def server_parser() -> argparse.ArgumentParser:
                    help="--inprocess SSP/ASP: one host thread polling the workers' HIP events, or a thread "
                         "per worker (auto: events on a GPU unless a delay is injected)")
     g.add_argument("--bsp_schedule", default="reduce_bcast",
-                   choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer"],
+                   choices=["allreduce", "reduce_bcast", "sharded", "keyrange", "peer", "peer_sum"],
                    help="multi-rank Sequential consistency: RCCL all-reduce / reduce + broadcast / reduce-scatter + "
-                        "all-gather, the key-range server, or peer = the lanes push into the server GPU's inbox "
-                        "and pull from their receive slots over xGMI (--workers_per_rank > 1)")
+                        "all-gather, the key-range server, peer = the asynchronous loops with the sequential "
+                        "tracker, or peer_sum = each worker rank's round kernel stores its lane sum into the "
+                        "server GPU's inbox and the server kernel writes the new weights into every rank's receive "
+                        "slot over xGMI (dense, every rank on a GPU; no collective per round)")
     g.add_argument("--workers_per_rank", type=int, default=1,
                    help="multi-rank BSP on GPUs: logical workers per worker rank, one XCD each in one launch per "
                         "round (the native lanes loop)")

@@ -22,6 +22,18 @@ Sequential (BSP, c = 0) schedules, chosen with ``--bsp_schedule``:
                 Wide model (or ``keyrange``): the key-range sharded server of
                 keyrange.py -- each rank stores ONLY its key range and a round moves
                 the window's ids and values (pull / push by owner), never P floats.
+  peer_sum      dense, several workers per worker rank, every rank on a GPU (the
+                bench.py default for N > 1 GPUs): a dedicated server rank and NO
+                collective.  The last lane to finish a slice on a worker rank stores
+                the rank's lane sum straight into that rank's slot of the server
+                GPU's inbox (IPC-mapped fine-grained memory, xGMI) and tags it; the
+                server's persistent kernel sums the W ranks' slices in rank order,
+                applies w += lr * sum slice-parallel and writes the new slice into
+                every rank's receive slot with the round's tag; the next round's
+                launch -- already dispatched behind the current one -- starts its
+                solve once its slices' tags arrive.  No host, no kernel boundary and
+                no collective sits between a round's push and the next round's pull
+                (csrc/comm/peer_bus.h, LanesArgs::push, server_persist.h kSrvBspSum).
 On GPUs the BSP collectives are issued through a native RCCL communicator
 (psx.parallel.comm, csrc/comm/rccl_comm.h): a few us of host time per call
 instead of ~30 us through torch.distributed, which otherwise bounds the round.
@@ -200,7 +212,12 @@ class DistEngine:
         # worker ranks' persistent launches behind a reduce / broadcast
         self.peer_bsp = cfg.consistency_model == 0 and cfg.bsp_schedule == "peer"
         self.async_mode = cfg.consistency_model != 0 or self.peer_bsp
-        self.dedicated = self.async_mode or not cfg.server_colocated
+        # bsp_schedule "peer_sum": rank-level lane sums into the server GPU's inbox, the
+        # server kernel's slice-parallel sum + update into every rank's receive slot
+        self.peer_sum = cfg.consistency_model == 0 and cfg.bsp_schedule == "peer_sum"
+        if self.peer_sum and torch.device(device).type != "cuda":
+            raise ValueError("--bsp_schedule peer_sum: every rank (the server too) on a GPU")
+        self.dedicated = self.async_mode or self.peer_sum or not cfg.server_colocated
         wpr = max(1, int(cfg.workers_per_rank))
         n_worker_ranks = world - 1 if self.dedicated else world
         n_workers = n_worker_ranks * wpr
@@ -375,6 +392,8 @@ class DistEngine:
             # the deferred evaluation rows ride in the next solve's launches (the
             # update is a plain launch: it applies the reduced sum, not this delta)
             srv.pair.set_ride(True, fuse_update=False)
+        if self.peer_sum:  # (its receive slots carry the weights: seeded once, then every round's update)
+            return self._run_bsp_peer_sum()
         # bootstrap pull (vc 0): everybody starts from rank 0's weights
         boot = srv.w if srv is not None else (wk.w if wk is not None else zeros)
         dist.broadcast(boot, src=0)
@@ -577,7 +596,8 @@ class DistEngine:
         c = self.cfg
         if os.environ.get("PSX_NATIVE_LANES", "1") == "0" or not is_gpu(self.device):
             return False
-        if sched not in ("reduce_bcast", "allreduce") or self.wide or self.evalset is None or self.tracer.enabled:
+        if sched not in ("reduce_bcast", "allreduce", "peer_sum") or self.wide or self.evalset is None \
+                or self.tracer.enabled:
             return False
         if c.checkpoint_dir:
             return False
@@ -592,7 +612,7 @@ class DistEngine:
         cap = -(-int(c.max_buffer_size) // 32) * 32
         return bool(_native.hip().lanes_supported(self.spec.Fp, self.spec.K, cap))
 
-    def _run_bsp_lanes(self, comm, rounds: int) -> int:
+    def _run_bsp_lanes(self, comm, rounds: int, build_only: bool = False) -> int:
         from ..ops.lr import Fragments
 
         cfg, srv, sp, W = self.cfg, self.server, self.spec, self.workers
@@ -620,7 +640,8 @@ class DistEngine:
                      log_server=int(self.rank == 0), log_workers=int(bool(W) and cfg.log_workers),
                      # ranks sharing one GPU (IPC transport): worker rank i's lanes on XCDs
                      # i*wpr .. i*wpr + wpr - 1, so no two ranks' lanes share an XCD
-                     xcd0=(self.worker_id * len(W)) if (W and getattr(comm, "kind", "rccl") == "ipc") else 0,
+                     xcd0=(self.worker_id * len(W)) if (W and (getattr(comm, "kind", "rccl") == "ipc" or (
+                         comm is None and oversubscribed()))) else 0,
                      sink=self.log.native.handle if self.log is not None else 0,
                      tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0,
                      new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), new_ramp=int(cfg.iter_new_ramp))
@@ -633,14 +654,18 @@ class DistEngine:
                          sb=[f.b.data_ptr() for f in self._lane_frags])
             ev = self.evalset
             d.update(Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=ev.T)
-            lp = h.LanesLoop(d, comm.c)
+            lp = h.LanesLoop(d, comm.c if comm is not None else None)
+            if os.environ.get("PSX_LANES_TRACE_OUT"):  # (tools: the device phase stamps of every round)
+                lp.set_trace(8192)
             self._lanes = lp
         elif self.log is not None:
             lp.set_sink(self.log.native.handle)
+        if build_only:
+            return 0
         for i, w in enumerate(W):
             lp.set_next_local(i, int(w.source.next_local))
             lp.set_seen_at_solve(i, int(w._seen_at_solve))
-        stream = comm.compute_stream()
+        stream = comm.compute_stream() if comm is not None else torch.cuda.current_stream(self.device).cuda_stream
         try:
             n = self._lanes_chunks(lp, comm, stream, int(rounds), W)
             lp.flush(stream)
@@ -656,12 +681,109 @@ class DistEngine:
             w._seen_at_solve = int(lp.seen_at_solve(i))
             if w.ring.XT is not None:
                 w.ring.xt_stale = True
+        if os.environ.get("PSX_LANES_TRACE_OUT"):  # one JSON line per call: the rounds' device stamps
+            with open(f"{os.environ['PSX_LANES_TRACE_OUT']}.rank{self.rank}", "a") as fh:
+                fh.write(json.dumps({"rank": self.rank, "rows": [list(r) for r in lp.trace_take(stream)]}) + "\n")
         if W:
             lp.copy_out_all([w.solver.loss.data_ptr() for w in W], [w.solver.delta.data_ptr() for w in W], stream)
         if srv is not None and srv.frag is not None:
             srv.frag.refresh(srv.w)
         self.native_host_us_per_round = float(lp.host_us_per_round)
         return n
+
+    def _run_bsp_peer_sum(self) -> dict:
+        """BSP rounds over the peer data plane with rank-level sums (bsp_schedule
+        peer_sum; see the module docstring): the worker ranks run their native lanes
+        loop with the push / pull in the round kernel (LanesLoop.set_peer_sum), the
+        server rank runs the same rounds as commands of its persistent server kernel
+        (PeerServer.run_bsp: the ranks' sums applied in rank order, the weights written
+        into every rank's receive slot, the global model's server row per round).  No
+        collective per round; an unbounded run stops by a vote between chunks."""
+        cfg, srv, W = self.cfg, self.server, self.workers
+        if not self._lanes_cfg_ok("peer_sum"):
+            raise ValueError("--bsp_schedule peer_sum: dense bf16 windows of <= 8192 rows on GPUs, no tracing, "
+                             "checkpoints or injected faults (the native lanes loop)")
+        if not hasattr(self, "_psum_region"):
+            self._peer_sum_setup()
+        N = cfg.num_workers
+        t_start = time.time()
+        t0 = time.perf_counter()
+        if self.is_server:
+            n = self._lanes_chunks(None, None, None, int(cfg.max_iters), [])
+            t1 = time.perf_counter()
+            if srv.frag is not None:
+                srv.frag.refresh(srv.w)
+            srv.updates += N * n
+            self.native_host_us_per_round = float(self._pserver.host_us_per_round)
+            torch.cuda.synchronize(self.device)
+        else:
+            n = self._run_bsp_lanes(None, int(cfg.max_iters))
+            t1 = time.perf_counter()
+            if os.environ.get("PSX_PSUM_DIAG"):  # (diagnostics: receive / push slice tags; a synchronisation)
+                self._psum_tags = list(self._lanes.peer_sum_tags())
+        # (where a call's wall clock went: the rounds, then the tail -- bench.py gathers these)
+        self._phases = {"rounds_ms": round((t1 - t0) * 1e3, 3),
+                        "tail_ms": round((time.perf_counter() - t1) * 1e3, 3)}
+        self.rounds += n
+        for w in W:
+            w.vc = self.rounds
+        if self.log is not None:
+            self.log.drain()
+        elapsed = time.time() - t_start
+        return {"rounds": self.rounds, "updates": self.rounds * N, "elapsed_s": elapsed,
+                "updates_per_s": n * N / elapsed if elapsed > 0 else 0.0,
+                "max_vc_gap": int(srv.tracker.max_gap) if srv is not None else 0, "data_plane": "peer_sum",
+                "lanes": len(W)}
+
+    def _peer_sum_setup(self):
+        """peer_sum bring-up (collective, once per engine): the server exports its inbox
+        (one slot per worker RANK), every worker rank a receive slot, in fine-grained
+        device memory; the handles are exchanged and mapped, the server seeds every
+        receive slot with the current weights (round 0's pull) and drains one empty
+        launch of its kernel; each worker rank builds its lanes loop with the push / pull
+        addresses.  On one shared GPU (the rehearsals) the worker ranks' launches skip the
+        other ranks' and the server kernel's XCDs."""
+        cfg, sp = self.cfg, self.spec
+        h = _native.hip()
+        NS, Wr = sp.Fp // 32, self.world - 1
+        dev = self.device.index or 0
+        reg = h.PeerRegion(sp.P, NS, Wr if self.is_server else 1, dev)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, reg.handle())
+        self._psum_region = reg
+        wait_s = max(float(cfg.worker_timeout_s), float(cfg.idle_wait_s))
+        n_lanes = Wr * self.wpr
+        if oversubscribed() and n_lanes >= 8:
+            raise ValueError("one shared GPU: the worker ranks' lanes leave no XCD for the server kernel")
+        if self.is_server:
+            maps = [h.PeerMapping(handles[r], sp.P, NS, 1) for r in range(1, self.world)]
+            self._peer_maps = maps
+            d = dict(nworkers=Wr, lr=float(cfg.lr), K=sp.K, F=sp.F, FP=sp.Fp, P=int(sp.P),
+                     w=self.server.w.data_ptr(), inbox=reg.base, rx=[m.data(0) for m in maps],
+                     rx_tag=[m.tags(0) for m in maps], api=_native.host.capi(), tracker=self.server.tracker.handle,
+                     bsp=1, tag_wait_s=wait_s, worker_timeout_s=float(cfg.worker_timeout_s),
+                     # one shared GPU: the XCD after the worker ranks' lanes, half of its CUs (the
+                     # other ranks' per-round launches place -- and at once retire -- their
+                     # workgroups of that XCD on the other half)
+                     sxcd=n_lanes if oversubscribed() else 0, nwg=16 if oversubscribed() else 32)
+            ev = self.evalset
+            if self.log is not None and ev is not None:
+                d.update(sink=self.log.native.handle, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=int(ev.T))
+            self._pserver = h.PeerServer(d)
+            self._pserver.warm_up()
+            self._pserver.seed_rx()
+        else:
+            m = h.PeerMapping(handles[0], sp.P, NS, Wr)
+            self._peer_maps = [m]
+            self._run_bsp_lanes(None, 0, build_only=True)
+            lp = self._lanes
+            i = self.worker_id
+            lp.set_peer_sum(reg.data(0), reg.tags(0), m.data(i), m.tags(i), wait_s)
+            if oversubscribed():  # only this rank's lanes' XCDs: no rider spins on another process's CUs
+                mine = ((1 << self.wpr) - 1) << (i * self.wpr)
+                lp.set_xcd_skip(0xff & ~mine)
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
 
     def _lanes_chunks(self, lp, comm, stream, rounds: int, W) -> int:
         """Rounds of the native lanes loop: a bounded run in one call; an unbounded
@@ -674,23 +796,33 @@ class DistEngine:
         rank runs the same rounds per chunk (no deadline inside a chunk: the ranks'
         collectives must pair up)."""
         cfg = self.cfg
+        idle = float(cfg.idle_wait_s)
+        if lp is None:  # (peer_sum server rank: the persistent server kernel runs its rounds)
+            run = lambda k, r0: int(self._pserver.run_bsp(k, r0))
+        else:
+            run = lambda k, r0: int(lp.run(k, r0, stream, idle))
         if rounds:
-            return int(lp.run(rounds, int(self.rounds), stream))
+            return run(rounds, int(self.rounds))
         t_start = time.time()
         exhausted_since = None
-        flag = torch.zeros(2, dtype=torch.float32, device=self.device)
+        # (no communicator -- peer_sum: the vote over torch.distributed, on the device for nccl)
+        vdev = self.device if (comm is not None or dist.get_backend() == "nccl") else torch.device("cpu")
+        flag = torch.zeros(2, dtype=torch.float32, device=vdev)
         paced = cfg.stream_mode != "per_iter" or not cadence_free(cfg)
         chunk = 4 if paced else 256
         n = 0
         while True:
-            n += int(lp.run(chunk, int(self.rounds) + n, stream))
+            n += run(chunk, int(self.rounds) + n)
             now = time.time()
-            if W and all(lp.exhausted(i) for i in range(len(W))):
+            if lp is not None and W and all(lp.exhausted(i) for i in range(len(W))):
                 exhausted_since = exhausted_since or now
             done_data = not W or (exhausted_since is not None and now - exhausted_since >= cfg.idle_exit_s)
             flag[0] = 1.0 if (cfg.max_wallclock_s and now - t_start >= cfg.max_wallclock_s) else 0.0
             flag[1] = 0.0 if done_data else 1.0
-            comm.all_reduce(flag)
+            if comm is not None:
+                comm.all_reduce(flag)
+            else:
+                dist.all_reduce(flag)
             f = flag.tolist()
             if f[0] > 0 or f[1] == 0:
                 return n
@@ -881,6 +1013,10 @@ class DistEngine:
         for m in getattr(self, "_peer_maps", []):
             m.close()
         self._peer_maps = []
+        if hasattr(self, "_psum_region"):  # peer_sum: a later run sets the plane up afresh (tags from 0)
+            del self._psum_region
+            self._lanes = None
+            self._pserver = None
         if getattr(self, "_ctrl", None) is not None:
             if self.rank == 0:
                 self._ctrl.unlink()

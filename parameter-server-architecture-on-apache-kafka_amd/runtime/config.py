@@ -70,7 +70,9 @@ class PSConfig:
     verbose: bool = False
     # distributed
     # allreduce | reduce_bcast | sharded | keyrange (wide: sharded == keyrange) | peer (dense, several
-    # workers per rank: the sequential tracker over the peer data plane, csrc/comm/peer_bus.h)
+    # workers per rank: the sequential tracker over the peer data plane, csrc/comm/peer_bus.h) |
+    # peer_sum (dense, GPUs: rank-level lane sums into the server GPU's inbox, the server kernel's
+    # update written into every rank's receive slot; psx/parallel/dist.py)
     bsp_schedule: str = "allreduce"
     server_colocated: bool = True
     # logical workers per worker rank (one XCD each: the multi-lane round loop);

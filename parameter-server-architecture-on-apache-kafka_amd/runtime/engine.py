@@ -18,6 +18,7 @@ and logging code as the distributed engine.
 from __future__ import annotations
 
 import dataclasses
+import json
 import os
 import queue
 import threading
@@ -341,6 +342,8 @@ class LocalEngine:
         lp = h.LanesLoop(d, None)
         if self.tracer.enabled:  # --trace / --perf_log: phase times recorded by the kernels
             lp.set_trace(self._trace_cap)
+        elif os.environ.get("PSX_LANES_TRACE_OUT"):  # (tools: the device phase stamps of every round)
+            lp.set_trace(8192)
         lp.set_idle_wait(float(cfg.idle_wait_s))
         if os.environ.get("PSX_INJECT_SPIN_TIMEOUT"):  # tests: "round:polls"
             rr, sp_ = os.environ["PSX_INJECT_SPIN_TIMEOUT"].split(":")
@@ -441,6 +444,9 @@ class LocalEngine:
             lp.copy_out_all(ca[1], ca[2], stream)
             if srv.frag is not None:
                 srv.frag.refresh(srv.w)
+            if os.environ.get("PSX_LANES_TRACE_OUT") and not self.tracer.enabled:  # one JSON line per call
+                with open(os.environ["PSX_LANES_TRACE_OUT"], "a") as fh:
+                    fh.write(json.dumps({"rank": 0, "rows": [list(r) for r in lp.trace_take(stream)]}) + "\n")
             t_enq = time.time()
             torch.cuda.synchronize(self.device)
             t_sync = time.time()

@@ -15,6 +15,15 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
+    if mode in ("peer_sum", "peer_sum_vote"):
+        # BSP with rank-level sums over the peer data plane (--bsp_schedule peer_sum): 1 GPU server
+        # rank + worker ranks x 3 lanes, no collective per round; _vote: an unbounded run (1.5 s)
+        vote = mode == "peer_sum_vote"
+        return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,
+                        stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=0 if vote else 6,
+                        max_wallclock_s=1.5 if vote else 0.0, min_buffer_size=128, max_buffer_size=1024,
+                        init="random", seed=0, server_colocated=False, workers_per_rank=3, bsp_schedule="peer_sum",
+                        worker_timeout_s=20.0, idle_wait_s=20.0)
     if mode == "peer_bsp":  # sequential consistency over the peer data plane: 1 GPU server + ranks x 3 lanes
         return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,
                         stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=6, min_buffer_size=128,
@@ -50,6 +59,7 @@ def main():
     from psx.parallel.dist import DistEngine, init_from_env
     from psx.utils.data import synth_finefood
 
+    os.environ.setdefault("PSX_PSUM_DIAG", "1")
     rank, world, device = init_from_env()
     if mode.startswith("async") and rank == 0:  # (see test_async_lanes_worker_ranks; peer_*: a GPU server)
         device = torch.device("cpu")
@@ -57,9 +67,9 @@ def main():
     eng = DistEngine(cfg_for(world, mode), rank, world, device, train=train, test=test)
     kind = None
     out = eng.run()
-    res = {"rank": rank, "rounds": int(eng.rounds), "lanes": getattr(eng, "_lanes", None) is not None,
-           "updates": out.get("updates")}
-    for key in ("data_plane", "host_us_per_update"):
+    res = {"rank": rank, "rounds": int(eng.rounds),
+           "lanes": getattr(eng, "_lanes", None) is not None or bool(out.get("lanes")), "updates": out.get("updates")}
+    for key in ("data_plane", "host_us_per_update", "elapsed_s"):
         if key in out:
             res[key] = out[key]
     if rank == 0:
@@ -71,8 +81,11 @@ def main():
             res["arrivals"] = [list(a) for a in ps.arrivals]
     else:
         res["async_lanes"] = bool(out.get("async_lanes"))
+    if rank > 0 and mode.startswith("peer_sum"):  # (diagnostics) receive / push slice tags after the run
+        res["psum_tags"] = getattr(eng, "_psum_tags", None)
     with open(os.path.join(out_dir, f"{mode}_rank{rank}.json"), "w") as fh:
         json.dump(res, fh)
+    print("result:", json.dumps({k: v for k, v in res.items() if k != "server_rows"}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     del kind

@@ -662,6 +662,8 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("run_bsp", &PeerServer::run_bsp, py::arg("rounds"), py::arg("r0"), py::call_guard<py::gil_scoped_release>())
       .def("seed_rx", &PeerServer::seed_rx, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bsp_rounds", &PeerServer::bsp_rounds)
+      .def("set_trace", &PeerServer::set_trace, py::arg("cap"))
+      .def("trace_take", &PeerServer::trace_take)
       .def_property_readonly("host_us_per_round", &PeerServer::host_us_per_round)
       .def("fail", &PeerServer::fail, py::call_guard<py::gil_scoped_release>())
       .def("stop", &PeerServer::stop, py::call_guard<py::gil_scoped_release>())

@@ -98,6 +98,10 @@ struct SrvArgs {
   int cpar;
   int sxcd;                    // the XCD the server workgroups claim
   int nwg;                     // server workgroups (<= kSrvWg; each owns slices wg, wg + nwg, ...)
+  // (tools) per command n, workgroup 0's s_memrealtime stamps at tr[(n % tr_cap) * 4 + {0 command
+  // read, 1 its slices applied, 2 evaluation done, 3 the command number}]; null: off
+  long long* tr;
+  int tr_cap;
   long long launch;
   long long cmd_ticks;         // command wait budget (s_memrealtime ticks, 100 MHz)
   long long tag_ticks;         // inbox tag wait budget (ticks)

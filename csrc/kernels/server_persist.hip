@@ -130,6 +130,8 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
     srv_slice<FP>(a, cmd, s, err);
     if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
   }
+  long long* trn = (a.tr && wg == 0 && threadIdx.x == 0) ? a.tr + (size_t)(n % (unsigned long long)a.tr_cap) * 4 : nullptr;
+  if (trn) trn[1] = rt_now();
   if (cmd.log && cmd.slot_s) {  // the server row: every workgroup on the test tiles
     x_barrier(a.flags, wg, a.nwg, ++lw, err, a.spin);
     PairModels pm;
@@ -146,7 +148,10 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
     pm.bseq = cmd.seq_s;
     lane_pair_eval_at<FP>(lds, K, a.Xt, a.yt, a.T, wg, a.nwg, pm, a.acc, a.eticket);
   }
-  (void)n;
+  if (trn) {
+    trn[2] = rt_now();
+    trn[3] = (long long)n;
+  }
 }
 
 template <int FP>
@@ -193,8 +198,10 @@ __global__ __launch_bounds__(256) void server_persist_kernel(const SrvArgs pa) {
     // wait is bounded and ends in a stop command -- with the same poll budget the others'
     // faster polls would give up first during a long idle period)
     x_barrier(a.flags, wg, a.nwg, ++lw, err, 0x7fffffff);
-    if (wg == 0 && tid == 0)  // (its ring slot may be reused: the record is in the broadcast area)
+    if (wg == 0 && tid == 0) {  // (its ring slot may be reused: the record is in the broadcast area)
       __hip_atomic_store(a.consumed_host, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.tr) a.tr[(size_t)(n % (unsigned long long)a.tr_cap) * 4] = rt_now();
+    }
     SrvCmd cmd;
     {
       TagChunk ch[kCmdChunks];

@@ -464,6 +464,11 @@ void LanesLoop::set_peer_sum(uintptr_t rx, uintptr_t rx_tag, uintptr_t push, uin
   psum_push_ = reinterpret_cast<float*>(push);
   psum_push_tag_ = reinterpret_cast<unsigned*>(push_tag);
   psum_ticks_ = (long long)(std::min(std::max(wait_s, 1.0), 7200.0) * 1e8);
+  // the riders flush their counts with atomics and a ticket (no publish launch behind each
+  // round): on a GPU shared with the server kernel the publish launch waited 53 us behind
+  // the next round's lanes every other round (rocprofv3, profiles/r06/README.md), 88 vs 132
+  // us per round; in one process the two forms measure the same (90.1 / 89.8k updates/s)
+  slab_on_ = false;
 }
 
 // The previous round's rows as models of one evaluation pass: the lanes' local

@@ -81,6 +81,10 @@ class PeerServer {
   void seed_rx();
   int64_t bsp_rounds() const { return (int64_t)bsp_n_; }
   std::string bsp_tags() const;  // (failure reports) every rank's push / pull slice tags
+  // (tools) per-command device stamps of the next launches: a ring of cap commands;
+  // trace_take (the launch drained) -> {command, read, applied, evaluated} s_memrealtime ticks
+  void set_trace(int cap);
+  std::vector<std::vector<long long>> trace_take();
   double host_us_per_round() const { return bsp_run_ ? bsp_ns_ / 1000.0 / (double)bsp_run_ : 0.0; }
   // Stop the persistent launch and wait for it (idempotent).
   void stop();
@@ -138,6 +142,9 @@ class PeerServer {
   int64_t updates_ = 0, tokens_ = 0, updates_run_ = 0;
   double host_ns_ = 0.0;
   uint64_t bsp_n_ = 0;  // BSP rounds commanded so far (the tag of the last one)
+  long long* tr_ = nullptr;
+  int tr_cap_ = 0;
+  uint64_t tr_taken_ = 0;
   int64_t bsp_run_ = 0;
   double bsp_ns_ = 0.0;
 };

@@ -144,6 +144,7 @@ PeerServer::~PeerServer() {
   if (ws_) (void)hipFree(ws_);
   if (cmd_ring_) (void)hipHostFree(cmd_ring_);
   if (err_host_) (void)hipHostFree(err_host_);
+  if (tr_) (void)hipFree(tr_);
 }
 
 void PeerServer::check_api(int rc, const char* what) const {
@@ -353,6 +354,35 @@ std::string PeerServer::bsp_tags() const {
          ".." + std::to_string(b1);
   }
   return m;
+}
+
+void PeerServer::set_trace(int cap) {
+  if (running_) throw std::logic_error("PeerServer::set_trace: the launch is running");
+  if (tr_) (void)hipFree(tr_);
+  tr_ = nullptr;
+  tr_cap_ = cap > 0 ? cap : 0;
+  if (tr_cap_) {
+    hip_check(hipMalloc(&tr_, (size_t)tr_cap_ * 4 * sizeof(long long)), "hipMalloc(server trace)");
+    hip_check(hipMemset(tr_, 0, (size_t)tr_cap_ * 4 * sizeof(long long)), "hipMemset(server trace)");
+    hip_check(hipDeviceSynchronize(), "server trace");
+  }
+  args_.tr = tr_;
+  args_.tr_cap = tr_cap_;
+  tr_taken_ = cmds_;
+}
+
+std::vector<std::vector<long long>> PeerServer::trace_take() {
+  std::vector<std::vector<long long>> out;
+  if (!tr_ || running_) return out;
+  std::vector<long long> h((size_t)tr_cap_ * 4);
+  hip_check(hipMemcpy(h.data(), tr_, h.size() * sizeof(long long), hipMemcpyDeviceToHost), "server trace copy");
+  const uint64_t first = std::max<uint64_t>(tr_taken_ + 1, cmds_ > (uint64_t)tr_cap_ ? cmds_ - tr_cap_ + 1 : 1);
+  for (uint64_t n = first; n <= cmds_; ++n) {
+    const long long* e = h.data() + (size_t)(n % (uint64_t)tr_cap_) * 4;
+    if (e[3] == (long long)n) out.push_back({(long long)n, e[0], e[1], e[2]});
+  }
+  tr_taken_ = cmds_;
+  return out;
 }
 
 void PeerServer::seed_rx() {

@@ -715,6 +715,9 @@ class DistEngine:
                 srv.frag.refresh(srv.w)
             srv.updates += N * n
             self.native_host_us_per_round = float(self._pserver.host_us_per_round)
+            if os.environ.get("PSX_LANES_TRACE_OUT"):
+                with open(f"{os.environ['PSX_LANES_TRACE_OUT']}.rank0", "a") as fh:
+                    fh.write(json.dumps({"rank": 0, "server": [list(r) for r in self._pserver.trace_take()]}) + "\n")
             torch.cuda.synchronize(self.device)
         else:
             n = self._run_bsp_lanes(None, int(cfg.max_iters))
@@ -765,13 +768,16 @@ class DistEngine:
                      # one shared GPU: the XCD after the worker ranks' lanes, half of its CUs (the
                      # other ranks' per-round launches place -- and at once retire -- their
                      # workgroups of that XCD on the other half)
-                     sxcd=n_lanes if oversubscribed() else 0, nwg=16 if oversubscribed() else 32)
+                     sxcd=n_lanes if oversubscribed() else 0,
+                     nwg=int(os.environ.get("PSX_PSUM_NWG", 16 if oversubscribed() else 32)))
             ev = self.evalset
-            if self.log is not None and ev is not None:
+            if self.log is not None and ev is not None and os.environ.get("PSX_PSUM_NO_SERVER_ROWS") != "1":
                 d.update(sink=self.log.native.handle, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=int(ev.T))
             self._pserver = h.PeerServer(d)
             self._pserver.warm_up()
             self._pserver.seed_rx()
+            if os.environ.get("PSX_LANES_TRACE_OUT"):  # (tools: the server kernel's per-round stamps)
+                self._pserver.set_trace(8192)
         else:
             m = h.PeerMapping(handles[0], sp.P, NS, Wr)
             self._peer_maps = [m]

@@ -591,6 +591,7 @@ PYBIND11_MODULE(_psx_hip, m) {
            }),
            py::arg("P"), py::arg("NS"), py::arg("slots"), py::arg("device") = 0)
       .def("handle", [](const PeerRegion& r) { return py::bytes(r.handle()); })
+      .def("fill_tags", &PeerRegion::fill_tags, py::arg("value"))
       .def_property_readonly("base", &PeerRegion::base)
       .def_property_readonly("stride", [](const PeerRegion& r) { return r.layout().stride(); })
       .def_property_readonly("nbytes", [](const PeerRegion& r) { return r.layout().bytes(); })
@@ -642,6 +643,8 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.sxcd = (int)I("sxcd", 0);
              c.bsp = I("bsp", 0) != 0;
              c.nwg = (int)I("nwg", kSrvWg);
+             c.batch = (int)I("batch", 64);
+             c.standin = I("standin", 0) != 0;
              c.tag_wait_s = d.contains("tag_wait_s") ? d["tag_wait_s"].cast<double>() : 600.0;
              prepare_kernels();
              return std::make_unique<PeerServer>(c, nullptr);
@@ -663,6 +666,9 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def("seed_rx", &PeerServer::seed_rx, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bsp_rounds", &PeerServer::bsp_rounds)
       .def("set_trace", &PeerServer::set_trace, py::arg("cap"))
+      .def("bench_async", &PeerServer::bench_async, py::arg("deltas"), py::arg("log_every") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("deltas_per_command", &PeerServer::deltas_per_command)
       .def("trace_take", &PeerServer::trace_take)
       .def_property_readonly("host_us_per_round", &PeerServer::host_us_per_round)
       .def("fail", &PeerServer::fail, py::call_guard<py::gil_scoped_release>())

@@ -50,6 +50,7 @@ class PeerRegion {
   PeerRegion(const PeerRegion&) = delete;
   PeerRegion& operator=(const PeerRegion&) = delete;
   std::string handle() const;  // 64-byte hipIpcMemHandle_t for the other ranks
+  void fill_tags(unsigned value);  // (tools) every slice tag of every slot = value
   uintptr_t base() const { return reinterpret_cast<uintptr_t>(p_); }
   const PeerLayout& layout() const { return lay_; }
   float* data(int slot) const { return reinterpret_cast<float*>(p_) + (size_t)slot * (size_t)lay_.stride(); }

@@ -1,6 +1,8 @@
 // Peer data plane regions (see peer_bus.h).
 #include "peer_bus.h"
 
+#include <vector>
+
 #include <cstring>
 #include <stdexcept>
 
@@ -23,6 +25,12 @@ PeerRegion::PeerRegion(const PeerLayout& lay, int device) : lay_(lay) {
 
 PeerRegion::~PeerRegion() {
   if (p_) (void)hipFree(p_);
+}
+
+void PeerRegion::fill_tags(unsigned value) {
+  std::vector<unsigned> h((size_t)lay_.slots * lay_.NS, value);
+  ck(hipMemcpy(static_cast<char*>(p_) + lay_.tag_off(), h.data(), h.size() * 4, hipMemcpyHostToDevice), "tags");
+  ck(hipDeviceSynchronize(), "sync");
 }
 
 std::string PeerRegion::handle() const {

@@ -41,6 +41,15 @@ constexpr int kSrvWg = 32;        // workgroups of the server launch (one XCD)
 // w += lr * sum, and write the new weights into every rank of relmask's receive slot with
 // tag dtag (ServerProcessor.java:111-120: every worker answered once the round is complete)
 constexpr int kSrvBspSum = -2;
+// SrvCmd::k of a BATCH of asynchronous deltas (the tokens the host had popped when it
+// wrote the command): dtag = the entry count m <= kSrvMaxBatch, relmask = the index of the
+// first entry (0-based) in the pinned entry ring; log / slot_s / seq_s belong to the last
+// entry (the host ends a batch at a logging delta).  Each slice applies the m deltas in
+// entry order -- the single GRADIENTS_TOPIC partition's order, ServerProcessor.java:143-183
+// -- and writes each entry's releases right after ITS update.
+constexpr int kSrvBatch = -3;
+constexpr int kSrvMaxBatch = 64;
+constexpr int kEntChunks = 2;  // 32-B entries {tag, k, dtag, 0} {tag, relmask lo, relmask hi, 0}
 constexpr int kSrvMaxWorkers = 64;  // the release mask's width
 constexpr int kCmdChunks = 4;     // 64-B command records
 
@@ -69,6 +78,21 @@ PSX_HD inline void unpack_cmd(const TagChunk* ch, SrvCmd& c) {
   c.seq_s = ch[2].c;
 }
 
+struct SrvEnt {
+  int k;                        // worker whose delta is applied
+  unsigned dtag;                // its inbox tag (vc + 1)
+  unsigned long long relmask;   // workers released right after this delta's update
+};
+PSX_HD inline void pack_ent(const SrvEnt& e, unsigned tag, TagChunk* ch) {
+  ch[0] = TagChunk{tag, (unsigned)e.k, e.dtag, 0u};
+  ch[1] = TagChunk{tag, (unsigned)e.relmask, (unsigned)(e.relmask >> 32), 0u};
+}
+PSX_HD inline void unpack_ent(const TagChunk* ch, SrvEnt& e) {
+  e.k = (int)ch[0].a;
+  e.dtag = ch[0].b;
+  e.relmask = ((unsigned long long)ch[1].b << 32) | ch[1].a;
+}
+
 struct SrvArgs {
   int K, F, FP, P;
   int N;                       // workers
@@ -84,6 +108,9 @@ struct SrvArgs {
   unsigned* ptag;              // [N][FP/32] pulls sent per worker and slice (this GPU)
   TagChunk* cmd;               // pinned command ring [ring][kCmdChunks]
   int ring;
+  TagChunk* ent;               // pinned entry ring [ent_cap][kEntChunks] of batch commands
+  int ent_cap;
+  unsigned long long* erec;    // [kSrvMaxBatch * kEntChunks * 2] the batch's entries broadcast (device)
   unsigned long long cmd0;     // commands consumed before this launch
   unsigned long long* consumed_host;  // pinned: the last command read (the host's ring flow control)
   unsigned long long* err_host;  // pinned: (command << 8) | code of a timed-out wait

@@ -34,7 +34,121 @@ __device__ __forceinline__ void srv_wait_cmd(const SrvArgs& a, unsigned long lon
     c = TagChunk{(unsigned)want, tid == 0 ? 1u : 0u, 0u, 0u};  // stop
     if (tid == 0) __hip_atomic_store(a.err_host, (want << 8) | 7ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // a batch command: its entries too, every lane one 16-B chunk per pass (all in flight),
+  // into the entry broadcast area -- the barrier behind this publishes both
+  const int k0 = (int)__shfl(c.b, 0, 64);
+  if (ok && k0 == kSrvBatch) {
+    const int m = (int)__shfl(c.c, 0, 64);
+    const unsigned long long e0 = ((unsigned long long)__shfl(c.c, 1, 64) << 32) | __shfl(c.b, 1, 64);
+    const int nch = (m < kSrvMaxBatch ? m : kSrvMaxBatch) * kEntChunks;
+    for (int i0 = 0; i0 < nch && ok; i0 += 64) {
+      const int i = i0 + tid;
+      const bool mine = i < nch;
+      const unsigned long long e = e0 + (unsigned long long)(i / kEntChunks);
+      const TagChunk* es = a.ent + (size_t)(e % (unsigned long long)a.ent_cap) * kEntChunks + (i % kEntChunks);
+      TagChunk v = TagChunk{0, 0, 0, 0};
+      for (;;) {
+        if (mine) v = srv_ld_sys_chunk(es, 16u, 0u);
+        ok = __all(!mine || v.tag == (unsigned)(e + 1ull));
+        if (ok || rt_now() > t_end) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (mine) ((TagChunk*)a.erec)[i] = v;
+    }
+    if (!ok) {  // (never expected: the host writes the entries before their command)
+      c = TagChunk{(unsigned)want, tid == 0 ? 1u : 0u, 0u, 0u};
+      if (tid == 0) __hip_atomic_store(a.err_host, (want << 8) | 8ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   if (tid < kCmdChunks) ((TagChunk*)a.rec)[tid] = c;
+}
+
+// Slice s of a batch command: the entries' deltas in entry order, each entry's releases
+// written right after its update (ServerProcessor.java:143-183: apply, then answer).  The
+// deltas' loads go out kBChunk at a time; w is stored once, after the last.
+template <int FP>
+__device__ __forceinline__ void srv_batch_slice(const SrvArgs& a, const SrvCmd& cmd, int s, unsigned long long* err) {
+  constexpr int NS = FP / 32;
+  constexpr int kBChunk = 8;
+  const int tid = threadIdx.x, K = a.K;
+  const int c = tid >> 5, f = s * 32 + (tid & 31);
+  const bool coef = c < K, icpt = s == 0 && tid < K;
+  const size_t e = (size_t)c * FP + f, ei = (size_t)K * FP + tid;
+  const int m = (int)(cmd.dtag < (unsigned)kSrvMaxBatch ? cmd.dtag : (unsigned)kSrvMaxBatch);
+  __shared__ SrvEnt ents[kSrvMaxBatch];
+  __shared__ int ok_s;
+  if (tid < m) {
+    TagChunk ch[kEntChunks];
+#pragma unroll
+    for (int q = 0; q < kEntChunks; ++q)
+      ch[q] = __builtin_bit_cast(TagChunk, __builtin_nontemporal_load((const u32x4*)(a.erec + 2 * (tid * kEntChunks + q))));
+    unpack_ent(ch, ents[tid]);
+  }
+  __syncthreads();
+  // every entry's tag of this slice, one lane per entry (wave 0), then the acquire
+  if (tid < 64) {
+    bool late = false;
+    if (tid < m) {
+      const unsigned* tg = a.inbox_tag + (size_t)ents[tid].k * NS + s;
+      const long long t_end = rt_now() + a.tag_ticks;
+      while ((int)(ld_sys_u32(tg) - ents[tid].dtag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
+    }
+    const bool any_late = __any(late);
+    if (tid == 0) {
+      ok_s = any_late ? 0 : 1;
+      if (any_late) xstore(err, 11ull);  // a delta never arrived: apply none of the batch's
+      // (no acquire: the deltas are read with system-scope loads below)
+    }
+  }
+  __syncthreads();
+  float nw = coef ? ld_sc1(a.w + e) : 0.f;
+  float nb = icpt ? ld_sc1(a.w + ei) : 0.f;
+  if (ok_s) {
+    for (int j0 = 0; j0 < m; j0 += kBChunk) {
+      float dl[kBChunk], di[kBChunk];
+#pragma unroll
+      for (int u = 0; u < kBChunk; ++u) {  // this chunk's loads all in flight
+        dl[u] = di[u] = 0.f;
+        if (j0 + u < m) {
+          const float* d = a.inbox + (size_t)ents[j0 + u].k * (size_t)a.in_stride;
+          if (coef) dl[u] = ld_sys_f32(d + e);
+          if (icpt) di[u] = ld_sys_f32(d + ei);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kBChunk; ++u) {
+        if (j0 + u >= m) break;
+        nw += a.lr * dl[u];
+        nb += a.lr * di[u];
+        for (unsigned long long rm = ents[j0 + u].relmask; rm; rm &= rm - 1) {  // the weights right after it
+          float* dst = a.rx[__builtin_ctzll(rm)];
+          if (coef) st_sys_f32(dst + e, nw);
+          if (icpt) st_sys_f32(dst + ei, nb);
+        }
+      }
+    }
+    if (coef) st_sc1(a.w + e, nw);
+    if (icpt) st_sc1(a.w + ei, nb);
+  }
+  if (cmd.log) {  // the global model after the batch's last (logging) delta
+    if (coef) write_frag(a.shi, a.slo, c, f, f < a.F ? nw : 0.f);
+    if (icpt) a.sb[tid] = nb;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    // (no release fence: the receive slots were written with sc0 sc1 stores, drained by
+    // every wave's vmcnt(0) above -- a system-scope release would write back the XCD's L2)
+    for (int j = 0; j < m; ++j)
+      for (unsigned long long rm = ents[j].relmask; rm; rm &= rm - 1) {
+        const int r = __builtin_ctzll(rm);
+        unsigned* pt = a.ptag + (size_t)r * NS + s;
+        const unsigned t = __hip_atomic_load((g_u32*)pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        __hip_atomic_store((g_u32*)pt, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sys_u32(a.rx_tag[r] + s, t);
+      }
+  }
+  __syncthreads();  // (ents / ok_s: the next slice of this workgroup)
 }
 
 // Slice s of command `cmd` (one workgroup; every thread calls it).
@@ -63,9 +177,8 @@ __device__ __forceinline__ void srv_slice(const SrvArgs& a, const SrvCmd& cmd, i
       }
       ok_s = !late;
       if (late) xstore(err, 11ull);  // a delta never arrived: apply nothing
-      // (the inbox is read with system-scope loads; a BSP round's sums were stored sc0 sc1
-      // and need no acquire -- the per-worker deltas of the asynchronous plane keep it)
-      if (cmd.k != kSrvBspSum) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      // (no acquire: the inbox is read with system-scope loads, and its writers drained
+      // their stores before the tag)
     }
     __syncthreads();
     if (ok_s) {
@@ -102,9 +215,8 @@ __device__ __forceinline__ void srv_slice(const SrvArgs& a, const SrvCmd& cmd, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      // (a BSP round: the slices are sc0 sc1 stores, drained above -- no release fence, which
-      // would write back this XCD's L2 on the round's critical path)
-      if (cmd.k != kSrvBspSum) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      // (no release fence: the slices are sc0 sc1 stores, drained above -- a system-scope
+      // release would write back this XCD's L2 on the path to the released workers)
       for (unsigned long long m = cmd.relmask; m; m &= m - 1) {
         const int j = __builtin_ctzll(m);
         unsigned* pt = a.ptag + (size_t)j * NS + s;
@@ -127,8 +239,12 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
   // workgroup wg owns slices wg, wg + nwg, ... (nwg < NS: a server launch that leaves CUs of
   // its XCD to other processes on a shared GPU)
   for (int s = wg; s < NS; s += a.nwg) {
-    srv_slice<FP>(a, cmd, s, err);
-    if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
+    if (cmd.k == kSrvBatch) {
+      srv_batch_slice<FP>(a, cmd, s, err);
+    } else {
+      srv_slice<FP>(a, cmd, s, err);
+      if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
+    }
   }
   long long* trn = (a.tr && wg == 0 && threadIdx.x == 0) ? a.tr + (size_t)(n % (unsigned long long)a.tr_cap) * 4 : nullptr;
   if (trn) trn[1] = rt_now();

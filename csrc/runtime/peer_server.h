@@ -55,6 +55,12 @@ struct PeerServerCfg {
   // workgroups of the server launch on its XCD (<= 32, each owns every nwg-th slice): a
   // GPU shared with other ranks' launches gets fewer, leaving CUs of the XCD to them
   int nwg = kSrvWg;
+  // asynchronous plane: deltas per server command (1..64) -- the tokens already popped when
+  // a command is written go as ONE batch command, applied in token order slice-parallel
+  // (1: one command per delta)
+  int batch = 64;
+  // stand-in workers (tools/peer_server_bench.py): no token / reply queues needed
+  bool standin = false;
 };
 
 class PeerServer {
@@ -80,6 +86,13 @@ class PeerServer {
   // pull of round 0)
   void seed_rx();
   int64_t bsp_rounds() const { return (int64_t)bsp_n_; }
+  // deltas per command of the asynchronous plane so far (batching)
+  double deltas_per_command() const { return batches_ ? (double)batched_deltas_ / (double)batches_ : 0.0; }
+  // Microbenchmark (stand-in workers, inbox tags pre-armed): `deltas` asynchronous deltas
+  // (ASP: worker i % N, each releasing itself) through the tracker, the commands (batches of
+  // cfg.batch) and the server kernel, no reply queues; worker 0's deltas produce server rows
+  // when a sink is bound; returns {seconds to drain, host seconds}
+  std::vector<double> bench_async(int64_t deltas, int log_every);
   std::string bsp_tags() const;  // (failure reports) every rank's push / pull slice tags
   // (tools) per-command device stamps of the next launches: a ring of cap commands;
   // trace_take (the launch drained) -> {command, read, applied, evaluated} s_memrealtime ticks
@@ -112,9 +125,13 @@ class PeerServer {
   void check_api(int rc, const char* what) const;
   void check_device() const;
   void launch();
+  void wait_ring();  // until the next command's ring slot is free
   void write_cmd(const SrvCmd& c);
-  // command k (-1: none) + releases (ks, vs) + replies; returns after the host part
+  // command k (-1: none) + releases (ks, vs) + replies; returns after the host part.
+  // A delta (k >= 0) joins the open batch (flushed by flush_batch, at a logging delta or
+  // when full); a release-only command flushes the batch first
   void issue(int k, int64_t vc, const int* ks, const int64_t* vs, int n);
+  void flush_batch();
   int log_worker() const;
 
   PeerServerCfg cfg_;
@@ -139,6 +156,17 @@ class PeerServer {
   std::vector<int> rel_k_;
   std::vector<int64_t> rel_v_;
   std::vector<std::pair<int, int64_t>> arrivals_;
+  // the open batch: entries, its server-row slot (the last entry's), the replies owed
+  TagChunk* ent_ring_ = nullptr;  // pinned [ent_cap_][kEntChunks]
+  int ent_cap_ = 0;
+  uint64_t ents_ = 0;             // entries written (the kernel's numbering: 1..ents_)
+  std::vector<SrvEnt> bat_;
+  int bat_slot_ = -1;
+  uint64_t bat_seq_ = 0;
+  uintptr_t bat_addr_ = 0;
+  int64_t bat_vc_ = 0;
+  std::vector<CtrlToken> bat_rep_;
+  int64_t batches_ = 0, batched_deltas_ = 0;
   int64_t updates_ = 0, tokens_ = 0, updates_run_ = 0;
   double host_ns_ = 0.0;
   uint64_t bsp_n_ = 0;  // BSP rounds commanded so far (the tag of the last one)

@@ -28,7 +28,7 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   (void)stream;  // the persistent launch gets a stream of its own (nothing else is ordered behind it)
   const int N = cfg.nworkers;
   if (N < 1 || N > kSrvMaxWorkers) throw std::invalid_argument("PeerServer: 1 .. 64 workers");
-  if (!cfg.api || (!cfg.bsp && (!cfg.tracker || !cfg.ctrl)))
+  if (!cfg.api || (!cfg.bsp && (!cfg.tracker || (!cfg.ctrl && !cfg.standin))))
     throw std::invalid_argument("PeerServer: missing host runtime handles");
   api_ = reinterpret_cast<const HostApi*>(cfg.api);
   if (api_->version != kHostApiVersion) throw std::runtime_error("PeerServer: host runtime C ABI version mismatch");
@@ -39,11 +39,14 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   NS_ = cfg.FP / 32;
   if (!cfg.inbox || cfg.lay.P != cfg.P || cfg.lay.NS != NS_ || cfg.lay.slots < N)
     throw std::invalid_argument("PeerServer: inbox region layout");
-  if ((int)cfg.rx.size() != N || (int)cfg.rx_tag.size() != N || (!cfg.bsp && (int)cfg.replies.size() != N))
+  if ((int)cfg.rx.size() != N || (int)cfg.rx_tag.size() != N ||
+      (!cfg.bsp && !cfg.standin && (int)cfg.replies.size() != N))
     throw std::invalid_argument("PeerServer: one receive slot, tag array and reply queue per worker");
+  const bool need_q = !cfg.bsp && !cfg.standin;  // (token / reply queues)
   for (int j = 0; j < N; ++j)
-    if (!cfg.rx[j] || !cfg.rx_tag[j] || (!cfg.bsp && !cfg.replies[j]))
+    if (!cfg.rx[j] || !cfg.rx_tag[j] || (need_q && !cfg.replies[j]))
       throw std::invalid_argument("PeerServer: null peer handle");
+  if (cfg.batch < 1 || cfg.batch > kSrvMaxBatch) throw std::invalid_argument("PeerServer: batch 1 .. 64");
   if (cfg.sink && (!cfg.Xt || !cfg.yt || cfg.T < 1)) throw std::invalid_argument("PeerServer: server rows need the test set");
   if (cfg.sxcd < 0 || cfg.sxcd > 7) throw std::invalid_argument("PeerServer: sxcd in 0..7");
   // device workspace (ALL device memory and its zero-fill here, before any
@@ -66,6 +69,7 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   const size_t o_flags = take((size_t)(kSrvWg + 1) * 32 * 8);
   const size_t o_rec = take(32 * 8);
   const size_t o_claim = take(64 * 4);
+  const size_t o_erec = take((size_t)kSrvMaxBatch * kEntChunks * 16);
   hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(peer server)");
   hip_check(hipMalloc(&ws_, off), "hipMalloc(peer server workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(peer server workspace)");
@@ -78,6 +82,11 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   hip_check(hipHostMalloc((void**)&err_host_, 2 * sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped),
             "hipHostMalloc(error word)");
   std::memset((void*)cmd_ring_, 0, sizeof(TagChunk) * kCmdChunks * ring_);
+  ent_cap_ = (ring_ + 1) * kSrvMaxBatch;  // (every command in flight holds <= kSrvMaxBatch entries)
+  hip_check(hipHostMalloc((void**)&ent_ring_, sizeof(TagChunk) * kEntChunks * (size_t)ent_cap_,
+                          hipHostMallocCoherent | hipHostMallocMapped),
+            "hipHostMalloc(entry ring)");
+  std::memset((void*)ent_ring_, 0, sizeof(TagChunk) * kEntChunks * (size_t)ent_cap_);
   err_host_[0] = err_host_[1] = 0;
   consumed_host_ = err_host_ + 1;
   hip_check(hipDeviceSynchronize(), "peer server setup");
@@ -101,6 +110,9 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   a.ptag = reinterpret_cast<unsigned*>(b + o_ptag);
   a.cmd = cmd_ring_;
   a.ring = ring_;
+  a.ent = ent_ring_;
+  a.ent_cap = ent_cap_;
+  a.erec = reinterpret_cast<unsigned long long*>(b + o_erec);
   a.consumed_host = consumed_host_;
   a.err_host = err_host_;
   a.Xt = cfg.Xt;
@@ -143,6 +155,7 @@ PeerServer::~PeerServer() {
   }
   if (ws_) (void)hipFree(ws_);
   if (cmd_ring_) (void)hipHostFree(cmd_ring_);
+  if (ent_ring_) (void)hipHostFree(ent_ring_);
   if (err_host_) (void)hipHostFree(err_host_);
   if (tr_) (void)hipFree(tr_);
 }
@@ -201,8 +214,11 @@ void PeerServer::launch() {
   running_ = true;
 }
 
-void PeerServer::write_cmd(const SrvCmd& c) {
-  // ring flow control: slot (n - 1) % ring is free once the kernel read command n - ring
+void PeerServer::wait_ring() {
+  // ring flow control: slot (n - 1) % ring is free once the kernel read command n - ring --
+  // and with it every entry of that command (a command in flight holds <= kSrvMaxBatch
+  // entries, the entry ring ring_ + 1 times that: the next command's entries never overwrite
+  // those of a command the kernel has not read)
   const uint64_t n = cmds_ + 1;
   if (n > (uint64_t)ring_) {
     const double t0 = now_s();
@@ -212,6 +228,11 @@ void PeerServer::write_cmd(const SrvCmd& c) {
       _mm_pause();
     }
   }
+}
+
+void PeerServer::write_cmd(const SrvCmd& c) {
+  wait_ring();
+  const uint64_t n = cmds_ + 1;
   TagChunk ch[kCmdChunks];
   pack_cmd(c, (unsigned)n, ch);
   volatile TagChunk* dst = cmd_ring_ + (size_t)((n - 1) % (uint64_t)ring_) * kCmdChunks;
@@ -225,43 +246,100 @@ void PeerServer::write_cmd(const SrvCmd& c) {
 }
 
 void PeerServer::issue(int k, int64_t vc, const int* ks, const int64_t* vs, int n) {
-  SrvCmd c{};
-  c.k = k;
-  c.dtag = k >= 0 ? (unsigned)(vc + 1) : 0u;
-  int slot = -1;
-  uint64_t seq = 0;
-  if (k >= 0 && cfg_.sink && k == log_worker()) {  // the global model's test metrics: one server row
-    uintptr_t addr = 0;
-    slot = api().sink_acquire((void*)cfg_.sink, &seq, &addr);
-    check_api(slot, "metrics sink acquire");
-    c.log = 1;
-    c.slot_s = addr;
-    c.seq_s = (unsigned)seq;
-  }
+  if (k < 0) flush_batch();  // (a release-only command: after the deltas before it)
+  SrvEnt e{};
+  e.k = k;
+  e.dtag = k >= 0 ? (unsigned)(vc + 1) : 0u;
   const double t = now_s();
   for (int i = 0; i < n; ++i) {
     const int j = ks[i];
     if (j < 0 || j >= cfg_.nworkers) throw std::logic_error("PeerServer: release of an unknown worker");
     if (finished_[j]) continue;
-    c.relmask |= 1ull << j;
-  }
-  write_cmd(c);
-  // the replies: which worker the weights in flight are for, and their pull tag
-  for (int i = 0; i < n; ++i) {
-    const int j = ks[i];
-    if (finished_[j]) continue;
+    e.relmask |= 1ull << j;
     busy_since_[j] = t;
+    // the replies: which worker the weights in flight are for, and their pull tag (the
+    // kernel bumps a slot's tag once per release, in command / entry order)
     CtrlToken r{};
     r.worker = j;
     r.vc = vs[i];
     r.aux = (int64_t)++ptag_[j];
-    if (api().ctrl_push((void*)cfg_.replies[j], &r, cfg_.worker_timeout_s) != 1)
-      throw std::runtime_error("PeerServer: reply queue of worker " + std::to_string(j) + " full");
+    bat_rep_.push_back(r);
   }
-  if (slot >= 0) {
-    SinkRecord rec{slot, 1 | kSinkTagged, seq, -1, -1, vc, 0};
+  const bool logs = k >= 0 && cfg_.sink && k == log_worker();
+  if (k < 0) {  // releases only: a command of its own
+    SrvCmd c{};
+    c.k = -1;
+    c.relmask = e.relmask;
+    write_cmd(c);
+    flush_batch();  // (the replies)
+    return;
+  }
+  bat_.push_back(e);
+  if (logs) {  // the global model's test metrics after this delta: one server row, ending the batch
+    uintptr_t addr = 0;
+    bat_slot_ = api().sink_acquire((void*)cfg_.sink, &bat_seq_, &addr);
+    check_api(bat_slot_, "metrics sink acquire");
+    bat_addr_ = addr;
+    bat_vc_ = vc;
+  }
+  if (logs || (int)bat_.size() >= cfg_.batch) flush_batch();
+}
+
+void PeerServer::flush_batch() {
+  const int m = (int)bat_.size();
+  if (m == 1) {  // one delta: the classic command
+    SrvCmd c{};
+    c.k = bat_[0].k;
+    c.dtag = bat_[0].dtag;
+    c.relmask = bat_[0].relmask;
+    if (bat_slot_ >= 0) {
+      c.log = 1;
+      c.slot_s = bat_addr_;
+      c.seq_s = (unsigned)bat_seq_;
+    }
+    write_cmd(c);
+  } else if (m > 1) {  // the entries first (the kernel reads them after the command's tag)
+    wait_ring();  // (the command's slot free: so is every entry slot written below)
+    const uint64_t e0 = ents_;
+    for (int j = 0; j < m; ++j) {
+      TagChunk ch[kEntChunks];
+      pack_ent(bat_[j], (unsigned)(e0 + (uint64_t)j + 1), ch);
+      volatile TagChunk* dst = ent_ring_ + (size_t)((e0 + (uint64_t)j) % (uint64_t)ent_cap_) * kEntChunks;
+      for (int q = 0; q < kEntChunks; ++q) {
+        __m128i v;
+        std::memcpy(&v, &ch[q], 16);
+        _mm_store_si128((__m128i*)(void*)&dst[q], v);
+      }
+    }
+    ents_ = e0 + (uint64_t)m;
+    std::atomic_thread_fence(std::memory_order_release);
+    SrvCmd c{};
+    c.k = kSrvBatch;
+    c.dtag = (unsigned)m;
+    c.relmask = e0;
+    if (bat_slot_ >= 0) {
+      c.log = 1;
+      c.slot_s = bat_addr_;
+      c.seq_s = (unsigned)bat_seq_;
+    }
+    write_cmd(c);
+  }
+  if (m > 0) {
+    ++batches_;
+    batched_deltas_ += m;
+  }
+  for (const CtrlToken& r : bat_rep_) {
+    if (cfg_.standin) continue;
+    if (api().ctrl_push((void*)cfg_.replies[r.worker], &r, cfg_.worker_timeout_s) != 1)
+      throw std::runtime_error("PeerServer: reply queue of worker " + std::to_string(r.worker) + " full");
+  }
+  if (bat_slot_ >= 0) {
+    SinkRecord rec{bat_slot_, 1 | kSinkTagged, bat_seq_, -1, -1, bat_vc_, 0};
     check_api(api().sink_submit_many((void*)cfg_.sink, 1, &rec), "metrics sink submit");
   }
+  bat_.clear();
+  bat_rep_.clear();
+  bat_slot_ = -1;
 }
 
 void PeerServer::begin() {
@@ -302,6 +380,7 @@ void PeerServer::fail(int k) {
 
 void PeerServer::stop() {
   if (!running_) return;
+  flush_batch();  // (deltas of an open batch before the stop command)
   SrvCmd c{};
   c.stop = 1;
   write_cmd(c);
@@ -320,6 +399,32 @@ void PeerServer::stop() {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   check_device();
+}
+
+std::vector<double> PeerServer::bench_async(int64_t deltas, int log_every) {
+  if (!cfg_.standin) throw std::logic_error("PeerServer::bench_async: needs stand-in workers (cfg standin)");
+  const int N = cfg_.nworkers;
+  // every stand-in worker holds the weights of its clock (the bootstrap), as after begin()
+  std::fill(finished_.begin(), finished_.end(), 0);
+  launch();
+  std::vector<int64_t> vc(N, 0);
+  for (int j = 0; j < N; ++j) vc[j] = api().tracker_clock((void*)cfg_.tracker, j);
+  const double t0 = now_s();
+  for (int64_t i = 0; i < deltas; ++i) {
+    const int k = (int)(i % N);
+    const int n = api().tracker_on_delta((void*)cfg_.tracker, k, vc[k], rel_k_.data(), rel_v_.data(), (int)rel_k_.size());
+    check_api(n, "tracker on_delta");
+    // (with a metrics sink, worker 0's deltas produce the server rows, as in run())
+    issue(k, vc[k], rel_k_.data(), rel_v_.data(), n);
+    ++vc[k];
+    ++updates_;
+  }
+  flush_batch();
+  (void)log_every;
+  const double t1 = now_s();
+  stop();
+  const double t2 = now_s();
+  return {t2 - t0, t1 - t0};
 }
 
 std::string PeerServer::bsp_tags() const {
@@ -439,8 +544,18 @@ AsyncStatus PeerServer::run(int64_t checkpoint_every) {
     for (int j = 0; j < cfg_.nworkers; ++j) open += !finished_[j];
     if (open == 0) break;
     CtrlToken t;
-    const int got = api().ctrl_pop((void*)cfg_.ctrl, &t, poll);
-    check_api(got, "token pop");
+    int got = 0;
+    if (!bat_.empty()) {  // an open batch takes the tokens already queued, then goes out
+      got = api().ctrl_pop((void*)cfg_.ctrl, &t, 0.0);
+      check_api(got, "token pop");
+      if (!got) {
+        flush_batch();
+        continue;
+      }
+    } else {
+      got = api().ctrl_pop((void*)cfg_.ctrl, &t, poll);
+      check_api(got, "token pop");
+    }
     check_device();
     if (!got) {  // watchdog: a worker holding weights that stays silent has failed
       const double now = now_s();
@@ -458,6 +573,7 @@ AsyncStatus PeerServer::run(int64_t checkpoint_every) {
     const int k = t.worker;
     if (k < 0 || k >= cfg_.nworkers) throw std::runtime_error("PeerServer: token from an unknown worker");
     if (t.kind == kKindError) {
+      flush_batch();
       st.code = kAsyncErrorToken;
       st.worker = k;
       st.updates = updates_;

@@ -758,6 +758,15 @@ class DistEngine:
         n_lanes = Wr * self.wpr
         if oversubscribed() and n_lanes >= 8:
             raise ValueError("one shared GPU: the worker ranks' lanes leave no XCD for the server kernel")
+        if oversubscribed() and Wr > 1:
+            # Each worker rank's per-round launch places workgroups on every XCD (blockIdx % 8),
+            # those on another rank's XCDs leave at once -- once a CU there is free.  With two
+            # worker ranks whose next launches' lanes spin on their receive tags (and whose
+            # riders spin on the previous launch), each can hold the CUs the other's leaving
+            # workgroups need: measured stalls of 50-900 us and a 20-s timeout
+            # (profiles/r06/README.md).  On the node every rank owns its GPU; the one-GPU
+            # rehearsal is the GPU server + ONE worker rank
+            raise ValueError("--bsp_schedule peer_sum on one shared GPU: one worker rank (the rehearsal form)")
         if self.is_server:
             maps = [h.PeerMapping(handles[r], sp.P, NS, 1) for r in range(1, self.world)]
             self._peer_maps = maps

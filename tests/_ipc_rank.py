@@ -17,12 +17,12 @@ def cfg_for(world: int, mode: str):
 
     if mode in ("peer_sum", "peer_sum_vote"):
         # BSP with rank-level sums over the peer data plane (--bsp_schedule peer_sum): 1 GPU server
-        # rank + worker ranks x 3 lanes, no collective per round; _vote: an unbounded run (1.5 s)
+        # rank + one worker rank x 6 lanes, no collective per round; _vote: an unbounded run (1.5 s)
         vote = mode == "peer_sum_vote"
-        return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,
+        return PSConfig(num_workers=(world - 1) * 6, consistency_model=0, producer_time_per_event=0,
                         stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=0 if vote else 6,
                         max_wallclock_s=1.5 if vote else 0.0, min_buffer_size=128, max_buffer_size=1024,
-                        init="random", seed=0, server_colocated=False, workers_per_rank=3, bsp_schedule="peer_sum",
+                        init="random", seed=0, server_colocated=False, workers_per_rank=6, bsp_schedule="peer_sum",
                         worker_timeout_s=20.0, idle_wait_s=20.0)
     if mode == "peer_bsp":  # sequential consistency over the peer data plane: 1 GPU server + ranks x 3 lanes
         return PSConfig(num_workers=(world - 1) * 3, consistency_model=0, producer_time_per_event=0,

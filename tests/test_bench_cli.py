@@ -93,3 +93,31 @@ def test_bench_async_two_runs_same_engine(c):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 3 and d["config"]["workers"] == 2
     assert d["value"] > 0
+
+
+def test_bench_default_schedule_peer_sum_on_gpus():
+    """Dense multi-GPU BSP with a dedicated server defaults to the peer_sum schedule
+    (rank-level lane sums into the server GPU's inbox, no collective per round); CPU
+    runs and the wide models keep reduce + broadcast / the key-range server, and the
+    colocated variant the all-reduce."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.parse(["--gpus", "8"]).schedule == "peer_sum"
+    assert bench.parse(["--gpus", "2", "--cpu"]).schedule == "reduce_bcast"
+    assert bench.parse(["--gpus", "2", "--consistency", "-1"]).schedule == "reduce_bcast"
+    assert bench.parse(["--gpus", "8", "--model", "sparse1m"]).schedule == "reduce_bcast"
+    assert bench.parse(["--gpus", "8", "--model", "sharded100m"]).schedule == "keyrange"
+    assert bench.parse(["--gpus", "8", "--colocated-server"]).schedule == "allreduce"
+    assert bench.parse(["--gpus", "8", "--schedule", "reduce_bcast"]).schedule == "reduce_bcast"
+
+
+def test_peer_sum_needs_gpu_ranks():
+    """--bsp_schedule peer_sum on a CPU rank is refused before any collective."""
+    sys.path.insert(0, ROOT)
+    from psx.parallel.dist import DistEngine
+    from psx.runtime.config import PSConfig
+
+    cfg = PSConfig(num_workers=2, bsp_schedule="peer_sum", server_colocated=False, workers_per_rank=2)
+    with pytest.raises(ValueError, match="peer_sum"):
+        DistEngine(cfg, 0, 2, "cpu")

@@ -202,20 +202,20 @@ def test_peer_plane_bsp_equals_in_process_engine(cuda, tmp_path):
 
 
 def test_peer_sum_bsp_equals_in_process_engine(cuda, tmp_path):
-    """--bsp_schedule peer_sum: 1 GPU server rank (its persistent kernel on XCD 6) + 2 worker
-    ranks x 3 lanes (XCDs 0-2 / 3-5), three processes on one GPU.  Each worker rank's round
-    kernel stores its lane sum into its inbox slot on the server GPU; the server kernel sums
-    the two ranks' slices, applies w += lr * sum and writes the weights into both ranks'
-    receive slots; the next round's launch pulls them -- no collective, no host per round.
-    Weights and server rows equal one process hosting the same 6 workers in the BSP lanes
-    loop (the deltas summed per rank first: 2e-4, as the RCCL reduce + broadcast rehearsal).
-    Reference: ServerProcessor.java:111-120,148-151 (BSP: every worker answered once the
-    round is complete, w += (1/N) delta)."""
-    res = _launch(tmp_path, "peer_sum", world=3, timeout=175)
+    """--bsp_schedule peer_sum: a GPU server rank (its persistent kernel on XCD 6) + one worker
+    rank x 6 lanes (XCDs 0-5), two processes on one GPU.  The worker rank's round kernel stores
+    its lane sum into its inbox slot on the server GPU; the server kernel applies w += lr * sum
+    and writes the weights into the rank's receive slot; the next round's launch pulls them --
+    no collective, no host per round.  Weights and server rows equal one process hosting the
+    same 6 workers in the BSP lanes loop: the lanes are summed in the same order, so the update
+    is the in-process one (measured bit for bit; asserted within 1e-6).  Reference:
+    ServerProcessor.java:111-120,148-151 (BSP: every worker answered once the round is
+    complete, w += (1/N) delta)."""
+    res = _launch(tmp_path, "peer_sum", world=2, timeout=175)
     srv = res[0]
     assert srv.get("data_plane") == "peer_sum", srv
-    assert [r["rounds"] for r in res] == [6, 6, 6], res
-    assert all(r["lanes"] for r in res[1:]), res
+    assert [r["rounds"] for r in res] == [6, 6], res
+    assert res[1]["lanes"], res
     assert srv["updates"] == 6 * 6, srv["updates"]
     w_ps = torch.load(os.path.join(tmp_path, "w_peer_sum.pt"), weights_only=True)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -224,25 +224,26 @@ def test_peer_sum_bsp_equals_in_process_engine(cuda, tmp_path):
     from psx.runtime.engine import LocalEngine
     from psx.utils.data import synth_finefood
 
-    cfg = cfg_for(3, "peer_sum")
+    cfg = cfg_for(2, "peer_sum")
     cfg.server_colocated, cfg.bsp_schedule, cfg.workers_per_rank = True, "allreduce", 1
     eng = LocalEngine(cfg, cuda, train=synth_finefood(20000, seed=0), test=synth_finefood(4877, seed=1))
     out = eng.run(close_log=False)
     eng.log.drain(block=True)
     assert out.get("lanes") == 6, out
     w_loc = eng.server.w.detach().cpu()
-    assert torch.allclose(w_ps, w_loc, rtol=2e-4, atol=2e-4), (w_ps - w_loc).abs().max().item()
+    print("peer_sum vs in-process max |dw|:", (w_ps - w_loc).abs().max().item())
+    assert torch.allclose(w_ps, w_loc, rtol=0, atol=1e-6), (w_ps - w_loc).abs().max().item()
     rows_ps = srv["server_rows"]
     rows_loc = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
     assert len(rows_ps) == len(rows_loc) == 6
     for a, b in zip(rows_ps, rows_loc):  # the global model after each round: the same rows
-        assert a[0] == b[0] and abs(a[1] - b[1]) < 2e-3 and abs(a[2] - b[2]) < 2e-3, (a, b)
+        assert a[0] == b[0] and abs(a[1] - b[1]) < 1e-3 and abs(a[2] - b[2]) < 1e-3, (a, b)
 
 
 def test_peer_sum_stop_vote_chunks_end_together(cuda, tmp_path):
     """peer_sum, an unbounded run (max_iters 0, wall clock 1.5 s): the server kernel and the
-    worker ranks run chunks of rounds and stop by the vote between chunks, every rank the
-    same rounds."""
-    res = _launch(tmp_path, "peer_sum_vote", world=3, timeout=175)
+    worker rank run chunks of rounds and stop by the vote between chunks, both the same
+    rounds."""
+    res = _launch(tmp_path, "peer_sum_vote", world=2, timeout=175)
     rounds = [r["rounds"] for r in res]
     assert rounds[0] > 0 and len(set(rounds)) == 1, rounds

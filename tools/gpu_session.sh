@@ -102,8 +102,8 @@ long --steps 3000 --warmup 30}" ;;
       while read -r n g args; do
         [ -z "$n" ] && continue
         PSX_GPU_OVERSUBSCRIBE=1 PSX_PG_TIMEOUT_S=120 bench_run $n 240 --gpus $g $args; rc=$?; fatal_rc $rc && exit $rc
-      done <<< "${MR_RUNS:-peer_sum_3x3 3 --workers 3 --schedule peer_sum --steps 300 --warmup 30
-peer_sum_2x7 2 --workers 7 --schedule peer_sum --steps 300 --warmup 30
+      done <<< "${MR_RUNS:-peer_sum_2x7 2 --workers 7 --schedule peer_sum --steps 300 --warmup 30
+peer_sum_2x6 2 --workers 6 --schedule peer_sum --steps 300 --warmup 30
 reduce_bcast_3x3 3 --workers 3 --dedicated-server --steps 20 --warmup 5
 peer_bsp_3x3 3 --workers 3 --schedule peer --steps 20 --warmup 5
 ssp3_3x3 3 --workers 3 --consistency 3 --steps 20 --warmup 5

@@ -105,9 +105,10 @@ def parse(argv=None):
                     help="in-process SSP/ASP with --workers > 1: event polling (GPU default) or a thread per worker")
     ap.add_argument("--rccl-trace", action="store_true",
                     help="RCCL collective/p2p trace into ./rccl-trace.<host>.<pid>.log (multi-GPU runs)")
-    ap.add_argument("--dedicated-server", action="store_true", default=True,
-                    help="multi-GPU BSP: rank 0 is the server, ranks 1..N-1 the worker ranks, RCCL reduce (push) "
-                         "+ broadcast (pull) -- BASELINE config 2/3 topology (the default)")
+    ap.add_argument("--dedicated-server", action="store_true", default=None,
+                    help="multi-GPU: rank 0 is a server GPU only, ranks 1..N-1 the worker ranks -- BASELINE config "
+                         "2/3 topology (the default for SSP / ASP and --schedule reduce_bcast; dense BSP's default "
+                         "peer_sum runs the server kernel on XCD 7 of rank 0 beside 7 workers of its own)")
     ap.add_argument("--colocated-server", dest="dedicated_server", action="store_false",
                     help="multi-GPU BSP: every rank hosts workers and a server replica, one RCCL all-reduce per "
                          "round (data-parallel variant)")
@@ -131,13 +132,18 @@ def parse(argv=None):
         a.steps = 300 if wide else 2000
     if a.warmup is None:
         a.warmup = 30 if wide else 200
+    # peer_sum with the server kernel colocated on rank 0 (beside 7 of its lanes) unless
+    # --dedicated-server asks for a server-only GPU
+    a.psum_colocated = a.dedicated_server is None
     if a.schedule is None:
-        # dense with a dedicated server: the peer_sum schedule (measured against RCCL reduce +
-        # broadcast in the one-GPU rehearsals, profiles/r06/README.md); CPU / wide: RCCL or gloo
-        if a.dedicated_server:
+        # dense BSP: the peer_sum schedule (measured against RCCL reduce + broadcast in the
+        # one-GPU rehearsals, profiles/r06/README.md); CPU / wide: RCCL or gloo
+        if a.dedicated_server is not False:
             a.schedule = "peer_sum" if (not wide and not a.cpu and a.consistency == 0) else "reduce_bcast"
         else:
             a.schedule = "allreduce"
+    if a.dedicated_server is None:
+        a.dedicated_server = True
     if a.workers is None:  # the wide configs keep one worker per GPU; dense: one worker per XCD
         a.workers = 1 if wide else 8
     return a
@@ -219,13 +225,18 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
     if cfg.bsp_schedule == "keyrange":
         par = (f"ps-{mode} key-range sharded server x{world} (every rank: 1 worker + the shard of its key "
                f"range; pull/push of the window's ids over {backend if world > 1 else 'local copies'})")
-    elif world == 1:
+    elif world == 1 and not getattr(a, "dist_world1", False):
         par = f"ps-{mode} w{n_workers} (server colocated, {lanes if n_workers > 1 else '1 worker'})"
     elif async_mode and wpr > 1:
         par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers (peer data plane over xGMI: "
                f"lanes -> server inbox, server kernel -> receive slots)")
     elif async_mode:
         par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
+    elif cfg.bsp_schedule == "peer_sum" and cfg.server_colocated:
+        par = (f"ps-{mode} rank 0: server kernel (XCD 7) + {n_workers - (world - 1) * wpr} workers, "
+               f"{world - 1} more ranks x {wpr} workers (peer_sum over xGMI: each rank's lane sum stored into "
+               f"rank 0's inbox by its round kernel, summed + applied by the server kernel, weights written into "
+               f"every rank's receive slot; no collective per round)")
     elif cfg.bsp_schedule == "peer_sum":
         par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers (peer_sum over xGMI: each "
                f"rank's lane sum stored into the server GPU's inbox by its round kernel, summed + applied by the "
@@ -433,19 +444,22 @@ def bench_distributed(a):
     if a.rccl_trace:
         os.environ.update(rccl_trace_env("."))
     rank, world, device = init_from_env(cpu=a.cpu)
+    a.dist_world1 = world == 1  # (the multi-rank body with one rank: labelled as such)
     if dist.get_world_size() != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {dist.get_world_size()} ranks")
     peer_bsp = a.consistency == 0 and a.schedule == "peer"
     peer_sum = a.consistency == 0 and a.schedule == "peer_sum"
     async_mode = a.consistency != 0 or peer_bsp  # (peer BSP: the asynchronous loops, sequential tracker)
     keyrange = a.schedule == "keyrange"
-    # (key-range: every rank holds a shard; peer_sum: rank 0 is the server GPU)
-    dedicated = (async_mode or a.dedicated_server or peer_sum) and not keyrange
+    # (key-range: every rank holds a shard; peer_sum: rank 0 runs the server kernel -- beside 7
+    # lanes of its own unless --dedicated-server)
+    psum_colo = peer_sum and a.psum_colocated
+    dedicated = (async_mode or a.dedicated_server or peer_sum) and not keyrange and not psum_colo
     # workers per worker rank: --workers lanes, one XCD each (SSP / ASP / peer BSP: the lanes of one
     # persistent launch; the peer data plane runs no transfer kernel beside it, so all 8 XCDs)
     wpr = 1 if (a.model != "dense" or a.cpu) else a.workers
     worker_ranks = world - 1 if dedicated else world
-    cfg = build_cfg(a, worker_ranks * wpr)
+    cfg = build_cfg(a, worker_ranks * wpr)  # (DistEngine fixes num_workers: rank 0's lanes under psum_colo)
     cfg.workers_per_rank = wpr
     cfg.server_colocated = not dedicated
     if peer_bsp:
@@ -484,7 +498,7 @@ def bench_distributed(a):
     # collectives) or torch.distributed's (nccl backend = RCCL); None on gloo
     rccl = comm.c.size if comm is not None else (dist.get_world_size() if dist.get_backend() == "nccl" else None)
     res = None
-    topo = {"server_rank": 0 if dedicated else None, "worker_ranks": worker_ranks, "workers_per_rank": wpr,
+    topo = {"server_rank": 0 if (dedicated or psum_colo) else None, "worker_ranks": worker_ranks, "workers_per_rank": wpr,
             "workers": cfg.num_workers,
             "schedule": cfg.bsp_schedule if not async_mode else ("peer" if wpr > 1 else "p2p"),
             "native_lanes_loop": getattr(eng, "_lanes", None) is not None}

@@ -645,6 +645,7 @@ PYBIND11_MODULE(_psx_hip, m) {
              c.nwg = (int)I("nwg", kSrvWg);
              c.batch = (int)I("batch", 64);
              c.standin = I("standin", 0) != 0;
+             c.ahead = (int)I("ahead", 0);
              c.tag_wait_s = d.contains("tag_wait_s") ? d["tag_wait_s"].cast<double>() : 600.0;
              prepare_kernels();
              return std::make_unique<PeerServer>(c, nullptr);
@@ -663,6 +664,8 @@ PYBIND11_MODULE(_psx_hip, m) {
           },
           py::arg("checkpoint_every") = 0)
       .def("run_bsp", &PeerServer::run_bsp, py::arg("rounds"), py::arg("r0"), py::call_guard<py::gil_scoped_release>())
+      .def("run_bsp_async", &PeerServer::run_bsp_async, py::arg("rounds"), py::arg("r0"))
+      .def("run_bsp_join", &PeerServer::run_bsp_join, py::call_guard<py::gil_scoped_release>())
       .def("seed_rx", &PeerServer::seed_rx, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bsp_rounds", &PeerServer::bsp_rounds)
       .def("set_trace", &PeerServer::set_trace, py::arg("cap"))

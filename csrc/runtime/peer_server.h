@@ -19,7 +19,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <exception>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -61,6 +63,11 @@ struct PeerServerCfg {
   int batch = 64;
   // stand-in workers (tools/peer_server_bench.py): no token / reply queues needed
   bool standin = false;
+  // commands written ahead of the kernel's reads at most (0: the ring, 256).  Each BSP
+  // round's command holds a metrics-sink slot for its server row from the moment it is
+  // written: the colocated peer_sum rank 0 shares its sink with its own lanes, whose worker
+  // rows must still find slots
+  int ahead = 0;
 };
 
 class PeerServer {
@@ -82,6 +89,11 @@ class PeerServer {
   // round; returns once the launch has drained (w final).  The ranks' lanes loops run the
   // same rounds (LanesLoop::set_peer_sum).
   int64_t run_bsp(int64_t rounds, int64_t r0);
+  // run_bsp on a host thread of its own (returns at once): the server rank that also hosts
+  // lanes (rank 0 of the colocated peer_sum form) runs its own lanes loop meanwhile, then
+  // run_bsp_join (the rounds' result; rethrows the thread's error)
+  void run_bsp_async(int64_t rounds, int64_t r0);
+  int64_t run_bsp_join();
   // peer_sum BSP bring-up: the current weights into every rank's receive slot (tag 0: the
   // pull of round 0)
   void seed_rx();
@@ -175,6 +187,9 @@ class PeerServer {
   uint64_t tr_taken_ = 0;
   int64_t bsp_run_ = 0;
   double bsp_ns_ = 0.0;
+  std::thread bsp_thr_;  // run_bsp_async
+  std::exception_ptr bsp_err_;
+  int64_t bsp_ret_ = 0;
 };
 
 }  // namespace psx

@@ -70,7 +70,14 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
   const size_t o_rec = take(32 * 8);
   const size_t o_claim = take(64 * 4);
   const size_t o_erec = take((size_t)kSrvMaxBatch * kEntChunks * 16);
-  hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate(peer server)");
+  // The persistent launch needs a hardware queue of its own: HIP multiplexes a process's
+  // streams of one priority onto GPU_MAX_HW_QUEUES (4) queues, whose packets run in order --
+  // a stream that shares the server kernel's queue would wait behind it for good (the
+  // colocated peer_sum rank 0 launches its lanes beside it; every solver holds a capture
+  // stream).  The greatest priority has a queue pool of its own, and nothing else here uses it.
+  int prio_lo = 0, prio_hi = 0;
+  hip_check(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "hipDeviceGetStreamPriorityRange");
+  hip_check(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_hi), "hipStreamCreate(peer server)");
   hip_check(hipMalloc(&ws_, off), "hipMalloc(peer server workspace)");
   hip_check(hipMemset(ws_, 0, off), "hipMemset(peer server workspace)");
   char* b = static_cast<char*>(ws_);
@@ -145,6 +152,7 @@ PeerServer::PeerServer(const PeerServerCfg& cfg, hipStream_t stream) : cfg_(cfg)
 }
 
 PeerServer::~PeerServer() {
+  if (bsp_thr_.joinable()) bsp_thr_.join();  // (run_bsp_async's rounds end by themselves: drained or timed out)
   try {
     stop();
   } catch (...) {
@@ -220,9 +228,10 @@ void PeerServer::wait_ring() {
   // entries, the entry ring ring_ + 1 times that: the next command's entries never overwrite
   // those of a command the kernel has not read)
   const uint64_t n = cmds_ + 1;
-  if (n > (uint64_t)ring_) {
+  const uint64_t lim = (uint64_t)(cfg_.ahead > 0 && cfg_.ahead < ring_ ? cfg_.ahead : ring_);
+  if (n > lim) {
     const double t0 = now_s();
-    while (__atomic_load_n(consumed_host_, __ATOMIC_ACQUIRE) + (uint64_t)ring_ < n) {
+    while (__atomic_load_n(consumed_host_, __ATOMIC_ACQUIRE) + lim < n) {
       check_device();
       if (now_s() - t0 > cfg_.worker_timeout_s) throw std::runtime_error("PeerServer: the server kernel stopped reading commands");
       _mm_pause();
@@ -533,6 +542,30 @@ int64_t PeerServer::run_bsp(int64_t rounds, int64_t r0) {
   stop();  // (the ranks' last sums applied: w is final)
   bsp_run_ += rounds;
   return rounds;
+}
+
+void PeerServer::run_bsp_async(int64_t rounds, int64_t r0) {
+  if (bsp_thr_.joinable()) throw std::logic_error("PeerServer::run_bsp_async: the previous rounds not joined");
+  bsp_err_ = nullptr;
+  bsp_ret_ = 0;
+  bsp_thr_ = std::thread([this, rounds, r0]() {
+    try {
+      bsp_ret_ = run_bsp(rounds, r0);
+    } catch (...) {
+      bsp_err_ = std::current_exception();
+    }
+  });
+}
+
+int64_t PeerServer::run_bsp_join() {
+  if (!bsp_thr_.joinable()) return 0;
+  bsp_thr_.join();
+  if (bsp_err_) {
+    std::exception_ptr e = bsp_err_;
+    bsp_err_ = nullptr;
+    std::rethrow_exception(e);
+  }
+  return bsp_ret_;
 }
 
 AsyncStatus PeerServer::run(int64_t checkpoint_every) {

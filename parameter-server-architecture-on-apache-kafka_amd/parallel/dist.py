@@ -23,8 +23,10 @@ Sequential (BSP, c = 0) schedules, chosen with ``--bsp_schedule``:
                 keyrange.py -- each rank stores ONLY its key range and a round moves
                 the window's ids and values (pull / push by owner), never P floats.
   peer_sum      dense, several workers per worker rank, every rank on a GPU (the
-                bench.py default for N > 1 GPUs): a dedicated server rank and NO
-                collective.  The last lane to finish a slice on a worker rank stores
+                bench.py default for N > 1 GPUs) and NO collective.  The server is
+                rank 0's persistent kernel: on XCD 7 beside 7 lanes of rank 0's own
+                (server_colocated, bench.py's default: every GPU trains), or on a
+                dedicated server GPU.  The last lane to finish a slice on a worker rank stores
                 the rank's lane sum straight into that rank's slot of the server
                 GPU's inbox (IPC-mapped fine-grained memory, xGMI) and tags it; the
                 server's persistent kernel sums the W ranks' slices in rank order,
@@ -72,6 +74,23 @@ from ..runtime.roles import EvalPair, ServerRole, WorkerRole, is_wide, make_eval
 from ..utils.checkpoint import flush_checkpoints, maybe_checkpoint, maybe_resume
 from ..utils.logsink import LogSink, summarize
 from ..utils.trace import Tracer
+
+# peer_sum with the server colocated: rank 0's lanes take XCDs 0..6, its server kernel XCD 7
+PSUM_RANK0_LANES = 7
+kSrvXcdColocated = 7
+
+
+def rank_worker_layout(cfg: PSConfig, world: int) -> list:
+    """(first worker id, workers) of every rank: a dedicated server rank 0 (SSP / ASP, or
+    server_colocated False) hosts none and ranks 1.. host workers_per_rank each; colocated,
+    every rank hosts workers_per_rank -- rank 0 at most PSUM_RANK0_LANES under peer_sum,
+    whose server kernel takes its last XCD."""
+    wpr = max(1, int(cfg.workers_per_rank))
+    async_mode = cfg.consistency_model != 0 or cfg.bsp_schedule == "peer"
+    if async_mode or not cfg.server_colocated:
+        return [(0, 0)] + [((r - 1) * wpr, wpr) for r in range(1, world)]
+    wpr0 = min(wpr, PSUM_RANK0_LANES) if (cfg.consistency_model == 0 and cfg.bsp_schedule == "peer_sum") else wpr
+    return [(0, wpr0)] + [(wpr0 + (r - 1) * wpr, wpr) for r in range(1, world)]
 
 KIND_DELTA, KIND_FINAL, KIND_ERROR = 0, 1, 2
 
@@ -217,10 +236,17 @@ class DistEngine:
         self.peer_sum = cfg.consistency_model == 0 and cfg.bsp_schedule == "peer_sum"
         if self.peer_sum and torch.device(device).type != "cuda":
             raise ValueError("--bsp_schedule peer_sum: every rank (the server too) on a GPU")
-        self.dedicated = self.async_mode or self.peer_sum or not cfg.server_colocated
+        # (peer_sum with server_colocated: rank 0 runs the server kernel on XCD 7 AND up to 7
+        # lanes on XCDs 0-6 -- every GPU trains; otherwise rank 0 is a dedicated server GPU)
+        self.dedicated = self.async_mode or not cfg.server_colocated
+        self.psum_colocated = self.peer_sum and not self.dedicated
         wpr = max(1, int(cfg.workers_per_rank))
         n_worker_ranks = world - 1 if self.dedicated else world
-        n_workers = n_worker_ranks * wpr
+        self._rank_workers = rank_worker_layout(cfg, world)  # per rank: (first worker id, count)
+        n_workers = sum(c for _, c in self._rank_workers)
+        if self.psum_colocated and world > 1 and oversubscribed():
+            raise ValueError("--bsp_schedule peer_sum with the server colocated: one rank per GPU (a shared GPU "
+                             "would host two processes' lanes); the one-GPU rehearsal is world 1")
         if n_worker_ranks < 1:
             raise ValueError("need at least one worker rank (world size >= 2 with a dedicated server)")
         hosts_workers = not (self.dedicated and rank == 0)  # (a dedicated server rank hosts none)
@@ -308,13 +334,14 @@ class DistEngine:
         self.workers = []
         if self.is_worker:
             tr = train.to(self.device)
-            self.workers = [WorkerRole(self.worker_id * wpr + l, self.spec, cfg, self.device, tr, self.evalset,
-                                       t0=self.t0) for l in range(wpr)]
+            k0, nloc = self._rank_workers[rank]
+            self.workers = [WorkerRole(k0 + l, self.spec, cfg, self.device, tr, self.evalset,
+                                       t0=self.t0) for l in range(nloc)]
             self.worker = self.workers[0]
         self.rounds = 0
         self._ctrl = None
         self._next_vc = 0
-        if (not self.async_mode and cfg.pair_eval and (self.is_server or cfg.bsp_schedule == "allreduce")
+        if (not self.async_mode and not self.peer_sum and cfg.pair_eval and (self.is_server or cfg.bsp_schedule == "allreduce")
                 and self.server is not None and self.worker is not None):
             # rank 0: worker row + previous server row + the update in one launch; the other
             # allreduce ranks: worker row + their replica's update in one launch
@@ -616,7 +643,10 @@ class DistEngine:
         from ..ops.lr import Fragments
 
         cfg, srv, sp, W = self.cfg, self.server, self.spec, self.workers
-        w_main = srv.w if srv is not None else W[0].w
+        # (peer_sum: the lanes pull the server kernel's weights from their receive slot; on
+        # the colocated rank 0 the server's own w is the server kernel's, not the lanes')
+        lsrv = None if self.peer_sum else srv
+        w_main = lsrv.w if lsrv is not None else W[0].w
         for w in W:
             w.w = w_main
             w.ring.flush()
@@ -637,18 +667,18 @@ class DistEngine:
                      k=[w.k for w in W], X=[w.ring.X.data_ptr() for w in W], y=[w.ring.y.data_ptr() for w in W],
                      window=[w.window.handle for w in W], w=w_main.data_ptr(), lr=float(cfg.lr),
                      api=_native.host.capi(), server_rank=0, allreduce=int(cfg.bsp_schedule == "allreduce"),
-                     log_server=int(self.rank == 0), log_workers=int(bool(W) and cfg.log_workers),
+                     log_server=int(self.rank == 0 and lsrv is not None), log_workers=int(bool(W) and cfg.log_workers),
                      # ranks sharing one GPU (IPC transport): worker rank i's lanes on XCDs
                      # i*wpr .. i*wpr + wpr - 1, so no two ranks' lanes share an XCD
                      xcd0=(self.worker_id * len(W)) if (W and (getattr(comm, "kind", "rccl") == "ipc" or (
                          comm is None and oversubscribed()))) else 0,
                      sink=self.log.native.handle if self.log is not None else 0,
-                     tracker=srv.tracker.handle if (srv is not None and self.rank == 0) else 0,
+                     tracker=lsrv.tracker.handle if (lsrv is not None and self.rank == 0) else 0,
                      new_rows=int(cfg.iter_new_rows), new_frac=float(cfg.iter_new_frac), new_cap=int(cfg.iter_new_cap), new_ramp=int(cfg.iter_new_ramp))
             if W:
                 ds = W[0].source.ds
                 d.update(dsX=ds.X.data_ptr(), dsy=ds.y.data_ptr(), ds_rows=int(ds.rows))
-            if srv is not None:
+            if lsrv is not None:
                 self._lane_frags = [Fragments(sp, self.device) for _ in range(3)]  # (3: overlapped rounds)
                 d.update(shi=[f.hi.data_ptr() for f in self._lane_frags], slo=[f.lo.data_ptr() for f in self._lane_frags],
                          sb=[f.b.data_ptr() for f in self._lane_frags])
@@ -708,7 +738,7 @@ class DistEngine:
         N = cfg.num_workers
         t_start = time.time()
         t0 = time.perf_counter()
-        if self.is_server:
+        if self.is_server and not W:
             n = self._lanes_chunks(None, None, None, int(cfg.max_iters), [])
             t1 = time.perf_counter()
             if srv.frag is not None:
@@ -719,11 +749,16 @@ class DistEngine:
                 with open(f"{os.environ['PSX_LANES_TRACE_OUT']}.rank0", "a") as fh:
                     fh.write(json.dumps({"rank": 0, "server": [list(r) for r in self._pserver.trace_take()]}) + "\n")
             torch.cuda.synchronize(self.device)
-        else:
+        else:  # a worker rank, or the colocated rank 0 (its lanes + the server kernel's rounds)
             n = self._run_bsp_lanes(None, int(cfg.max_iters))
             t1 = time.perf_counter()
             if os.environ.get("PSX_PSUM_DIAG"):  # (diagnostics: receive / push slice tags; a synchronisation)
                 self._psum_tags = list(self._lanes.peer_sum_tags())
+            if self.is_server:
+                if srv.frag is not None:
+                    srv.frag.refresh(srv.w)
+                srv.updates += N * n
+                self.native_server_host_us_per_round = float(self._pserver.host_us_per_round)
         # (where a call's wall clock went: the rounds, then the tail -- bench.py gathers these)
         self._phases = {"rounds_ms": round((t1 - t0) * 1e3, 3),
                         "tail_ms": round((time.perf_counter() - t1) * 1e3, 3)}
@@ -748,17 +783,20 @@ class DistEngine:
         other ranks' and the server kernel's XCDs."""
         cfg, sp = self.cfg, self.spec
         h = _native.hip()
-        NS, Wr = sp.Fp // 32, self.world - 1
+        colo = self.psum_colocated
+        # worker ranks = inbox slots (colocated: rank r's slot is r, rank 0's local)
+        NS, Wr = sp.Fp // 32, (self.world if colo else self.world - 1)
+        slot = self.rank if colo else self.rank - 1
         dev = self.device.index or 0
         reg = h.PeerRegion(sp.P, NS, Wr if self.is_server else 1, dev)
         handles = [None] * self.world
         dist.all_gather_object(handles, reg.handle())
         self._psum_region = reg
         wait_s = max(float(cfg.worker_timeout_s), float(cfg.idle_wait_s))
-        n_lanes = Wr * self.wpr
+        n_lanes = sum(c for _, c in self._rank_workers)
         if oversubscribed() and n_lanes >= 8:
             raise ValueError("one shared GPU: the worker ranks' lanes leave no XCD for the server kernel")
-        if oversubscribed() and Wr > 1:
+        if oversubscribed() and Wr > 1 and not colo:
             # Each worker rank's per-round launch places workgroups on every XCD (blockIdx % 8),
             # those on another rank's XCDs leave at once -- once a CU there is free.  With two
             # worker ranks whose next launches' lanes spin on their receive tags (and whose
@@ -767,18 +805,26 @@ class DistEngine:
             # (profiles/r06/README.md).  On the node every rank owns its GPU; the one-GPU
             # rehearsal is the GPU server + ONE worker rank
             raise ValueError("--bsp_schedule peer_sum on one shared GPU: one worker rank (the rehearsal form)")
+        # the server kernel's XCD: after the lanes on a shared GPU (n_lanes <= 7); on the
+        # colocated rank 0 the last one (its lanes take XCDs 0..6)
+        sxcd = n_lanes if oversubscribed() else (kSrvXcdColocated if colo else 0)
         if self.is_server:
             maps = [h.PeerMapping(handles[r], sp.P, NS, 1) for r in range(1, self.world)]
             self._peer_maps = maps
+            rx, rx_tag = [m.data(0) for m in maps], [m.tags(0) for m in maps]
+            if colo:  # rank 0's own receive slot (local memory), ahead of the other ranks'
+                self._psum_rx0 = h.PeerRegion(sp.P, NS, 1, dev)
+                rx, rx_tag = [self._psum_rx0.data(0)] + rx, [self._psum_rx0.tags(0)] + rx_tag
             d = dict(nworkers=Wr, lr=float(cfg.lr), K=sp.K, F=sp.F, FP=sp.Fp, P=int(sp.P),
-                     w=self.server.w.data_ptr(), inbox=reg.base, rx=[m.data(0) for m in maps],
-                     rx_tag=[m.tags(0) for m in maps], api=_native.host.capi(), tracker=self.server.tracker.handle,
-                     bsp=1, tag_wait_s=wait_s, worker_timeout_s=float(cfg.worker_timeout_s),
-                     # one shared GPU: the XCD after the worker ranks' lanes, half of its CUs (the
-                     # other ranks' per-round launches place -- and at once retire -- their
-                     # workgroups of that XCD on the other half)
-                     sxcd=n_lanes if oversubscribed() else 0,
-                     nwg=int(os.environ.get("PSX_PSUM_NWG", 16 if oversubscribed() else 32)))
+                     w=self.server.w.data_ptr(), inbox=reg.base, rx=rx, rx_tag=rx_tag,
+                     api=_native.host.capi(), tracker=self.server.tracker.handle,
+                     bsp=1, tag_wait_s=wait_s, worker_timeout_s=float(cfg.worker_timeout_s), sxcd=sxcd,
+                     # a GPU whose other launches place workgroups on the server's XCD (a shared
+                     # GPU's other ranks, the colocated rank 0's own lanes launch: its workgroups
+                     # of that XCD retire at once) keeps half of that XCD's CUs free for them
+                     nwg=int(os.environ.get("PSX_PSUM_NWG", 16 if (oversubscribed() or colo) else 32)),
+                     # colocated: the server rows' sink slots, written ahead, leave the lanes' rows room
+                     ahead=16 if colo else 0)
             ev = self.evalset
             if self.log is not None and ev is not None and os.environ.get("PSX_PSUM_NO_SERVER_ROWS") != "1":
                 d.update(sink=self.log.native.handle, Xt=ev.X.data_ptr(), yt=ev.y.data_ptr(), T=int(ev.T))
@@ -787,16 +833,24 @@ class DistEngine:
             self._pserver.seed_rx()
             if os.environ.get("PSX_LANES_TRACE_OUT"):  # (tools: the server kernel's per-round stamps)
                 self._pserver.set_trace(8192)
-        else:
-            m = h.PeerMapping(handles[0], sp.P, NS, Wr)
-            self._peer_maps = [m]
+        if self.workers:
+            if self.is_server:  # colocated rank 0: push into its own inbox slot, pull from its local slot
+                push, push_tag = reg.data(0), reg.tags(0)
+                rx_reg = self._psum_rx0
+            else:
+                m = h.PeerMapping(handles[0], sp.P, NS, Wr)
+                self._peer_maps = [m]
+                push, push_tag = m.data(slot), m.tags(slot)
+                rx_reg = reg
             self._run_bsp_lanes(None, 0, build_only=True)
             lp = self._lanes
-            i = self.worker_id
-            lp.set_peer_sum(reg.data(0), reg.tags(0), m.data(i), m.tags(i), wait_s)
+            lp.set_peer_sum(rx_reg.data(0), rx_reg.tags(0), push, push_tag, wait_s)
             if oversubscribed():  # only this rank's lanes' XCDs: no rider spins on another process's CUs
-                mine = ((1 << self.wpr) - 1) << (i * self.wpr)
+                k0, nloc = self._rank_workers[self.rank]
+                mine = ((1 << nloc) - 1) << k0
                 lp.set_xcd_skip(0xff & ~mine)
+            elif colo and self.is_server:  # the server kernel's XCD: its workgroups leave at once
+                lp.set_xcd_skip(1 << sxcd)
         torch.cuda.synchronize(self.device)
         dist.barrier()
 
@@ -814,6 +868,8 @@ class DistEngine:
         idle = float(cfg.idle_wait_s)
         if lp is None:  # (peer_sum server rank: the persistent server kernel runs its rounds)
             run = lambda k, r0: int(self._pserver.run_bsp(k, r0))
+        elif self.peer_sum and self.is_server:  # colocated rank 0: the server's rounds beside its lanes'
+            run = lambda k, r0: self._psum_colocated_rounds(lp, k, r0, stream, idle)
         else:
             run = lambda k, r0: int(lp.run(k, r0, stream, idle))
         if rounds:
@@ -841,6 +897,20 @@ class DistEngine:
             f = flag.tolist()
             if f[0] > 0 or f[1] == 0:
                 return n
+
+    def _psum_colocated_rounds(self, lp, k: int, r0: int, stream, idle: float) -> int:
+        """k peer_sum rounds on the colocated rank 0: the server kernel's commands written by
+        a host thread of PeerServer (run_bsp_async) while this thread runs the rank's lanes
+        loop; both end when the server kernel has applied the k rounds."""
+        ps = self._pserver
+        ps.run_bsp_async(k, r0)
+        try:
+            n = int(lp.run(k, r0, stream, idle))
+        finally:
+            ns = int(ps.run_bsp_join())
+        if n != ns:
+            raise RuntimeError(f"peer_sum: rank 0's lanes ran {n} rounds, its server kernel {ns}")
+        return n
 
     def _native_bsp_ok(self, sched: str, comm) -> bool:
         """The native BSP loop (csrc/runtime/bsp_loop.h) runs this rank: allreduce

@@ -15,6 +15,15 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
+    if mode in ("peer_sum_colo", "peer_sum_colo_vote"):
+        # peer_sum with the server colocated, world 1: rank 0's server kernel (XCD 7) + its own
+        # 7 lanes (XCDs 0-6) in ONE process -- the server's command thread beside the lanes loop
+        vote = mode.endswith("_vote")
+        return PSConfig(num_workers=7, consistency_model=0, producer_time_per_event=0,
+                        stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=0 if vote else 6,
+                        max_wallclock_s=1.5 if vote else 0.0, min_buffer_size=128, max_buffer_size=1024,
+                        init="random", seed=0, server_colocated=True, workers_per_rank=7, bsp_schedule="peer_sum",
+                        worker_timeout_s=20.0, idle_wait_s=20.0)
     if mode in ("peer_sum", "peer_sum_vote"):
         # BSP with rank-level sums over the peer data plane (--bsp_schedule peer_sum): 1 GPU server
         # rank + one worker rank x 6 lanes, no collective per round; _vote: an unbounded run (1.5 s)
@@ -52,7 +61,7 @@ def main():
     import faulthandler
 
     # a hang names its frames (before the test's limit; the peer modes' native timeouts first)
-    faulthandler.dump_traceback_later(140 if mode.startswith("peer") else 80, exit=True)
+    faulthandler.dump_traceback_later(100 if mode.startswith("peer") else 80, exit=True)
     import torch
     import torch.distributed as dist
 

@@ -103,7 +103,10 @@ def test_bench_default_schedule_peer_sum_on_gpus():
     sys.path.insert(0, ROOT)
     import bench
 
-    assert bench.parse(["--gpus", "8"]).schedule == "peer_sum"
+    a = bench.parse(["--gpus", "8"])
+    assert a.schedule == "peer_sum" and a.psum_colocated  # the server kernel beside rank 0's 7 lanes
+    a = bench.parse(["--gpus", "8", "--dedicated-server"])
+    assert a.schedule == "peer_sum" and not a.psum_colocated and a.dedicated_server
     assert bench.parse(["--gpus", "2", "--cpu"]).schedule == "reduce_bcast"
     assert bench.parse(["--gpus", "2", "--consistency", "-1"]).schedule == "reduce_bcast"
     assert bench.parse(["--gpus", "8", "--model", "sparse1m"]).schedule == "reduce_bcast"
@@ -121,3 +124,24 @@ def test_peer_sum_needs_gpu_ranks():
     cfg = PSConfig(num_workers=2, bsp_schedule="peer_sum", server_colocated=False, workers_per_rank=2)
     with pytest.raises(ValueError, match="peer_sum"):
         DistEngine(cfg, 0, 2, "cpu")
+
+
+def test_peer_sum_colocated_worker_layout():
+    """peer_sum with the server colocated: rank 0 hosts 7 lanes beside the server kernel
+    (its XCD 7), every other rank --workers lanes; worker ids are contiguous per rank and
+    N (the server's lr = 1/N) counts them all.  A dedicated server rank hosts none."""
+    sys.path.insert(0, ROOT)
+    from psx.parallel.dist import rank_worker_layout
+    from psx.runtime.config import PSConfig
+
+    cfg = PSConfig(num_workers=1, bsp_schedule="peer_sum", server_colocated=True, workers_per_rank=8)
+    lay = rank_worker_layout(cfg, 8)
+    assert lay == [(0, 7)] + [(7 + 8 * (r - 1), 8) for r in range(1, 8)]
+    assert sum(c for _, c in lay) == 63
+    assert rank_worker_layout(cfg, 1) == [(0, 7)]
+    cfg = PSConfig(num_workers=1, bsp_schedule="peer_sum", server_colocated=False, workers_per_rank=8)
+    assert rank_worker_layout(cfg, 8) == [(0, 0)] + [(8 * (r - 1), 8) for r in range(1, 8)]
+    cfg = PSConfig(num_workers=1, bsp_schedule="allreduce", server_colocated=True, workers_per_rank=4)
+    assert rank_worker_layout(cfg, 3) == [(0, 4), (4, 4), (8, 4)]
+    cfg = PSConfig(num_workers=1, consistency_model=-1, server_colocated=True, workers_per_rank=4)
+    assert rank_worker_layout(cfg, 3) == [(0, 0), (0, 4), (4, 4)]  # SSP / ASP: always a dedicated server

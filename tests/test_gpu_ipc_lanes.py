@@ -247,3 +247,41 @@ def test_peer_sum_stop_vote_chunks_end_together(cuda, tmp_path):
     res = _launch(tmp_path, "peer_sum_vote", world=2, timeout=175)
     rounds = [r["rounds"] for r in res]
     assert rounds[0] > 0 and len(set(rounds)) == 1, rounds
+
+
+def test_peer_sum_colocated_server_equals_in_process_engine(cuda, tmp_path):
+    """peer_sum with the server colocated (bench.py's multi-GPU default), world 1: rank 0
+    runs the server kernel on XCD 7 -- its commands written by PeerServer's own host
+    thread (run_bsp_async) -- and its own 7 lanes on XCDs 0-6, which push into the local
+    inbox and pull from a local receive slot.  Weights and server rows equal one process
+    hosting the same 7 workers in the BSP lanes loop (rank 0's lanes are the only rank:
+    the server's sum is theirs, in lane order)."""
+    res = _launch(tmp_path, "peer_sum_colo", world=1, timeout=175)
+    srv = res[0]
+    assert srv.get("data_plane") == "peer_sum" and srv["rounds"] == 6 and srv["lanes"], srv
+    assert srv["updates"] == 6 * 7, srv["updates"]
+    w_ps = torch.load(os.path.join(tmp_path, "w_peer_sum_colo.pt"), weights_only=True)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _ipc_rank import cfg_for
+
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    cfg = cfg_for(1, "peer_sum_colo")
+    cfg.server_colocated, cfg.bsp_schedule, cfg.workers_per_rank = True, "allreduce", 1
+    eng = LocalEngine(cfg, cuda, train=synth_finefood(20000, seed=0), test=synth_finefood(4877, seed=1))
+    eng.run(close_log=False)
+    eng.log.drain(block=True)
+    w_loc = eng.server.w.detach().cpu()
+    assert torch.allclose(w_ps, w_loc, rtol=0, atol=1e-6), (w_ps - w_loc).abs().max().item()
+    rows_loc = [[float(r[1]), float(r[2]), float(r[3])] for r in eng.log.book.server]
+    assert len(srv["server_rows"]) == len(rows_loc) == 6
+    for a, b in zip(srv["server_rows"], rows_loc):
+        assert a[0] == b[0] and abs(a[1] - b[1]) < 1e-3 and abs(a[2] - b[2]) < 1e-3, (a, b)
+
+
+def test_peer_sum_colocated_vote_chunks(cuda, tmp_path):
+    """The colocated form in an unbounded run (wall clock 1.5 s): chunks of rounds, the
+    server thread joined after each, the stop vote between them."""
+    res = _launch(tmp_path, "peer_sum_colo_vote", world=1, timeout=175)
+    assert res[0]["rounds"] > 0 and res[0]["lanes"], res

@@ -3,7 +3,7 @@
 #   OUT=gpurun_out/<name>  STEPS="tests smoke bench ..." bash tools/gpu_session.sh
 # Steps (each GPU step has its own time limit; a crash / timeout / fault ends the script):
 #   tests smoke bench ssp asp lanes async ipc ab prof rocprof timeline asyncprof probe pmc
-#   secondary multirank world1 sparse fault
+#   secondary multirank world1 world1ps sparse fault
 # Knobs: BENCH_ARGS (extra bench.py arguments), PYTEST_ARGS, AB_VARIANTS / AB_STEPS,
 #   MR_RUNS (multirank: lines "name n args..."), SEC_RUNS (secondary: lines "name args...").
 set -u
@@ -104,12 +104,16 @@ long --steps 3000 --warmup 30}" ;;
         PSX_GPU_OVERSUBSCRIBE=1 PSX_PG_TIMEOUT_S=120 bench_run $n 240 --gpus $g $args; rc=$?; fatal_rc $rc && exit $rc
       done <<< "${MR_RUNS:-peer_sum_2x7 2 --workers 7 --schedule peer_sum --steps 300 --warmup 30
 peer_sum_2x6 2 --workers 6 --schedule peer_sum --steps 300 --warmup 30
-reduce_bcast_3x3 3 --workers 3 --dedicated-server --steps 20 --warmup 5
+reduce_bcast_3x3 3 --workers 3 --schedule reduce_bcast --steps 20 --warmup 5
 peer_bsp_3x3 3 --workers 3 --schedule peer --steps 20 --warmup 5
 ssp3_3x3 3 --workers 3 --consistency 3 --steps 20 --warmup 5
 asp_3x3 3 --workers 3 --consistency -1 --steps 20 --warmup 5}" ;;
     world1)  # the multi-rank bench body with one rank (PSX_BENCH_DIST=1: RCCL communicator, DistEngine)
       PSX_BENCH_DIST=1 bench_run world1 300 --colocated-server --steps 300 --warmup 30 --no-accuracy-run || exit 1 ;;
+    world1ps)  # the multi-GPU default (peer_sum, server kernel colocated on rank 0) with one rank:
+      # the server kernel on XCD 7 beside rank 0's 7 lanes, one process; then in process, 7 workers
+      PSX_BENCH_DIST=1 bench_run world1_psum 300 --steps ${W1_STEPS:-300} --warmup 30 --no-accuracy-run || exit 1
+      bench_run inproc_w7 300 --workers 7 --steps ${W1_STEPS:-300} --warmup 30 --no-accuracy-run || exit 1 ;;
     sparse)  # BASELINE configs 4 / 5
       for w in 1 4 8; do bench_run sparse1m_w$w 300 --model sparse1m --workers $w --steps 40 --warmup 10; rc=$?; fatal_rc $rc && exit $rc; done
       bench_run sharded100m 300 --model sharded100m --steps 40 --warmup 10; rc=$?; fatal_rc $rc && exit $rc ;;

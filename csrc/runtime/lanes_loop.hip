@@ -285,7 +285,20 @@ LanesLoop::LanesLoop(const LanesLoopCfg& cfg, Comm* comm)
   const char* sl = std::getenv("PSX_RIDERS_SLAB");
   slab_on_ = ovl_ && tile_riders_ && !(sl && sl[0] == '0');
   if (ovl_) {
-    hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
+    // The two streams of the overlapped launches must not share a hardware queue (packets
+    // of one queue run in order: the next round's launch would wait for the previous one to
+    // END, the very thing the overlap removes).  HIP spreads a process's streams of one
+    // priority over GPU_MAX_HW_QUEUES (4) queues, and every solver holds a capture stream,
+    // RCCL / torch.distributed a few more: the second stream takes the least priority,
+    // whose queue pool is its own (PSX_OVL_STREAM=normal: the previous form, for A/B).
+    const char* os = std::getenv("PSX_OVL_STREAM");
+    if (os && os[0] == 'n') {
+      hip_check(hipStreamCreateWithFlags(&ostream_, hipStreamNonBlocking), "hipStreamCreate(overlap)");
+    } else {
+      int prio_lo = 0, prio_hi = 0;
+      hip_check(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), "hipDeviceGetStreamPriorityRange");
+      hip_check(hipStreamCreateWithPriority(&ostream_, hipStreamNonBlocking, prio_lo), "hipStreamCreate(overlap)");
+    }
     hip_check(hipEventCreateWithFlags(&ovl_in_, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&ovl_out_, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventCreateWithFlags(&ovl_last_, hipEventDisableTiming), "hipEventCreate");

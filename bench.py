@@ -233,8 +233,9 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
     elif async_mode:
         par = f"ps-{mode} 1 server rank + {n_workers} worker ranks ({backend} p2p{', sparse push' if a.model != 'dense' else ''})"
     elif cfg.bsp_schedule == "peer_sum" and cfg.server_colocated:
-        par = (f"ps-{mode} rank 0: server kernel (XCD 7) + {n_workers - (world - 1) * wpr} workers, "
-               f"{world - 1} more ranks x {wpr} workers (peer_sum over xGMI: each rank's lane sum stored into "
+        more = f", {world - 1} more ranks x {wpr} workers" if world > 1 else " (one rank)"
+        par = (f"ps-{mode} rank 0: server kernel (XCD 7) + {n_workers - (world - 1) * wpr} workers{more} "
+               f"(peer_sum over xGMI: each rank's lane sum stored into "
                f"rank 0's inbox by its round kernel, summed + applied by the server kernel, weights written into "
                f"every rank's receive slot; no collective per round)")
     elif cfg.bsp_schedule == "peer_sum":

@@ -15,6 +15,13 @@ sys.path.insert(0, ROOT)
 def cfg_for(world: int, mode: str):
     from psx.runtime.config import PSConfig
 
+    if mode == "peer_sum_colo2":
+        # (one-off rehearsal, PSX_PSUM_REHEARSE_MULTI=1) the colocated form across two ranks:
+        # rank 0 = the server kernel + 3 lanes, rank 1 = 3 lanes pushing into inbox slot 1
+        return PSConfig(num_workers=6, consistency_model=0, producer_time_per_event=0,
+                        stream_mode="per_iter", rows_per_iter=1024, epochs=1000, max_iters=6,
+                        min_buffer_size=128, max_buffer_size=1024, init="random", seed=0, server_colocated=True,
+                        workers_per_rank=3, bsp_schedule="peer_sum", worker_timeout_s=20.0, idle_wait_s=20.0)
     if mode in ("peer_sum_colo", "peer_sum_colo_vote"):
         # peer_sum with the server colocated, world 1: rank 0's server kernel (XCD 7) + its own
         # 7 lanes (XCDs 0-6) in ONE process -- the server's command thread beside the lanes loop

@@ -285,3 +285,29 @@ def test_peer_sum_colocated_vote_chunks(cuda, tmp_path):
     server thread joined after each, the stop vote between them."""
     res = _launch(tmp_path, "peer_sum_colo_vote", world=1, timeout=175)
     assert res[0]["rounds"] > 0 and res[0]["lanes"], res
+
+
+@pytest.mark.skipif(os.environ.get("PSX_PSUM_REHEARSE_MULTI") != "1",
+                    reason="one-off rehearsal: two processes' lanes on one GPU can deadlock on each other's CUs")
+def test_peer_sum_colocated_two_ranks_rehearsal(cuda, tmp_path):
+    """The colocated form across ranks (the N-GPU default's indexing: rank 0's lanes push into
+    its local inbox slot 0, rank 1's into slot 1 over the IPC mapping; the server writes rank
+    0's local receive slot and rank 1's mapped one), rehearsed on one GPU: rank 0 = the server
+    kernel (XCD 6) + 3 lanes (XCDs 0-2), rank 1 = 3 lanes (XCDs 3-5).  Weights equal one process
+    hosting the 6 workers within 2e-4 (the ranks' sums are added per rank first)."""
+    res = _launch(tmp_path, "peer_sum_colo2", world=2, timeout=175)
+    assert [r["rounds"] for r in res] == [6, 6] and all(r["lanes"] for r in res), res
+    w_ps = torch.load(os.path.join(tmp_path, "w_peer_sum_colo2.pt"), weights_only=True)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _ipc_rank import cfg_for
+
+    from psx.runtime.engine import LocalEngine
+    from psx.utils.data import synth_finefood
+
+    cfg = cfg_for(2, "peer_sum_colo2")
+    cfg.bsp_schedule, cfg.workers_per_rank = "allreduce", 1
+    eng = LocalEngine(cfg, cuda, train=synth_finefood(20000, seed=0), test=synth_finefood(4877, seed=1))
+    eng.run(close_log=False)
+    eng.log.drain(block=True)
+    w_loc = eng.server.w.detach().cpu()
+    assert torch.allclose(w_ps, w_loc, rtol=0, atol=2e-4), (w_ps - w_loc).abs().max().item()

@@ -244,7 +244,10 @@ class DistEngine:
         n_worker_ranks = world - 1 if self.dedicated else world
         self._rank_workers = rank_worker_layout(cfg, world)  # per rank: (first worker id, count)
         n_workers = sum(c for _, c in self._rank_workers)
-        if self.psum_colocated and world > 1 and oversubscribed():
+        if self.psum_colocated and world > 1 and oversubscribed() and os.environ.get("PSX_PSUM_REHEARSE_MULTI") != "1":
+            # (PSX_PSUM_REHEARSE_MULTI=1: a short one-off rehearsal of the rank indexing; two
+            # processes' lanes on one GPU can deadlock on each other's CUs, section 2 of
+            # profiles/r06/README.md)
             raise ValueError("--bsp_schedule peer_sum with the server colocated: one rank per GPU (a shared GPU "
                              "would host two processes' lanes); the one-GPU rehearsal is world 1")
         if n_worker_ranks < 1:
@@ -670,7 +673,7 @@ class DistEngine:
                      log_server=int(self.rank == 0 and lsrv is not None), log_workers=int(bool(W) and cfg.log_workers),
                      # ranks sharing one GPU (IPC transport): worker rank i's lanes on XCDs
                      # i*wpr .. i*wpr + wpr - 1, so no two ranks' lanes share an XCD
-                     xcd0=(self.worker_id * len(W)) if (W and (getattr(comm, "kind", "rccl") == "ipc" or (
+                     xcd0=self._rank_workers[self.rank][0] if (W and (getattr(comm, "kind", "rccl") == "ipc" or (
                          comm is None and oversubscribed()))) else 0,
                      sink=self.log.native.handle if self.log is not None else 0,
                      tracker=lsrv.tracker.handle if (lsrv is not None and self.rank == 0) else 0,
@@ -759,6 +762,9 @@ class DistEngine:
                     srv.frag.refresh(srv.w)
                 srv.updates += N * n
                 self.native_server_host_us_per_round = float(self._pserver.host_us_per_round)
+                if os.environ.get("PSX_LANES_TRACE_OUT"):
+                    with open(f"{os.environ['PSX_LANES_TRACE_OUT']}.rank0", "a") as fh:
+                        fh.write(json.dumps({"rank": 0, "server": [list(r) for r in self._pserver.trace_take()]}) + "\n")
         # (where a call's wall clock went: the rounds, then the tail -- bench.py gathers these)
         self._phases = {"rounds_ms": round((t1 - t0) * 1e3, 3),
                         "tail_ms": round((time.perf_counter() - t1) * 1e3, 3)}
@@ -796,7 +802,7 @@ class DistEngine:
         n_lanes = sum(c for _, c in self._rank_workers)
         if oversubscribed() and n_lanes >= 8:
             raise ValueError("one shared GPU: the worker ranks' lanes leave no XCD for the server kernel")
-        if oversubscribed() and Wr > 1 and not colo:
+        if oversubscribed() and Wr > 1 and not colo and os.environ.get("PSX_PSUM_REHEARSE_MULTI") != "1":
             # Each worker rank's per-round launch places workgroups on every XCD (blockIdx % 8),
             # those on another rank's XCDs leave at once -- once a CU there is free.  With two
             # worker ranks whose next launches' lanes spin on their receive tags (and whose

@@ -151,6 +151,103 @@ __device__ __forceinline__ void srv_batch_slice(const SrvArgs& a, const SrvCmd& 
   __syncthreads();  // (ents / ok_s: the next slice of this workgroup)
 }
 
+// A BSP round (kSrvBspSum) on workgroup wg's slices wg, wg + nwg, ... -- up to kBspSl of them
+// in ONE pass: every (slice, rank) tag polled by a lane of its own, all the ranks' slice loads
+// in flight, the receive slots' stores drained together, then every (slice, rank) tag by a
+// thread of its own.  A launch with fewer workgroups than slices (the colocated rank 0 and
+// the shared-GPU rehearsals keep half of the XCD's CUs free) then pays each xGMI / memory
+// round trip once per round, not once per slice.  The sums are the per-slice ones of
+// srv_slice: ranks in rank order, w += lr * sum.
+template <int FP>
+__device__ __forceinline__ void srv_bsp_slices(const SrvArgs& a, const SrvCmd& cmd, int wg, unsigned long long* err) {
+  constexpr int NS = FP / 32;
+  constexpr int kBspSl = 4;
+  const int tid = threadIdx.x, K = a.K, N = a.N;
+  __shared__ int ok_s;
+  for (int s0 = wg; s0 < NS; s0 += kBspSl * a.nwg) {
+    int nsl = 0;
+    for (int j = 0; j < kBspSl; ++j) nsl += s0 + j * a.nwg < NS ? 1 : 0;
+    // the (slice, rank) tags: wave 0, one lane each (a wall-clock budget per pass)
+    if (tid < 64) {
+      bool late = false;
+      const long long t_end = rt_now() + a.tag_ticks;
+      for (int i = tid; i < nsl * N; i += 64) {
+        const int j = i / N, r = i - j * N;
+        const unsigned* tg = a.inbox_tag + (size_t)r * NS + (s0 + j * a.nwg);
+        while ((int)(ld_sys_u32(tg) - cmd.dtag) < 0 && !(late = rt_now() > t_end)) __builtin_amdgcn_s_sleep(2);
+        if (late) break;
+      }
+      const bool any_late = __any(late);
+      if (tid == 0) {
+        ok_s = any_late ? 0 : 1;
+        if (any_late) xstore(err, 11ull);  // a rank's sum never arrived: apply nothing
+      }
+    }
+    __syncthreads();
+    const int c = tid >> 5;
+    const bool coef = c < K;
+    float nw[kBspSl], nb = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBspSl; ++j) {
+      const int sj = s0 + j * a.nwg;
+      nw[j] = (j < nsl && coef) ? ld_sc1(a.w + (size_t)c * FP + sj * 32 + (tid & 31)) : 0.f;
+    }
+    const bool icpt = s0 == 0 && tid < K;  // (slice 0 is always the pass's first)
+    if (icpt) nb = ld_sc1(a.w + (size_t)K * FP + tid);
+    if (ok_s) {
+      float sum[kBspSl], sumi = 0.f;
+#pragma unroll
+      for (int j = 0; j < kBspSl; ++j) sum[j] = 0.f;
+      for (int r = 0; r < N; ++r) {  // ranks in rank order (the loads of a rank's slices in flight together)
+        const float* d = a.inbox + (size_t)r * (size_t)a.in_stride;
+        float v[kBspSl];
+#pragma unroll
+        for (int j = 0; j < kBspSl; ++j)
+          v[j] = (j < nsl && coef) ? ld_sys_f32(d + (size_t)c * FP + (s0 + j * a.nwg) * 32 + (tid & 31)) : 0.f;
+        const float vi = icpt ? ld_sys_f32(d + (size_t)K * FP + tid) : 0.f;
+#pragma unroll
+        for (int j = 0; j < kBspSl; ++j) sum[j] += v[j];
+        sumi += vi;
+      }
+#pragma unroll
+      for (int j = 0; j < kBspSl; ++j)
+        if (j < nsl && coef) {
+          nw[j] += a.lr * sum[j];
+          st_sc1(a.w + (size_t)c * FP + (s0 + j * a.nwg) * 32 + (tid & 31), nw[j]);
+        }
+      if (icpt) {
+        nb += a.lr * sumi;
+        st_sc1(a.w + (size_t)K * FP + tid, nb);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kBspSl; ++j) {
+      if (j >= nsl) break;
+      const int f = (s0 + j * a.nwg) * 32 + (tid & 31);
+      if (cmd.log && coef) write_frag(a.shi, a.slo, c, f, f < a.F ? nw[j] : 0.f);
+      for (unsigned long long m = cmd.relmask; m; m &= m - 1) {  // the new slice into every rank's receive slot
+        float* dst = a.rx[__builtin_ctzll(m)];
+        if (coef) st_sys_f32(dst + (size_t)c * FP + f, nw[j]);
+      }
+    }
+    if (icpt) {
+      if (cmd.log) a.sb[tid] = nb;
+      for (unsigned long long m = cmd.relmask; m; m &= m - 1) st_sys_f32(a.rx[__builtin_ctzll(m)] + (size_t)K * FP + tid, nb);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the (slice, rank) tags, a thread each (no release fence: sc0 sc1 stores, drained above)
+    for (int i = tid; i < nsl * 64; i += 256) {
+      const int j = i >> 6, r = i & 63;
+      if (!((cmd.relmask >> r) & 1ull)) continue;
+      const int sj = s0 + j * a.nwg;
+      __hip_atomic_store((g_u32*)(a.ptag + (size_t)r * NS + sj), cmd.dtag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_sys_u32(a.rx_tag[r] + sj, cmd.dtag);
+    }
+    __syncthreads();  // (ok_s: the next pass)
+  }
+}
+
 // Slice s of command `cmd` (one workgroup; every thread calls it).
 template <int FP>
 __device__ __forceinline__ void srv_slice(const SrvArgs& a, const SrvCmd& cmd, int s, unsigned long long* err) {
@@ -238,12 +335,16 @@ __device__ __forceinline__ void srv_command(char* lds, const SrvArgs& a, const S
   const int K = a.K;
   // workgroup wg owns slices wg, wg + nwg, ... (nwg < NS: a server launch that leaves CUs of
   // its XCD to other processes on a shared GPU)
-  for (int s = wg; s < NS; s += a.nwg) {
-    if (cmd.k == kSrvBatch) {
-      srv_batch_slice<FP>(a, cmd, s, err);
-    } else {
-      srv_slice<FP>(a, cmd, s, err);
-      if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
+  if (cmd.k == kSrvBspSum) {
+    srv_bsp_slices<FP>(a, cmd, wg, err);
+  } else {
+    for (int s = wg; s < NS; s += a.nwg) {
+      if (cmd.k == kSrvBatch) {
+        srv_batch_slice<FP>(a, cmd, s, err);
+      } else {
+        srv_slice<FP>(a, cmd, s, err);
+        if (a.nwg < NS) __syncthreads();  // (ok_s / the tag lanes of the next slice)
+      }
     }
   }
   long long* trn = (a.tr && wg == 0 && threadIdx.x == 0) ? a.tr + (size_t)(n % (unsigned long long)a.tr_cap) * 4 : nullptr;

@@ -7,13 +7,14 @@
 constexpr int kND = 3 + 2 * psx::kMaxHist;
 using namespace psx;
 __global__ void kctrl(SolverCfg cfg, const double* dg, Ctrl* g, long long* t) {
-  __shared__ Ctrl c;
+  __shared__ Ctrl c, snap;
   __shared__ CtrlScratch ws;
   __shared__ double dots[3][64];
   if (threadIdx.x == 0) { c = *g; ctrl_init(c); for (int s = 0; s < 3; ++s) for (int i = 0; i < 64; ++i) dots[s][i] = dg[s * 64 + i]; }
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int s = 0; s < 3; ++s) {
+      if (s == 1) snap = c;
       const long long t0 = __builtin_amdgcn_s_memrealtime();
       ctrl_step(c, cfg, dots[s][kND], dots[s], s, ws);
       __builtin_amdgcn_s_waitcnt(0);
@@ -21,6 +22,12 @@ __global__ void kctrl(SolverCfg cfg, const double* dg, Ctrl* g, long long* t) {
       t[2 * s] = t1 - t0;
       t[2 * s + 1] = c.action;
     }
+    // the accepting step again, its code now in the instruction cache
+    c = snap;
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    ctrl_step(c, cfg, dots[1][kND], dots[1], 1, ws);
+    __builtin_amdgcn_s_waitcnt(0);
+    t[6] = __builtin_amdgcn_s_memrealtime() - t0;
   }
   __syncthreads();
   if (threadIdx.x == 0) *g = c;
@@ -40,10 +47,10 @@ int main() {
   hipMemset(g, 0, sizeof(Ctrl));
   for (int rep = 0; rep < 3; ++rep) {
     kctrl<<<1, 256>>>(cfg, dg, g, t);
-    long long ht[6];
+    long long ht[7];
     hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
-    printf("{\"rep\": %d, \"us\": [%.2f, %.2f, %.2f], \"action\": [%lld, %lld, %lld]}\n", rep, ht[0] / 100.0, ht[2] / 100.0,
-           ht[4] / 100.0, ht[1], ht[3], ht[5]);
+    printf("{\"rep\": %d, \"us\": [%.2f, %.2f, %.2f], \"action\": [%lld, %lld, %lld], \"accept_again_us\": %.2f}\n", rep,
+           ht[0] / 100.0, ht[2] / 100.0, ht[4] / 100.0, ht[1], ht[3], ht[5], ht[6] / 100.0);
   }
   return 0;
 }

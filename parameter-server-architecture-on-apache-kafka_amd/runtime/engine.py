@@ -640,6 +640,11 @@ class LocalEngine:
                 "updates_per_s": (srv.updates - u0) / elapsed if elapsed > 0 else 0.0, "native_loop": True}
 
     def _run_bsp(self) -> dict:
+        # one worker: the native loop around the one-XCD persistent solve beats the lanes
+        # loop's one-lane launch (14.4-14.5k against 12.4-12.6k updates/s, profiles/r06/s37);
+        # runs it cannot take (tracing, checkpoints, wall clock, cadence) stay on the lanes
+        if len(self.workers) == 1 and self._native_bsp_ok():
+            return self._run_bsp_native()
         if self._lanes_ok():
             return self._run_bsp_lanes()
         if self._native_bsp_ok():

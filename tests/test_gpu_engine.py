@@ -139,7 +139,10 @@ def test_paired_eval_rows_match_unpaired(cuda, N):
 def test_riding_eval_matches_separate_launches(cuda, monkeypatch, N):
     """Evaluation rows riding in the next solve's bwd_update launches (and, for one
     worker, the server update fused into the solve's finalisation) log exactly the
-    rows of the separate evaluation / update launches, and end at the same model."""
+    rows of the separate evaluation / update launches, and end at the same model.  (The
+    Python round loop, where riding is a choice: the native loops always ride.)"""
+    monkeypatch.setenv("PSX_NATIVE_LANES", "0")
+    monkeypatch.setenv("PSX_NATIVE_BSP", "0")
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     kw = dict(num_workers=N, max_iters=10, init="random", min_buffer_size=512, max_buffer_size=512)
     res = []
@@ -271,6 +274,7 @@ def test_fused_ingest_matches_ring_copy(cuda, monkeypatch, rows):
     kMaxFusedIngest = 1024 rows per solve, a fully fresh window included) end at the
     same model and log the same rows as the separate ring-ingest launch (Python
     loop), and as the native loop (which always fuses)."""
+    monkeypatch.setenv("PSX_NATIVE_LANES", "0")  # (the single-worker loops; the lanes loop has its own tests)
     train, test = synth_finefood(8000, seed=0), synth_finefood(1000, seed=1)
     res = []
     for fused, native in ((True, "0"), (False, "0"), (True, "1")):

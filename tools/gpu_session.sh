@@ -98,12 +98,13 @@ w4_short --workers 4 --steps 20 --warmup 5
 w1 --workers 1 --steps 300 --warmup 30
 buf4096 --buffer 4096 --steps 100 --warmup 10
 long --steps 3000 --warmup 30}" ;;
-    multirank)  # bench.py's multi-rank paths with every rank on GPU 0 (disjoint XCDs, gloo control plane)
+    multirank)  # bench.py's multi-rank paths with every rank on GPU 0 (disjoint XCDs, gloo control plane;
+      # peer_sum with a dedicated server rank: the colocated default needs a GPU per rank, world1ps)
       while read -r n g args; do
         [ -z "$n" ] && continue
         PSX_GPU_OVERSUBSCRIBE=1 PSX_PG_TIMEOUT_S=120 bench_run $n 240 --gpus $g $args; rc=$?; fatal_rc $rc && exit $rc
-      done <<< "${MR_RUNS:-peer_sum_2x7 2 --workers 7 --schedule peer_sum --steps 300 --warmup 30
-peer_sum_2x6 2 --workers 6 --schedule peer_sum --steps 300 --warmup 30
+      done <<< "${MR_RUNS:-peer_sum_2x7 2 --workers 7 --schedule peer_sum --dedicated-server --steps 300 --warmup 30
+peer_sum_2x6 2 --workers 6 --schedule peer_sum --dedicated-server --steps 300 --warmup 30
 reduce_bcast_3x3 3 --workers 3 --schedule reduce_bcast --steps 20 --warmup 5
 peer_bsp_3x3 3 --workers 3 --schedule peer --steps 20 --warmup 5
 ssp3_3x3 3 --workers 3 --consistency 3 --steps 20 --warmup 5

@@ -490,6 +490,31 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("workspace_bytes", &WideSolver::workspace_bytes)
       .def_property_readonly("kernels_per_solve", &WideSolver::kernels_per_solve);
 
+  py::class_<WideLanes>(m, "WideLanes")
+      .def(py::init([](py::list solvers, int xcd0) {
+             std::vector<WideSolver*> v;
+             for (auto o : solvers) v.push_back(o.cast<WideSolver*>());
+             return std::make_unique<WideLanes>(v, xcd0);
+           }),
+           py::arg("solvers"), py::arg("xcd0") = 0, py::keep_alive<1, 2>())
+      .def("run",
+           [](WideLanes& s, const std::vector<int>& B, const std::vector<int>& start, uintptr_t stream) {
+             s.run(B, start, S(stream));
+           })
+      .def("eval",
+           [](WideLanes& s, uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int T, uintptr_t w, int nov,
+              const std::vector<uintptr_t>& slots, const std::vector<unsigned long long>& seqs, uintptr_t server_slot,
+              unsigned long long server_seq, uintptr_t stream) {
+             s.eval(P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val), P<const int32_t>(y), T,
+                    P<const float>(w), nov, slots, seqs, server_slot, server_seq, S(stream));
+           })
+      .def("apply",
+           [](WideLanes& s, uintptr_t w, float lr, const std::vector<int>& order, uintptr_t stream) {
+             s.apply(P<float>(w), lr, order, S(stream));
+           })
+      .def_property_readonly("lanes", &WideLanes::lanes)
+      .def_property_readonly("launches", &WideLanes::launches);
+
   m.def("sparse_ring_ingest", [](uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int64_t src_first,
                                  int64_t src_step, int64_t n, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz,
                                  uintptr_t ry, int64_t dst_first, int cap, int NZ, uintptr_t trunc, uintptr_t stream) {

@@ -166,6 +166,48 @@ void wide_launch_persist(const WideCfg& c, const WideDev& d, int B, int start, i
 int wide_persist_grid();
 void wide_launch_finalize(const WideCfg& c, const WideDev& d, hipStream_t s);
 int wide_dots_blocks(int64_t PLmax);
+size_t wide_persist_lds(const WideCfg& c, const WideDev& d);
+
+// ---------------------------------------------------------------------------
+// Wide lanes: the local solves of up to kWideMaxLanes in-process workers in ONE
+// launch, lane l on XCD xcd0 + l with kWideLaneWg co-resident workgroups (the
+// persistent solve's phases, its grid barriers inside the XCD's L2).  Workgroups
+// claim their lane from their XCC_ID (lanes_kernels.hip's claim), so the dispatch
+// order of the grid does not matter.  devs: [L] WideDev table in device memory (each
+// lane's own workspace and ring; w_old = the server weights every lane pulled).
+constexpr int kWideMaxLanes = 8;
+constexpr int kWideLaneWg = 32;
+struct WideLanesArgs {
+  int L;
+  int xcd0;
+  unsigned* claim;  // [2][16] per-XCD slot counters; launch parity cpar, the other one cleared
+  int cpar;
+  int B[kWideMaxLanes];
+  int start[kWideMaxLanes];
+};
+void wide_launch_lanes(const WideCfg& c, const WideDev* devs, const WideLanesArgs& a, size_t lds, hipStream_t s);
+int wide_lanes_grid();
+
+// Test-set evaluation of up to kWideMaxEval models of the wide model in ONE pass:
+// model m < nov = the common weights w overlaid with lane m's window solution
+// (htab / hmask / wloc, the worker row of a lane), and with `plain` one more model, w
+// itself (a server row).  Each non-zero's row of w is gathered once.  The last
+// workgroup publishes every model's counts into its pinned EvalSlot (+ the loss).
+constexpr int kWideMaxEval = kWideMaxLanes + 1;
+struct WideEvalModels {
+  int nov;    // overlay models
+  int plain;  // 1: model nov is w itself
+  const int2* htab[kWideMaxLanes];
+  unsigned hmask[kWideMaxLanes];
+  const float* wloc[kWideMaxLanes];
+  const float* loss[kWideMaxEval];
+  char* slot[kWideMaxEval];
+  unsigned long long seq[kWideMaxEval];
+};
+// acc: [kWideMaxEval][256] cells at stride kAccStride (zero between passes)
+void launch_wide_eval_multi(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                            const int32_t* y, int T, const float* w, const WideEvalModels& m, int* acc,
+                            unsigned* ticket, hipStream_t s);
 
 // Ring ingest: rows src_first + i*src_step of a CSR matrix (i < n) -> ring
 // slots (dst_first + i) % cap; rows longer than NZ are truncated and counted

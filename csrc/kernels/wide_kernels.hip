@@ -818,13 +818,12 @@ __device__ __forceinline__ void wide_gen_barrier(unsigned* bar, unsigned G, unsi
   __syncthreads();
 }
 
+// The persistent solve's phases for workgroup blk of G (the whole grid of
+// wide_persist_kernel, or one lane's XCD in wide_lanes_kernel).
 template <int KP, int NQ>
-__global__ __launch_bounds__(512) void wide_persist_kernel(WideCfg c, WideDev d, int B, int start, int phases) {
-  extern __shared__ __attribute__((aligned(16))) int pl_lds[];
-  __shared__ WideFwdShared fsh;
-  __shared__ WideDotsShared dsh;
-  __shared__ int phase_s;
-  const int G = gridDim.x, blk = blockIdx.x;
+__device__ __forceinline__ void wide_persist_body(const WideCfg& c, const WideDev& d, int B, int start, int phases,
+                                                  int G, int blk, int* pl_lds, WideFwdShared& fsh,
+                                                  WideDotsShared& dsh, int& phase_s) {
   const int ngr = (c.cap + d.RB - 1) / d.RB;
   unsigned* err = d.cnt + 3;
   if (phases & 1) {
@@ -854,6 +853,62 @@ __global__ __launch_bounds__(512) void wide_persist_kernel(WideCfg c, WideDev d,
     wide_gen_barrier(d.pbar, G, err);
   }
   wide_finalize_body(c, d, blk, G);
+}
+
+template <int KP, int NQ>
+__global__ __launch_bounds__(512) void wide_persist_kernel(WideCfg c, WideDev d, int B, int start, int phases) {
+  extern __shared__ __attribute__((aligned(16))) int pl_lds[];
+  __shared__ WideFwdShared fsh;
+  __shared__ WideDotsShared dsh;
+  __shared__ int phase_s;
+  wide_persist_body<KP, NQ>(c, d, B, start, phases, (int)gridDim.x, (int)blockIdx.x, pl_lds, fsh, dsh, phase_s);
+}
+
+// wide_lanes_kernel: up to 8 workers' persistent solves in one launch, lane l on
+// XCD xcd0 + l.  Two workers' separate persistent launches deadlock (each waits for
+// CUs the other's workgroups hold: the dispatcher places a launch's workgroups in
+// order, profiles/r02_v5), and the launch chain is ~14 kernels per solve on the
+// workers' streams, which HIP's 4 hardware queues serialise pairwise
+// (profiles/r06/README.md section 7).  One launch of 8 x 32 workgroups instead: a
+// workgroup claims the next of the 32 slots of its XCD's lane, so the lane's grid
+// barriers and dot-product tickets stay inside one L2, and surplus workgroups
+// (an XCD dealt more than 32, or no lane) leave at once.
+template <int KP, int NQ>
+__global__ __launch_bounds__(512) void wide_lanes_kernel(WideCfg c, const WideDev* __restrict__ devs,
+                                                         WideLanesArgs a) {
+  extern __shared__ __attribute__((aligned(16))) int pl_lds[];
+  __shared__ WideFwdShared fsh;
+  __shared__ WideDotsShared dsh;
+  __shared__ int phase_s;
+  __shared__ int role_s;
+  if (threadIdx.x == 0) {
+    // the other parity's counters (the previous launch, complete in stream order) for the next launch
+    if (blockIdx.x < 16)
+      __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
+    const int lx = xcc - a.xcd0;
+    int r = -1;
+    if (lx >= 0 && lx < a.L) {
+      const unsigned k = __hip_atomic_fetch_add(a.claim + 16 * a.cpar + lx, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      if (k < (unsigned)kWideLaneWg) r = lx * kWideLaneWg + (int)k;
+    }
+    role_s = r;
+  }
+  __syncthreads();
+  const int r = __builtin_amdgcn_readfirstlane(role_s);
+  if (r < 0) return;
+  const int l = r / kWideLaneWg, blk = r - l * kWideLaneWg;
+  // the lane's window: constant-index reads of the kernel argument (a runtime index
+  // would copy the argument block into scratch, lanes_body.h pick())
+  int B = a.B[0], start = a.start[0];
+#pragma unroll
+  for (int i = 1; i < kWideMaxLanes; ++i)
+    if (l == i) {
+      B = a.B[i];
+      start = a.start[i];
+    }
+  wide_persist_body<KP, NQ>(c, devs[l], B, start, 3, kWideLaneWg, blk, pl_lds, fsh, dsh, phase_s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1013,6 +1068,44 @@ void wide_launch_persist(const WideCfg& c, const WideDev& d, int B, int start, i
     case 4: launch_persist_kp<4>(c, d, B, start, phases, s); break;
     case 8: launch_persist_kp<8>(c, d, B, start, phases, s); break;
     default: launch_persist_kp<16>(c, d, B, start, phases, s); break;
+  }
+}
+
+// 8 XCDs x 32 lanes' workgroups, twice over: an XCD the dispatcher deals fewer than
+// 32 of the first 256 still gets its lane's 32 (the surplus leaves at once)
+int wide_lanes_grid() { return 2 * 8 * kWideLaneWg; }
+
+template <int KP, int NQ>
+static void set_lanes_attr() {
+  (void)hipFuncSetAttribute((const void*)wide_lanes_kernel<KP, NQ>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            96 * 1024);
+}
+
+template <int KP>
+static void launch_lanes_kp(const WideCfg& c, const WideDev* devs, const WideLanesArgs& a, size_t lds,
+                            hipStream_t s) {
+  static const bool prepared = (set_lanes_attr<KP, 1>(), set_lanes_attr<KP, 2>(), set_lanes_attr<KP, 4>(),
+                                set_lanes_attr<KP, 8>(), true);
+  (void)prepared;
+  const int nq = (c.NZ + 63) / 64;
+  const int G = wide_lanes_grid();
+  if (nq <= 1)
+    wide_lanes_kernel<KP, 1><<<G, 512, lds, s>>>(c, devs, a);
+  else if (nq <= 2)
+    wide_lanes_kernel<KP, 2><<<G, 512, lds, s>>>(c, devs, a);
+  else if (nq <= 4)
+    wide_lanes_kernel<KP, 4><<<G, 512, lds, s>>>(c, devs, a);
+  else
+    wide_lanes_kernel<KP, 8><<<G, 512, lds, s>>>(c, devs, a);
+}
+
+void wide_launch_lanes(const WideCfg& c, const WideDev* devs, const WideLanesArgs& a, size_t lds, hipStream_t s) {
+  switch (c.KP) {
+    case 1: launch_lanes_kp<1>(c, devs, a, lds, s); break;
+    case 2: launch_lanes_kp<2>(c, devs, a, lds, s); break;
+    case 4: launch_lanes_kp<4>(c, devs, a, lds, s); break;
+    case 8: launch_lanes_kp<8>(c, devs, a, lds, s); break;
+    default: launch_lanes_kp<16>(c, devs, a, lds, s); break;
   }
 }
 
@@ -1252,6 +1345,129 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
   }
 }
 
+// wide_eval_multi_kernel: see launch_wide_eval_multi.  16 lanes per row (4 rows per
+// wave), each lane one non-zero at a time: the row of w gathered once, every
+// overlay's table probed for the feature (independent loads, in flight together),
+// the lane's local coefficients where it maps the feature.
+template <int KP>
+__global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, const int64_t* __restrict__ indptr,
+                                                              const int32_t* __restrict__ idx,
+                                                              const uint16_t* __restrict__ val,
+                                                              const int32_t* __restrict__ y, int T,
+                                                              const float* __restrict__ w, WideEvalModels m, int* acc,
+                                                              unsigned* ticket) {
+  __shared__ int cl[kWideMaxEval][256];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int M = m.nov + m.plain;
+  for (int j = 0; j < kWideMaxEval; ++j) cl[j][tid] = 0;
+  __syncthreads();
+  for (int64_t r0 = (int64_t)blockIdx.x * 16; r0 < T; r0 += (int64_t)gridDim.x * 16) {
+    const int64_t row = r0 + (tid >> 4);
+    const bool valid = row < T;
+    float z[kWideMaxEval][KP];
+#pragma unroll
+    for (int j = 0; j < kWideMaxEval; ++j)
+#pragma unroll
+      for (int k = 0; k < KP; ++k) z[j][k] = 0.f;
+    if (valid) {
+      const int64_t a0 = indptr[row], b0 = indptr[row + 1];
+      for (int64_t e = a0 + (lane & 15); e < b0; e += 16) {
+        const int f = idx[e];
+        const float v = bf2f(val[e]);
+        float wv[KP];
+        ldk<KP>(w + (int64_t)f * KP, wv);
+        int li[kWideMaxLanes];
+#pragma unroll
+        for (int j = 0; j < kWideMaxLanes; ++j) li[j] = j < m.nov ? wide_find(m.htab[j], m.hmask[j], f) : -1;
+#pragma unroll
+        for (int j = 0; j < kWideMaxLanes; ++j) {
+          if (j >= m.nov) break;
+          float ov[KP];
+          if (li[j] >= 0) {
+            ldk<KP>(m.wloc[j] + KP + (int64_t)li[j] * KP, ov);
+          } else {
+#pragma unroll
+            for (int k = 0; k < KP; ++k) ov[k] = wv[k];
+          }
+#pragma unroll
+          for (int k = 0; k < KP; ++k) z[j][k] += v * ov[k];
+        }
+        if (m.plain) {
+#pragma unroll
+          for (int j = 0; j < kWideMaxEval; ++j)
+            if (j == m.nov) {
+#pragma unroll
+              for (int k = 0; k < KP; ++k) z[j][k] += v * wv[k];
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kWideMaxEval; ++j) {
+      if (j >= M) break;
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) z[j][k] += __shfl_xor(z[j][k], o, 64);
+    }
+    if ((lane & 15) == 0 && valid) {
+      int yl = y[row];
+      if (K == 1) yl = yl > 0 ? 1 : 0;
+      yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
+#pragma unroll
+      for (int j = 0; j < kWideMaxEval; ++j) {
+        if (j >= M) break;
+        float bv[KP];
+        const bool ovl = j < m.nov;
+        const float* bsrc = w + F * KP;  // the intercepts: the overlay's own, or w's
+#pragma unroll
+        for (int i = 0; i < kWideMaxLanes; ++i)
+          if (i == j && ovl) bsrc = m.wloc[i];
+        ldk<KP>(bsrc, bv);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) z[j][k] += bv[k];
+        atomicAdd(&cl[j][yl * 16 + wide_argmax<KP>(K, z[j])], 1);
+      }
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < M; ++j) {
+    const int v = cl[j][tid];
+    if (v) atomicAdd(acc + (j * 256 + tid) * kAccStride, v);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  // publication as in wide_eval_kernel: drained system-scope stores into the uncached
+  // host slots, then each slot's sequence number
+#pragma unroll
+  for (int j = 0; j < kWideMaxEval; ++j) {
+    if (j >= M) break;
+    char* slot = m.slot[j];
+    const float* loss = m.loss[j];
+    const int tot = __hip_atomic_exchange(acc + (j * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0)
+      __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int j = 0; j < kWideMaxEval; ++j) {
+      if (j >= M) break;
+      __hip_atomic_store((unsigned long long*)(m.slot[j] + 1032), m.seq[j], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <int KP>
 __global__ __launch_bounds__(256) void wide_logits_kernel(int64_t F, const int64_t* __restrict__ indptr,
                                                           const int32_t* __restrict__ idx,
@@ -1299,6 +1515,27 @@ void launch_wide_eval(int K, int KP, int64_t F, const int64_t* indptr, const int
       break;
   }
 #undef PSX_WE
+}
+
+void launch_wide_eval_multi(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
+                            const int32_t* y, int T, const float* w, const WideEvalModels& m, int* acc,
+                            unsigned* ticket, hipStream_t s) {
+  if (T <= 0 || m.nov + m.plain <= 0) return;
+  const int grid = grid_for((int64_t)T * 16, 1024);  // 16 rows per workgroup pass
+#define PSX_WM(KV)                                                                                         \
+  case KV:                                                                                                 \
+    wide_eval_multi_kernel<KV><<<grid, 256, 0, s>>>(K, F, indptr, idx, val, y, T, w, m, acc, ticket); \
+    break;
+  switch (KP) {
+    PSX_WM(1)
+    PSX_WM(2)
+    PSX_WM(4)
+    PSX_WM(8)
+    PSX_WM(16)
+    default:
+      break;
+  }
+#undef PSX_WM
 }
 
 void launch_wide_logits(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,

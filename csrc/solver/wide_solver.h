@@ -65,6 +65,7 @@ class WideSolver {
   // s_memrealtime ticks (100 MHz): entry, last block in, dots reduced, ctrl loaded, ctrl stepped, ctrl stored
   std::vector<long long> read_stamps(hipStream_t stream);
   size_t workspace_bytes() const { return ws_bytes_; }
+  const WideDev& dev() const { return dv_; }
   int kernels_per_solve() const {
     if (cfg_.persist) return 1;
     const int nf = cfg_.sc.mode == 1 ? cfg_.sc.nslots : std::min(cfg_.sc.nslots, 1 + cfg_.sc.iters);
@@ -97,5 +98,42 @@ class WideSolver {
 };
 
 const void* wide_begin_symbol();
+
+// Several in-process workers' solves in ONE launch (wide_lanes_kernel): lane l runs
+// solvers[l]'s persistent solve on XCD xcd0 + l.  The solvers keep their own
+// workspaces and outputs (delta, local model, table, loss, stats), so everything that
+// reads a WideSolver after run() reads it after a lanes launch too.  Every solver
+// must be bound to the same w_old (the server weights) and share one configuration.
+// Also the lanes' evaluation pass (launch_wide_eval_multi): the worker rows of the
+// last launch + optionally one server row of w.
+class WideLanes {
+ public:
+  WideLanes(const std::vector<WideSolver*>& solvers, int xcd0);
+  ~WideLanes();
+  WideLanes(const WideLanes&) = delete;
+  WideLanes& operator=(const WideLanes&) = delete;
+  int lanes() const { return (int)solvers_.size(); }
+  void run(const std::vector<int>& B, const std::vector<int>& start, hipStream_t stream);
+  // worker rows of lanes [0, nov) (slot / seq per lane, their losses) and with
+  // server_slot != 0 the row of the plain weights w (the model every lane pulled)
+  void eval(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y, int T, const float* w,
+            int nov, const std::vector<uintptr_t>& slots, const std::vector<unsigned long long>& seqs,
+            uintptr_t server_slot, unsigned long long server_seq, hipStream_t stream);
+  // the server update of the lanes' sparse pushes, one after the other in `order`:
+  // w[uniq[i] * KP + c] += lr * dloc[KP + i * KP + c] (ServerProcessor.java:148-151)
+  void apply(float* w, float lr, const std::vector<int>& order, hipStream_t stream);
+  int64_t launches() const { return launches_; }
+
+ private:
+  std::vector<WideSolver*> solvers_;
+  WideCfg cfg_;
+  int xcd0_;
+  size_t lds_ = 0;
+  WideDev* devs_ = nullptr;   // [L] device table
+  unsigned* claim_ = nullptr; // [2][16]
+  int* acc_ = nullptr;        // [kWideMaxEval][256] cells at stride kAccStride
+  unsigned* ticket_ = nullptr;
+  int64_t launches_ = 0;
+};
 
 }  // namespace psx

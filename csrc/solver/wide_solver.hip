@@ -5,7 +5,8 @@
 #include <string>
 #include <vector>
 
-#include "solver.h"  // hip_check
+#include "../kernels/common.h"  // kAccStride
+#include "solver.h"            // hip_check
 
 namespace psx {
 
@@ -252,6 +253,103 @@ std::vector<long long> WideSolver::read_stamps(hipStream_t stream) {
 void WideSolver::read_ctrl(Ctrl* out, hipStream_t stream) {
   hip_check(hipMemcpyAsync(out, dv_.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, stream), "read ctrl");
   hip_check(hipStreamSynchronize(stream), "sync");
+}
+
+// ---------------------------------------------------------------------------
+WideLanes::WideLanes(const std::vector<WideSolver*>& solvers, int xcd0) : solvers_(solvers), xcd0_(xcd0) {
+  const int L = (int)solvers_.size();
+  if (L < 1 || L > kWideMaxLanes) throw std::invalid_argument("WideLanes: 1..8 solvers");
+  if (!solvers_[0]) throw std::invalid_argument("WideLanes: null solver");
+  if (xcd0 < 0 || xcd0 + L > 8) throw std::invalid_argument("WideLanes: lanes xcd0 .. xcd0 + L - 1 must be XCDs 0..7");
+  cfg_ = solvers_[0]->cfg();
+  std::vector<WideDev> devs(L);
+  for (int l = 0; l < L; ++l) {
+    const WideSolver* s = solvers_[l];
+    if (!s) throw std::invalid_argument("WideLanes: null solver");
+    const WideCfg& c = s->cfg();
+    if (c.pulled) throw std::invalid_argument("WideLanes: pull-mode solvers have two phases");
+    if (c.dense_delta) throw std::invalid_argument("WideLanes: sparse deltas only");
+    if (c.K != cfg_.K || c.KP != cfg_.KP || c.F != cfg_.F || c.cap != cfg_.cap || c.NZ != cfg_.NZ ||
+        c.sc.nslots != cfg_.sc.nslots || c.sc.iters != cfg_.sc.iters || c.sc.hist != cfg_.sc.hist)
+      throw std::invalid_argument("WideLanes: every solver needs one configuration");
+    if (s->dev().w_old != solvers_[0]->dev().w_old)
+      throw std::invalid_argument("WideLanes: every lane pulls the same weights");
+    devs[l] = s->dev();
+    const size_t b = wide_persist_lds(c, devs[l]);
+    if (b > lds_) lds_ = b;
+  }
+  if (lds_ > 96 * 1024) throw std::invalid_argument("WideLanes: ring rows too wide for the persistent solve's LDS");
+  hip_check(hipMalloc(&devs_, sizeof(WideDev) * L), "hipMalloc(wide lanes table)");
+  hip_check(hipMemcpy(devs_, devs.data(), sizeof(WideDev) * L, hipMemcpyHostToDevice), "wide lanes table");
+  hip_check(hipMalloc(&claim_, 2 * 16 * sizeof(unsigned)), "hipMalloc(claim)");
+  hip_check(hipMemset(claim_, 0, 2 * 16 * sizeof(unsigned)), "hipMemset(claim)");
+  const size_t acc_bytes = (size_t)kWideMaxEval * 256 * kAccStride * sizeof(int);
+  hip_check(hipMalloc(&acc_, acc_bytes), "hipMalloc(eval accumulators)");
+  hip_check(hipMemset(acc_, 0, acc_bytes), "hipMemset(eval accumulators)");
+  hip_check(hipMalloc(&ticket_, 64), "hipMalloc(ticket)");
+  hip_check(hipMemset(ticket_, 0, 64), "hipMemset(ticket)");
+}
+
+WideLanes::~WideLanes() {
+  if (devs_) (void)hipFree(devs_);
+  if (claim_) (void)hipFree(claim_);
+  if (acc_) (void)hipFree(acc_);
+  if (ticket_) (void)hipFree(ticket_);
+}
+
+void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hipStream_t stream) {
+  const int L = lanes();
+  if ((int)B.size() != L || (int)start.size() != L) throw std::invalid_argument("WideLanes::run: one window per lane");
+  WideLanesArgs a{};
+  a.L = L;
+  a.xcd0 = xcd0_;
+  a.claim = claim_;
+  a.cpar = (int)(launches_ & 1);
+  for (int l = 0; l < L; ++l) {
+    if (B[l] <= 0) throw std::invalid_argument("local solve on an empty buffer");
+    if (B[l] > cfg_.cap || start[l] < 0 || start[l] >= cfg_.cap) throw std::invalid_argument("window out of ring bounds");
+    a.B[l] = B[l];
+    a.start[l] = start[l];
+  }
+  wide_launch_lanes(cfg_, devs_, a, lds_, stream);
+  hip_check(hipGetLastError(), "wide lanes launch");
+  ++launches_;
+}
+
+void WideLanes::apply(float* w, float lr, const std::vector<int>& order, hipStream_t stream) {
+  for (int l : order) {
+    if (l < 0 || l >= lanes()) throw std::invalid_argument("WideLanes::apply: lane out of range");
+    const WideSolver* s = solvers_[l];
+    launch_wide_apply_sparse(w, cfg_.F, cfg_.KP, s->ucount_dev(), 0, s->uniq(), s->dev().dloc, lr, cfg_.umax, stream);
+  }
+  hip_check(hipGetLastError(), "wide lanes apply launch");
+}
+
+void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y, int T,
+                     const float* w, int nov, const std::vector<uintptr_t>& slots,
+                     const std::vector<unsigned long long>& seqs, uintptr_t server_slot,
+                     unsigned long long server_seq, hipStream_t stream) {
+  if (nov < 0 || nov > lanes() || (int)slots.size() != nov || (int)seqs.size() != nov)
+    throw std::invalid_argument("WideLanes::eval: one slot per evaluated lane");
+  WideEvalModels m{};
+  m.nov = nov;
+  m.plain = server_slot ? 1 : 0;
+  for (int j = 0; j < nov; ++j) {
+    const WideDev& d = solvers_[j]->dev();
+    m.htab[j] = d.htab;
+    m.hmask[j] = d.hmask;
+    m.wloc[j] = d.wloc;
+    m.loss[j] = d.loss;
+    m.slot[j] = reinterpret_cast<char*>(slots[j]);
+    m.seq[j] = seqs[j];
+  }
+  if (server_slot) {
+    m.loss[nov] = nullptr;
+    m.slot[nov] = reinterpret_cast<char*>(server_slot);
+    m.seq[nov] = server_seq;
+  }
+  launch_wide_eval_multi(cfg_.K, cfg_.KP, cfg_.F, indptr, idx, val, y, T, w, m, acc_, ticket_, stream);
+  hip_check(hipGetLastError(), "wide lanes evaluation launch");
 }
 
 }  // namespace psx

@@ -179,6 +179,8 @@ class LocalEngine:
             out = self._run_bsp()
         elif self._async_lanes_ok():
             out = self._run_async_lanes()
+        elif self._wide_lanes_ok():  # the wide model's workers: one solve launch per round
+            out = self._run_wide_lanes()
         # the Python SSP / ASP schedulers: the runs the native lanes loop cannot take --
         # CPU runs, the wide model, fp32 rings, windows over 8,192 rows, shards shorter than
         # a ring.  Their dense-GPU branch stays exercised by tests/test_gpu_engine.py
@@ -649,6 +651,8 @@ class LocalEngine:
             return self._run_bsp_lanes()
         if self._native_bsp_ok():
             return self._run_bsp_native()
+        if self._wide_lanes_ok():
+            return self._run_wide_lanes()
         cfg, srv = self.cfg, self.server
         # bootstrap broadcast, vc 0 (ServerProcessor.java:75-87).  Under BSP every
         # worker pulls the same version right after the server update, and all
@@ -719,6 +723,155 @@ class LocalEngine:
                 "updates_per_s": srv.updates / elapsed if elapsed > 0 else 0.0}
 
     # ------------------------------------------------------------------
+    def _wide_lanes_ok(self) -> bool:
+        """The wide / sparse model with 2..8 in-process GPU workers runs in rounds of
+        ONE launch (csrc/solver/wide_solver.h WideLanes: every worker's persistent
+        solve on an XCD of its own), one evaluation pass and the ordered sparse
+        applies -- instead of ~14 launches per solve on per-worker streams that HIP's
+        4 hardware queues serialise (profiles/r06/README.md section 7).  Runs that
+        need Python between a worker's solves (tracing, injected faults) keep the
+        per-worker schedulers."""
+        c = self.cfg
+        if os.environ.get("PSX_WIDE_LANES", "1") == "0" or not is_gpu(self.device) or self.evalset is None:
+            return False
+        W = [w for w in self.workers if w.k not in self.failed]
+        if not 2 <= len(W) <= 8 or self.tracer.enabled:
+            return False
+        if any(not w.wide or w.solver.dense_delta for w in W):
+            return False
+        if any(c.inject_worker_delay_ms.values()) or c.inject_worker_crash or c.inject_worker_stop:
+            return False
+        return True
+
+    def _wide_lanes_for(self, W):
+        """The WideLanes object over these workers' solvers, every one bound to the
+        server weights (each lane pulls them in-kernel: no per-worker copy of the
+        F*KP-float vector per release)."""
+        for w in W:
+            w.solver._bind(w.ring, self.server.w)
+        key = tuple((w.k, id(w.solver._native)) for w in W)
+        lp = getattr(self, "_wlanes", None)
+        if lp is None or self._wlanes_key != key:
+            lp = _native.hip().WideLanes([w.solver._native for w in W], 0)
+            self._wlanes, self._wlanes_key = lp, key
+        return lp
+
+    def _run_wide_lanes(self) -> dict:
+        """Rounds of the wide model's workers in one process (BSP, SSP and ASP):
+
+        1. every worker ingests its new tuples (WorkerSamplingProcessor.java:50-113);
+        2. ONE launch solves every worker's window from the current server weights,
+           worker l on XCD l (LogisticRegressionTaskSpark.java:142-221);
+        3. ONE evaluation pass: the worker rows of these solves (local models,
+           LogisticRegressionTaskSpark.java:186) and the server row of the previous
+           round (the global model, unchanged until step 4);
+        4. the server applies the sparse pushes one after the other, worker 0's last
+           (ServerProcessor.java:143-151: each delta on arrival; the server row,
+           ServerProcessor.java:154-165, follows worker 0's delta and is the model the
+           next round's pass evaluates), and the tracker records the deltas.
+
+        Under SSP / ASP every worker is released on its own delta; the round only
+        fixes one interleaving of arrivals the reference could produce (deltas that
+        arrive together, applied in order).  A worker re-pulls at the next launch."""
+        cfg, srv = self.cfg, self.server
+        W = [w for w in self.workers if w.k not in self.failed]
+        L = len(W)
+        lp = self._wide_lanes_for(W)
+        ev = self.evalset
+        ds = ev.ds
+        stream = stream_handle(self.device)
+        bsp = cfg.consistency_model == 0
+        lr = float(cfg.lr)
+        order = list(range(1, L)) + [0]  # worker 0 (the server-row worker) last
+        row_w = min(range(L), key=lambda i: W[i].k)  # the lowest live worker logs the server rows
+        if row_w != 0:
+            order = [i for i in range(L) if i != row_w] + [row_w]
+        native = self.log.native
+        r0 = r = self.rounds
+        if not bsp:
+            for w in W:  # bootstrap: the current version to everybody (as _run_async_events)
+                u = int(srv.tracker.clock(w.k))
+                if u > 0:
+                    srv.tracker.sent(w.k, u)
+                w.vc = u
+        else:
+            for w in W:
+                w.vc = r
+        for w in W:
+            w.w = srv.w
+        pending_srv = None  # (vc) the server row of the last round, evaluated by the next pass
+        t_start = time.time()
+        exhausted_since = None
+        try:
+            while not self._stop(r - r0, t_start, exhausted_since):
+                for w in W:
+                    w.ingest()
+                if all(w.source.exhausted for w in W):
+                    exhausted_since = exhausted_since or time.time()
+                if not all(w.ready() for w in W):
+                    if all(w.window.size <= 0 and w.source.exhausted for w in W):
+                        break
+                    time.sleep(0.0005)
+                    continue
+                Bs, starts, seen = [], [], []
+                for w in W:
+                    Bs.append(int(w.window.size))
+                    starts.append(int(w.window.start))
+                    w._seen_at_solve = w.tuples_seen
+                    seen.append(w._seen_at_solve)
+                lp.run(Bs, starts, stream)
+                # worker rows of this round + the server row of the previous one, one pass
+                slots, seqs, subs = [], [], []
+                for i, w in enumerate(W):
+                    s_, q_, a_ = native.acquire()
+                    slots.append(a_)
+                    seqs.append(q_)
+                    subs.append((s_, q_, 0, w.k, w.vc, seen[i]))
+                ss = sq = 0
+                if pending_srv is not None:
+                    s_, sq, ss = native.acquire()
+                    subs.insert(0, (s_, sq, 1, -1, pending_srv, 0))
+                lp.eval(ds.indptr.data_ptr(), ds.idx.data_ptr(), ds.val.data_ptr(), ds.y.data_ptr(), ev.T,
+                        srv.w.data_ptr(), L, slots, seqs, ss, sq, stream)
+                for s_, q_, kind, part, vc, ns in subs:
+                    native.submit(s_, q_, kind, -1, part, int(vc), int(ns))
+                lp.apply(srv.w.data_ptr(), lr, order, stream)
+                srv.updates += L
+                if bsp:
+                    for w in W:
+                        srv.tracker.received(w.k, r)
+                    for w in W:
+                        srv.tracker.sent(w.k, r + 1)
+                        w.vc = r + 1
+                    pending_srv = r
+                else:
+                    rel = {}
+                    for i in order:
+                        v = W[i].vc
+                        for j, u in srv.tracker.on_delta(W[i].k, v):
+                            rel[j] = u
+                        if i == row_w:
+                            pending_srv = v
+                    if len(rel) != L:
+                        raise RuntimeError(f"wide lanes: the tracker released {sorted(rel)} of {L} workers after a round")
+                    for w in W:
+                        w.vc = rel[w.k]
+                for w in W:
+                    w.iters += 1
+                r += 1
+                maybe_checkpoint(cfg, srv, srv.updates if not bsp else r, W)
+            if pending_srv is not None:  # the last round's server row
+                s_, sq, ss = native.acquire()
+                lp.eval(ds.indptr.data_ptr(), ds.idx.data_ptr(), ds.val.data_ptr(), ds.y.data_ptr(), ev.T,
+                        srv.w.data_ptr(), 0, [], [], ss, sq, stream)
+                native.submit(s_, sq, 1, -1, -1, int(pending_srv), 0)
+        finally:
+            torch.cuda.synchronize(self.device)
+        self.rounds = r if bsp else int(srv.tracker.min_clock())
+        elapsed = time.time() - t_start
+        return {"rounds": self.rounds, "updates": srv.updates, "elapsed_s": elapsed,
+                "updates_per_s": (r - r0) * L / elapsed if elapsed > 0 else 0.0, "wide_lanes": L}
+
     def _event_scheduler(self) -> bool:
         """SSP/ASP in one process: event polling (True) or a thread per worker."""
         mode = self.cfg.async_scheduler

@@ -329,6 +329,72 @@ def test_engine_wide_gpu(cuda, c, N):
     del cfg
 
 
+def _wide_lanes_run(dev, N, c, iters=8, env=None):
+    import os
+
+    from psx.runtime.engine import LocalEngine
+
+    ds, spec = _problem(F=2000, rows=1600)
+    te, _ = _problem(F=2000, rows=300, seed=7)
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        eng = LocalEngine(_wide_cfg(N, c, iters), dev, train=ds, test=te)
+        out = eng.run(close_log=False)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    book = eng.log.book
+    eng.log.close()
+    return eng, out, book, te
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [0, -1, 2])
+def test_gpu_wide_lanes_match_cpu_rounds(cuda, c):
+    """Several wide workers in ONE solve launch per round (WideLanes, one XCD each):
+    every round's solves start from the same server weights and the pushes are applied
+    in order, so BSP, SSP and ASP all land on the weights of the CPU engine's BSP rounds
+    (whose workers solve with the float64-oracle path, ops/sparse.py _run_cpu)."""
+    N, iters = 4, 8
+    eng, out, book, te = _wide_lanes_run(cuda, N, c, iters)
+    assert out.get("wide_lanes") == N, out  # the one-launch path ran
+    assert out["updates"] == N * iters
+    assert len(book.worker) == N * iters and len(book.server) == iters
+    assert all(math.isfinite(r[3]) and r[3] > 0 for r in book.worker), "worker rows carry the solve loss"
+    ref, _, _, _ = _wide_lanes_run("cpu", N, 0, iters)
+    wc, wg = ref.server.w.cpu(), eng.server.w.cpu()
+    assert (wc - wg).abs().max().item() < 5e-3 * wc.abs().max().item()
+    # the last server row (the flush pass) evaluates the final global model
+    conf = WideEvalSet(ref.spec, te, "cpu").confusion_cpu(wg).view(16, 16)[:6, :6].double()
+    assert abs(book.server[-1][3] - float(conf.trace() / conf.sum())) < 2e-3
+
+
+@pytest.mark.gpu
+def test_gpu_wide_lanes_rows_equal_separate_passes(cuda):
+    """The multi-model evaluation pass: every worker row equals the worker's local model
+    evaluated on its own (the overlay pass of test_gpu_wide_eval_overlay)."""
+    from psx.utils.logsink import LogSink
+
+    N = 3
+    eng, out, book, te = _wide_lanes_run(cuda, N, -1, 1)
+    assert out.get("wide_lanes") == N
+    # one round from the initial weights: rebuild them and evaluate each local model alone
+    w0 = eng.spec.init("random", seed=eng.cfg.seed, device=cuda)
+    ev = WideEvalSet(eng.spec, te, cuda)
+    log = LogSink(eng.spec.eval_classes, cuda)
+    for w in eng.workers:
+        log.worker_eval(ev, w.solver, w0, EvalScratch(cuda), w.solver.loss, w.k, 0, 0)
+    alone = log.book.worker
+    log.close()
+    rows = sorted(book.worker, key=lambda r: r[1])
+    for a, b in zip(rows, sorted(alone, key=lambda r: r[1])):
+        assert a[1] == b[1] and a[3:6] == b[3:6], (a, b)  # partition, loss, F1, accuracy
+
+
 def test_cli_libsvm_inprocess(tmp_path):
     """ServerAppRunner on LIBSVM files picks the wide model (reference CLI flags + new ones)."""
     import os

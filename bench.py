@@ -348,6 +348,12 @@ def main(argv=None):
     out.update(summarize(eng.log.book))
     ups = (eng.server.updates - u0) / dt
     res = describe(a, 1, cfg, ups, dt, out, eng.workers[0].tuples_seen)
+    if out.get("wide_lanes"):  # the wide model's workers: every solve of a round in one launch
+        nl = int(out["wide_lanes"])
+        mode = res["config"]["parallelism"].split()[0]
+        res["config"]["parallelism"] = (f"{mode} w{nl} (server colocated, {nl} workers/GPU: one solve launch per "
+                                        f"round, {max(1, 8 // nl)} XCD(s) per worker)")
+        res["config"]["workers_per_gpu"] = nl
     res["native"] = {"lanes": out.get("lanes"), "hand_off_scope": out.get("hand_off_scope"),
                      "host_us_per_round": round(getattr(eng, "native_host_us_per_round", 0.0), 2),
                      "host_phases_us": getattr(eng, "native_host_phases_us", None)}

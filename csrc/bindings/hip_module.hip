@@ -515,6 +515,25 @@ PYBIND11_MODULE(_psx_hip, m) {
       .def_property_readonly("lanes", &WideLanes::lanes)
       .def_property_readonly("launches", &WideLanes::launches);
 
+  // jobs: (src_first, src_step, n, dst_first, ridx, rval, rnnz, ry, trunc) per ring
+  m.def("sparse_ring_ingest_many", [](uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y,
+                                      const std::vector<std::vector<int64_t>>& jobs, int cap, int NZ,
+                                      uintptr_t stream) {
+    SparseIngestJobs a{};
+    if (jobs.size() > (size_t)kMaxIngestJobs) throw std::invalid_argument("sparse_ring_ingest_many: <= 16 jobs");
+    a.njobs = (int)jobs.size();
+    a.cap = cap;
+    a.NZ = NZ;
+    for (size_t q = 0; q < jobs.size(); ++q) {
+      const auto& v = jobs[q];
+      if (v.size() != 9) throw std::invalid_argument("sparse_ring_ingest_many: 9 fields per job");
+      a.job[q] = SparseIngestJob{v[0], v[1], v[2], v[3], P<int32_t>((uintptr_t)v[4]), P<uint16_t>((uintptr_t)v[5]),
+                                 P<int32_t>((uintptr_t)v[6]), P<int32_t>((uintptr_t)v[7]), P<int>((uintptr_t)v[8])};
+    }
+    launch_sparse_ring_ingest_many(P<const int64_t>(indptr), P<const int32_t>(idx), P<const uint16_t>(val),
+                                   P<const int32_t>(y), a, S(stream));
+    hip_check(hipGetLastError(), "sparse_ring_ingest_many launch");
+  });
   m.def("sparse_ring_ingest", [](uintptr_t indptr, uintptr_t idx, uintptr_t val, uintptr_t y, int64_t src_first,
                                  int64_t src_step, int64_t n, uintptr_t ridx, uintptr_t rval, uintptr_t rnnz,
                                  uintptr_t ry, int64_t dst_first, int cap, int NZ, uintptr_t trunc, uintptr_t stream) {

@@ -170,23 +170,31 @@ size_t wide_persist_lds(const WideCfg& c, const WideDev& d);
 
 // ---------------------------------------------------------------------------
 // Wide lanes: the local solves of up to kWideMaxLanes in-process workers in ONE
-// launch, lane l on XCD xcd0 + l with kWideLaneWg co-resident workgroups (the
-// persistent solve's phases, its grid barriers inside the XCD's L2).  Workgroups
-// claim their lane from their XCC_ID (lanes_kernels.hip's claim), so the dispatch
-// order of the grid does not matter.  devs: [L] WideDev table in device memory (each
+// launch, lane l on the `per` XCDs xcd0 + l * per .. with per * kWideLaneWg
+// co-resident workgroups (the persistent solve's phases; per = 8 / L, so fewer
+// workers still fill the GPU).  Workgroups claim their lane from their XCC_ID
+// (lanes_kernels.hip's claim), so the dispatch order of the grid does not matter.  devs: [L] WideDev table in device memory (each
 // lane's own workspace and ring; w_old = the server weights every lane pulled).
 constexpr int kWideMaxLanes = 8;
 constexpr int kWideLaneWg = 32;
 struct WideLanesArgs {
   int L;
   int xcd0;
-  unsigned* claim;  // [2][16] per-XCD slot counters; launch parity cpar, the other one cleared
+  int per;          // XCDs per lane (L * per <= 8 - xcd0)
+  int gpx;          // workgroups per XCD and lane: 32 x the CU's co-resident lane workgroups (1 or 2)
+  unsigned* claim;  // [2][16] per-lane slot counters; launch parity cpar, the other one cleared
   int cpar;
   int B[kWideMaxLanes];
   int start[kWideMaxLanes];
 };
 void wide_launch_lanes(const WideCfg& c, const WideDev* devs, const WideLanesArgs& a, size_t lds, hipStream_t s);
-int wide_lanes_grid();
+int wide_lanes_grid(int gpx);
+// co-resident lane workgroups per CU of the lanes kernel for this configuration (LDS,
+// registers), capped at 2 -- a lane may only count on workgroups that ARE co-resident
+int wide_lanes_per_cu(const WideCfg& c, size_t lds);
+// bm [L][nw] (nw = (F + 31) / 32 words, zeroed by the caller): bit f of lane l set for
+// every feature of lane l's last window (devs[l].uniq[0 .. U))
+void wide_lanes_bitmap(const WideDev* devs, int L, unsigned* bm, int64_t nw, hipStream_t s);
 
 // Test-set evaluation of up to kWideMaxEval models of the wide model in ONE pass:
 // model m < nov = the common weights w overlaid with lane m's window solution
@@ -197,6 +205,10 @@ constexpr int kWideMaxEval = kWideMaxLanes + 1;
 struct WideEvalModels {
   int nov;    // overlay models
   int plain;  // 1: model nov is w itself
+  // optional [nov][nw] bitmaps of the overlays' window features (wide_lanes_bitmap): a
+  // table is probed only for a feature whose bit is set (null: always probed)
+  const unsigned* bm;
+  int64_t nw;
   const int2* htab[kWideMaxLanes];
   unsigned hmask[kWideMaxLanes];
   const float* wloc[kWideMaxLanes];
@@ -216,6 +228,24 @@ void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const 
                                int64_t src_first, int64_t src_step, int64_t n, int32_t* ridx, uint16_t* rval,
                                int32_t* rnnz, int32_t* ry, int64_t dst_first, int cap, int NZ, int* trunc,
                                hipStream_t s);
+
+// The same for several rings of one geometry (cap, NZ) fed from one dataset, in ONE
+// launch: job q = rows src_first + i*src_step (i < n) -> its ring's slots (dst_first + i) % cap.
+constexpr int kMaxIngestJobs = 16;
+struct SparseIngestJob {
+  int64_t src_first, src_step, n, dst_first;
+  int32_t* ridx;
+  uint16_t* rval;
+  int32_t* rnnz;
+  int32_t* ry;
+  int* trunc;
+};
+struct SparseIngestJobs {
+  int njobs, cap, NZ;
+  SparseIngestJob job[kMaxIngestJobs];
+};
+void launch_sparse_ring_ingest_many(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y,
+                                    const SparseIngestJobs& a, hipStream_t s);
 
 // Test-set evaluation of a dense wide model (optionally overlaid with a
 // worker's local solution: features the solver's table htab maps to a local id

@@ -790,12 +790,16 @@ __global__ __launch_bounds__(256) void wide_finalize_kernel(WideCfg c, WideDev d
 // generation).  On MI355X a kernel boundary of the launch chain costs ~4.5-5 us
 // of device time even for an empty phase (profiles/r03_v4), a barrier ~2-3 us.
 // phases: bit 0 = begin + plan, bit 1 = assign .. finalize.
-__device__ __forceinline__ void wide_gen_barrier(unsigned* bar, unsigned G, unsigned* err) {
+// xl (XCD-local): every party runs on ONE XCD and shares its L2 -- the drained stores
+// have reached that L2 through the write-through L1, so the release (an L2 write-back
+// of the XCD's dirty lines, 1.7-6.5 us, MI355X_MICROARCH.md) is skipped; the acquire
+// (this CU's L1 invalidated) stays.
+__device__ __forceinline__ void wide_gen_barrier(unsigned* bar, unsigned G, unsigned* err, bool xl = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned g = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (!xl) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (old == G - 1) {
@@ -823,35 +827,41 @@ __device__ __forceinline__ void wide_gen_barrier(unsigned* bar, unsigned G, unsi
 template <int KP, int NQ>
 __device__ __forceinline__ void wide_persist_body(const WideCfg& c, const WideDev& d, int B, int start, int phases,
                                                   int G, int blk, int* pl_lds, WideFwdShared& fsh,
-                                                  WideDotsShared& dsh, int& phase_s) {
+                                                  WideDotsShared& dsh, int& phase_s, bool xl = false) {
   const int ngr = (c.cap + d.RB - 1) / d.RB;
   unsigned* err = d.cnt + 3;
+  // PSX_WIDE_STAMPS: [7] the body's entry, [slot * 8 + 6] slot's forward begins, [15] finalize
+  // (next to wide_dots_body's [slot * 8 + 0..5]; nslots >= 2 in every configuration)
+  const bool st = d.dbg && blk == 0 && threadIdx.x == 0;
+  if (st) d.dbg[7] = (long long)__builtin_amdgcn_s_memrealtime();
   if (phases & 1) {
     wide_begin_body(d, B, start, blk, G);
-    wide_gen_barrier(d.pbar, G, err);
+    wide_gen_barrier(d.pbar, G, err, xl);
     for (int grp = blk; grp < ngr; grp += G) wide_plan_body(c, d, grp, pl_lds);
-    wide_gen_barrier(d.pbar, G, err);
+    wide_gen_barrier(d.pbar, G, err, xl);
   }
   if (!(phases & 2)) return;
   wide_assign_body(c, d, blk, G);
-  wide_gen_barrier(d.pbar, G, err);
+  wide_gen_barrier(d.pbar, G, err, xl);
   for (int grp = blk; grp < ngr; grp += G) wide_stats_body(c, d, grp, pl_lds);
-  wide_gen_barrier(d.pbar, G, err);
+  wide_gen_barrier(d.pbar, G, err, xl);
   wide_prep_body(c, d, blk, G);
-  wide_gen_barrier(d.pbar, G, err);
+  wide_gen_barrier(d.pbar, G, err, xl);
   for (int slot = 0; slot < c.sc.nslots; ++slot) {
     if (threadIdx.x == 0)
       phase_s = __hip_atomic_load(&d.ctrl->phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (phase_s == kPhDone) break;  // uniform: every workgroup read the word after the last barrier
     const int Bw = d.prm->B;
+    if (st) d.dbg[slot * 8 + 6] = (long long)__builtin_amdgcn_s_memrealtime();
     for (int grp = blk; grp * d.RB < Bw; grp += G) wide_fwdbwd_body<KP, NQ>(c, d, slot, grp, (float*)pl_lds, fsh);
-    wide_gen_barrier(d.pbar, G, err);
+    wide_gen_barrier(d.pbar, G, err, xl);
     wide_dots_body(c, d, slot, blk, G, dsh);
-    wide_gen_barrier(d.pbar, G, err);
+    wide_gen_barrier(d.pbar, G, err, xl);
     wide_apply_body(c, d, slot, blk, G);
-    wide_gen_barrier(d.pbar, G, err);
+    wide_gen_barrier(d.pbar, G, err, xl);
   }
+  if (st && c.sc.nslots >= 2) d.dbg[15] = (long long)__builtin_amdgcn_s_memrealtime();
   wide_finalize_body(c, d, blk, G);
 }
 
@@ -887,18 +897,23 @@ __global__ __launch_bounds__(512) void wide_lanes_kernel(WideCfg c, const WideDe
       __hip_atomic_store(a.claim + 16 * (a.cpar ^ 1) + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u);  // HW_REG_XCC_ID
     const int lx = xcc - a.xcd0;
+    const int G = a.gpx * a.per;
     int r = -1;
-    if (lx >= 0 && lx < a.L) {
-      const unsigned k = __hip_atomic_fetch_add(a.claim + 16 * a.cpar + lx, 1u, __ATOMIC_RELAXED,
+    if (lx >= 0 && lx < a.L * a.per) {
+      const int lane = lx / a.per;
+      const unsigned k = __hip_atomic_fetch_add(a.claim + 16 * a.cpar + lane, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-      if (k < (unsigned)kWideLaneWg) r = lx * kWideLaneWg + (int)k;
+      if (k < (unsigned)G) r = lane * G + (int)k;
     }
     role_s = r;
   }
   __syncthreads();
   const int r = __builtin_amdgcn_readfirstlane(role_s);
   if (r < 0) return;
-  const int l = r / kWideLaneWg, blk = r - l * kWideLaneWg;
+  // (a lane over several XCDs: its barriers and tickets are agent-scope atomics and its
+  // hand-offs agent-scope fences, coherent across the XCDs' L2s)
+  const int G = a.gpx * a.per;
+  const int l = r / G, blk = r - l * G;
   // the lane's window: constant-index reads of the kernel argument (a runtime index
   // would copy the argument block into scratch, lanes_body.h pick())
   int B = a.B[0], start = a.start[0];
@@ -908,7 +923,7 @@ __global__ __launch_bounds__(512) void wide_lanes_kernel(WideCfg c, const WideDe
       B = a.B[i];
       start = a.start[i];
     }
-  wide_persist_body<KP, NQ>(c, devs[l], B, start, 3, kWideLaneWg, blk, pl_lds, fsh, dsh, phase_s);
+  wide_persist_body<KP, NQ>(c, devs[l], B, start, 3, G, blk, pl_lds, fsh, dsh, phase_s, a.per == 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1073,7 +1088,50 @@ void wide_launch_persist(const WideCfg& c, const WideDev& d, int B, int start, i
 
 // 8 XCDs x 32 lanes' workgroups, twice over: an XCD the dispatcher deals fewer than
 // 32 of the first 256 still gets its lane's 32 (the surplus leaves at once)
-int wide_lanes_grid() { return 2 * 8 * kWideLaneWg; }
+int wide_lanes_grid(int gpx) { return 2 * 8 * gpx; }
+
+__global__ __launch_bounds__(256) void wide_lanes_bitmap_kernel(const WideDev* __restrict__ devs, int L, unsigned* bm,
+                                                                int64_t nw) {
+  for (int l = 0; l < L; ++l) {
+    const WideDev& d = devs[l];
+    const unsigned U = d.cnt[0];
+    unsigned* b = bm + (int64_t)l * nw;
+    for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+      const unsigned f = (unsigned)d.uniq[i];
+      atomicOr(b + (f >> 5), 1u << (f & 31));
+    }
+  }
+}
+
+void wide_lanes_bitmap(const WideDev* devs, int L, unsigned* bm, int64_t nw, hipStream_t s) {
+  wide_lanes_bitmap_kernel<<<256, 256, 0, s>>>(devs, L, bm, nw);
+}
+
+template <int KP, int NQ>
+static int lanes_per_cu_kp(size_t lds) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)wide_lanes_kernel<KP, NQ>, 512, lds) != hipSuccess)
+    return 1;
+  return n >= 2 ? 2 : 1;
+}
+
+int wide_lanes_per_cu(const WideCfg& c, size_t lds) {
+  const int nq = (c.NZ + 63) / 64;
+#define PSX_OCC(KV)                                                                                          \
+  case KV:                                                                                                   \
+    return nq <= 1 ? lanes_per_cu_kp<KV, 1>(lds)                                                             \
+                   : (nq <= 2 ? lanes_per_cu_kp<KV, 2>(lds)                                                  \
+                              : (nq <= 4 ? lanes_per_cu_kp<KV, 4>(lds) : lanes_per_cu_kp<KV, 8>(lds)));
+  switch (c.KP) {
+    PSX_OCC(1)
+    PSX_OCC(2)
+    PSX_OCC(4)
+    PSX_OCC(8)
+    default:
+      PSX_OCC(16)
+  }
+#undef PSX_OCC
+}
 
 template <int KP, int NQ>
 static void set_lanes_attr() {
@@ -1088,7 +1146,7 @@ static void launch_lanes_kp(const WideCfg& c, const WideDev* devs, const WideLan
                                 set_lanes_attr<KP, 8>(), true);
   (void)prepared;
   const int nq = (c.NZ + 63) / 64;
-  const int G = wide_lanes_grid();
+  const int G = wide_lanes_grid(a.gpx);
   if (nq <= 1)
     wide_lanes_kernel<KP, 1><<<G, 512, lds, s>>>(c, devs, a);
   else if (nq <= 2)
@@ -1150,6 +1208,50 @@ void launch_sparse_ring_ingest(const int64_t* indptr, const int32_t* idx, const 
   if (n <= 0) return;
   sparse_ring_ingest_kernel<<<grid_for(n * 64, 2048), 256, 0, s>>>(indptr, idx, val, y, src_first, src_step, n, ridx,
                                                                    rval, rnnz, ry, dst_first, cap, NZ, trunc);
+}
+
+// Several rings' deliveries from one dataset in one launch (the wide lanes' ingest:
+// blockIdx.y = job).  A job's fields are read with constant indices (unrolled selects
+// on the uniform job id): a run-time index into the argument block would copy it into
+// scratch (lanes_body.h pick()).
+__global__ __launch_bounds__(256) void sparse_ring_ingest_many_kernel(const int64_t* __restrict__ indptr,
+                                                                      const int32_t* __restrict__ idx,
+                                                                      const uint16_t* __restrict__ val,
+                                                                      const int32_t* __restrict__ y,
+                                                                      SparseIngestJobs a) {
+  const int jy = (int)blockIdx.y;
+  SparseIngestJob j = a.job[0];
+#pragma unroll
+  for (int q = 1; q < kMaxIngestJobs; ++q)
+    if (q == jy) j = a.job[q];
+  const int lane = threadIdx.x & 63;
+  const int cap = a.cap, NZ = a.NZ;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < j.n; i += (int64_t)gridDim.x * 4) {
+    const int64_t sr = j.src_first + i * j.src_step;
+    const int64_t dr = (j.dst_first + i) % cap;
+    const int64_t a0 = indptr[sr], b0 = indptr[sr + 1];
+    const int64_t len = b0 - a0;
+    const int nz = len < NZ ? (int)len : NZ;
+    for (int e = lane; e < nz; e += 64) {
+      j.ridx[dr * NZ + e] = idx[a0 + e];
+      j.rval[dr * NZ + e] = val[a0 + e];
+    }
+    if (lane == 0) {
+      j.rnnz[dr] = nz;
+      j.ry[dr] = y[sr];
+      if (len > NZ && j.trunc) atomicAdd(j.trunc, 1);
+    }
+  }
+}
+
+void launch_sparse_ring_ingest_many(const int64_t* indptr, const int32_t* idx, const uint16_t* val, const int32_t* y,
+                                    const SparseIngestJobs& a, hipStream_t s) {
+  if (a.njobs <= 0) return;
+  int64_t nmax = 0;
+  for (int q = 0; q < a.njobs; ++q) nmax = a.job[q].n > nmax ? a.job[q].n : nmax;
+  if (nmax <= 0) return;
+  const dim3 grid((unsigned)grid_for(nmax * 64, 512), (unsigned)a.njobs);
+  sparse_ring_ingest_many_kernel<<<grid, 256, 0, s>>>(indptr, idx, val, y, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -1346,9 +1448,11 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
 }
 
 // wide_eval_multi_kernel: see launch_wide_eval_multi.  16 lanes per row (4 rows per
-// wave), each lane one non-zero at a time: the row of w gathered once, every
-// overlay's table probed for the feature (independent loads, in flight together),
-// the lane's local coefficients where it maps the feature.
+// wave), two non-zeros per lane in flight: the row of w gathered once per non-zero,
+// every overlay's table probed for the feature at its home slot (independent loads, in
+// flight together; a collision walks on), the lane's local coefficients where it maps
+// the feature.  Every model loop is unrolled over kWideMaxEval with run-time guards, so
+// the margins stay in registers (a runtime model index would put them in scratch).
 template <int KP>
 __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, const int64_t* __restrict__ indptr,
                                                               const int32_t* __restrict__ idx,
@@ -1356,10 +1460,12 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
                                                               const int32_t* __restrict__ y, int T,
                                                               const float* __restrict__ w, WideEvalModels m, int* acc,
                                                               unsigned* ticket) {
+  constexpr int NE = 2;  // non-zeros per lane in flight
   __shared__ int cl[kWideMaxEval][256];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int M = m.nov + m.plain;
+  const int nov = m.nov, M = m.nov + m.plain;
+#pragma unroll
   for (int j = 0; j < kWideMaxEval; ++j) cl[j][tid] = 0;
   __syncthreads();
   for (int64_t r0 = (int64_t)blockIdx.x * 16; r0 < T; r0 += (int64_t)gridDim.x * 16) {
@@ -1372,44 +1478,85 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
       for (int k = 0; k < KP; ++k) z[j][k] = 0.f;
     if (valid) {
       const int64_t a0 = indptr[row], b0 = indptr[row + 1];
-      for (int64_t e = a0 + (lane & 15); e < b0; e += 16) {
-        const int f = idx[e];
-        const float v = bf2f(val[e]);
-        float wv[KP];
-        ldk<KP>(w + (int64_t)f * KP, wv);
-        int li[kWideMaxLanes];
+      for (int64_t e0 = a0 + (lane & 15); e0 < b0; e0 += 16 * NE) {
+        int f[NE];
+        float v[NE];
 #pragma unroll
-        for (int j = 0; j < kWideMaxLanes; ++j) li[j] = j < m.nov ? wide_find(m.htab[j], m.hmask[j], f) : -1;
+        for (int u = 0; u < NE; ++u) {
+          const int64_t e = e0 + 16 * u;
+          const bool ok = e < b0;
+          f[u] = ok ? idx[e] : -1;
+          v[u] = ok ? bf2f(val[e]) : 0.f;
+        }
+        float wv[NE][KP];
+        int2 pr[NE][kWideMaxLanes];
 #pragma unroll
-        for (int j = 0; j < kWideMaxLanes; ++j) {
-          if (j >= m.nov) break;
-          float ov[KP];
-          if (li[j] >= 0) {
-            ldk<KP>(m.wloc[j] + KP + (int64_t)li[j] * KP, ov);
+        for (int u = 0; u < NE; ++u) {
+          if (f[u] >= 0) {
+            ldk<KP>(w + (int64_t)f[u] * KP, wv[u]);
           } else {
 #pragma unroll
-            for (int k = 0; k < KP; ++k) ov[k] = wv[k];
+            for (int k = 0; k < KP; ++k) wv[u][k] = 0.f;
+          }
+          bool in[kWideMaxLanes];  // the feature is in lane j's window (bitmap; no bitmap: maybe)
+#pragma unroll
+          for (int j = 0; j < kWideMaxLanes; ++j)
+            in[j] = j < nov && f[u] >= 0 &&
+                    (m.bm == nullptr || ((m.bm[(int64_t)j * m.nw + (f[u] >> 5)] >> (f[u] & 31)) & 1u));
+#pragma unroll
+          for (int j = 0; j < kWideMaxLanes; ++j)
+            pr[u][j] = in[j] ? m.htab[j][wide_gslot(f[u], m.hmask[j])] : make_int2(-1, -1);
+        }
+#pragma unroll
+        for (int u = 0; u < NE; ++u) {
+#pragma unroll
+          for (int j = 0; j < kWideMaxLanes; ++j) {
+            if (j < nov) {
+              int li = -1;
+              if (f[u] >= 0 && pr[u][j].x != -1) {
+                if (pr[u][j].x == f[u]) {
+                  li = pr[u][j].y;
+                } else if (pr[u][j].x != -1) {  // collision: walk on from the home slot
+                  unsigned h = wide_gslot(f[u], m.hmask[j]);
+                  while (true) {
+                    h = (h + 1) & m.hmask[j];
+                    const int2 e = m.htab[j][h];
+                    if (e.x == f[u]) {
+                      li = e.y;
+                      break;
+                    }
+                    if (e.x == -1) break;
+                  }
+                }
+              }
+              if (li >= 0) {
+                float ov[KP];
+                ldk<KP>(m.wloc[j] + KP + (int64_t)li * KP, ov);
+#pragma unroll
+                for (int k = 0; k < KP; ++k) z[j][k] += v[u] * ov[k];
+              } else {
+#pragma unroll
+                for (int k = 0; k < KP; ++k) z[j][k] += v[u] * wv[u][k];
+              }
+            }
           }
 #pragma unroll
-          for (int k = 0; k < KP; ++k) z[j][k] += v * ov[k];
-        }
-        if (m.plain) {
-#pragma unroll
           for (int j = 0; j < kWideMaxEval; ++j)
-            if (j == m.nov) {
+            if (m.plain && j == nov) {
 #pragma unroll
-              for (int k = 0; k < KP; ++k) z[j][k] += v * wv[k];
+              for (int k = 0; k < KP; ++k) z[j][k] += v[u] * wv[u][k];
             }
         }
       }
     }
 #pragma unroll
     for (int j = 0; j < kWideMaxEval; ++j) {
-      if (j >= M) break;
+      if (j < M) {
 #pragma unroll
-      for (int k = 0; k < KP; ++k)
+        for (int k = 0; k < KP; ++k)
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) z[j][k] += __shfl_xor(z[j][k], o, 64);
+          for (int o = 1; o < 16; o <<= 1) z[j][k] += __shfl_xor(z[j][k], o, 64);
+      }
     }
     if ((lane & 15) == 0 && valid) {
       int yl = y[row];
@@ -1417,24 +1564,25 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
       yl = yl < 0 ? 0 : (yl > 15 ? 15 : yl);
 #pragma unroll
       for (int j = 0; j < kWideMaxEval; ++j) {
-        if (j >= M) break;
-        float bv[KP];
-        const bool ovl = j < m.nov;
-        const float* bsrc = w + F * KP;  // the intercepts: the overlay's own, or w's
+        if (j < M) {
+          // the intercepts: the overlay's own, or w's
+          const float* bsrc = (j < kWideMaxLanes && j < nov) ? m.wloc[j < kWideMaxLanes ? j : 0] : w + F * KP;
+          float bv[KP];
+          ldk<KP>(bsrc, bv);
 #pragma unroll
-        for (int i = 0; i < kWideMaxLanes; ++i)
-          if (i == j && ovl) bsrc = m.wloc[i];
-        ldk<KP>(bsrc, bv);
-#pragma unroll
-        for (int k = 0; k < KP; ++k) z[j][k] += bv[k];
-        atomicAdd(&cl[j][yl * 16 + wide_argmax<KP>(K, z[j])], 1);
+          for (int k = 0; k < KP; ++k) z[j][k] += bv[k];
+          atomicAdd(&cl[j][yl * 16 + wide_argmax<KP>(K, z[j])], 1);
+        }
       }
     }
   }
   __syncthreads();
-  for (int j = 0; j < M; ++j) {
-    const int v = cl[j][tid];
-    if (v) atomicAdd(acc + (j * 256 + tid) * kAccStride, v);
+#pragma unroll
+  for (int j = 0; j < kWideMaxEval; ++j) {
+    if (j < M) {
+      const int v = cl[j][tid];
+      if (v) atomicAdd(acc + (j * 256 + tid) * kAccStride, v);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1446,25 +1594,25 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
   // host slots, then each slot's sequence number
 #pragma unroll
   for (int j = 0; j < kWideMaxEval; ++j) {
-    if (j >= M) break;
-    char* slot = m.slot[j];
-    const float* loss = m.loss[j];
-    const int tot = __hip_atomic_exchange(acc + (j * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (tid == 0)
-      __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (j < M) {
+      char* slot = m.slot[j];
+      const float* loss = m.loss[j];
+      const int tot = __hip_atomic_exchange(acc + (j * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tid == 0)
+        __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int j = 0; j < kWideMaxEval; ++j) {
-      if (j >= M) break;
-      __hip_atomic_store((unsigned long long*)(m.slot[j] + 1032), m.seq[j], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    for (int j = 0; j < kWideMaxEval; ++j)
+      if (j < M)
+        __hip_atomic_store((unsigned long long*)(m.slot[j] + 1032), m.seq[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

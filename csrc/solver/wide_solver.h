@@ -133,6 +133,9 @@ class WideLanes {
   unsigned* claim_ = nullptr; // [2][16]
   int* acc_ = nullptr;        // [kWideMaxEval][256] cells at stride kAccStride
   unsigned* ticket_ = nullptr;
+  unsigned* bm_ = nullptr;    // [L][nw_] window-feature bitmaps of the evaluation pass (null: off)
+  int64_t nw_ = 0;
+  int gpx_ = 32;              // lane workgroups per XCD (32 x co-resident lane workgroups per CU)
   int64_t launches_ = 0;
 };
 

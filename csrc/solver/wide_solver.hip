@@ -1,5 +1,6 @@
 #include "wide_solver.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -288,6 +289,21 @@ WideLanes::WideLanes(const std::vector<WideSolver*>& solvers, int xcd0) : solver
   hip_check(hipMemset(acc_, 0, acc_bytes), "hipMemset(eval accumulators)");
   hip_check(hipMalloc(&ticket_, 64), "hipMalloc(ticket)");
   hip_check(hipMemset(ticket_, 0, 64), "hipMemset(ticket)");
+  // two lane workgroups per CU when both fit (LDS, registers): twice the workgroups per
+  // lane on the same XCD -- the solve's row groups and vector phases are latency-bound
+  gpx_ = 32 * wide_lanes_per_cu(cfg_, lds_);
+  if (const char* e = std::getenv("PSX_WIDE_LANE_PER_CU")) {
+    const int v = std::atoi(e);
+    if (v == 1 || v == 2) gpx_ = 32 * std::min(v, gpx_ / 32);
+  }
+  // the evaluation pass's bitmaps of the lanes' window features (up to 64 MB)
+  nw_ = (cfg_.F + 31) / 32;
+  const size_t bm_bytes = (size_t)L * (size_t)nw_ * 4;
+  if (bm_bytes <= ((size_t)64 << 20) && std::getenv("PSX_WIDE_EVAL_BITMAP") == nullptr) {
+    hip_check(hipMalloc(&bm_, bm_bytes), "hipMalloc(eval bitmaps)");
+  } else if (const char* e = std::getenv("PSX_WIDE_EVAL_BITMAP"); e && std::atoi(e) != 0 && bm_bytes <= ((size_t)64 << 20)) {
+    hip_check(hipMalloc(&bm_, bm_bytes), "hipMalloc(eval bitmaps)");
+  }
 }
 
 WideLanes::~WideLanes() {
@@ -295,6 +311,7 @@ WideLanes::~WideLanes() {
   if (claim_) (void)hipFree(claim_);
   if (acc_) (void)hipFree(acc_);
   if (ticket_) (void)hipFree(ticket_);
+  if (bm_) (void)hipFree(bm_);
 }
 
 void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hipStream_t stream) {
@@ -303,6 +320,13 @@ void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hi
   WideLanesArgs a{};
   a.L = L;
   a.xcd0 = xcd0_;
+  a.per = (8 - xcd0_) / L;  // every XCD from xcd0 on (an XCD's lane workgroups co-resident)
+  if (a.per < 1) a.per = 1;
+  if (const char* e = std::getenv("PSX_WIDE_LANE_XCDS")) {  // (measurements: XCDs per lane)
+    const int v = std::atoi(e);
+    if (v >= 1 && v * L <= 8 - xcd0_) a.per = v;
+  }
+  a.gpx = gpx_;
   a.claim = claim_;
   a.cpar = (int)(launches_ & 1);
   for (int l = 0; l < L; ++l) {
@@ -342,6 +366,12 @@ void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* 
     m.loss[j] = d.loss;
     m.slot[j] = reinterpret_cast<char*>(slots[j]);
     m.seq[j] = seqs[j];
+  }
+  if (bm_ && nov > 0) {  // this pass's overlays: their window features' bitmaps
+    hip_check(hipMemsetAsync(bm_, 0, (size_t)nov * (size_t)nw_ * 4, stream), "clear eval bitmaps");
+    wide_lanes_bitmap(devs_, nov, bm_, nw_, stream);
+    m.bm = bm_;
+    m.nw = nw_;
   }
   if (server_slot) {
     m.loss[nov] = nullptr;

@@ -78,10 +78,14 @@ class SparseRing:
         self.nnz = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
         self.y = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
         self.trunc = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.batch: IngestBatch | None = None  # set: deliveries are collected, one launch for every ring
 
     def ingest_from(self, ds: SparseDataset, src_first: int, src_step: int, n: int, dst_first: int):
         """Copy rows src_first + i*src_step (i < n) of ``ds`` into slots (dst_first + i) % cap."""
         if n <= 0:
+            return
+        if self.batch is not None and is_gpu(self.device):
+            self.batch.add(self, ds, src_first, src_step, n, dst_first)
             return
         if is_gpu(self.device):
             _native.hip().sparse_ring_ingest(ds.indptr.data_ptr(), ds.idx.data_ptr(), ds.val.data_ptr(),
@@ -102,6 +106,33 @@ class SparseRing:
             self.val[d, :k] = ds.val[a:a + k]
             self.nnz[d] = k
             self.y[d] = ds.y[s]
+
+
+class IngestBatch:
+    """Deliveries of several :class:`SparseRing` s (one geometry, one dataset) collected
+    and copied in ONE launch (the wide lanes' rounds: one ingest launch, not one per
+    worker and epoch split)."""
+
+    def __init__(self):
+        self.jobs: list[list[int]] = []
+        self.ds = None
+        self.geom = None
+
+    def add(self, ring: SparseRing, ds: SparseDataset, src_first: int, src_step: int, n: int, dst_first: int):
+        if (self.ds is not None and ds is not self.ds) or (self.geom is not None and self.geom != (ring.cap, ring.NZ)) \
+                or len(self.jobs) >= 16:
+            self.flush(ring.device)
+        self.ds, self.geom = ds, (ring.cap, ring.NZ)
+        self.jobs.append([int(src_first), int(src_step), int(n), int(dst_first), ring.idx.data_ptr(),
+                          ring.val.data_ptr(), ring.nnz.data_ptr(), ring.y.data_ptr(), ring.trunc.data_ptr()])
+
+    def flush(self, device):
+        if self.jobs:
+            ds = self.ds
+            _native.hip().sparse_ring_ingest_many(ds.indptr.data_ptr(), ds.idx.data_ptr(), ds.val.data_ptr(),
+                                                  ds.y.data_ptr(), self.jobs, self.geom[0], self.geom[1],
+                                                  stream_handle(device))
+        self.jobs, self.ds, self.geom = [], None, None
 
 
 class SparseDelta:
@@ -374,5 +405,5 @@ def nz_capacity(max_nnz: int) -> int:
     return n
 
 
-__all__ = ["SparseDataset", "SparseRing", "SparseDelta", "WideSolveOp", "WideEvalSet", "wide_server_apply",
+__all__ = ["SparseDataset", "SparseRing", "IngestBatch", "SparseDelta", "WideSolveOp", "WideEvalSet", "wide_server_apply",
            "wide_logits", "nz_capacity"]

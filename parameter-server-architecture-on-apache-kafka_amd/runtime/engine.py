@@ -802,10 +802,16 @@ class LocalEngine:
         pending_srv = None  # (vc) the server row of the last round, evaluated by the next pass
         t_start = time.time()
         exhausted_since = None
+        from ..ops.sparse import IngestBatch
+
+        batch = IngestBatch()  # every worker's deliveries of a round: one launch
+        for w in W:
+            w.ring.batch = batch
         try:
             while not self._stop(r - r0, t_start, exhausted_since):
                 for w in W:
                     w.ingest()
+                batch.flush(self.device)
                 if all(w.source.exhausted for w in W):
                     exhausted_since = exhausted_since or time.time()
                 if not all(w.ready() for w in W):
@@ -866,6 +872,9 @@ class LocalEngine:
                         srv.w.data_ptr(), 0, [], [], ss, sq, stream)
                 native.submit(s_, sq, 1, -1, -1, int(pending_srv), 0)
         finally:
+            batch.flush(self.device)
+            for w in W:
+                w.ring.batch = None
             torch.cuda.synchronize(self.device)
         self.rounds = r if bsp else int(srv.tracker.min_clock())
         elapsed = time.time() - t_start

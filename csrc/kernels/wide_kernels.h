@@ -195,6 +195,20 @@ int wide_lanes_per_cu(const WideCfg& c, size_t lds);
 // bm [L][nw] (nw = (F + 31) / 32 words, zeroed by the caller): bit f of lane l set for
 // every feature of lane l's last window (devs[l].uniq[0 .. U))
 void wide_lanes_bitmap(const WideDev* devs, int L, unsigned* bm, int64_t nw, hipStream_t s);
+// the overlay table of the lanes' last windows (set: pres bits + rows + local ids lidt
+// [F][kWideMaxLanes]; clear: pres words of those features back to 0 -- the rows need no
+// clearing, pres guards them)
+void wide_lanes_overlay(const WideDev* devs, int L, int KP, unsigned* pres, float* ov, int* lidt, bool set,
+                        hipStream_t s);
+// the lanes' pushes in order ord[0 .. n) in one launch, reading the overlay table (which it
+// clears): one thread per window feature adds the deltas in that order (= one launch per
+// push, bit for bit); needs the table of THESE solves (wide_lanes_overlay set)
+struct WideLanesOrder {
+  int n;
+  int ord[kWideMaxLanes];
+};
+void wide_lanes_apply(const WideDev* devs, int L, const WideLanesOrder& o, int64_t F, int KP, float* w, float lr,
+                      unsigned* pres, const int* lidt, hipStream_t s);
 
 // Test-set evaluation of up to kWideMaxEval models of the wide model in ONE pass:
 // model m < nov = the common weights w overlaid with lane m's window solution
@@ -209,6 +223,11 @@ struct WideEvalModels {
   // table is probed only for a feature whose bit is set (null: always probed)
   const unsigned* bm;
   int64_t nw;
+  // optional overlay table (wide_lanes_overlay): pres[f] bit j = f is in lane j's window,
+  // ov[(f * kWideMaxLanes + j) * KP ..] = lane j's local coefficients of f; replaces the
+  // bitmaps and table probes (one presence word + one contiguous row block per non-zero)
+  const unsigned* pres;
+  const float* ov;
   const int2* htab[kWideMaxLanes];
   unsigned hmask[kWideMaxLanes];
   const float* wloc[kWideMaxLanes];
@@ -216,7 +235,10 @@ struct WideEvalModels {
   char* slot[kWideMaxEval];
   unsigned long long seq[kWideMaxEval];
 };
-// acc: [kWideMaxEval][256] cells at stride kAccStride (zero between passes)
+// acc: [kWideEvalCopies][kWideMaxEval][256] cells at stride kAccStride (zero between
+// passes): workgroup b adds into copy b % kWideEvalCopies -- one copy took every
+// workgroup's atomics on the same 9 x 36 cells, serialised (135 us for 9 models)
+constexpr int kWideEvalCopies = 8;
 void launch_wide_eval_multi(int K, int KP, int64_t F, const int64_t* indptr, const int32_t* idx, const uint16_t* val,
                             const int32_t* y, int T, const float* w, const WideEvalModels& m, int* acc,
                             unsigned* ticket, hipStream_t s);

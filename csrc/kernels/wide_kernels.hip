@@ -1103,6 +1103,86 @@ __global__ __launch_bounds__(256) void wide_lanes_bitmap_kernel(const WideDev* _
   }
 }
 
+// blockIdx.y = lane.  set: lane l's row of every window feature f (and its local id) into
+// the table, bit l into pres[f]; clear: pres[f] = 0.
+__global__ __launch_bounds__(256) void wide_lanes_overlay_kernel(const WideDev* __restrict__ devs, int KP,
+                                                                 unsigned* pres, float* ov, int* lidt, int set) {
+  const int l = (int)blockIdx.y;
+  const WideDev& d = devs[l];
+  const unsigned U = d.cnt[0];
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+    const int f = d.uniq[i];
+    if (set) {
+      float* dst = ov + ((int64_t)f * kWideMaxLanes + l) * KP;
+      const float* src = d.wloc + KP + (int64_t)i * KP;
+      if (KP % 4 == 0) {
+        for (int k = 0; k < KP; k += 4) *(float4*)(dst + k) = *(const float4*)(src + k);
+      } else {
+        for (int k = 0; k < KP; ++k) dst[k] = src[k];
+      }
+      lidt[(int64_t)f * kWideMaxLanes + l] = (int)i;
+      atomicOr(pres + f, 1u << l);
+    } else {
+      pres[f] = 0u;
+    }
+  }
+}
+
+void wide_lanes_overlay(const WideDev* devs, int L, int KP, unsigned* pres, float* ov, int* lidt, bool set,
+                        hipStream_t s) {
+  wide_lanes_overlay_kernel<<<dim3(128, (unsigned)L), 256, 0, s>>>(devs, KP, pres, ov, lidt, set ? 1 : 0);
+}
+
+// The lanes' sparse pushes in ONE launch, in the order `ord` (= one launch per push in that
+// order, bit for bit): every window feature is updated by ONE thread -- the one of the lowest
+// lane holding it (pres bits) -- which adds the lanes' deltas in `ord`, then clears pres[f];
+// the intercepts by one thread per class.  w[f * KP + c] += lr * dloc_j[KP + lid * KP + c].
+__global__ __launch_bounds__(256) void wide_lanes_apply_kernel(const WideDev* __restrict__ devs, WideLanesOrder o,
+                                                               int64_t F, int KP, float* w, float lr, unsigned* pres,
+                                                               const int* __restrict__ lidt) {
+  const int l = (int)blockIdx.y;
+  const WideDev& d = devs[l];
+  const unsigned U = d.cnt[0];
+  for (unsigned i = blockIdx.x * 256 + threadIdx.x; i < U; i += gridDim.x * 256) {
+    const int f = d.uniq[i];
+    const unsigned bits = pres[f];
+    if (bits == 0u || (int)__builtin_ctz(bits) != l) continue;  // another lane's thread owns f
+    float* wf = w + (int64_t)f * KP;
+    float acc[16];  // (constant indices only: registers)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = k < KP ? wf[k] : 0.f;
+#pragma unroll
+    for (int q = 0; q < kWideMaxLanes; ++q) {
+      if (q < o.n) {
+        const int j = o.ord[q];
+        if ((bits >> j) & 1u) {
+          const int li = lidt[(int64_t)f * kWideMaxLanes + j];
+          const float* dl = devs[j].dloc + KP + (int64_t)li * KP;
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (k < KP) acc[k] += lr * dl[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < KP) wf[k] = acc[k];
+    pres[f] = 0u;
+  }
+  if (l == 0 && blockIdx.x == 0 && (int)threadIdx.x < KP) {  // the intercepts
+    float b = w[F * KP + threadIdx.x];
+#pragma unroll
+    for (int q = 0; q < kWideMaxLanes; ++q)
+      if (q < o.n) b += lr * devs[o.ord[q]].dloc[threadIdx.x];
+    w[F * KP + threadIdx.x] = b;
+  }
+}
+
+void wide_lanes_apply(const WideDev* devs, int L, const WideLanesOrder& o, int64_t F, int KP, float* w, float lr,
+                      unsigned* pres, const int* lidt, hipStream_t s) {
+  wide_lanes_apply_kernel<<<dim3(128, (unsigned)L), 256, 0, s>>>(devs, o, F, KP, w, lr, pres, lidt);
+}
+
 void wide_lanes_bitmap(const WideDev* devs, int L, unsigned* bm, int64_t nw, hipStream_t s) {
   wide_lanes_bitmap_kernel<<<256, 256, 0, s>>>(devs, L, bm, nw);
 }
@@ -1414,11 +1494,14 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
   }
   __syncthreads();
   const int ast = slot ? kAccStride : 1;  // slot mode: one cell per 128-B line (see test_eval_kernel)
+  // slot mode: workgroup b adds into copy b % kWideEvalCopies of the [2][256] cells (one
+  // copy serialises every workgroup's atomics on the same few cells)
+  int* accb = slot ? acc + (int)(blockIdx.x % kWideEvalCopies) * 512 * kAccStride : acc;
   const int v = cl[0][tid];
-  if (v) atomicAdd(acc + tid * ast, v);
+  if (v) atomicAdd(accb + tid * ast, v);
   if constexpr (PAIR) {
     const int v2 = cl[1][tid];
-    if (v2) atomicAdd(acc + (256 + tid) * ast, v2);
+    if (v2) atomicAdd(accb + (256 + tid) * ast, v2);
   }
   if (slot == nullptr) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1429,11 +1512,22 @@ __global__ __launch_bounds__(256) void wide_eval_kernel(int K, int64_t F, const 
   if (!last) return;
   // publication as in test_eval_kernel: drained system-scope stores into the
   // uncached host slot, then the sequence number (no L2-writeback fence)
-  const int tot = __hip_atomic_exchange(acc + tid * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int part[kWideEvalCopies];
+#pragma unroll
+  for (int q = 0; q < kWideEvalCopies; ++q)
+    part[q] = __hip_atomic_exchange(acc + (q * 512 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int tot = 0;
+#pragma unroll
+  for (int q = 0; q < kWideEvalCopies; ++q) tot += part[q];
   __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid == 0) __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if constexpr (PAIR) {
-    const int tot2 = __hip_atomic_exchange(acc + (256 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int tot2 = 0;
+#pragma unroll
+    for (int q = 0; q < kWideEvalCopies; ++q)
+      part[q] = __hip_atomic_exchange(acc + (q * 512 + 256 + tid) * ast, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int q = 0; q < kWideEvalCopies; ++q) tot2 += part[q];
     __hip_atomic_store((int*)slot2 + tid, tot2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid == 0) __hip_atomic_store((float*)(slot2 + 1024), 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1487,6 +1581,45 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
           const bool ok = e < b0;
           f[u] = ok ? idx[e] : -1;
           v[u] = ok ? bf2f(val[e]) : 0.f;
+        }
+        if (m.pres) {  // the lanes' overlay table: one presence word + the lanes' rows of f
+          float wv[NE][KP];
+          unsigned pm[NE];
+#pragma unroll
+          for (int u = 0; u < NE; ++u) {
+            if (f[u] >= 0) {
+              ldk<KP>(w + (int64_t)f[u] * KP, wv[u]);
+              pm[u] = m.pres[f[u]];
+            } else {
+#pragma unroll
+              for (int k = 0; k < KP; ++k) wv[u][k] = 0.f;
+              pm[u] = 0u;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < NE; ++u) {
+#pragma unroll
+            for (int j = 0; j < kWideMaxLanes; ++j) {
+              if (j < nov) {
+                if ((pm[u] >> j) & 1u) {
+                  float ov[KP];
+                  ldk<KP>(m.ov + ((int64_t)f[u] * kWideMaxLanes + j) * KP, ov);
+#pragma unroll
+                  for (int k = 0; k < KP; ++k) z[j][k] += v[u] * ov[k];
+                } else {
+#pragma unroll
+                  for (int k = 0; k < KP; ++k) z[j][k] += v[u] * wv[u][k];
+                }
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < kWideMaxEval; ++j)
+              if (m.plain && j == nov) {
+#pragma unroll
+                for (int k = 0; k < KP; ++k) z[j][k] += v[u] * wv[u][k];
+              }
+          }
+          continue;
         }
         float wv[NE][KP];
         int2 pr[NE][kWideMaxLanes];
@@ -1581,7 +1714,7 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
   for (int j = 0; j < kWideMaxEval; ++j) {
     if (j < M) {
       const int v = cl[j][tid];
-      if (v) atomicAdd(acc + (j * 256 + tid) * kAccStride, v);
+      if (v) atomicAdd(acc + (((int)(blockIdx.x % kWideEvalCopies) * kWideMaxEval + j) * 256 + tid) * kAccStride, v);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1597,8 +1730,14 @@ __global__ __launch_bounds__(256) void wide_eval_multi_kernel(int K, int64_t F, 
     if (j < M) {
       char* slot = m.slot[j];
       const float* loss = m.loss[j];
-      const int tot = __hip_atomic_exchange(acc + (j * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
+      int part[kWideEvalCopies];  // every copy's exchange in flight before the sum
+#pragma unroll
+      for (int q = 0; q < kWideEvalCopies; ++q)
+        part[q] = __hip_atomic_exchange(acc + ((q * kWideMaxEval + j) * 256 + tid) * kAccStride, 0, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+      int tot = 0;
+#pragma unroll
+      for (int q = 0; q < kWideEvalCopies; ++q) tot += part[q];
       __hip_atomic_store((int*)slot + tid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if (tid == 0)
         __hip_atomic_store((float*)(slot + 1024), loss ? *loss : 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -131,8 +131,12 @@ class WideLanes {
   size_t lds_ = 0;
   WideDev* devs_ = nullptr;   // [L] device table
   unsigned* claim_ = nullptr; // [2][16]
-  int* acc_ = nullptr;        // [kWideMaxEval][256] cells at stride kAccStride
+  int* acc_ = nullptr;        // [kWideEvalCopies][kWideMaxEval][256] cells at stride kAccStride
   unsigned* ticket_ = nullptr;
+  unsigned* pres_ = nullptr;  // [F] overlay presence words of the evaluation pass (null: table probes)
+  float* ov_ = nullptr;       // [F][kWideMaxLanes][KP] the lanes' local coefficients
+  int* lidt_ = nullptr;       // [F][kWideMaxLanes] their local ids
+  bool ov_live_ = false;      // the table holds the last eval's lanes (apply consumes it)
   unsigned* bm_ = nullptr;    // [L][nw_] window-feature bitmaps of the evaluation pass (null: off)
   int64_t nw_ = 0;
   int gpx_ = 32;              // lane workgroups per XCD (32 x co-resident lane workgroups per CU)

@@ -284,7 +284,7 @@ WideLanes::WideLanes(const std::vector<WideSolver*>& solvers, int xcd0) : solver
   hip_check(hipMemcpy(devs_, devs.data(), sizeof(WideDev) * L, hipMemcpyHostToDevice), "wide lanes table");
   hip_check(hipMalloc(&claim_, 2 * 16 * sizeof(unsigned)), "hipMalloc(claim)");
   hip_check(hipMemset(claim_, 0, 2 * 16 * sizeof(unsigned)), "hipMemset(claim)");
-  const size_t acc_bytes = (size_t)kWideMaxEval * 256 * kAccStride * sizeof(int);
+  const size_t acc_bytes = (size_t)kWideEvalCopies * kWideMaxEval * 256 * kAccStride * sizeof(int);
   hip_check(hipMalloc(&acc_, acc_bytes), "hipMalloc(eval accumulators)");
   hip_check(hipMemset(acc_, 0, acc_bytes), "hipMemset(eval accumulators)");
   hip_check(hipMalloc(&ticket_, 64), "hipMalloc(ticket)");
@@ -296,14 +296,22 @@ WideLanes::WideLanes(const std::vector<WideSolver*>& solvers, int xcd0) : solver
     const int v = std::atoi(e);
     if (v == 1 || v == 2) gpx_ = 32 * std::min(v, gpx_ / 32);
   }
+  // the evaluation pass's overlay table: F presence words + F x 8 lanes' coefficient rows
+  // (256 MB at 2^20 features and KP 8; up to 2 GB of the 288 GB HBM), else bitmaps + probes
+  const size_t ov_bytes = (size_t)cfg_.F * kWideMaxLanes * cfg_.KP * 4;
+  const char* eo = std::getenv("PSX_WIDE_EVAL_OVERLAY");
+  if (ov_bytes <= ((size_t)2 << 30) && !(eo && std::atoi(eo) == 0)) {
+    hip_check(hipMalloc(&ov_, ov_bytes), "hipMalloc(eval overlay rows)");
+    hip_check(hipMalloc(&pres_, (size_t)cfg_.F * 4), "hipMalloc(eval overlay presence)");
+    hip_check(hipMalloc(&lidt_, (size_t)cfg_.F * kWideMaxLanes * 4), "hipMalloc(eval overlay local ids)");
+    hip_check(hipMemset(pres_, 0, (size_t)cfg_.F * 4), "hipMemset(eval overlay presence)");
+  }
   // the evaluation pass's bitmaps of the lanes' window features (up to 64 MB)
   nw_ = (cfg_.F + 31) / 32;
   const size_t bm_bytes = (size_t)L * (size_t)nw_ * 4;
-  if (bm_bytes <= ((size_t)64 << 20) && std::getenv("PSX_WIDE_EVAL_BITMAP") == nullptr) {
+  const char* eb = std::getenv("PSX_WIDE_EVAL_BITMAP");
+  if (!pres_ && bm_bytes <= ((size_t)64 << 20) && !(eb && std::atoi(eb) == 0))
     hip_check(hipMalloc(&bm_, bm_bytes), "hipMalloc(eval bitmaps)");
-  } else if (const char* e = std::getenv("PSX_WIDE_EVAL_BITMAP"); e && std::atoi(e) != 0 && bm_bytes <= ((size_t)64 << 20)) {
-    hip_check(hipMalloc(&bm_, bm_bytes), "hipMalloc(eval bitmaps)");
-  }
 }
 
 WideLanes::~WideLanes() {
@@ -312,6 +320,9 @@ WideLanes::~WideLanes() {
   if (acc_) (void)hipFree(acc_);
   if (ticket_) (void)hipFree(ticket_);
   if (bm_) (void)hipFree(bm_);
+  if (pres_) (void)hipFree(pres_);
+  if (ov_) (void)hipFree(ov_);
+  if (lidt_) (void)hipFree(lidt_);
 }
 
 void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hipStream_t stream) {
@@ -341,6 +352,24 @@ void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hi
 }
 
 void WideLanes::apply(float* w, float lr, const std::vector<int>& order, hipStream_t stream) {
+  if (ov_live_ && (int)order.size() == lanes()) {  // one launch over the overlay table of these solves
+    WideLanesOrder o{};
+    o.n = lanes();
+    std::vector<int> seen(lanes(), 0);
+    for (int q = 0; q < o.n; ++q) {
+      const int l = order[q];
+      if (l < 0 || l >= lanes() || seen[l]++) throw std::invalid_argument("WideLanes::apply: order must permute the lanes");
+      o.ord[q] = l;
+    }
+    wide_lanes_apply(devs_, lanes(), o, cfg_.F, cfg_.KP, w, lr, pres_, lidt_, stream);
+    hip_check(hipGetLastError(), "wide lanes apply launch");
+    ov_live_ = false;
+    return;
+  }
+  if (ov_live_) {  // a partial order: the per-push launches; the table is cleared
+    wide_lanes_overlay(devs_, lanes(), cfg_.KP, pres_, nullptr, nullptr, false, stream);
+    ov_live_ = false;
+  }
   for (int l : order) {
     if (l < 0 || l >= lanes()) throw std::invalid_argument("WideLanes::apply: lane out of range");
     const WideSolver* s = solvers_[l];
@@ -367,7 +396,15 @@ void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* 
     m.slot[j] = reinterpret_cast<char*>(slots[j]);
     m.seq[j] = seqs[j];
   }
-  if (bm_ && nov > 0) {  // this pass's overlays: their window features' bitmaps
+  if (pres_ && ov_live_) {  // an earlier pass's table nobody applied: cleared first
+    wide_lanes_overlay(devs_, lanes(), cfg_.KP, pres_, nullptr, nullptr, false, stream);
+    ov_live_ = false;
+  }
+  if (pres_ && nov > 0) {  // this pass's overlays: the table of their window rows
+    wide_lanes_overlay(devs_, nov, cfg_.KP, pres_, ov_, lidt_, true, stream);
+    m.pres = pres_;
+    m.ov = ov_;
+  } else if (bm_ && nov > 0) {  // this pass's overlays: their window features' bitmaps
     hip_check(hipMemsetAsync(bm_, 0, (size_t)nov * (size_t)nw_ * 4, stream), "clear eval bitmaps");
     wide_lanes_bitmap(devs_, nov, bm_, nw_, stream);
     m.bm = bm_;
@@ -380,6 +417,14 @@ void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* 
   }
   launch_wide_eval_multi(cfg_.K, cfg_.KP, cfg_.F, indptr, idx, val, y, T, w, m, acc_, ticket_, stream);
   hip_check(hipGetLastError(), "wide lanes evaluation launch");
+  if (m.pres) {
+    if (nov == lanes()) {
+      ov_live_ = true;  // the next apply() reads the table and clears it
+    } else {
+      wide_lanes_overlay(devs_, nov, cfg_.KP, pres_, nullptr, nullptr, false, stream);  // presence back to 0
+      hip_check(hipGetLastError(), "wide lanes overlay clear");
+    }
+  }
 }
 
 }  // namespace psx

@@ -353,8 +353,9 @@ class EvalScratch:
     """Private accumulator + ticket of one evaluation caller (stays zero between calls)."""
 
     def __init__(self, device):
-        # [2 models][16][16] cells, one per 128-B line (kAccStride in csrc/kernels/lr_kernels.h)
-        self.acc = torch.zeros(2 * 256 * ACC_STRIDE, dtype=torch.int32, device=device)
+        # [2 models][16][16] cells, one per 128-B line (kAccStride in csrc/kernels/lr_kernels.h);
+        # x kWideEvalCopies (8): the wide evaluation spreads its workgroups' atomics over copies
+        self.acc = torch.zeros(8 * 2 * 256 * ACC_STRIDE, dtype=torch.int32, device=device)
         self.ticket = torch.zeros(8, dtype=torch.int32, device=device)
 
 

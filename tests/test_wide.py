@@ -353,14 +353,16 @@ def _wide_lanes_run(dev, N, c, iters=8, env=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("c", [0, -1, 2])
-def test_gpu_wide_lanes_match_cpu_rounds(cuda, c):
+@pytest.mark.parametrize("c,overlay", [(0, "1"), (-1, "1"), (2, "1"), (-1, "0")])
+def test_gpu_wide_lanes_match_cpu_rounds(cuda, c, overlay):
     """Several wide workers in ONE solve launch per round (WideLanes, one XCD each):
     every round's solves start from the same server weights and the pushes are applied
     in order, so BSP, SSP and ASP all land on the weights of the CPU engine's BSP rounds
-    (whose workers solve with the float64-oracle path, ops/sparse.py _run_cpu)."""
+    (whose workers solve with the float64-oracle path, ops/sparse.py _run_cpu).
+    overlay "1": the evaluation reads the overlay table and the pushes are applied in
+    one launch over it; "0": bitmaps + table probes and one launch per push."""
     N, iters = 4, 8
-    eng, out, book, te = _wide_lanes_run(cuda, N, c, iters)
+    eng, out, book, te = _wide_lanes_run(cuda, N, c, iters, env={"PSX_WIDE_EVAL_OVERLAY": overlay})
     assert out.get("wide_lanes") == N, out  # the one-launch path ran
     assert out["updates"] == N * iters
     assert len(book.worker) == N * iters and len(book.server) == iters

@@ -840,13 +840,20 @@ __device__ __forceinline__ void wide_persist_body(const WideCfg& c, const WideDe
     for (int grp = blk; grp < ngr; grp += G) wide_plan_body(c, d, grp, pl_lds);
     wide_gen_barrier(d.pbar, G, err, xl);
   }
+  // (stamps of the prefix's phases, where nslots >= 6: [23] planned, [31] assigned,
+  // [39] window statistics, [47] prepared)
+  const bool stp = st && c.sc.nslots >= 6;
+  if (stp) d.dbg[23] = (long long)__builtin_amdgcn_s_memrealtime();
   if (!(phases & 2)) return;
   wide_assign_body(c, d, blk, G);
   wide_gen_barrier(d.pbar, G, err, xl);
+  if (stp) d.dbg[31] = (long long)__builtin_amdgcn_s_memrealtime();
   for (int grp = blk; grp < ngr; grp += G) wide_stats_body(c, d, grp, pl_lds);
   wide_gen_barrier(d.pbar, G, err, xl);
+  if (stp) d.dbg[39] = (long long)__builtin_amdgcn_s_memrealtime();
   wide_prep_body(c, d, blk, G);
   wide_gen_barrier(d.pbar, G, err, xl);
+  if (stp) d.dbg[47] = (long long)__builtin_amdgcn_s_memrealtime();
   for (int slot = 0; slot < c.sc.nslots; ++slot) {
     if (threadIdx.x == 0)
       phase_s = __hip_atomic_load(&d.ctrl->phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

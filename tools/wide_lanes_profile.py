@@ -49,7 +49,9 @@ def main():
             if not row[6] or row[6] < t0:
                 break
             slots.append({"fwd": us(row[6]), "dots": us(row[0]), "last_in": us(row[1]), "ctrl_done": us(row[5])})
-        print(json.dumps({"worker": w.k, "U": w.solver.host_count(), "slots": slots, "finalize": us(st[15]),
+        prefix = {"planned": us(st[23]), "assigned": us(st[31]), "stats": us(st[39]), "prepared": us(st[47])}
+        print(json.dumps({"worker": w.k, "U": w.solver.host_count(), "prefix": prefix, "slots": slots,
+                          "finalize": us(st[15]),
                           "wide_lanes": out.get("wide_lanes")}))
 
 

@@ -329,6 +329,38 @@ def test_engine_wide_gpu(cuda, c, N):
     del cfg
 
 
+def test_wide_lanes_selection_cpu():
+    """The one-launch wide rounds are a GPU schedule: CPU engines, one worker, tracing and
+    injected faults keep the per-worker schedulers (engine.py _wide_lanes_ok)."""
+    from psx.runtime.engine import LocalEngine
+
+    ds, _ = _problem(F=800, rows=400)
+    te, _ = _problem(F=800, rows=100, seed=7)
+    eng = LocalEngine(_wide_cfg(3, -1, 2), "cpu", train=ds, test=te)
+    assert not eng._wide_lanes_ok()
+    out = eng.run()
+    assert "wide_lanes" not in out and out["updates"] >= 2
+
+
+def test_ingest_batch_groups_jobs():
+    """IngestBatch collects every ring's deliveries of a round (one launch on the GPU);
+    a different geometry or dataset starts a new batch."""
+    from psx.ops.sparse import IngestBatch
+
+    ds, _ = _problem(F=500, rows=64)
+    rings = [SparseRing(32, 48, "cpu") for _ in range(3)]
+    b = IngestBatch()
+    flushed = []
+    b.flush = lambda device: (flushed.append(list(b.jobs)), setattr(b, "jobs", []), setattr(b, "ds", None),
+                              setattr(b, "geom", None))
+    for i, r in enumerate(rings):
+        b.add(r, ds, i, 3, 8, 5)
+    assert len(b.jobs) == 3 and b.geom == (32, 48) and not flushed
+    assert [j[:4] for j in b.jobs] == [[0, 3, 8, 5], [1, 3, 8, 5], [2, 3, 8, 5]]
+    b.add(SparseRing(16, 48, "cpu"), ds, 0, 1, 4, 0)  # another geometry: the open batch goes first
+    assert len(flushed) == 1 and len(flushed[0]) == 3 and len(b.jobs) == 1
+
+
 def _wide_lanes_run(dev, N, c, iters=8, env=None):
     import os
 

@@ -186,6 +186,12 @@ struct WideLanesArgs {
   int cpar;
   int B[kWideMaxLanes];
   int start[kWideMaxLanes];
+  // the evaluation's overlay table (WideEvalModels::pres / ov, lidt [F][kWideMaxLanes]),
+  // built by each lane right after its finalisation (null: not built here); the table
+  // must be clear (every pres word 0) at launch
+  unsigned* pres;
+  float* ov;
+  int* lidt;
 };
 void wide_launch_lanes(const WideCfg& c, const WideDev* devs, const WideLanesArgs& a, size_t lds, hipStream_t s);
 int wide_lanes_grid(int gpx);

@@ -930,7 +930,23 @@ __global__ __launch_bounds__(512) void wide_lanes_kernel(WideCfg c, const WideDe
       B = a.B[i];
       start = a.start[i];
     }
-  wide_persist_body<KP, NQ>(c, devs[l], B, start, 3, G, blk, pl_lds, fsh, dsh, phase_s, a.per == 1);
+  const WideDev& d = devs[l];
+  wide_persist_body<KP, NQ>(c, d, B, start, 3, G, blk, pl_lds, fsh, dsh, phase_s, a.per == 1);
+  if (a.pres) {
+    // the lane's rows of the evaluation's overlay table: the same thread-to-feature map as
+    // wide_finalize_body's, so every thread reads back the wloc rows it has just written
+    const unsigned U = d.cnt[0];
+    const int64_t gs = (int64_t)G * blockDim.x;
+    for (int64_t i = (int64_t)blk * blockDim.x + threadIdx.x; i < (int64_t)U; i += gs) {
+      const int f = d.uniq[i];
+      float* dst = a.ov + ((int64_t)f * kWideMaxLanes + l) * KP;
+      const float* src = d.wloc + KP + i * KP;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) dst[k] = src[k];
+      a.lidt[(int64_t)f * kWideMaxLanes + l] = (int)i;
+      atomicOr(a.pres + f, 1u << l);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -346,9 +346,16 @@ void WideLanes::run(const std::vector<int>& B, const std::vector<int>& start, hi
     a.B[l] = B[l];
     a.start[l] = start[l];
   }
+  if (pres_) {  // the lanes build this launch's overlay table (a table nobody applied: cleared first)
+    if (ov_live_) wide_lanes_overlay(devs_, L, cfg_.KP, pres_, nullptr, nullptr, false, stream);
+    a.pres = pres_;
+    a.ov = ov_;
+    a.lidt = lidt_;
+  }
   wide_launch_lanes(cfg_, devs_, a, lds_, stream);
   hip_check(hipGetLastError(), "wide lanes launch");
   ++launches_;
+  ov_live_ = pres_ != nullptr;  // this launch's table (eval reads it, apply clears it)
 }
 
 void WideLanes::apply(float* w, float lr, const std::vector<int>& order, hipStream_t stream) {
@@ -396,12 +403,7 @@ void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* 
     m.slot[j] = reinterpret_cast<char*>(slots[j]);
     m.seq[j] = seqs[j];
   }
-  if (pres_ && ov_live_) {  // an earlier pass's table nobody applied: cleared first
-    wide_lanes_overlay(devs_, lanes(), cfg_.KP, pres_, nullptr, nullptr, false, stream);
-    ov_live_ = false;
-  }
-  if (pres_ && nov > 0) {  // this pass's overlays: the table of their window rows
-    wide_lanes_overlay(devs_, nov, cfg_.KP, pres_, ov_, lidt_, true, stream);
+  if (pres_ && nov > 0 && ov_live_) {  // the last launch built the table of its lanes' windows
     m.pres = pres_;
     m.ov = ov_;
   } else if (bm_ && nov > 0) {  // this pass's overlays: their window features' bitmaps
@@ -417,14 +419,7 @@ void WideLanes::eval(const int64_t* indptr, const int32_t* idx, const uint16_t* 
   }
   launch_wide_eval_multi(cfg_.K, cfg_.KP, cfg_.F, indptr, idx, val, y, T, w, m, acc_, ticket_, stream);
   hip_check(hipGetLastError(), "wide lanes evaluation launch");
-  if (m.pres) {
-    if (nov == lanes()) {
-      ov_live_ = true;  // the next apply() reads the table and clears it
-    } else {
-      wide_lanes_overlay(devs_, nov, cfg_.KP, pres_, nullptr, nullptr, false, stream);  // presence back to 0
-      hip_check(hipGetLastError(), "wide lanes overlay clear");
-    }
-  }
+
 }
 
 }  // namespace psx

@@ -2,18 +2,19 @@
 # PMC counter passes over a short bench.py run (rocprofv3 --pmc, csv).
 # Each pass is its own profiler run with counters only (no runtime/sys trace),
 # sized to the gfx950 slot limits (SQ 8, TCC 4: FETCH_SIZE costs 3, WRITE_SIZE 2).
+# PMC_BENCH_ARGS: extra bench.py arguments (e.g. --model sparse1m --workers 8); PMC_OUT: output dir.
 # Output: gpurun_out/pmc/passN/..._counter_collection.csv; summary via
 #   python tools/pmc_summary.py gpurun_out/pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 STEPS="${PMC_STEPS:-150}"
 run_pass() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o $name -- \
-    python3 bench.py --steps $STEPS --warmup 20 --no-accuracy-run > $OUT/$name.log 2>&1
+    python3 bench.py --steps $STEPS --warmup 20 --no-accuracy-run ${PMC_BENCH_ARGS:-} > $OUT/$name.log 2>&1
   local rc=$?
   echo "$name rc=$rc"
   return $rc

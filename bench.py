@@ -226,6 +226,8 @@ def describe(a, world, cfg, ups, dt, summ, tuples_seen=None, rccl_ranks=None, to
         par = (f"ps-{mode} key-range sharded server x{world} (every rank: 1 worker + the shard of its key "
                f"range; pull/push of the window's ids over {backend if world > 1 else 'local copies'})")
     elif world == 1 and not getattr(a, "dist_world1", False):
+        if a.model != "dense" and n_workers > 1:  # (the wide model's in-process workers: a stream each)
+            lanes = f"{n_workers} workers/GPU, one HIP stream each"
         par = f"ps-{mode} w{n_workers} (server colocated, {lanes if n_workers > 1 else '1 worker'})"
     elif async_mode and wpr > 1:
         par = (f"ps-{mode} 1 server rank + {world - 1} worker ranks x {wpr} workers (peer data plane over xGMI: "

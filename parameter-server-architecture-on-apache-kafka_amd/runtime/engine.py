@@ -732,10 +732,16 @@ class LocalEngine:
         need Python between a worker's solves (tracing, injected faults) keep the
         per-worker schedulers."""
         c = self.cfg
-        if os.environ.get("PSX_WIDE_LANES", "1") == "0" or not is_gpu(self.device) or self.evalset is None:
+        mode = os.environ.get("PSX_WIDE_LANES", "auto")  # 0: never, 1: 2..8 workers, auto: 5..8
+        if mode == "0" or not is_gpu(self.device) or self.evalset is None:
             return False
         W = [w for w in self.workers if w.k not in self.failed]
-        if not 2 <= len(W) <= 8 or self.tracer.enabled:
+        # auto: from 5 workers on.  With 2-4 the per-worker graphs on their streams measured
+        # faster (6.5k / 7.7k / 9.4k against 5.7k / 7.2k / 9.1k updates/s: a lane's one-XCD
+        # solve is latency-bound, and 2-4 chains of full-GPU launches overlap well), with 8
+        # the lanes (15.0k against 8.9k) -- profiles/r06/README.md section 9
+        lo = 2 if mode == "1" else 5
+        if not lo <= len(W) <= 8 or self.tracer.enabled:
             return False
         if any(not w.wide or w.solver.dense_delta for w in W):
             return False

@@ -394,7 +394,8 @@ def test_gpu_wide_lanes_match_cpu_rounds(cuda, c, overlay):
     overlay "1": the evaluation reads the overlay table and the pushes are applied in
     one launch over it; "0": bitmaps + table probes and one launch per push."""
     N, iters = 4, 8
-    eng, out, book, te = _wide_lanes_run(cuda, N, c, iters, env={"PSX_WIDE_EVAL_OVERLAY": overlay})
+    eng, out, book, te = _wide_lanes_run(cuda, N, c, iters, env={"PSX_WIDE_EVAL_OVERLAY": overlay,
+                                                                   "PSX_WIDE_LANES": "1"})
     assert out.get("wide_lanes") == N, out  # the one-launch path ran
     assert out["updates"] == N * iters
     assert len(book.worker) == N * iters and len(book.server) == iters
@@ -414,7 +415,7 @@ def test_gpu_wide_lanes_rows_equal_separate_passes(cuda):
     from psx.utils.logsink import LogSink
 
     N = 3
-    eng, out, book, te = _wide_lanes_run(cuda, N, -1, 1)
+    eng, out, book, te = _wide_lanes_run(cuda, N, -1, 1, env={"PSX_WIDE_LANES": "1"})
     assert out.get("wide_lanes") == N
     # one round from the initial weights: rebuild them and evaluate each local model alone
     w0 = eng.spec.init("random", seed=eng.cfg.seed, device=cuda)

@@ -1453,10 +1453,9 @@ class DistEngine:
                 # the token says "my delta is complete": the server serves tokens in
                 # arrival order, so it must not wait on a delta still being computed.
                 # Poll this solve's completion event (no full stream synchronisation:
-                # the evaluation row enqueued behind it keeps running); each miss yields
-                # the core (sleep(0): the GIL and the scheduler, no timer wait)
+                # the evaluation row enqueued behind it keeps running)
                 while not done.query():
-                    time.sleep(0)
+                    pass
             U = wk.solver.host_count() if self.sparse_push else 0
             tok.n = U
             if not self._ctrl.push(tok, 600.0):
